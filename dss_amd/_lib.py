@@ -1,0 +1,146 @@
+"""ctypes binding of libdss_amd.so (include/dssgpu.h).
+
+The product path has no CPU fallback: if the gfx950 library is missing or no
+gfx950 device is visible, every entry point raises.  The library lives in the
+package directory (built in-tree by ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdss_amd.so")
+
+DSSG_OK = 0
+DSSG_ERR_INVALID = 1
+DSSG_ERR_CAPACITY = 2
+DSSG_ERR_DEVICE = 3
+DSSG_ERR_NOMEM = 4
+DSSG_ERR_NO_DEVICE = 5
+
+ST_OK = 0
+ST_BAD_COORD_SET = 1
+ST_NOT_ENOUGH_POINTS = 2
+ST_ODD_COORDS = 3
+ST_RADIUS = 4
+ST_AREA_TOO_LARGE = 5
+
+KIND_POLYGON = 0
+KIND_CIRCLE = 1
+KIND_POINTS = 2
+
+TIME_NULL_START = -(2**63)
+TIME_NULL_END = -(2**63)
+TIME_NULL_END_Q = 2**63 - 1
+
+
+class DssgError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"dssg error {code}: {msg}")
+        self.code = code
+
+
+class Cells(C.Structure):
+    _fields_ = [("n", C.c_int64), ("offs", C.c_void_p), ("cells", C.c_void_p), ("status", C.c_void_p),
+                ("area_km2", C.c_void_p), ("total_cells", C.c_int64)]
+
+
+class Pairs(C.Structure):
+    _fields_ = [("q", C.c_void_p), ("e", C.c_void_p), ("n", C.c_int64)]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load the HIP library; raises if it was not built."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise DssgError(DSSG_ERR_NO_DEVICE,
+                            f"{LIB_PATH} missing: build it with __graft_entry__.build() (no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        P, vp = C.POINTER, C.c_void_p
+        i32, i64, d, f = C.c_int32, C.c_int64, C.c_double, C.c_float
+        u32, u64 = C.c_uint32, C.c_uint64
+        L.dssg_create.argtypes = [C.c_int, P(vp)]
+        L.dssg_destroy.argtypes = [vp]
+        L.dssg_destroy.restype = None
+        L.dssg_strerror.argtypes = [C.c_int]
+        L.dssg_strerror.restype = C.c_char_p
+        L.dssg_last_error.argtypes = [vp]
+        L.dssg_last_error.restype = C.c_char_p
+        L.dssg_cover_batch.argtypes = [vp, i64, P(i32), P(i64), P(d), P(d), P(f), P(i64), P(u64), i64, P(i64),
+                                       P(i32), P(d)]
+        L.dssg_cover_batch_device.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, P(Cells)]
+        L.dssg_area_to_cell_ids.argtypes = [vp, C.c_char_p, P(u64), i64, P(i64), P(i32), P(d)]
+        L.dssg_index_build.argtypes = [vp, i64, P(i64), P(u64), P(f), P(f), P(i64), P(i64), P(i32), P(vp)]
+        L.dssg_index_build_device.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, P(vp)]
+        L.dssg_index_free.argtypes = [vp]
+        L.dssg_index_free.restype = None
+        L.dssg_index_num_postings.argtypes = [vp]
+        L.dssg_index_num_postings.restype = i64
+        L.dssg_index_num_cells.argtypes = [vp]
+        L.dssg_index_num_cells.restype = i64
+        L.dssg_search_device.argtypes = [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, P(Pairs)]
+        L.dssg_search.argtypes = [vp, vp, i64, P(i64), P(u64), P(f), P(f), P(i64), P(i64), P(i32), P(u32), P(u32),
+                                  i64, P(i64)]
+        L.dssg_search_operations.argtypes = [vp, vp, i64, P(i64), P(u64), P(f), P(f), P(i64), P(i64), i64, P(u32),
+                                             P(u32), i64, P(i64)]
+        L.dssg_search_isas.argtypes = [vp, vp, i64, P(i64), P(u64), P(i64), P(i64), P(u32), P(u32), i64, P(i64)]
+        L.dssg_search_subscriptions.argtypes = [vp, vp, i64, P(i64), P(u64), P(i32), i64, P(u32), P(u32), i64,
+                                                P(i64)]
+        L.dssg_phase_times.argtypes = [vp, P(d), P(d), P(d)]
+        L.dssg_set_timing.argtypes = [vp, C.c_int]
+        L.dssg_set_timing.restype = None
+        L.dssg_copy_to_host.argtypes = [vp, vp, vp, C.c_size_t]
+        L.dssg_selftest_math.argtypes = [vp, C.c_int, i64, P(d), P(d), P(d)]
+        _lib = L
+        return L
+
+
+class Context:
+    """One engine context (device, stream, scratch) -- `dssg_ctx`."""
+
+    def __init__(self, device: int = 0):
+        L = load()
+        h = C.c_void_p()
+        rc = L.dssg_create(device, C.byref(h))
+        if rc != DSSG_OK:
+            raise DssgError(rc, L.dssg_strerror(rc).decode())
+        self.h = h
+        self.L = L
+        self.device = device
+
+    def check(self, rc: int):
+        if rc not in (DSSG_OK,):
+            raise DssgError(rc, self.L.dssg_last_error(self.h).decode() or self.L.dssg_strerror(rc).decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.dssg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_ctx = {}
+
+
+def context(device: int = 0) -> Context:
+    with _lock:
+        pass
+    c = _ctx.get(device)
+    if c is None:
+        c = Context(device)
+        _ctx[device] = c
+    return c

@@ -1,0 +1,484 @@
+// C ABI (include/dssgpu.h) over the gfx950 covering and search engines.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cerrno>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "cover.hpp"
+#include "search.hpp"
+
+struct dssg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    dss::CoverEngine cover;
+    dss::SearchEngine search;
+    std::string last_error;
+    bool timing = false;
+    double cover_ms = 0, join_ms = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // host-API staging
+    dss::DevBuf<int32_t> d_kind, d_owner;
+    dss::DevBuf<int64_t> d_voff, d_qoffs, d_tlo, d_thi;
+    dss::DevBuf<double> d_lat, d_lng;
+    dss::DevBuf<float> d_rad, d_alo, d_ahi;
+    dss::DevBuf<uint64_t> d_cells;
+};
+
+namespace {
+
+template <typename F>
+int guarded(dssg_ctx *ctx, F &&f)
+{
+    try {
+        if (ctx) DSS_HIP(hipSetDevice(ctx->device));
+        f();
+        return DSSG_OK;
+    } catch (const dss::Error &e) {
+        if (ctx) ctx->last_error = e.what();
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        if (ctx) ctx->last_error = "out of host memory";
+        return DSSG_ERR_NOMEM;
+    } catch (const std::exception &e) {
+        if (ctx) ctx->last_error = e.what();
+        return DSSG_ERR_DEVICE;
+    }
+}
+
+template <typename T>
+T *upload(dss::DevBuf<T> &b, const T *h, int64_t n, hipStream_t s)
+{
+    T *d = b.ensure((size_t)(n > 0 ? n : 1));
+    if (n > 0) DSS_HIP(hipMemcpyAsync(d, h, sizeof(T) * (size_t)n, hipMemcpyHostToDevice, s));
+    return d;
+}
+
+// strconv.ParseFloat(s, 64) grammar (Go 1.14): [+-] (decimal | hex-with-p |
+// inf | infinity | nan), no underscores in the forms the DSS ever sees; a
+// value out of float64 range is an error (ErrRange).  Returns false on error.
+bool go_parse_float(const std::string &s, double &out)
+{
+    if (s.empty()) return false;
+    size_t i = 0;
+    std::string t = s;
+    if (t[0] == '+' || t[0] == '-') i = 1;
+    std::string body = t.substr(i);
+    std::string lower = body;
+    for (auto &c : lower) c = (char)std::tolower((unsigned char)c);
+    if (lower == "inf" || lower == "infinity") {
+        out = (t[0] == '-') ? -HUGE_VAL : HUGE_VAL;
+        return true;
+    }
+    if (lower == "nan") {
+        if (i) return false;  // Go rejects a signed NaN
+        out = std::nan("");
+        return true;
+    }
+    bool hex = lower.size() > 2 && lower[0] == '0' && lower[1] == 'x';
+    size_t k = hex ? 2 : 0;
+    bool digits = false, dot = false, exp = false;
+    for (; k < lower.size(); k++) {
+        char c = lower[k];
+        if ((hex ? std::isxdigit((unsigned char)c) : std::isdigit((unsigned char)c)) != 0) { digits = true; continue; }
+        if (c == '.' && !dot) { dot = true; continue; }
+        break;
+    }
+    if (!digits) return false;
+    if (k < lower.size()) {
+        char c = lower[k];
+        if ((hex && c == 'p') || (!hex && c == 'e')) {
+            exp = true;
+            k++;
+            if (k < lower.size() && (lower[k] == '+' || lower[k] == '-')) k++;
+            size_t d0 = k;
+            while (k < lower.size() && std::isdigit((unsigned char)lower[k])) k++;
+            if (k == d0) return false;
+        }
+    }
+    if (k != lower.size()) return false;
+    if (hex && !exp) return false;  // "hexadecimal mantissa requires a 'p' exponent"
+    errno = 0;
+    char *end = nullptr;
+    double v = std::strtod(t.c_str(), &end);
+    if (end != t.c_str() + t.size()) return false;
+    if (errno == ERANGE && std::isinf(v)) return false;
+    out = v;
+    return true;
+}
+
+std::string trim_space(const std::string &s)
+{
+    size_t a = 0, b = s.size();
+    auto sp = [](unsigned char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r'; };
+    while (a < b && sp((unsigned char)s[a])) a++;
+    while (b > a && sp((unsigned char)s[b - 1])) b--;
+    return s.substr(a, b - a);
+}
+
+void sort_pairs_host(uint32_t *q, uint32_t *e, int64_t n)
+{
+    std::vector<uint64_t> k((size_t)n);
+    for (int64_t i = 0; i < n; i++) k[i] = ((uint64_t)q[i] << 32) | e[i];
+    std::sort(k.begin(), k.end());
+    for (int64_t i = 0; i < n; i++) {
+        q[i] = (uint32_t)(k[i] >> 32);
+        e[i] = (uint32_t)k[i];
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *dssg_strerror(int code)
+{
+    switch (code) {
+    case DSSG_OK: return "ok";
+    case DSSG_ERR_INVALID: return "invalid argument";
+    case DSSG_ERR_CAPACITY: return "output capacity too small";
+    case DSSG_ERR_DEVICE: return "device error";
+    case DSSG_ERR_NOMEM: return "out of memory";
+    case DSSG_ERR_NO_DEVICE: return "no gfx950 device";
+    default: return "unknown error";
+    }
+}
+
+const char *dssg_last_error(dssg_ctx *ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+
+int dssg_create(int device, dssg_ctx **out)
+{
+    if (!out) return DSSG_ERR_INVALID;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= device || device < 0) return DSSG_ERR_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return DSSG_ERR_NO_DEVICE;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return DSSG_ERR_NO_DEVICE;
+    dssg_ctx *c = new (std::nothrow) dssg_ctx();
+    if (!c) return DSSG_ERR_NOMEM;
+    c->device = device;
+    int rc = guarded(c, [&] { DSS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)); });
+    if (rc) {
+        delete c;
+        return rc;
+    }
+    *out = c;
+    return DSSG_OK;
+}
+
+void dssg_destroy(dssg_ctx *ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+void dssg_set_timing(dssg_ctx *ctx, int enabled)
+{
+    if (!ctx) return;
+    ctx->timing = enabled != 0;
+    ctx->search.set_timing(ctx->timing);
+}
+
+int dssg_phase_times(dssg_ctx *ctx, double *cover_ms, double *join_ms, double *join_kernel_ms)
+{
+    if (!ctx) return DSSG_ERR_INVALID;
+    if (cover_ms) *cover_ms = ctx->cover_ms;
+    if (join_ms) *join_ms = ctx->join_ms;
+    if (join_kernel_ms) *join_kernel_ms = ctx->search.last_join_kernel_ms();
+    return DSSG_OK;
+}
+
+int dssg_cover_batch_device(dssg_ctx *ctx, int64_t n, const int32_t *d_kind, const int64_t *d_voff, const double *d_lat,
+                            const double *d_lng, const float *d_radius_m, void *stream, dssg_cells *out)
+{
+    if (!ctx || !out || n < 0 || (n > 0 && (!d_kind || !d_voff || !d_lat || !d_lng || !d_radius_m)))
+        return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        if (ctx->timing) {
+            if (!ctx->ev0) { DSS_HIP(hipEventCreate(&ctx->ev0)); DSS_HIP(hipEventCreate(&ctx->ev1)); }
+            DSS_HIP(hipEventRecord(ctx->ev0, s));
+        }
+        ctx->cover.run(n, d_kind, d_voff, d_lat, d_lng, d_radius_m, s, out);
+        if (ctx->timing) {
+            DSS_HIP(hipEventRecord(ctx->ev1, s));
+            DSS_HIP(hipEventSynchronize(ctx->ev1));
+            float ms = 0;
+            DSS_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+            ctx->cover_ms = ms;
+        }
+    });
+}
+
+int dssg_cover_batch(dssg_ctx *ctx, int64_t n, const int32_t *kind, const int64_t *voff, const double *lat,
+                     const double *lng, const float *radius_m, int64_t *out_offs, uint64_t *out_cells,
+                     int64_t cells_cap, int64_t *cells_needed, int32_t *status, double *area_km2)
+{
+    if (!ctx || n < 0 || !cells_needed || !out_offs || !status) return DSSG_ERR_INVALID;
+    if (n > 0 && (!kind || !voff || !lat || !lng)) return DSSG_ERR_INVALID;
+    int64_t nvtx = n > 0 ? voff[n] : 0;
+    if (nvtx < 0) return DSSG_ERR_INVALID;
+    int code = DSSG_OK;
+    int rc = guarded(ctx, [&] {
+        hipStream_t s = ctx->stream;
+        const int32_t *dk = upload(ctx->d_kind, kind, n, s);
+        const int64_t *dv = upload(ctx->d_voff, voff, n + 1, s);
+        const double *dla = upload(ctx->d_lat, lat, nvtx, s);
+        const double *dln = upload(ctx->d_lng, lng, nvtx, s);
+        std::vector<float> zeros;
+        if (!radius_m) zeros.assign((size_t)(n > 0 ? n : 1), 0.0f);
+        const float *dr = upload(ctx->d_rad, radius_m ? radius_m : zeros.data(), n, s);
+        dssg_cells res;
+        ctx->cover.run(n, dk, dv, dla, dln, dr, s, &res);
+        DSS_HIP(hipMemcpyAsync(out_offs, res.offs, sizeof(int64_t) * (size_t)(n + 1), hipMemcpyDeviceToHost, s));
+        if (n > 0) DSS_HIP(hipMemcpyAsync(status, res.status, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, s));
+        if (n > 0 && area_km2)
+            DSS_HIP(hipMemcpyAsync(area_km2, res.area_km2, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, s));
+        *cells_needed = res.total_cells;
+        if (res.total_cells <= cells_cap && res.total_cells > 0) {
+            if (!out_cells) throw dss::Error(DSSG_ERR_INVALID, "out_cells is NULL");
+            DSS_HIP(hipMemcpyAsync(out_cells, res.cells, sizeof(uint64_t) * (size_t)res.total_cells, hipMemcpyDeviceToHost, s));
+        }
+        DSS_HIP(hipStreamSynchronize(s));
+        if (res.total_cells > cells_cap) code = DSSG_ERR_CAPACITY;
+    });
+    return rc ? rc : code;
+}
+
+int dssg_area_to_cell_ids(dssg_ctx *ctx, const char *area, uint64_t *out_cells, int64_t cap, int64_t *needed,
+                          int32_t *status, double *area_km2)
+{
+    if (!ctx || !area || !needed || !status) return DSSG_ERR_INVALID;
+    *needed = 0;
+    if (area_km2) *area_km2 = 0;
+    // pkg/geo/s2.go:136-142: count check precedes parsing.
+    std::string a(area);
+    int64_t num_coords = (int64_t)std::count(a.begin(), a.end(), ',') + 1;
+    if (num_coords % 2 == 1) { *status = DSSG_ST_ODD_COORDS; return DSSG_OK; }
+    if (num_coords / 2 < 3) { *status = DSSG_ST_NOT_ENOUGH_POINTS; return DSSG_OK; }
+    std::vector<double> lat, lng;
+    size_t pos = 0;
+    int64_t counter = 0;
+    double la = 0;
+    while (true) {  // bufio.Scanner with splitAtComma
+        size_t c = a.find(',', pos);
+        std::string tok = trim_space(a.substr(pos, c == std::string::npos ? std::string::npos : c - pos));
+        double v;
+        if (!go_parse_float(tok, v)) { *status = DSSG_ST_BAD_COORD_SET; return DSSG_OK; }
+        if (counter % 2 == 0) la = v;
+        else { lat.push_back(la); lng.push_back(v); }
+        counter++;
+        if (c == std::string::npos) break;
+        pos = c + 1;
+    }
+    int32_t kind = DSSG_KIND_POINTS;
+    int64_t voff[2] = {0, (int64_t)lat.size()};
+    float r = 0;
+    int64_t offs[2];
+    double ar = 0;
+    int rc = dssg_cover_batch(ctx, 1, &kind, voff, lat.data(), lng.data(), &r, offs, out_cells, cap, needed, status, &ar);
+    if (area_km2) *area_km2 = ar;
+    return rc;
+}
+
+int dssg_index_build_device(dssg_ctx *ctx, int64_t n, const int64_t *d_cell_offs, const uint64_t *d_cells,
+                            const float *d_alt_lo, const float *d_alt_hi, const int64_t *d_t0, const int64_t *d_t1,
+                            const int32_t *d_owner, void *stream, dssg_index **out)
+{
+    if (!ctx || !out || n < 0 || !d_cell_offs || (n > 0 && (!d_alt_lo || !d_alt_hi || !d_t0 || !d_t1)))
+        return DSSG_ERR_INVALID;
+    *out = nullptr;
+    dssg_index *idx = new (std::nothrow) dssg_index();
+    if (!idx) return DSSG_ERR_NOMEM;
+    idx->device = ctx->device;
+    int rc = guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        ctx->search.build(idx, n, d_cell_offs, d_cells, d_alt_lo, d_alt_hi, d_t0, d_t1, d_owner, s);
+    });
+    if (rc) {
+        delete idx;
+        return rc;
+    }
+    *out = idx;
+    return DSSG_OK;
+}
+
+int dssg_index_build(dssg_ctx *ctx, int64_t n, const int64_t *cell_offs, const uint64_t *cells, const float *alt_lo,
+                     const float *alt_hi, const int64_t *t0, const int64_t *t1, const int32_t *owner, dssg_index **out)
+{
+    if (!ctx || !out || n < 0 || !cell_offs) return DSSG_ERR_INVALID;
+    *out = nullptr;
+    int64_t P = cell_offs[n];
+    dss::DevBuf<int64_t> offs, dt0, dt1;
+    dss::DevBuf<uint64_t> dc;
+    dss::DevBuf<float> dlo, dhi;
+    dss::DevBuf<int32_t> down;
+    const int64_t *o = nullptr, *a0 = nullptr, *a1 = nullptr;
+    const uint64_t *c = nullptr;
+    const float *lo = nullptr, *hi = nullptr;
+    const int32_t *ow = nullptr;
+    int rc = guarded(ctx, [&] {
+        hipStream_t s = ctx->stream;
+        o = upload(offs, cell_offs, n + 1, s);
+        c = upload(dc, cells, P, s);
+        lo = upload(dlo, alt_lo, n, s);
+        hi = upload(dhi, alt_hi, n, s);
+        a0 = upload(dt0, t0, n, s);
+        a1 = upload(dt1, t1, n, s);
+        if (owner) ow = upload(down, owner, n, s);
+        DSS_HIP(hipStreamSynchronize(s));
+    });
+    if (rc) return rc;
+    return dssg_index_build_device(ctx, n, o, c, lo, hi, a0, a1, ow, nullptr, out);
+}
+
+void dssg_index_free(dssg_index *idx)
+{
+    if (!idx) return;
+    (void)hipSetDevice(idx->device);
+    delete idx;
+}
+int64_t dssg_index_num_postings(const dssg_index *idx) { return idx ? idx->n_p : 0; }
+int64_t dssg_index_num_cells(const dssg_index *idx) { return idx ? idx->n_reg : 0; }
+
+int dssg_search_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *d_q_offs,
+                       const uint64_t *d_q_cells, const float *d_q_alt_lo, const float *d_q_alt_hi,
+                       const int64_t *d_q_tlo, const int64_t *d_q_thi, const int32_t *d_q_owner, void *stream,
+                       dssg_pairs *out)
+{
+    if (!ctx || !idx || !out || nq < 0 || (nq > 0 && (!d_q_offs || !d_q_alt_lo || !d_q_alt_hi || !d_q_tlo || !d_q_thi)))
+        return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        if (ctx->timing) {
+            if (!ctx->ev0) { DSS_HIP(hipEventCreate(&ctx->ev0)); DSS_HIP(hipEventCreate(&ctx->ev1)); }
+            DSS_HIP(hipEventRecord(ctx->ev0, s));
+        }
+        ctx->search.search(idx, nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo, d_q_thi, d_q_owner, s, out);
+        if (ctx->timing) {
+            DSS_HIP(hipEventRecord(ctx->ev1, s));
+            DSS_HIP(hipEventSynchronize(ctx->ev1));
+            float ms = 0;
+            DSS_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+            ctx->join_ms = ms;
+        }
+    });
+}
+
+int dssg_search(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
+                const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
+                const int32_t *q_owner, uint32_t *out_q, uint32_t *out_e, int64_t cap, int64_t *needed)
+{
+    if (!ctx || !idx || !needed || nq < 0 || !q_offs) return DSSG_ERR_INVALID;
+    if (nq > 0 && (!q_alt_lo || !q_alt_hi || !q_tlo || !q_thi)) return DSSG_ERR_INVALID;
+    int code = DSSG_OK;
+    int rc = guarded(ctx, [&] {
+        // per-query sort + unique (CellUnion order; UnionVolumes4D output is
+        // unsorted, quirk Q14)
+        std::vector<int64_t> offs((size_t)nq + 1, 0);
+        std::vector<uint64_t> cells;
+        cells.reserve((size_t)q_offs[nq]);
+        for (int64_t q = 0; q < nq; q++) {
+            if (q_tlo[q] == INT64_MIN) throw dss::Error(DSSG_ERR_INVALID, "query tlo must not be NULL");
+            size_t b = cells.size();
+            cells.insert(cells.end(), q_cells + q_offs[q], q_cells + q_offs[q + 1]);
+            std::sort(cells.begin() + (long)b, cells.end());
+            cells.erase(std::unique(cells.begin() + (long)b, cells.end()), cells.end());
+            offs[(size_t)q + 1] = (int64_t)cells.size();
+        }
+        hipStream_t s = ctx->stream;
+        const int64_t *dqo = upload(ctx->d_qoffs, offs.data(), nq + 1, s);
+        const uint64_t *dqc = upload(ctx->d_cells, cells.data(), (int64_t)cells.size(), s);
+        const float *dlo = upload(ctx->d_alo, q_alt_lo, nq, s);
+        const float *dhi = upload(ctx->d_ahi, q_alt_hi, nq, s);
+        const int64_t *dtl = upload(ctx->d_tlo, q_tlo, nq, s);
+        const int64_t *dth = upload(ctx->d_thi, q_thi, nq, s);
+        const int32_t *dow = q_owner ? upload(ctx->d_owner, q_owner, nq, s) : nullptr;
+        dssg_pairs res;
+        ctx->search.search(idx, nq, dqo, dqc, dlo, dhi, dtl, dth, dow, s, &res);
+        *needed = res.n;
+        if (res.n > cap) {
+            code = DSSG_ERR_CAPACITY;
+            return;
+        }
+        if (res.n > 0) {
+            if (!out_q || !out_e) throw dss::Error(DSSG_ERR_INVALID, "output pointers are NULL");
+            DSS_HIP(hipMemcpyAsync(out_q, res.q, sizeof(uint32_t) * (size_t)res.n, hipMemcpyDeviceToHost, s));
+            DSS_HIP(hipMemcpyAsync(out_e, res.e, sizeof(uint32_t) * (size_t)res.n, hipMemcpyDeviceToHost, s));
+            DSS_HIP(hipStreamSynchronize(s));
+            sort_pairs_host(out_q, out_e, res.n);
+        }
+    });
+    return rc ? rc : code;
+}
+
+int dssg_search_operations(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *q_offs,
+                           const uint64_t *q_cells, const float *q_alt_lo, const float *q_alt_hi,
+                           const int64_t *q_start, const int64_t *q_end, int64_t now_us, uint32_t *out_q,
+                           uint32_t *out_e, int64_t cap, int64_t *needed)
+{
+    if (nq < 0 || (nq > 0 && (!q_start || !q_end))) return DSSG_ERR_INVALID;
+    if (now_us == INT64_MIN) return DSSG_ERR_INVALID;
+    // operations.go:398-402: COALESCE(ends_at >= start, true) AND ends_at >= now
+    std::vector<int64_t> tlo((size_t)nq), thi((size_t)nq);
+    for (int64_t q = 0; q < nq; q++) {
+        tlo[q] = std::max(q_start[q], now_us);
+        thi[q] = q_end[q];
+    }
+    return dssg_search(ctx, idx, nq, q_offs, q_cells, q_alt_lo, q_alt_hi, tlo.data(), thi.data(), nullptr, out_q, out_e,
+                       cap, needed);
+}
+
+int dssg_search_isas(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
+                     const int64_t *earliest, const int64_t *latest, uint32_t *out_q, uint32_t *out_e, int64_t cap,
+                     int64_t *needed)
+{
+    if (nq < 0 || (nq > 0 && (!earliest || !latest))) return DSSG_ERR_INVALID;
+    // identification_service_area.go:176-180: ends_at >= earliest AND
+    // COALESCE(starts_at <= latest, true); no altitude predicate.
+    std::vector<float> lo((size_t)nq, -INFINITY), hi((size_t)nq, INFINITY);
+    return dssg_search(ctx, idx, nq, q_offs, q_cells, lo.data(), hi.data(), earliest, latest, nullptr, out_q, out_e, cap,
+                       needed);
+}
+
+int dssg_search_subscriptions(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *q_offs,
+                              const uint64_t *q_cells, const int32_t *owner, int64_t now_us, uint32_t *out_q,
+                              uint32_t *out_e, int64_t cap, int64_t *needed)
+{
+    if (nq < 0 || now_us == INT64_MIN) return DSSG_ERR_INVALID;
+    // subscriptions.go:229-232,256-260: cells && $1 [AND owner = $2] AND ends_at >= now
+    std::vector<float> lo((size_t)nq, -INFINITY), hi((size_t)nq, INFINITY);
+    std::vector<int64_t> tlo((size_t)nq, now_us), thi((size_t)nq, INT64_MAX);
+    return dssg_search(ctx, idx, nq, q_offs, q_cells, lo.data(), hi.data(), tlo.data(), thi.data(), owner, out_q, out_e,
+                       cap, needed);
+}
+
+int dssg_copy_to_host(dssg_ctx *ctx, void *dst, const void *src, size_t bytes)
+{
+    if (!ctx || (bytes && (!dst || !src))) return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        if (bytes) DSS_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    });
+}
+
+int dssg_selftest_math(dssg_ctx *ctx, int op, int64_t n, const double *x, const double *y, double *out)
+{
+    if (!ctx || n < 0 || (n > 0 && (!x || !out))) return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        if (n) dss::selftest_math(op, n, x, y, out, ctx->stream);
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,59 @@
+// Shared host-side plumbing for the dss_amd HIP library: error handling,
+// grow-only device buffers, scans.  No torch types anywhere in the library.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "../../include/dssgpu.h"
+
+namespace dss {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+#define DSS_HIP(expr)                                                                                     \
+    do {                                                                                                  \
+        hipError_t e_ = (expr);                                                                           \
+        if (e_ != hipSuccess)                                                                             \
+            throw ::dss::Error(DSSG_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));      \
+    } while (0)
+
+// Grow-only device allocation; contents are not preserved on growth.
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    T *ensure(size_t n)
+    {
+        if (n <= cap && p) return p;
+        release();
+        size_t c = n < 16 ? 16 : n + n / 4;
+        DSS_HIP(hipMalloc(&p, c * sizeof(T)));
+        cap = c;
+        return p;
+    }
+};
+
+inline unsigned grid_for(int64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
+
+// Exclusive prefix sum of n int64 values into out (n+1 entries, out[n] = total),
+// returns nothing; implemented in scan.hip with hipcub.
+void selftest_math(int op, int64_t n, const double *x, const double *y, double *out, hipStream_t s);
+void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, DevBuf<unsigned char> &tmp, hipStream_t s);
+
+}  // namespace dss

@@ -1,0 +1,627 @@
+// Level-13 S2 covering of DSS footprints on gfx950.
+//
+// Reference semantics: pkg/geo/s2.go:99-122 (Covering: area check, in-place
+// reversal, zero-area -> open polyline), pkg/models/geo.go:224-268 (circle
+// 20-gon, polygon range checks), golang/geo RegionCoverer{13,13}: the result
+// is the sorted set of level-13 cells c with region.IntersectsCell(c).
+//
+// Pipeline (one batch of N footprints, all device resident):
+//   k_nverts   vertex slots per footprint (polygon V, circle 20) -> scan
+//   k_setup    one thread per footprint: lat/lng -> S2 xyz with Go's Cephes
+//              trig, RegularLoop, loop origin containment, Loop.Area,
+//              reversal, status/mode, touched-face mask
+//   k_clip     ClipToPaddedFace of every edge on every touched face, with the
+//              exact reference padding (fine, level-13 decisions) and a
+//              1e-9 padding (coarse, pruning only)
+//   k_start    <= 4 start cells per face around the clipped-edge bound
+//   k_expand_* level-synchronous descent over ALL footprints' frontier nodes
+//              at once.  Coarse levels prune with the enlarged padding; a node
+//              no edge touches is uniform: its centre's containment decides
+//              the whole subtree (emitted as a range).  Level 13 applies the
+//              reference test exactly.  Children are written in Hilbert (=id)
+//              order behind an exclusive scan, so each footprint's output is
+//              sorted by construction -- no sort pass.
+//   k_emit     expand ranges into level-13 ids (CSR per footprint).
+// Roofline: FP64 VALU (edge clip / crossing tests); see DESIGN.md.
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "cover.hpp"
+#include "loopdev.cuh"
+
+namespace dss {
+using namespace s2;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr double kCoarsePad = 1e-9;  // pruning padding, >> FACE_CLIP_PLUS_RECT_ERR (2.36e-15)
+constexpr double kFinePad = DSS_FACE_CLIP_PLUS_RECT_ERR;
+
+enum : uint8_t { MODE_NONE = 0, MODE_LOOP = 1, MODE_POLYLINE = 2 };
+enum : uint8_t { FL_SMALL = 1 };
+// node meta: level (bits 0-4), orientation (5-6), done (7), face (8-10)
+__device__ __forceinline__ uint32_t pack_meta(int level, int orient, int done, int face)
+{
+    return (uint32_t)level | ((uint32_t)orient << 5) | ((uint32_t)done << 7) | ((uint32_t)face << 8);
+}
+__device__ __forceinline__ int meta_level(uint32_t m) { return (int)(m & 31u); }
+__device__ __forceinline__ int meta_orient(uint32_t m) { return (int)((m >> 5) & 3u); }
+__device__ __forceinline__ int meta_done(uint32_t m) { return (int)((m >> 7) & 1u); }
+__device__ __forceinline__ int meta_face(uint32_t m) { return (int)((m >> 8) & 7u); }
+
+__device__ __forceinline__ int64_t tid64() { return (int64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+
+__global__ void k_nverts(int64_t n, const int32_t *kind, const int64_t *voff, int64_t *nv)
+{
+    int64_t f = tid64();
+    if (f >= n) return;
+    nv[f] = kind[f] == DSSG_KIND_CIRCLE ? 20 : (voff[f + 1] - voff[f]);
+}
+
+__device__ bool edge_inside_face(V3 a, V3 b, int face)
+{
+    if (xyz_face(a) != face || xyz_face(b) != face) return false;
+    double u0, v0, u1, v1;
+    valid_face_xyz_to_uv(face, a, u0, v0);
+    valid_face_xyz_to_uv(face, b, u1, v1);
+    const double lim = 1.0 - 1e-6;
+    return __builtin_fabs(u0) <= lim && __builtin_fabs(v0) <= lim && __builtin_fabs(u1) <= lim &&
+           __builtin_fabs(v1) <= lim;
+}
+
+// One thread per footprint.
+__global__ void k_setup(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
+                        const float *radius_m, const int64_t *xoff, V3 *xyz, int32_t *status, double *area_out,
+                        uint8_t *mode, uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx)
+{
+    int64_t f = tid64();
+    if (f >= n) return;
+    int k = kind[f];
+    int64_t v0 = voff[f];
+    V3 *p = xyz + xoff[f];
+    int st = DSSG_ST_OK;
+    uint8_t md = MODE_NONE;
+    double area = 0;
+    int nv = 0;
+    bool small = false;
+    LoopView l{p, 0, false};
+    if (k == DSSG_KIND_CIRCLE) {
+        double la = lat[v0], ln = lng[v0];
+        float r = radius_m[f];
+        if (la > 90.0 || la < -90.0 || ln > 180.0 || ln < -180.0) st = DSSG_ST_BAD_COORD_SET;
+        else if (!(r > 0)) st = DSSG_ST_RADIUS;
+        else {
+            // regular_loop.go RegularLoop(center, DistanceMetersToAngle(r), 20)
+            V3 c = point_from_degrees(la, ln);
+            double radius = (double)r / DSS_RADIUS_EARTH_M;
+            V3 c1 = ortho(c), c0 = cross(c1, c);
+            double z = go_cos(radius), rr = go_sin(radius);
+            double step = 2 * DSS_PI / 20.0;
+            for (int i = 0; i < 20; i++) {
+                double ang = (double)i * step;
+                double px = rr * go_cos(ang), py = rr * go_sin(ang), pz = z;
+                V3 q = v3(c0.x * px + c1.x * py + c.x * pz, c0.y * px + c1.y * py + c.y * pz,
+                          c0.z * px + c1.z * py + c.z * pz);
+                p[i] = normalize(q);
+            }
+            nv = 20;
+            l.n = 20;
+            loop_init_origin(l);
+            md = MODE_LOOP;
+            small = radius < 0.5;
+        }
+    } else {
+        nv = (int)(voff[f + 1] - v0);
+        if (k == DSSG_KIND_POLYGON) {  // Q17: range check precedes the count check
+            for (int i = 0; i < nv; i++) {
+                double la = lat[v0 + i], ln = lng[v0 + i];
+                if (la > 90.0 || la < -90.0 || ln > 180.0 || ln < -180.0) { st = DSSG_ST_BAD_COORD_SET; break; }
+            }
+        }
+        if (st == DSSG_ST_OK && nv < 3) st = DSSG_ST_NOT_ENOUGH_POINTS;
+        if (st == DSSG_ST_OK) {
+            for (int i = 0; i < nv; i++) p[i] = point_from_degrees(lat[v0 + i], lng[v0 + i]);
+            l.n = nv;
+            loop_init_origin(l);
+            area = loop_area_km2(l);
+            if (area > DSS_MAX_AREA_KM2) {  // Q4: reverse in place and rebuild
+                for (int i = 0, j = nv - 1; i < j; i++, j--) {
+                    V3 t = p[i];
+                    p[i] = p[j];
+                    p[j] = t;
+                }
+                loop_init_origin(l);
+            }
+            area = loop_area_km2(l);
+            if (area > DSS_MAX_AREA_KM2) st = DSSG_ST_AREA_TOO_LARGE;
+            else if (area <= 0) md = MODE_POLYLINE;  // Q3: open polyline, no closing edge
+            else { md = MODE_LOOP; small = true; }
+        }
+    }
+    uint8_t mask = 0;
+    bool inner = true;
+    if (md != MODE_NONE) {
+        int ne = md == MODE_LOOP ? nv : nv - 1;
+        int face0 = xyz_face(p[0]);
+        for (int e = 0; e < ne; e++) {
+            V3 a = p[e], b = p[(e + 1) % nv];
+            if (edge_inside_face(a, b, face0)) { mask |= (uint8_t)(1u << face0); continue; }
+            inner = false;
+            for (int fc = 0; fc < 6; fc++) {
+                double uv[4];
+                if (clip_to_padded_face(a, b, fc, kCoarsePad, uv)) mask |= (uint8_t)(1u << fc);
+            }
+        }
+        if (md == MODE_POLYLINE) {
+            for (int i = 0; i < nv; i++)
+                for (int fc = 0; fc < 6; fc++) {
+                    double u, v;
+                    if (face_xyz_to_uv(fc, p[i], u, v) && __builtin_fabs(u) <= 1 + kCoarsePad &&
+                        __builtin_fabs(v) <= 1 + kCoarsePad)
+                        mask |= (uint8_t)(1u << fc);
+                }
+        }
+    }
+    status[f] = st;
+    area_out[f] = area;
+    mode[f] = md;
+    origin_in[f] = l.origin_inside ? 1 : 0;
+    fmask[f] = mask;
+    // bbox-limited start is valid for polylines (no interior) and for loops
+    // whose edges all lie inside one face and whose interior is the small side.
+    flags[f] = (md == MODE_POLYLINE || (md == MODE_LOOP && inner && small && __builtin_popcount(mask) == 1)) ? FL_SMALL : 0;
+    nvx[f] = nv;
+}
+
+__device__ __forceinline__ int num_edges(uint8_t md, int nv) { return md == MODE_LOOP ? nv : (md == MODE_POLYLINE ? nv - 1 : 0); }
+
+__global__ void k_edge_counts(int64_t n, const uint8_t *mode, const uint8_t *fmask, const int32_t *nvx, int64_t *cnt)
+{
+    int64_t f = tid64();
+    if (f >= n) return;
+    cnt[f] = (int64_t)__builtin_popcount(fmask[f]) * num_edges(mode[f], nvx[f]);
+}
+
+// Clip every edge to every touched face (ascending face order).
+__global__ void k_clip(int64_t n, const int64_t *xoff, const V3 *xyz, const uint8_t *mode, const uint8_t *fmask,
+                       const int32_t *nvx, const int64_t *eoff, double4 *clip_f, double4 *clip_c, uint8_t *cflags)
+{
+    int64_t f = tid64();
+    if (f >= n) return;
+    uint8_t md = mode[f];
+    if (md == MODE_NONE) return;
+    int nv = nvx[f], ne = num_edges(md, nv);
+    const V3 *p = xyz + xoff[f];
+    int64_t base = eoff[f];
+    int fi = 0;
+    for (int fc = 0; fc < 6; fc++) {
+        if (!(fmask[f] >> fc & 1)) continue;
+        for (int e = 0; e < ne; e++) {
+            V3 a = p[e], b = p[(e + 1) % nv];
+            double uf[4], uc[4];
+            bool okf = clip_to_padded_face(a, b, fc, kFinePad, uf);
+            bool okc = clip_to_padded_face(a, b, fc, kCoarsePad, uc);
+            int64_t k = base + (int64_t)fi * ne + e;
+            clip_f[k] = make_double4(uf[0], uf[1], uf[2], uf[3]);
+            clip_c[k] = make_double4(uc[0], uc[1], uc[2], uc[3]);
+            cflags[k] = (uint8_t)((okf ? 1 : 0) | (okc ? 2 : 0));
+        }
+        fi++;
+    }
+}
+
+struct FaceBox {
+    double ulo, uhi, vlo, vhi;
+};
+
+// Coarse bound of footprint f on face fc (clipped edges, plus polyline vertex
+// projections), expanded by the coarse padding.  Returns false if empty.
+__device__ bool face_box(const V3 *p, int nv, uint8_t md, const double4 *clip_c, const uint8_t *cflags, int64_t base,
+                         int ne, FaceBox &b, int fc)
+{
+    double ulo = 1e300, uhi = -1e300, vlo = 1e300, vhi = -1e300;
+    bool any = false;
+    for (int e = 0; e < ne; e++) {
+        if (!(cflags[base + e] & 2)) continue;
+        double4 c = clip_c[base + e];
+        ulo = fmin(ulo, fmin(c.x, c.z));
+        uhi = fmax(uhi, fmax(c.x, c.z));
+        vlo = fmin(vlo, fmin(c.y, c.w));
+        vhi = fmax(vhi, fmax(c.y, c.w));
+        any = true;
+    }
+    if (md == MODE_POLYLINE) {
+        for (int i = 0; i < nv; i++) {
+            double u, v;
+            if (face_xyz_to_uv(fc, p[i], u, v) && __builtin_fabs(u) <= 1 + kCoarsePad && __builtin_fabs(v) <= 1 + kCoarsePad) {
+                ulo = fmin(ulo, u); uhi = fmax(uhi, u);
+                vlo = fmin(vlo, v); vhi = fmax(vhi, v);
+                any = true;
+            }
+        }
+    }
+    const double m = 1e-7;  // generous: the start region only has to contain the bound
+    b = FaceBox{ulo - m, uhi + m, vlo - m, vhi + m};
+    return any;
+}
+
+// Start cells for one face: <= 2x2 block of cells at the deepest level (<=13)
+// whose i and j spans cover the bound.  Writes up to 4 (id, i0, j0, meta)
+// sorted by id; returns the count.
+__device__ int start_cells(const FaceBox &b, int fc, uint64_t *id, uint32_t *ii, uint32_t *jj, uint32_t *meta)
+{
+    double ulo = fmax(b.ulo, -1.0), uhi = fmin(b.uhi, 1.0), vlo = fmax(b.vlo, -1.0), vhi = fmin(b.vhi, 1.0);
+    int i0 = st_to_ij(uv_to_st(ulo)), i1 = st_to_ij(uv_to_st(uhi));
+    int j0 = st_to_ij(uv_to_st(vlo)), j1 = st_to_ij(uv_to_st(vhi));
+    int L = kCoverLevel;
+    while (L > 0 && (((i1 >> (kMaxLevel - L)) - (i0 >> (kMaxLevel - L))) > 1 || ((j1 >> (kMaxLevel - L)) - (j0 >> (kMaxLevel - L))) > 1))
+        L--;
+    int sh = kMaxLevel - L;
+    int cnt = 0;
+    for (int a = i0 >> sh; a <= (i1 >> sh); a++)
+        for (int c = j0 >> sh; c <= (j1 >> sh); c++) {
+            int o;
+            uint64_t cid = cell_from_face_ij_level(fc, a << sh, c << sh, L, o);
+            // insertion sort by id
+            int k = cnt++;
+            while (k > 0 && id[k - 1] > cid) {
+                id[k] = id[k - 1]; ii[k] = ii[k - 1]; jj[k] = jj[k - 1]; meta[k] = meta[k - 1];
+                k--;
+            }
+            id[k] = cid;
+            ii[k] = (uint32_t)(a << sh);
+            jj[k] = (uint32_t)(c << sh);
+            meta[k] = pack_meta(L, o, 0, fc);
+        }
+    return cnt;
+}
+
+// Face-cell id for face fc (level 0).
+__device__ __forceinline__ uint64_t face_cell(int fc) { return ((uint64_t)fc << 61) | (1ull << 60); }
+
+__device__ V3 node_center(int face, uint32_t i0, uint32_t j0, int level)
+{
+    // cellid.go faceSiTi / rawPoint: centre in (si, ti) = 2*i0 + size, exact.
+    double size = (double)(1u << (kMaxLevel - level));
+    const double half = 0.5 / (double)kMaxSize;
+    double s = half * (2.0 * (double)i0 + size), t = half * (2.0 * (double)j0 + size);
+    return normalize(face_uv_to_xyz(face, st_to_uv(s), st_to_uv(t)));
+}
+
+// Count (pass 0) or write (pass 1) start nodes; big loops also get whole-face
+// nodes for faces without edges whose centre the loop contains.
+template <int PASS>
+__global__ void k_start(int64_t n, const int64_t *xoff, const V3 *xyz, const uint8_t *mode, const uint8_t *fmask,
+                        const uint8_t *flags, const uint8_t *origin_in, const int32_t *nvx, const int64_t *eoff,
+                        const double4 *clip_c, const uint8_t *cflags, int64_t *cnt, const int64_t *soff,
+                        uint32_t *nf, uint64_t *nid, uint32_t *ni, uint32_t *nj, uint32_t *nmeta)
+{
+    int64_t f = tid64();
+    if (f >= n) return;
+    uint8_t md = mode[f];
+    int64_t c = 0;
+    if (md != MODE_NONE) {
+        int nv = nvx[f], ne = num_edges(md, nv);
+        const V3 *p = xyz + xoff[f];
+        LoopView l{p, nv, origin_in[f] != 0};
+        int64_t w = PASS ? soff[f] : 0;
+        int fi = 0;
+        for (int fc = 0; fc < 6; fc++) {
+            bool touched = (fmask[f] >> fc) & 1;
+            if (!touched) {
+                if (md == MODE_LOOP && !(flags[f] & FL_SMALL)) {
+                    V3 ctr = node_center(fc, 0, 0, 0);
+                    if (loop_contains(l, ctr)) {
+                        if (PASS) {
+                            nf[w] = (uint32_t)f; nid[w] = face_cell(fc); ni[w] = 0; nj[w] = 0;
+                            nmeta[w] = pack_meta(0, fc & 1, 1, fc);
+                            w++;
+                        }
+                        c++;
+                    }
+                }
+                continue;
+            }
+            if (flags[f] & FL_SMALL) {
+                FaceBox b;
+                if (face_box(p, nv, md, clip_c, cflags, eoff[f] + (int64_t)fi * ne, ne, b, fc)) {
+                    uint64_t id[4];
+                    uint32_t ii[4], jj[4], mt[4];
+                    int k = start_cells(b, fc, id, ii, jj, mt);
+                    if (PASS)
+                        for (int q = 0; q < k; q++, w++) {
+                            nf[w] = (uint32_t)f; nid[w] = id[q]; ni[w] = ii[q]; nj[w] = jj[q]; nmeta[w] = mt[q];
+                        }
+                    c += k;
+                }
+            } else {
+                if (PASS) {
+                    nf[w] = (uint32_t)f; nid[w] = face_cell(fc); ni[w] = 0; nj[w] = 0;
+                    nmeta[w] = pack_meta(0, fc & 1, 0, fc);
+                    w++;
+                }
+                c++;
+            }
+            fi++;
+        }
+    }
+    if (!PASS) cnt[f] = c;
+}
+
+// golang/geo polyline.go Polyline.IntersectsCell for a level-13 node.
+__device__ bool polyline_intersects_cell(const V3 *p, int nv, int face, double ulo, double uhi, double vlo, double vhi)
+{
+    if (nv == 0) return false;
+    const double m = DSS_DBL_EPS;  // cell.go ContainsPoint: uv bound expanded by dblEpsilon
+    for (int i = 0; i < nv; i++) {
+        double u, v;
+        if (face_xyz_to_uv(face, p[i], u, v) && (ulo - m) <= u && u <= (uhi + m) && (vlo - m) <= v && v <= (vhi + m))
+            return true;
+    }
+    V3 cv[4] = {normalize(face_uv_to_xyz(face, ulo, vlo)), normalize(face_uv_to_xyz(face, uhi, vlo)),
+                normalize(face_uv_to_xyz(face, uhi, vhi)), normalize(face_uv_to_xyz(face, ulo, vhi))};
+    for (int j = 0; j < 4; j++) {
+        EdgeCrosser e;
+        e.init(cv[j], cv[(j + 1) & 3]);
+        e.restart_at(p[0]);
+        for (int i = 1; i < nv; i++)
+            if (e.chain_crossing_sign(p[i]) != DO_NOT_CROSS) return true;
+    }
+    return false;
+}
+
+// Classify each frontier node: 0 drop, 1 keep (done), 2 subdivide (4 children).
+__global__ void k_expand_count(int64_t nn, const uint32_t *nf, const uint32_t *ni, const uint32_t *nj,
+                               const uint32_t *nmeta, uint8_t *act, int64_t *cnt, const int64_t *xoff, const V3 *xyz,
+                               const uint8_t *mode, const uint8_t *fmask, const uint8_t *origin_in, const int32_t *nvx,
+                               const int64_t *eoff, const double4 *clip_f, const double4 *clip_c, const uint8_t *cflags)
+{
+    int64_t k = tid64();
+    if (k >= nn) return;
+    uint32_t m = nmeta[k];
+    uint8_t a;
+    if (meta_done(m)) {
+        a = 1;
+    } else {
+        uint32_t f = nf[k];
+        int level = meta_level(m), face = meta_face(m);
+        uint8_t md = mode[f];
+        int nv = nvx[f], ne = num_edges(md, nv);
+        uint8_t mask = fmask[f];
+        int fi = __builtin_popcount((unsigned)mask & ((1u << face) - 1u));
+        int64_t base = eoff[f] + (int64_t)fi * ne;
+        uint32_t size = 1u << (kMaxLevel - level);
+        double ulo = st_to_uv((double)ni[k] / (double)kMaxSize), uhi = st_to_uv((double)(ni[k] + size) / (double)kMaxSize);
+        double vlo = st_to_uv((double)nj[k] / (double)kMaxSize), vhi = st_to_uv((double)(nj[k] + size) / (double)kMaxSize);
+        const V3 *p = xyz + xoff[f];
+        if (level < kCoverLevel) {
+            const double pm = kCoarsePad;
+            bool hit = false;
+            for (int e = 0; e < ne && !hit; e++) {
+                if (!(cflags[base + e] & 2)) continue;
+                double4 c = clip_c[base + e];
+                hit = edge_intersects_rect(c.x, c.y, c.z, c.w, ulo - pm, uhi + pm, vlo - pm, vhi + pm);
+            }
+            if (!hit && md == MODE_POLYLINE) {
+                for (int i = 0; i < nv && !hit; i++) {
+                    double u, v;
+                    hit = face_xyz_to_uv(face, p[i], u, v) && (ulo - pm) <= u && u <= (uhi + pm) && (vlo - pm) <= v && v <= (vhi + pm);
+                }
+            }
+            if (hit) a = 2;
+            else if (md == MODE_LOOP) {
+                LoopView l{p, nv, origin_in[f] != 0};
+                a = loop_contains(l, node_center(face, ni[k], nj[k], level)) ? 1 : 0;
+            } else a = 0;
+        } else {
+            bool in;
+            if (md == MODE_LOOP) {
+                // loop.go IntersectsCell: padded edge test, else centre containment
+                const double pm = kFinePad;
+                in = false;
+                for (int e = 0; e < ne && !in; e++) {
+                    if (!(cflags[base + e] & 1)) continue;
+                    double4 c = clip_f[base + e];
+                    in = edge_intersects_rect(c.x, c.y, c.z, c.w, ulo - pm, uhi + pm, vlo - pm, vhi + pm);
+                }
+                if (!in) {
+                    LoopView l{p, nv, origin_in[f] != 0};
+                    in = loop_contains(l, node_center(face, ni[k], nj[k], level));
+                }
+            } else {
+                in = polyline_intersects_cell(p, nv, face, ulo, uhi, vlo, vhi);
+            }
+            a = in ? 1 : 0;
+        }
+    }
+    act[k] = a;
+    cnt[k] = a == 2 ? 4 : a;
+}
+
+__global__ void k_expand_write(int64_t nn, const uint32_t *nf, const uint64_t *nid, const uint32_t *ni, const uint32_t *nj,
+                               const uint32_t *nmeta, const uint8_t *act, const int64_t *pos, uint32_t *of, uint64_t *oid,
+                               uint32_t *oi, uint32_t *oj, uint32_t *ometa, int *any_open)
+{
+    int64_t k = tid64();
+    if (k >= nn) return;
+    uint8_t a = act[k];
+    if (a == 0) return;
+    int64_t w = pos[k];
+    uint32_t m = nmeta[k];
+    if (a == 1) {
+        of[w] = nf[k]; oid[w] = nid[k]; oi[w] = ni[k]; oj[w] = nj[k];
+        ometa[w] = m | (1u << 7);  // done
+        return;
+    }
+    int level = meta_level(m), o = meta_orient(m), face = meta_face(m);
+    uint64_t id = nid[k];
+    uint64_t lsb = lsb_for_level(level);
+    uint64_t child = id - lsb + (lsb >> 2);  // cellid.go ChildBegin
+    uint32_t half = 1u << (kMaxLevel - level - 1);
+    for (int c = 0; c < 4; c++, child += (lsb >> 1)) {
+        int ij = pos_to_ij(o, c);
+        of[w + c] = nf[k];
+        oid[w + c] = child;
+        oi[w + c] = ni[k] + ((ij >> 1) ? half : 0);
+        oj[w + c] = nj[k] + ((ij & 1) ? half : 0);
+        ometa[w + c] = pack_meta(level + 1, o ^ pos_to_orientation(c), 0, face);
+    }
+    *any_open = 1;
+}
+
+// Final items -> per-footprint counts.
+__global__ void k_item_counts(int64_t nn, const uint32_t *nf, const uint32_t *nmeta, int64_t *icnt, unsigned long long *fcnt)
+{
+    int64_t k = tid64();
+    if (k >= nn) return;
+    int level = meta_level(nmeta[k]);
+    int64_t c = (int64_t)1 << (2 * (kCoverLevel - level));
+    icnt[k] = c;
+    atomicAdd(&fcnt[nf[k]], (unsigned long long)c);
+}
+
+__global__ void k_emit(int64_t nn, const uint64_t *nid, const uint32_t *nmeta, const int64_t *ipos, uint64_t *cells,
+                       uint32_t *big, int *nbig)
+{
+    int64_t k = tid64();
+    if (k >= nn) return;
+    int level = meta_level(nmeta[k]);
+    int64_t c = (int64_t)1 << (2 * (kCoverLevel - level));
+    uint64_t id = nid[k];
+    if (c > 256) {
+        big[atomicAdd(nbig, 1)] = (uint32_t)k;
+        return;
+    }
+    uint64_t lsb13 = lsb_for_level(kCoverLevel);
+    uint64_t first = id - cellid_lsb_dev(id) + lsb13;
+    int64_t w = ipos[k];
+    for (int64_t q = 0; q < c; q++) cells[w + q] = first + (uint64_t)q * (lsb13 << 1);
+}
+
+__global__ void k_emit_big(const uint32_t *big, const uint64_t *nid, const uint32_t *nmeta, const int64_t *ipos, uint64_t *cells)
+{
+    uint32_t k = big[blockIdx.x];
+    int level = meta_level(nmeta[k]);
+    int64_t c = (int64_t)1 << (2 * (kCoverLevel - level));
+    uint64_t id = nid[k];
+    uint64_t lsb13 = lsb_for_level(kCoverLevel);
+    uint64_t first = id - cellid_lsb_dev(id) + lsb13;
+    int64_t w = ipos[k];
+    for (int64_t q = threadIdx.x; q < c; q += blockDim.x) cells[w + q] = first + (uint64_t)q * (lsb13 << 1);
+}
+
+__global__ void k_u64_to_i64(int64_t n, const unsigned long long *a, int64_t *b)
+{
+    int64_t k = tid64();
+    if (k < n) b[k] = (int64_t)a[k];
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- host side
+void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
+                      const float *radius_m, hipStream_t s, dssg_cells *out)
+{
+    const unsigned B = kBlock;
+    out->n = n;
+    int64_t *nv = cnt_.ensure(n + 1);
+    int64_t *xoff = xoff_.ensure(n + 1);
+    int32_t *status = status_.ensure(n + 1);
+    double *area = area_.ensure(n + 1);
+    uint8_t *mode = mode_.ensure(n + 1), *orig = orig_.ensure(n + 1), *fmask = fmask_.ensure(n + 1),
+            *flags = flags_.ensure(n + 1);
+    int32_t *nvx = nvx_.ensure(n + 1);
+    int64_t *offs = offs_.ensure(n + 1);
+    if (n == 0) {
+        DSS_HIP(hipMemsetAsync(offs, 0, sizeof(int64_t), s));
+        out->offs = offs; out->cells = cells_.ensure(1); out->status = status; out->area_km2 = area; out->total_cells = 0;
+        return;
+    }
+    hipLaunchKernelGGL(k_nverts, dim3(grid_for(n, B)), dim3(B), 0, s, n, kind, voff, nv);
+    exclusive_scan_i64(nv, xoff, n, tmp_, s);
+    int64_t nx = 0;
+    DSS_HIP(hipMemcpyAsync(&nx, xoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    V3 *xyz = (V3 *)xyz_.ensure((size_t)nx * 3 + 3);
+    hipLaunchKernelGGL(k_setup, dim3(grid_for(n, 64)), dim3(64), 0, s, n, kind, voff, lat, lng, radius_m, xoff, xyz,
+                       status, area, mode, orig, fmask, flags, nvx);
+    int64_t *eoff = eoff_.ensure(n + 1);
+    hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, nvx, nv);
+    exclusive_scan_i64(nv, eoff, n, tmp_, s);
+    int64_t ne = 0;
+    DSS_HIP(hipMemcpyAsync(&ne, eoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    double4 *clip_f = clipf_.ensure(ne + 1), *clip_c = clipc_.ensure(ne + 1);
+    uint8_t *cflags = cflags_.ensure(ne + 1);
+    hipLaunchKernelGGL(k_clip, dim3(grid_for(n, 64)), dim3(64), 0, s, n, xoff, xyz, mode, fmask, nvx, eoff, clip_f,
+                       clip_c, cflags);
+    // start nodes
+    int64_t *soff = soff_.ensure(n + 1);
+    hipLaunchKernelGGL(k_start<0>, dim3(grid_for(n, 64)), dim3(64), 0, s, n, xoff, xyz, mode, fmask, flags, orig, nvx,
+                       eoff, clip_c, cflags, nv, soff, nullptr, nullptr, nullptr, nullptr, nullptr);
+    exclusive_scan_i64(nv, soff, n, tmp_, s);
+    int64_t nn = 0;
+    DSS_HIP(hipMemcpyAsync(&nn, soff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    int cur = 0;
+    Frontier *F = &fr_[cur];
+    F->ensure(nn + 1);
+    hipLaunchKernelGGL(k_start<1>, dim3(grid_for(n, 64)), dim3(64), 0, s, n, xoff, xyz, mode, fmask, flags, orig, nvx,
+                       eoff, clip_c, cflags, nullptr, soff, F->f.p, F->id.p, F->i.p, F->j.p, F->meta.p);
+    int *any_open = flag_.ensure(1);
+    for (int iter = 0; iter < 32 && nn > 0; iter++) {
+        uint8_t *act = act_.ensure(nn + 1);
+        int64_t *c = ncnt_.ensure(nn + 1);
+        int64_t *pos = npos_.ensure(nn + 1);
+        hipLaunchKernelGGL(k_expand_count, dim3(grid_for(nn, 64)), dim3(64), 0, s, nn, F->f.p, F->i.p, F->j.p, F->meta.p,
+                           act, c, xoff, xyz, mode, fmask, orig, nvx, eoff, clip_f, clip_c, cflags);
+        exclusive_scan_i64(c, pos, nn, tmp_, s);
+        int64_t nn2 = 0;
+        DSS_HIP(hipMemcpyAsync(&nn2, pos + nn, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipMemsetAsync(any_open, 0, sizeof(int), s));
+        DSS_HIP(hipStreamSynchronize(s));
+        Frontier *G = &fr_[cur ^ 1];
+        G->ensure(nn2 + 1);
+        hipLaunchKernelGGL(k_expand_write, dim3(grid_for(nn, B)), dim3(B), 0, s, nn, F->f.p, F->id.p, F->i.p, F->j.p,
+                           F->meta.p, act, pos, G->f.p, G->id.p, G->i.p, G->j.p, G->meta.p, any_open);
+        int open = 0;
+        DSS_HIP(hipMemcpyAsync(&open, any_open, sizeof(int), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipStreamSynchronize(s));
+        cur ^= 1;
+        F = G;
+        nn = nn2;
+        if (!open) break;
+    }
+    // items -> CSR
+    unsigned long long *fcnt = fcnt_.ensure(n + 1);
+    DSS_HIP(hipMemsetAsync(fcnt, 0, sizeof(unsigned long long) * (n + 1), s));
+    int64_t *icnt = ncnt_.ensure(nn + 1), *ipos = npos_.ensure(nn + 1);
+    if (nn > 0)
+        hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nn, B)), dim3(B), 0, s, nn, F->f.p, F->meta.p, icnt, fcnt);
+    int64_t *fc64 = fc64_.ensure(n + 1);
+    hipLaunchKernelGGL(k_u64_to_i64, dim3(grid_for(n, B)), dim3(B), 0, s, n, fcnt, fc64);
+    exclusive_scan_i64(fc64, offs, n, tmp_, s);
+    int64_t total = 0;
+    if (nn > 0) exclusive_scan_i64(icnt, ipos, nn, tmp_, s);
+    DSS_HIP(hipMemcpyAsync(&total, offs + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    uint64_t *cells = cells_.ensure(total + 1);
+    if (nn > 0) {
+        uint32_t *big = big_.ensure(nn + 1);
+        int *nbig = flag_.ensure(1);
+        DSS_HIP(hipMemsetAsync(nbig, 0, sizeof(int), s));
+        hipLaunchKernelGGL(k_emit, dim3(grid_for(nn, B)), dim3(B), 0, s, nn, F->id.p, F->meta.p, ipos, cells, big, nbig);
+        int hb = 0;
+        DSS_HIP(hipMemcpyAsync(&hb, nbig, sizeof(int), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipStreamSynchronize(s));
+        if (hb > 0) hipLaunchKernelGGL(k_emit_big, dim3(hb), dim3(256), 0, s, big, F->id.p, F->meta.p, ipos, cells);
+    }
+    out->offs = offs;
+    out->cells = cells;
+    out->status = status;
+    out->area_km2 = area;
+    out->total_cells = total;
+}
+
+}  // namespace dss

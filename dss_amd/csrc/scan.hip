@@ -1,0 +1,19 @@
+// Device-wide scans (hipcub / rocPRIM) used by the covering and search
+// pipelines for order-preserving compaction.
+#include <hipcub/hipcub.hpp>
+
+#include "common.hpp"
+
+namespace dss {
+
+void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, DevBuf<unsigned char> &tmp, hipStream_t s)
+{
+    DSS_HIP(hipMemsetAsync(out, 0, sizeof(int64_t), s));
+    if (n <= 0) return;
+    size_t bytes = 0;
+    DSS_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, in, out + 1, (int)n, s));
+    tmp.ensure(bytes + 16);
+    DSS_HIP(hipcub::DeviceScan::InclusiveSum(tmp.p, bytes, in, out + 1, (int)n, s));
+}
+
+}  // namespace dss

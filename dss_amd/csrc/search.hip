@@ -1,0 +1,438 @@
+// Entity index + 4D overlap join on gfx950.
+//
+// Replaces the CockroachDB side of the reference search:
+//   scd_cells_operations PK (cell_id, operation_id) + scd_operations
+//     (pkg/scd/store/cockroach/store.go:120-147) and the query at
+//     pkg/scd/store/cockroach/operations.go:376-402;
+//   RID `cells INT64[]` + INVERTED INDEX (pkg/rid/cockroach/store.go:122-151)
+//     and the `cells && $n` queries (identification_service_area.go:170-180,
+//     subscriptions.go:222-273).
+//
+// Index layout in HBM (built once, resident): postings sorted by
+// (cell, entity), structure-of-arrays with the filter attributes inlined
+// (entity u32 | alt float2 | time longlong2 = 28 B), so a cell's posting list
+// streams with 16-byte coalesced loads.  Level-13 cells are found with one
+// dense lookup (slot = cell >> 35, a 29-bit face+Hilbert prefix); any other
+// id (the reference tests use invalid face-7 ids as opaque keys, Q12) goes
+// through a small sorted side table.
+//
+// Join: one wavefront per query walks its cells in ascending order; lanes
+// stream the cell's postings, apply the fused altitude/time/owner predicate,
+// and keep a pair only at the smallest cell the query and the entity share
+// (the SQL DISTINCT, Q13, without a dedupe pass; it also lets cell-range
+// shards emit disjoint pair sets).  Survivors are staged per wave in LDS and
+// flushed with one atomic per batch.
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include "search.hpp"
+
+namespace dss {
+namespace {
+
+constexpr unsigned kBlock = 256;
+constexpr uint32_t kFirstBit = 0x80000000u;
+constexpr uint64_t kLsb13 = 1ull << 34;
+
+__device__ __forceinline__ int64_t tid64() { return (int64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+__host__ __device__ __forceinline__ bool is_regular(uint64_t c)
+{
+    return (c & ((kLsb13 << 1) - 1)) == kLsb13 && (c >> 61) < 6;  // level 13, valid face
+}
+
+__global__ void k_expand(int64_t n, const int64_t *offs, uint32_t *val)
+{
+    int64_t e = tid64();
+    if (e >= n) return;
+    for (int64_t k = offs[e]; k < offs[e + 1]; k++) val[k] = (uint32_t)e;
+}
+
+__global__ void k_keep_flags(int64_t P, const uint64_t *key, const uint32_t *val, int64_t *keep, int64_t *reg,
+                             int64_t *irr)
+{
+    int64_t i = tid64();
+    if (i >= P) return;
+    bool k = i == 0 || key[i] != key[i - 1] || val[i] != val[i - 1];
+    bool r = is_regular(key[i]);
+    keep[i] = k;
+    reg[i] = k && r;
+    irr[i] = k && !r;
+}
+
+__global__ void k_scatter_unique(int64_t P, const uint64_t *key, const uint32_t *val, const int64_t *keep,
+                                 const int64_t *kpos, uint64_t *ukey, uint32_t *uval)
+{
+    int64_t i = tid64();
+    if (i >= P || !keep[i]) return;
+    ukey[kpos[i]] = key[i];
+    uval[kpos[i]] = val[i];
+}
+
+__global__ void k_scatter_part(int64_t P, const uint64_t *key, const uint32_t *val, const int64_t *reg,
+                               const int64_t *rpos, const int64_t *irr, const int64_t *ipos, int64_t n_reg,
+                               uint64_t *p_cell, uint32_t *p_e)
+{
+    int64_t i = tid64();
+    if (i >= P) return;
+    if (reg[i]) {
+        p_cell[rpos[i]] = key[i];
+        p_e[rpos[i]] = val[i];
+    } else if (irr[i]) {
+        p_cell[n_reg + ipos[i]] = key[i];
+        p_e[n_reg + ipos[i]] = val[i];
+    }
+}
+
+__global__ void k_count_by_entity(int64_t P, const uint32_t *e, unsigned long long *cnt)
+{
+    int64_t i = tid64();
+    if (i < P) atomicAdd(&cnt[e[i]], 1ull);
+}
+
+__global__ void k_u64_to_i64(int64_t n, const unsigned long long *a, int64_t *b)
+{
+    int64_t k = tid64();
+    if (k < n) b[k] = (int64_t)a[k];
+}
+
+__global__ void k_attrs(int64_t P, const uint64_t *p_cell, uint32_t *p_e, const int64_t *e_offs, const uint64_t *e_cells,
+                        const float *alo, const float *ahi, const int64_t *t0, const int64_t *t1, const int32_t *owner,
+                        float2 *p_alt, longlong2 *p_t, int32_t *p_owner)
+{
+    int64_t i = tid64();
+    if (i >= P) return;
+    uint32_t e = p_e[i];
+    bool first = e_cells[e_offs[e]] == p_cell[i];
+    p_e[i] = e | (first ? kFirstBit : 0u);
+    p_alt[i] = make_float2(alo[e], ahi[e]);
+    p_t[i] = make_longlong2(t0[e], t1[e]);
+    if (owner) p_owner[i] = owner[e];
+}
+
+__global__ void k_dense_hist(int64_t n_reg, const uint64_t *p_cell, uint64_t kmin, unsigned long long *cnt)
+{
+    int64_t i = tid64();
+    if (i < n_reg) atomicAdd(&cnt[(p_cell[i] >> 35) - kmin], 1ull);
+}
+
+__global__ void k_i64_to_u32(int64_t n, const int64_t *a, uint32_t *b)
+{
+    int64_t k = tid64();
+    if (k < n) b[k] = (uint32_t)a[k];
+}
+
+__global__ void k_irr_runs(int64_t n_irr_p, const uint64_t *cells, int64_t *flag)
+{
+    int64_t i = tid64();
+    if (i < n_irr_p) flag[i] = (i == 0 || cells[i] != cells[i - 1]) ? 1 : 0;
+}
+__global__ void k_irr_scatter(int64_t n_irr_p, const uint64_t *cells, const int64_t *flag, const int64_t *pos,
+                              int64_t n_reg, uint64_t *irr_cells, uint32_t *irr_start)
+{
+    int64_t i = tid64();
+    if (i < n_irr_p && flag[i]) {
+        irr_cells[pos[i]] = cells[i];
+        irr_start[pos[i]] = (uint32_t)(n_reg + i);
+    }
+}
+
+struct JoinArgs {
+    // queries
+    int64_t nq;
+    const int64_t *q_offs;
+    const uint64_t *q_cells;
+    const float *q_alo, *q_ahi;
+    const int64_t *q_tlo, *q_thi;
+    const int32_t *q_owner;
+    // index
+    const uint32_t *p_e;
+    const float2 *p_alt;
+    const longlong2 *p_t;
+    const int32_t *p_owner;
+    const int64_t *e_offs;
+    const uint64_t *e_cells;
+    uint64_t kmin;
+    int64_t n_dense;
+    const uint32_t *dense;
+    int64_t n_irr;
+    const uint64_t *irr_cells;
+    const uint32_t *irr_start;
+    // output
+    uint32_t *out_q, *out_e;
+    unsigned long long *counter;
+    int64_t cap;
+};
+
+__device__ __forceinline__ void lookup(const JoinArgs &a, uint64_t c, uint32_t &s, uint32_t &e)
+{
+    s = e = 0;
+    if (is_regular(c)) {
+        uint64_t k = c >> 35;
+        if (k >= a.kmin && (int64_t)(k - a.kmin) < a.n_dense) {
+            s = a.dense[k - a.kmin];
+            e = a.dense[k - a.kmin + 1];
+        }
+        return;
+    }
+    int64_t lo = 0, hi = a.n_irr;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (a.irr_cells[mid] < c) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo < a.n_irr && a.irr_cells[lo] == c) {
+        s = a.irr_start[lo];
+        e = a.irr_start[lo + 1];
+    }
+}
+
+// True iff no cell < c is shared by the query (cells qc[0..nqc), all < c)
+// and the entity.
+__device__ bool smallest_shared(const JoinArgs &a, uint32_t ent, uint64_t c, const uint64_t *qc, int64_t nqc)
+{
+    const uint64_t *ec = a.e_cells + a.e_offs[ent];
+    int64_t ne = a.e_offs[ent + 1] - a.e_offs[ent];
+    int64_t i = 0, j = 0;
+    while (i < nqc && j < ne) {
+        uint64_t x = qc[i], y = ec[j];
+        if (y >= c) break;
+        if (x == y) return false;
+        if (x < y) i++;
+        else j++;
+    }
+    return true;
+}
+
+constexpr int kStage = 256;  // pairs staged per wave in LDS
+
+__global__ __launch_bounds__(kBlock) void k_join(JoinArgs a)
+{
+    __shared__ uint32_t sq[kBlock / 64][kStage];
+    __shared__ uint32_t se[kBlock / 64][kStage];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int64_t q = (int64_t)blockIdx.x * (kBlock / 64) + w;
+    int staged = 0;
+    auto flush = [&]() {
+        unsigned long long base = 0;
+        if (lane == 0 && staged) base = atomicAdd(a.counter, (unsigned long long)staged);
+        base = __shfl(base, 0);
+        for (int k = lane; k < staged; k += 64) {
+            unsigned long long o = base + (unsigned long long)k;
+            if ((int64_t)o < a.cap) {
+                a.out_q[o] = sq[w][k];
+                a.out_e[o] = se[w][k];
+            }
+        }
+        staged = 0;
+    };
+    if (q < a.nq) {
+        const int64_t tlo = a.q_tlo[q], thi = a.q_thi[q];
+        const float alo = a.q_alo[q], ahi = a.q_ahi[q];
+        const int32_t own = a.q_owner ? a.q_owner[q] : -1;
+        const int64_t c0 = a.q_offs[q], c1 = a.q_offs[q + 1];
+        const uint64_t *qc = a.q_cells + c0;
+        for (int64_t ci = c0; ci < c1; ci++) {
+            uint64_t c = a.q_cells[ci];
+            uint32_t s, e;
+            lookup(a, c, s, e);
+            for (uint32_t base = s; base < e; base += 64) {
+                uint32_t p = base + lane;
+                bool pass = false;
+                uint32_t ent = 0;
+                if (p < e) {
+                    uint32_t pe = a.p_e[p];
+                    float2 alt = a.p_alt[p];
+                    longlong2 t = a.p_t[p];
+                    ent = pe & ~kFirstBit;
+                    // COALESCE'd predicates of operations.go:394-402 after
+                    // the NULL->sentinel mapping (dssgpu.h)
+                    pass = t.y >= tlo && t.x <= thi && alt.y >= alo && alt.x <= ahi;
+                    if (pass && own >= 0) pass = a.p_owner[p] == own;
+                    if (pass && ci != c0 && !(pe & kFirstBit)) pass = smallest_shared(a, ent, c, qc, ci - c0);
+                }
+                unsigned long long m = __ballot(pass);
+                int nsurv = __popcll(m);
+                if (nsurv == 0) continue;
+                if (staged + nsurv > kStage) flush();
+                if (pass) {
+                    int r = __popcll(m & ((1ull << lane) - 1ull));
+                    sq[w][staged + r] = (uint32_t)q;
+                    se[w][staged + r] = ent;
+                }
+                staged += nsurv;
+            }
+        }
+    }
+    flush();
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- build
+void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, const uint64_t *cells,
+                         const float *alt_lo, const float *alt_hi, const int64_t *t0, const int64_t *t1,
+                         const int32_t *owner, hipStream_t s)
+{
+    idx->n_e = n;
+    idx->has_owner = owner != nullptr;
+    int64_t P = 0;
+    DSS_HIP(hipMemcpyAsync(&P, cell_offs + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    if (P >= (int64_t)0x7fffffff) throw Error(DSSG_ERR_INVALID, "index: more than 2^31 postings per device");
+    if (n >= (int64_t)0x7fffffff) throw Error(DSSG_ERR_INVALID, "index: more than 2^31 entities per device");
+    const int64_t Pa = P + 1;
+    uint64_t *ka = k0_.ensure(Pa), *kb = k1_.ensure(Pa);
+    uint32_t *va = v0_.ensure(Pa), *vb = v1_.ensure(Pa);
+    DSS_HIP(hipMemcpyAsync(ka, cells, sizeof(uint64_t) * P, hipMemcpyDeviceToDevice, s));
+    if (n) hipLaunchKernelGGL(k_expand, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, cell_offs, va);
+    // sort postings by cell (stable: entity order preserved within a cell)
+    size_t bytes = 0;
+    if (P) {
+        DSS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, ka, kb, va, vb, (int)P, 0, 64, s));
+        tmp_.ensure(bytes + 16);
+        DSS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_.p, bytes, ka, kb, va, vb, (int)P, 0, 64, s));
+    }
+    // unique (cell, entity) + regular/irregular partition
+    int64_t *keep = c0_.ensure(3 * Pa), *reg = keep + Pa, *irr = reg + Pa;
+    int64_t *kpos = c1_.ensure(3 * (Pa + 1)), *rpos = kpos + (Pa + 1), *ipos = rpos + (Pa + 1);
+    if (P) hipLaunchKernelGGL(k_keep_flags, dim3(grid_for(P, kBlock)), dim3(kBlock), 0, s, P, kb, vb, keep, reg, irr);
+    exclusive_scan_i64(keep, kpos, P, tmp_, s);
+    exclusive_scan_i64(reg, rpos, P, tmp_, s);
+    exclusive_scan_i64(irr, ipos, P, tmp_, s);
+    int64_t counts[3] = {0, 0, 0};
+    DSS_HIP(hipMemcpyAsync(&counts[0], kpos + P, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipMemcpyAsync(&counts[1], rpos + P, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipMemcpyAsync(&counts[2], ipos + P, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    const int64_t Pu = counts[0], n_reg = counts[1], n_irr_p = counts[2];
+    idx->n_p = Pu;
+    idx->n_reg = n_reg;
+    uint64_t *p_cell = idx->p_cell.ensure(Pu + 1);
+    uint32_t *p_e = idx->p_e.ensure(Pu + 1);
+    if (P)
+        hipLaunchKernelGGL(k_scatter_part, dim3(grid_for(P, kBlock)), dim3(kBlock), 0, s, P, kb, vb, reg, rpos, irr, ipos,
+                           n_reg, p_cell, p_e);
+    // entity -> sorted unique cell lists: unique postings in cell order, then
+    // a stable sort by entity.
+    if (P)
+        hipLaunchKernelGGL(k_scatter_unique, dim3(grid_for(P, kBlock)), dim3(kBlock), 0, s, P, kb, vb, keep, kpos, ka, va);
+    uint64_t *e_cells = idx->e_cells.ensure(Pu + 1);
+    uint32_t *vsorted = vb;
+    if (Pu) {
+        bytes = 0;
+        DSS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, va, vb, ka, e_cells, (int)Pu, 0, 32, s));
+        tmp_.ensure(bytes + 16);
+        DSS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_.p, bytes, va, vb, ka, e_cells, (int)Pu, 0, 32, s));
+    }
+    DevBuf<unsigned long long> ecnt;
+    unsigned long long *ec = ecnt.ensure(n + 1);
+    DSS_HIP(hipMemsetAsync(ec, 0, sizeof(unsigned long long) * (n + 1), s));
+    if (Pu) hipLaunchKernelGGL(k_count_by_entity, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, vsorted, ec);
+    int64_t *ec64 = c0_.ensure(3 * Pa > n + 1 ? 3 * Pa : n + 1);
+    if (n) hipLaunchKernelGGL(k_u64_to_i64, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, ec, ec64);
+    int64_t *e_offs = idx->e_offs.ensure(n + 1);
+    exclusive_scan_i64(ec64, e_offs, n, tmp_, s);
+    // inline attributes + first-cell flag
+    float2 *p_alt = idx->p_alt.ensure(Pu + 1);
+    longlong2 *p_t = idx->p_t.ensure(Pu + 1);
+    int32_t *p_owner = idx->p_owner.ensure(Pu + 1);
+    if (Pu)
+        hipLaunchKernelGGL(k_attrs, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, p_cell, p_e, e_offs, e_cells,
+                           alt_lo, alt_hi, t0, t1, owner, p_alt, p_t, p_owner);
+    // dense lookup over regular postings
+    idx->n_dense = 0;
+    idx->kmin = 0;
+    if (n_reg > 0) {
+        uint64_t first = 0, last = 0;
+        DSS_HIP(hipMemcpyAsync(&first, p_cell, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipMemcpyAsync(&last, p_cell + n_reg - 1, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipStreamSynchronize(s));
+        idx->kmin = first >> 35;
+        idx->n_dense = (int64_t)((last >> 35) - idx->kmin + 1);
+        DevBuf<unsigned long long> h;
+        unsigned long long *hc = h.ensure(idx->n_dense + 1);
+        DSS_HIP(hipMemsetAsync(hc, 0, sizeof(unsigned long long) * (idx->n_dense + 1), s));
+        hipLaunchKernelGGL(k_dense_hist, dim3(grid_for(n_reg, kBlock)), dim3(kBlock), 0, s, n_reg, p_cell, idx->kmin, hc);
+        DevBuf<int64_t> h64, hs;
+        int64_t *a64 = h64.ensure(idx->n_dense + 1), *sc = hs.ensure(idx->n_dense + 2);
+        hipLaunchKernelGGL(k_u64_to_i64, dim3(grid_for(idx->n_dense, kBlock)), dim3(kBlock), 0, s, idx->n_dense, hc, a64);
+        exclusive_scan_i64(a64, sc, idx->n_dense, tmp_, s);
+        uint32_t *dense = idx->dense.ensure(idx->n_dense + 1);
+        hipLaunchKernelGGL(k_i64_to_u32, dim3(grid_for(idx->n_dense + 1, kBlock)), dim3(kBlock), 0, s, idx->n_dense + 1, sc,
+                           dense);
+        DSS_HIP(hipStreamSynchronize(s));
+    } else {
+        idx->dense.ensure(2);
+        DSS_HIP(hipMemsetAsync(idx->dense.p, 0, 2 * sizeof(uint32_t), s));
+    }
+    // irregular side table
+    idx->n_irr = 0;
+    uint32_t *irr_start = nullptr;
+    if (n_irr_p > 0) {
+        DevBuf<int64_t> fl, fp;
+        int64_t *f = fl.ensure(n_irr_p + 1), *fpo = fp.ensure(n_irr_p + 2);
+        hipLaunchKernelGGL(k_irr_runs, dim3(grid_for(n_irr_p, kBlock)), dim3(kBlock), 0, s, n_irr_p, p_cell + n_reg, f);
+        exclusive_scan_i64(f, fpo, n_irr_p, tmp_, s);
+        int64_t nu = 0;
+        DSS_HIP(hipMemcpyAsync(&nu, fpo + n_irr_p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipStreamSynchronize(s));
+        idx->n_irr = nu;
+        uint64_t *ic = idx->irr_cells.ensure(nu + 1);
+        irr_start = idx->irr_start.ensure(nu + 1);
+        hipLaunchKernelGGL(k_irr_scatter, dim3(grid_for(n_irr_p, kBlock)), dim3(kBlock), 0, s, n_irr_p, p_cell + n_reg, f, fpo,
+                           n_reg, ic, irr_start);
+        uint32_t endv = (uint32_t)Pu;
+        DSS_HIP(hipMemcpyAsync(irr_start + nu, &endv, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    } else {
+        idx->irr_cells.ensure(1);
+        idx->irr_start.ensure(1);
+    }
+    DSS_HIP(hipStreamSynchronize(s));
+}
+
+// ---------------------------------------------------------------- search
+void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
+                          const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
+                          const int32_t *q_owner, hipStream_t s, dssg_pairs *out)
+{
+    if (q_owner && !idx->has_owner) throw Error(DSSG_ERR_INVALID, "search by owner on an index built without owners");
+    unsigned long long *counter = counter_.ensure(1);
+    if (out_cap_ == 0) out_cap_ = (size_t)(nq > 0 ? nq : 1) * 16 + 1024;
+    for (int attempt = 0; attempt < 3; attempt++) {
+        uint32_t *oq = oq_.ensure(out_cap_), *oe = oe_.ensure(out_cap_);
+        DSS_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned long long), s));
+        JoinArgs a;
+        a.nq = nq; a.q_offs = q_offs; a.q_cells = q_cells; a.q_alo = q_alt_lo; a.q_ahi = q_alt_hi;
+        a.q_tlo = q_tlo; a.q_thi = q_thi; a.q_owner = q_owner;
+        a.p_e = idx->p_e.p; a.p_alt = idx->p_alt.p; a.p_t = idx->p_t.p; a.p_owner = idx->p_owner.p;
+        a.e_offs = idx->e_offs.p; a.e_cells = idx->e_cells.p;
+        a.kmin = idx->kmin; a.n_dense = idx->n_dense; a.dense = idx->dense.p;
+        a.n_irr = idx->n_irr; a.irr_cells = idx->irr_cells.p; a.irr_start = idx->irr_start.p;
+        a.out_q = oq; a.out_e = oe; a.counter = counter; a.cap = (int64_t)out_cap_;
+        if (timing_) {
+            if (!ev0_) { DSS_HIP(hipEventCreate(&ev0_)); DSS_HIP(hipEventCreate(&ev1_)); }
+            DSS_HIP(hipEventRecord(ev0_, s));
+        }
+        if (nq > 0) hipLaunchKernelGGL(k_join, dim3(grid_for(nq, kBlock / 64)), dim3(kBlock), 0, s, a);
+        if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
+        unsigned long long total = 0;
+        DSS_HIP(hipMemcpyAsync(&total, counter, sizeof(total), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipStreamSynchronize(s));
+        if (timing_) {
+            float ms = 0;
+            DSS_HIP(hipEventElapsedTime(&ms, ev0_, ev1_));
+            join_ms_ = ms;
+        }
+        if (total <= out_cap_) {
+            out->q = oq;
+            out->e = oe;
+            out->n = (int64_t)total;
+            return;
+        }
+        out_cap_ = (size_t)(total + total / 8 + 1024);
+    }
+    throw Error(DSSG_ERR_DEVICE, "search: output size did not converge");
+}
+
+}  // namespace dss

@@ -1,0 +1,213 @@
+"""Store-side search API mirroring the reference's store interfaces.
+
+  scdstore.OperationStore.SearchOperations   pkg/scd/store/store.go:29
+      impl pkg/scd/store/cockroach/operations.go:374-445
+  repos.ISA.SearchISAs                       pkg/rid/repos/isa.go:27
+      impl pkg/rid/cockroach/identification_service_area.go:166-197
+      app clamp pkg/rid/application/isa.go:38-45
+  repos.Subscription.SearchSubscriptions[ByOwner] pkg/rid/repos/subscription.go:26-29
+      impl pkg/rid/cockroach/subscriptions.go:222-273
+  scdstore.SubscriptionStore.SearchSubscriptions pkg/scd/store/store.go:35
+      impl pkg/scd/store/cockroach/subscriptions.go:498-545 (Q7: cells ignored)
+
+Stored entities live in a GPU-resident `EntityIndex` (dssg_index).  Entity
+ids are dense 0..n-1 indices that the caller maps to its rows (UUIDs).
+Times are int64 microseconds; None means SQL NULL.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from .geo import GeoError, Volume4D
+
+NULL_START = _lib.TIME_NULL_START
+NULL_END = _lib.TIME_NULL_END
+NULL_END_Q = _lib.TIME_NULL_END_Q
+
+
+class BadRequest(ValueError):
+    """dsserr.BadRequest (pkg/errors/errors.go:88-90) -> codes.InvalidArgument."""
+
+
+class Internal(RuntimeError):
+    """dsserr.Internal -> codes.Internal."""
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def _csr(cell_lists: Sequence[Sequence[int]]) -> Tuple[np.ndarray, np.ndarray]:
+    offs = np.zeros(len(cell_lists) + 1, dtype=np.int64)
+    for i, c in enumerate(cell_lists):
+        offs[i + 1] = offs[i] + len(c)
+    cells = np.zeros(int(offs[-1]), dtype=np.uint64)
+    for i, c in enumerate(cell_lists):
+        cells[offs[i]:offs[i + 1]] = np.asarray([int(x) & (2**64 - 1) for x in c], dtype=np.uint64)
+    return offs, cells
+
+
+def _f32_or(v: Optional[float], null: float) -> float:
+    return null if v is None else float(np.float32(v))
+
+
+class EntityIndex:
+    """GPU-resident index of stored entities (operational intents, ISAs,
+    subscriptions): replaces scd_cells_operations / RID cells INT64[] +
+    INVERTED INDEX.  NULL conventions as include/dssgpu.h."""
+
+    def __init__(self, cell_offs, cells, alt_lo=None, alt_hi=None, t0=None, t1=None, owner=None, device: int = 0):
+        self.ctx = _lib.context(device)
+        offs = np.ascontiguousarray(cell_offs, dtype=np.int64)
+        n = len(offs) - 1
+        cells = np.ascontiguousarray(cells, dtype=np.uint64)
+        alo = np.ascontiguousarray(alt_lo if alt_lo is not None else np.full(n, -np.inf), dtype=np.float32)
+        ahi = np.ascontiguousarray(alt_hi if alt_hi is not None else np.full(n, np.inf), dtype=np.float32)
+        a0 = np.ascontiguousarray(t0 if t0 is not None else np.full(n, NULL_START), dtype=np.int64)
+        a1 = np.ascontiguousarray(t1 if t1 is not None else np.full(n, 2**63 - 1), dtype=np.int64)
+        own = np.ascontiguousarray(owner, dtype=np.int32) if owner is not None else None
+        h = C.c_void_p()
+        rc = self.ctx.L.dssg_index_build(self.ctx.h, n, _p(offs, C.c_int64), _p(cells, C.c_uint64),
+                                         _p(alo, C.c_float), _p(ahi, C.c_float), _p(a0, C.c_int64),
+                                         _p(a1, C.c_int64),
+                                         _p(own, C.c_int32) if own is not None else C.POINTER(C.c_int32)(),
+                                         C.byref(h))
+        self.ctx.check(rc)
+        self.h = h
+        self.n = n
+
+    @classmethod
+    def from_lists(cls, cell_lists, alt_lo=None, alt_hi=None, t0=None, t1=None, owner=None, device=0):
+        offs, cells = _csr(cell_lists)
+        return cls(offs, cells, alt_lo, alt_hi, t0, t1, owner, device)
+
+    @property
+    def num_postings(self) -> int:
+        return int(self.ctx.L.dssg_index_num_postings(self.h))
+
+    def free(self):
+        if getattr(self, "h", None):
+            self.ctx.L.dssg_index_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    # -------------------------------------------------------------- batches
+    def _call(self, fn, nq, *args) -> Tuple[np.ndarray, np.ndarray]:
+        need = C.c_int64(0)
+        cap = max(1024, nq * 8)
+        while True:
+            oq = np.zeros(cap, dtype=np.uint32)
+            oe = np.zeros(cap, dtype=np.uint32)
+            rc = fn(self.ctx.h, self.h, nq, *args, _p(oq, C.c_uint32), _p(oe, C.c_uint32), cap, C.byref(need))
+            if rc == _lib.DSSG_ERR_CAPACITY:
+                cap = int(need.value) + 1
+                continue
+            self.ctx.check(rc)
+            return oq[: need.value].copy(), oe[: need.value].copy()
+
+    def search_batch(self, q_offs, q_cells, alt_lo, alt_hi, tlo, thi, owner=None):
+        """Generic join (dssg_search); pairs sorted by (query, entity)."""
+        q_offs = np.ascontiguousarray(q_offs, dtype=np.int64)
+        q_cells = np.ascontiguousarray(q_cells, dtype=np.uint64)
+        nq = len(q_offs) - 1
+        lo = np.ascontiguousarray(alt_lo, dtype=np.float32)
+        hi = np.ascontiguousarray(alt_hi, dtype=np.float32)
+        tl = np.ascontiguousarray(tlo, dtype=np.int64)
+        th = np.ascontiguousarray(thi, dtype=np.int64)
+        ow = np.ascontiguousarray(owner, dtype=np.int32) if owner is not None else None
+        return self._call(self.ctx.L.dssg_search, nq, _p(q_offs, C.c_int64), _p(q_cells, C.c_uint64),
+                          _p(lo, C.c_float), _p(hi, C.c_float), _p(tl, C.c_int64), _p(th, C.c_int64),
+                          _p(ow, C.c_int32) if ow is not None else C.POINTER(C.c_int32)())
+
+    def search_operations_batch(self, q_offs, q_cells, alt_lo, alt_hi, start, end, now_us):
+        q_offs = np.ascontiguousarray(q_offs, dtype=np.int64)
+        q_cells = np.ascontiguousarray(q_cells, dtype=np.uint64)
+        nq = len(q_offs) - 1
+        lo = np.ascontiguousarray(alt_lo, dtype=np.float32)
+        hi = np.ascontiguousarray(alt_hi, dtype=np.float32)
+        s = np.ascontiguousarray(start, dtype=np.int64)
+        e = np.ascontiguousarray(end, dtype=np.int64)
+        return self._call(self.ctx.L.dssg_search_operations, nq, _p(q_offs, C.c_int64), _p(q_cells, C.c_uint64),
+                          _p(lo, C.c_float), _p(hi, C.c_float), _p(s, C.c_int64), _p(e, C.c_int64), int(now_us))
+
+    def search_isas_batch(self, q_offs, q_cells, earliest, latest):
+        q_offs = np.ascontiguousarray(q_offs, dtype=np.int64)
+        q_cells = np.ascontiguousarray(q_cells, dtype=np.uint64)
+        nq = len(q_offs) - 1
+        ea = np.ascontiguousarray(earliest, dtype=np.int64)
+        la = np.ascontiguousarray(latest, dtype=np.int64)
+        return self._call(self.ctx.L.dssg_search_isas, nq, _p(q_offs, C.c_int64), _p(q_cells, C.c_uint64),
+                          _p(ea, C.c_int64), _p(la, C.c_int64))
+
+    def search_subscriptions_batch(self, q_offs, q_cells, now_us, owner=None):
+        q_offs = np.ascontiguousarray(q_offs, dtype=np.int64)
+        q_cells = np.ascontiguousarray(q_cells, dtype=np.uint64)
+        nq = len(q_offs) - 1
+        ow = np.ascontiguousarray(owner, dtype=np.int32) if owner is not None else None
+        return self._call(self.ctx.L.dssg_search_subscriptions, nq, _p(q_offs, C.c_int64), _p(q_cells, C.c_uint64),
+                          _p(ow, C.c_int32) if ow is not None else C.POINTER(C.c_int32)(), int(now_us))
+
+
+# ------------------------------------------------------------ reference API
+def SearchOperations(index: EntityIndex, v4d: Volume4D, owner=None, now_us: int = 0) -> List[int]:
+    """operations.go:374-445 searchOperations; `owner` is ignored (Q6)."""
+    if v4d.SpatialVolume is None or v4d.SpatialVolume.Footprint is None:
+        raise BadRequest("missing geospatial footprint for query")
+    try:
+        cells = v4d.SpatialVolume.Footprint.CalculateCovering()
+    except GeoError as err:
+        raise BadRequest(str(err)) from err
+    if len(cells) == 0:
+        raise BadRequest("missing cell IDs for query")
+    offs, cc = _csr([cells])
+    sv = v4d.SpatialVolume
+    _, e = index.search_operations_batch(
+        offs, cc, [_f32_or(sv.AltitudeLo, -np.inf)], [_f32_or(sv.AltitudeHi, np.inf)],
+        [NULL_START if v4d.StartTime is None else v4d.StartTime],
+        [NULL_END_Q if v4d.EndTime is None else v4d.EndTime], now_us)
+    return [int(x) for x in e]
+
+
+def SearchISAs(index: EntityIndex, cells: Sequence[int], earliest: Optional[int], latest: Optional[int]) -> List[int]:
+    """identification_service_area.go:166-197 (store layer, no clamp)."""
+    if len(cells) == 0:
+        raise BadRequest("missing cell IDs for query")
+    if earliest is None:
+        raise Internal("must call with an earliest start time.")
+    offs, cc = _csr([cells])
+    _, e = index.search_isas_batch(offs, cc, [earliest], [NULL_END_Q if latest is None else latest])
+    return [int(x) for x in e]
+
+
+def AppSearchISAs(index: EntityIndex, cells, earliest: Optional[int], latest: Optional[int], now_us: int):
+    """pkg/rid/application/isa.go:38-45: earliest = max(now, earliest) (Q15)."""
+    if earliest is None or earliest < now_us:
+        earliest = now_us
+    return SearchISAs(index, cells, earliest, latest)
+
+
+def SearchSubscriptions(index: EntityIndex, cells: Sequence[int], now_us: int) -> List[int]:
+    """RID subscriptions.go:222-245."""
+    if len(cells) == 0:
+        raise BadRequest("no location provided")
+    offs, cc = _csr([cells])
+    _, e = index.search_subscriptions_batch(offs, cc, now_us)
+    return [int(x) for x in e]
+
+
+def SearchSubscriptionsByOwner(index: EntityIndex, cells: Sequence[int], owner: int, now_us: int) -> List[int]:
+    """RID subscriptions.go:247-273."""
+    if len(cells) == 0:
+        raise BadRequest("no location provided")
+    offs, cc = _csr([cells])
+    _, e = index.search_subscriptions_batch(offs, cc, now_us, [owner])
+    return [int(x) for x in e]

@@ -1,0 +1,173 @@
+"""Seeded synthetic workloads for the BASELINE.json configs.
+
+numpy default_rng(seed), seed = 20201015 + i with i the index in
+BASELINE.json `configs`.  All outputs are flat numpy arrays in the layout the
+C ABI takes (kind, voff, lat, lng, radius_m for footprints; SoA attributes).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+KIND_POLYGON = 0
+KIND_CIRCLE = 1
+T0_US = 1_600_000_000_000_000  # "T" of the generator: an arbitrary UTC instant (2020-09-13)
+HOUR_US = 3_600_000_000
+MIN_US = 60_000_000
+R_EARTH = 6371010.0
+
+METRO = (37.2, 37.9, -122.55, -121.75)       # SF Bay (configs 0, 1)
+CALIFORNIA = (32.5, 42.0, -124.4, -114.1)    # config 2
+NYC = (40.49, 40.92, -74.26, -73.70)         # config 3
+CONUS = (25.0, 49.0, -124.5, -67.0)          # config 4
+CA_HOTSPOTS = [(34.05, -118.25), (37.77, -122.42), (32.72, -117.16), (38.58, -121.49)]
+
+
+@dataclass
+class Footprints:
+    kind: np.ndarray      # int32 [n]
+    voff: np.ndarray      # int64 [n+1]
+    lat: np.ndarray       # float64 [voff[n]]
+    lng: np.ndarray       # float64
+    radius_m: np.ndarray  # float32 [n]
+
+    @property
+    def n(self) -> int:
+        return len(self.kind)
+
+    def subset(self, idx: np.ndarray) -> "Footprints":
+        idx = np.asarray(idx)
+        counts = self.voff[idx + 1] - self.voff[idx]
+        voff = np.zeros(len(idx) + 1, dtype=np.int64)
+        np.cumsum(counts, out=voff[1:])
+        take = np.concatenate([np.arange(self.voff[i], self.voff[i + 1]) for i in idx]) if len(idx) else np.zeros(0, np.int64)
+        return Footprints(self.kind[idx].copy(), voff, self.lat[take].copy(), self.lng[take].copy(),
+                          self.radius_m[idx].copy())
+
+
+def _offset(lat0, lng0, dx, dy):
+    """Local tangent-plane offset (metres east dx, north dy) -> degrees."""
+    dlat = np.degrees(dy / R_EARTH)
+    dlng = np.degrees(dx / (R_EARTH * np.cos(np.radians(lat0))))
+    return lat0 + dlat, lng0 + dlng
+
+
+def _centres(rng, n, region, hotspots=None, hot_frac=0.0, sigma_m=15000.0):
+    la0, la1, ln0, ln1 = region
+    lat = rng.uniform(la0, la1, n)
+    lng = rng.uniform(ln0, ln1, n)
+    if hotspots and hot_frac > 0:
+        hot = rng.random(n) < hot_frac
+        k = rng.integers(0, len(hotspots), n)
+        hs = np.asarray(hotspots)
+        dx = rng.normal(0, sigma_m, n)
+        dy = rng.normal(0, sigma_m, n)
+        hl, hg = _offset(hs[k, 0], hs[k, 1], dx, dy)
+        lat = np.where(hot, np.clip(hl, la0, la1), lat)
+        lng = np.where(hot, np.clip(hg, ln0, ln1), lng)
+    return lat, lng
+
+
+def metro_footprints(rng, n, region=METRO, circle_frac=0.3, hotspots=None, hot_frac=0.0, sigma_m=15000.0,
+                     rmin=100.0, rmax=3000.0) -> Footprints:
+    """Polygons (V ~ U{3..12}, radius ~ logU[rmin, rmax], radial jitter
+    U[0.6, 1.0], 50% clockwise, 25% closed rings) and circles (radius f32 ~
+    U[50, 2000] m), polygon:circle = (1-circle_frac):circle_frac."""
+    clat, clng = _centres(rng, n, region, hotspots, hot_frac, sigma_m)
+    is_circle = rng.random(n) < circle_frac
+    nv = rng.integers(3, 13, n)
+    closed = (rng.random(n) < 0.25) & ~is_circle
+    cw = rng.random(n) < 0.5
+    radius = np.exp(rng.uniform(np.log(rmin), np.log(rmax), n))
+    counts = np.where(is_circle, 1, nv + closed.astype(np.int64))
+    voff = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(counts, out=voff[1:])
+    tot = int(voff[-1])
+    lat = np.empty(tot)
+    lng = np.empty(tot)
+    # vectorised polygon construction: angles theta0 + 2*pi*k/nv with a
+    # +-0.2-spacing jitter, so consecutive gaps stay < pi and the polygon is
+    # star-shaped about its centre, hence simple (the generator contract's
+    # "sorted U[0,2pi) angles" can produce self-intersecting, i.e. invalid,
+    # S2 loops whose parity interior is most of the sphere).
+    maxv = 13
+    col = np.arange(maxv)[None, :]
+    valid = col < nv[:, None]
+    spacing = 2 * np.pi / nv[:, None]
+    ang = rng.uniform(0, 2 * np.pi, (n, 1)) + spacing * (col + rng.uniform(-0.2, 0.2, (n, maxv)))
+    jit = rng.uniform(0.6, 1.0, (n, maxv))
+    # clockwise: reverse vertex order among the first nv
+    rev_idx = np.where(valid, nv[:, None] - 1 - col, col)
+    ang = np.where(cw[:, None], np.take_along_axis(ang, rev_idx, axis=1), ang)
+    jit = np.where(cw[:, None], np.take_along_axis(jit, rev_idx, axis=1), jit)
+    r = radius[:, None] * jit
+    plat, plng = _offset(clat[:, None], clng[:, None], r * np.cos(ang), r * np.sin(ang))
+    poly = ~is_circle
+    rows = np.repeat(np.arange(n)[poly], nv[poly])
+    cols = np.concatenate([np.arange(v) for v in nv[poly]]) if poly.any() else np.zeros(0, np.int64)
+    dst = voff[rows] + cols
+    lat[dst] = plat[rows, cols]
+    lng[dst] = plng[rows, cols]
+    cidx = np.nonzero(closed)[0]
+    lat[voff[cidx] + nv[cidx]] = lat[voff[cidx]]
+    lng[voff[cidx] + nv[cidx]] = lng[voff[cidx]]
+    ci = np.nonzero(is_circle)[0]
+    lat[voff[ci]] = clat[ci]
+    lng[voff[ci]] = clng[ci]
+    radius_m = np.where(is_circle, rng.uniform(50.0, 2000.0, n), 0.0).astype(np.float32)
+    kind = np.where(is_circle, KIND_CIRCLE, KIND_POLYGON).astype(np.int32)
+    return Footprints(kind, voff, lat, lng, radius_m)
+
+
+@dataclass
+class Attrs:
+    alt_lo: np.ndarray  # float32
+    alt_hi: np.ndarray
+    t0: np.ndarray      # int64 us (NULL start -> INT64_MIN)
+    t1: np.ndarray      # int64 us (NULL end  -> INT64_MAX for queries)
+
+
+def intent_attrs(rng, n) -> Attrs:
+    lo = rng.uniform(0, 400, n).astype(np.float32)
+    hi = (lo + rng.uniform(10, 200, n)).astype(np.float32)
+    t0 = T0_US + rng.integers(0, 24 * HOUR_US, n)
+    t1 = t0 + rng.integers(5 * MIN_US, 2 * HOUR_US + 1, n)
+    return Attrs(lo, hi, t0.astype(np.int64), t1.astype(np.int64))
+
+
+def query_attrs(rng, n) -> Attrs:
+    lo = rng.uniform(0, 400, n).astype(np.float32)
+    hi = (lo + rng.uniform(10, 200, n)).astype(np.float32)
+    miss = rng.random(n) < 0.05           # Q8: missing SCD altitude -> 0.0
+    lo = np.where(miss, np.float32(0), lo).astype(np.float32)
+    hi = np.where(miss, np.float32(0), hi).astype(np.float32)
+    t0 = T0_US + rng.integers(0, 24 * HOUR_US, n)
+    t1 = t0 + rng.integers(1 * MIN_US, 30 * MIN_US + 1, n)
+    nulls = rng.random(n) < 0.05
+    which = rng.random(n) < 0.5
+    t0 = np.where(nulls & which, np.iinfo(np.int64).min, t0)
+    t1 = np.where(nulls & ~which, np.iinfo(np.int64).max, t1)
+    return Attrs(lo, hi, t0.astype(np.int64), t1.astype(np.int64))
+
+
+def config(i: int, scale: float = 1.0):
+    """Return (rng, queries, q_attrs, intents, i_attrs, now_us) for BASELINE config i.
+
+    `scale` shrinks the counts (tests); the shapes and distributions stay."""
+    rng = np.random.default_rng(20201015 + i)
+    if i == 0:
+        nq, ni, region, kw = 10_000, 100_000, METRO, {}
+    elif i == 1:
+        nq, ni, region, kw = 1_000_000, 1_000_000, METRO, {}
+    elif i == 2:
+        nq, ni, region, kw = 1_000_000, 10_000_000, CALIFORNIA, dict(hotspots=CA_HOTSPOTS, hot_frac=0.7, sigma_m=15000.0)
+    else:
+        raise ValueError(f"config {i} not generated here")
+    nq = max(1, int(nq * scale))
+    ni = max(1, int(ni * scale))
+    intents = metro_footprints(rng, ni, region, **kw)
+    ia = intent_attrs(rng, ni)
+    queries = metro_footprints(rng, nq, region, **kw)
+    qa = query_attrs(rng, nq)
+    return rng, queries, qa, intents, ia, T0_US

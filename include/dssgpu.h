@@ -1,0 +1,186 @@
+/* dssgpu.h -- C ABI of the MI355X (gfx950) spatial-discovery / 4D-conflict
+ * engine.  Plain C types only (no HIP, no torch): a Go cgo adapter binds it
+ * directly.
+ *
+ * The engine replaces two halves of the reference (InterUSS DSS,
+ * /root/reference) hot path:
+ *   covering  pkg/geo/s2.go:99-166 (Covering, AreaToCellIDs) and
+ *             pkg/models/geo.go:224-268 (GeoCircle / GeoPolygon
+ *             .CalculateCovering), computed by golang/geo's RegionCoverer
+ *             {MinLevel:13, MaxLevel:13} (pkg/geo/s2.go:30-35);
+ *   search    the CockroachDB overlap queries behind
+ *             scdstore.OperationStore.SearchOperations (pkg/scd/store/store.go:29,
+ *             impl pkg/scd/store/cockroach/operations.go:374-445),
+ *             repos.ISA.SearchISAs (pkg/rid/repos/isa.go:27, impl
+ *             pkg/rid/cockroach/identification_service_area.go:166-197) and
+ *             repos.Subscription.SearchSubscriptions[ByOwner]
+ *             (pkg/rid/repos/subscription.go:26-29, impl
+ *             pkg/rid/cockroach/subscriptions.go:222-273).
+ *
+ * Conventions (cgo rule: C keeps no Go pointer after returning):
+ *   - cells are uint64 S2 CellIDs (level 13 on every covering output); the
+ *     store's INT64 columns are the same bits reinterpreted (quirk Q12);
+ *   - times are int64 microseconds since the Unix epoch (CRDB TIMESTAMPTZ
+ *     resolution, quirk Q19); altitudes float32 metres (REAL columns, Q20);
+ *   - NULLs: stored/query NULL altitude -> -INFINITY (lower) / +INFINITY
+ *     (upper); stored NULL starts_at -> DSSG_TIME_NULL_START; stored NULL
+ *     ends_at -> DSSG_TIME_NULL_END (such a row never matches, Q9); query
+ *     NULL start -> DSSG_TIME_NULL_START, query NULL end -> DSSG_TIME_NULL_END_Q.
+ *   - variable-size outputs use two-call sizing: pass capacity, get `*needed`;
+ *     DSSG_ERR_CAPACITY means "call again with capacity >= *needed".
+ *   - *_device entry points take device pointers (HBM resident) and a
+ *     hipStream_t passed as void*; outputs stay in context-owned device memory
+ *     until the next call on the same context.
+ * Every function returns 0 on success or a DSSG_ERR_* code; per-item covering
+ * errors are reported in a status array using the DSSG_ST_* codes.
+ */
+#ifndef DSSGPU_H
+#define DSSGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes ---------------------------------------------------- */
+#define DSSG_OK 0
+#define DSSG_ERR_INVALID 1   /* bad argument (null pointer, negative size) */
+#define DSSG_ERR_CAPACITY 2  /* output buffer too small; see *needed */
+#define DSSG_ERR_DEVICE 3    /* HIP runtime failure */
+#define DSSG_ERR_NOMEM 4
+#define DSSG_ERR_NO_DEVICE 5 /* no gfx950 device visible */
+
+/* ---- per-footprint covering status: the Go sentinel errors ----------- */
+#define DSSG_ST_OK 0
+#define DSSG_ST_BAD_COORD_SET 1     /* errBadCoordSet pkg/geo/s2.go:39, pkg/models/geo.go:37 */
+#define DSSG_ST_NOT_ENOUGH_POINTS 2 /* errNotEnoughPointsInPolygon pkg/geo/s2.go:38, pkg/models/geo.go:36 */
+#define DSSG_ST_ODD_COORDS 3        /* errOddNumberOfCoordinatesInAreaString pkg/geo/s2.go:37 */
+#define DSSG_ST_RADIUS 4            /* errRadiusMustBeLargerThan0 pkg/models/geo.go:38 */
+#define DSSG_ST_AREA_TOO_LARGE 5    /* *ErrAreaTooLarge pkg/geo/s2.go:59-66; area in area_km2[] */
+
+/* ---- footprint kinds --------------------------------------------------- */
+#define DSSG_KIND_POLYGON 0 /* models.GeoPolygon.CalculateCovering  pkg/models/geo.go:252-268 */
+#define DSSG_KIND_CIRCLE 1  /* models.GeoCircle.CalculateCovering   pkg/models/geo.go:224-239 */
+#define DSSG_KIND_POINTS 2  /* geo.Covering on parsed points (no lat/lng range check, Q5) pkg/geo/s2.go:99 */
+
+/* ---- time sentinels ---------------------------------------------------- */
+#define DSSG_TIME_NULL_START INT64_MIN
+#define DSSG_TIME_NULL_END INT64_MIN         /* stored ends_at NULL: row excluded */
+#define DSSG_TIME_NULL_END_Q INT64_MAX       /* query end NULL: COALESCE(..., true) */
+
+typedef struct dssg_ctx dssg_ctx;
+typedef struct dssg_index dssg_index;
+
+/* Device-resident covering result (context-owned, valid until next call). */
+typedef struct {
+    int64_t n;              /* footprints */
+    const int64_t *offs;    /* device, n+1 */
+    const uint64_t *cells;  /* device, offs[n] level-13 cells, sorted per footprint */
+    const int32_t *status;  /* device, n (DSSG_ST_*) */
+    const double *area_km2; /* device, n (loopAreaKm2 after the reversal step; 0 for circles) */
+    int64_t total_cells;
+} dssg_cells;
+
+/* Device-resident search result: unordered set of (query, entity) pairs,
+ * each pair once (SQL DISTINCT, quirk Q13). */
+typedef struct {
+    const uint32_t *q; /* device */
+    const uint32_t *e; /* device */
+    int64_t n;
+} dssg_pairs;
+
+/* ---- context ----------------------------------------------------------- */
+int dssg_create(int device, dssg_ctx **out);
+void dssg_destroy(dssg_ctx *ctx);
+const char *dssg_strerror(int code);
+const char *dssg_last_error(dssg_ctx *ctx);
+
+/* ---- covering ----------------------------------------------------------
+ * Footprint f: kind[f]; polygon/points vertices lat/lng[voff[f] .. voff[f+1]);
+ * circle centre lat/lng[voff[f]] with radius_m[f] (float32 metres, as
+ * GeoCircle.RadiusMeter).  Replaces geo.Covering / GeoPolygon / GeoCircle
+ * .CalculateCovering (pkg/geo/s2.go:99, pkg/models/geo.go:224,252).
+ */
+int dssg_cover_batch(dssg_ctx *ctx, int64_t n, const int32_t *kind, const int64_t *voff, const double *lat,
+                     const double *lng, const float *radius_m, int64_t *out_offs, uint64_t *out_cells,
+                     int64_t cells_cap, int64_t *cells_needed, int32_t *status, double *area_km2);
+int dssg_cover_batch_device(dssg_ctx *ctx, int64_t n, const int32_t *d_kind, const int64_t *d_voff,
+                            const double *d_lat, const double *d_lng, const float *d_radius_m, void *stream,
+                            dssg_cells *out);
+
+/* geo.AreaToCellIDs (pkg/geo/s2.go:129-166): parse "lat0,lng0,lat1,lng1,..."
+ * then Covering.  Status via *status (DSSG_ST_*). */
+int dssg_area_to_cell_ids(dssg_ctx *ctx, const char *area, uint64_t *out_cells, int64_t cap, int64_t *needed,
+                          int32_t *status, double *area_km2);
+
+/* ---- entity index (intents / ISAs / subscriptions) ----------------------
+ * Replaces the CRDB tables scd_operations + scd_cells_operations
+ * (pkg/scd/store/cockroach/store.go:120-147) and the RID INT64[] cells
+ * columns with INVERTED INDEX (pkg/rid/cockroach/store.go:122-151).
+ * Entity e: cells[cell_offs[e] .. cell_offs[e+1]), altitude [alt_lo, alt_hi],
+ * time [t0, t1] (us), owner id (int32, for SearchSubscriptionsByOwner).
+ */
+int dssg_index_build(dssg_ctx *ctx, int64_t n, const int64_t *cell_offs, const uint64_t *cells, const float *alt_lo,
+                     const float *alt_hi, const int64_t *t0, const int64_t *t1, const int32_t *owner,
+                     dssg_index **out);
+int dssg_index_build_device(dssg_ctx *ctx, int64_t n, const int64_t *d_cell_offs, const uint64_t *d_cells,
+                            const float *d_alt_lo, const float *d_alt_hi, const int64_t *d_t0, const int64_t *d_t1,
+                            const int32_t *d_owner, void *stream, dssg_index **out);
+void dssg_index_free(dssg_index *idx);
+int64_t dssg_index_num_postings(const dssg_index *idx);
+int64_t dssg_index_num_cells(const dssg_index *idx);
+
+/* ---- search -------------------------------------------------------------
+ * Generic 4D overlap join, the predicate every store search reduces to:
+ *   cells(q) && cells(e)  AND  e.t1 >= q.tlo  AND  e.t0 <= q.thi
+ *   AND e.alt_hi >= q.alt_lo AND e.alt_lo <= q.alt_hi
+ *   AND (q.owner < 0 OR e.owner == q.owner)
+ * q.tlo must be > INT64_MIN (it always carries `now` or `earliest`).
+ */
+int dssg_search_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *d_q_offs,
+                       const uint64_t *d_q_cells, const float *d_q_alt_lo, const float *d_q_alt_hi,
+                       const int64_t *d_q_tlo, const int64_t *d_q_thi, const int32_t *d_q_owner, void *stream,
+                       dssg_pairs *out);
+int dssg_search(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
+                const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
+                const int32_t *q_owner, uint32_t *out_q, uint32_t *out_e, int64_t cap, int64_t *needed);
+
+/* scdstore SearchOperations semantics (operations.go:374-435) for a batch of
+ * already-covered query volumes: q_start/q_end may be DSSG_TIME_NULL_START /
+ * DSSG_TIME_NULL_END_Q; altitudes NULL -> -/+INFINITY (SCD protos always set
+ * them, quirk Q8); `now_us` is the store clock.  Owner is ignored (Q6). */
+int dssg_search_operations(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *q_offs,
+                           const uint64_t *q_cells, const float *q_alt_lo, const float *q_alt_hi,
+                           const int64_t *q_start, const int64_t *q_end, int64_t now_us, uint32_t *out_q,
+                           uint32_t *out_e, int64_t cap, int64_t *needed);
+/* repos.ISA.SearchISAs (identification_service_area.go:166-197): earliest
+ * required (the app layer clamps it to now, pkg/rid/application/isa.go:38-45),
+ * latest may be DSSG_TIME_NULL_END_Q.  No altitude filter. */
+int dssg_search_isas(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *q_offs,
+                     const uint64_t *q_cells, const int64_t *earliest, const int64_t *latest, uint32_t *out_q,
+                     uint32_t *out_e, int64_t cap, int64_t *needed);
+/* repos.Subscription.SearchSubscriptions / SearchSubscriptionsByOwner
+ * (subscriptions.go:222-273): owner < 0 means "any owner". */
+int dssg_search_subscriptions(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *q_offs,
+                              const uint64_t *q_cells, const int32_t *owner, int64_t now_us, uint32_t *out_q,
+                              uint32_t *out_e, int64_t cap, int64_t *needed);
+
+/* ---- diagnostics --------------------------------------------------------
+ * Average device time (ms) of the most recent launches of the named kernel
+ * phase, measured with HIP events on the launching stream (bench.py). */
+int dssg_phase_times(dssg_ctx *ctx, double *cover_ms, double *join_ms, double *join_kernel_ms);
+void dssg_set_timing(dssg_ctx *ctx, int enabled);
+/* Copy `bytes` from an engine-owned device buffer (dssg_cells / dssg_pairs)
+ * to host memory, on the context's device. */
+int dssg_copy_to_host(dssg_ctx *ctx, void *dst, const void *src, size_t bytes);
+/* Evaluate the device restatement of a Go math routine on n inputs
+ * (op: 0 sin, 1 cos, 2 tan, 3 atan, 4 atan2(x, y), 5 asin, 6 sqrt, 7 x/y,
+ * 8 stToUV, 9 uvToST, 10 PointFromLatLng(x, y).X) -- for bit-exact tests. */
+int dssg_selftest_math(dssg_ctx *ctx, int op, int64_t n, const double *x, const double *y, double *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -30,6 +30,21 @@
 void orc_free(void *p) { free(p); }
 
 /* ------------------------------------------------------------ covering */
+/* pkg/geo/s2.go:145-165: AreaToCellIDs converts without a range check (Q5)
+ * and needs >= 3 points, then Covering. */
+static int points_covering(const double *lat, const double *lng, int n, uint64_t *out, size_t cap, size_t *needed,
+                           double *area)
+{
+    *needed = 0;
+    *area = 0;
+    if (n < 3) return ORC_ERR_NOT_ENOUGH_POINTS;
+    double *xyz = (double *)malloc(sizeof(double) * 3 * (size_t)n);
+    if (!xyz) return ORC_ERR_NOMEM;
+    for (int i = 0; i < n; i++) orc_point_from_degrees(lat[i], lng[i], xyz + 3 * i);
+    int rc = orc_covering_xyz(xyz, n, out, cap, needed, area);
+    free(xyz);
+    return rc;
+}
 typedef struct {
     int64_t n;
     const int32_t *kind;
@@ -64,6 +79,8 @@ static void *cover_worker(void *arg)
                 int64_t v0 = j->voff[f], nv = j->voff[f + 1] - v0;
                 if (j->kind[f] == ORC_KIND_CIRCLE)
                     rc = orc_circle_covering(j->lat[v0], j->lng[v0], j->radius_m[f], buf, cap, &needed);
+                else if (j->kind[f] == ORC_KIND_POINTS_XYZ)
+                    rc = points_covering(j->lat + v0, j->lng + v0, (int)nv, buf, cap, &needed, &area);
                 else
                     rc = orc_polygon_covering(j->lat + v0, j->lng + v0, (int)nv, buf, cap, &needed, &area);
                 if (rc == ORC_OK && needed > cap) {

@@ -9,6 +9,7 @@
 #include <stdint.h>
 
 #define ORC_COVER_LEVEL 13
+#define ORC_MAX_CELLS (1u << 24) /* oracle refuses coverings above this */
 
 /* Status codes: one per Go sentinel error on the path (same numbering as the
  * product ABI, include/dssgpu.h). */

@@ -1091,7 +1091,13 @@ static int cover_descend(void *ctx, IntersectsFn fn, uint64_t id, int level, U64
 {
     Cell c = cell_from_id(id);
     if (!fn(ctx, &c)) return 0;
-    if (level == ORC_COVER_LEVEL) return u64_push(out, id);
+    if (level == ORC_COVER_LEVEL) {
+        /* safety valve for invalid (self-intersecting) loops whose parity
+         * interior is most of the sphere: the reference would try to emit
+         * ~4e8 cells; the oracle reports it instead. */
+        if (out->n >= ORC_MAX_CELLS) return -1;
+        return u64_push(out, id);
+    }
     uint64_t ch = cellid_child_begin(id);
     for (int k = 0; k < 4; k++, ch = cellid_next(ch))
         if (cover_descend(ctx, fn, ch, level + 1, out)) return -1;

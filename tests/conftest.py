@@ -1,0 +1,31 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a gfx950 (MI355X) device and libdss_amd.so")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import oracle as O
+    O.build()
+    return O
+
+
+@pytest.fixture(scope="session")
+def golden_covering():
+    import numpy as np
+    return dict(np.load(os.path.join(ROOT, "tests", "golden", "covering.npz"), allow_pickle=False))
+
+
+@pytest.fixture(scope="session")
+def golden_search():
+    import numpy as np
+    return dict(np.load(os.path.join(ROOT, "tests", "golden", "search.npz"), allow_pickle=False))

@@ -1,0 +1,125 @@
+"""CPU: the oracle against the reference's own known-answer tests.
+
+Pins the covering restatement on pkg/models/geo_test.go:10-55 (exact 20-cell
+KAT) and the status-level cases of pkg/geo/s2_test.go:12-52 and the prober.
+"""
+import math
+
+import numpy as np
+import pytest
+
+KAT_TOKENS = ("808fb0ac 808fb744 808fb754 808fb75c 808fb9fc 808fba04 808fba0c 808fba14 808fba1c 808fba5c "
+              "808fba64 808fba6c 808fba74 808fba8c 808fbad4 808fbadc 808fbae4 808fbaec 808fbaf4 808fbb2c").split()
+
+
+def area_to_cell_ids(O, area: str):
+    """pkg/geo/s2.go:129-166 restated on top of the oracle's Covering."""
+    num = area.count(",") + 1
+    if num % 2 == 1:
+        return O.ERR_ODD_COORDS, None
+    if num // 2 < 3:
+        return O.ERR_NOT_ENOUGH_POINTS, None
+    vals = []
+    for tok in area.split(","):
+        try:
+            vals.append(float(tok.strip()))
+        except ValueError:
+            return O.ERR_BAD_COORD_SET, None
+    pts = [O.point_from_degrees(vals[i], vals[i + 1]) for i in range(0, len(vals), 2)]
+    rc, cells, _ = O.covering_xyz(np.array(pts))
+    return rc, cells
+
+
+def test_polygon_covering_kat(oracle):
+    # pkg/models/geo_test.go:10-55
+    rc, cells, _ = oracle.polygon_covering([37.427636, 37.408799, 37.421265], [-122.170502, -122.064069, -122.086504])
+    assert rc == oracle.OK
+    assert [oracle.token(int(c)) for c in cells] == KAT_TOKENS
+
+
+@pytest.mark.parametrize("area,ok", [
+    ("37.4047,-122.1474,37.4037,-122.1485,37.4035,-122.1466", True),            # s2_test.go:12-16
+    ("0.000,0.000, 0.000,0.005, -0.005,0.0025", True),                           # :18-22 (CW -> reversal)
+    ("37.4047,-122.1474,37.4037,-122.1485,37.4035,-122.1466,37.4035,-122.1466", True),  # :24-28
+    ("37.427636,-122.170502,37.408799,-122.064069,37.421265,-122.086504", True),  # :30-34 testdata.Loop
+    ("", False),                                                                 # :36-40
+    ("37.427636,-122.170502,37.408799,-122.064069", False),                     # :42-46 two points
+    ("37.427636,-122.170502,37.408799", False),                                  # :48-52 odd coords
+])
+def test_area_to_cell_ids_status(oracle, area, ok):
+    rc, cells = area_to_cell_ids(oracle, area)
+    assert (rc == oracle.OK) == ok
+    if ok:
+        assert cells is not None and len(cells) > 0
+
+
+def test_area_too_large_prober_huge(oracle):
+    # monitoring/prober/rid/common.py:29-49 HUGE polygon -> 413 (AreaTooLarge)
+    rc, cells, area = oracle.polygon_covering([-23, -24, -24, -23], [130, 130, 132, 132])
+    assert rc == oracle.ERR_AREA_TOO_LARGE
+    # Q1 + Q4: the box (~2.27e4 km^2, pi^2-inflated to ~2.24e5) is over the cap
+    # in its given order, so it is reversed, and the error reports the area of
+    # the reversed loop -- its complement on the sphere.
+    assert area > 5.0e9
+    _, _, area2 = oracle.polygon_covering([-23, -23, -24, -24], [130, 132, 132, 130])
+    assert 2.0e5 < area2 < 2.5e5
+
+
+def test_degenerate_polygon_is_polyline(oracle):
+    # op_request_3.json: three identical vertices -> zero area -> Polyline covering
+    lat, lng = 37.78943798147498, -122.45464324951172
+    rc, cells, area = oracle.polygon_covering([lat] * 3, [lng] * 3)
+    assert rc == oracle.OK and area == 0.0
+    assert [int(c) for c in cells] == [oracle.cellid_from_degrees(lat, lng, 13)]
+
+
+def test_polygon_checks_coordinates_before_count(oracle):
+    # Q17: pkg/models/geo.go:257-266
+    rc, _, _ = oracle.polygon_covering([91.0, 0.0], [0.0, 0.0])
+    assert rc == oracle.ERR_BAD_COORD_SET
+    rc, _, _ = oracle.polygon_covering([90.0, 0.0], [180.0, 0.0])
+    assert rc == oracle.ERR_NOT_ENOUGH_POINTS
+
+
+def test_circle_status(oracle):
+    assert oracle.circle_covering(0, 0, 0)[0] == oracle.ERR_RADIUS
+    assert oracle.circle_covering(0, 0, float("nan"))[0] == oracle.ERR_RADIUS
+    assert oracle.circle_covering(91, 0, 10)[0] == oracle.ERR_BAD_COORD_SET
+    rc, cells = oracle.circle_covering(-56, 178, 50)   # scd/test_operation_simple.py:18
+    assert rc == oracle.OK and len(cells) >= 1
+
+
+def test_circle_overlap_pins(oracle):
+    # scd/test_operation_simple.py: op circle r=50 m found by query r=300 m
+    _, a = oracle.circle_covering(-56, 178, 50)
+    _, b = oracle.circle_covering(-56, 178, 300)
+    assert set(a.tolist()) <= set(b.tolist())
+    # scd/test_subscription_simple.py:22,96
+    _, c = oracle.circle_covering(12, -34, 300)
+    _, d = oracle.circle_covering(12.00001, -34.00001, 50)
+    assert set(c.tolist()) & set(d.tolist())
+
+
+def test_go_math_close_to_libm(oracle):
+    rng = np.random.default_rng(1)
+    for x in rng.uniform(-7, 7, 200):
+        for go, ref in ((oracle.lib().orc_go_sin, math.sin), (oracle.lib().orc_go_cos, math.cos),
+                        (oracle.lib().orc_go_atan, math.atan)):
+            assert abs(go(x) - ref(x)) <= 2 * math.ulp(ref(x)) + 1e-300
+        y = rng.uniform(-3, 3)
+        assert abs(oracle.lib().orc_go_atan2(y, x) - math.atan2(y, x)) <= 4e-16 * max(1, abs(math.atan2(y, x)))
+
+
+def test_regular_loop_is_ccw_20gon(oracle):
+    import ctypes as C
+    xyz = np.zeros(60)
+    oracle.lib().orc_regular_loop(37.0, -122.0, 1000.0, 20, xyz.ctypes.data_as(C.POINTER(C.c_double)))
+    pts = xyz.reshape(20, 3)
+    assert np.allclose(np.linalg.norm(pts, axis=1), 1.0, atol=1e-15)
+    c = oracle.point_from_degrees(37.0, -122.0)
+    d = np.arccos(np.clip(pts @ c, -1, 1)) * 6371010.0
+    assert np.allclose(d, 1000.0, rtol=1e-6)  # arccos near 1 is ill-conditioned
+    # counter-clockwise about the centre (the interior is the small cap)
+    for k in range(20):
+        a, b = pts[k] - c, pts[(k + 1) % 20] - c
+        assert np.dot(np.cross(a, b), c) > 0
