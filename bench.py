@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""Benchmark: 4D conflict queries/s against a resident N-intent airspace.
+
+BASELINE.json metric "4D conflict queries/sec vs N-intent airspace
+(1/2/4/8 GPU); coverings/sec", workload configs[1]: 1M polygon/circle query
+footprints per GPU step against a 1M-intent index, SF-Bay metro region
+(seeded synthetic data, SURVEY.md s8(d) generator).
+
+One step = cover the rank's 1M query footprints on the GPU (level-13 S2
+coverings) -> overlap join against the HBM-resident index -> fused
+altitude/time/now filter -> deduplicated (query, intent) pairs resident in
+HBM.  The index (intent coverings + posting lists) is built before timing.
+
+Multi-GPU (torchrun, one process per GPU): the index fits every GPU's HBM
+many times over (~0.3 GB for 1M intents), so each rank holds a replica and
+owns a disjoint 1M-query slice of the global batch -- no exchange on the data
+path ("scaling": "weak").  Timing: barrier + synchronize on
+both sides of exactly --steps steps, max over ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 vector (spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=1)
+    ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug only; invalid for the metric)")
+    ap.add_argument("--cpu-sample", type=int, default=20000, help="queries in the CPU-baseline sample (0: skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from dss_amd import _lib, device as D, workload as W
+
+    ctx = _lib.context(local)
+    dev = f"cuda:{local}"
+
+    # ---------------------------------------------------------------- setup
+    t_setup = time.time()
+    rng_i = np.random.default_rng(20201015 + args.config)   # same airspace on every rank
+    cfg_n = {0: (10_000, 100_000), 1: (1_000_000, 1_000_000)}[args.config]
+    nq = max(1, int(cfg_n[0] * args.scale))
+    ni = max(1, int(cfg_n[1] * args.scale))
+    intents = W.metro_footprints(rng_i, ni)
+    ia = W.intent_attrs(rng_i, ni)
+    rng_q = np.random.default_rng(20201015 + args.config + 1000 * (rank + 1))  # rank's query slice
+    queries = W.metro_footprints(rng_q, nq)
+    qa = W.query_attrs(rng_q, nq)
+    now = W.T0_US
+    tlo = np.maximum(qa.t0, now)  # operations.go:398-402 COALESCE(ends_at >= start) AND ends_at >= now
+    t = lambda a: torch.as_tensor(a, device=dev)  # noqa: E731
+    d_int = D.DeviceFootprints.upload(intents, dev)
+    d_q = D.DeviceFootprints.upload(queries, dev)
+    q_alo, q_ahi, q_tlo, q_thi = t(qa.alt_lo), t(qa.alt_hi), t(tlo), t(qa.t1)
+    i_alo, i_ahi, i_t0, i_t1 = t(ia.alt_lo), t(ia.alt_hi), t(ia.t0), t(ia.t1)
+    torch.cuda.synchronize()
+    tb = time.time()
+    icells = D.cover(ctx, d_int)
+    index = D.build_index(ctx, icells, i_alo, i_ahi, i_t0, i_t1)
+    torch.cuda.synchronize()
+    build_s = time.time() - tb
+    n_post = int(ctx.L.dssg_index_num_postings(index))
+    # keep intent cells for the CPU baseline before the next cover() reuses buffers
+    i_offs_h = D.copy_back(ctx, icells.offs, ni + 1, np.int64) if rank == 0 else None
+    i_cells_h = D.copy_back(ctx, icells.cells, int(i_offs_h[-1]), np.uint64) if rank == 0 else None
+    log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s, index build {build_s:.2f}s, postings {n_post}")
+
+    def step():
+        cells = D.cover(ctx, d_q)
+        pairs = D.search(ctx, index, cells, q_alo, q_ahi, q_tlo, q_thi)
+        return cells, pairs
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # ------------------------------------------------------------ timed steps
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        cells, pairs = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ms_per_step = 1000.0 * elapsed / max(1, args.steps)
+    value = world * nq * args.steps / elapsed
+
+    # ------------------------------------------- phase timing + roofline
+    ctx.L.dssg_set_timing(ctx.h, 1)
+    cover_ms, join_ms, kern_ms = [], [], []
+    for _ in range(3):
+        cells, pairs = step()
+        a, b, c = (np.zeros(1), np.zeros(1), np.zeros(1))
+        import ctypes as C
+        ca, cb, cc = C.c_double(), C.c_double(), C.c_double()
+        ctx.L.dssg_phase_times(ctx.h, C.byref(ca), C.byref(cb), C.byref(cc))
+        cover_ms.append(ca.value)
+        join_ms.append(cb.value)
+        kern_ms.append(cc.value)
+    ctx.L.dssg_set_timing(ctx.h, 0)
+    import ctypes as C
+    m_tot, d_tot = C.c_int64(), C.c_int64()
+    ctx.check(ctx.L.dssg_search_stats_device(ctx.h, index, cells.n, C.c_void_p(cells.offs), C.c_void_p(cells.cells),
+                                             D._stream_ptr(), C.byref(m_tot), C.byref(d_tot)))
+    c_tot = int(cells.total_cells)
+    r_tot = int(pairs.n)
+    join_bytes = 8 * c_tot + 12 * m_tot.value + 24 * d_tot.value + 8 * r_tot   # SURVEY s8(d) B_q summed
+    kern_avg_ms = float(np.mean(kern_ms))
+    achieved = join_bytes / (kern_avg_ms * 1e-3) / 1e9
+    cover_avg = float(np.mean(cover_ms))
+    join_avg = float(np.mean(join_ms))
+
+    result = None
+    if rank == 0:
+        cpu = None
+        if args.cpu_sample > 0:
+            cpu = cpu_baseline(args, intents, ia, queries, qa, now, i_offs_h, i_cells_h)
+        result = {
+            "metric": "4D conflict queries/sec vs N-intent airspace",
+            "value": value,
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded SURVEY s8(d) generator; no datasets)",
+            "config": {"workload": f"configs[{args.config}]: {nq} query footprints/GPU/step (70% polygon, 30% circle)"
+                                   f" vs {ni}-intent resident index, SF-Bay metro, S2 level 13",
+                       "queries_per_gpu_step": nq, "intents": ni, "postings": n_post,
+                       "parallelism": f"query-sharded x{world}, index replicated", "scale": args.scale},
+            "coverings_per_s": world * nq / (cover_avg * 1e-3),
+            "phase_ms": {"cover": cover_avg, "join": join_avg, "join_kernel": kern_avg_ms},
+            "pairs_per_step": r_tot,
+            "index_build_s": build_s,
+            "roofline": {"kernel": "k_join (overlap join + fused filter)", "bound": "hbm",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "algorithmic_bytes": join_bytes,
+                         "counts": {"C": c_tot, "M": m_tot.value, "D": d_tot.value, "R": r_tot}},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    ctx.L.dssg_index_free(index)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, intents, ia, queries, qa, now, i_offs, i_cells):
+    """The CPU restatement (oracle/, kind "port") timed on this host on a
+    bounded sample: cover `cpu_sample` queries + search them against the
+    same 1M-intent posting list (built untimed)."""
+    from oracle import oracle as O
+    O.build()
+    n = min(args.cpu_sample, queries.n)
+    sub = queries.subset(np.arange(n))
+    th = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    idx = O.Index(i_offs, i_cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1)
+    t0 = time.perf_counter()
+    qo, qc, _, _ = O.cover_batch(sub.kind, sub.voff, sub.lat, sub.lng, sub.radius_m, nthreads=th)
+    t1 = time.perf_counter()
+    tlo = np.maximum(qa.t0[:n], now)
+    idx.search(qo, qc, qa.alt_lo[:n], qa.alt_hi[:n], tlo, qa.t1[:n], nthreads=th)
+    t2 = time.perf_counter()
+    return {"value": n / (t2 - t0), "unit": "queries/s", "cores": th, "kind": "port",
+            "sample": f"{n} queries (cover + search) vs the full {intents.n}-intent index",
+            "coverings_per_s": n / (t1 - t0), "seconds": t2 - t0}
+
+
+if __name__ == "__main__":
+    main()

@@ -64,6 +64,14 @@ def load():
         if not os.path.exists(LIB_PATH):
             raise DssgError(DSSG_ERR_NO_DEVICE,
                             f"{LIB_PATH} missing: build it with __graft_entry__.build() (no CPU fallback exists)")
+        # One HIP runtime per process: the torch wheel bundles its own
+        # libamdhip64.so.7 (same SONAME as /opt/rocm's).  If torch is
+        # importable, load it first so this library binds to the same runtime
+        # torch's device buffers come from (torch is plumbing only).
+        try:
+            import torch  # noqa: F401
+        except Exception:
+            pass
         L = C.CDLL(LIB_PATH)
         P, vp = C.POINTER, C.c_void_p
         i32, i64, d, f = C.c_int32, C.c_int64, C.c_double, C.c_float
@@ -98,6 +106,7 @@ def load():
         L.dssg_phase_times.argtypes = [vp, P(d), P(d), P(d)]
         L.dssg_set_timing.argtypes = [vp, C.c_int]
         L.dssg_set_timing.restype = None
+        L.dssg_search_stats_device.argtypes = [vp, vp, i64, vp, vp, vp, P(i64), P(i64)]
         L.dssg_copy_to_host.argtypes = [vp, vp, vp, C.c_size_t]
         L.dssg_selftest_math.argtypes = [vp, C.c_int, i64, P(d), P(d), P(d)]
         _lib = L

@@ -465,6 +465,16 @@ int dssg_search_subscriptions(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, 
                        cap, needed);
 }
 
+int dssg_search_stats_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *d_q_offs,
+                             const uint64_t *d_q_cells, void *stream, int64_t *matched, int64_t *distinct)
+{
+    if (!ctx || !idx || nq < 0 || !matched || !distinct || (nq > 0 && !d_q_offs)) return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        ctx->search.stats(idx, nq, d_q_offs, d_q_cells, s, matched, distinct);
+    });
+}
+
 int dssg_copy_to_host(dssg_ctx *ctx, void *dst, const void *src, size_t bytes)
 {
     if (!ctx || (bytes && (!dst || !src))) return DSSG_ERR_INVALID;

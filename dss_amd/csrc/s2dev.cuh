@@ -458,7 +458,7 @@ DSS_HD bool edge_intersects_rect(double au, double av, double bu, double bv, dou
 // packed 2 bits per entry, 8 bits per orientation row.
 DSS_HD int ij_to_pos(int orientation, int ij) { return (int)((0x361E9CB4u >> (8 * orientation + 2 * ij)) & 3u); }
 DSS_HD int pos_to_ij(int orientation, int pos) { return (int)((0x874B78B4u >> (8 * orientation + 2 * pos)) & 3u); }
-DSS_HD int pos_to_orientation(int pos) { return (int)((0xC4u >> (2 * pos)) & 3u); }  // {1,0,0,3}
+DSS_HD int pos_to_orientation(int pos) { return (int)((0xC1u >> (2 * pos)) & 3u); }  // {1,0,0,3}
 
 DSS_HD uint64_t lsb_for_level(int level) { return 1ull << (2 * (kMaxLevel - level)); }
 DSS_HD uint64_t cellid_lsb_dev(uint64_t id) { return id & (~id + 1); }

@@ -162,6 +162,10 @@ struct JoinArgs {
     uint32_t *out_q, *out_e;
     unsigned long long *counter;
     int64_t cap;
+    // stats mode (roofline accounting): predicate off, count postings
+    // scanned (M) and canonical survivors (= distinct candidates D)
+    int stats;
+    unsigned long long *stat_m, *stat_d;
 };
 
 __device__ __forceinline__ void lookup(const JoinArgs &a, uint64_t c, uint32_t &s, uint32_t &e)
@@ -213,6 +217,7 @@ __global__ __launch_bounds__(kBlock) void k_join(JoinArgs a)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int64_t q = (int64_t)blockIdx.x * (kBlock / 64) + w;
     int staged = 0;
+    unsigned long long my_m = 0, my_d = 0;
     auto flush = [&]() {
         unsigned long long base = 0;
         if (lane == 0 && staged) base = atomicAdd(a.counter, (unsigned long long)staged);
@@ -247,12 +252,17 @@ __global__ __launch_bounds__(kBlock) void k_join(JoinArgs a)
                     ent = pe & ~kFirstBit;
                     // COALESCE'd predicates of operations.go:394-402 after
                     // the NULL->sentinel mapping (dssgpu.h)
-                    pass = t.y >= tlo && t.x <= thi && alt.y >= alo && alt.x <= ahi;
-                    if (pass && own >= 0) pass = a.p_owner[p] == own;
+                    pass = a.stats || (t.y >= tlo && t.x <= thi && alt.y >= alo && alt.x <= ahi);
+                    if (pass && own >= 0 && !a.stats) pass = a.p_owner[p] == own;
                     if (pass && ci != c0 && !(pe & kFirstBit)) pass = smallest_shared(a, ent, c, qc, ci - c0);
                 }
                 unsigned long long m = __ballot(pass);
                 int nsurv = __popcll(m);
+                if (a.stats) {
+                    my_m += (unsigned long long)(e - base < 64 ? e - base : 64);
+                    my_d += (unsigned long long)nsurv;
+                    continue;
+                }
                 if (nsurv == 0) continue;
                 if (staged + nsurv > kStage) flush();
                 if (pass) {
@@ -263,6 +273,13 @@ __global__ __launch_bounds__(kBlock) void k_join(JoinArgs a)
                 staged += nsurv;
             }
         }
+    }
+    if (a.stats) {
+        if (lane == 0 && (my_m || my_d)) {
+            atomicAdd(a.stat_m, my_m);
+            atomicAdd(a.stat_d, my_d);
+        }
+        return;
     }
     flush();
 }
@@ -392,6 +409,47 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
 }
 
 // ---------------------------------------------------------------- search
+static JoinArgs make_args(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
+                          const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
+                          const int32_t *q_owner)
+{
+    JoinArgs a{};
+    a.nq = nq; a.q_offs = q_offs; a.q_cells = q_cells; a.q_alo = q_alt_lo; a.q_ahi = q_alt_hi;
+    a.q_tlo = q_tlo; a.q_thi = q_thi; a.q_owner = q_owner;
+    a.p_e = idx->p_e.p; a.p_alt = idx->p_alt.p; a.p_t = idx->p_t.p; a.p_owner = idx->p_owner.p;
+    a.e_offs = idx->e_offs.p; a.e_cells = idx->e_cells.p;
+    a.kmin = idx->kmin; a.n_dense = idx->n_dense; a.dense = idx->dense.p;
+    a.n_irr = idx->n_irr; a.irr_cells = idx->irr_cells.p; a.irr_start = idx->irr_start.p;
+    return a;
+}
+
+void SearchEngine::stats(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells, hipStream_t s,
+                         int64_t *matched, int64_t *distinct)
+{
+    unsigned long long *cnt = counter_.ensure(4);
+    DSS_HIP(hipMemsetAsync(cnt, 0, 4 * sizeof(unsigned long long), s));
+    JoinArgs a = make_args(idx, nq, q_offs, q_cells, nullptr, nullptr, nullptr, nullptr, nullptr);
+    // the predicate reads are skipped in stats mode; give the kernel valid
+    // (unused) query attribute pointers anyway
+    DevBuf<float> fz;
+    DevBuf<int64_t> iz;
+    float *f = fz.ensure(nq + 1);
+    int64_t *t = iz.ensure(nq + 1);
+    DSS_HIP(hipMemsetAsync(f, 0, sizeof(float) * (nq + 1), s));
+    DSS_HIP(hipMemsetAsync(t, 0, sizeof(int64_t) * (nq + 1), s));
+    a.q_alo = f; a.q_ahi = f; a.q_tlo = t; a.q_thi = t;
+    a.stats = 1;
+    a.stat_m = cnt + 1;
+    a.stat_d = cnt + 2;
+    a.counter = cnt;
+    if (nq > 0) hipLaunchKernelGGL(k_join, dim3(grid_for(nq, kBlock / 64)), dim3(kBlock), 0, s, a);
+    unsigned long long h[4];
+    DSS_HIP(hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    *matched = (int64_t)h[1];
+    *distinct = (int64_t)h[2];
+}
+
 void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
                           const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
                           const int32_t *q_owner, hipStream_t s, dssg_pairs *out)
@@ -402,13 +460,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     for (int attempt = 0; attempt < 3; attempt++) {
         uint32_t *oq = oq_.ensure(out_cap_), *oe = oe_.ensure(out_cap_);
         DSS_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned long long), s));
-        JoinArgs a;
-        a.nq = nq; a.q_offs = q_offs; a.q_cells = q_cells; a.q_alo = q_alt_lo; a.q_ahi = q_alt_hi;
-        a.q_tlo = q_tlo; a.q_thi = q_thi; a.q_owner = q_owner;
-        a.p_e = idx->p_e.p; a.p_alt = idx->p_alt.p; a.p_t = idx->p_t.p; a.p_owner = idx->p_owner.p;
-        a.e_offs = idx->e_offs.p; a.e_cells = idx->e_cells.p;
-        a.kmin = idx->kmin; a.n_dense = idx->n_dense; a.dense = idx->dense.p;
-        a.n_irr = idx->n_irr; a.irr_cells = idx->irr_cells.p; a.irr_start = idx->irr_start.p;
+        JoinArgs a = make_args(idx, nq, q_offs, q_cells, q_alt_lo, q_alt_hi, q_tlo, q_thi, q_owner);
         a.out_q = oq; a.out_e = oe; a.counter = counter; a.cap = (int64_t)out_cap_;
         if (timing_) {
             if (!ev0_) { DSS_HIP(hipEventCreate(&ev0_)); DSS_HIP(hipEventCreate(&ev1_)); }

@@ -37,6 +37,10 @@ class SearchEngine {
     void search(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
                 const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
                 const int32_t *q_owner, hipStream_t s, dssg_pairs *out);
+    // Roofline accounting: postings scanned and distinct candidate entities
+    // (predicate disabled), i.e. sum_q M_q and sum_q D_q of SURVEY s8(d).
+    void stats(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells, hipStream_t s,
+               int64_t *matched, int64_t *distinct);
     void set_timing(bool on) { timing_ = on; }
     double last_join_kernel_ms() const { return join_ms_; }
 

@@ -172,6 +172,11 @@ int dssg_search_subscriptions(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, 
  * phase, measured with HIP events on the launching stream (bench.py). */
 int dssg_phase_times(dssg_ctx *ctx, double *cover_ms, double *join_ms, double *join_kernel_ms);
 void dssg_set_timing(dssg_ctx *ctx, int enabled);
+/* Roofline accounting for a device query batch: total postings the join
+ * scans (sum of M_q) and distinct candidate entities before the
+ * altitude/time filter (sum of D_q), SURVEY.md s8(d). */
+int dssg_search_stats_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *d_q_offs,
+                             const uint64_t *d_q_cells, void *stream, int64_t *matched, int64_t *distinct);
 /* Copy `bytes` from an engine-owned device buffer (dssg_cells / dssg_pairs)
  * to host memory, on the context's device. */
 int dssg_copy_to_host(dssg_ctx *ctx, void *dst, const void *src, size_t bytes);

@@ -241,29 +241,67 @@ static void *search_worker(void *arg)
     return NULL;
 }
 
-int64_t orc_search(int64_t ne, const int64_t *e_offs, const uint64_t *e_cells, const float *e_alt_lo,
-                   const float *e_alt_hi, const int64_t *e_t0, const int64_t *e_t1, const int32_t *e_owner,
-                   int64_t nq, const int64_t *q_offs, const uint64_t *q_cells, const float *q_alt_lo,
-                   const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi, const int32_t *q_owner,
-                   int nthreads, uint32_t **out_q, uint32_t **out_e)
+struct orc_index {
+    Posting *post;
+    int64_t np, ne;
+    float *alo, *ahi;
+    int64_t *t0, *t1;
+    int32_t *owner;
+};
+
+orc_index *orc_index_new(int64_t ne, const int64_t *e_offs, const uint64_t *e_cells, const float *e_alt_lo,
+                         const float *e_alt_hi, const int64_t *e_t0, const int64_t *e_t1, const int32_t *e_owner)
 {
+    orc_index *x = (orc_index *)calloc(1, sizeof(orc_index));
     int64_t np = e_offs[ne];
-    Posting *post = (Posting *)malloc(sizeof(Posting) * (size_t)(np ? np : 1));
+    x->np = np;
+    x->ne = ne;
+    x->post = (Posting *)malloc(sizeof(Posting) * (size_t)(np ? np : 1));
     for (int64_t e = 0; e < ne; e++)
         for (int64_t k = e_offs[e]; k < e_offs[e + 1]; k++) {
-            post[k].cell = e_cells[k];
-            post[k].e = (uint32_t)e;
+            x->post[k].cell = e_cells[k];
+            x->post[k].e = (uint32_t)e;
         }
-    qsort(post, (size_t)np, sizeof(Posting), cmp_posting);
+    qsort(x->post, (size_t)np, sizeof(Posting), cmp_posting);
+    size_t n1 = (size_t)(ne ? ne : 1);
+    x->alo = (float *)malloc(n1 * sizeof(float));
+    x->ahi = (float *)malloc(n1 * sizeof(float));
+    x->t0 = (int64_t *)malloc(n1 * sizeof(int64_t));
+    x->t1 = (int64_t *)malloc(n1 * sizeof(int64_t));
+    x->owner = (int32_t *)calloc(n1, sizeof(int32_t));
+    memcpy(x->alo, e_alt_lo, (size_t)ne * sizeof(float));
+    memcpy(x->ahi, e_alt_hi, (size_t)ne * sizeof(float));
+    memcpy(x->t0, e_t0, (size_t)ne * sizeof(int64_t));
+    memcpy(x->t1, e_t1, (size_t)ne * sizeof(int64_t));
+    if (e_owner) memcpy(x->owner, e_owner, (size_t)ne * sizeof(int32_t));
+    return x;
+}
+
+void orc_index_free(orc_index *x)
+{
+    if (!x) return;
+    free(x->post);
+    free(x->alo);
+    free(x->ahi);
+    free(x->t0);
+    free(x->t1);
+    free(x->owner);
+    free(x);
+}
+
+int64_t orc_index_search(const orc_index *x, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
+                         const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
+                         const int32_t *q_owner, int nthreads, uint32_t **out_q, uint32_t **out_e)
+{
     SearchJob j;
     memset(&j, 0, sizeof(j));
-    j.post = post;
-    j.np = np;
-    j.e_alt_lo = e_alt_lo;
-    j.e_alt_hi = e_alt_hi;
-    j.e_t0 = e_t0;
-    j.e_t1 = e_t1;
-    j.e_owner = e_owner;
+    j.post = x->post;
+    j.np = x->np;
+    j.e_alt_lo = x->alo;
+    j.e_alt_hi = x->ahi;
+    j.e_t0 = x->t0;
+    j.e_t1 = x->t1;
+    j.e_owner = x->owner;
     j.q_offs = q_offs;
     j.q_cells = q_cells;
     j.q_alt_lo = q_alt_lo;
@@ -296,8 +334,20 @@ int64_t orc_search(int64_t ne, const int64_t *e_offs, const uint64_t *e_cells, c
     }
     free(j.res);
     free(j.cnt);
-    free(post);
     *out_q = oq;
     *out_e = oe;
     return total;
+}
+
+int64_t orc_search(int64_t ne, const int64_t *e_offs, const uint64_t *e_cells, const float *e_alt_lo,
+                   const float *e_alt_hi, const int64_t *e_t0, const int64_t *e_t1, const int32_t *e_owner,
+                   int64_t nq, const int64_t *q_offs, const uint64_t *q_cells, const float *q_alt_lo,
+                   const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi, const int32_t *q_owner,
+                   int nthreads, uint32_t **out_q, uint32_t **out_e)
+{
+    orc_index *x = orc_index_new(ne, e_offs, e_cells, e_alt_lo, e_alt_hi, e_t0, e_t1, e_owner);
+    int64_t n = orc_index_search(x, nq, q_offs, q_cells, q_alt_lo, q_alt_hi, q_tlo, q_thi, q_owner, nthreads, out_q,
+                                 out_e);
+    orc_index_free(x);
+    return n;
 }

@@ -43,6 +43,7 @@ int orc_robust_sign(const double *a, const double *b, const double *c);
 int orc_loop_contains(const double *xyz, int n, const double *p);
 void orc_cell_uv_bound(uint64_t id, double out[4]);
 void orc_cell_center(uint64_t id, double out[3]);
+uint64_t orc_cellid_from_face_ij_level(int face, int i, int j, int level, int *orientation);
 double orc_go_sin(double x);
 double orc_go_cos(double x);
 double orc_go_tan(double x);
@@ -72,6 +73,15 @@ int64_t orc_search(int64_t ne, const int64_t *e_offs, const uint64_t *e_cells, c
                    int64_t nq, const int64_t *q_offs, const uint64_t *q_cells, const float *q_alt_lo,
                    const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi, const int32_t *q_owner,
                    int nthreads, uint32_t **out_q, uint32_t **out_e);
+
+/* Same search with the posting list built once (CPU-baseline timing). */
+typedef struct orc_index orc_index;
+orc_index *orc_index_new(int64_t ne, const int64_t *e_offs, const uint64_t *e_cells, const float *e_alt_lo,
+                         const float *e_alt_hi, const int64_t *e_t0, const int64_t *e_t1, const int32_t *e_owner);
+int64_t orc_index_search(const orc_index *x, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
+                         const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
+                         const int32_t *q_owner, int nthreads, uint32_t **out_q, uint32_t **out_e);
+void orc_index_free(orc_index *x);
 
 void orc_free(void *p);
 

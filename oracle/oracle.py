@@ -56,6 +56,8 @@ def lib():
         L.orc_regular_loop.argtypes = [d, d, C.c_float, C.c_int, P(d)]
         L.orc_cell_uv_bound.argtypes = [u64, P(d)]
         L.orc_cell_center.argtypes = [u64, P(d)]
+        L.orc_cellid_from_face_ij_level.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, P(C.c_int)]
+        L.orc_cellid_from_face_ij_level.restype = u64
         for name in ("sin", "cos", "tan", "atan", "asin"):
             f = getattr(L, f"orc_go_{name}")
             f.argtypes = [d]
@@ -69,6 +71,12 @@ def lib():
                                  i64, P(i64), P(u64), P(C.c_float), P(C.c_float), P(i64), P(i64), P(i32),
                                  C.c_int, P(P(C.c_uint32)), P(P(C.c_uint32))]
         L.orc_search.restype = i64
+        L.orc_index_new.argtypes = [i64, P(i64), P(u64), P(C.c_float), P(C.c_float), P(i64), P(i64), P(i32)]
+        L.orc_index_new.restype = C.c_void_p
+        L.orc_index_search.argtypes = [C.c_void_p, i64, P(i64), P(u64), P(C.c_float), P(C.c_float), P(i64),
+                                       P(i64), P(i32), C.c_int, P(P(C.c_uint32)), P(P(C.c_uint32))]
+        L.orc_index_search.restype = i64
+        L.orc_index_free.argtypes = [C.c_void_p]
         L.orc_free.argtypes = [C.c_void_p]
         _lib = L
     return _lib
@@ -190,6 +198,45 @@ def search(e_offs, e_cells, e_alt_lo, e_alt_hi, e_t0, e_t1, e_owner,
     L.orc_free(C.cast(oq, C.c_void_p))
     L.orc_free(C.cast(oe, C.c_void_p))
     return rq, re
+
+
+class Index:
+    """Posting list built once; `search` is the timed CPU-baseline call."""
+
+    def __init__(self, e_offs, e_cells, e_alt_lo, e_alt_hi, e_t0, e_t1, e_owner=None):
+        L = lib()
+        a = lambda x, t: np.ascontiguousarray(x, dtype=t)  # noqa: E731
+        self._keep = [a(e_offs, np.int64), a(e_cells, np.uint64), a(e_alt_lo, np.float32), a(e_alt_hi, np.float32),
+                      a(e_t0, np.int64), a(e_t1, np.int64)]
+        o, c, lo, hi, t0, t1 = self._keep
+        own = a(e_owner, np.int32) if e_owner is not None else None
+        self.h = L.orc_index_new(len(o) - 1, _p(o, C.c_int64), _p(c, C.c_uint64), _p(lo, C.c_float),
+                                 _p(hi, C.c_float), _p(t0, C.c_int64), _p(t1, C.c_int64),
+                                 _p(own, C.c_int32) if own is not None else C.POINTER(C.c_int32)())
+
+    def search(self, q_offs, q_cells, q_alt_lo, q_alt_hi, q_tlo, q_thi, q_owner=None, nthreads=8):
+        L = lib()
+        a = lambda x, t: np.ascontiguousarray(x, dtype=t)  # noqa: E731
+        qo, qc = a(q_offs, np.int64), a(q_cells, np.uint64)
+        lo, hi, tl, th = a(q_alt_lo, np.float32), a(q_alt_hi, np.float32), a(q_tlo, np.int64), a(q_thi, np.int64)
+        own = a(q_owner, np.int32) if q_owner is not None else None
+        oq = C.POINTER(C.c_uint32)()
+        oe = C.POINTER(C.c_uint32)()
+        n = L.orc_index_search(self.h, len(qo) - 1, _p(qo, C.c_int64), _p(qc, C.c_uint64), _p(lo, C.c_float),
+                               _p(hi, C.c_float), _p(tl, C.c_int64), _p(th, C.c_int64),
+                               _p(own, C.c_int32) if own is not None else C.POINTER(C.c_int32)(), nthreads,
+                               C.byref(oq), C.byref(oe))
+        rq = np.ctypeslib.as_array(oq, shape=(max(n, 1),))[:n].copy()
+        re = np.ctypeslib.as_array(oe, shape=(max(n, 1),))[:n].copy()
+        L.orc_free(C.cast(oq, C.c_void_p))
+        L.orc_free(C.cast(oe, C.c_void_p))
+        return rq, re
+
+    def __del__(self):
+        try:
+            lib().orc_index_free(self.h)
+        except Exception:
+            pass
 
 
 def token(cell: int) -> str:

@@ -1305,6 +1305,14 @@ void orc_cell_center(uint64_t id, double out[3])
     out[1] = p.y;
     out[2] = p.z;
 }
+uint64_t orc_cellid_from_face_ij_level(int face, int i, int j, int level, int *orientation)
+{
+    ensure_lookup();
+    uint64_t id = cellid_parent(cellid_from_face_ij(face, i, j), level);
+    int f, ii, jj;
+    cellid_face_ij_orientation(id, &f, &ii, &jj, orientation);
+    return id;
+}
 double orc_go_sin(double x) { return go_sin(x); }
 double orc_go_cos(double x) { return go_cos(x); }
 double orc_go_tan(double x) { return go_tan(x); }
