@@ -284,6 +284,200 @@ __global__ __launch_bounds__(kBlock) void k_join(JoinArgs a)
     flush();
 }
 
+
+// ---------------------------------------------------------------- tiled join
+// The batch's (query, cell) pairs are grouped by index slot (radix sort), and
+// each workgroup joins one tile: kTileP postings of one cell (one per lane,
+// loaded once) against up to kTileQ of that cell's queries staged in LDS.
+constexpr int kTileP = 256;
+constexpr int kTileQ = 256;
+constexpr uint32_t kRank0 = 0x80000000u;
+
+// slot of cell c in the index (dense slot, or n_dense + irregular index);
+// returns false if the index holds no posting for c.
+__device__ __forceinline__ bool cell_slot(const JoinArgs &a, uint64_t c, uint32_t &slot)
+{
+    if (is_regular(c)) {
+        uint64_t k = c >> 35;
+        if (k < a.kmin || (int64_t)(k - a.kmin) >= a.n_dense) return false;
+        uint32_t sl = (uint32_t)(k - a.kmin);
+        if (a.dense[sl + 1] == a.dense[sl]) return false;
+        slot = sl;
+        return true;
+    }
+    int64_t lo = 0, hi = a.n_irr;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (a.irr_cells[mid] < c) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo < a.n_irr && a.irr_cells[lo] == c) {
+        slot = (uint32_t)(a.n_dense + lo);
+        return true;
+    }
+    return false;
+}
+__device__ __forceinline__ void slot_range(const JoinArgs &a, uint32_t slot, uint32_t &s, uint32_t &e, uint64_t &cell)
+{
+    if ((int64_t)slot < a.n_dense) {
+        s = a.dense[slot];
+        e = a.dense[slot + 1];
+        cell = ((a.kmin + slot) << 35) | kLsb13;
+    } else {
+        uint32_t k = slot - (uint32_t)a.n_dense;
+        s = a.irr_start[k];
+        e = a.irr_start[k + 1];
+        cell = a.irr_cells[k];
+    }
+}
+
+template <int PASS>
+__global__ void k_qc(JoinArgs a, int64_t *cnt, const int64_t *off, uint32_t *key, uint32_t *val)
+{
+    int64_t q = tid64();
+    if (q >= a.nq) return;
+    int64_t c0 = a.q_offs[q], c1 = a.q_offs[q + 1];
+    int64_t n = 0, w = PASS ? off[q] : 0;
+    for (int64_t k = c0; k < c1; k++) {
+        uint32_t slot;
+        if (!cell_slot(a, a.q_cells[k], slot)) continue;
+        if (PASS) {
+            key[w] = slot;
+            val[w] = (uint32_t)q | (k == c0 ? kRank0 : 0u);
+            w++;
+        }
+        n++;
+    }
+    if (!PASS) cnt[q] = n;
+}
+
+template <int PASS>
+__global__ void k_tiles(int64_t nruns, JoinArgs a, const uint32_t *ukey, const int64_t *rstart, int64_t *cnt,
+                        const int64_t *toff, uint32_t *t_run, uint32_t *t_p, uint32_t *t_q)
+{
+    int64_t r = tid64();
+    if (r >= nruns) return;
+    uint32_t s, e;
+    uint64_t cell;
+    slot_range(a, ukey[r], s, e, cell);
+    int64_t np = (int64_t)(e - s), nq = rstart[r + 1] - rstart[r];
+    int64_t tp = (np + kTileP - 1) / kTileP, tq = (nq + kTileQ - 1) / kTileQ;
+    if (!PASS) {
+        cnt[r] = tp * tq;
+        return;
+    }
+    int64_t w = toff[r];
+    for (int64_t i = 0; i < tp; i++)
+        for (int64_t j = 0; j < tq; j++, w++) {
+            t_run[w] = (uint32_t)r;
+            t_p[w] = (uint32_t)i;
+            t_q[w] = (uint32_t)j;
+        }
+}
+
+struct QAttr {
+    int64_t tlo, thi;
+    float alo, ahi;
+    uint32_t qv;  // query id | kRank0 if the cell is the query's first cell
+    int32_t own;
+};
+
+// True iff q and entity `ent` share no cell smaller than c (both lists sorted).
+__device__ bool smallest_shared_q(const JoinArgs &a, uint32_t ent, uint64_t c, uint32_t q)
+{
+    const uint64_t *ec = a.e_cells + a.e_offs[ent];
+    int64_t ne = a.e_offs[ent + 1] - a.e_offs[ent];
+    const uint64_t *qc = a.q_cells + a.q_offs[q];
+    int64_t nq = a.q_offs[q + 1] - a.q_offs[q];
+    int64_t i = 0, j = 0;
+    while (i < nq && j < ne) {
+        uint64_t x = qc[i], y = ec[j];
+        if (x >= c || y >= c) break;
+        if (x == y) return false;
+        if (x < y) i++;
+        else j++;
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(kTileP) void k_join_tile(JoinArgs a, const uint32_t *ukey, const int64_t *rstart,
+                                                      const uint32_t *sval, const uint32_t *t_run, const uint32_t *t_p,
+                                                      const uint32_t *t_q)
+{
+    __shared__ QAttr sq_attr[kTileQ];
+    __shared__ uint32_t sq[kTileP / 64][kStage];
+    __shared__ uint32_t se[kTileP / 64][kStage];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t r = t_run[blockIdx.x];
+    uint32_t ps, pe;
+    uint64_t cell;
+    slot_range(a, ukey[r], ps, pe, cell);
+    const int64_t q0 = rstart[r] + (int64_t)t_q[blockIdx.x] * kTileQ;
+    const int64_t q1 = min(rstart[r + 1], q0 + kTileQ);
+    const int nqt = (int)(q1 - q0);
+    if (tid < nqt) {
+        uint32_t v = sval[q0 + tid];
+        uint32_t q = v & ~kRank0;
+        QAttr qa;
+        qa.tlo = a.q_tlo[q];
+        qa.thi = a.q_thi[q];
+        qa.alo = a.q_alo[q];
+        qa.ahi = a.q_ahi[q];
+        qa.qv = v;
+        qa.own = a.q_owner ? a.q_owner[q] : -1;
+        sq_attr[tid] = qa;
+    }
+    const uint32_t p = ps + t_p[blockIdx.x] * kTileP + tid;
+    const bool valid = p < pe;
+    uint32_t pev = 0;
+    float2 alt = make_float2(0.f, 0.f);
+    longlong2 t = make_longlong2(0, 0);
+    int32_t pown = 0;
+    if (valid) {
+        pev = a.p_e[p];
+        alt = a.p_alt[p];
+        t = a.p_t[p];
+        if (a.q_owner) pown = a.p_owner[p];
+    }
+    const uint32_t ent = pev & ~kFirstBit;
+    const bool efirst = (pev & kFirstBit) != 0;
+    __syncthreads();
+    int staged = 0;
+    auto flush = [&]() {
+        __builtin_amdgcn_wave_barrier();
+        unsigned long long base = 0;
+        if (lane == 0 && staged) base = atomicAdd(a.counter, (unsigned long long)staged);
+        base = __shfl(base, 0);
+        for (int k = lane; k < staged; k += 64) {
+            unsigned long long o = base + (unsigned long long)k;
+            if ((int64_t)o < a.cap) {
+                a.out_q[o] = sq[w][k];
+                a.out_e[o] = se[w][k];
+            }
+        }
+        staged = 0;
+        __builtin_amdgcn_wave_barrier();
+    };
+    for (int k = 0; k < nqt; k++) {
+        const QAttr qa = sq_attr[k];
+        // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels)
+        bool pass = valid && t.y >= qa.tlo && t.x <= qa.thi && alt.y >= qa.alo && alt.x <= qa.ahi;
+        if (qa.own >= 0) pass = pass && pown == qa.own;
+        if (pass && !efirst && !(qa.qv & kRank0)) pass = smallest_shared_q(a, ent, cell, qa.qv & ~kRank0);
+        unsigned long long m = __ballot(pass);
+        if (m == 0) continue;
+        int nsurv = __popcll(m);
+        if (staged + nsurv > kStage) flush();
+        if (pass) {
+            int rk = __popcll(m & ((1ull << lane) - 1ull));
+            sq[w][staged + rk] = qa.qv & ~kRank0;
+            se[w][staged + rk] = ent;
+        }
+        staged += nsurv;
+    }
+    flush();
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- build
@@ -456,17 +650,68 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
 {
     if (q_owner && !idx->has_owner) throw Error(DSSG_ERR_INVALID, "search by owner on an index built without owners");
     unsigned long long *counter = counter_.ensure(1);
+    JoinArgs a = make_args(idx, nq, q_offs, q_cells, q_alt_lo, q_alt_hi, q_tlo, q_thi, q_owner);
+    if (timing_) {
+        if (!ev0_) { DSS_HIP(hipEventCreate(&ev0_)); DSS_HIP(hipEventCreate(&ev1_)); }
+    }
+    // (1) (slot, query) pairs for every query cell that has postings
+    int64_t *qcnt = c0_.ensure(nq + 1), *qoff = c1_.ensure(nq + 2);
+    if (nq > 0) hipLaunchKernelGGL(k_qc<0>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, a, qcnt, nullptr, nullptr, nullptr);
+    exclusive_scan_i64(qcnt, qoff, nq, tmp_, s);
+    int64_t npairs = 0;
+    DSS_HIP(hipMemcpyAsync(&npairs, qoff + nq, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    if (npairs == 0) {
+        out->q = oq_.ensure(1);
+        out->e = oe_.ensure(1);
+        out->n = 0;
+        return;
+    }
+    uint32_t *key = v0_.ensure(npairs + 1), *val = v1_.ensure(npairs + 1);
+    uint32_t *skey = sk_.ensure(npairs + 1), *sval = sv_.ensure(npairs + 1);
+    hipLaunchKernelGGL(k_qc<1>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, a, nullptr, qoff, key, val);
+    // (2) group by slot (stable: query order kept within a slot)
+    int64_t nslots = idx->n_dense + idx->n_irr;
+    int bits = 1;
+    while (bits < 32 && ((int64_t)1 << bits) <= nslots) bits++;
+    size_t bytes = 0;
+    DSS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, key, skey, val, sval, (int)npairs, 0, bits, s));
+    tmp_.ensure(bytes + 16);
+    DSS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_.p, bytes, key, skey, val, sval, (int)npairs, 0, bits, s));
+    // (3) runs of equal slots
+    uint32_t *ukey = uk_.ensure(npairs + 1);
+    int64_t *rcnt = rc_.ensure(npairs + 1), *rstart = rs_.ensure(npairs + 2);
+    int64_t *nruns_d = nr_.ensure(2);
+    bytes = 0;
+    DSS_HIP(hipcub::DeviceRunLengthEncode::Encode(nullptr, bytes, skey, ukey, rcnt, nruns_d, (int)npairs, s));
+    tmp_.ensure(bytes + 16);
+    DSS_HIP(hipcub::DeviceRunLengthEncode::Encode(tmp_.p, bytes, skey, ukey, rcnt, nruns_d, (int)npairs, s));
+    int64_t nruns = 0;
+    DSS_HIP(hipMemcpyAsync(&nruns, nruns_d, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    exclusive_scan_i64(rcnt, rstart, nruns, tmp_, s);
+    // (4) tiles
+    int64_t *tcnt = tc_.ensure(nruns + 1), *toff = to_.ensure(nruns + 2);
+    hipLaunchKernelGGL(k_tiles<0>, dim3(grid_for(nruns, kBlock)), dim3(kBlock), 0, s, nruns, a, ukey, rstart, tcnt, nullptr,
+                       nullptr, nullptr, nullptr);
+    exclusive_scan_i64(tcnt, toff, nruns, tmp_, s);
+    int64_t ntiles = 0;
+    DSS_HIP(hipMemcpyAsync(&ntiles, toff + nruns, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    uint32_t *t_run = tr_.ensure(ntiles + 1), *t_p = tp_.ensure(ntiles + 1), *t_q = tq_.ensure(ntiles + 1);
+    hipLaunchKernelGGL(k_tiles<1>, dim3(grid_for(nruns, kBlock)), dim3(kBlock), 0, s, nruns, a, ukey, rstart, nullptr, toff,
+                       t_run, t_p, t_q);
+    // (5) join tiles; grow the output and rerun if the guess was too small
     if (out_cap_ == 0) out_cap_ = (size_t)(nq > 0 ? nq : 1) * 16 + 1024;
     for (int attempt = 0; attempt < 3; attempt++) {
         uint32_t *oq = oq_.ensure(out_cap_), *oe = oe_.ensure(out_cap_);
         DSS_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned long long), s));
-        JoinArgs a = make_args(idx, nq, q_offs, q_cells, q_alt_lo, q_alt_hi, q_tlo, q_thi, q_owner);
-        a.out_q = oq; a.out_e = oe; a.counter = counter; a.cap = (int64_t)out_cap_;
-        if (timing_) {
-            if (!ev0_) { DSS_HIP(hipEventCreate(&ev0_)); DSS_HIP(hipEventCreate(&ev1_)); }
-            DSS_HIP(hipEventRecord(ev0_, s));
-        }
-        if (nq > 0) hipLaunchKernelGGL(k_join, dim3(grid_for(nq, kBlock / 64)), dim3(kBlock), 0, s, a);
+        a.out_q = oq;
+        a.out_e = oe;
+        a.counter = counter;
+        a.cap = (int64_t)out_cap_;
+        if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
+        hipLaunchKernelGGL(k_join_tile, dim3((unsigned)ntiles), dim3(kTileP), 0, s, a, ukey, rstart, sval, t_run, t_p, t_q);
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
         unsigned long long total = 0;
         DSS_HIP(hipMemcpyAsync(&total, counter, sizeof(total), hipMemcpyDeviceToHost, s));

@@ -51,6 +51,9 @@ class SearchEngine {
     DevBuf<int64_t> c0_, c1_;
     DevBuf<uint8_t> fl_;
     DevBuf<unsigned long long> counter_;
+    // tiled-join scratch
+    DevBuf<uint32_t> sk_, sv_, uk_, tr_, tp_, tq_;
+    DevBuf<int64_t> rc_, rs_, nr_, tc_, to_;
     DevBuf<uint32_t> oq_, oe_;
     size_t out_cap_ = 0;
     bool timing_ = false;
