@@ -289,6 +289,8 @@ __global__ __launch_bounds__(kBlock) void k_join(JoinArgs a)
 // The batch's (query, cell) pairs are grouped by index slot (radix sort), and
 // each workgroup joins one tile: kTileP postings of one cell (one per lane,
 // loaded once) against up to kTileQ of that cell's queries staged in LDS.
+__device__ __forceinline__ int s2pos_to_ij(int o, int pos) { return (int)((0x874B78B4u >> (8 * o + 2 * pos)) & 3u); }
+__device__ __forceinline__ int s2pos_to_orientation(int pos) { return (int)((0xC1u >> (2 * pos)) & 3u); }
 constexpr int kTileP = 256;
 constexpr int kTileQ = 256;
 constexpr uint32_t kRank0 = 0x80000000u;
@@ -379,7 +381,7 @@ struct QAttr {
     int64_t tlo, thi;
     float alo, ahi;
     uint32_t qv;  // query id | kRank0 if the cell is the query's first cell
-    int32_t own;
+    int32_t own;  // owner filter, or -1; bit 30 of `compact` below
 };
 
 // True iff q and entity `ent` share no cell smaller than c (both lists sorted).
@@ -400,11 +402,68 @@ __device__ bool smallest_shared_q(const JoinArgs &a, uint32_t ent, uint64_t c, u
     return true;
 }
 
+// Level-13 (face, i, j) of a cell id (cellid.go faceIJOrientation, walked one
+// level at a time); false for ids that are not valid level-13 cells.
+__device__ __forceinline__ bool decode13(uint64_t c, int &face, int &i, int &j)
+{
+    if (!is_regular(c)) return false;
+    face = (int)(c >> 61);
+    int o = face & 1;
+    i = j = 0;
+#pragma unroll
+    for (int l = 0; l < 13; l++) {
+        int pos = (int)((c >> (59 - 2 * l)) & 3);
+        int ij = s2pos_to_ij(o, pos);
+        i = (i << 1) | (ij >> 1);
+        j = (j << 1) | (ij & 1);
+        o ^= s2pos_to_orientation(pos);
+    }
+    return true;
+}
+
+// Prefix signature of a sorted cell list: one bit per (i mod 16, j mod 16)
+// (256 bits) for every cell < c; `compact` iff all of them lie within +-7
+// cells of c on c's face, so that equal bits imply equal cells.
+struct Sig256 {
+    uint64_t w[4];
+};
+__device__ __forceinline__ void prefix_sig(const uint64_t *cells, int64_t n, uint64_t c, int fc, int ic, int jc,
+                                           bool cvalid, Sig256 &sig, bool &compact)
+{
+    sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = 0;
+    compact = cvalid;
+    for (int64_t k = 0; k < n; k++) {
+        uint64_t x = cells[k];
+        if (x >= c) break;
+        int f, i, j;
+        if (decode13(x, f, i, j)) {
+            int b = ((i & 15) << 4) | (j & 15);
+            uint64_t bit = 1ull << (b & 63);
+            int wi = b >> 6;
+            sig.w[0] |= wi == 0 ? bit : 0;
+            sig.w[1] |= wi == 1 ? bit : 0;
+            sig.w[2] |= wi == 2 ? bit : 0;
+            sig.w[3] |= wi == 3 ? bit : 0;
+            int di = i - ic, dj = j - jc;
+            if (f != fc || di < -7 || di > 7 || dj < -7 || dj > 7) compact = false;
+        } else {
+            sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = ~0ull;  // unknown position: force the exact check
+            compact = false;
+        }
+    }
+}
+__device__ __forceinline__ bool sig_overlap(const Sig256 &a, const uint64_t *b)
+{
+    return ((a.w[0] & b[0]) | (a.w[1] & b[1]) | (a.w[2] & b[2]) | (a.w[3] & b[3])) != 0;
+}
+
 __global__ __launch_bounds__(kTileP) void k_join_tile(JoinArgs a, const uint32_t *ukey, const int64_t *rstart,
                                                       const uint32_t *sval, const uint32_t *t_run, const uint32_t *t_p,
                                                       const uint32_t *t_q)
 {
     __shared__ QAttr sq_attr[kTileQ];
+    __shared__ uint64_t sq_sig[kTileQ][4];
+    __shared__ uint8_t sq_compact[kTileQ];
     __shared__ uint32_t sq[kTileP / 64][kStage];
     __shared__ uint32_t se[kTileP / 64][kStage];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -415,6 +474,8 @@ __global__ __launch_bounds__(kTileP) void k_join_tile(JoinArgs a, const uint32_t
     const int64_t q0 = rstart[r] + (int64_t)t_q[blockIdx.x] * kTileQ;
     const int64_t q1 = min(rstart[r + 1], q0 + kTileQ);
     const int nqt = (int)(q1 - q0);
+    int fc = 0, ic = 0, jc = 0;
+    const bool cvalid = decode13(cell, fc, ic, jc);
     if (tid < nqt) {
         uint32_t v = sval[q0 + tid];
         uint32_t q = v & ~kRank0;
@@ -425,7 +486,15 @@ __global__ __launch_bounds__(kTileP) void k_join_tile(JoinArgs a, const uint32_t
         qa.ahi = a.q_ahi[q];
         qa.qv = v;
         qa.own = a.q_owner ? a.q_owner[q] : -1;
+        bool cp;
+        Sig256 qs;
+        prefix_sig(a.q_cells + a.q_offs[q], a.q_offs[q + 1] - a.q_offs[q], cell, fc, ic, jc, cvalid, qs, cp);
         sq_attr[tid] = qa;
+        sq_sig[tid][0] = qs.w[0];
+        sq_sig[tid][1] = qs.w[1];
+        sq_sig[tid][2] = qs.w[2];
+        sq_sig[tid][3] = qs.w[3];
+        sq_compact[tid] = cp ? 1 : 0;
     }
     const uint32_t p = ps + t_p[blockIdx.x] * kTileP + tid;
     const bool valid = p < pe;
@@ -441,6 +510,11 @@ __global__ __launch_bounds__(kTileP) void k_join_tile(JoinArgs a, const uint32_t
     }
     const uint32_t ent = pev & ~kFirstBit;
     const bool efirst = (pev & kFirstBit) != 0;
+    Sig256 esig;
+    esig.w[0] = esig.w[1] = esig.w[2] = esig.w[3] = 0;
+    bool ecompact = true;
+    if (valid && !efirst)
+        prefix_sig(a.e_cells + a.e_offs[ent], a.e_offs[ent + 1] - a.e_offs[ent], cell, fc, ic, jc, cvalid, esig, ecompact);
     __syncthreads();
     int staged = 0;
     auto flush = [&]() {
@@ -463,7 +537,11 @@ __global__ __launch_bounds__(kTileP) void k_join_tile(JoinArgs a, const uint32_t
         // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels)
         bool pass = valid && t.y >= qa.tlo && t.x <= qa.thi && alt.y >= qa.alo && alt.x <= qa.ahi;
         if (qa.own >= 0) pass = pass && pown == qa.own;
-        if (pass && !efirst && !(qa.qv & kRank0)) pass = smallest_shared_q(a, ent, cell, qa.qv & ~kRank0);
+        // keep the pair only at the smallest shared cell (SQL DISTINCT, Q13)
+        if (pass && !efirst && !(qa.qv & kRank0) && sig_overlap(esig, sq_sig[k])) {
+            if (ecompact && sq_compact[k]) pass = false;  // a shared smaller cell exists
+            else pass = smallest_shared_q(a, ent, cell, qa.qv & ~kRank0);
+        }
         unsigned long long m = __ballot(pass);
         if (m == 0) continue;
         int nsurv = __popcll(m);
