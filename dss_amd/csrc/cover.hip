@@ -39,7 +39,7 @@ constexpr double kCoarsePad = 1e-9;  // pruning padding, >> FACE_CLIP_PLUS_RECT_
 constexpr double kFinePad = DSS_FACE_CLIP_PLUS_RECT_ERR;
 
 enum : uint8_t { MODE_NONE = 0, MODE_LOOP = 1, MODE_POLYLINE = 2 };
-enum : uint8_t { FL_SMALL = 1 };
+enum : uint8_t { FL_SMALL = 1, FL_PLANAR = 2 };
 // node meta: level (bits 0-4), orientation (5-6), done (7), face (8-10)
 __device__ __forceinline__ uint32_t pack_meta(int level, int orient, int done, int face)
 {
@@ -170,7 +170,25 @@ __global__ void k_setup(int64_t n, const int32_t *kind, const int64_t *voff, con
     fmask[f] = mask;
     // bbox-limited start is valid for polylines (no interior) and for loops
     // whose edges all lie inside one face and whose interior is the small side.
-    flags[f] = (md == MODE_POLYLINE || (md == MODE_LOOP && inner && small && __builtin_popcount(mask) == 1)) ? FL_SMALL : 0;
+    uint8_t fl = (md == MODE_POLYLINE || (md == MODE_LOOP && inner && small && __builtin_popcount(mask) == 1)) ? FL_SMALL : 0;
+    // Planar containment (see contains_node): a single-face small loop whose
+    // (u,v) bound does not come near OriginPoint's projection.
+    if (md == MODE_LOOP && (fl & FL_SMALL)) {
+        int face0 = xyz_face(p[0]);
+        bool near_origin = false;
+        if (face0 == xyz_face(origin_point())) {
+            double ou, ov, ulo = 1e300, uhi = -1e300, vlo = 1e300, vhi = -1e300;
+            valid_face_xyz_to_uv(face0, origin_point(), ou, ov);
+            for (int i = 0; i < nv; i++) {
+                double u, v;
+                valid_face_xyz_to_uv(face0, p[i], u, v);
+                ulo = fmin(ulo, u); uhi = fmax(uhi, u); vlo = fmin(vlo, v); vhi = fmax(vhi, v);
+            }
+            near_origin = ou >= ulo - 1e-6 && ou <= uhi + 1e-6 && ov >= vlo - 1e-6 && ov <= vhi + 1e-6;
+        }
+        if (!near_origin) fl |= FL_PLANAR;
+    }
+    flags[f] = fl;
     nvx[f] = nv;
 }
 
@@ -289,6 +307,32 @@ __device__ V3 node_center(int face, uint32_t i0, uint32_t j0, int level)
     return normalize(face_uv_to_xyz(face, st_to_uv(s), st_to_uv(t)));
 }
 
+// Containment of a node centre that no loop edge comes near (the node is
+// uniform, or a level-13 cell the padded edge test rejected): the centre is
+// at least half a cell from every edge, so for a loop that lies inside one
+// face the even-odd ray cast over the edges' gnomonic (u,v) images (great
+// circles are straight lines there) decides it exactly.  Crossing parity is
+// path independent, so it equals the parity S2 counts along OriginPoint->p
+// (loop.go bruteForceContainsPoint), flipped by originInside; FL_PLANAR
+// excludes loops whose bound surrounds OriginPoint's own projection.
+__device__ bool contains_node(const LoopView &l, bool planar, const double4 *clip, int ne, int face, uint32_t i0, uint32_t j0,
+                              int level)
+{
+    if (!planar) return loop_contains(l, node_center(face, i0, j0, level));
+    double size = (double)(1u << (kMaxLevel - level));
+    const double half = 0.5 / (double)kMaxSize;
+    double uc = st_to_uv(half * (2.0 * (double)i0 + size)), vc = st_to_uv(half * (2.0 * (double)j0 + size));
+    bool par = false;
+    for (int e = 0; e < ne; e++) {
+        double4 c = clip[e];
+        if ((c.y > vc) != (c.w > vc)) {
+            double x = c.x + (vc - c.y) * (c.z - c.x) / (c.w - c.y);
+            if (uc < x) par = !par;
+        }
+    }
+    return l.origin_inside != par;
+}
+
 // Count (pass 0) or write (pass 1) start nodes; big loops also get whole-face
 // nodes for faces without edges whose centre the loop contains.
 template <int PASS>
@@ -375,7 +419,8 @@ __device__ bool polyline_intersects_cell(const V3 *p, int nv, int face, double u
 __global__ void k_expand_count(int64_t nn, const uint32_t *nf, const uint32_t *ni, const uint32_t *nj,
                                const uint32_t *nmeta, uint8_t *act, int64_t *cnt, const int64_t *xoff, const V3 *xyz,
                                const uint8_t *mode, const uint8_t *fmask, const uint8_t *origin_in, const int32_t *nvx,
-                               const int64_t *eoff, const double4 *clip_f, const double4 *clip_c, const uint8_t *cflags)
+                               const int64_t *eoff, const double4 *clip_f, const double4 *clip_c, const uint8_t *cflags,
+                               const uint8_t *flags)
 {
     int64_t k = tid64();
     if (k >= nn) return;
@@ -412,7 +457,7 @@ __global__ void k_expand_count(int64_t nn, const uint32_t *nf, const uint32_t *n
             if (hit) a = 2;
             else if (md == MODE_LOOP) {
                 LoopView l{p, nv, origin_in[f] != 0};
-                a = loop_contains(l, node_center(face, ni[k], nj[k], level)) ? 1 : 0;
+                a = contains_node(l, (flags[f] & FL_PLANAR) != 0, clip_f + base, ne, face, ni[k], nj[k], level) ? 1 : 0;
             } else a = 0;
         } else {
             bool in;
@@ -427,7 +472,7 @@ __global__ void k_expand_count(int64_t nn, const uint32_t *nf, const uint32_t *n
                 }
                 if (!in) {
                     LoopView l{p, nv, origin_in[f] != 0};
-                    in = loop_contains(l, node_center(face, ni[k], nj[k], level));
+                    in = contains_node(l, (flags[f] & FL_PLANAR) != 0, clip_f + base, ne, face, ni[k], nj[k], level);
                 }
             } else {
                 in = polyline_intersects_cell(p, nv, face, ulo, uhi, vlo, vhi);
@@ -575,7 +620,7 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
         int64_t *c = ncnt_.ensure(nn + 1);
         int64_t *pos = npos_.ensure(nn + 1);
         hipLaunchKernelGGL(k_expand_count, dim3(grid_for(nn, 64)), dim3(64), 0, s, nn, F->f.p, F->i.p, F->j.p, F->meta.p,
-                           act, c, xoff, xyz, mode, fmask, orig, nvx, eoff, clip_f, clip_c, cflags);
+                           act, c, xoff, xyz, mode, fmask, orig, nvx, eoff, clip_f, clip_c, cflags, flags);
         exclusive_scan_i64(c, pos, nn, tmp_, s);
         int64_t nn2 = 0;
         DSS_HIP(hipMemcpyAsync(&nn2, pos + nn, sizeof(int64_t), hipMemcpyDeviceToHost, s));

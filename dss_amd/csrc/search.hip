@@ -84,6 +84,27 @@ __global__ void k_scatter_part(int64_t P, const uint64_t *key, const uint32_t *v
     }
 }
 
+__global__ void k_time_keys(int64_t n, const uint32_t *p_e, const int64_t *t0, uint64_t *key, uint32_t *perm)
+{
+    int64_t i = tid64();
+    if (i >= n) return;
+    key[i] = (uint64_t)t0[p_e[i]] ^ 0x8000000000000000ull;  // signed order as unsigned
+    perm[i] = (uint32_t)i;
+}
+__global__ void k_gather_cell(int64_t n, const uint64_t *cell, const uint32_t *perm, uint64_t *out)
+{
+    int64_t i = tid64();
+    if (i < n) out[i] = cell[perm[i]];
+}
+__global__ void k_apply_perm(int64_t n, const uint32_t *perm, const uint64_t *cell_in, const uint32_t *e_in,
+                             uint64_t *cell_out, uint32_t *e_out)
+{
+    int64_t i = tid64();
+    if (i >= n) return;
+    cell_out[i] = cell_in[perm[i]];
+    e_out[i] = e_in[perm[i]];
+}
+
 __global__ void k_count_by_entity(int64_t P, const uint32_t *e, unsigned long long *cnt)
 {
     int64_t i = tid64();
@@ -510,12 +531,32 @@ __global__ __launch_bounds__(kTileP) void k_join_tile(JoinArgs a, const uint32_t
     }
     const uint32_t ent = pev & ~kFirstBit;
     const bool efirst = (pev & kFirstBit) != 0;
+    // time bounds of this posting tile (postings are ordered by start time
+    // within a cell): queries whose window misses them are skipped whole
+    __shared__ long long s_tmin[kTileP / 64], s_tmax[kTileP / 64];
+    {
+        long long mn = valid ? t.x : LLONG_MAX, mx = valid ? t.y : LLONG_MIN;
+        for (int o = 32; o > 0; o >>= 1) {
+            mn = min(mn, __shfl_xor(mn, o));
+            mx = max(mx, __shfl_xor(mx, o));
+        }
+        if (lane == 0) {
+            s_tmin[w] = mn;
+            s_tmax[w] = mx;
+        }
+    }
     Sig256 esig;
     esig.w[0] = esig.w[1] = esig.w[2] = esig.w[3] = 0;
     bool ecompact = true;
     if (valid && !efirst)
         prefix_sig(a.e_cells + a.e_offs[ent], a.e_offs[ent + 1] - a.e_offs[ent], cell, fc, ic, jc, cvalid, esig, ecompact);
     __syncthreads();
+    long long tmin = s_tmin[0], tmax = s_tmax[0];
+#pragma unroll
+    for (int k = 1; k < kTileP / 64; k++) {
+        tmin = min(tmin, s_tmin[k]);
+        tmax = max(tmax, s_tmax[k]);
+    }
     int staged = 0;
     auto flush = [&]() {
         __builtin_amdgcn_wave_barrier();
@@ -534,6 +575,7 @@ __global__ __launch_bounds__(kTileP) void k_join_tile(JoinArgs a, const uint32_t
     };
     for (int k = 0; k < nqt; k++) {
         const QAttr qa = sq_attr[k];
+        if (qa.thi < tmin || qa.tlo > tmax) continue;  // no posting of the tile can match
         // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels)
         bool pass = valid && t.y >= qa.tlo && t.x <= qa.thi && alt.y >= qa.alo && alt.x <= qa.ahi;
         if (qa.own >= 0) pass = pass && pown == qa.own;
@@ -602,6 +644,42 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     if (P)
         hipLaunchKernelGGL(k_scatter_part, dim3(grid_for(P, kBlock)), dim3(kBlock), 0, s, P, kb, vb, reg, rpos, irr, ipos,
                            n_reg, p_cell, p_e);
+    // within each cell, order postings by start time (segments sorted apart
+    // so regular postings stay in front): sort by t0, then stable by cell
+    {
+        DevBuf<uint64_t> tk, tk2, cb;
+        DevBuf<uint32_t> pm, pm2;
+        DevBuf<uint64_t> pc2;
+        DevBuf<uint32_t> pe2;
+        uint64_t *tkey = tk.ensure(Pu + 1), *tkey2 = tk2.ensure(Pu + 1), *cbuf = cb.ensure(Pu + 1), *pcn = pc2.ensure(Pu + 1);
+        uint32_t *perm = pm.ensure(Pu + 1), *perm2 = pm2.ensure(Pu + 1), *pen = pe2.ensure(Pu + 1);
+        int64_t segs[2][2] = {{0, n_reg}, {n_reg, Pu}};
+        for (auto &sg : segs) {
+            int64_t o = sg[0], m = sg[1] - sg[0];
+            if (m <= 1) {
+                if (m == 1) {
+                    DSS_HIP(hipMemcpyAsync(pcn + o, p_cell + o, sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+                    DSS_HIP(hipMemcpyAsync(pen + o, p_e + o, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+                }
+                continue;
+            }
+            hipLaunchKernelGGL(k_time_keys, dim3(grid_for(m, kBlock)), dim3(kBlock), 0, s, m, p_e + o, t0, tkey, perm);
+            size_t b2 = 0;
+            DSS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b2, tkey, tkey2, perm, perm2, (int)m, 0, 64, s));
+            tmp_.ensure(b2 + 16);
+            DSS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_.p, b2, tkey, tkey2, perm, perm2, (int)m, 0, 64, s));
+            hipLaunchKernelGGL(k_gather_cell, dim3(grid_for(m, kBlock)), dim3(kBlock), 0, s, m, p_cell + o, perm2, cbuf);
+            b2 = 0;
+            DSS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b2, cbuf, tkey, perm2, perm, (int)m, 0, 64, s));
+            tmp_.ensure(b2 + 16);
+            DSS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_.p, b2, cbuf, tkey, perm2, perm, (int)m, 0, 64, s));
+            hipLaunchKernelGGL(k_apply_perm, dim3(grid_for(m, kBlock)), dim3(kBlock), 0, s, m, perm, p_cell + o, p_e + o,
+                               pcn + o, pen + o);
+        }
+        DSS_HIP(hipMemcpyAsync(p_cell, pcn, sizeof(uint64_t) * Pu, hipMemcpyDeviceToDevice, s));
+        DSS_HIP(hipMemcpyAsync(p_e, pen, sizeof(uint32_t) * Pu, hipMemcpyDeviceToDevice, s));
+        DSS_HIP(hipStreamSynchronize(s));
+    }
     // entity -> sorted unique cell lists: unique postings in cell order, then
     // a stable sort by entity.
     if (P)
