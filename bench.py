@@ -133,6 +133,9 @@ def main():
         kern_ms.append(cc.value)
     ctx.L.dssg_set_timing(ctx.h, 0)
     import ctypes as C
+    n_keys, n_units, n_runs, n_iters, n_tests = (C.c_int64() for _ in range(5))
+    ctx.check(ctx.L.dssg_search_counters(ctx.h, C.byref(n_keys), C.byref(n_units), C.byref(n_runs), C.byref(n_iters),
+                                         C.byref(n_tests)))
     m_tot, d_tot = C.c_int64(), C.c_int64()
     ctx.check(ctx.L.dssg_search_stats_device(ctx.h, index, cells.n, C.c_void_p(cells.offs), C.c_void_p(cells.cells),
                                              D._stream_ptr(), C.byref(m_tot), C.byref(d_tot)))
@@ -169,6 +172,8 @@ def main():
             "coverings_per_s": world * nq / (cover_avg * 1e-3),
             "phase_ms": {"cover": cover_avg, "join": join_avg, "join_kernel": kern_avg_ms},
             "pairs_per_step": r_tot,
+            "join_work": {"keys": n_keys.value, "units": n_units.value, "runs": n_runs.value,
+                          "wave_iters": n_iters.value, "lane_tests": n_tests.value},
             "index_build_s": build_s,
             "roofline": {"kernel": "k_join (overlap join + fused filter)", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -200,6 +200,19 @@ int dssg_phase_times(dssg_ctx *ctx, double *cover_ms, double *join_ms, double *j
     return DSSG_OK;
 }
 
+int dssg_search_counters(dssg_ctx *ctx, int64_t *keys, int64_t *units, int64_t *runs, int64_t *iters, int64_t *tests)
+{
+    if (!ctx) return DSSG_ERR_INVALID;
+    int64_t r, i, t;
+    ctx->search.last_work(&r, &i, &t);
+    if (keys) *keys = ctx->search.last_keys();
+    if (units) *units = ctx->search.last_units();
+    if (runs) *runs = r;
+    if (iters) *iters = i;
+    if (tests) *tests = t;
+    return DSSG_OK;
+}
+
 int dssg_cover_batch_device(dssg_ctx *ctx, int64_t n, const int32_t *d_kind, const int64_t *d_voff, const double *d_lat,
                             const double *d_lng, const float *d_radius_m, void *stream, dssg_cells *out)
 {
@@ -351,7 +364,7 @@ void dssg_index_free(dssg_index *idx)
     delete idx;
 }
 int64_t dssg_index_num_postings(const dssg_index *idx) { return idx ? idx->n_p : 0; }
-int64_t dssg_index_num_cells(const dssg_index *idx) { return idx ? idx->n_reg : 0; }
+int64_t dssg_index_num_cells(const dssg_index *idx) { return idx ? idx->n_cells : 0; }
 
 int dssg_search_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *d_q_offs,
                        const uint64_t *d_q_cells, const float *d_q_alt_lo, const float *d_q_alt_hi,

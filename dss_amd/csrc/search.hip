@@ -8,20 +8,23 @@
 //     and the `cells && $n` queries (identification_service_area.go:170-180,
 //     subscriptions.go:222-273).
 //
-// Index layout in HBM (built once, resident): postings sorted by
-// (cell, entity), structure-of-arrays with the filter attributes inlined
-// (entity u32 | alt float2 | time longlong2 = 28 B), so a cell's posting list
-// streams with 16-byte coalesced loads.  Level-13 cells are found with one
-// dense lookup (slot = cell >> 35, a 29-bit face+Hilbert prefix); any other
-// id (the reference tests use invalid face-7 ids as opaque keys, Q12) goes
-// through a small sorted side table.
+// Index layout in HBM (built once, resident):
+//  * plain postings sorted by (cell, entity) -- the cell -> entity map the
+//    SQL index holds; level-13 cells found with one dense lookup (slot =
+//    cell >> 35, a 29-bit face+Hilbert prefix), any other id (the reference
+//    tests use invalid face-7 ids as opaque keys, Q12) via a sorted side table;
+//  * time-bucketed postings: each posting is copied into every time bucket
+//    its [t0, t1] touches (entities spanning more than kLongSpan buckets go,
+//    once, to the "long" bucket 63), sorted by (slot, bucket, entity), SoA
+//    with the filter attributes and a 256-bit "prefix signature" inlined.
 //
-// Join: one wavefront per query walks its cells in ascending order; lanes
-// stream the cell's postings, apply the fused altitude/time/owner predicate,
-// and keep a pair only at the smallest cell the query and the entity share
-// (the SQL DISTINCT, Q13, without a dedupe pass; it also lets cell-range
-// shards emit disjoint pair sets).  Survivors are staged per wave in LDS and
-// flushed with one atomic per batch.
+// Join: the batch's (query cell, bucket) keys are radix-sorted
+// so every non-empty (slot, bucket) group meets all its queries at once; one
+// wavefront owns 64 postings of a group (one per lane, loaded once) and
+// sweeps the group's query records with scalar loads, applying the fused
+// altitude/time/owner predicate.  A pair is kept exactly once -- at the
+// smallest cell the query and the entity share and in their first common
+// bucket -- which is the SQL DISTINCT (Q13) without a dedupe pass.
 #include <hip/hip_runtime.h>
 
 #include <hipcub/hipcub.hpp>
@@ -34,13 +37,198 @@ namespace {
 constexpr unsigned kBlock = 256;
 constexpr uint32_t kFirstBit = 0x80000000u;
 constexpr uint64_t kLsb13 = 1ull << 34;
+constexpr int kLongBucket = 63;
+constexpr int kLongSpan = 8;     // entities touching more buckets go to kLongBucket
+constexpr int kMaxBuckets = 61;  // regular buckets 0..nb-1
+constexpr int kWaves = 4;        // join units per workgroup
+constexpr int kQChunk = 1024;    // query records per join unit
+constexpr int kStage = 256;      // pairs staged per wave in LDS
+constexpr uint32_t kRank0 = 0x80000000u;    // record: the cell is the query's first cell
+constexpr uint32_t kCompact = 0x40000000u;  // record: the query's prefix is compact
 
 __device__ __forceinline__ int64_t tid64() { return (int64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 __host__ __device__ __forceinline__ bool is_regular(uint64_t c)
 {
     return (c & ((kLsb13 << 1) - 1)) == kLsb13 && (c >> 61) < 6;  // level 13, valid face
 }
+__host__ __device__ __forceinline__ unsigned long long order_key(long long t)
+{
+    return (unsigned long long)t ^ 0x8000000000000000ull;  // signed order as unsigned
+}
 
+struct Buckets {
+    long long tbase;
+    int shift;
+    int nb;
+};
+// Monotone in t, so B(max(a, b)) = max(B(a), B(b)).
+__device__ __forceinline__ int bucket_of(long long t, const Buckets &bk)
+{
+    if (t <= bk.tbase) return 0;
+    unsigned long long d = ((unsigned long long)t - (unsigned long long)bk.tbase) >> bk.shift;
+    return d >= (unsigned long long)bk.nb ? bk.nb - 1 : (int)d;
+}
+
+// Device view of a dssg_index.
+struct IndexView {
+    uint64_t kmin;
+    int64_t n_dense;
+    const uint32_t *dense;
+    int64_t n_irr;
+    const uint64_t *irr_cells;
+    const uint32_t *irr_start;
+    const uint32_t *p_e;
+    const int64_t *e_offs;
+    const uint64_t *e_cells;
+    const unsigned long long *s_mask;
+    const uint32_t *s_base;
+    const uint32_t *bk_start;
+    const uint32_t *b_e;
+    const float2 *b_alt;
+    const longlong2 *b_t;
+    const uint8_t *b_meta;
+    const ulonglong2 *b_sig;
+    const int32_t *b_owner;
+    Buckets bk;
+};
+
+IndexView view_of(const dssg_index *idx)
+{
+    IndexView v{};
+    v.kmin = idx->kmin;
+    v.n_dense = idx->n_dense;
+    v.dense = idx->dense.p;
+    v.n_irr = idx->n_irr;
+    v.irr_cells = idx->irr_cells.p;
+    v.irr_start = idx->irr_start.p;
+    v.p_e = idx->p_e.p;
+    v.e_offs = idx->e_offs.p;
+    v.e_cells = idx->e_cells.p;
+    v.s_mask = idx->s_mask.p;
+    v.s_base = idx->s_base.p;
+    v.bk_start = idx->bk_start.p;
+    v.b_e = idx->b_e.p;
+    v.b_alt = idx->b_alt.p;
+    v.b_t = idx->b_t.p;
+    v.b_meta = idx->b_meta.p;
+    v.b_sig = idx->b_sig.p;
+    v.b_owner = idx->has_owner ? idx->b_owner.p : nullptr;
+    v.bk = Buckets{idx->tbase, idx->shift, idx->nb};
+    return v;
+}
+
+// Slot of cell c, or false if c is in neither table.
+__device__ __forceinline__ bool find_slot(const IndexView &a, uint64_t c, uint32_t &slot)
+{
+    if (is_regular(c)) {
+        uint64_t k = c >> 35;
+        if (k < a.kmin || (int64_t)(k - a.kmin) >= a.n_dense) return false;
+        slot = (uint32_t)(k - a.kmin);
+        return true;
+    }
+    int64_t lo = 0, hi = a.n_irr;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (a.irr_cells[mid] < c) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo < a.n_irr && a.irr_cells[lo] == c) {
+        slot = (uint32_t)(a.n_dense + lo);
+        return true;
+    }
+    return false;
+}
+__device__ __forceinline__ uint64_t cell_of_slot(const IndexView &a, uint32_t slot)
+{
+    if ((int64_t)slot < a.n_dense) return ((a.kmin + slot) << 35) | kLsb13;
+    return a.irr_cells[slot - (uint32_t)a.n_dense];
+}
+__device__ __forceinline__ void plain_range(const IndexView &a, uint32_t slot, uint32_t &s, uint32_t &e)
+{
+    if ((int64_t)slot < a.n_dense) {
+        s = a.dense[slot];
+        e = a.dense[slot + 1];
+    } else {
+        uint32_t k = slot - (uint32_t)a.n_dense;
+        s = a.irr_start[k];
+        e = a.irr_start[k + 1];
+    }
+}
+
+// ---- level-13 decode + prefix signatures -----------------------------------
+__device__ __forceinline__ int s2pos_to_ij(int o, int pos) { return (int)((0x874B78B4u >> (8 * o + 2 * pos)) & 3u); }
+__device__ __forceinline__ int s2pos_to_orientation(int pos) { return (int)((0xC1u >> (2 * pos)) & 3u); }
+
+// Level-13 (face, i, j) of a cell id (cellid.go faceIJOrientation, walked one
+// level at a time); false for ids that are not valid level-13 cells.
+__device__ __forceinline__ bool decode13(uint64_t c, int &face, int &i, int &j)
+{
+    if (!is_regular(c)) return false;
+    face = (int)(c >> 61);
+    int o = face & 1;
+    i = j = 0;
+#pragma unroll
+    for (int l = 0; l < 13; l++) {
+        int pos = (int)((c >> (59 - 2 * l)) & 3);
+        int ij = s2pos_to_ij(o, pos);
+        i = (i << 1) | (ij >> 1);
+        j = (j << 1) | (ij & 1);
+        o ^= s2pos_to_orientation(pos);
+    }
+    return true;
+}
+
+// Prefix signature of a sorted cell list: one bit per (i mod 16, j mod 16)
+// for every cell < c; `compact` iff all of them lie within +-7 cells of c on
+// c's face, so that equal bits imply equal cells.  Two lists can share a cell
+// < c only if their signatures overlap.
+struct Sig256 {
+    unsigned long long w[4];
+};
+__device__ __forceinline__ void prefix_sig(const uint64_t *cells, int64_t n, uint64_t c, Sig256 &sig, bool &compact)
+{
+    int fc = 0, ic = 0, jc = 0;
+    const bool cvalid = decode13(c, fc, ic, jc);
+    sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = 0;
+    compact = cvalid;
+    for (int64_t k = 0; k < n; k++) {
+        uint64_t x = cells[k];
+        if (x >= c) break;
+        int f, i, j;
+        if (decode13(x, f, i, j)) {
+            int b = ((i & 15) << 4) | (j & 15);
+            unsigned long long bit = 1ull << (b & 63);
+            int wi = b >> 6;
+            sig.w[0] |= wi == 0 ? bit : 0;
+            sig.w[1] |= wi == 1 ? bit : 0;
+            sig.w[2] |= wi == 2 ? bit : 0;
+            sig.w[3] |= wi == 3 ? bit : 0;
+            int di = i - ic, dj = j - jc;
+            if (f != fc || di < -7 || di > 7 || dj < -7 || dj > 7) compact = false;
+        } else {
+            sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = ~0ull;  // position unknown: force the exact check
+            compact = false;
+        }
+    }
+}
+
+// True iff the query (cells qc[0..nq)) and the entity share no cell < c.
+__device__ bool no_smaller_shared(const IndexView &a, uint32_t ent, uint64_t c, const uint64_t *qc, int64_t nq)
+{
+    const uint64_t *ec = a.e_cells + a.e_offs[ent];
+    int64_t ne = a.e_offs[ent + 1] - a.e_offs[ent];
+    int64_t i = 0, j = 0;
+    while (i < nq && j < ne) {
+        uint64_t x = qc[i], y = ec[j];
+        if (x >= c || y >= c) break;
+        if (x == y) return false;
+        if (x < y) i++;
+        else j++;
+    }
+    return true;
+}
+
+// ============================================================== build kernels
 __global__ void k_expand(int64_t n, const int64_t *offs, uint32_t *val)
 {
     int64_t e = tid64();
@@ -84,27 +272,6 @@ __global__ void k_scatter_part(int64_t P, const uint64_t *key, const uint32_t *v
     }
 }
 
-__global__ void k_time_keys(int64_t n, const uint32_t *p_e, const int64_t *t0, uint64_t *key, uint32_t *perm)
-{
-    int64_t i = tid64();
-    if (i >= n) return;
-    key[i] = (uint64_t)t0[p_e[i]] ^ 0x8000000000000000ull;  // signed order as unsigned
-    perm[i] = (uint32_t)i;
-}
-__global__ void k_gather_cell(int64_t n, const uint64_t *cell, const uint32_t *perm, uint64_t *out)
-{
-    int64_t i = tid64();
-    if (i < n) out[i] = cell[perm[i]];
-}
-__global__ void k_apply_perm(int64_t n, const uint32_t *perm, const uint64_t *cell_in, const uint32_t *e_in,
-                             uint64_t *cell_out, uint32_t *e_out)
-{
-    int64_t i = tid64();
-    if (i >= n) return;
-    cell_out[i] = cell_in[perm[i]];
-    e_out[i] = e_in[perm[i]];
-}
-
 __global__ void k_count_by_entity(int64_t P, const uint32_t *e, unsigned long long *cnt)
 {
     int64_t i = tid64();
@@ -117,30 +284,26 @@ __global__ void k_u64_to_i64(int64_t n, const unsigned long long *a, int64_t *b)
     if (k < n) b[k] = (int64_t)a[k];
 }
 
-__global__ void k_attrs(int64_t P, const uint64_t *p_cell, uint32_t *p_e, const int64_t *e_offs, const uint64_t *e_cells,
-                        const float *alo, const float *ahi, const int64_t *t0, const int64_t *t1, const int32_t *owner,
-                        float2 *p_alt, longlong2 *p_t, int32_t *p_owner)
+__global__ void k_i64_to_u32(int64_t n, const int64_t *a, uint32_t *b)
+{
+    int64_t k = tid64();
+    if (k < n) b[k] = (uint32_t)a[k];
+}
+
+__global__ void k_first_flags(int64_t P, const uint64_t *p_cell, uint32_t *p_e, const int64_t *e_offs,
+                              const uint64_t *e_cells, unsigned long long *n_cells)
 {
     int64_t i = tid64();
     if (i >= P) return;
     uint32_t e = p_e[i];
-    bool first = e_cells[e_offs[e]] == p_cell[i];
-    p_e[i] = e | (first ? kFirstBit : 0u);
-    p_alt[i] = make_float2(alo[e], ahi[e]);
-    p_t[i] = make_longlong2(t0[e], t1[e]);
-    if (owner) p_owner[i] = owner[e];
+    if (e_cells[e_offs[e]] == p_cell[i]) p_e[i] = e | kFirstBit;
+    if (i == 0 || p_cell[i] != p_cell[i - 1]) atomicAdd(n_cells, 1ull);
 }
 
 __global__ void k_dense_hist(int64_t n_reg, const uint64_t *p_cell, uint64_t kmin, unsigned long long *cnt)
 {
     int64_t i = tid64();
     if (i < n_reg) atomicAdd(&cnt[(p_cell[i] >> 35) - kmin], 1ull);
-}
-
-__global__ void k_i64_to_u32(int64_t n, const int64_t *a, uint32_t *b)
-{
-    int64_t k = tid64();
-    if (k < n) b[k] = (uint32_t)a[k];
 }
 
 __global__ void k_irr_runs(int64_t n_irr_p, const uint64_t *cells, int64_t *flag)
@@ -158,473 +321,482 @@ __global__ void k_irr_scatter(int64_t n_irr_p, const uint64_t *cells, const int6
     }
 }
 
-struct JoinArgs {
-    // queries
-    int64_t nq;
-    const int64_t *q_offs;
-    const uint64_t *q_cells;
-    const float *q_alo, *q_ahi;
-    const int64_t *q_tlo, *q_thi;
-    const int32_t *q_owner;
-    // index
-    const uint32_t *p_e;
-    const float2 *p_alt;
-    const longlong2 *p_t;
-    const int32_t *p_owner;
-    const int64_t *e_offs;
-    const uint64_t *e_cells;
-    uint64_t kmin;
-    int64_t n_dense;
-    const uint32_t *dense;
-    int64_t n_irr;
-    const uint64_t *irr_cells;
-    const uint32_t *irr_start;
-    // output
-    uint32_t *out_q, *out_e;
-    unsigned long long *counter;
-    int64_t cap;
-    // stats mode (roofline accounting): predicate off, count postings
-    // scanned (M) and canonical survivors (= distinct candidates D)
-    int stats;
-    unsigned long long *stat_m, *stat_d;
-};
-
-__device__ __forceinline__ void lookup(const JoinArgs &a, uint64_t c, uint32_t &s, uint32_t &e)
+// Time span of the rows that can match (stored NULL ends never do, Q9).
+__global__ void k_time_range(int64_t n, const int64_t *t0, const int64_t *t1, unsigned long long *mm)
 {
-    s = e = 0;
-    if (is_regular(c)) {
-        uint64_t k = c >> 35;
-        if (k >= a.kmin && (int64_t)(k - a.kmin) < a.n_dense) {
-            s = a.dense[k - a.kmin];
-            e = a.dense[k - a.kmin + 1];
-        }
-        return;
+    unsigned long long lo = ~0ull, hi = 0;
+    for (int64_t e = tid64(); e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        long long a = t0[e], b = t1[e];
+        if (b == INT64_MIN) continue;
+        long long x = a < b ? a : b, y = a < b ? b : a;
+        if (x != INT64_MIN) lo = min(lo, order_key(x));
+        hi = max(hi, order_key(y));
     }
-    int64_t lo = 0, hi = a.n_irr;
-    while (lo < hi) {
-        int64_t mid = (lo + hi) >> 1;
-        if (a.irr_cells[mid] < c) lo = mid + 1;
-        else hi = mid;
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, __shfl_xor(lo, o));
+        hi = max(hi, __shfl_xor(hi, o));
     }
-    if (lo < a.n_irr && a.irr_cells[lo] == c) {
-        s = a.irr_start[lo];
-        e = a.irr_start[lo + 1];
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&mm[0], lo);
+        atomicMax(&mm[1], hi);
     }
 }
 
-// True iff no cell < c is shared by the query (cells qc[0..nqc), all < c)
-// and the entity.
-__device__ bool smallest_shared(const JoinArgs &a, uint32_t ent, uint64_t c, const uint64_t *qc, int64_t nqc)
+// Entity bucket range [lo, hi] of [min(t0,t1), max(t0,t1)].
+__device__ __forceinline__ void entity_buckets(long long t0, long long t1, const Buckets &bk, int &lo, int &hi)
 {
-    const uint64_t *ec = a.e_cells + a.e_offs[ent];
-    int64_t ne = a.e_offs[ent + 1] - a.e_offs[ent];
-    int64_t i = 0, j = 0;
-    while (i < nqc && j < ne) {
-        uint64_t x = qc[i], y = ec[j];
-        if (y >= c) break;
-        if (x == y) return false;
-        if (x < y) i++;
-        else j++;
-    }
-    return true;
+    lo = bucket_of(t0 < t1 ? t0 : t1, bk);
+    hi = bucket_of(t0 < t1 ? t1 : t0, bk);
 }
 
-constexpr int kStage = 256;  // pairs staged per wave in LDS
-
-__global__ __launch_bounds__(kBlock) void k_join(JoinArgs a)
+__global__ void k_plain_slot(int64_t P, const uint64_t *p_cell, IndexView a, uint32_t *pslot)
 {
-    __shared__ uint32_t sq[kBlock / 64][kStage];
-    __shared__ uint32_t se[kBlock / 64][kStage];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int64_t q = (int64_t)blockIdx.x * (kBlock / 64) + w;
-    int staged = 0;
-    unsigned long long my_m = 0, my_d = 0;
-    auto flush = [&]() {
-        unsigned long long base = 0;
-        if (lane == 0 && staged) base = atomicAdd(a.counter, (unsigned long long)staged);
-        base = __shfl(base, 0);
-        for (int k = lane; k < staged; k += 64) {
-            unsigned long long o = base + (unsigned long long)k;
-            if ((int64_t)o < a.cap) {
-                a.out_q[o] = sq[w][k];
-                a.out_e[o] = se[w][k];
-            }
-        }
-        staged = 0;
-    };
-    if (q < a.nq) {
-        const int64_t tlo = a.q_tlo[q], thi = a.q_thi[q];
-        const float alo = a.q_alo[q], ahi = a.q_ahi[q];
-        const int32_t own = a.q_owner ? a.q_owner[q] : -1;
-        const int64_t c0 = a.q_offs[q], c1 = a.q_offs[q + 1];
-        const uint64_t *qc = a.q_cells + c0;
-        for (int64_t ci = c0; ci < c1; ci++) {
-            uint64_t c = a.q_cells[ci];
-            uint32_t s, e;
-            lookup(a, c, s, e);
-            for (uint32_t base = s; base < e; base += 64) {
-                uint32_t p = base + lane;
-                bool pass = false;
-                uint32_t ent = 0;
-                if (p < e) {
-                    uint32_t pe = a.p_e[p];
-                    float2 alt = a.p_alt[p];
-                    longlong2 t = a.p_t[p];
-                    ent = pe & ~kFirstBit;
-                    // COALESCE'd predicates of operations.go:394-402 after
-                    // the NULL->sentinel mapping (dssgpu.h)
-                    pass = a.stats || (t.y >= tlo && t.x <= thi && alt.y >= alo && alt.x <= ahi);
-                    if (pass && own >= 0 && !a.stats) pass = a.p_owner[p] == own;
-                    if (pass && ci != c0 && !(pe & kFirstBit)) pass = smallest_shared(a, ent, c, qc, ci - c0);
-                }
-                unsigned long long m = __ballot(pass);
-                int nsurv = __popcll(m);
-                if (a.stats) {
-                    my_m += (unsigned long long)(e - base < 64 ? e - base : 64);
-                    my_d += (unsigned long long)nsurv;
-                    continue;
-                }
-                if (nsurv == 0) continue;
-                if (staged + nsurv > kStage) flush();
-                if (pass) {
-                    int r = __popcll(m & ((1ull << lane) - 1ull));
-                    sq[w][staged + r] = (uint32_t)q;
-                    se[w][staged + r] = ent;
-                }
-                staged += nsurv;
-            }
-        }
-    }
-    if (a.stats) {
-        if (lane == 0 && (my_m || my_d)) {
-            atomicAdd(a.stat_m, my_m);
-            atomicAdd(a.stat_d, my_d);
-        }
-        return;
-    }
-    flush();
-}
-
-
-// ---------------------------------------------------------------- tiled join
-// The batch's (query, cell) pairs are grouped by index slot (radix sort), and
-// each workgroup joins one tile: kTileP postings of one cell (one per lane,
-// loaded once) against up to kTileQ of that cell's queries staged in LDS.
-__device__ __forceinline__ int s2pos_to_ij(int o, int pos) { return (int)((0x874B78B4u >> (8 * o + 2 * pos)) & 3u); }
-__device__ __forceinline__ int s2pos_to_orientation(int pos) { return (int)((0xC1u >> (2 * pos)) & 3u); }
-constexpr int kTileP = 256;
-constexpr int kTileQ = 256;
-constexpr uint32_t kRank0 = 0x80000000u;
-
-// slot of cell c in the index (dense slot, or n_dense + irregular index);
-// returns false if the index holds no posting for c.
-__device__ __forceinline__ bool cell_slot(const JoinArgs &a, uint64_t c, uint32_t &slot)
-{
-    if (is_regular(c)) {
-        uint64_t k = c >> 35;
-        if (k < a.kmin || (int64_t)(k - a.kmin) >= a.n_dense) return false;
-        uint32_t sl = (uint32_t)(k - a.kmin);
-        if (a.dense[sl + 1] == a.dense[sl]) return false;
-        slot = sl;
-        return true;
-    }
-    int64_t lo = 0, hi = a.n_irr;
-    while (lo < hi) {
-        int64_t mid = (lo + hi) >> 1;
-        if (a.irr_cells[mid] < c) lo = mid + 1;
-        else hi = mid;
-    }
-    if (lo < a.n_irr && a.irr_cells[lo] == c) {
-        slot = (uint32_t)(a.n_dense + lo);
-        return true;
-    }
-    return false;
-}
-__device__ __forceinline__ void slot_range(const JoinArgs &a, uint32_t slot, uint32_t &s, uint32_t &e, uint64_t &cell)
-{
-    if ((int64_t)slot < a.n_dense) {
-        s = a.dense[slot];
-        e = a.dense[slot + 1];
-        cell = ((a.kmin + slot) << 35) | kLsb13;
-    } else {
-        uint32_t k = slot - (uint32_t)a.n_dense;
-        s = a.irr_start[k];
-        e = a.irr_start[k + 1];
-        cell = a.irr_cells[k];
-    }
+    int64_t i = tid64();
+    if (i >= P) return;
+    uint32_t s = 0;
+    find_slot(a, p_cell[i], s);  // always found: the tables are built from p_cell
+    pslot[i] = s;
 }
 
 template <int PASS>
-__global__ void k_qc(JoinArgs a, int64_t *cnt, const int64_t *off, uint32_t *key, uint32_t *val)
+__global__ void k_bucket_copies(int64_t P, const uint32_t *p_e, const uint32_t *pslot, const int64_t *t0,
+                                const int64_t *t1, Buckets bk, int64_t *cnt, const int64_t *off, uint64_t *key,
+                                uint32_t *val)
+{
+    int64_t i = tid64();
+    if (i >= P) return;
+    uint32_t e = p_e[i] & ~kFirstBit;
+    long long a = t0[e], b = t1[e];
+    if (b == INT64_MIN) {  // stored NULL end: never matches
+        if (!PASS) cnt[i] = 0;
+        return;
+    }
+    int lo, hi;
+    entity_buckets(a, b, bk, lo, hi);
+    bool lng = hi - lo + 1 > kLongSpan;
+    if (!PASS) {
+        cnt[i] = lng ? 1 : hi - lo + 1;
+        return;
+    }
+    uint64_t sk = (uint64_t)pslot[i] << 6;
+    int64_t w = off[i];
+    if (lng) {
+        key[w] = sk | kLongBucket;
+        val[w] = (uint32_t)i;
+        return;
+    }
+    for (int b2 = lo; b2 <= hi; b2++, w++) {
+        key[w] = sk | (uint64_t)b2;
+        val[w] = (uint32_t)i;
+    }
+}
+
+__global__ void k_bucket_gather(int64_t NB, const uint32_t *sval, const uint64_t *p_cell, const uint32_t *p_e,
+                                const int64_t *e_offs, const uint64_t *e_cells, const float *alo, const float *ahi,
+                                const int64_t *t0, const int64_t *t1, const int32_t *owner, Buckets bk, uint32_t *b_e,
+                                float2 *b_alt, longlong2 *b_t, uint8_t *b_meta, ulonglong2 *b_sig, int32_t *b_owner)
+{
+    int64_t j = tid64();
+    if (j >= NB) return;
+    uint32_t i = sval[j];
+    uint32_t pe = p_e[i];
+    uint32_t e = pe & ~kFirstBit;
+    long long a = t0[e], b = t1[e];
+    int lo, hi;
+    entity_buckets(a, b, bk, lo, hi);
+    Sig256 sig;
+    bool compact = false;
+    if (!(pe & kFirstBit))
+        prefix_sig(e_cells + e_offs[e], e_offs[e + 1] - e_offs[e], p_cell[i], sig, compact);
+    else
+        sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = 0;
+    b_e[j] = pe;
+    b_alt[j] = make_float2(alo[e], ahi[e]);
+    b_t[j] = make_longlong2(a, b);
+    b_meta[j] = (uint8_t)(lo | (compact ? 0x80 : 0));
+    b_sig[2 * j] = make_ulonglong2(sig.w[0], sig.w[1]);
+    b_sig[2 * j + 1] = make_ulonglong2(sig.w[2], sig.w[3]);
+    if (owner) b_owner[j] = owner[e];
+}
+
+__global__ void k_group_mask(int64_t ng, const uint64_t *gkey, unsigned long long *s_mask)
+{
+    int64_t g = tid64();
+    if (g < ng) atomicOr(&s_mask[gkey[g] >> 6], 1ull << (gkey[g] & 63));
+}
+__global__ void k_slot_pop(int64_t ns, const unsigned long long *s_mask, int64_t *cnt)
+{
+    int64_t s = tid64();
+    if (s < ns) cnt[s] = __popcll(s_mask[s]);
+}
+
+// ============================================================== search kernels
+struct QueryView {
+    int64_t nq;
+    const int64_t *offs;
+    const uint64_t *cells;
+    const float *alo, *ahi;
+    const int64_t *tlo, *thi;
+    const int32_t *owner;
+};
+
+// (1) one key (slot << 6 | bucket) per non-empty group a query cell meets:
+// the buckets of [min(tlo,thi), max(tlo,thi)] plus the long bucket.
+template <int PASS>
+__global__ void k_qkeys(IndexView a, QueryView qv, int64_t *cnt, const int64_t *off, uint64_t *key, uint32_t *val)
 {
     int64_t q = tid64();
-    if (q >= a.nq) return;
-    int64_t c0 = a.q_offs[q], c1 = a.q_offs[q + 1];
+    if (q >= qv.nq) return;
+    const long long tlo = qv.tlo[q], thi = qv.thi[q];
+    const int bq0 = bucket_of(tlo < thi ? tlo : thi, a.bk), bq1 = bucket_of(tlo < thi ? thi : tlo, a.bk);
+    const unsigned long long range = ((1ull << (bq1 + 1)) - 1ull) & ~((1ull << bq0) - 1ull);
+    const int64_t c0 = qv.offs[q], c1 = qv.offs[q + 1];
     int64_t n = 0, w = PASS ? off[q] : 0;
     for (int64_t k = c0; k < c1; k++) {
         uint32_t slot;
-        if (!cell_slot(a, a.q_cells[k], slot)) continue;
-        if (PASS) {
-            key[w] = slot;
-            val[w] = (uint32_t)q | (k == c0 ? kRank0 : 0u);
+        if (!find_slot(a, qv.cells[k], slot)) continue;
+        const unsigned long long m0 = a.s_mask[slot];
+        unsigned long long m = (m0 & range) | (m0 & (1ull << kLongBucket));
+        if (!PASS) {
+            n += __popcll(m);
+            continue;
+        }
+        const uint32_t v = (uint32_t)q | (k == c0 ? kRank0 : 0u);
+        while (m) {
+            int b = __builtin_ctzll(m);
+            m &= m - 1;
+            key[w] = ((uint64_t)slot << 6) | (uint64_t)b;
+            val[w] = v;
             w++;
         }
-        n++;
     }
     if (!PASS) cnt[q] = n;
 }
 
+// Query record: what one predicate sweep needs, read with scalar loads.
+struct alignas(64) QRec {
+    long long tlo, thi;
+    float alo, ahi;
+    uint32_t qv;  // query | kRank0 | kCompact
+    int32_t own;  // owner filter or -1
+    unsigned long long sig[4];
+};
+static_assert(sizeof(QRec) == 64, "QRec layout");
+
+__global__ void k_qrec(int64_t n, IndexView a, QueryView qv, const uint64_t *skey, const uint32_t *sval, QRec *recs)
+{
+    int64_t j = tid64();
+    if (j >= n) return;
+    const uint32_t v = sval[j];
+    const uint32_t q = v & ~kRank0;
+    QRec r;
+    r.tlo = qv.tlo[q];
+    r.thi = qv.thi[q];
+    r.alo = qv.alo[q];
+    r.ahi = qv.ahi[q];
+    r.own = qv.owner ? qv.owner[q] : -1;
+    Sig256 sig;
+    bool compact = false;
+    if (!(v & kRank0)) {
+        uint64_t c = cell_of_slot(a, (uint32_t)(skey[j] >> 6));
+        prefix_sig(qv.cells + qv.offs[q], qv.offs[q + 1] - qv.offs[q], c, sig, compact);
+    } else {
+        sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = 0;
+    }
+    r.qv = v | (compact ? kCompact : 0u);
+    r.sig[0] = sig.w[0];
+    r.sig[1] = sig.w[1];
+    r.sig[2] = sig.w[2];
+    r.sig[3] = sig.w[3];
+    recs[j] = r;
+}
+
+__device__ __forceinline__ uint32_t group_of(const IndexView &a, uint64_t key)
+{
+    const uint32_t slot = (uint32_t)(key >> 6);
+    const int b = (int)(key & 63);
+    return a.s_base[slot] + (uint32_t)__popcll(a.s_mask[slot] & ((1ull << b) - 1ull));
+}
+
+// (2) join units: (run, 64-posting tile, kQChunk-query chunk)
 template <int PASS>
-__global__ void k_tiles(int64_t nruns, JoinArgs a, const uint32_t *ukey, const int64_t *rstart, int64_t *cnt,
-                        const int64_t *toff, uint32_t *t_run, uint32_t *t_p, uint32_t *t_q)
+__global__ void k_units(int64_t nruns, IndexView a, const uint64_t *ukey, const int64_t *rstart, int64_t *cnt,
+                        const int64_t *uoff, uint32_t *u_run, uint32_t *u_pt, uint32_t *u_qt)
 {
     int64_t r = tid64();
     if (r >= nruns) return;
-    uint32_t s, e;
-    uint64_t cell;
-    slot_range(a, ukey[r], s, e, cell);
-    int64_t np = (int64_t)(e - s), nq = rstart[r + 1] - rstart[r];
-    int64_t tp = (np + kTileP - 1) / kTileP, tq = (nq + kTileQ - 1) / kTileQ;
+    const uint32_t g = group_of(a, ukey[r]);
+    const int64_t np = (int64_t)a.bk_start[g + 1] - a.bk_start[g];
+    const int64_t nq = rstart[r + 1] - rstart[r];
+    const int64_t tp = (np + 63) / 64, tq = (nq + kQChunk - 1) / kQChunk;
     if (!PASS) {
         cnt[r] = tp * tq;
         return;
     }
-    int64_t w = toff[r];
+    int64_t w = uoff[r];
     for (int64_t i = 0; i < tp; i++)
         for (int64_t j = 0; j < tq; j++, w++) {
-            t_run[w] = (uint32_t)r;
-            t_p[w] = (uint32_t)i;
-            t_q[w] = (uint32_t)j;
+            u_run[w] = (uint32_t)r;
+            u_pt[w] = (uint32_t)i;
+            u_qt[w] = (uint32_t)j;
         }
 }
 
-struct QAttr {
-    int64_t tlo, thi;
-    float alo, ahi;
-    uint32_t qv;  // query id | kRank0 if the cell is the query's first cell
-    int32_t own;  // owner filter, or -1; bit 30 of `compact` below
+// Diagnostics (timing mode): sum over runs of records x 64-posting tiles
+// (wave iterations before the time pre-filter) and of records x postings
+// (useful lane tests).
+__global__ void k_work_stats(int64_t nruns, IndexView a, const uint64_t *ukey, const int64_t *rstart,
+                             unsigned long long *stat)
+{
+    int64_t r = tid64();
+    unsigned long long it = 0, lt = 0;
+    if (r < nruns) {
+        const uint32_t g = group_of(a, ukey[r]);
+        const unsigned long long np = a.bk_start[g + 1] - a.bk_start[g];
+        const unsigned long long nq = (unsigned long long)(rstart[r + 1] - rstart[r]);
+        it = nq * ((np + 63) / 64);
+        lt = nq * np;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        it += __shfl_xor(it, o);
+        lt += __shfl_xor(lt, o);
+    }
+    if ((threadIdx.x & 63) == 0 && (it || lt)) {
+        atomicAdd(&stat[0], it);
+        atomicAdd(&stat[1], lt);
+    }
+}
+
+struct JoinArgs {
+    IndexView ix;
+    QueryView qv;
+    int64_t nunits;
+    const uint64_t *ukey;
+    const int64_t *rstart;
+    int64_t cap;
 };
 
-// True iff q and entity `ent` share no cell smaller than c (both lists sorted).
-__device__ bool smallest_shared_q(const JoinArgs &a, uint32_t ent, uint64_t c, uint32_t q)
+// (3) one wavefront per unit; 64 postings in lanes, query records uniform.
+// Pointers passed apart and __restrict__ so that the uniform record and unit
+// loads compile to scalar (s_load) loads.
+__global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__restrict__ recs,
+                                                      const uint32_t *__restrict__ u_run, const uint32_t *__restrict__ u_pt,
+                                                      const uint32_t *__restrict__ u_qt, uint32_t *__restrict__ out_q,
+                                                      uint32_t *__restrict__ out_e, unsigned long long *__restrict__ counter)
 {
-    const uint64_t *ec = a.e_cells + a.e_offs[ent];
-    int64_t ne = a.e_offs[ent + 1] - a.e_offs[ent];
-    const uint64_t *qc = a.q_cells + a.q_offs[q];
-    int64_t nq = a.q_offs[q + 1] - a.q_offs[q];
-    int64_t i = 0, j = 0;
-    while (i < nq && j < ne) {
-        uint64_t x = qc[i], y = ec[j];
-        if (x >= c || y >= c) break;
-        if (x == y) return false;
-        if (x < y) i++;
-        else j++;
-    }
-    return true;
-}
-
-// Level-13 (face, i, j) of a cell id (cellid.go faceIJOrientation, walked one
-// level at a time); false for ids that are not valid level-13 cells.
-__device__ __forceinline__ bool decode13(uint64_t c, int &face, int &i, int &j)
-{
-    if (!is_regular(c)) return false;
-    face = (int)(c >> 61);
-    int o = face & 1;
-    i = j = 0;
-#pragma unroll
-    for (int l = 0; l < 13; l++) {
-        int pos = (int)((c >> (59 - 2 * l)) & 3);
-        int ij = s2pos_to_ij(o, pos);
-        i = (i << 1) | (ij >> 1);
-        j = (j << 1) | (ij & 1);
-        o ^= s2pos_to_orientation(pos);
-    }
-    return true;
-}
-
-// Prefix signature of a sorted cell list: one bit per (i mod 16, j mod 16)
-// (256 bits) for every cell < c; `compact` iff all of them lie within +-7
-// cells of c on c's face, so that equal bits imply equal cells.
-struct Sig256 {
-    uint64_t w[4];
-};
-__device__ __forceinline__ void prefix_sig(const uint64_t *cells, int64_t n, uint64_t c, int fc, int ic, int jc,
-                                           bool cvalid, Sig256 &sig, bool &compact)
-{
-    sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = 0;
-    compact = cvalid;
-    for (int64_t k = 0; k < n; k++) {
-        uint64_t x = cells[k];
-        if (x >= c) break;
-        int f, i, j;
-        if (decode13(x, f, i, j)) {
-            int b = ((i & 15) << 4) | (j & 15);
-            uint64_t bit = 1ull << (b & 63);
-            int wi = b >> 6;
-            sig.w[0] |= wi == 0 ? bit : 0;
-            sig.w[1] |= wi == 1 ? bit : 0;
-            sig.w[2] |= wi == 2 ? bit : 0;
-            sig.w[3] |= wi == 3 ? bit : 0;
-            int di = i - ic, dj = j - jc;
-            if (f != fc || di < -7 || di > 7 || dj < -7 || dj > 7) compact = false;
-        } else {
-            sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = ~0ull;  // unknown position: force the exact check
-            compact = false;
-        }
-    }
-}
-__device__ __forceinline__ bool sig_overlap(const Sig256 &a, const uint64_t *b)
-{
-    return ((a.w[0] & b[0]) | (a.w[1] & b[1]) | (a.w[2] & b[2]) | (a.w[3] & b[3])) != 0;
-}
-
-__global__ __launch_bounds__(kTileP) void k_join_tile(JoinArgs a, const uint32_t *ukey, const int64_t *rstart,
-                                                      const uint32_t *sval, const uint32_t *t_run, const uint32_t *t_p,
-                                                      const uint32_t *t_q)
-{
-    __shared__ QAttr sq_attr[kTileQ];
-    __shared__ uint64_t sq_sig[kTileQ][4];
-    __shared__ uint8_t sq_compact[kTileQ];
-    __shared__ uint32_t sq[kTileP / 64][kStage];
-    __shared__ uint32_t se[kTileP / 64][kStage];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t r = t_run[blockIdx.x];
-    uint32_t ps, pe;
-    uint64_t cell;
-    slot_range(a, ukey[r], ps, pe, cell);
-    const int64_t q0 = rstart[r] + (int64_t)t_q[blockIdx.x] * kTileQ;
-    const int64_t q1 = min(rstart[r + 1], q0 + kTileQ);
-    const int nqt = (int)(q1 - q0);
-    int fc = 0, ic = 0, jc = 0;
-    const bool cvalid = decode13(cell, fc, ic, jc);
-    if (tid < nqt) {
-        uint32_t v = sval[q0 + tid];
-        uint32_t q = v & ~kRank0;
-        QAttr qa;
-        qa.tlo = a.q_tlo[q];
-        qa.thi = a.q_thi[q];
-        qa.alo = a.q_alo[q];
-        qa.ahi = a.q_ahi[q];
-        qa.qv = v;
-        qa.own = a.q_owner ? a.q_owner[q] : -1;
-        bool cp;
-        Sig256 qs;
-        prefix_sig(a.q_cells + a.q_offs[q], a.q_offs[q + 1] - a.q_offs[q], cell, fc, ic, jc, cvalid, qs, cp);
-        sq_attr[tid] = qa;
-        sq_sig[tid][0] = qs.w[0];
-        sq_sig[tid][1] = qs.w[1];
-        sq_sig[tid][2] = qs.w[2];
-        sq_sig[tid][3] = qs.w[3];
-        sq_compact[tid] = cp ? 1 : 0;
-    }
-    const uint32_t p = ps + t_p[blockIdx.x] * kTileP + tid;
-    const bool valid = p < pe;
+    __shared__ uint32_t sq[kWaves][kStage];
+    __shared__ uint32_t se[kWaves][kStage];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t u = (int64_t)blockIdx.x * kWaves + w;
+    if (u >= a.nunits) return;
+    const IndexView &ix = a.ix;
+    const uint32_t r = u_run[u];
+    const uint64_t key = a.ukey[r];
+    const int b = (int)(key & 63);
+    const uint32_t g = group_of(ix, key);
+    const uint32_t gs = ix.bk_start[g], ge = ix.bk_start[g + 1];
+    const uint32_t p = gs + u_pt[u] * 64u + (uint32_t)lane;
+    const bool valid = p < ge;
     uint32_t pev = 0;
     float2 alt = make_float2(0.f, 0.f);
     longlong2 t = make_longlong2(0, 0);
     int32_t pown = 0;
+    uint8_t meta = 0;
+    ulonglong2 s01 = make_ulonglong2(0, 0), s23 = make_ulonglong2(0, 0);
     if (valid) {
-        pev = a.p_e[p];
-        alt = a.p_alt[p];
-        t = a.p_t[p];
-        if (a.q_owner) pown = a.p_owner[p];
+        pev = ix.b_e[p];
+        alt = ix.b_alt[p];
+        t = ix.b_t[p];
+        meta = ix.b_meta[p];
+        if (ix.b_owner) pown = ix.b_owner[p];
+        if (!(pev & kFirstBit)) {
+            s01 = ix.b_sig[2 * (size_t)p];
+            s23 = ix.b_sig[2 * (size_t)p + 1];
+        }
     }
     const uint32_t ent = pev & ~kFirstBit;
     const bool efirst = (pev & kFirstBit) != 0;
-    // time bounds of this posting tile (postings are ordered by start time
-    // within a cell): queries whose window misses them are skipped whole
-    __shared__ long long s_tmin[kTileP / 64], s_tmax[kTileP / 64];
-    {
-        long long mn = valid ? t.x : LLONG_MAX, mx = valid ? t.y : LLONG_MIN;
-        for (int o = 32; o > 0; o >>= 1) {
-            mn = min(mn, __shfl_xor(mn, o));
-            mx = max(mx, __shfl_xor(mx, o));
-        }
-        if (lane == 0) {
-            s_tmin[w] = mn;
-            s_tmax[w] = mx;
-        }
+    const int be0 = meta & 0x3f;
+    const bool ecompact = (meta & 0x80) != 0;
+    // time bounds of the unit: records whose window misses all 64 are skipped
+    long long tmin = valid ? t.x : LLONG_MAX, tmax = valid ? t.y : LLONG_MIN;
+    for (int o = 32; o > 0; o >>= 1) {
+        tmin = min(tmin, __shfl_xor(tmin, o));
+        tmax = max(tmax, __shfl_xor(tmax, o));
     }
-    Sig256 esig;
-    esig.w[0] = esig.w[1] = esig.w[2] = esig.w[3] = 0;
-    bool ecompact = true;
-    if (valid && !efirst)
-        prefix_sig(a.e_cells + a.e_offs[ent], a.e_offs[ent + 1] - a.e_offs[ent], cell, fc, ic, jc, cvalid, esig, ecompact);
-    __syncthreads();
-    long long tmin = s_tmin[0], tmax = s_tmax[0];
-#pragma unroll
-    for (int k = 1; k < kTileP / 64; k++) {
-        tmin = min(tmin, s_tmin[k]);
-        tmax = max(tmax, s_tmax[k]);
-    }
+    const uint64_t cell = cell_of_slot(ix, (uint32_t)(key >> 6));
+    const int64_t k0 = a.rstart[r] + (int64_t)u_qt[u] * kQChunk;
+    const int64_t k1 = min(a.rstart[r + 1], k0 + kQChunk);
     int staged = 0;
     auto flush = [&]() {
         __builtin_amdgcn_wave_barrier();
         unsigned long long base = 0;
-        if (lane == 0 && staged) base = atomicAdd(a.counter, (unsigned long long)staged);
+        if (lane == 0 && staged) base = atomicAdd(counter, (unsigned long long)staged);
         base = __shfl(base, 0);
         for (int k = lane; k < staged; k += 64) {
             unsigned long long o = base + (unsigned long long)k;
             if ((int64_t)o < a.cap) {
-                a.out_q[o] = sq[w][k];
-                a.out_e[o] = se[w][k];
+                out_q[o] = sq[w][k];
+                out_e[o] = se[w][k];
             }
         }
         staged = 0;
         __builtin_amdgcn_wave_barrier();
     };
-    for (int k = 0; k < nqt; k++) {
-        const QAttr qa = sq_attr[k];
-        if (qa.thi < tmin || qa.tlo > tmax) continue;  // no posting of the tile can match
-        // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels)
-        bool pass = valid && t.y >= qa.tlo && t.x <= qa.thi && alt.y >= qa.alo && alt.x <= qa.ahi;
-        if (qa.own >= 0) pass = pass && pown == qa.own;
-        // keep the pair only at the smallest shared cell (SQL DISTINCT, Q13)
-        if (pass && !efirst && !(qa.qv & kRank0) && sig_overlap(esig, sq_sig[k])) {
-            if (ecompact && sq_compact[k]) pass = false;  // a shared smaller cell exists
-            else pass = smallest_shared_q(a, ent, cell, qa.qv & ~kRank0);
+    // Records are fetched 64 at a time, one per lane (coalesced 16-byte loads
+    // instead of a serial chain of scalar loads), pre-filtered against the
+    // unit's time bounds with one ballot, and broadcast with readlane.
+    const int4 *rec4 = reinterpret_cast<const int4 *>(recs);
+    for (int64_t base = k0; base < k1; base += 64) {
+        const int64_t kk = base + lane;
+        int4 r0 = make_int4(0, 0, 0, 0), r1 = r0, r2 = r0, r3 = r0;
+        bool rel = false;
+        int rbq0 = 0;
+        if (kk < k1) {
+            r0 = rec4[4 * kk];
+            r1 = rec4[4 * kk + 1];
+            r2 = rec4[4 * kk + 2];
+            r3 = rec4[4 * kk + 3];
+            const long long tlo = ((long long)r0.y << 32) | (uint32_t)r0.x;
+            const long long thi = ((long long)r0.w << 32) | (uint32_t)r0.z;
+            rel = !(tmax < tlo || tmin > thi);  // else no posting of the unit can match
+            rbq0 = bucket_of(tlo < thi ? tlo : thi, ix.bk);
         }
-        unsigned long long m = __ballot(pass);
-        if (m == 0) continue;
-        int nsurv = __popcll(m);
-        if (staged + nsurv > kStage) flush();
-        if (pass) {
-            int rk = __popcll(m & ((1ull << lane) - 1ull));
-            sq[w][staged + rk] = qa.qv & ~kRank0;
-            se[w][staged + rk] = ent;
+        unsigned long long todo = __ballot(rel);
+        while (todo) {
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const long long tlo = ((long long)__builtin_amdgcn_readlane(r0.y, j) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readlane(r0.x, j);
+            const long long thi = ((long long)__builtin_amdgcn_readlane(r0.w, j) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readlane(r0.z, j);
+            const float alo = __int_as_float(__builtin_amdgcn_readlane(r1.x, j));
+            const float ahi = __int_as_float(__builtin_amdgcn_readlane(r1.y, j));
+            const uint32_t qv = (uint32_t)__builtin_amdgcn_readlane(r1.z, j);
+            const int32_t own = __builtin_amdgcn_readlane(r1.w, j);
+            // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels)
+            bool pass = valid && t.y >= tlo && t.x <= thi && alt.y >= alo && alt.x <= ahi;
+            if (own >= 0) pass = pass && pown == own;
+            // keep the pair only in its first common bucket ...
+            if (b != kLongBucket) {
+                const int bq0 = __builtin_amdgcn_readlane(rbq0, j);
+                pass = pass && b == (bq0 > be0 ? bq0 : be0);
+            }
+            // ... and at the smallest shared cell (SQL DISTINCT, Q13)
+            bool need = pass && !efirst && !(qv & kRank0);
+            if (__ballot(need)) {
+                const unsigned long long q0 = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(r2.y, j) << 32) |
+                                              (uint32_t)__builtin_amdgcn_readlane(r2.x, j);
+                const unsigned long long q1 = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(r2.w, j) << 32) |
+                                              (uint32_t)__builtin_amdgcn_readlane(r2.z, j);
+                const unsigned long long q2 = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(r3.y, j) << 32) |
+                                              (uint32_t)__builtin_amdgcn_readlane(r3.x, j);
+                const unsigned long long q3 = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(r3.w, j) << 32) |
+                                              (uint32_t)__builtin_amdgcn_readlane(r3.z, j);
+                if (need && ((s01.x & q0) | (s01.y & q1) | (s23.x & q2) | (s23.y & q3))) {
+                    if (ecompact && (qv & kCompact)) {
+                        pass = false;  // equal bits within +-7 cells: a shared smaller cell exists
+                    } else {
+                        const uint32_t q = qv & ~(kRank0 | kCompact);
+                        pass = no_smaller_shared(ix, ent, cell, a.qv.cells + a.qv.offs[q],
+                                                 a.qv.offs[q + 1] - a.qv.offs[q]);
+                    }
+                }
+            }
+            const unsigned long long m = __ballot(pass);
+            if (m == 0) continue;
+            const int nsurv = __popcll(m);
+            if (staged + nsurv > kStage) flush();
+            if (pass) {
+                const int rk = __popcll(m & ((1ull << lane) - 1ull));
+                sq[w][staged + rk] = qv & ~(kRank0 | kCompact);
+                se[w][staged + rk] = ent;
+            }
+            staged += nsurv;
         }
-        staged += nsurv;
     }
     flush();
 }
 
+// Roofline accounting over the plain postings, predicate off: M = postings
+// scanned query-cell by query-cell, D = pairs surviving the smallest-shared-
+// cell rule (= distinct candidate entities per query, summed).
+__global__ __launch_bounds__(kBlock) void k_stats(IndexView a, QueryView qv, unsigned long long *stat)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    unsigned long long my_m = 0, my_d = 0;
+    if (q < qv.nq) {
+        const int64_t c0 = qv.offs[q], c1 = qv.offs[q + 1];
+        for (int64_t ci = c0; ci < c1; ci++) {
+            const uint64_t c = qv.cells[ci];
+            uint32_t slot, s = 0, e = 0;
+            if (find_slot(a, c, slot)) plain_range(a, slot, s, e);
+            for (uint32_t base = s; base < e; base += 64) {
+                const uint32_t p = base + lane;
+                bool pass = false;
+                if (p < e) {
+                    const uint32_t pe = a.p_e[p];
+                    pass = ci == c0 || (pe & kFirstBit) ||
+                           no_smaller_shared(a, pe & ~kFirstBit, c, qv.cells + c0, ci - c0);
+                }
+                my_m += (unsigned long long)(e - base < 64 ? e - base : 64);
+                my_d += (unsigned long long)__popcll(__ballot(pass));
+            }
+        }
+    }
+    if (lane == 0 && (my_m || my_d)) {
+        atomicAdd(&stat[0], my_m);
+        atomicAdd(&stat[1], my_d);
+    }
+}
+
+template <typename K, typename V>
+void sort_pairs(const K *ki, K *ko, const V *vi, V *vo, int64_t n, int bits, DevBuf<unsigned char> &tmp, hipStream_t s)
+{
+    if (n <= 0) return;
+    size_t bytes = 0;
+    DSS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, ki, ko, vi, vo, (int)n, 0, bits, s));
+    tmp.ensure(bytes + 16);
+    DSS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, bytes, ki, ko, vi, vo, (int)n, 0, bits, s));
+}
+
+int bits_for(int64_t n)
+{
+    int b = 1;
+    while (b < 63 && ((int64_t)1 << b) <= n) b++;
+    return b;
+}
+
+int64_t fetch_i64(const int64_t *p, hipStream_t s)
+{
+    int64_t v = 0;
+    DSS_HIP(hipMemcpyAsync(&v, p, sizeof(v), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    return v;
+}
+
 }  // namespace
 
-// ---------------------------------------------------------------- build
+// ================================================================== build
 void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, const uint64_t *cells,
                          const float *alt_lo, const float *alt_hi, const int64_t *t0, const int64_t *t1,
                          const int32_t *owner, hipStream_t s)
 {
     idx->n_e = n;
     idx->has_owner = owner != nullptr;
-    int64_t P = 0;
-    DSS_HIP(hipMemcpyAsync(&P, cell_offs + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    DSS_HIP(hipStreamSynchronize(s));
+    const int64_t P = fetch_i64(cell_offs + n, s);
     if (P >= (int64_t)0x7fffffff) throw Error(DSSG_ERR_INVALID, "index: more than 2^31 postings per device");
     if (n >= (int64_t)0x7fffffff) throw Error(DSSG_ERR_INVALID, "index: more than 2^31 entities per device");
     const int64_t Pa = P + 1;
     uint64_t *ka = k0_.ensure(Pa), *kb = k1_.ensure(Pa);
     uint32_t *va = v0_.ensure(Pa), *vb = v1_.ensure(Pa);
-    DSS_HIP(hipMemcpyAsync(ka, cells, sizeof(uint64_t) * P, hipMemcpyDeviceToDevice, s));
+    if (P) DSS_HIP(hipMemcpyAsync(ka, cells, sizeof(uint64_t) * P, hipMemcpyDeviceToDevice, s));
     if (n) hipLaunchKernelGGL(k_expand, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, cell_offs, va);
-    // sort postings by cell (stable: entity order preserved within a cell)
-    size_t bytes = 0;
-    if (P) {
-        DSS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, ka, kb, va, vb, (int)P, 0, 64, s));
-        tmp_.ensure(bytes + 16);
-        DSS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_.p, bytes, ka, kb, va, vb, (int)P, 0, 64, s));
-    }
-    // unique (cell, entity) + regular/irregular partition
+    // (1) plain postings: sort by cell (stable: entity order kept), unique,
+    // regular/irregular partition
+    sort_pairs(ka, kb, va, vb, P, 64, tmp_, s);
     int64_t *keep = c0_.ensure(3 * Pa), *reg = keep + Pa, *irr = reg + Pa;
     int64_t *kpos = c1_.ensure(3 * (Pa + 1)), *rpos = kpos + (Pa + 1), *ipos = rpos + (Pa + 1);
     if (P) hipLaunchKernelGGL(k_keep_flags, dim3(grid_for(P, kBlock)), dim3(kBlock), 0, s, P, kb, vb, keep, reg, irr);
@@ -644,70 +816,31 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     if (P)
         hipLaunchKernelGGL(k_scatter_part, dim3(grid_for(P, kBlock)), dim3(kBlock), 0, s, P, kb, vb, reg, rpos, irr, ipos,
                            n_reg, p_cell, p_e);
-    // within each cell, order postings by start time (segments sorted apart
-    // so regular postings stay in front): sort by t0, then stable by cell
-    {
-        DevBuf<uint64_t> tk, tk2, cb;
-        DevBuf<uint32_t> pm, pm2;
-        DevBuf<uint64_t> pc2;
-        DevBuf<uint32_t> pe2;
-        uint64_t *tkey = tk.ensure(Pu + 1), *tkey2 = tk2.ensure(Pu + 1), *cbuf = cb.ensure(Pu + 1), *pcn = pc2.ensure(Pu + 1);
-        uint32_t *perm = pm.ensure(Pu + 1), *perm2 = pm2.ensure(Pu + 1), *pen = pe2.ensure(Pu + 1);
-        int64_t segs[2][2] = {{0, n_reg}, {n_reg, Pu}};
-        for (auto &sg : segs) {
-            int64_t o = sg[0], m = sg[1] - sg[0];
-            if (m <= 1) {
-                if (m == 1) {
-                    DSS_HIP(hipMemcpyAsync(pcn + o, p_cell + o, sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
-                    DSS_HIP(hipMemcpyAsync(pen + o, p_e + o, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-                }
-                continue;
-            }
-            hipLaunchKernelGGL(k_time_keys, dim3(grid_for(m, kBlock)), dim3(kBlock), 0, s, m, p_e + o, t0, tkey, perm);
-            size_t b2 = 0;
-            DSS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b2, tkey, tkey2, perm, perm2, (int)m, 0, 64, s));
-            tmp_.ensure(b2 + 16);
-            DSS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_.p, b2, tkey, tkey2, perm, perm2, (int)m, 0, 64, s));
-            hipLaunchKernelGGL(k_gather_cell, dim3(grid_for(m, kBlock)), dim3(kBlock), 0, s, m, p_cell + o, perm2, cbuf);
-            b2 = 0;
-            DSS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b2, cbuf, tkey, perm2, perm, (int)m, 0, 64, s));
-            tmp_.ensure(b2 + 16);
-            DSS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_.p, b2, cbuf, tkey, perm2, perm, (int)m, 0, 64, s));
-            hipLaunchKernelGGL(k_apply_perm, dim3(grid_for(m, kBlock)), dim3(kBlock), 0, s, m, perm, p_cell + o, p_e + o,
-                               pcn + o, pen + o);
-        }
-        DSS_HIP(hipMemcpyAsync(p_cell, pcn, sizeof(uint64_t) * Pu, hipMemcpyDeviceToDevice, s));
-        DSS_HIP(hipMemcpyAsync(p_e, pen, sizeof(uint32_t) * Pu, hipMemcpyDeviceToDevice, s));
-        DSS_HIP(hipStreamSynchronize(s));
-    }
-    // entity -> sorted unique cell lists: unique postings in cell order, then
-    // a stable sort by entity.
+    // (2) entity -> sorted unique cell lists: unique postings in cell order,
+    // then a stable sort by entity
     if (P)
         hipLaunchKernelGGL(k_scatter_unique, dim3(grid_for(P, kBlock)), dim3(kBlock), 0, s, P, kb, vb, keep, kpos, ka, va);
     uint64_t *e_cells = idx->e_cells.ensure(Pu + 1);
-    uint32_t *vsorted = vb;
-    if (Pu) {
-        bytes = 0;
-        DSS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, va, vb, ka, e_cells, (int)Pu, 0, 32, s));
-        tmp_.ensure(bytes + 16);
-        DSS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_.p, bytes, va, vb, ka, e_cells, (int)Pu, 0, 32, s));
-    }
+    sort_pairs(va, vb, ka, e_cells, Pu, 32, tmp_, s);
     DevBuf<unsigned long long> ecnt;
-    unsigned long long *ec = ecnt.ensure(n + 1);
-    DSS_HIP(hipMemsetAsync(ec, 0, sizeof(unsigned long long) * (n + 1), s));
-    if (Pu) hipLaunchKernelGGL(k_count_by_entity, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, vsorted, ec);
+    unsigned long long *ec = ecnt.ensure(n + 2);
+    DSS_HIP(hipMemsetAsync(ec, 0, sizeof(unsigned long long) * (n + 2), s));
+    if (Pu) hipLaunchKernelGGL(k_count_by_entity, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, vb, ec);
     int64_t *ec64 = c0_.ensure(3 * Pa > n + 1 ? 3 * Pa : n + 1);
     if (n) hipLaunchKernelGGL(k_u64_to_i64, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, ec, ec64);
     int64_t *e_offs = idx->e_offs.ensure(n + 1);
     exclusive_scan_i64(ec64, e_offs, n, tmp_, s);
-    // inline attributes + first-cell flag
-    float2 *p_alt = idx->p_alt.ensure(Pu + 1);
-    longlong2 *p_t = idx->p_t.ensure(Pu + 1);
-    int32_t *p_owner = idx->p_owner.ensure(Pu + 1);
+    unsigned long long *ncell = ec + n + 1;  // scratch counter (zeroed above)
     if (Pu)
-        hipLaunchKernelGGL(k_attrs, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, p_cell, p_e, e_offs, e_cells,
-                           alt_lo, alt_hi, t0, t1, owner, p_alt, p_t, p_owner);
-    // dense lookup over regular postings
+        hipLaunchKernelGGL(k_first_flags, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, p_cell, p_e, e_offs, e_cells,
+                           ncell);
+    {
+        unsigned long long h = 0;
+        DSS_HIP(hipMemcpyAsync(&h, ncell, sizeof(h), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipStreamSynchronize(s));
+        idx->n_cells = (int64_t)h;
+    }
+    // (3) dense lookup over regular postings
     idx->n_dense = 0;
     idx->kmin = 0;
     if (n_reg > 0) {
@@ -733,71 +866,129 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
         idx->dense.ensure(2);
         DSS_HIP(hipMemsetAsync(idx->dense.p, 0, 2 * sizeof(uint32_t), s));
     }
-    // irregular side table
+    // (4) irregular side table
     idx->n_irr = 0;
-    uint32_t *irr_start = nullptr;
     if (n_irr_p > 0) {
         DevBuf<int64_t> fl, fp;
         int64_t *f = fl.ensure(n_irr_p + 1), *fpo = fp.ensure(n_irr_p + 2);
         hipLaunchKernelGGL(k_irr_runs, dim3(grid_for(n_irr_p, kBlock)), dim3(kBlock), 0, s, n_irr_p, p_cell + n_reg, f);
         exclusive_scan_i64(f, fpo, n_irr_p, tmp_, s);
-        int64_t nu = 0;
-        DSS_HIP(hipMemcpyAsync(&nu, fpo + n_irr_p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        DSS_HIP(hipStreamSynchronize(s));
+        const int64_t nu = fetch_i64(fpo + n_irr_p, s);
         idx->n_irr = nu;
         uint64_t *ic = idx->irr_cells.ensure(nu + 1);
-        irr_start = idx->irr_start.ensure(nu + 1);
+        uint32_t *irr_start = idx->irr_start.ensure(nu + 1);
         hipLaunchKernelGGL(k_irr_scatter, dim3(grid_for(n_irr_p, kBlock)), dim3(kBlock), 0, s, n_irr_p, p_cell + n_reg, f, fpo,
                            n_reg, ic, irr_start);
         uint32_t endv = (uint32_t)Pu;
         DSS_HIP(hipMemcpyAsync(irr_start + nu, &endv, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        DSS_HIP(hipStreamSynchronize(s));
     } else {
         idx->irr_cells.ensure(1);
         idx->irr_start.ensure(1);
     }
-    DSS_HIP(hipStreamSynchronize(s));
+    const int64_t n_slots = idx->n_dense + idx->n_irr;
+    // (5) time buckets over the span of the rows that can match
+    {
+        DevBuf<unsigned long long> mmb;
+        unsigned long long *mm = mmb.ensure(2), hmm[2] = {~0ull, 0ull};
+        DSS_HIP(hipMemcpyAsync(mm, hmm, sizeof(hmm), hipMemcpyHostToDevice, s));
+        if (n) {
+            unsigned g = grid_for(n, kBlock);
+            hipLaunchKernelGGL(k_time_range, dim3(g < 1024 ? g : 1024), dim3(kBlock), 0, s, n, t0, t1, mm);
+        }
+        DSS_HIP(hipMemcpyAsync(hmm, mm, sizeof(hmm), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipStreamSynchronize(s));
+        idx->tbase = 0;
+        idx->shift = 0;
+        idx->nb = 1;
+        if (hmm[1] != 0) {  // some row can match
+            const long long tmax = (long long)(hmm[1] ^ 0x8000000000000000ull);
+            const long long tmin = hmm[0] == ~0ull ? tmax : (long long)(hmm[0] ^ 0x8000000000000000ull);
+            const unsigned long long span = tmax > tmin ? (unsigned long long)tmax - (unsigned long long)tmin : 0;
+            int sh = 0;
+            while ((span >> sh) >= (unsigned long long)kMaxBuckets) sh++;
+            idx->tbase = tmin;
+            idx->shift = sh;
+            idx->nb = (int)(span >> sh) + 1;
+        }
+    }
+    const Buckets bk{idx->tbase, idx->shift, idx->nb};
+    // (6) bucketed postings
+    const IndexView pv = view_of(idx);
+    DevBuf<uint32_t> ps_buf;
+    uint32_t *pslot = ps_buf.ensure(Pu + 1);
+    if (Pu) hipLaunchKernelGGL(k_plain_slot, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, p_cell, pv, pslot);
+    int64_t *bcnt = c0_.ensure(Pu + 1), *boff = c1_.ensure(Pu + 2);
+    if (Pu)
+        hipLaunchKernelGGL(k_bucket_copies<0>, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, p_e, pslot, t0, t1, bk,
+                           bcnt, nullptr, nullptr, nullptr);
+    exclusive_scan_i64(bcnt, boff, Pu, tmp_, s);
+    const int64_t NB = fetch_i64(boff + Pu, s);
+    if (NB >= (int64_t)0x7fffffff) throw Error(DSSG_ERR_INVALID, "index: more than 2^31 bucketed postings per device");
+    idx->n_b = NB;
+    uint64_t *bk0 = k0_.ensure(NB + 1), *bk1 = k1_.ensure(NB + 1);
+    uint32_t *bv0 = v0_.ensure(NB + 1), *bv1 = v1_.ensure(NB + 1);
+    if (Pu)
+        hipLaunchKernelGGL(k_bucket_copies<1>, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, p_e, pslot, t0, t1, bk,
+                           nullptr, boff, bk0, bv0);
+    sort_pairs(bk0, bk1, bv0, bv1, NB, bits_for(n_slots) + 6, tmp_, s);
+    uint32_t *b_e = idx->b_e.ensure(NB + 1);
+    float2 *b_alt = idx->b_alt.ensure(NB + 1);
+    longlong2 *b_t = idx->b_t.ensure(NB + 1);
+    uint8_t *b_meta = idx->b_meta.ensure(NB + 1);
+    ulonglong2 *b_sig = idx->b_sig.ensure(2 * (NB + 1));
+    int32_t *b_owner = idx->b_owner.ensure(owner ? NB + 1 : 1);
+    if (NB)
+        hipLaunchKernelGGL(k_bucket_gather, dim3(grid_for(NB, kBlock)), dim3(kBlock), 0, s, NB, bv1, p_cell, p_e, e_offs,
+                           e_cells, alt_lo, alt_hi, t0, t1, owner, bk, b_e, b_alt, b_t, b_meta, b_sig, b_owner);
+    // (7) groups = runs of equal (slot, bucket)
+    unsigned long long *s_mask = idx->s_mask.ensure(n_slots + 1);
+    DSS_HIP(hipMemsetAsync(s_mask, 0, sizeof(unsigned long long) * (n_slots + 1), s));
+    int64_t ng = 0;
+    if (NB) {
+        uint64_t *gkey = bk0;  // reuse
+        int64_t *gcnt = c0_.ensure(NB + 1), *ngd = c1_.ensure(2);
+        size_t bytes = 0;
+        DSS_HIP(hipcub::DeviceRunLengthEncode::Encode(nullptr, bytes, bk1, gkey, gcnt, ngd, (int)NB, s));
+        tmp_.ensure(bytes + 16);
+        DSS_HIP(hipcub::DeviceRunLengthEncode::Encode(tmp_.p, bytes, bk1, gkey, gcnt, ngd, (int)NB, s));
+        ng = fetch_i64(ngd, s);
+        DevBuf<int64_t> gs;
+        int64_t *gst = gs.ensure(ng + 2);
+        exclusive_scan_i64(gcnt, gst, ng, tmp_, s);
+        uint32_t *bk_start = idx->bk_start.ensure(ng + 1);
+        hipLaunchKernelGGL(k_i64_to_u32, dim3(grid_for(ng + 1, kBlock)), dim3(kBlock), 0, s, ng + 1, gst, bk_start);
+        hipLaunchKernelGGL(k_group_mask, dim3(grid_for(ng, kBlock)), dim3(kBlock), 0, s, ng, gkey, s_mask);
+        DSS_HIP(hipStreamSynchronize(s));
+    } else {
+        idx->bk_start.ensure(1);
+        DSS_HIP(hipMemsetAsync(idx->bk_start.p, 0, sizeof(uint32_t), s));
+    }
+    {
+        DevBuf<int64_t> pc, po;
+        int64_t *pcnt = pc.ensure(n_slots + 1), *poff = po.ensure(n_slots + 2);
+        if (n_slots)
+            hipLaunchKernelGGL(k_slot_pop, dim3(grid_for(n_slots, kBlock)), dim3(kBlock), 0, s, n_slots, s_mask, pcnt);
+        exclusive_scan_i64(pcnt, poff, n_slots, tmp_, s);
+        uint32_t *s_base = idx->s_base.ensure(n_slots + 1);
+        hipLaunchKernelGGL(k_i64_to_u32, dim3(grid_for(n_slots + 1, kBlock)), dim3(kBlock), 0, s, n_slots + 1, poff, s_base);
+        DSS_HIP(hipStreamSynchronize(s));
+    }
 }
 
-// ---------------------------------------------------------------- search
-static JoinArgs make_args(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
-                          const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
-                          const int32_t *q_owner)
-{
-    JoinArgs a{};
-    a.nq = nq; a.q_offs = q_offs; a.q_cells = q_cells; a.q_alo = q_alt_lo; a.q_ahi = q_alt_hi;
-    a.q_tlo = q_tlo; a.q_thi = q_thi; a.q_owner = q_owner;
-    a.p_e = idx->p_e.p; a.p_alt = idx->p_alt.p; a.p_t = idx->p_t.p; a.p_owner = idx->p_owner.p;
-    a.e_offs = idx->e_offs.p; a.e_cells = idx->e_cells.p;
-    a.kmin = idx->kmin; a.n_dense = idx->n_dense; a.dense = idx->dense.p;
-    a.n_irr = idx->n_irr; a.irr_cells = idx->irr_cells.p; a.irr_start = idx->irr_start.p;
-    return a;
-}
-
+// ================================================================== search
 void SearchEngine::stats(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells, hipStream_t s,
                          int64_t *matched, int64_t *distinct)
 {
     unsigned long long *cnt = counter_.ensure(4);
     DSS_HIP(hipMemsetAsync(cnt, 0, 4 * sizeof(unsigned long long), s));
-    JoinArgs a = make_args(idx, nq, q_offs, q_cells, nullptr, nullptr, nullptr, nullptr, nullptr);
-    // the predicate reads are skipped in stats mode; give the kernel valid
-    // (unused) query attribute pointers anyway
-    DevBuf<float> fz;
-    DevBuf<int64_t> iz;
-    float *f = fz.ensure(nq + 1);
-    int64_t *t = iz.ensure(nq + 1);
-    DSS_HIP(hipMemsetAsync(f, 0, sizeof(float) * (nq + 1), s));
-    DSS_HIP(hipMemsetAsync(t, 0, sizeof(int64_t) * (nq + 1), s));
-    a.q_alo = f; a.q_ahi = f; a.q_tlo = t; a.q_thi = t;
-    a.stats = 1;
-    a.stat_m = cnt + 1;
-    a.stat_d = cnt + 2;
-    a.counter = cnt;
-    if (nq > 0) hipLaunchKernelGGL(k_join, dim3(grid_for(nq, kBlock / 64)), dim3(kBlock), 0, s, a);
+    QueryView qv{nq, q_offs, q_cells, nullptr, nullptr, nullptr, nullptr, nullptr};
+    if (nq > 0) hipLaunchKernelGGL(k_stats, dim3(grid_for(nq, kBlock / 64)), dim3(kBlock), 0, s, view_of(idx), qv, cnt);
     unsigned long long h[4];
     DSS_HIP(hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
-    *matched = (int64_t)h[1];
-    *distinct = (int64_t)h[2];
+    *matched = (int64_t)h[0];
+    *distinct = (int64_t)h[1];
 }
 
 void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
@@ -805,69 +996,85 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
                           const int32_t *q_owner, hipStream_t s, dssg_pairs *out)
 {
     if (q_owner && !idx->has_owner) throw Error(DSSG_ERR_INVALID, "search by owner on an index built without owners");
-    unsigned long long *counter = counter_.ensure(1);
-    JoinArgs a = make_args(idx, nq, q_offs, q_cells, q_alt_lo, q_alt_hi, q_tlo, q_thi, q_owner);
-    if (timing_) {
-        if (!ev0_) { DSS_HIP(hipEventCreate(&ev0_)); DSS_HIP(hipEventCreate(&ev1_)); }
+    if (nq >= (int64_t)kCompact) throw Error(DSSG_ERR_INVALID, "search: more than 2^30 queries per batch");
+    if (timing_ && !ev0_) {
+        DSS_HIP(hipEventCreate(&ev0_));
+        DSS_HIP(hipEventCreate(&ev1_));
     }
-    // (1) (slot, query) pairs for every query cell that has postings
-    int64_t *qcnt = c0_.ensure(nq + 1), *qoff = c1_.ensure(nq + 2);
-    if (nq > 0) hipLaunchKernelGGL(k_qc<0>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, a, qcnt, nullptr, nullptr, nullptr);
-    exclusive_scan_i64(qcnt, qoff, nq, tmp_, s);
-    int64_t npairs = 0;
-    DSS_HIP(hipMemcpyAsync(&npairs, qoff + nq, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    DSS_HIP(hipStreamSynchronize(s));
-    if (npairs == 0) {
+    const IndexView ix = view_of(idx);
+    const QueryView qv{nq, q_offs, q_cells, q_alt_lo, q_alt_hi, q_tlo, q_thi, q_owner};
+    auto empty = [&]() {
         out->q = oq_.ensure(1);
         out->e = oe_.ensure(1);
         out->n = 0;
-        return;
-    }
-    uint32_t *key = v0_.ensure(npairs + 1), *val = v1_.ensure(npairs + 1);
-    uint32_t *skey = sk_.ensure(npairs + 1), *sval = sv_.ensure(npairs + 1);
-    hipLaunchKernelGGL(k_qc<1>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, a, nullptr, qoff, key, val);
-    // (2) group by slot (stable: query order kept within a slot)
-    int64_t nslots = idx->n_dense + idx->n_irr;
-    int bits = 1;
-    while (bits < 32 && ((int64_t)1 << bits) <= nslots) bits++;
+        units_ = keys_ = 0;
+        join_ms_ = 0;
+    };
+    if (nq <= 0 || idx->n_b == 0) return empty();
+    // (1) keys (slot << 6 | bucket) for every group a query cell meets
+    int64_t *qcnt = c0_.ensure(nq + 1), *qoff = c1_.ensure(nq + 2);
+    hipLaunchKernelGGL(k_qkeys<0>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, ix, qv, qcnt, nullptr, nullptr, nullptr);
+    exclusive_scan_i64(qcnt, qoff, nq, tmp_, s);
+    const int64_t nkeys = fetch_i64(qoff + nq, s);
+    keys_ = nkeys;
+    if (nkeys == 0) return empty();
+    if (nkeys >= (int64_t)0x7fffffff) throw Error(DSSG_ERR_CAPACITY, "search: more than 2^31 (cell, bucket) keys per batch");
+    uint64_t *key = k0_.ensure(nkeys + 1), *skey = k1_.ensure(nkeys + 1);
+    uint32_t *val = v0_.ensure(nkeys + 1), *sval = v1_.ensure(nkeys + 1);
+    hipLaunchKernelGGL(k_qkeys<1>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, ix, qv, nullptr, qoff, key, val);
+    // (2) group by key (stable: query order kept within a group)
+    sort_pairs(key, skey, val, sval, nkeys, bits_for(idx->n_dense + idx->n_irr) + 6, tmp_, s);
+    uint64_t *ukey = uk_.ensure(nkeys + 1);
+    int64_t *rcnt = rc_.ensure(nkeys + 1), *rstart = rs_.ensure(nkeys + 2), *nruns_d = nr_.ensure(2);
     size_t bytes = 0;
-    DSS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, key, skey, val, sval, (int)npairs, 0, bits, s));
+    DSS_HIP(hipcub::DeviceRunLengthEncode::Encode(nullptr, bytes, skey, ukey, rcnt, nruns_d, (int)nkeys, s));
     tmp_.ensure(bytes + 16);
-    DSS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_.p, bytes, key, skey, val, sval, (int)npairs, 0, bits, s));
-    // (3) runs of equal slots
-    uint32_t *ukey = uk_.ensure(npairs + 1);
-    int64_t *rcnt = rc_.ensure(npairs + 1), *rstart = rs_.ensure(npairs + 2);
-    int64_t *nruns_d = nr_.ensure(2);
-    bytes = 0;
-    DSS_HIP(hipcub::DeviceRunLengthEncode::Encode(nullptr, bytes, skey, ukey, rcnt, nruns_d, (int)npairs, s));
-    tmp_.ensure(bytes + 16);
-    DSS_HIP(hipcub::DeviceRunLengthEncode::Encode(tmp_.p, bytes, skey, ukey, rcnt, nruns_d, (int)npairs, s));
-    int64_t nruns = 0;
-    DSS_HIP(hipMemcpyAsync(&nruns, nruns_d, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    DSS_HIP(hipStreamSynchronize(s));
+    DSS_HIP(hipcub::DeviceRunLengthEncode::Encode(tmp_.p, bytes, skey, ukey, rcnt, nruns_d, (int)nkeys, s));
+    // query records (independent of the run boundaries)
+    QRec *recs = (QRec *)rec_.ensure(sizeof(QRec) * (nkeys + 1));
+    hipLaunchKernelGGL(k_qrec, dim3(grid_for(nkeys, kBlock)), dim3(kBlock), 0, s, nkeys, ix, qv, skey, sval, recs);
+    const int64_t nruns = fetch_i64(nruns_d, s);
     exclusive_scan_i64(rcnt, rstart, nruns, tmp_, s);
-    // (4) tiles
-    int64_t *tcnt = tc_.ensure(nruns + 1), *toff = to_.ensure(nruns + 2);
-    hipLaunchKernelGGL(k_tiles<0>, dim3(grid_for(nruns, kBlock)), dim3(kBlock), 0, s, nruns, a, ukey, rstart, tcnt, nullptr,
+    // (3) join units
+    int64_t *ucnt = uc_.ensure(nruns + 1), *uoff = uo_.ensure(nruns + 2);
+    hipLaunchKernelGGL(k_units<0>, dim3(grid_for(nruns, kBlock)), dim3(kBlock), 0, s, nruns, ix, ukey, rstart, ucnt, nullptr,
                        nullptr, nullptr, nullptr);
-    exclusive_scan_i64(tcnt, toff, nruns, tmp_, s);
-    int64_t ntiles = 0;
-    DSS_HIP(hipMemcpyAsync(&ntiles, toff + nruns, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    DSS_HIP(hipStreamSynchronize(s));
-    uint32_t *t_run = tr_.ensure(ntiles + 1), *t_p = tp_.ensure(ntiles + 1), *t_q = tq_.ensure(ntiles + 1);
-    hipLaunchKernelGGL(k_tiles<1>, dim3(grid_for(nruns, kBlock)), dim3(kBlock), 0, s, nruns, a, ukey, rstart, nullptr, toff,
-                       t_run, t_p, t_q);
-    // (5) join tiles; grow the output and rerun if the guess was too small
-    if (out_cap_ == 0) out_cap_ = (size_t)(nq > 0 ? nq : 1) * 16 + 1024;
+    exclusive_scan_i64(ucnt, uoff, nruns, tmp_, s);
+    const int64_t nunits = fetch_i64(uoff + nruns, s);
+    units_ = nunits;
+    if (timing_) {
+        unsigned long long *st = counter_.ensure(4) + 2;
+        DSS_HIP(hipMemsetAsync(st, 0, 2 * sizeof(unsigned long long), s));
+        hipLaunchKernelGGL(k_work_stats, dim3(grid_for(nruns, kBlock)), dim3(kBlock), 0, s, nruns, ix, ukey, rstart, st);
+        unsigned long long h[2];
+        DSS_HIP(hipMemcpyAsync(h, st, sizeof(h), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipStreamSynchronize(s));
+        iters_ = (int64_t)h[0];
+        tests_ = (int64_t)h[1];
+        runs_ = nruns;
+    }
+    if (nunits >= (int64_t)0xffffffffll * kWaves) throw Error(DSSG_ERR_CAPACITY, "search: too many join units");
+    uint32_t *u_run = ur_.ensure(nunits + 1), *u_pt = up_.ensure(nunits + 1), *u_qt = uq_.ensure(nunits + 1);
+    hipLaunchKernelGGL(k_units<1>, dim3(grid_for(nruns, kBlock)), dim3(kBlock), 0, s, nruns, ix, ukey, rstart, nullptr, uoff,
+                       u_run, u_pt, u_qt);
+    // (4) join; grow the output and rerun if the guess was too small
+    JoinArgs ja{};
+    ja.ix = ix;
+    ja.qv = qv;
+    ja.nunits = nunits;
+    ja.ukey = ukey;
+    ja.rstart = rstart;
+    unsigned long long *counter = counter_.ensure(1);
+    if (out_cap_ == 0) out_cap_ = (size_t)nq * 16 + 1024;
+    const unsigned nblocks = (unsigned)((nunits + kWaves - 1) / kWaves);
     for (int attempt = 0; attempt < 3; attempt++) {
         uint32_t *oq = oq_.ensure(out_cap_), *oe = oe_.ensure(out_cap_);
         DSS_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned long long), s));
-        a.out_q = oq;
-        a.out_e = oe;
-        a.counter = counter;
-        a.cap = (int64_t)out_cap_;
+        ja.cap = (int64_t)out_cap_;
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
-        hipLaunchKernelGGL(k_join_tile, dim3((unsigned)ntiles), dim3(kTileP), 0, s, a, ukey, rstart, sval, t_run, t_p, t_q);
+        if (nblocks)
+            hipLaunchKernelGGL(k_join, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs, (const uint32_t *)u_run,
+                               (const uint32_t *)u_pt, (const uint32_t *)u_qt, oq, oe, counter);
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
         unsigned long long total = 0;
         DSS_HIP(hipMemcpyAsync(&total, counter, sizeof(total), hipMemcpyDeviceToHost, s));

@@ -5,25 +5,42 @@
 struct dssg_index {
     int64_t n_e = 0;      // entities
     int64_t n_p = 0;      // unique (cell, entity) postings
-    int64_t n_reg = 0;    // postings whose cell is a valid level-13 id (dense lookup)
+    int64_t n_reg = 0;    // of which on valid level-13 cells (dense lookup)
+    int64_t n_cells = 0;  // distinct cells
+    int64_t n_b = 0;      // time-bucketed postings (the join's working set)
     bool has_owner = false;
-    // postings sorted by (cell, entity); regular first, irregular after
+    // ---- plain postings, sorted by (cell, entity); regular first -------------
+    // A cell's "slot" is its dense slot (level-13 cells) or n_dense + its index
+    // in the irregular side table.
     dss::DevBuf<uint64_t> p_cell;
-    dss::DevBuf<uint32_t> p_e;      // bit 31: "cell is the entity's smallest cell"
-    dss::DevBuf<float2> p_alt;      // (alt_lo, alt_hi)
-    dss::DevBuf<longlong2> p_t;     // (t0, t1) microseconds
-    dss::DevBuf<int32_t> p_owner;
-    // entity -> sorted unique cells (canonical-cell dedupe)
+    dss::DevBuf<uint32_t> p_e;  // bit 31: the cell is the entity's smallest cell
+    uint64_t kmin = 0;          // dense slot k <-> cell (kmin + k) << 35 | 1 << 34
+    int64_t n_dense = 0;
+    dss::DevBuf<uint32_t> dense;  // n_dense + 1 plain posting offsets
+    int64_t n_irr = 0;
+    dss::DevBuf<uint64_t> irr_cells;  // sorted, n_irr
+    dss::DevBuf<uint32_t> irr_start;  // n_irr + 1, absolute plain offsets
+    // entity -> sorted unique cells (smallest-shared-cell rule)
     dss::DevBuf<int64_t> e_offs;
     dss::DevBuf<uint64_t> e_cells;
-    // dense lookup over level-13 cells: key k = cell >> 35 in [kmin, kmin + n_dense)
-    uint64_t kmin = 0;
-    int64_t n_dense = 0;              // slots; dense has n_dense + 1 entries
-    dss::DevBuf<uint32_t> dense;
-    // irregular cells (not level 13 / invalid face): sorted unique + starts
-    int64_t n_irr = 0;
-    dss::DevBuf<uint64_t> irr_cells;
-    dss::DevBuf<uint32_t> irr_start;  // n_irr + 1, absolute posting indices
+    // ---- time buckets ---------------------------------------------------------
+    // bucket(t) = clamp((t - tbase) >> shift, 0, nb - 1), nb <= 61; bucket 63
+    // holds, once, the entities spanning more than kLongSpan buckets.
+    int64_t tbase = 0;
+    int shift = 0;
+    int nb = 1;
+    // ---- bucketed postings, sorted by (slot, bucket, entity) -----------------
+    // Group g = one non-empty (slot, bucket); g = s_base[slot] +
+    // popcount(s_mask[slot] & ((1 << bucket) - 1)); postings [bk_start[g], bk_start[g+1]).
+    dss::DevBuf<unsigned long long> s_mask;  // n_slots
+    dss::DevBuf<uint32_t> s_base;            // n_slots + 1
+    dss::DevBuf<uint32_t> bk_start;          // n_groups + 1
+    dss::DevBuf<uint32_t> b_e;               // entity | first bit
+    dss::DevBuf<float2> b_alt;               // (alt_lo, alt_hi)
+    dss::DevBuf<longlong2> b_t;              // (t0, t1) microseconds
+    dss::DevBuf<uint8_t> b_meta;             // entity's first bucket | compact << 7
+    dss::DevBuf<ulonglong2> b_sig;           // 2 per posting: 256-bit prefix signature
+    dss::DevBuf<int32_t> b_owner;
     int device = 0;
 };
 
@@ -43,21 +60,28 @@ class SearchEngine {
                int64_t *matched, int64_t *distinct);
     void set_timing(bool on) { timing_ = on; }
     double last_join_kernel_ms() const { return join_ms_; }
+    int64_t last_units() const { return units_; }
+    int64_t last_keys() const { return keys_; }
+    // timing mode only: runs, wave iterations (records x tiles), useful lane tests
+    void last_work(int64_t *runs, int64_t *iters, int64_t *tests) const
+    {
+        *runs = runs_;
+        *iters = iters_;
+        *tests = tests_;
+    }
 
    private:
     DevBuf<unsigned char> tmp_;
-    DevBuf<uint64_t> k0_, k1_;
-    DevBuf<uint32_t> v0_, v1_;
-    DevBuf<int64_t> c0_, c1_;
-    DevBuf<uint8_t> fl_;
+    DevBuf<uint64_t> k0_, k1_, uk_;
+    DevBuf<uint32_t> v0_, v1_, ur_, up_, uq_;
+    DevBuf<int64_t> c0_, c1_, rc_, rs_, nr_, uc_, uo_;
     DevBuf<unsigned long long> counter_;
-    // tiled-join scratch
-    DevBuf<uint32_t> sk_, sv_, uk_, tr_, tp_, tq_;
-    DevBuf<int64_t> rc_, rs_, nr_, tc_, to_;
     DevBuf<uint32_t> oq_, oe_;
+    DevBuf<unsigned char> rec_;
     size_t out_cap_ = 0;
     bool timing_ = false;
     double join_ms_ = 0;
+    int64_t units_ = 0, keys_ = 0, runs_ = 0, iters_ = 0, tests_ = 0;
     hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
 };
 

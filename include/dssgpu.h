@@ -172,6 +172,13 @@ int dssg_search_subscriptions(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, 
  * phase, measured with HIP events on the launching stream (bench.py). */
 int dssg_phase_times(dssg_ctx *ctx, double *cover_ms, double *join_ms, double *join_kernel_ms);
 void dssg_set_timing(dssg_ctx *ctx, int enabled);
+/* Work counters of the most recent search: (cell, time bucket) keys sorted,
+ * join units (64 postings x <= 1024 query records) launched, and -- with
+ * timing enabled -- runs (non-empty groups met), wave iterations (records x
+ * 64-posting tiles) and useful lane tests (records x postings).  Any
+ * pointer may be NULL. */
+int dssg_search_counters(dssg_ctx *ctx, int64_t *keys, int64_t *units, int64_t *runs, int64_t *iters,
+                         int64_t *tests);
 /* Roofline accounting for a device query batch: total postings the join
  * scans (sum of M_q) and distinct candidate entities before the
  * altitude/time filter (sum of D_q), SURVEY.md s8(d). */
