@@ -42,7 +42,9 @@ constexpr int kLongSpan = 8;     // entities touching more buckets go to kLongBu
 constexpr int kMaxBuckets = 61;  // regular buckets 0..nb-1
 constexpr int kWaves = 4;        // join units per workgroup
 constexpr int kQChunk = 1024;    // query records per join unit
-constexpr int kStage = 256;      // pairs staged per wave in LDS
+constexpr int kStage = 512;      // pairs staged per wave in LDS
+constexpr int kGrab = 4;         // join units a persistent wave takes per queue access
+constexpr int kJoinBlocksPerCU = 5;  // LDS: 32 KiB per workgroup
 constexpr uint32_t kRank0 = 0x80000000u;    // record: the cell is the query's first cell
 constexpr uint32_t kCompact = 0x40000000u;  // record: the query's prefix is compact
 
@@ -473,17 +475,18 @@ __global__ void k_qkeys(IndexView a, QueryView qv, int64_t *cnt, const int64_t *
     if (!PASS) cnt[q] = n;
 }
 
-// Query record: what one predicate sweep needs, read with scalar loads.
+// Query record (one per sorted key): what one predicate sweep needs.
 struct alignas(64) QRec {
     long long tlo, thi;
     float alo, ahi;
-    uint32_t qv;  // query | kRank0 | kCompact
-    int32_t own;  // owner filter or -1
+    uint32_t qv;   // query | kRank0 | kCompact
+    int32_t bq0;   // first bucket of [min(tlo,thi), max(tlo,thi)]
     unsigned long long sig[4];
 };
 static_assert(sizeof(QRec) == 64, "QRec layout");
 
-__global__ void k_qrec(int64_t n, IndexView a, QueryView qv, const uint64_t *skey, const uint32_t *sval, QRec *recs)
+__global__ void k_qrec(int64_t n, IndexView a, QueryView qv, const uint64_t *skey, const uint32_t *sval, QRec *recs,
+                       int32_t *rown)
 {
     int64_t j = tid64();
     if (j >= n) return;
@@ -494,7 +497,8 @@ __global__ void k_qrec(int64_t n, IndexView a, QueryView qv, const uint64_t *ske
     r.thi = qv.thi[q];
     r.alo = qv.alo[q];
     r.ahi = qv.ahi[q];
-    r.own = qv.owner ? qv.owner[q] : -1;
+    r.bq0 = bucket_of(r.tlo < r.thi ? r.tlo : r.thi, a.bk);
+    if (rown) rown[j] = qv.owner[q];
     Sig256 sig;
     bool compact = false;
     if (!(v & kRank0)) {
@@ -518,7 +522,13 @@ __device__ __forceinline__ uint32_t group_of(const IndexView &a, uint64_t key)
     return a.s_base[slot] + (uint32_t)__popcll(a.s_mask[slot] & ((1ull << b) - 1ull));
 }
 
-// (2) join units: (run, 64-posting tile, kQChunk-query chunk)
+// Postings per lane in a join unit: a unit covers up to 64 * kSlots postings
+// of one group, so a typical group (SURVEY config 1: ~75 postings) is one unit
+// and each broadcast record is tested against all of it.
+constexpr int kSlots = 2;
+
+// (2) join units: (run, tile of <= 64 * kSlots postings, kQChunk-record chunk).
+// u_pt = tile | (slots - 1) << 28.
 template <int PASS>
 __global__ void k_units(int64_t nruns, IndexView a, const uint64_t *ukey, const int64_t *rstart, int64_t *cnt,
                         const int64_t *uoff, uint32_t *u_run, uint32_t *u_pt, uint32_t *u_qt)
@@ -528,7 +538,8 @@ __global__ void k_units(int64_t nruns, IndexView a, const uint64_t *ukey, const 
     const uint32_t g = group_of(a, ukey[r]);
     const int64_t np = (int64_t)a.bk_start[g + 1] - a.bk_start[g];
     const int64_t nq = rstart[r + 1] - rstart[r];
-    const int64_t tp = (np + 63) / 64, tq = (nq + kQChunk - 1) / kQChunk;
+    const int64_t k = min((int64_t)kSlots, max((int64_t)1, (np + 63) / 64));
+    const int64_t tp = (np + 64 * k - 1) / (64 * k), tq = (nq + kQChunk - 1) / kQChunk;
     if (!PASS) {
         cnt[r] = tp * tq;
         return;
@@ -537,14 +548,14 @@ __global__ void k_units(int64_t nruns, IndexView a, const uint64_t *ukey, const 
     for (int64_t i = 0; i < tp; i++)
         for (int64_t j = 0; j < tq; j++, w++) {
             u_run[w] = (uint32_t)r;
-            u_pt[w] = (uint32_t)i;
+            u_pt[w] = (uint32_t)i | (uint32_t)(k - 1) << 28;
             u_qt[w] = (uint32_t)j;
         }
 }
 
-// Diagnostics (timing mode): sum over runs of records x 64-posting tiles
-// (wave iterations before the time pre-filter) and of records x postings
-// (useful lane tests).
+// Diagnostics (timing mode): sum over runs of records x tiles (wave
+// iterations before the time pre-filter) and of records x postings (useful
+// lane tests).
 __global__ void k_work_stats(int64_t nruns, IndexView a, const uint64_t *ukey, const int64_t *rstart,
                              unsigned long long *stat)
 {
@@ -554,7 +565,8 @@ __global__ void k_work_stats(int64_t nruns, IndexView a, const uint64_t *ukey, c
         const uint32_t g = group_of(a, ukey[r]);
         const unsigned long long np = a.bk_start[g + 1] - a.bk_start[g];
         const unsigned long long nq = (unsigned long long)(rstart[r + 1] - rstart[r]);
-        it = nq * ((np + 63) / 64);
+        const unsigned long long k = np > 64 ? kSlots : 1;
+        it = nq * ((np + 64 * k - 1) / (64 * k));
         lt = nq * np;
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -576,58 +588,59 @@ struct JoinArgs {
     int64_t cap;
 };
 
-// (3) one wavefront per unit; 64 postings in lanes, query records uniform.
-// Pointers passed apart and __restrict__ so that the uniform record and unit
-// loads compile to scalar (s_load) loads.
-__global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__restrict__ recs,
-                                                      const uint32_t *__restrict__ u_run, const uint32_t *__restrict__ u_pt,
-                                                      const uint32_t *__restrict__ u_qt, uint32_t *__restrict__ out_q,
-                                                      uint32_t *__restrict__ out_e, unsigned long long *__restrict__ counter)
+// One posting held by a lane.
+struct Slot {
+    bool valid, first, compact;
+    uint32_t ent;
+    int be0;
+    float2 alt;
+    longlong2 t;
+    int32_t own;
+    ulonglong2 s01, s23;
+};
+
+__device__ __forceinline__ void load_slot(const IndexView &ix, uint32_t p, uint32_t pe, bool owner, Slot &s)
 {
+    s.valid = p < pe;
+    s.first = s.compact = false;
+    s.ent = 0;
+    s.be0 = 0;
+    s.alt = make_float2(0.f, 0.f);
+    s.t = make_longlong2(LLONG_MAX, LLONG_MIN);  // matches nothing
+    s.own = 0;
+    s.s01 = s.s23 = make_ulonglong2(0, 0);
+    if (!s.valid) return;
+    const uint32_t v = ix.b_e[p];
+    const uint8_t m = ix.b_meta[p];
+    s.ent = v & ~kFirstBit;
+    s.first = (v & kFirstBit) != 0;
+    s.be0 = m & 0x3f;
+    s.compact = (m & 0x80) != 0;
+    s.alt = ix.b_alt[p];
+    s.t = ix.b_t[p];
+    if (owner) s.own = ix.b_owner[p];
+    if (!s.first) {
+        s.s01 = ix.b_sig[2 * (size_t)p];
+        s.s23 = ix.b_sig[2 * (size_t)p + 1];
+    }
+}
+
+// (3) one wavefront per unit: up to 64 * kSlots postings in registers, the
+// unit's query records staged through LDS 64 at a time and broadcast.
+template <bool OWNER>
+__global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__restrict__ recs,
+                                                      const int32_t *__restrict__ rown, const uint32_t *__restrict__ u_run,
+                                                      const uint32_t *__restrict__ u_pt, const uint32_t *__restrict__ u_qt,
+                                                      uint32_t *__restrict__ out_q, uint32_t *__restrict__ out_e,
+                                                      unsigned long long *__restrict__ counter,
+                                                      uint32_t *__restrict__ work)
+{
+    __shared__ int4 s_rec[kWaves][4][64];  // 64-byte records, split in 16-byte columns
+    __shared__ int32_t s_own[kWaves][OWNER ? 64 : 1];
     __shared__ uint32_t sq[kWaves][kStage];
     __shared__ uint32_t se[kWaves][kStage];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t u = (int64_t)blockIdx.x * kWaves + w;
-    if (u >= a.nunits) return;
-    const IndexView &ix = a.ix;
-    const uint32_t r = u_run[u];
-    const uint64_t key = a.ukey[r];
-    const int b = (int)(key & 63);
-    const uint32_t g = group_of(ix, key);
-    const uint32_t gs = ix.bk_start[g], ge = ix.bk_start[g + 1];
-    const uint32_t p = gs + u_pt[u] * 64u + (uint32_t)lane;
-    const bool valid = p < ge;
-    uint32_t pev = 0;
-    float2 alt = make_float2(0.f, 0.f);
-    longlong2 t = make_longlong2(0, 0);
-    int32_t pown = 0;
-    uint8_t meta = 0;
-    ulonglong2 s01 = make_ulonglong2(0, 0), s23 = make_ulonglong2(0, 0);
-    if (valid) {
-        pev = ix.b_e[p];
-        alt = ix.b_alt[p];
-        t = ix.b_t[p];
-        meta = ix.b_meta[p];
-        if (ix.b_owner) pown = ix.b_owner[p];
-        if (!(pev & kFirstBit)) {
-            s01 = ix.b_sig[2 * (size_t)p];
-            s23 = ix.b_sig[2 * (size_t)p + 1];
-        }
-    }
-    const uint32_t ent = pev & ~kFirstBit;
-    const bool efirst = (pev & kFirstBit) != 0;
-    const int be0 = meta & 0x3f;
-    const bool ecompact = (meta & 0x80) != 0;
-    // time bounds of the unit: records whose window misses all 64 are skipped
-    long long tmin = valid ? t.x : LLONG_MAX, tmax = valid ? t.y : LLONG_MIN;
-    for (int o = 32; o > 0; o >>= 1) {
-        tmin = min(tmin, __shfl_xor(tmin, o));
-        tmax = max(tmax, __shfl_xor(tmax, o));
-    }
-    const uint64_t cell = cell_of_slot(ix, (uint32_t)(key >> 6));
-    const int64_t k0 = a.rstart[r] + (int64_t)u_qt[u] * kQChunk;
-    const int64_t k1 = min(a.rstart[r + 1], k0 + kQChunk);
     int staged = 0;
     auto flush = [&]() {
         __builtin_amdgcn_wave_barrier();
@@ -644,76 +657,138 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
         staged = 0;
         __builtin_amdgcn_wave_barrier();
     };
-    // Records are fetched 64 at a time, one per lane (coalesced 16-byte loads
-    // instead of a serial chain of scalar loads), pre-filtered against the
-    // unit's time bounds with one ballot, and broadcast with readlane.
-    const int4 *rec4 = reinterpret_cast<const int4 *>(recs);
-    for (int64_t base = k0; base < k1; base += 64) {
-        const int64_t kk = base + lane;
-        int4 r0 = make_int4(0, 0, 0, 0), r1 = r0, r2 = r0, r3 = r0;
-        bool rel = false;
-        int rbq0 = 0;
-        if (kk < k1) {
-            r0 = rec4[4 * kk];
-            r1 = rec4[4 * kk + 1];
-            r2 = rec4[4 * kk + 2];
-            r3 = rec4[4 * kk + 3];
-            const long long tlo = ((long long)r0.y << 32) | (uint32_t)r0.x;
-            const long long thi = ((long long)r0.w << 32) | (uint32_t)r0.z;
-            rel = !(tmax < tlo || tmin > thi);  // else no posting of the unit can match
-            rbq0 = bucket_of(tlo < thi ? tlo : thi, ix.bk);
-        }
-        unsigned long long todo = __ballot(rel);
-        while (todo) {
-            const int j = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            const long long tlo = ((long long)__builtin_amdgcn_readlane(r0.y, j) << 32) |
-                                  (uint32_t)__builtin_amdgcn_readlane(r0.x, j);
-            const long long thi = ((long long)__builtin_amdgcn_readlane(r0.w, j) << 32) |
-                                  (uint32_t)__builtin_amdgcn_readlane(r0.z, j);
-            const float alo = __int_as_float(__builtin_amdgcn_readlane(r1.x, j));
-            const float ahi = __int_as_float(__builtin_amdgcn_readlane(r1.y, j));
-            const uint32_t qv = (uint32_t)__builtin_amdgcn_readlane(r1.z, j);
-            const int32_t own = __builtin_amdgcn_readlane(r1.w, j);
-            // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels)
-            bool pass = valid && t.y >= tlo && t.x <= thi && alt.y >= alo && alt.x <= ahi;
-            if (own >= 0) pass = pass && pown == own;
-            // keep the pair only in its first common bucket ...
-            if (b != kLongBucket) {
-                const int bq0 = __builtin_amdgcn_readlane(rbq0, j);
-                pass = pass && b == (bq0 > be0 ? bq0 : be0);
+    const IndexView &ix = a.ix;
+    // persistent waves: grab kGrab units at a time until the queue drains;
+    // the staging buffer carries over between units, so the output counter
+    // sees one atomic per kStage pairs
+    for (;;) {
+        uint32_t ub = 0;
+        if (lane == 0) ub = atomicAdd(work, (uint32_t)kGrab);
+        ub = __builtin_amdgcn_readfirstlane(__shfl(ub, 0));
+        if ((int64_t)ub >= a.nunits) break;
+        const uint32_t ue = (uint32_t)min((int64_t)ub + kGrab, a.nunits);
+        for (uint32_t u = ub; u < ue; u++) {
+            const uint32_t r = u_run[u];
+            const uint64_t key = a.ukey[r];
+            const int b = (int)(key & 63);
+            const uint32_t g = group_of(ix, key);
+            const uint32_t gs = ix.bk_start[g], ge = ix.bk_start[g + 1];
+            const uint32_t pt = u_pt[u];
+            const int nslot = (int)(pt >> 28) + 1;
+            const uint32_t p0 = gs + (pt & 0x0fffffffu) * 64u * (uint32_t)nslot + (uint32_t)lane;
+            Slot sl[kSlots];
+#pragma unroll
+            for (int k = 0; k < kSlots; k++) {
+                if (k < nslot) load_slot(ix, p0 + 64u * k, ge, OWNER, sl[k]);
+                else load_slot(ix, ge, ge, OWNER, sl[k]);
             }
-            // ... and at the smallest shared cell (SQL DISTINCT, Q13)
-            bool need = pass && !efirst && !(qv & kRank0);
-            if (__ballot(need)) {
-                const unsigned long long q0 = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(r2.y, j) << 32) |
-                                              (uint32_t)__builtin_amdgcn_readlane(r2.x, j);
-                const unsigned long long q1 = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(r2.w, j) << 32) |
-                                              (uint32_t)__builtin_amdgcn_readlane(r2.z, j);
-                const unsigned long long q2 = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(r3.y, j) << 32) |
-                                              (uint32_t)__builtin_amdgcn_readlane(r3.x, j);
-                const unsigned long long q3 = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(r3.w, j) << 32) |
-                                              (uint32_t)__builtin_amdgcn_readlane(r3.z, j);
-                if (need && ((s01.x & q0) | (s01.y & q1) | (s23.x & q2) | (s23.y & q3))) {
-                    if (ecompact && (qv & kCompact)) {
-                        pass = false;  // equal bits within +-7 cells: a shared smaller cell exists
-                    } else {
-                        const uint32_t q = qv & ~(kRank0 | kCompact);
-                        pass = no_smaller_shared(ix, ent, cell, a.qv.cells + a.qv.offs[q],
-                                                 a.qv.offs[q + 1] - a.qv.offs[q]);
+            // time bounds of the unit: records whose window misses all postings are skipped
+            long long tmin = LLONG_MAX, tmax = LLONG_MIN;
+#pragma unroll
+            for (int k = 0; k < kSlots; k++) {
+                tmin = min(tmin, sl[k].t.x);
+                tmax = max(tmax, sl[k].t.y);
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                tmin = min(tmin, __shfl_xor(tmin, o));
+                tmax = max(tmax, __shfl_xor(tmax, o));
+            }
+            const uint64_t cell = cell_of_slot(ix, (uint32_t)(key >> 6));
+            const int64_t k0 = a.rstart[r] + (int64_t)u_qt[u] * kQChunk;
+            const int64_t k1 = min(a.rstart[r + 1], k0 + kQChunk);
+            const int4 *rec4 = reinterpret_cast<const int4 *>(recs);
+            for (int64_t base = k0; base < k1; base += 64) {
+                const int64_t kk = base + lane;
+                bool rel = false;
+                __builtin_amdgcn_wave_barrier();
+                if (kk < k1) {
+                    const int4 c0 = rec4[4 * kk], c1 = rec4[4 * kk + 1], c2 = rec4[4 * kk + 2], c3 = rec4[4 * kk + 3];
+                    s_rec[w][0][lane] = c0;
+                    s_rec[w][1][lane] = c1;
+                    s_rec[w][2][lane] = c2;
+                    s_rec[w][3][lane] = c3;
+                    if (OWNER) s_own[w][lane] = rown[kk];
+                    const long long tlo = ((long long)c0.y << 32) | (uint32_t)c0.x;
+                    const long long thi = ((long long)c0.w << 32) | (uint32_t)c0.z;
+                    rel = !(tmax < tlo || tmin > thi);  // else no posting of the unit can match
+                }
+                __builtin_amdgcn_wave_barrier();
+                unsigned long long todo = __ballot(rel);
+                while (todo) {
+                    const int j = __builtin_ctzll(todo);
+                    todo &= todo - 1;
+                    const int4 c0 = s_rec[w][0][j], c1 = s_rec[w][1][j];
+                    const long long tlo = ((long long)c0.y << 32) | (uint32_t)c0.x;
+                    const long long thi = ((long long)c0.w << 32) | (uint32_t)c0.z;
+                    const float alo = __int_as_float(c1.x), ahi = __int_as_float(c1.y);
+                    const uint32_t qv = (uint32_t)c1.z;
+                    const int bq0 = c1.w;
+                    const int32_t own = OWNER ? s_own[w][j] : -1;
+                    const uint32_t q = qv & ~(kRank0 | kCompact);
+                    bool pass[kSlots];
+                    bool any_need = false;
+#pragma unroll
+                    for (int k = 0; k < kSlots; k++) {
+                        const Slot &s = sl[k];
+                        // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels),
+                        // evaluated branch-free (bitwise &, no short-circuit)
+                        bool p = (s.t.y >= tlo) & (s.t.x <= thi) & (s.alt.y >= alo) & (s.alt.x <= ahi);
+                        if (OWNER) p = p & ((own < 0) | (s.own == own));
+                        // keep the pair only in its first common bucket ...
+                        p = p & ((b == kLongBucket) | (b == max(bq0, s.be0)));
+                        pass[k] = p;
+                        any_need = any_need | (p & !s.first);
+                    }
+                    // ... and at the smallest shared cell (SQL DISTINCT, Q13)
+                    if (!(qv & kRank0) && __ballot(any_need)) {
+                        const int4 c2 = s_rec[w][2][j], c3 = s_rec[w][3][j];
+                        const unsigned long long q0 = ((unsigned long long)(uint32_t)c2.y << 32) | (uint32_t)c2.x;
+                        const unsigned long long q1 = ((unsigned long long)(uint32_t)c2.w << 32) | (uint32_t)c2.z;
+                        const unsigned long long q2 = ((unsigned long long)(uint32_t)c3.y << 32) | (uint32_t)c3.x;
+                        const unsigned long long q3 = ((unsigned long long)(uint32_t)c3.w << 32) | (uint32_t)c3.z;
+                        const bool qcompact = (qv & kCompact) != 0;
+                        bool ex[kSlots];
+                        bool any_ex = false;
+#pragma unroll
+                        for (int k = 0; k < kSlots; k++) {
+                            const Slot &s = sl[k];
+                            const bool ov = ((s.s01.x & q0) | (s.s01.y & q1) | (s.s23.x & q2) | (s.s23.y & q3)) != 0;
+                            const bool chk = pass[k] & !s.first & ov;
+                            const bool both = s.compact & qcompact;
+                            pass[k] = pass[k] & !(chk & both);  // equal bits within +-7 cells: a shared smaller cell exists
+                            ex[k] = chk & !both;                // signature inconclusive: merge the cell lists
+                            any_ex = any_ex | ex[k];
+                        }
+                        if (__ballot(any_ex)) {
+                            const uint64_t *qc = a.qv.cells + a.qv.offs[q];
+                            const int64_t nqc = a.qv.offs[q + 1] - a.qv.offs[q];
+#pragma unroll
+                            for (int k = 0; k < kSlots; k++)
+                                if (ex[k]) pass[k] = no_smaller_shared(ix, sl[k].ent, cell, qc, nqc);
+                        }
+                    }
+                    unsigned long long m[kSlots];
+                    int tot = 0;
+#pragma unroll
+                    for (int k = 0; k < kSlots; k++) {
+                        m[k] = __ballot(pass[k]);
+                        tot += __popcll(m[k]);
+                    }
+                    if (tot == 0) continue;
+                    if (staged + tot > kStage) flush();
+                    const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+                    for (int k = 0; k < kSlots; k++) {
+                        if (pass[k]) {
+                            const int rk = staged + __popcll(m[k] & below);
+                            sq[w][rk] = q;
+                            se[w][rk] = sl[k].ent;
+                        }
+                        staged += __popcll(m[k]);
                     }
                 }
             }
-            const unsigned long long m = __ballot(pass);
-            if (m == 0) continue;
-            const int nsurv = __popcll(m);
-            if (staged + nsurv > kStage) flush();
-            if (pass) {
-                const int rk = __popcll(m & ((1ull << lane) - 1ull));
-                sq[w][staged + rk] = qv & ~(kRank0 | kCompact);
-                se[w][staged + rk] = ent;
-            }
-            staged += nsurv;
+
         }
     }
     flush();
@@ -1032,7 +1107,8 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     DSS_HIP(hipcub::DeviceRunLengthEncode::Encode(tmp_.p, bytes, skey, ukey, rcnt, nruns_d, (int)nkeys, s));
     // query records (independent of the run boundaries)
     QRec *recs = (QRec *)rec_.ensure(sizeof(QRec) * (nkeys + 1));
-    hipLaunchKernelGGL(k_qrec, dim3(grid_for(nkeys, kBlock)), dim3(kBlock), 0, s, nkeys, ix, qv, skey, sval, recs);
+    int32_t *rown = q_owner ? (int32_t *)own_.ensure(nkeys + 1) : nullptr;
+    hipLaunchKernelGGL(k_qrec, dim3(grid_for(nkeys, kBlock)), dim3(kBlock), 0, s, nkeys, ix, qv, skey, sval, recs, rown);
     const int64_t nruns = fetch_i64(nruns_d, s);
     exclusive_scan_i64(rcnt, rstart, nruns, tmp_, s);
     // (3) join units
@@ -1053,7 +1129,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         tests_ = (int64_t)h[1];
         runs_ = nruns;
     }
-    if (nunits >= (int64_t)0xffffffffll * kWaves) throw Error(DSSG_ERR_CAPACITY, "search: too many join units");
+    if (nunits >= (int64_t)0xffffffffll - kGrab) throw Error(DSSG_ERR_CAPACITY, "search: too many join units");
     uint32_t *u_run = ur_.ensure(nunits + 1), *u_pt = up_.ensure(nunits + 1), *u_qt = uq_.ensure(nunits + 1);
     hipLaunchKernelGGL(k_units<1>, dim3(grid_for(nruns, kBlock)), dim3(kBlock), 0, s, nruns, ix, ukey, rstart, nullptr, uoff,
                        u_run, u_pt, u_qt);
@@ -1066,15 +1142,30 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     ja.rstart = rstart;
     unsigned long long *counter = counter_.ensure(1);
     if (out_cap_ == 0) out_cap_ = (size_t)nq * 16 + 1024;
-    const unsigned nblocks = (unsigned)((nunits + kWaves - 1) / kWaves);
+    // persistent grid: a few workgroups per CU (LDS-limited), units pulled from a queue
+    if (n_cu_ == 0) {
+        int dev = 0, ncu = 0;
+        DSS_HIP(hipGetDevice(&dev));
+        DSS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        n_cu_ = ncu > 0 ? ncu : 256;
+    }
+    const int64_t want = (nunits + kWaves - 1) / kWaves;
+    const unsigned nblocks = (unsigned)min(want, (int64_t)n_cu_ * kJoinBlocksPerCU);
+    uint32_t *work = work_.ensure(1);
     for (int attempt = 0; attempt < 3; attempt++) {
         uint32_t *oq = oq_.ensure(out_cap_), *oe = oe_.ensure(out_cap_);
         DSS_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned long long), s));
+        DSS_HIP(hipMemsetAsync(work, 0, sizeof(uint32_t), s));
         ja.cap = (int64_t)out_cap_;
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
-        if (nblocks)
-            hipLaunchKernelGGL(k_join, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs, (const uint32_t *)u_run,
-                               (const uint32_t *)u_pt, (const uint32_t *)u_qt, oq, oe, counter);
+        if (nblocks && q_owner)
+            hipLaunchKernelGGL(k_join<true>, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
+                               (const int32_t *)rown, (const uint32_t *)u_run, (const uint32_t *)u_pt, (const uint32_t *)u_qt,
+                               oq, oe, counter, work);
+        else if (nblocks)
+            hipLaunchKernelGGL(k_join<false>, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
+                               (const int32_t *)nullptr, (const uint32_t *)u_run, (const uint32_t *)u_pt,
+                               (const uint32_t *)u_qt, oq, oe, counter, work);
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
         unsigned long long total = 0;
         DSS_HIP(hipMemcpyAsync(&total, counter, sizeof(total), hipMemcpyDeviceToHost, s));

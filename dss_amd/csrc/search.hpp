@@ -78,6 +78,9 @@ class SearchEngine {
     DevBuf<unsigned long long> counter_;
     DevBuf<uint32_t> oq_, oe_;
     DevBuf<unsigned char> rec_;
+    DevBuf<int32_t> own_;
+    DevBuf<uint32_t> work_;
+    int n_cu_ = 0;
     size_t out_cap_ = 0;
     bool timing_ = false;
     double join_ms_ = 0;
