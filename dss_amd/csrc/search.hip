@@ -463,7 +463,7 @@ __global__ void k_qkeys(IndexView a, QueryView qv, int64_t *cnt, const int64_t *
             n += __popcll(m);
             continue;
         }
-        const uint32_t v = (uint32_t)q | (k == c0 ? kRank0 : 0u);
+        const uint32_t v = (uint32_t)k;  // query-cell index: selects the record
         while (m) {
             int b = __builtin_ctzll(m);
             m &= m - 1;
@@ -475,44 +475,76 @@ __global__ void k_qkeys(IndexView a, QueryView qv, int64_t *cnt, const int64_t *
     if (!PASS) cnt[q] = n;
 }
 
-// Query record (one per sorted key): what one predicate sweep needs.
+// Query record, one per query cell: what one predicate sweep needs.
 struct alignas(64) QRec {
     long long tlo, thi;
     float alo, ahi;
     uint32_t qv;   // query | kRank0 | kCompact
     int32_t bq0;   // first bucket of [min(tlo,thi), max(tlo,thi)]
-    unsigned long long sig[4];
+    unsigned long long sig[4];  // prefix signature of the query's cells before this one
 };
 static_assert(sizeof(QRec) == 64, "QRec layout");
 
-__global__ void k_qrec(int64_t n, IndexView a, QueryView qv, const uint64_t *skey, const uint32_t *sval, QRec *recs,
-                       int32_t *rown)
+// One thread per query walks its sorted cells once, decoding each and
+// growing the prefix signature (prefix_sig semantics: an undecodable cell
+// saturates the signature; `compact` = every earlier cell on this cell's face
+// within +-7 cells in i and j).
+__global__ void k_qcellrec(IndexView a, QueryView qv, QRec *crec, int32_t *cown)
 {
-    int64_t j = tid64();
-    if (j >= n) return;
-    const uint32_t v = sval[j];
-    const uint32_t q = v & ~kRank0;
-    QRec r;
-    r.tlo = qv.tlo[q];
-    r.thi = qv.thi[q];
-    r.alo = qv.alo[q];
-    r.ahi = qv.ahi[q];
-    r.bq0 = bucket_of(r.tlo < r.thi ? r.tlo : r.thi, a.bk);
-    if (rown) rown[j] = qv.owner[q];
+    const int64_t q = tid64();
+    if (q >= qv.nq) return;
+    const long long tlo = qv.tlo[q], thi = qv.thi[q];
+    const float alo = qv.alo[q], ahi = qv.ahi[q];
+    const int bq0 = bucket_of(tlo < thi ? tlo : thi, a.bk);
+    const int32_t own = cown ? qv.owner[q] : -1;
+    const int64_t c0 = qv.offs[q], c1 = qv.offs[q + 1];
     Sig256 sig;
-    bool compact = false;
-    if (!(v & kRank0)) {
-        uint64_t c = cell_of_slot(a, (uint32_t)(skey[j] >> 6));
-        prefix_sig(qv.cells + qv.offs[q], qv.offs[q + 1] - qv.offs[q], c, sig, compact);
-    } else {
-        sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = 0;
+    sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = 0;
+    bool bad = false;  // an undecodable cell in the prefix
+    int pf = -1;       // face of every prefix cell, -2 if mixed
+    int imin = 0, imax = 0, jmin = 0, jmax = 0;
+    for (int64_t k = c0; k < c1; k++) {
+        int f = 0, i = 0, j = 0;
+        const bool v = decode13(qv.cells[k], f, i, j);
+        const bool compact = v && !bad &&
+                             (k == c0 || (pf == f && imin >= i - 7 && imax <= i + 7 && jmin >= j - 7 && jmax <= j + 7));
+        QRec r;
+        r.tlo = tlo;
+        r.thi = thi;
+        r.alo = alo;
+        r.ahi = ahi;
+        r.qv = (uint32_t)q | (k == c0 ? kRank0 : 0u) | (compact ? kCompact : 0u);
+        r.bq0 = bq0;
+        r.sig[0] = sig.w[0];
+        r.sig[1] = sig.w[1];
+        r.sig[2] = sig.w[2];
+        r.sig[3] = sig.w[3];
+        crec[k] = r;
+        if (cown) cown[k] = own;
+        if (v) {
+            const int bit = ((i & 15) << 4) | (j & 15);
+            const unsigned long long m = 1ull << (bit & 63);
+            const int wi = bit >> 6;  // selects, not an indexed store: keeps sig in registers
+            sig.w[0] |= wi == 0 ? m : 0;
+            sig.w[1] |= wi == 1 ? m : 0;
+            sig.w[2] |= wi == 2 ? m : 0;
+            sig.w[3] |= wi == 3 ? m : 0;
+            if (k == c0) {
+                pf = f;
+                imin = imax = i;
+                jmin = jmax = j;
+            } else {
+                if (pf != f) pf = -2;
+                imin = min(imin, i);
+                imax = max(imax, i);
+                jmin = min(jmin, j);
+                jmax = max(jmax, j);
+            }
+        } else {
+            bad = true;
+            sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = ~0ull;
+        }
     }
-    r.qv = v | (compact ? kCompact : 0u);
-    r.sig[0] = sig.w[0];
-    r.sig[1] = sig.w[1];
-    r.sig[2] = sig.w[2];
-    r.sig[3] = sig.w[3];
-    recs[j] = r;
 }
 
 __device__ __forceinline__ uint32_t group_of(const IndexView &a, uint64_t key)
@@ -629,6 +661,7 @@ __device__ __forceinline__ void load_slot(const IndexView &ix, uint32_t p, uint3
 // unit's query records staged through LDS 64 at a time and broadcast.
 template <bool OWNER>
 __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__restrict__ recs,
+                                                      const uint32_t *__restrict__ sval,
                                                       const int32_t *__restrict__ rown, const uint32_t *__restrict__ u_run,
                                                       const uint32_t *__restrict__ u_pt, const uint32_t *__restrict__ u_qt,
                                                       uint32_t *__restrict__ out_q, uint32_t *__restrict__ out_e,
@@ -702,12 +735,13 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
                 bool rel = false;
                 __builtin_amdgcn_wave_barrier();
                 if (kk < k1) {
-                    const int4 c0 = rec4[4 * kk], c1 = rec4[4 * kk + 1], c2 = rec4[4 * kk + 2], c3 = rec4[4 * kk + 3];
+                    const uint32_t ci = sval[kk];
+                    const int4 c0 = rec4[4 * ci], c1 = rec4[4 * ci + 1], c2 = rec4[4 * ci + 2], c3 = rec4[4 * ci + 3];
                     s_rec[w][0][lane] = c0;
                     s_rec[w][1][lane] = c1;
                     s_rec[w][2][lane] = c2;
                     s_rec[w][3][lane] = c3;
-                    if (OWNER) s_own[w][lane] = rown[kk];
+                    if (OWNER) s_own[w][lane] = rown[ci];
                     const long long tlo = ((long long)c0.y << 32) | (uint32_t)c0.x;
                     const long long thi = ((long long)c0.w << 32) | (uint32_t)c0.z;
                     rel = !(tmax < tlo || tmin > thi);  // else no posting of the unit can match
@@ -1090,10 +1124,19 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     int64_t *qcnt = c0_.ensure(nq + 1), *qoff = c1_.ensure(nq + 2);
     hipLaunchKernelGGL(k_qkeys<0>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, ix, qv, qcnt, nullptr, nullptr, nullptr);
     exclusive_scan_i64(qcnt, qoff, nq, tmp_, s);
-    const int64_t nkeys = fetch_i64(qoff + nq, s);
+    int64_t hk[2] = {0, 0};
+    DSS_HIP(hipMemcpyAsync(&hk[0], qoff + nq, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipMemcpyAsync(&hk[1], q_offs + nq, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    const int64_t nkeys = hk[0], nqc = hk[1];
     keys_ = nkeys;
     if (nkeys == 0) return empty();
     if (nkeys >= (int64_t)0x7fffffff) throw Error(DSSG_ERR_CAPACITY, "search: more than 2^31 (cell, bucket) keys per batch");
+    // query-cell records (independent of the sort)
+    if (nqc >= (int64_t)0xffffffffll) throw Error(DSSG_ERR_CAPACITY, "search: more than 2^32 query cells per batch");
+    QRec *recs = (QRec *)rec_.ensure(sizeof(QRec) * (nqc + 1));
+    int32_t *rown = q_owner ? (int32_t *)own_.ensure(nqc + 1) : nullptr;
+    hipLaunchKernelGGL(k_qcellrec, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, ix, qv, recs, rown);
     uint64_t *key = k0_.ensure(nkeys + 1), *skey = k1_.ensure(nkeys + 1);
     uint32_t *val = v0_.ensure(nkeys + 1), *sval = v1_.ensure(nkeys + 1);
     hipLaunchKernelGGL(k_qkeys<1>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, ix, qv, nullptr, qoff, key, val);
@@ -1106,9 +1149,6 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     tmp_.ensure(bytes + 16);
     DSS_HIP(hipcub::DeviceRunLengthEncode::Encode(tmp_.p, bytes, skey, ukey, rcnt, nruns_d, (int)nkeys, s));
     // query records (independent of the run boundaries)
-    QRec *recs = (QRec *)rec_.ensure(sizeof(QRec) * (nkeys + 1));
-    int32_t *rown = q_owner ? (int32_t *)own_.ensure(nkeys + 1) : nullptr;
-    hipLaunchKernelGGL(k_qrec, dim3(grid_for(nkeys, kBlock)), dim3(kBlock), 0, s, nkeys, ix, qv, skey, sval, recs, rown);
     const int64_t nruns = fetch_i64(nruns_d, s);
     exclusive_scan_i64(rcnt, rstart, nruns, tmp_, s);
     // (3) join units
@@ -1160,11 +1200,11 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
         if (nblocks && q_owner)
             hipLaunchKernelGGL(k_join<true>, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
-                               (const int32_t *)rown, (const uint32_t *)u_run, (const uint32_t *)u_pt, (const uint32_t *)u_qt,
+                               (const uint32_t *)sval, (const int32_t *)rown, (const uint32_t *)u_run, (const uint32_t *)u_pt, (const uint32_t *)u_qt,
                                oq, oe, counter, work);
         else if (nblocks)
             hipLaunchKernelGGL(k_join<false>, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
-                               (const int32_t *)nullptr, (const uint32_t *)u_run, (const uint32_t *)u_pt,
+                               (const uint32_t *)sval, (const int32_t *)nullptr, (const uint32_t *)u_run, (const uint32_t *)u_pt,
                                (const uint32_t *)u_qt, oq, oe, counter, work);
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
         unsigned long long total = 0;
