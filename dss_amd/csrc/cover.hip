@@ -39,7 +39,10 @@ constexpr double kCoarsePad = 1e-9;  // pruning padding, >> FACE_CLIP_PLUS_RECT_
 constexpr double kFinePad = DSS_FACE_CLIP_PLUS_RECT_ERR;
 
 enum : uint8_t { MODE_NONE = 0, MODE_LOOP = 1, MODE_POLYLINE = 2 };
-enum : uint8_t { FL_SMALL = 1, FL_PLANAR = 2 };
+enum : uint8_t { FL_SMALL = 1, FL_PLANAR = 2, FL_FAST = 4 };
+// Direct candidate path: single-face small loops whose start block is at
+// level >= kFastMinLevel (<= 4 * 4^(13 - L) level-13 candidates).
+constexpr int kFastMinLevel = 10;
 // node meta: level (bits 0-4), orientation (5-6), done (7), face (8-10)
 __device__ __forceinline__ uint32_t pack_meta(int level, int orient, int done, int face)
 {
@@ -59,6 +62,10 @@ __global__ void k_nverts(int64_t n, const int32_t *kind, const int64_t *voff, in
     nv[f] = kind[f] == DSSG_KIND_CIRCLE ? 20 : (voff[f + 1] - voff[f]);
 }
 
+// cos/sin of the 20 RegularLoop angles i * 2pi/20 (regular_loop.go), computed
+// on the host with the same Go-math restatement (gomath.cuh is host+device).
+__constant__ double c_circle_cos[20], c_circle_sin[20];
+
 __device__ bool edge_inside_face(V3 a, V3 b, int face)
 {
     if (xyz_face(a) != face || xyz_face(b) != face) return false;
@@ -68,165 +75,6 @@ __device__ bool edge_inside_face(V3 a, V3 b, int face)
     const double lim = 1.0 - 1e-6;
     return __builtin_fabs(u0) <= lim && __builtin_fabs(v0) <= lim && __builtin_fabs(u1) <= lim &&
            __builtin_fabs(v1) <= lim;
-}
-
-// One thread per footprint.
-__global__ void k_setup(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
-                        const float *radius_m, const int64_t *xoff, V3 *xyz, int32_t *status, double *area_out,
-                        uint8_t *mode, uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx)
-{
-    int64_t f = tid64();
-    if (f >= n) return;
-    int k = kind[f];
-    int64_t v0 = voff[f];
-    V3 *p = xyz + xoff[f];
-    int st = DSSG_ST_OK;
-    uint8_t md = MODE_NONE;
-    double area = 0;
-    int nv = 0;
-    bool small = false;
-    LoopView l{p, 0, false};
-    if (k == DSSG_KIND_CIRCLE) {
-        double la = lat[v0], ln = lng[v0];
-        float r = radius_m[f];
-        if (la > 90.0 || la < -90.0 || ln > 180.0 || ln < -180.0) st = DSSG_ST_BAD_COORD_SET;
-        else if (!(r > 0)) st = DSSG_ST_RADIUS;
-        else {
-            // regular_loop.go RegularLoop(center, DistanceMetersToAngle(r), 20)
-            V3 c = point_from_degrees(la, ln);
-            double radius = (double)r / DSS_RADIUS_EARTH_M;
-            V3 c1 = ortho(c), c0 = cross(c1, c);
-            double z = go_cos(radius), rr = go_sin(radius);
-            double step = 2 * DSS_PI / 20.0;
-            for (int i = 0; i < 20; i++) {
-                double ang = (double)i * step;
-                double px = rr * go_cos(ang), py = rr * go_sin(ang), pz = z;
-                V3 q = v3(c0.x * px + c1.x * py + c.x * pz, c0.y * px + c1.y * py + c.y * pz,
-                          c0.z * px + c1.z * py + c.z * pz);
-                p[i] = normalize(q);
-            }
-            nv = 20;
-            l.n = 20;
-            loop_init_origin(l);
-            md = MODE_LOOP;
-            small = radius < 0.5;
-        }
-    } else {
-        nv = (int)(voff[f + 1] - v0);
-        if (k == DSSG_KIND_POLYGON) {  // Q17: range check precedes the count check
-            for (int i = 0; i < nv; i++) {
-                double la = lat[v0 + i], ln = lng[v0 + i];
-                if (la > 90.0 || la < -90.0 || ln > 180.0 || ln < -180.0) { st = DSSG_ST_BAD_COORD_SET; break; }
-            }
-        }
-        if (st == DSSG_ST_OK && nv < 3) st = DSSG_ST_NOT_ENOUGH_POINTS;
-        if (st == DSSG_ST_OK) {
-            for (int i = 0; i < nv; i++) p[i] = point_from_degrees(lat[v0 + i], lng[v0 + i]);
-            l.n = nv;
-            loop_init_origin(l);
-            area = loop_area_km2(l);
-            if (area > DSS_MAX_AREA_KM2) {  // Q4: reverse in place and rebuild
-                for (int i = 0, j = nv - 1; i < j; i++, j--) {
-                    V3 t = p[i];
-                    p[i] = p[j];
-                    p[j] = t;
-                }
-                loop_init_origin(l);
-            }
-            area = loop_area_km2(l);
-            if (area > DSS_MAX_AREA_KM2) st = DSSG_ST_AREA_TOO_LARGE;
-            else if (area <= 0) md = MODE_POLYLINE;  // Q3: open polyline, no closing edge
-            else { md = MODE_LOOP; small = true; }
-        }
-    }
-    uint8_t mask = 0;
-    bool inner = true;
-    if (md != MODE_NONE) {
-        int ne = md == MODE_LOOP ? nv : nv - 1;
-        int face0 = xyz_face(p[0]);
-        for (int e = 0; e < ne; e++) {
-            V3 a = p[e], b = p[(e + 1) % nv];
-            if (edge_inside_face(a, b, face0)) { mask |= (uint8_t)(1u << face0); continue; }
-            inner = false;
-            for (int fc = 0; fc < 6; fc++) {
-                double uv[4];
-                if (clip_to_padded_face(a, b, fc, kCoarsePad, uv)) mask |= (uint8_t)(1u << fc);
-            }
-        }
-        if (md == MODE_POLYLINE) {
-            for (int i = 0; i < nv; i++)
-                for (int fc = 0; fc < 6; fc++) {
-                    double u, v;
-                    if (face_xyz_to_uv(fc, p[i], u, v) && __builtin_fabs(u) <= 1 + kCoarsePad &&
-                        __builtin_fabs(v) <= 1 + kCoarsePad)
-                        mask |= (uint8_t)(1u << fc);
-                }
-        }
-    }
-    status[f] = st;
-    area_out[f] = area;
-    mode[f] = md;
-    origin_in[f] = l.origin_inside ? 1 : 0;
-    fmask[f] = mask;
-    // bbox-limited start is valid for polylines (no interior) and for loops
-    // whose edges all lie inside one face and whose interior is the small side.
-    uint8_t fl = (md == MODE_POLYLINE || (md == MODE_LOOP && inner && small && __builtin_popcount(mask) == 1)) ? FL_SMALL : 0;
-    // Planar containment (see contains_node): a single-face small loop whose
-    // (u,v) bound does not come near OriginPoint's projection.
-    if (md == MODE_LOOP && (fl & FL_SMALL)) {
-        int face0 = xyz_face(p[0]);
-        bool near_origin = false;
-        if (face0 == xyz_face(origin_point())) {
-            double ou, ov, ulo = 1e300, uhi = -1e300, vlo = 1e300, vhi = -1e300;
-            valid_face_xyz_to_uv(face0, origin_point(), ou, ov);
-            for (int i = 0; i < nv; i++) {
-                double u, v;
-                valid_face_xyz_to_uv(face0, p[i], u, v);
-                ulo = fmin(ulo, u); uhi = fmax(uhi, u); vlo = fmin(vlo, v); vhi = fmax(vhi, v);
-            }
-            near_origin = ou >= ulo - 1e-6 && ou <= uhi + 1e-6 && ov >= vlo - 1e-6 && ov <= vhi + 1e-6;
-        }
-        if (!near_origin) fl |= FL_PLANAR;
-    }
-    flags[f] = fl;
-    nvx[f] = nv;
-}
-
-__device__ __forceinline__ int num_edges(uint8_t md, int nv) { return md == MODE_LOOP ? nv : (md == MODE_POLYLINE ? nv - 1 : 0); }
-
-__global__ void k_edge_counts(int64_t n, const uint8_t *mode, const uint8_t *fmask, const int32_t *nvx, int64_t *cnt)
-{
-    int64_t f = tid64();
-    if (f >= n) return;
-    cnt[f] = (int64_t)__builtin_popcount(fmask[f]) * num_edges(mode[f], nvx[f]);
-}
-
-// Clip every edge to every touched face (ascending face order).
-__global__ void k_clip(int64_t n, const int64_t *xoff, const V3 *xyz, const uint8_t *mode, const uint8_t *fmask,
-                       const int32_t *nvx, const int64_t *eoff, double4 *clip_f, double4 *clip_c, uint8_t *cflags)
-{
-    int64_t f = tid64();
-    if (f >= n) return;
-    uint8_t md = mode[f];
-    if (md == MODE_NONE) return;
-    int nv = nvx[f], ne = num_edges(md, nv);
-    const V3 *p = xyz + xoff[f];
-    int64_t base = eoff[f];
-    int fi = 0;
-    for (int fc = 0; fc < 6; fc++) {
-        if (!(fmask[f] >> fc & 1)) continue;
-        for (int e = 0; e < ne; e++) {
-            V3 a = p[e], b = p[(e + 1) % nv];
-            double uf[4], uc[4];
-            bool okf = clip_to_padded_face(a, b, fc, kFinePad, uf);
-            bool okc = clip_to_padded_face(a, b, fc, kCoarsePad, uc);
-            int64_t k = base + (int64_t)fi * ne + e;
-            clip_f[k] = make_double4(uf[0], uf[1], uf[2], uf[3]);
-            clip_c[k] = make_double4(uc[0], uc[1], uc[2], uc[3]);
-            cflags[k] = (uint8_t)((okf ? 1 : 0) | (okc ? 2 : 0));
-        }
-        fi++;
-    }
 }
 
 struct FaceBox {
@@ -295,6 +143,190 @@ __device__ int start_cells(const FaceBox &b, int fc, uint64_t *id, uint32_t *ii,
     return cnt;
 }
 
+// One thread per footprint.
+__global__ void k_setup(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
+                        const float *radius_m, const int64_t *xoff, V3 *xyz, int32_t *status, double *area_out,
+                        uint8_t *mode, uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx, double2 *uv,
+                        uint64_t *st_id, uint32_t *st_i, uint32_t *st_j, uint32_t *finfo, int64_t *ncand)
+{
+    int64_t f = tid64();
+    if (f >= n) return;
+    int k = kind[f];
+    int64_t v0 = voff[f];
+    V3 *p = xyz + xoff[f];
+    int st = DSSG_ST_OK;
+    uint8_t md = MODE_NONE;
+    double area = 0;
+    int nv = 0;
+    bool small = false;
+    LoopView l{p, 0, false};
+    if (k == DSSG_KIND_CIRCLE) {
+        double la = lat[v0], ln = lng[v0];
+        float r = radius_m[f];
+        if (la > 90.0 || la < -90.0 || ln > 180.0 || ln < -180.0) st = DSSG_ST_BAD_COORD_SET;
+        else if (!(r > 0)) st = DSSG_ST_RADIUS;
+        else {
+            // regular_loop.go RegularLoop(center, DistanceMetersToAngle(r), 20)
+            V3 c = point_from_degrees(la, ln);
+            double radius = (double)r / DSS_RADIUS_EARTH_M;
+            V3 c1 = ortho(c), c0 = cross(c1, c);
+            double z = go_cos(radius), rr = go_sin(radius);
+            for (int i = 0; i < 20; i++) {
+                double px = rr * c_circle_cos[i], py = rr * c_circle_sin[i], pz = z;
+                V3 q = v3(c0.x * px + c1.x * py + c.x * pz, c0.y * px + c1.y * py + c.y * pz,
+                          c0.z * px + c1.z * py + c.z * pz);
+                p[i] = normalize(q);
+            }
+            nv = 20;
+            l.n = 20;
+            loop_init_origin(l);
+            md = MODE_LOOP;
+            small = radius < 0.5;
+        }
+    } else {
+        nv = (int)(voff[f + 1] - v0);
+        if (k == DSSG_KIND_POLYGON) {  // Q17: range check precedes the count check
+            for (int i = 0; i < nv; i++) {
+                double la = lat[v0 + i], ln = lng[v0 + i];
+                if (la > 90.0 || la < -90.0 || ln > 180.0 || ln < -180.0) { st = DSSG_ST_BAD_COORD_SET; break; }
+            }
+        }
+        if (st == DSSG_ST_OK && nv < 3) st = DSSG_ST_NOT_ENOUGH_POINTS;
+        if (st == DSSG_ST_OK) {
+            for (int i = 0; i < nv; i++) p[i] = point_from_degrees(lat[v0 + i], lng[v0 + i]);
+            l.n = nv;
+            loop_init_origin(l);
+            area = loop_area_km2(l);
+            if (area > DSS_MAX_AREA_KM2) {  // Q4: reverse in place and rebuild
+                for (int i = 0, j = nv - 1; i < j; i++, j--) {
+                    V3 t = p[i];
+                    p[i] = p[j];
+                    p[j] = t;
+                }
+                loop_init_origin(l);
+                area = loop_area_km2(l);
+            }
+            if (area > DSS_MAX_AREA_KM2) st = DSSG_ST_AREA_TOO_LARGE;
+            else if (area <= 0) md = MODE_POLYLINE;  // Q3: open polyline, no closing edge
+            else { md = MODE_LOOP; small = true; }
+        }
+    }
+    uint8_t mask = 0;
+    bool inner = true;
+    if (md != MODE_NONE) {
+        int ne = md == MODE_LOOP ? nv : nv - 1;
+        int face0 = xyz_face(p[0]);
+        for (int e = 0; e < ne; e++) {
+            V3 a = p[e], b = p[(e + 1) % nv];
+            if (edge_inside_face(a, b, face0)) { mask |= (uint8_t)(1u << face0); continue; }
+            inner = false;
+            for (int fc = 0; fc < 6; fc++) {
+                double uv[4];
+                if (clip_to_padded_face(a, b, fc, kCoarsePad, uv)) mask |= (uint8_t)(1u << fc);
+            }
+        }
+        if (md == MODE_POLYLINE) {
+            for (int i = 0; i < nv; i++)
+                for (int fc = 0; fc < 6; fc++) {
+                    double u, v;
+                    if (face_xyz_to_uv(fc, p[i], u, v) && __builtin_fabs(u) <= 1 + kCoarsePad &&
+                        __builtin_fabs(v) <= 1 + kCoarsePad)
+                        mask |= (uint8_t)(1u << fc);
+                }
+        }
+    }
+    status[f] = st;
+    area_out[f] = area;
+    mode[f] = md;
+    origin_in[f] = l.origin_inside ? 1 : 0;
+    fmask[f] = mask;
+    // bbox-limited start is valid for polylines (no interior) and for loops
+    // whose edges all lie inside one face and whose interior is the small side.
+    uint8_t fl = (md == MODE_POLYLINE || (md == MODE_LOOP && inner && small && __builtin_popcount(mask) == 1)) ? FL_SMALL : 0;
+    // Planar containment (see contains_node): a single-face small loop whose
+    // (u,v) bound does not come near OriginPoint's projection.
+    int64_t nc = 0;
+    if (md == MODE_LOOP && (fl & FL_SMALL)) {
+        const int face0 = xyz_face(p[0]);
+        double2 *uvp = uv + xoff[f];
+        double ulo = 1e300, uhi = -1e300, vlo = 1e300, vhi = -1e300;
+        for (int i = 0; i < nv; i++) {
+            double u, v;
+            valid_face_xyz_to_uv(face0, p[i], u, v);  // = ClipToPaddedFace's same-face fast path
+            uvp[i] = make_double2(u, v);
+            ulo = fmin(ulo, u); uhi = fmax(uhi, u); vlo = fmin(vlo, v); vhi = fmax(vhi, v);
+        }
+        bool near_origin = false;
+        if (face0 == xyz_face(origin_point())) {
+            double ou, ov;
+            valid_face_xyz_to_uv(face0, origin_point(), ou, ov);
+            near_origin = ou >= ulo - 1e-6 && ou <= uhi + 1e-6 && ov >= vlo - 1e-6 && ov <= vhi + 1e-6;
+        }
+        if (!near_origin) fl |= FL_PLANAR;
+        // start block (as k_start would choose it); small enough -> direct candidates
+        const double m = 1e-7;
+        FaceBox b{ulo - m, uhi + m, vlo - m, vhi + m};
+        uint64_t id[4];
+        uint32_t ii[4], jj[4], mt[4];
+        const int k = start_cells(b, face0, id, ii, jj, mt);
+        const int L = meta_level(mt[0]);
+        if (k > 0 && L >= kFastMinLevel) {
+            fl |= FL_FAST;
+            uint32_t info = (uint32_t)L | ((uint32_t)k << 5);
+            for (int q = 0; q < k; q++) {
+                st_id[4 * f + q] = id[q];
+                st_i[4 * f + q] = ii[q];
+                st_j[4 * f + q] = jj[q];
+                info |= (uint32_t)meta_orient(mt[q]) << (8 + 2 * q);
+            }
+            finfo[f] = info;
+            nc = (int64_t)k << (2 * (kCoverLevel - L));
+        }
+    }
+    ncand[f] = nc;
+    flags[f] = fl;
+    nvx[f] = nv;
+}
+
+__device__ __forceinline__ int num_edges(uint8_t md, int nv) { return md == MODE_LOOP ? nv : (md == MODE_POLYLINE ? nv - 1 : 0); }
+
+__global__ void k_edge_counts(int64_t n, const uint8_t *mode, const uint8_t *fmask, const uint8_t *flags, const int32_t *nvx,
+                              int64_t *cnt)
+{
+    int64_t f = tid64();
+    if (f >= n) return;
+    cnt[f] = (flags[f] & FL_FAST) ? 0 : (int64_t)__builtin_popcount(fmask[f]) * num_edges(mode[f], nvx[f]);
+}
+
+// Clip every edge to every touched face (ascending face order).
+__global__ void k_clip(int64_t n, const int64_t *xoff, const V3 *xyz, const uint8_t *mode, const uint8_t *fmask,
+                       const uint8_t *flags, const int32_t *nvx, const int64_t *eoff, double4 *clip_f, double4 *clip_c,
+                       uint8_t *cflags)
+{
+    int64_t f = tid64();
+    if (f >= n) return;
+    uint8_t md = mode[f];
+    if (md == MODE_NONE || (flags[f] & FL_FAST)) return;
+    int nv = nvx[f], ne = num_edges(md, nv);
+    const V3 *p = xyz + xoff[f];
+    int64_t base = eoff[f];
+    int fi = 0;
+    for (int fc = 0; fc < 6; fc++) {
+        if (!(fmask[f] >> fc & 1)) continue;
+        for (int e = 0; e < ne; e++) {
+            V3 a = p[e], b = p[(e + 1) % nv];
+            double uf[4], uc[4];
+            bool okf = clip_to_padded_face(a, b, fc, kFinePad, uf);
+            bool okc = clip_to_padded_face(a, b, fc, kCoarsePad, uc);
+            int64_t k = base + (int64_t)fi * ne + e;
+            clip_f[k] = make_double4(uf[0], uf[1], uf[2], uf[3]);
+            clip_c[k] = make_double4(uc[0], uc[1], uc[2], uc[3]);
+            cflags[k] = (uint8_t)((okf ? 1 : 0) | (okc ? 2 : 0));
+        }
+        fi++;
+    }
+}
+
 // Face-cell id for face fc (level 0).
 __device__ __forceinline__ uint64_t face_cell(int fc) { return ((uint64_t)fc << 61) | (1ull << 60); }
 
@@ -345,7 +377,7 @@ __global__ void k_start(int64_t n, const int64_t *xoff, const V3 *xyz, const uin
     if (f >= n) return;
     uint8_t md = mode[f];
     int64_t c = 0;
-    if (md != MODE_NONE) {
+    if (md != MODE_NONE && !(flags[f] & FL_FAST)) {
         int nv = nvx[f], ne = num_edges(md, nv);
         const V3 *p = xyz + xoff[f];
         LoopView l{p, nv, origin_in[f] != 0};
@@ -526,8 +558,17 @@ __global__ void k_item_counts(int64_t nn, const uint32_t *nf, const uint32_t *nm
     atomicAdd(&fcnt[nf[k]], (unsigned long long)c);
 }
 
-__global__ void k_emit(int64_t nn, const uint64_t *nid, const uint32_t *nmeta, const int64_t *ipos, uint64_t *cells,
-                       uint32_t *big, int *nbig)
+// Descent items are numbered among themselves (ipos); dpre[f] = descent cells
+// of the footprints before f, offs[f] = all cells before f.
+__device__ __forceinline__ int64_t item_pos(int64_t k, const uint32_t *nf, const int64_t *ipos, const int64_t *dpre,
+                                            const int64_t *offs)
+{
+    const uint32_t f = nf[k];
+    return offs[f] + (ipos[k] - dpre[f]);
+}
+
+__global__ void k_emit(int64_t nn, const uint32_t *nf, const uint64_t *nid, const uint32_t *nmeta, const int64_t *ipos,
+                       const int64_t *dpre, const int64_t *offs, uint64_t *cells, uint32_t *big, int *nbig)
 {
     int64_t k = tid64();
     if (k >= nn) return;
@@ -540,11 +581,12 @@ __global__ void k_emit(int64_t nn, const uint64_t *nid, const uint32_t *nmeta, c
     }
     uint64_t lsb13 = lsb_for_level(kCoverLevel);
     uint64_t first = id - cellid_lsb_dev(id) + lsb13;
-    int64_t w = ipos[k];
+    int64_t w = item_pos(k, nf, ipos, dpre, offs);
     for (int64_t q = 0; q < c; q++) cells[w + q] = first + (uint64_t)q * (lsb13 << 1);
 }
 
-__global__ void k_emit_big(const uint32_t *big, const uint64_t *nid, const uint32_t *nmeta, const int64_t *ipos, uint64_t *cells)
+__global__ void k_emit_big(const uint32_t *big, const uint32_t *nf, const uint64_t *nid, const uint32_t *nmeta,
+                           const int64_t *ipos, const int64_t *dpre, const int64_t *offs, uint64_t *cells)
 {
     uint32_t k = big[blockIdx.x];
     int level = meta_level(nmeta[k]);
@@ -552,8 +594,122 @@ __global__ void k_emit_big(const uint32_t *big, const uint64_t *nid, const uint3
     uint64_t id = nid[k];
     uint64_t lsb13 = lsb_for_level(kCoverLevel);
     uint64_t first = id - cellid_lsb_dev(id) + lsb13;
-    int64_t w = ipos[k];
+    int64_t w = item_pos(k, nf, ipos, dpre, offs);
     for (int64_t q = threadIdx.x; q < c; q += blockDim.x) cells[w + q] = first + (uint64_t)q * (lsb13 << 1);
+}
+
+// ---------------------------------------------------------------------------
+// Direct candidate path (FL_FAST footprints).  The level-13 descendants of a
+// footprint's <= 4 start cells, taken start cell by start cell in id order,
+// are consecutive ids, so enumerating them by index lists the footprint's
+// candidates sorted; each is tested exactly as k_expand_count tests a level-13
+// node, and an order-preserving scan compacts the survivors.
+__global__ void k_cand_owner(int64_t n, const int64_t *coff, uint32_t *cand_f)
+{
+    int64_t f = tid64();
+    if (f >= n) return;
+    for (int64_t c = coff[f]; c < coff[f + 1]; c++) cand_f[c] = (uint32_t)f;
+}
+
+// Level-13 (i, j) and id of candidate c of footprint f.
+__device__ __forceinline__ void cand_cell(int64_t c, uint32_t f, const int64_t *coff, const uint64_t *st_id,
+                                          const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, int &face,
+                                          uint32_t &i, uint32_t &j, uint64_t &id)
+{
+    const int64_t d = c - coff[f];
+    const uint32_t info = finfo[f];
+    const int L = (int)(info & 31u);
+    const int sh = 2 * (kCoverLevel - L);
+    const int s = (int)(d >> sh);
+    const uint32_t r = (uint32_t)(d & ((1ll << sh) - 1));
+    int o = (int)((info >> (8 + 2 * s)) & 3u);
+    i = st_i[4 * f + s];
+    j = st_j[4 * f + s];
+    for (int l = L + 1; l <= kCoverLevel; l++) {
+        const int digit = (int)((r >> (2 * (kCoverLevel - l))) & 3u);
+        const int ij = pos_to_ij(o, digit);
+        const uint32_t half = 1u << (kMaxLevel - l);
+        if (ij >> 1) i += half;
+        if (ij & 1) j += half;
+        o ^= pos_to_orientation(digit);
+    }
+    const uint64_t sid = st_id[4 * f + s];
+    const uint64_t lsb13 = lsb_for_level(kCoverLevel);
+    face = (int)(sid >> 61);
+    id = sid - lsb_for_level(L) + lsb13 + (uint64_t)r * (lsb13 << 1);  // cellid.go ChildBeginAtLevel + r steps
+}
+
+__global__ void k_cand_test(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
+                            const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const int64_t *xoff,
+                            const V3 *xyz, const double2 *uv, const int32_t *nvx, const uint8_t *origin_in,
+                            const uint8_t *flags, int64_t *kept)
+{
+    const int64_t c = tid64();
+    if (c >= NC) return;
+    const uint32_t f = cand_f[c];
+    int face;
+    uint32_t i, j;
+    uint64_t id;
+    cand_cell(c, f, coff, st_id, st_i, st_j, finfo, face, i, j, id);
+    const int nv = nvx[f];
+    const double2 *up = uv + xoff[f];
+    const uint32_t size = 1u << (kMaxLevel - kCoverLevel);
+    const double ulo = st_to_uv((double)i / (double)kMaxSize), uhi = st_to_uv((double)(i + size) / (double)kMaxSize);
+    const double vlo = st_to_uv((double)j / (double)kMaxSize), vhi = st_to_uv((double)(j + size) / (double)kMaxSize);
+    // loop.go IntersectsCell: padded edge test, else centre containment
+    const double pm = kFinePad;
+    bool in = false;
+    for (int e = 0; e < nv && !in; e++) {
+        const double2 a = up[e], b = up[e + 1 == nv ? 0 : e + 1];
+        in = edge_intersects_rect(a.x, a.y, b.x, b.y, ulo - pm, uhi + pm, vlo - pm, vhi + pm);
+    }
+    if (!in) {
+        const bool origin = origin_in[f] != 0;
+        if (flags[f] & FL_PLANAR) {
+            // contains_node's planar ray cast, on the same (u,v) edge images
+            const double sz = (double)size;
+            const double half = 0.5 / (double)kMaxSize;
+            const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
+            bool par = false;
+            for (int e = 0; e < nv; e++) {
+                const double2 a = up[e], b = up[e + 1 == nv ? 0 : e + 1];
+                if ((a.y > vc) != (b.y > vc)) {
+                    const double x = a.x + (vc - a.y) * (b.x - a.x) / (b.y - a.y);
+                    if (uc < x) par = !par;
+                }
+            }
+            in = origin != par;
+        } else {
+            LoopView l{xyz + xoff[f], nv, origin};
+            in = loop_contains(l, node_center(face, i, j, kCoverLevel));
+        }
+    }
+    kept[c] = in ? 1 : 0;
+}
+
+// Per-footprint cell counts: direct-path count from the candidate scan plus
+// the descent count the item atomics left in dcnt.
+__global__ void k_counts(int64_t n, const int64_t *coff, const int64_t *kpos, const unsigned long long *dcnt,
+                         int64_t *total, int64_t *dc64)
+{
+    int64_t f = tid64();
+    if (f >= n) return;
+    total[f] = (kpos[coff[f + 1]] - kpos[coff[f]]) + (int64_t)dcnt[f];
+    dc64[f] = (int64_t)dcnt[f];
+}
+
+__global__ void k_cand_emit(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
+                            const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const int64_t *kept,
+                            const int64_t *kpos, const int64_t *offs, uint64_t *cells)
+{
+    const int64_t c = tid64();
+    if (c >= NC || !kept[c]) return;
+    const uint32_t f = cand_f[c];
+    int face;
+    uint32_t i, j;
+    uint64_t id;
+    cand_cell(c, f, coff, st_id, st_i, st_j, finfo, face, i, j, id);
+    cells[offs[f] + (kpos[c] - kpos[coff[f]])] = id;
 }
 
 __global__ void k_u64_to_i64(int64_t n, const unsigned long long *a, int64_t *b)
@@ -570,6 +726,18 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
 {
     const unsigned B = kBlock;
     out->n = n;
+    if (!tables_) {  // RegularLoop angles, bit-identical host evaluation of the Go math
+        double cs[20], sn[20];
+        const double step = 2 * DSS_PI / 20.0;
+        for (int i = 0; i < 20; i++) {
+            const double ang = (double)i * step;
+            cs[i] = go_cos(ang);
+            sn[i] = go_sin(ang);
+        }
+        DSS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_circle_cos), cs, sizeof(cs), 0, hipMemcpyHostToDevice, s));
+        DSS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_circle_sin), sn, sizeof(sn), 0, hipMemcpyHostToDevice, s));
+        tables_ = true;
+    }
     int64_t *nv = cnt_.ensure(n + 1);
     int64_t *xoff = xoff_.ensure(n + 1);
     int32_t *status = status_.ensure(n + 1);
@@ -589,19 +757,35 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     DSS_HIP(hipMemcpyAsync(&nx, xoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
     V3 *xyz = (V3 *)xyz_.ensure((size_t)nx * 3 + 3);
+    double2 *uv = uv_.ensure(nx + 1);
+    uint64_t *st_id = st_id_.ensure(4 * n + 4);
+    uint32_t *st_i = st_i_.ensure(4 * n + 4), *st_j = st_j_.ensure(4 * n + 4), *finfo = finfo_.ensure(n + 1);
+    int64_t *ncand = ncand_.ensure(n + 1), *coff = coff_.ensure(n + 1);
     hipLaunchKernelGGL(k_setup, dim3(grid_for(n, 64)), dim3(64), 0, s, n, kind, voff, lat, lng, radius_m, xoff, xyz,
-                       status, area, mode, orig, fmask, flags, nvx);
+                       status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, ncand);
     int64_t *eoff = eoff_.ensure(n + 1);
-    hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, nvx, nv);
+    hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv);
     exclusive_scan_i64(nv, eoff, n, tmp_, s);
-    int64_t ne = 0;
-    DSS_HIP(hipMemcpyAsync(&ne, eoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    exclusive_scan_i64(ncand, coff, n, tmp_, s);
+    int64_t h2[2] = {0, 0};
+    DSS_HIP(hipMemcpyAsync(&h2[0], eoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipMemcpyAsync(&h2[1], coff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
+    const int64_t ne = h2[0], NC = h2[1];
+    // direct candidates (most footprints): test now, compact after the counts
+    uint32_t *cand_f = cand_f_.ensure(NC + 1);
+    int64_t *kept = kept_.ensure(NC + 1), *kpos = kpos_.ensure(NC + 2);
+    if (NC > 0) {
+        hipLaunchKernelGGL(k_cand_owner, dim3(grid_for(n, B)), dim3(B), 0, s, n, coff, cand_f);
+        hipLaunchKernelGGL(k_cand_test, dim3(grid_for(NC, B)), dim3(B), 0, s, NC, cand_f, coff, st_id, st_i, st_j, finfo,
+                           xoff, xyz, uv, nvx, orig, flags, kept);
+    }
+    exclusive_scan_i64(kept, kpos, NC, tmp_, s);
+    // hierarchical descent for the rest (big, multi-face, polyline footprints)
     double4 *clip_f = clipf_.ensure(ne + 1), *clip_c = clipc_.ensure(ne + 1);
     uint8_t *cflags = cflags_.ensure(ne + 1);
-    hipLaunchKernelGGL(k_clip, dim3(grid_for(n, 64)), dim3(64), 0, s, n, xoff, xyz, mode, fmask, nvx, eoff, clip_f,
+    hipLaunchKernelGGL(k_clip, dim3(grid_for(n, 64)), dim3(64), 0, s, n, xoff, xyz, mode, fmask, flags, nvx, eoff, clip_f,
                        clip_c, cflags);
-    // start nodes
     int64_t *soff = soff_.ensure(n + 1);
     hipLaunchKernelGGL(k_start<0>, dim3(grid_for(n, 64)), dim3(64), 0, s, n, xoff, xyz, mode, fmask, flags, orig, nvx,
                        eoff, clip_c, cflags, nv, soff, nullptr, nullptr, nullptr, nullptr, nullptr);
@@ -612,8 +796,9 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     int cur = 0;
     Frontier *F = &fr_[cur];
     F->ensure(nn + 1);
-    hipLaunchKernelGGL(k_start<1>, dim3(grid_for(n, 64)), dim3(64), 0, s, n, xoff, xyz, mode, fmask, flags, orig, nvx,
-                       eoff, clip_c, cflags, nullptr, soff, F->f.p, F->id.p, F->i.p, F->j.p, F->meta.p);
+    if (nn > 0)
+        hipLaunchKernelGGL(k_start<1>, dim3(grid_for(n, 64)), dim3(64), 0, s, n, xoff, xyz, mode, fmask, flags, orig, nvx,
+                           eoff, clip_c, cflags, nullptr, soff, F->f.p, F->id.p, F->i.p, F->j.p, F->meta.p);
     int *any_open = flag_.ensure(1);
     for (int iter = 0; iter < 32 && nn > 0; iter++) {
         uint8_t *act = act_.ensure(nn + 1);
@@ -638,29 +823,38 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
         nn = nn2;
         if (!open) break;
     }
-    // items -> CSR
-    unsigned long long *fcnt = fcnt_.ensure(n + 1);
-    DSS_HIP(hipMemsetAsync(fcnt, 0, sizeof(unsigned long long) * (n + 1), s));
+    // per-footprint counts (direct: from the scan; descent: item atomics) -> CSR
+    unsigned long long *dcnt = fcnt_.ensure(n + 1);
+    DSS_HIP(hipMemsetAsync(dcnt, 0, sizeof(unsigned long long) * (n + 1), s));
     int64_t *icnt = ncnt_.ensure(nn + 1), *ipos = npos_.ensure(nn + 1);
     if (nn > 0)
-        hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nn, B)), dim3(B), 0, s, nn, F->f.p, F->meta.p, icnt, fcnt);
-    int64_t *fc64 = fc64_.ensure(n + 1);
-    hipLaunchKernelGGL(k_u64_to_i64, dim3(grid_for(n, B)), dim3(B), 0, s, n, fcnt, fc64);
-    exclusive_scan_i64(fc64, offs, n, tmp_, s);
+        hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nn, B)), dim3(B), 0, s, nn, F->f.p, F->meta.p, icnt, dcnt);
+    int64_t *tot64 = fc64_.ensure(n + 1), *dc64 = dc64_.ensure(n + 1), *dpre = dpre_.ensure(n + 1);
+    hipLaunchKernelGGL(k_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, coff, kpos, dcnt, tot64, dc64);
+    exclusive_scan_i64(tot64, offs, n, tmp_, s);
     int64_t total = 0;
-    if (nn > 0) exclusive_scan_i64(icnt, ipos, nn, tmp_, s);
+    if (nn > 0) {
+        exclusive_scan_i64(icnt, ipos, nn, tmp_, s);
+        exclusive_scan_i64(dc64, dpre, n, tmp_, s);
+    }
     DSS_HIP(hipMemcpyAsync(&total, offs + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
     uint64_t *cells = cells_.ensure(total + 1);
+    if (NC > 0)
+        hipLaunchKernelGGL(k_cand_emit, dim3(grid_for(NC, B)), dim3(B), 0, s, NC, cand_f, coff, st_id, st_i, st_j, finfo,
+                           kept, kpos, offs, cells);
     if (nn > 0) {
         uint32_t *big = big_.ensure(nn + 1);
         int *nbig = flag_.ensure(1);
         DSS_HIP(hipMemsetAsync(nbig, 0, sizeof(int), s));
-        hipLaunchKernelGGL(k_emit, dim3(grid_for(nn, B)), dim3(B), 0, s, nn, F->id.p, F->meta.p, ipos, cells, big, nbig);
+        hipLaunchKernelGGL(k_emit, dim3(grid_for(nn, B)), dim3(B), 0, s, nn, F->f.p, F->id.p, F->meta.p, ipos, dpre, offs,
+                           cells, big, nbig);
         int hb = 0;
         DSS_HIP(hipMemcpyAsync(&hb, nbig, sizeof(int), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipStreamSynchronize(s));
-        if (hb > 0) hipLaunchKernelGGL(k_emit_big, dim3(hb), dim3(256), 0, s, big, F->id.p, F->meta.p, ipos, cells);
+        if (hb > 0)
+            hipLaunchKernelGGL(k_emit_big, dim3(hb), dim3(256), 0, s, big, F->f.p, F->id.p, F->meta.p, ipos, dpre, offs,
+                               cells);
     }
     out->offs = offs;
     out->cells = cells;

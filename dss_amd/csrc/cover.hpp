@@ -36,6 +36,12 @@ class CoverEngine {
     DevBuf<uint64_t> cells_;
     DevBuf<uint32_t> big_;
     Frontier fr_[2];
+    // direct candidate path
+    DevBuf<double2> uv_;
+    DevBuf<uint64_t> st_id_;
+    DevBuf<uint32_t> st_i_, st_j_, finfo_, cand_f_;
+    DevBuf<int64_t> ncand_, coff_, kept_, kpos_, dc64_, dpre_;
+    bool tables_ = false;
 };
 
 }  // namespace dss

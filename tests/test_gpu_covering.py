@@ -58,7 +58,13 @@ def _check_batch(g, res):
     assert np.array_equal(res.status, g["status"]), np.nonzero(res.status != g["status"])
     bad = np.nonzero(np.diff(res.offs) != np.diff(g["offs"]))[0]
     assert len(bad) == 0, f"cell-count mismatch at footprints {bad[:10]}"
-    assert np.array_equal(res.cells, g["cells"])
+    if not np.array_equal(res.cells, g["cells"]):
+        diff = np.nonzero(res.cells != g["cells"])[0]
+        fps = np.unique(np.searchsorted(g["offs"], diff, side="right") - 1)
+        f = int(fps[0])
+        a, b = int(g["offs"][f]), int(g["offs"][f + 1])
+        raise AssertionError(f"{len(fps)} footprints differ, first {f}: got {[tok(c) for c in res.cells[a:b]]} "
+                             f"want {[tok(c) for c in g['cells'][a:b]]}")
     assert np.array_equal(res.area_km2.view(np.uint64), g["area_km2"].view(np.uint64))
 
 
