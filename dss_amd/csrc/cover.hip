@@ -43,6 +43,7 @@ enum : uint8_t { FL_SMALL = 1, FL_PLANAR = 2, FL_FAST = 4 };
 // Direct candidate path: single-face small loops whose start block is at
 // level >= kFastMinLevel (<= 4 * 4^(13 - L) level-13 candidates).
 constexpr int kFastMinLevel = 10;
+constexpr int kCandBlock = 256;
 // node meta: level (bits 0-4), orientation (5-6), done (7), face (8-10)
 __device__ __forceinline__ uint32_t pack_meta(int level, int orient, int done, int face)
 {
@@ -147,7 +148,8 @@ __device__ int start_cells(const FaceBox &b, int fc, uint64_t *id, uint32_t *ii,
 __global__ void k_setup(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
                         const float *radius_m, const int64_t *xoff, V3 *xyz, int32_t *status, double *area_out,
                         uint8_t *mode, uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx, double2 *uv,
-                        uint64_t *st_id, uint32_t *st_i, uint32_t *st_j, uint32_t *finfo, int64_t *ncand)
+                        uint64_t *st_id, uint32_t *st_i, uint32_t *st_j, uint32_t *finfo, int64_t *ncand,
+                        uint4 *fbox)
 {
     int64_t f = tid64();
     if (f >= n) return;
@@ -281,6 +283,14 @@ __global__ void k_setup(int64_t n, const int32_t *kind, const int64_t *voff, con
             }
             finfo[f] = info;
             nc = (int64_t)k << (2 * (kCoverLevel - L));
+            // level-13 (i, j) range of the padded bound: candidates outside it
+            // are > 1e-7 (uv) from every vertex, so neither touch an edge nor
+            // lie inside this single-face loop
+            const int sh13 = kMaxLevel - kCoverLevel;
+            fbox[f] = make_uint4((uint32_t)(st_to_ij(uv_to_st(fmax(b.ulo, -1.0))) >> sh13),
+                                 (uint32_t)(st_to_ij(uv_to_st(fmin(b.uhi, 1.0))) >> sh13),
+                                 (uint32_t)(st_to_ij(uv_to_st(fmax(b.vlo, -1.0))) >> sh13),
+                                 (uint32_t)(st_to_ij(uv_to_st(fmin(b.vhi, 1.0))) >> sh13));
         }
     }
     ncand[f] = nc;
@@ -639,9 +649,11 @@ __device__ __forceinline__ void cand_cell(int64_t c, uint32_t f, const int64_t *
     id = sid - lsb_for_level(L) + lsb13 + (uint64_t)r * (lsb13 << 1);  // cellid.go ChildBeginAtLevel + r steps
 }
 
+// kept: 0 / 1, or 2 = undecided (centre containment needs the exact S2 test,
+// done by k_cand_exact so that this kernel stays register-light).
 __global__ void k_cand_test(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
-                            const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const int64_t *xoff,
-                            const V3 *xyz, const double2 *uv, const int32_t *nvx, const uint8_t *origin_in,
+                            const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const uint4 *fbox,
+                            const int64_t *xoff, const double2 *uv, const int32_t *nvx, const uint8_t *origin_in,
                             const uint8_t *flags, int64_t *kept)
 {
     const int64_t c = tid64();
@@ -651,6 +663,12 @@ __global__ void k_cand_test(int64_t NC, const uint32_t *cand_f, const int64_t *c
     uint32_t i, j;
     uint64_t id;
     cand_cell(c, f, coff, st_id, st_i, st_j, finfo, face, i, j, id);
+    const uint4 bx = fbox[f];
+    const uint32_t i13 = i >> (kMaxLevel - kCoverLevel), j13 = j >> (kMaxLevel - kCoverLevel);
+    if (i13 < bx.x || i13 > bx.y || j13 < bx.z || j13 > bx.w) {
+        kept[c] = 0;
+        return;
+    }
     const int nv = nvx[f];
     const double2 *up = uv + xoff[f];
     const uint32_t size = 1u << (kMaxLevel - kCoverLevel);
@@ -663,8 +681,8 @@ __global__ void k_cand_test(int64_t NC, const uint32_t *cand_f, const int64_t *c
         const double2 a = up[e], b = up[e + 1 == nv ? 0 : e + 1];
         in = edge_intersects_rect(a.x, a.y, b.x, b.y, ulo - pm, uhi + pm, vlo - pm, vhi + pm);
     }
+    int64_t r = in ? 1 : 0;
     if (!in) {
-        const bool origin = origin_in[f] != 0;
         if (flags[f] & FL_PLANAR) {
             // contains_node's planar ray cast, on the same (u,v) edge images
             const double sz = (double)size;
@@ -678,13 +696,28 @@ __global__ void k_cand_test(int64_t NC, const uint32_t *cand_f, const int64_t *c
                     if (uc < x) par = !par;
                 }
             }
-            in = origin != par;
+            r = ((origin_in[f] != 0) != par) ? 1 : 0;
         } else {
-            LoopView l{xyz + xoff[f], nv, origin};
-            in = loop_contains(l, node_center(face, i, j, kCoverLevel));
+            r = 2;
         }
     }
-    kept[c] = in ? 1 : 0;
+    kept[c] = r;
+}
+
+// Undecided candidates: exact S2 containment of the cell centre.
+__global__ void k_cand_exact(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
+                             const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const int64_t *xoff,
+                             const V3 *xyz, const int32_t *nvx, const uint8_t *origin_in, int64_t *kept)
+{
+    const int64_t c = tid64();
+    if (c >= NC || kept[c] != 2) return;
+    const uint32_t f = cand_f[c];
+    int face;
+    uint32_t i, j;
+    uint64_t id;
+    cand_cell(c, f, coff, st_id, st_i, st_j, finfo, face, i, j, id);
+    LoopView l{xyz + xoff[f], nvx[f], origin_in[f] != 0};
+    kept[c] = loop_contains(l, node_center(face, i, j, kCoverLevel)) ? 1 : 0;
 }
 
 // Per-footprint cell counts: direct-path count from the candidate scan plus
@@ -761,8 +794,9 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     uint64_t *st_id = st_id_.ensure(4 * n + 4);
     uint32_t *st_i = st_i_.ensure(4 * n + 4), *st_j = st_j_.ensure(4 * n + 4), *finfo = finfo_.ensure(n + 1);
     int64_t *ncand = ncand_.ensure(n + 1), *coff = coff_.ensure(n + 1);
+    uint4 *fbox = fbox_.ensure(n + 1);
     hipLaunchKernelGGL(k_setup, dim3(grid_for(n, 64)), dim3(64), 0, s, n, kind, voff, lat, lng, radius_m, xoff, xyz,
-                       status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, ncand);
+                       status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, ncand, fbox);
     int64_t *eoff = eoff_.ensure(n + 1);
     hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv);
     exclusive_scan_i64(nv, eoff, n, tmp_, s);
@@ -777,8 +811,10 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     int64_t *kept = kept_.ensure(NC + 1), *kpos = kpos_.ensure(NC + 2);
     if (NC > 0) {
         hipLaunchKernelGGL(k_cand_owner, dim3(grid_for(n, B)), dim3(B), 0, s, n, coff, cand_f);
-        hipLaunchKernelGGL(k_cand_test, dim3(grid_for(NC, B)), dim3(B), 0, s, NC, cand_f, coff, st_id, st_i, st_j, finfo,
-                           xoff, xyz, uv, nvx, orig, flags, kept);
+        hipLaunchKernelGGL(k_cand_test, dim3(grid_for(NC, kCandBlock)), dim3(kCandBlock), 0, s, NC, cand_f, coff, st_id,
+                           st_i, st_j, finfo, fbox, xoff, uv, nvx, orig, flags, kept);
+        hipLaunchKernelGGL(k_cand_exact, dim3(grid_for(NC, B)), dim3(B), 0, s, NC, cand_f, coff, st_id, st_i, st_j, finfo,
+                           xoff, xyz, nvx, orig, kept);
     }
     exclusive_scan_i64(kept, kpos, NC, tmp_, s);
     // hierarchical descent for the rest (big, multi-face, polyline footprints)

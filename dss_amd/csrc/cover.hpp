@@ -41,6 +41,7 @@ class CoverEngine {
     DevBuf<uint64_t> st_id_;
     DevBuf<uint32_t> st_i_, st_j_, finfo_, cand_f_;
     DevBuf<int64_t> ncand_, coff_, kept_, kpos_, dc64_, dpre_;
+    DevBuf<uint4> fbox_;
     bool tables_ = false;
 };
 
