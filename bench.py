@@ -43,7 +43,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=1)
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug only; invalid for the metric)")
-    ap.add_argument("--cpu-sample", type=int, default=20000, help="queries in the CPU-baseline sample (0: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=-1,
+                    help="queries in the CPU-baseline sample (-1: the whole step's batch, 0: skip)")
+    ap.add_argument("--no-verify", action="store_true", help="skip the full-size GPU-vs-oracle parity check")
+    ap.add_argument("--survey-model", type=int, default=1, help="also count SURVEY s8(d)'s per-query byte model")
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
 
@@ -88,8 +91,8 @@ def main():
     build_s = time.time() - tb
     n_post = int(ctx.L.dssg_index_num_postings(index))
     # keep intent cells for the CPU baseline before the next cover() reuses buffers
-    i_offs_h = D.copy_back(ctx, icells.offs, ni + 1, np.int64) if rank == 0 else None
-    i_cells_h = D.copy_back(ctx, icells.cells, int(i_offs_h[-1]), np.uint64) if rank == 0 else None
+    i_offs_h = D.copy_back(ctx, icells.offs, ni + 1, np.int64)
+    i_cells_h = D.copy_back(ctx, icells.cells, int(i_offs_h[-1]), np.uint64)
     log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s, index build {build_s:.2f}s, postings {n_post}")
 
     def step():
@@ -120,38 +123,49 @@ def main():
     value = world * nq * args.steps / elapsed
 
     # ------------------------------------------- phase timing + roofline
+    import ctypes as C
     ctx.L.dssg_set_timing(ctx.h, 1)
     cover_ms, join_ms, kern_ms = [], [], []
-    for _ in range(3):
+    for _ in range(5):
         cells, pairs = step()
-        a, b, c = (np.zeros(1), np.zeros(1), np.zeros(1))
-        import ctypes as C
         ca, cb, cc = C.c_double(), C.c_double(), C.c_double()
         ctx.L.dssg_phase_times(ctx.h, C.byref(ca), C.byref(cb), C.byref(cc))
         cover_ms.append(ca.value)
         join_ms.append(cb.value)
         kern_ms.append(cc.value)
     ctx.L.dssg_set_timing(ctx.h, 0)
-    import ctypes as C
     n_keys, n_units, n_runs, n_iters, n_tests = (C.c_int64() for _ in range(5))
     ctx.check(ctx.L.dssg_search_counters(ctx.h, C.byref(n_keys), C.byref(n_units), C.byref(n_runs), C.byref(n_iters),
                                          C.byref(n_tests)))
-    m_tot, d_tot = C.c_int64(), C.c_int64()
-    ctx.check(ctx.L.dssg_search_stats_device(ctx.h, index, cells.n, C.c_void_p(cells.offs), C.c_void_p(cells.cells),
-                                             D._stream_ptr(), C.byref(m_tot), C.byref(d_tot)))
     c_tot = int(cells.total_cells)
     r_tot = int(pairs.n)
-    join_bytes = 8 * c_tot + 12 * m_tot.value + 24 * d_tot.value + 8 * r_tot   # SURVEY s8(d) B_q summed
     kern_avg_ms = float(np.mean(kern_ms))
-    achieved = join_bytes / (kern_avg_ms * 1e-3) / 1e9
     cover_avg = float(np.mean(cover_ms))
     join_avg = float(np.mean(join_ms))
+    # Algorithmic bytes of one k_join launch: the batch's query
+    # inputs (24 B attributes + 8 B per covering cell), every posting of a
+    # cell the batch touches read once (28 B: entity id, alt pair, time
+    # pair), and the output pairs (8 B).
+    q_cells_h = D.copy_back(ctx, cells.cells, c_tot, np.uint64)
+    p_touched = touched_postings(i_cells_h, q_cells_h)
+    join_bytes = 24 * nq + 8 * c_tot + 28 * p_touched + 8 * r_tot
+    achieved = join_bytes / (kern_avg_ms * 1e-3) / 1e9
+    # SURVEY s8(d) per-query model (B_q summed over queries, each query
+    # charged for its own matched postings): what a query-at-a-time join
+    # would move; reported for reference, not as the roofline.
+    m_tot, d_tot = C.c_int64(), C.c_int64()
+    if args.survey_model:
+        ctx.check(ctx.L.dssg_search_stats_device(ctx.h, index, cells.n, C.c_void_p(cells.offs),
+                                                 C.c_void_p(cells.cells), D._stream_ptr(), C.byref(m_tot),
+                                                 C.byref(d_tot)))
+    survey_bytes = 8 * c_tot + 12 * m_tot.value + 24 * d_tot.value + 8 * r_tot
 
     result = None
     if rank == 0:
-        cpu = None
-        if args.cpu_sample > 0:
-            cpu = cpu_baseline(args, intents, ia, queries, qa, now, i_offs_h, i_cells_h)
+        cpu = parity = None
+        if args.cpu_sample != 0 and world == 1:
+            cpu, parity = cpu_baseline(args, ctx, intents, ia, queries, qa, now, i_offs_h, i_cells_h, cells, pairs)
+        traffic = pmc_traffic("k_join", nq, ni)
         result = {
             "metric": "4D conflict queries/sec vs N-intent airspace",
             "value": value,
@@ -175,12 +189,18 @@ def main():
             "join_work": {"keys": n_keys.value, "units": n_units.value, "runs": n_runs.value,
                           "wave_iters": n_iters.value, "lane_tests": n_tests.value},
             "index_build_s": build_s,
-            "roofline": {"kernel": "k_join (overlap join + fused filter)", "bound": "hbm",
+            "roofline": {"kernel": "k_join (overlap join + fused altitude/time filter)", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "algorithmic_bytes": join_bytes,
-                         "counts": {"C": c_tot, "M": m_tot.value, "D": d_tot.value, "R": r_tot}},
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic["bytes_per_launch"] if traffic else None,
+                         "traffic_source": traffic["source"] if traffic else None,
+                         "algorithmic_bytes": join_bytes, "launch_ms": kern_avg_ms,
+                         "counts": {"queries": nq, "C": c_tot, "P_touched": p_touched, "R": r_tot},
+                         "survey_per_query_model": {"bytes": survey_bytes, "M": m_tot.value, "D": d_tot.value,
+                                                    "equiv_GBs": survey_bytes / (kern_avg_ms * 1e-3) / 1e9}
+                         if args.survey_model else None},
             "cpu_baseline": cpu,
+            "parity": parity,
         }
         print(json.dumps(result), flush=True)
     ctx.L.dssg_index_free(index)
@@ -188,25 +208,64 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, intents, ia, queries, qa, now, i_offs, i_cells):
-    """The CPU restatement (oracle/, kind "port") timed on this host on a
-    bounded sample: cover `cpu_sample` queries + search them against the
-    same 1M-intent posting list (built untimed)."""
+def touched_postings(i_cells, q_cells):
+    """Postings whose cell is one of the batch's query cells (each counted once)."""
+    u, cnt = np.unique(i_cells, return_counts=True)
+    return int(cnt[np.isin(u, np.unique(q_cells), assume_unique=True)].sum())
+
+
+def pmc_traffic(kernel, nq, ni):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary (tools/pmc_summary.py --json; FETCH_SIZE x2 + WRITE_SIZE, the
+    gfx950 correction of MI355X_MICROARCH.md s HBM), if one exists for this
+    workload size."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    k = d.get("kernels", {}).get(kernel)
+    if not k or d.get("queries") != nq or d.get("intents") != ni:
+        return None
+    return {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": d.get("source", path)}
+
+
+def cpu_baseline(args, ctx, intents, ia, queries, qa, now, i_offs, i_cells, g_cells, g_pairs):
+    """The CPU restatement (oracle/, kind "port": pthreads over the box's
+    host cores) timed on the same step: cover the sample's query footprints
+    and search them against the same intent posting list (built untimed).
+    When the sample is the whole batch, the oracle's cell sets and pair set
+    are also compared with the GPU step's (full-size parity)."""
+    from dss_amd import device as D
     from oracle import oracle as O
     O.build()
-    n = min(args.cpu_sample, queries.n)
-    sub = queries.subset(np.arange(n))
+    n = queries.n if args.cpu_sample < 0 else min(args.cpu_sample, queries.n)
+    sub = queries if n == queries.n else queries.subset(np.arange(n))
     th = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     idx = O.Index(i_offs, i_cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1)
     t0 = time.perf_counter()
     qo, qc, _, _ = O.cover_batch(sub.kind, sub.voff, sub.lat, sub.lng, sub.radius_m, nthreads=th)
     t1 = time.perf_counter()
     tlo = np.maximum(qa.t0[:n], now)
-    idx.search(qo, qc, qa.alt_lo[:n], qa.alt_hi[:n], tlo, qa.t1[:n], nthreads=th)
+    rq, re = idx.search(qo, qc, qa.alt_lo[:n], qa.alt_hi[:n], tlo, qa.t1[:n], nthreads=th)
     t2 = time.perf_counter()
-    return {"value": n / (t2 - t0), "unit": "queries/s", "cores": th, "kind": "port",
-            "sample": f"{n} queries (cover + search) vs the full {intents.n}-intent index",
-            "coverings_per_s": n / (t1 - t0), "seconds": t2 - t0}
+    cpu = {"value": n / (t2 - t0), "unit": "queries/s", "cores": th, "kind": "port",
+           "sample": f"{n} of the step's {queries.n} queries (cover + search) vs the full {intents.n}-intent index",
+           "coverings_per_s": n / (t1 - t0), "seconds": t2 - t0}
+    parity = None
+    if n == queries.n and not args.no_verify:
+        g_offs = D.copy_back(ctx, g_cells.offs, n + 1, np.int64)
+        g_c = D.copy_back(ctx, g_cells.cells, int(g_offs[-1]), np.uint64)
+        gq = D.copy_back(ctx, g_pairs.q, int(g_pairs.n), np.uint32)
+        ge = D.copy_back(ctx, g_pairs.e, int(g_pairs.n), np.uint32)
+        gk = np.sort((gq.astype(np.uint64) << np.uint64(32)) | ge.astype(np.uint64))
+        ok = (rq.astype(np.uint64) << np.uint64(32)) | re.astype(np.uint64)
+        ok.sort()
+        parity = {"queries": n, "cells_equal": bool(np.array_equal(g_offs, qo) and np.array_equal(g_c, qc)),
+                  "pairs_equal": bool(np.array_equal(gk, ok)), "gpu_pairs": int(len(gk)), "oracle_pairs": int(len(ok)),
+                  "cells": int(len(qc))}
+    return cpu, parity
 
 
 if __name__ == "__main__":

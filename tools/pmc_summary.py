@@ -1,13 +1,21 @@
 #!/usr/bin/env python3
 """Summarize rocprofv3 output of tools/profile.sh: per kernel, the dispatch
 count, average duration (kernel trace) and the average of every collected
-counter per dispatch.  FETCH_SIZE is reported raw and x2 (gfx950 counts half
-the bytes of wide coalesced reads, MI355X_MICROARCH.md s HBM)."""
+counter per dispatch.
+
+HBM bytes per launch follow MI355X_MICROARCH.md s HBM: FETCH_SIZE and
+WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
+coalesced read, so hbm = 2 * 1024 * FETCH_SIZE + 1024 * WRITE_SIZE (an upper
+bound where a kernel's reads are narrower than 16 B per lane).
+
+usage: pmc_summary.py DIR [--json OUT --queries NQ --intents NI --source TAG]
+"""
+import argparse
 import csv
 import glob
+import json
 import os
 import re
-import sys
 from collections import defaultdict
 
 
@@ -16,30 +24,51 @@ def short(name):
     return m.group(1) if m else name[:40]
 
 
-def main(d):
+def collect(d):
     dur = defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        if not os.path.basename(f).startswith("kt"):
+            continue
         for r in csv.DictReader(open(f)):
-            if os.path.basename(f).startswith("kt"):
-                dur[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+            dur[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     ctr = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             ctr[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return dur, ctr
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir", nargs="?", default="gpurun_out/prof")
+    ap.add_argument("--json")
+    ap.add_argument("--queries", type=int)
+    ap.add_argument("--intents", type=int)
+    ap.add_argument("--source", default="")
+    a = ap.parse_args()
+    dur, ctr = collect(a.dir)
     names = sorted(set(dur) | set(ctr), key=lambda k: -sum(dur.get(k, [0])))
     cols = sorted({c for k in ctr for c in ctr[k]})
-    print("kernel,dispatches,avg_ms,total_ms," + ",".join(cols) + (",FETCH_SIZE_x2_bytes" if "FETCH_SIZE" in cols else ""))
+    print("kernel,dispatches,avg_ms,total_ms," + ",".join(cols) + ",hbm_bytes_per_launch")
+    out = {}
     for k in names:
         ds = dur.get(k, [])
+        avg = lambda c: (sum(ctr[k][c]) / len(ctr[k][c])) if ctr[k].get(c) else None  # noqa: E731
         row = [k, str(len(ds)), f"{(sum(ds) / len(ds)) if ds else 0:.4f}", f"{sum(ds):.3f}"]
-        for c in cols:
-            v = ctr[k].get(c, [])
-            row.append(f"{sum(v) / len(v):.6g}" if v else "")
-        if "FETCH_SIZE" in cols:
-            v = ctr[k].get("FETCH_SIZE", [])
-            row.append(f"{2 * 1024 * sum(v) / len(v):.6g}" if v else "")  # FETCH_SIZE is in KiB
+        row += [f"{avg(c):.6g}" if avg(c) is not None else "" for c in cols]
+        f, w = avg("FETCH_SIZE"), avg("WRITE_SIZE")
+        hbm = 2 * 1024 * f + 1024 * w if f is not None and w is not None else None
+        row.append(f"{hbm:.6g}" if hbm is not None else "")
         print(",".join(row))
+        out[k] = {"dispatches": len(ds), "avg_ms": (sum(ds) / len(ds)) if ds else None,
+                  "fetch_kib": f, "write_kib": w, "hbm_bytes_per_launch": hbm}
+    if a.json:
+        with open(a.json, "w") as fh:
+            json.dump({"source": a.source, "queries": a.queries, "intents": a.intents,
+                       "correction": "hbm = 2*1024*FETCH_SIZE + 1024*WRITE_SIZE (MI355X_MICROARCH.md s HBM)",
+                       "kernels": {k: v for k, v in out.items() if v["hbm_bytes_per_launch"] is not None}},
+                      fh, indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof")
+    main()
