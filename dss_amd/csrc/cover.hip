@@ -144,15 +144,133 @@ __device__ int start_cells(const FaceBox &b, int fc, uint64_t *id, uint32_t *ii,
     return cnt;
 }
 
-// One thread per footprint.
-__global__ void k_setup(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
-                        const float *radius_m, const int64_t *xoff, V3 *xyz, int32_t *status, double *area_out,
-                        uint8_t *mode, uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx, double2 *uv,
-                        uint64_t *st_id, uint32_t *st_i, uint32_t *st_j, uint32_t *finfo, int64_t *ncand,
-                        uint4 *fbox)
+// ---------------------------------------------------------------------------
+// Per-vertex pre-pass (FAST path).  The serial per-footprint work of loop
+// construction is dominated by transcendental FP64 (Go's Cephes trig in
+// PointFromLatLng and in every fan triangle's PointArea), so it is spread one
+// thread per vertex slot: no divergence between footprints of different
+// kind or size, and the per-footprint kernel only sums.
+//
+// k_circle_frames: RegularLoop's frame per circle (centre, ortho basis,
+// cos/sin of the radius) -- regular_loop.go, computed once per circle.
+struct CircleFrame {
+    V3 c, c0, c1;
+    double z, rr;
+};
+__global__ void k_circle_frames(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat,
+                                const double *lng, const float *radius_m, CircleFrame *fr)
 {
-    int64_t f = tid64();
+    const int64_t f = tid64();
+    if (f >= n || kind[f] != DSSG_KIND_CIRCLE) return;
+    const V3 c = point_from_degrees(lat[voff[f]], lng[voff[f]]);
+    const double radius = (double)radius_m[f] / DSS_RADIUS_EARTH_M;
+    const V3 c1 = ortho(c), c0 = cross(c1, c);
+    fr[f] = CircleFrame{c, c0, c1, go_cos(radius), go_sin(radius)};
+}
+
+// Owner footprint of every vertex slot.
+__global__ void k_vowner(int64_t n, const int64_t *xoff, uint32_t *vown)
+{
+    const int64_t f = tid64();
     if (f >= n) return;
+    for (int64_t x = xoff[f]; x < xoff[f + 1]; x++) vown[x] = (uint32_t)f;
+}
+
+// One thread per vertex slot: S2 point of a polygon vertex
+// (PointFromLatLng(LatLngFromDegrees)) or of a RegularLoop vertex.
+__global__ void k_verts(int64_t nx, const uint32_t *vown, const int32_t *kind, const int64_t *voff,
+                        const double *lat, const double *lng, const int64_t *xoff, const CircleFrame *fr, V3 *xyz)
+{
+    const int64_t x = tid64();
+    if (x >= nx) return;
+    const uint32_t f = vown[x];
+    const int i = (int)(x - xoff[f]);
+    if (kind[f] == DSSG_KIND_CIRCLE) {
+        const CircleFrame F = fr[f];
+        const double px = F.rr * c_circle_cos[i], py = F.rr * c_circle_sin[i], pz = F.z;
+        xyz[x] = normalize(v3(F.c0.x * px + F.c1.x * py + F.c.x * pz, F.c0.y * px + F.c1.y * py + F.c.y * pz,
+                              F.c0.z * px + F.c1.z * py + F.c.z * pz));
+    } else {
+        xyz[x] = point_from_degrees(lat[voff[f] + i], lng[voff[f] + i]);
+    }
+}
+
+// One thread per vertex slot of a polygon with n >= 3 vertices: the fan
+// triangle terms of loop.go surfaceIntegralFloat64(SignedArea) for the loop
+// as given (fwd, slot i = triangle (v0, vi, vi+1)) and for its reversal
+// (rev, triangle (v[n-1], v[n-1-i], v[n-2-i])), i = 1 .. n-2.  The fan
+// origin never moves for loops whose vertices all lie within
+// DSS_SURFACE_MAX_LENGTH of v0; any other loop, or an undecided sign, goes
+// to the exact per-footprint path (fan_fail).
+__global__ void k_fan(int64_t nx, const uint32_t *vown, const int32_t *kind, const int64_t *nslots, const int64_t *xoff,
+                      const V3 *xyz, double *fwd, double *rev, uint8_t *fan_fail)
+{
+    const int64_t x = tid64();
+    if (x >= nx) return;
+    const uint32_t f = vown[x];
+    if (kind[f] == DSSG_KIND_CIRCLE) return;
+    const int n = (int)nslots[f];
+    const int i = (int)(x - xoff[f]);
+    if (n < 3 || i < 1 || i > n - 2) return;
+    const V3 *p = xyz + xoff[f];
+    bool fail = false;
+    const V3 a = p[0], b = p[i], c = p[i + 1];
+    fail |= angle(c, a) > DSS_SURFACE_MAX_LENGTH;
+    fwd[x] = fastp::signed_area(a, b, c, fail);
+    const V3 ra = p[n - 1], rb = p[n - 1 - i], rc = p[n - 2 - i];
+    fail |= angle(rc, ra) > DSS_SURFACE_MAX_LENGTH;
+    rev[x] = fastp::signed_area(ra, rb, rc, fail);
+    if (fail) fan_fail[f] = 1;
+}
+
+// loop.go Area from the precomputed fan terms (same summation order as
+// surfaceIntegralFloat64), then loopAreaKm2.  Fails over to the exact path
+// in the bands where Area consults IsNormalized.
+__device__ __forceinline__ double fan_area_km2(const double *t, int n, bool &fail)
+{
+    double area = 0;
+    for (int i = 1; i + 1 < n; i++) area += t[i];
+    const double max_error = DSS_TURN_ANGLE_ERR_PER_VERTEX * (double)n;
+    if (area < 0) area += 4 * DSS_PI;
+    if (area > 4 * DSS_PI) area = 4 * DSS_PI;
+    if (area < 0) area = 0;
+    fail |= area < max_error || area > (4 * DSS_PI - max_error);
+    return (area * DSS_EARTH_AREA_KM2) / 4.0 * DSS_PI;
+}
+
+template <bool FAST>
+__device__ __forceinline__ void origin_of(LoopView &l, bool &fail)
+{
+    if constexpr (FAST) fastp::loop_init_origin(l, fail);
+    else loop_init_origin(l);
+}
+template <bool FAST>
+__device__ __forceinline__ double area_km2_of(const LoopView &l, bool &fail)
+{
+    if constexpr (FAST) return fastp::loop_area_km2(l, fail);
+    else return loop_area_km2(l);
+}
+
+// One thread per footprint.  FAST: triage-only predicates (no out-of-line
+// exact arithmetic, so no call-ABI spills); a footprint the triage cannot
+// decide is appended to slow_list and redone by the exact instance, a small
+// grid that strides over that list only.
+template <bool FAST>
+__device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsigned int *slow_n, const int32_t *kind,
+                                          const int64_t *voff, const double *lat, const double *lng,
+                                          const float *radius_m, const int64_t *xoff, V3 *xyz, int32_t *status,
+                                          double *area_out, uint8_t *mode, uint8_t *origin_in, uint8_t *fmask,
+                                          uint8_t *flags, int32_t *nvx, double2 *uv, uint64_t *st_id, uint32_t *st_i,
+                                          uint32_t *st_j, uint32_t *finfo, int64_t *ncand, uint4 *fbox,
+                                          const double *fwd, const double *rev, const uint8_t *fan_fail)
+{
+    bool fail = false;
+    auto bail = [&]() {
+        if constexpr (FAST) {
+            if (fail) slow_list[atomicAdd(slow_n, 1u)] = (uint32_t)f;
+        }
+        return FAST && fail;
+    };
     int k = kind[f];
     int64_t v0 = voff[f];
     V3 *p = xyz + xoff[f];
@@ -169,19 +287,22 @@ __global__ void k_setup(int64_t n, const int32_t *kind, const int64_t *voff, con
         else if (!(r > 0)) st = DSSG_ST_RADIUS;
         else {
             // regular_loop.go RegularLoop(center, DistanceMetersToAngle(r), 20)
-            V3 c = point_from_degrees(la, ln);
             double radius = (double)r / DSS_RADIUS_EARTH_M;
-            V3 c1 = ortho(c), c0 = cross(c1, c);
-            double z = go_cos(radius), rr = go_sin(radius);
-            for (int i = 0; i < 20; i++) {
-                double px = rr * c_circle_cos[i], py = rr * c_circle_sin[i], pz = z;
-                V3 q = v3(c0.x * px + c1.x * py + c.x * pz, c0.y * px + c1.y * py + c.y * pz,
-                          c0.z * px + c1.z * py + c.z * pz);
-                p[i] = normalize(q);
+            if constexpr (!FAST) {  // FAST: k_circle_frames + k_verts wrote the vertices
+                V3 c = point_from_degrees(la, ln);
+                V3 c1 = ortho(c), c0 = cross(c1, c);
+                double z = go_cos(radius), rr = go_sin(radius);
+                for (int i = 0; i < 20; i++) {
+                    double px = rr * c_circle_cos[i], py = rr * c_circle_sin[i], pz = z;
+                    V3 q = v3(c0.x * px + c1.x * py + c.x * pz, c0.y * px + c1.y * py + c.y * pz,
+                              c0.z * px + c1.z * py + c.z * pz);
+                    p[i] = normalize(q);
+                }
             }
             nv = 20;
             l.n = 20;
-            loop_init_origin(l);
+            origin_of<FAST>(l, fail);
+            if (bail()) return;
             md = MODE_LOOP;
             small = radius < 0.5;
         }
@@ -195,18 +316,26 @@ __global__ void k_setup(int64_t n, const int32_t *kind, const int64_t *voff, con
         }
         if (st == DSSG_ST_OK && nv < 3) st = DSSG_ST_NOT_ENOUGH_POINTS;
         if (st == DSSG_ST_OK) {
-            for (int i = 0; i < nv; i++) p[i] = point_from_degrees(lat[v0 + i], lng[v0 + i]);
+            if constexpr (!FAST) {  // FAST: k_verts wrote the vertices
+                for (int i = 0; i < nv; i++) p[i] = point_from_degrees(lat[v0 + i], lng[v0 + i]);
+            } else {
+                fail |= fan_fail[f] != 0;
+            }
             l.n = nv;
-            loop_init_origin(l);
-            area = loop_area_km2(l);
+            origin_of<FAST>(l, fail);
+            if constexpr (FAST) area = fan_area_km2(fwd + xoff[f], nv, fail);
+            else area = area_km2_of<FAST>(l, fail);
+            if (bail()) return;
             if (area > DSS_MAX_AREA_KM2) {  // Q4: reverse in place and rebuild
                 for (int i = 0, j = nv - 1; i < j; i++, j--) {
                     V3 t = p[i];
                     p[i] = p[j];
                     p[j] = t;
                 }
-                loop_init_origin(l);
-                area = loop_area_km2(l);
+                origin_of<FAST>(l, fail);
+                if constexpr (FAST) area = fan_area_km2(rev + xoff[f], nv, fail);
+                else area = area_km2_of<FAST>(l, fail);
+                if (bail()) return;
             }
             if (area > DSS_MAX_AREA_KM2) st = DSSG_ST_AREA_TOO_LARGE;
             else if (area <= 0) md = MODE_POLYLINE;  // Q3: open polyline, no closing edge
@@ -298,6 +427,27 @@ __global__ void k_setup(int64_t n, const int32_t *kind, const int64_t *voff, con
     nvx[f] = nv;
 }
 
+template <bool FAST>
+__global__ __launch_bounds__(64) void k_setup(uint32_t *slow_list, unsigned int *slow_n, int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
+                        const float *radius_m, const int64_t *xoff, V3 *xyz, int32_t *status, double *area_out,
+                        uint8_t *mode, uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx, double2 *uv,
+                        uint64_t *st_id, uint32_t *st_i, uint32_t *st_j, uint32_t *finfo, int64_t *ncand,
+                        uint4 *fbox, const double *fwd, const double *rev, const uint8_t *fan_fail)
+{
+    int64_t f = tid64();
+    if constexpr (FAST) {
+        if (f >= n) return;
+    } else {  // a small grid strides over the footprints the triage left undecided
+        for (int64_t i = f; i < (int64_t)*slow_n; i += (int64_t)gridDim.x * blockDim.x)
+            setup_one<false>(slow_list[i], nullptr, nullptr, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out,
+                             mode, origin_in, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, ncand, fbox, nullptr,
+                             nullptr, nullptr);
+        return;
+    }
+    setup_one<true>(f, slow_list, slow_n, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out, mode, origin_in,
+                    fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, ncand, fbox, fwd, rev, fan_fail);
+}
+
 __device__ __forceinline__ int num_edges(uint8_t md, int nv) { return md == MODE_LOOP ? nv : (md == MODE_POLYLINE ? nv - 1 : 0); }
 
 __global__ void k_edge_counts(int64_t n, const uint8_t *mode, const uint8_t *fmask, const uint8_t *flags, const int32_t *nvx,
@@ -309,7 +459,7 @@ __global__ void k_edge_counts(int64_t n, const uint8_t *mode, const uint8_t *fma
 }
 
 // Clip every edge to every touched face (ascending face order).
-__global__ void k_clip(int64_t n, const int64_t *xoff, const V3 *xyz, const uint8_t *mode, const uint8_t *fmask,
+__global__ __launch_bounds__(64) void k_clip(int64_t n, const int64_t *xoff, const V3 *xyz, const uint8_t *mode, const uint8_t *fmask,
                        const uint8_t *flags, const int32_t *nvx, const int64_t *eoff, double4 *clip_f, double4 *clip_c,
                        uint8_t *cflags)
 {
@@ -378,7 +528,7 @@ __device__ bool contains_node(const LoopView &l, bool planar, const double4 *cli
 // Count (pass 0) or write (pass 1) start nodes; big loops also get whole-face
 // nodes for faces without edges whose centre the loop contains.
 template <int PASS>
-__global__ void k_start(int64_t n, const int64_t *xoff, const V3 *xyz, const uint8_t *mode, const uint8_t *fmask,
+__global__ __launch_bounds__(64) void k_start(int64_t n, const int64_t *xoff, const V3 *xyz, const uint8_t *mode, const uint8_t *fmask,
                         const uint8_t *flags, const uint8_t *origin_in, const int32_t *nvx, const int64_t *eoff,
                         const double4 *clip_c, const uint8_t *cflags, int64_t *cnt, const int64_t *soff,
                         uint32_t *nf, uint64_t *nid, uint32_t *ni, uint32_t *nj, uint32_t *nmeta)
@@ -458,7 +608,7 @@ __device__ bool polyline_intersects_cell(const V3 *p, int nv, int face, double u
 }
 
 // Classify each frontier node: 0 drop, 1 keep (done), 2 subdivide (4 children).
-__global__ void k_expand_count(int64_t nn, const uint32_t *nf, const uint32_t *ni, const uint32_t *nj,
+__global__ __launch_bounds__(64) void k_expand_count(int64_t nn, const uint32_t *nf, const uint32_t *ni, const uint32_t *nj,
                                const uint32_t *nmeta, uint8_t *act, int64_t *cnt, const int64_t *xoff, const V3 *xyz,
                                const uint8_t *mode, const uint8_t *fmask, const uint8_t *origin_in, const int32_t *nvx,
                                const int64_t *eoff, const double4 *clip_f, const double4 *clip_c, const uint8_t *cflags,
@@ -705,7 +855,7 @@ __global__ void k_cand_test(int64_t NC, const uint32_t *cand_f, const int64_t *c
 }
 
 // Undecided candidates: exact S2 containment of the cell centre.
-__global__ void k_cand_exact(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
+__global__ __launch_bounds__(256) void k_cand_exact(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
                              const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const int64_t *xoff,
                              const V3 *xyz, const int32_t *nvx, const uint8_t *origin_in, int64_t *kept)
 {
@@ -795,8 +945,28 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     uint32_t *st_i = st_i_.ensure(4 * n + 4), *st_j = st_j_.ensure(4 * n + 4), *finfo = finfo_.ensure(n + 1);
     int64_t *ncand = ncand_.ensure(n + 1), *coff = coff_.ensure(n + 1);
     uint4 *fbox = fbox_.ensure(n + 1);
-    hipLaunchKernelGGL(k_setup, dim3(grid_for(n, 64)), dim3(64), 0, s, n, kind, voff, lat, lng, radius_m, xoff, xyz,
-                       status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, ncand, fbox);
+    uint32_t *slow = slow_.ensure(n + 1);
+    unsigned int *slow_n = slow_n_.ensure(1);
+    uint8_t *fan_fail = fanf_.ensure(n + 1);
+    CircleFrame *frames = (CircleFrame *)frames_.ensure(sizeof(CircleFrame) * (n + 1));
+    uint32_t *vown = vown_.ensure(nx + 1);
+    double *fwd = fwd_.ensure(nx + 1), *rev = rev_.ensure(nx + 1);
+    DSS_HIP(hipMemsetAsync(slow_n, 0, sizeof(unsigned int), s));
+    DSS_HIP(hipMemsetAsync(fan_fail, 0, n, s));
+    // per-vertex pre-pass: frames, owners, S2 points, fan terms
+    hipLaunchKernelGGL(k_circle_frames, dim3(grid_for(n, B)), dim3(B), 0, s, n, kind, voff, lat, lng, radius_m, frames);
+    hipLaunchKernelGGL(k_vowner, dim3(grid_for(n, B)), dim3(B), 0, s, n, xoff, vown);
+    if (nx > 0) {
+        hipLaunchKernelGGL(k_verts, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, kind, voff, lat, lng, xoff, frames, xyz);
+        hipLaunchKernelGGL(k_fan, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, kind, nv, xoff, xyz,
+                           fwd, rev, fan_fail);
+    }
+    hipLaunchKernelGGL(k_setup<true>, dim3(grid_for(n, 64)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng,
+                       radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo,
+                       ncand, fbox, fwd, rev, fan_fail);
+    hipLaunchKernelGGL(k_setup<false>, dim3(min(grid_for(n, 64), 512u)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat,
+                       lng, radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j,
+                       finfo, ncand, fbox, nullptr, nullptr, nullptr);
     int64_t *eoff = eoff_.ensure(n + 1);
     hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv);
     exclusive_scan_i64(nv, eoff, n, tmp_, s);

@@ -29,6 +29,11 @@ class CoverEngine {
     DevBuf<int32_t> status_, nvx_;
     DevBuf<double> area_, xyz_;
     DevBuf<uint8_t> mode_, orig_, fmask_, flags_, cflags_, act_;
+    DevBuf<uint32_t> slow_, vown_;
+    DevBuf<uint8_t> fanf_;
+    DevBuf<double> fwd_, rev_;
+    DevBuf<unsigned char> frames_;
+    DevBuf<unsigned int> slow_n_;
     DevBuf<double4> clipf_, clipc_;
     DevBuf<unsigned char> tmp_;
     DevBuf<int> flag_;

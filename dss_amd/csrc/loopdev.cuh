@@ -297,5 +297,62 @@ DSS_HD double loop_area(const LoopView &l)
 // pkg/geo/s2.go:89-95 loopAreaKm2 -- (Area * E) / 4.0 * math.Pi (quirk Q1)
 DSS_HD double loop_area_km2(const LoopView &l) { return (loop_area(l) * DSS_EARTH_AREA_KM2) / 4.0 * DSS_PI; }
 
+// ------------------------------------------------- triage-only loop pieces
+// (s2dev.cuh fastp): same results as the exact versions above whenever
+// `fail` stays false; Area fails over to the exact path in the two bands
+// where loop.go Area consults IsNormalized (the loop bound).
+namespace fastp {
+DSS_HD bool loop_contains(const LoopView &l, V3 p, bool &fail)
+{
+    EdgeCrosser e;
+    e.init(origin_point(), p);
+    e.restart_at(l.vertex(0));
+    bool inside = l.origin_inside;
+    for (int i = 1; i <= l.n; i++) inside = inside != edge_or_vertex_chain_crossing(e, l.vertex(i), fail);
+    return inside;
+}
+DSS_HD void loop_init_origin(LoopView &l, bool &fail)
+{
+    bool v1_inside = !eq(l.v[0], l.v[1]) && !eq(l.v[2], l.v[1]) && angle_contains_vertex(l.v[0], l.v[1], l.v[2], fail);
+    l.origin_inside = false;
+    if (v1_inside != loop_contains(l, l.v[1], fail)) l.origin_inside = true;
+}
+DSS_HD double signed_area(V3 a, V3 b, V3 c, bool &fail) { return (double)robust_sign(a, b, c, fail) * point_area(a, b, c); }
+DSS_HD double loop_signed_area_sum(const LoopView &l, bool &fail)
+{
+    const double max_length = DSS_SURFACE_MAX_LENGTH;
+    double sum = 0;
+    V3 v0 = l.vertex(0), origin = v0;
+    for (int i = 1; i + 1 < l.n; i++) {
+        V3 vi = l.vertex(i), vi1 = l.vertex(i + 1);
+        if (angle(vi1, origin) > max_length) {
+            V3 old = origin;
+            if (eq(origin, v0)) {
+                origin = normalize(point_cross(v0, vi));
+            } else if (angle(vi, v0) < max_length) {
+                origin = v0;
+            } else {
+                origin = cross(v0, old);
+                sum += signed_area(v0, old, origin, fail);
+            }
+            sum += signed_area(old, vi, origin, fail);
+        }
+        sum += signed_area(origin, vi, vi1, fail);
+    }
+    if (!eq(origin, v0)) sum += signed_area(origin, l.vertex(l.n - 1), v0, fail);
+    return sum;
+}
+DSS_HD double loop_area_km2(const LoopView &l, bool &fail)
+{
+    double area = loop_signed_area_sum(l, fail);
+    const double max_error = turning_angle_max_error(l);
+    if (area < 0) area += 4 * DSS_PI;
+    if (area > 4 * DSS_PI) area = 4 * DSS_PI;
+    if (area < 0) area = 0;
+    fail |= area < max_error || area > (4 * DSS_PI - max_error);
+    return (area * DSS_EARTH_AREA_KM2) / 4.0 * DSS_PI;
+}
+}  // namespace fastp
+
 }  // namespace s2
 }  // namespace dss

@@ -283,6 +283,85 @@ struct EdgeCrosser {
     }
 };
 
+// ------------------------------------------------- triage-only predicates
+// Variants for the hot kernels: they never reach the exact arithmetic
+// (exact_sign / crossing_sign_slow are out-of-line calls whose ABI spills
+// would dominate a one-thread-per-footprint kernel).  A case the triage
+// cannot decide sets `fail`; the caller then recomputes that footprint on
+// the exact path.  Whenever `fail` stays false the result equals the exact
+// predicate's (triage_sign is exact when it decides).
+namespace fastp {
+DSS_HD int robust_sign(V3 a, V3 b, V3 c, bool &fail)
+{
+    int s = triage_sign(a, b, c);
+    // expensive_sign answers INDETERMINATE itself for repeated points (the
+    // closed rings of the prober fixtures); only the rest needs exact_sign
+    if (s == INDETERMINATE && !(eq(a, b) || eq(b, c) || eq(c, a))) fail = true;
+    return s;
+}
+DSS_HD bool ordered_ccw(V3 a, V3 b, V3 c, V3 o, bool &fail)
+{
+    int sum = 0;
+    if (robust_sign(b, o, a, fail) != CLOCKWISE) sum++;
+    if (robust_sign(c, o, b, fail) != CLOCKWISE) sum++;
+    if (robust_sign(a, o, c, fail) == COUNTERCLOCKWISE) sum++;
+    return sum >= 2;
+}
+DSS_HD bool vertex_crossing(V3 a, V3 b, V3 c, V3 d, bool &fail)
+{
+    if (eq(a, b) || eq(c, d)) return false;
+    if (eq(a, c)) return eq(b, d) || ordered_ccw(ortho(a), d, b, a, fail);
+    if (eq(b, d)) return ordered_ccw(ortho(b), c, a, b, fail);
+    if (eq(a, d)) return eq(b, c) || ordered_ccw(ortho(a), c, b, a, fail);
+    if (eq(b, c)) return ordered_ccw(ortho(b), d, a, b, fail);
+    return false;
+}
+DSS_HD bool angle_contains_vertex(V3 a, V3 b, V3 c, bool &fail) { return !ordered_ccw(ortho(b), c, a, b, fail); }
+// EdgeCrosser::chain_crossing_sign with crossing_sign_slow inlined minus
+// its expensive_sign calls.
+DSS_HD int chain_crossing_sign(EdgeCrosser &x, V3 d, bool &fail)
+{
+    const int bda = triage_sign(x.a, x.b, d);
+    if (x.acb == -bda && bda != INDETERMINATE) {
+        x.c = d;
+        x.acb = -bda;
+        return DO_NOT_CROSS;
+    }
+    int result;
+    const double max_error = (1.5 + 1 / __builtin_sqrt(3.0)) * DSS_DBL_EPS;
+    if ((dot(x.c, x.a_tangent) > max_error && dot(d, x.a_tangent) > max_error) ||
+        (dot(x.c, x.b_tangent) > max_error && dot(d, x.b_tangent) > max_error)) {
+        result = DO_NOT_CROSS;
+    } else if (eq(x.a, x.c) || eq(x.a, d) || eq(x.b, x.c) || eq(x.b, d)) {
+        result = MAYBE_CROSS;
+    } else if (eq(x.a, x.b) || eq(x.c, d)) {
+        result = DO_NOT_CROSS;
+    } else if (x.acb == INDETERMINATE || bda == INDETERMINATE) {
+        fail = true;
+        result = DO_NOT_CROSS;
+    } else if (bda != x.acb) {
+        result = DO_NOT_CROSS;
+    } else if (-robust_sign(x.c, d, x.b, fail) != x.acb) {
+        result = DO_NOT_CROSS;
+    } else if (robust_sign(x.c, d, x.a, fail) != x.acb) {
+        result = DO_NOT_CROSS;
+    } else {
+        result = CROSS;
+    }
+    x.c = d;
+    x.acb = -bda;
+    return result;
+}
+DSS_HD bool edge_or_vertex_chain_crossing(EdgeCrosser &x, V3 d, bool &fail)
+{
+    const V3 c0 = x.c;
+    const int s = chain_crossing_sign(x, d, fail);
+    if (s == DO_NOT_CROSS) return false;
+    if (s == CROSS) return true;
+    return vertex_crossing(x.a, x.b, c0, d, fail);
+}
+}  // namespace fastp
+
 // ------------------------------------------------------------ projections
 // stuv.go (quadratic projection)
 constexpr int kMaxLevel = 30;
