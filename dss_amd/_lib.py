@@ -89,6 +89,9 @@ def load():
         L.dssg_area_to_cell_ids.argtypes = [vp, C.c_char_p, P(u64), i64, P(i64), P(i32), P(d)]
         L.dssg_index_build.argtypes = [vp, i64, P(i64), P(u64), P(f), P(f), P(i64), P(i64), P(i32), P(vp)]
         L.dssg_index_build_device.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, P(vp)]
+        L.dssg_index_build_range.argtypes = [vp, i64, P(i64), P(u64), P(f), P(f), P(i64), P(i64), P(i32), u64, u64,
+                                             P(vp)]
+        L.dssg_index_build_range_device.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, u64, u64, vp, P(vp)]
         L.dssg_index_free.argtypes = [vp]
         L.dssg_index_free.restype = None
         L.dssg_index_num_postings.argtypes = [vp]

@@ -306,11 +306,13 @@ int dssg_area_to_cell_ids(dssg_ctx *ctx, const char *area, uint64_t *out_cells, 
     return rc;
 }
 
-int dssg_index_build_device(dssg_ctx *ctx, int64_t n, const int64_t *d_cell_offs, const uint64_t *d_cells,
-                            const float *d_alt_lo, const float *d_alt_hi, const int64_t *d_t0, const int64_t *d_t1,
-                            const int32_t *d_owner, void *stream, dssg_index **out)
+int dssg_index_build_range_device(dssg_ctx *ctx, int64_t n, const int64_t *d_cell_offs, const uint64_t *d_cells,
+                                  const float *d_alt_lo, const float *d_alt_hi, const int64_t *d_t0, const int64_t *d_t1,
+                                  const int32_t *d_owner, uint64_t cell_lo, uint64_t cell_hi, void *stream,
+                                  dssg_index **out)
 {
-    if (!ctx || !out || n < 0 || !d_cell_offs || (n > 0 && (!d_alt_lo || !d_alt_hi || !d_t0 || !d_t1)))
+    if (!ctx || !out || n < 0 || !d_cell_offs || (n > 0 && (!d_alt_lo || !d_alt_hi || !d_t0 || !d_t1)) ||
+        cell_lo > cell_hi)
         return DSSG_ERR_INVALID;
     *out = nullptr;
     dssg_index *idx = new (std::nothrow) dssg_index();
@@ -318,7 +320,7 @@ int dssg_index_build_device(dssg_ctx *ctx, int64_t n, const int64_t *d_cell_offs
     idx->device = ctx->device;
     int rc = guarded(ctx, [&] {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-        ctx->search.build(idx, n, d_cell_offs, d_cells, d_alt_lo, d_alt_hi, d_t0, d_t1, d_owner, s);
+        ctx->search.build(idx, n, d_cell_offs, d_cells, d_alt_lo, d_alt_hi, d_t0, d_t1, d_owner, cell_lo, cell_hi, s);
     });
     if (rc) {
         delete idx;
@@ -328,8 +330,17 @@ int dssg_index_build_device(dssg_ctx *ctx, int64_t n, const int64_t *d_cell_offs
     return DSSG_OK;
 }
 
-int dssg_index_build(dssg_ctx *ctx, int64_t n, const int64_t *cell_offs, const uint64_t *cells, const float *alt_lo,
-                     const float *alt_hi, const int64_t *t0, const int64_t *t1, const int32_t *owner, dssg_index **out)
+int dssg_index_build_device(dssg_ctx *ctx, int64_t n, const int64_t *d_cell_offs, const uint64_t *d_cells,
+                            const float *d_alt_lo, const float *d_alt_hi, const int64_t *d_t0, const int64_t *d_t1,
+                            const int32_t *d_owner, void *stream, dssg_index **out)
+{
+    return dssg_index_build_range_device(ctx, n, d_cell_offs, d_cells, d_alt_lo, d_alt_hi, d_t0, d_t1, d_owner, 0,
+                                         ~0ull, stream, out);
+}
+
+int dssg_index_build_range(dssg_ctx *ctx, int64_t n, const int64_t *cell_offs, const uint64_t *cells,
+                           const float *alt_lo, const float *alt_hi, const int64_t *t0, const int64_t *t1,
+                           const int32_t *owner, uint64_t cell_lo, uint64_t cell_hi, dssg_index **out)
 {
     if (!ctx || !out || n < 0 || !cell_offs) return DSSG_ERR_INVALID;
     *out = nullptr;
@@ -354,7 +365,13 @@ int dssg_index_build(dssg_ctx *ctx, int64_t n, const int64_t *cell_offs, const u
         DSS_HIP(hipStreamSynchronize(s));
     });
     if (rc) return rc;
-    return dssg_index_build_device(ctx, n, o, c, lo, hi, a0, a1, ow, nullptr, out);
+    return dssg_index_build_range_device(ctx, n, o, c, lo, hi, a0, a1, ow, cell_lo, cell_hi, nullptr, out);
+}
+
+int dssg_index_build(dssg_ctx *ctx, int64_t n, const int64_t *cell_offs, const uint64_t *cells, const float *alt_lo,
+                     const float *alt_hi, const int64_t *t0, const int64_t *t1, const int32_t *owner, dssg_index **out)
+{
+    return dssg_index_build_range(ctx, n, cell_offs, cells, alt_lo, alt_hi, t0, t1, owner, 0, ~0ull, out);
 }
 
 void dssg_index_free(dssg_index *idx)

@@ -55,5 +55,10 @@ inline unsigned grid_for(int64_t n, unsigned block) { return (unsigned)((n + blo
 // returns nothing; implemented in scan.hip with hipcub.
 void selftest_math(int op, int64_t n, const double *x, const double *y, double *out, hipStream_t s);
 void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, DevBuf<unsigned char> &tmp, hipStream_t s);
+// perm = footprint indices with every non-circle before every circle (order
+// within each part unspecified): per-footprint kernels then run one kind's
+// code path per wave.
+void partition_polygons_first(const int32_t *kind, uint32_t *perm, unsigned long long *nsel, int64_t n,
+                              DevBuf<unsigned char> &tmp, hipStream_t s);
 
 }  // namespace dss

@@ -195,24 +195,34 @@ __global__ void k_verts(int64_t nx, const uint32_t *vown, const int32_t *kind, c
     }
 }
 
-// One thread per vertex slot of a polygon with n >= 3 vertices: the fan
-// triangle terms of loop.go surfaceIntegralFloat64(SignedArea) for the loop
-// as given (fwd, slot i = triangle (v0, vi, vi+1)) and for its reversal
-// (rev, triangle (v[n-1], v[n-1-i], v[n-2-i])), i = 1 .. n-2.  The fan
-// origin never moves for loops whose vertices all lie within
-// DSS_SURFACE_MAX_LENGTH of v0; any other loop, or an undecided sign, goes
-// to the exact per-footprint path (fan_fail).
+// One thread per vertex slot of a loop candidate (n >= 3 slots):
+//  * the (u,v) image of the vertex on the face of vertex 0 (the planar data
+//    k_setup keeps for single-face small loops) and whether edge (i, i+1) lies
+//    inside that face (any edge that does not clears the footprint's inner
+//    flag: not_inner[f] = 1);
+//  * polygons only: the fan triangle terms of loop.go
+//    surfaceIntegralFloat64(SignedArea) for the loop as given (fwd, slot i =
+//    triangle (v0, vi, vi+1)) and for its reversal (rev, triangle (v[n-1],
+//    v[n-1-i], v[n-2-i])), i = 1 .. n-2.  The fan origin never moves for
+//    loops whose vertices all lie within DSS_SURFACE_MAX_LENGTH of v0; any
+//    other loop, or an undecided sign, goes to the exact per-footprint path
+//    (fan_fail).
 __global__ void k_fan(int64_t nx, const uint32_t *vown, const int32_t *kind, const int64_t *nslots, const int64_t *xoff,
-                      const V3 *xyz, double *fwd, double *rev, uint8_t *fan_fail)
+                      const V3 *xyz, double *fwd, double *rev, uint8_t *fan_fail, double2 *uv, uint8_t *not_inner)
 {
     const int64_t x = tid64();
     if (x >= nx) return;
     const uint32_t f = vown[x];
-    if (kind[f] == DSSG_KIND_CIRCLE) return;
     const int n = (int)nslots[f];
     const int i = (int)(x - xoff[f]);
-    if (n < 3 || i < 1 || i > n - 2) return;
+    if (n < 3) return;
     const V3 *p = xyz + xoff[f];
+    const int face0 = xyz_face(p[0]);
+    double u, v;
+    valid_face_xyz_to_uv(face0, p[i], u, v);  // = ClipToPaddedFace's same-face fast path
+    uv[x] = make_double2(u, v);
+    if (!edge_inside_face(p[i], p[i + 1 == n ? 0 : i + 1], face0)) not_inner[f] = 1;
+    if (kind[f] == DSSG_KIND_CIRCLE || i < 1 || i > n - 2) return;
     bool fail = false;
     const V3 a = p[0], b = p[i], c = p[i + 1];
     fail |= angle(c, a) > DSS_SURFACE_MAX_LENGTH;
@@ -262,7 +272,8 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
                                           double *area_out, uint8_t *mode, uint8_t *origin_in, uint8_t *fmask,
                                           uint8_t *flags, int32_t *nvx, double2 *uv, uint64_t *st_id, uint32_t *st_i,
                                           uint32_t *st_j, uint32_t *finfo, int64_t *ncand, uint4 *fbox,
-                                          const double *fwd, const double *rev, const uint8_t *fan_fail)
+                                          const double *fwd, const double *rev, const uint8_t *fan_fail,
+                                          const uint8_t *not_inner)
 {
     bool fail = false;
     auto bail = [&]() {
@@ -331,6 +342,12 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
                     V3 t = p[i];
                     p[i] = p[j];
                     p[j] = t;
+                    if constexpr (FAST) {  // k_fan's (u,v) images follow the vertices
+                        double2 *uvp = uv + xoff[f];
+                        double2 w = uvp[i];
+                        uvp[i] = uvp[j];
+                        uvp[j] = w;
+                    }
                 }
                 origin_of<FAST>(l, fail);
                 if constexpr (FAST) area = fan_area_km2(rev + xoff[f], nv, fail);
@@ -344,7 +361,11 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
     }
     uint8_t mask = 0;
     bool inner = true;
-    if (md != MODE_NONE) {
+    bool fast_inner = false;
+    if constexpr (FAST) fast_inner = md == MODE_LOOP && !not_inner[f];
+    if (fast_inner) {  // k_fan: every edge lies inside the face of vertex 0
+        mask = (uint8_t)(1u << xyz_face(p[0]));
+    } else if (md != MODE_NONE) {
         int ne = md == MODE_LOOP ? nv : nv - 1;
         int face0 = xyz_face(p[0]);
         for (int e = 0; e < ne; e++) {
@@ -383,8 +404,14 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
         double ulo = 1e300, uhi = -1e300, vlo = 1e300, vhi = -1e300;
         for (int i = 0; i < nv; i++) {
             double u, v;
-            valid_face_xyz_to_uv(face0, p[i], u, v);  // = ClipToPaddedFace's same-face fast path
-            uvp[i] = make_double2(u, v);
+            if constexpr (FAST) {  // projected by k_fan
+                const double2 w = uvp[i];
+                u = w.x;
+                v = w.y;
+            } else {
+                valid_face_xyz_to_uv(face0, p[i], u, v);  // = ClipToPaddedFace's same-face fast path
+                uvp[i] = make_double2(u, v);
+            }
             ulo = fmin(ulo, u); uhi = fmax(uhi, u); vlo = fmin(vlo, v); vhi = fmax(vhi, v);
         }
         bool near_origin = false;
@@ -432,20 +459,22 @@ __global__ __launch_bounds__(64) void k_setup(uint32_t *slow_list, unsigned int 
                         const float *radius_m, const int64_t *xoff, V3 *xyz, int32_t *status, double *area_out,
                         uint8_t *mode, uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx, double2 *uv,
                         uint64_t *st_id, uint32_t *st_i, uint32_t *st_j, uint32_t *finfo, int64_t *ncand,
-                        uint4 *fbox, const double *fwd, const double *rev, const uint8_t *fan_fail)
+                        uint4 *fbox, const double *fwd, const double *rev, const uint8_t *fan_fail,
+                        const uint8_t *not_inner, const uint32_t *perm)
 {
     int64_t f = tid64();
     if constexpr (FAST) {
         if (f >= n) return;
+        f = perm[f];  // polygons first, then circles: waves run one kind's path
     } else {  // a small grid strides over the footprints the triage left undecided
         for (int64_t i = f; i < (int64_t)*slow_n; i += (int64_t)gridDim.x * blockDim.x)
             setup_one<false>(slow_list[i], nullptr, nullptr, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out,
                              mode, origin_in, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, ncand, fbox, nullptr,
-                             nullptr, nullptr);
+                             nullptr, nullptr, nullptr);
         return;
     }
     setup_one<true>(f, slow_list, slow_n, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out, mode, origin_in,
-                    fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, ncand, fbox, fwd, rev, fan_fail);
+                    fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, ncand, fbox, fwd, rev, fan_fail, not_inner);
 }
 
 __device__ __forceinline__ int num_edges(uint8_t md, int nv) { return md == MODE_LOOP ? nv : (md == MODE_POLYLINE ? nv - 1 : 0); }
@@ -839,11 +868,16 @@ __global__ void k_cand_test(int64_t NC, const uint32_t *cand_f, const int64_t *c
             const double half = 0.5 / (double)kMaxSize;
             const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
             bool par = false;
+            // uc < a.x + (vc - a.y)(b.x - a.x)/(b.y - a.y), multiplied through
+            // by (b.y - a.y): the edge misses the padded cell, so its crossing
+            // with v = vc is >= half a cell (1.2e-4) from uc and the rounding
+            // (~1e-16 relative) cannot flip the comparison
             for (int e = 0; e < nv; e++) {
                 const double2 a = up[e], b = up[e + 1 == nv ? 0 : e + 1];
                 if ((a.y > vc) != (b.y > vc)) {
-                    const double x = a.x + (vc - a.y) * (b.x - a.x) / (b.y - a.y);
-                    if (uc < x) par = !par;
+                    const double d = b.y - a.y;
+                    const double lhs = (uc - a.x) * d, rhs = (vc - a.y) * (b.x - a.x);
+                    if (d > 0 ? lhs < rhs : lhs > rhs) par = !par;
                 }
             }
             r = ((origin_in[f] != 0) != par) ? 1 : 0;
@@ -951,22 +985,26 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     CircleFrame *frames = (CircleFrame *)frames_.ensure(sizeof(CircleFrame) * (n + 1));
     uint32_t *vown = vown_.ensure(nx + 1);
     double *fwd = fwd_.ensure(nx + 1), *rev = rev_.ensure(nx + 1);
+    uint8_t *not_inner = ninner_.ensure(n + 1);
+    uint32_t *perm = perm_.ensure(n + 1);
     DSS_HIP(hipMemsetAsync(slow_n, 0, sizeof(unsigned int), s));
     DSS_HIP(hipMemsetAsync(fan_fail, 0, n, s));
+    DSS_HIP(hipMemsetAsync(not_inner, 0, n, s));
+    partition_polygons_first(kind, perm, fcnt_.ensure(n + 1), n, tmp_, s);
     // per-vertex pre-pass: frames, owners, S2 points, fan terms
     hipLaunchKernelGGL(k_circle_frames, dim3(grid_for(n, B)), dim3(B), 0, s, n, kind, voff, lat, lng, radius_m, frames);
     hipLaunchKernelGGL(k_vowner, dim3(grid_for(n, B)), dim3(B), 0, s, n, xoff, vown);
     if (nx > 0) {
         hipLaunchKernelGGL(k_verts, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, kind, voff, lat, lng, xoff, frames, xyz);
         hipLaunchKernelGGL(k_fan, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, kind, nv, xoff, xyz,
-                           fwd, rev, fan_fail);
+                           fwd, rev, fan_fail, uv, not_inner);
     }
     hipLaunchKernelGGL(k_setup<true>, dim3(grid_for(n, 64)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng,
                        radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo,
-                       ncand, fbox, fwd, rev, fan_fail);
+                       ncand, fbox, fwd, rev, fan_fail, not_inner, perm);
     hipLaunchKernelGGL(k_setup<false>, dim3(min(grid_for(n, 64), 512u)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat,
                        lng, radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j,
-                       finfo, ncand, fbox, nullptr, nullptr, nullptr);
+                       finfo, ncand, fbox, nullptr, nullptr, nullptr, nullptr, nullptr);
     int64_t *eoff = eoff_.ensure(n + 1);
     hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv);
     exclusive_scan_i64(nv, eoff, n, tmp_, s);

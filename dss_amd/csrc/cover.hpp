@@ -30,7 +30,8 @@ class CoverEngine {
     DevBuf<double> area_, xyz_;
     DevBuf<uint8_t> mode_, orig_, fmask_, flags_, cflags_, act_;
     DevBuf<uint32_t> slow_, vown_;
-    DevBuf<uint8_t> fanf_;
+    DevBuf<uint8_t> fanf_, ninner_;
+    DevBuf<uint32_t> perm_;
     DevBuf<double> fwd_, rev_;
     DevBuf<unsigned char> frames_;
     DevBuf<unsigned int> slow_n_;

@@ -29,6 +29,9 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <vector>
+
 #include "search.hpp"
 
 namespace dss {
@@ -238,16 +241,20 @@ __global__ void k_expand(int64_t n, const int64_t *offs, uint32_t *val)
     for (int64_t k = offs[e]; k < offs[e + 1]; k++) val[k] = (uint32_t)e;
 }
 
-__global__ void k_keep_flags(int64_t P, const uint64_t *key, const uint32_t *val, int64_t *keep, int64_t *reg,
-                             int64_t *irr)
+// keep: first of its (cell, entity) run (entity cell lists, always whole);
+// reg / irr: kept postings in this index's cell range [lo, hi] (a cell-range
+// shard holds only those), split regular level-13 / other ids.
+__global__ void k_keep_flags(int64_t P, const uint64_t *key, const uint32_t *val, uint64_t lo, uint64_t hi, int64_t *keep,
+                             int64_t *reg, int64_t *irr)
 {
     int64_t i = tid64();
     if (i >= P) return;
     bool k = i == 0 || key[i] != key[i - 1] || val[i] != val[i - 1];
+    bool in = key[i] >= lo && key[i] <= hi;
     bool r = is_regular(key[i]);
     keep[i] = k;
-    reg[i] = k && r;
-    irr[i] = k && !r;
+    reg[i] = k && in && r;
+    irr[i] = k && in && !r;
 }
 
 __global__ void k_scatter_unique(int64_t P, const uint64_t *key, const uint32_t *val, const int64_t *keep,
@@ -442,39 +449,6 @@ struct QueryView {
     const int32_t *owner;
 };
 
-// (1) one key (slot << 6 | bucket) per non-empty group a query cell meets:
-// the buckets of [min(tlo,thi), max(tlo,thi)] plus the long bucket.
-template <int PASS>
-__global__ void k_qkeys(IndexView a, QueryView qv, int64_t *cnt, const int64_t *off, uint64_t *key, uint32_t *val)
-{
-    int64_t q = tid64();
-    if (q >= qv.nq) return;
-    const long long tlo = qv.tlo[q], thi = qv.thi[q];
-    const int bq0 = bucket_of(tlo < thi ? tlo : thi, a.bk), bq1 = bucket_of(tlo < thi ? thi : tlo, a.bk);
-    const unsigned long long range = ((1ull << (bq1 + 1)) - 1ull) & ~((1ull << bq0) - 1ull);
-    const int64_t c0 = qv.offs[q], c1 = qv.offs[q + 1];
-    int64_t n = 0, w = PASS ? off[q] : 0;
-    for (int64_t k = c0; k < c1; k++) {
-        uint32_t slot;
-        if (!find_slot(a, qv.cells[k], slot)) continue;
-        const unsigned long long m0 = a.s_mask[slot];
-        unsigned long long m = (m0 & range) | (m0 & (1ull << kLongBucket));
-        if (!PASS) {
-            n += __popcll(m);
-            continue;
-        }
-        const uint32_t v = (uint32_t)k;  // query-cell index: selects the record
-        while (m) {
-            int b = __builtin_ctzll(m);
-            m &= m - 1;
-            key[w] = ((uint64_t)slot << 6) | (uint64_t)b;
-            val[w] = v;
-            w++;
-        }
-    }
-    if (!PASS) cnt[q] = n;
-}
-
 // Query record, one per query cell: what one predicate sweep needs.
 struct alignas(64) QRec {
     long long tlo, thi;
@@ -485,73 +459,143 @@ struct alignas(64) QRec {
 };
 static_assert(sizeof(QRec) == 64, "QRec layout");
 
-// One thread per query walks its sorted cells once, decoding each and
-// growing the prefix signature (prefix_sig semantics: an undecodable cell
-// saturates the signature; `compact` = every earlier cell on this cell's face
-// within +-7 cells in i and j).
-__global__ void k_qcellrec(IndexView a, QueryView qv, QRec *crec, int32_t *cown)
+// Owner query of every query cell.
+__global__ void k_cell_query(int64_t nq, const int64_t *offs, uint32_t *cq)
 {
     const int64_t q = tid64();
-    if (q >= qv.nq) return;
+    if (q >= nq) return;
+    for (int64_t k = offs[q]; k < offs[q + 1]; k++) cq[k] = (uint32_t)q;
+}
+
+// Level-13 (face, i, j) of every query cell, packed face << 26 | i << 13 | j,
+// or kNoDecode for ids that are not valid level-13 cells.
+constexpr uint32_t kNoDecode = 0xffffffffu;
+__global__ void k_qdecode(int64_t nqc, const uint64_t *cells, uint32_t *dec)
+{
+    const int64_t k = tid64();
+    if (k >= nqc) return;
+    int f = 0, i = 0, j = 0;
+    dec[k] = decode13(cells[k], f, i, j) ? ((uint32_t)f << 26 | (uint32_t)i << 13 | (uint32_t)j) : kNoDecode;
+}
+
+// Groups (non-empty (slot, bucket) runs of the index) query cell k meets:
+// the buckets of [min(tlo,thi), max(tlo,thi)] plus the long bucket.
+__device__ __forceinline__ unsigned long long cell_groups(const IndexView &a, uint64_t cell, long long tlo,
+                                                          long long thi, uint32_t &slot)
+{
+    if (!find_slot(a, cell, slot)) return 0;
+    const int bq0 = bucket_of(tlo < thi ? tlo : thi, a.bk), bq1 = bucket_of(tlo < thi ? thi : tlo, a.bk);
+    const unsigned long long range = ((1ull << (bq1 + 1)) - 1ull) & ~((1ull << bq0) - 1ull);
+    const unsigned long long m0 = a.s_mask[slot];
+    return (m0 & range) | (m0 & (1ull << kLongBucket));
+}
+
+// (1) one thread per query cell: PASS 0 counts the groups the cell meets;
+// PASS 1 writes one (group id, query cell) key per group at koff[k] and the
+// cell's query record.  The record's prefix signature covers the query's
+// cells before k (prefix_sig semantics: an undecodable cell saturates it;
+// `compact` = every earlier cell on this cell's face within +-7 cells).
+template <int PASS>
+__global__ void k_qcells(IndexView a, QueryView qv, int64_t nqc, const uint32_t *cq, const uint32_t *dec, int64_t *kcnt,
+                         const int64_t *koff, uint32_t *gkey, uint32_t *gval, QRec *crec, int32_t *cown)
+{
+    const int64_t k = tid64();
+    if (k >= nqc) return;
+    const uint32_t q = cq[k];
     const long long tlo = qv.tlo[q], thi = qv.thi[q];
-    const float alo = qv.alo[q], ahi = qv.ahi[q];
-    const int bq0 = bucket_of(tlo < thi ? tlo : thi, a.bk);
-    const int32_t own = cown ? qv.owner[q] : -1;
-    const int64_t c0 = qv.offs[q], c1 = qv.offs[q + 1];
+    const uint64_t cell = qv.cells[k];
+    uint32_t slot = 0;
+    unsigned long long m = cell_groups(a, cell, tlo, thi, slot);
+    if (!PASS) {
+        kcnt[k] = __popcll(m);
+        return;
+    }
+    int64_t w = koff[k];
+    if (m) {
+        const unsigned long long m0 = a.s_mask[slot];
+        const uint32_t base = a.s_base[slot];
+        while (m) {
+            const int b = __builtin_ctzll(m);
+            m &= m - 1;
+            gkey[w] = base + (uint32_t)__popcll(m0 & ((1ull << b) - 1ull));
+            gval[w] = (uint32_t)k;
+            w++;
+        }
+    }
+    // query record
+    const int64_t c0 = qv.offs[q];
     Sig256 sig;
     sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = 0;
     bool bad = false;  // an undecodable cell in the prefix
     int pf = -1;       // face of every prefix cell, -2 if mixed
     int imin = 0, imax = 0, jmin = 0, jmax = 0;
-    for (int64_t k = c0; k < c1; k++) {
-        int f = 0, i = 0, j = 0;
-        const bool v = decode13(qv.cells[k], f, i, j);
-        const bool compact = v && !bad &&
-                             (k == c0 || (pf == f && imin >= i - 7 && imax <= i + 7 && jmin >= j - 7 && jmax <= j + 7));
-        QRec r;
-        r.tlo = tlo;
-        r.thi = thi;
-        r.alo = alo;
-        r.ahi = ahi;
-        r.qv = (uint32_t)q | (k == c0 ? kRank0 : 0u) | (compact ? kCompact : 0u);
-        r.bq0 = bq0;
-        r.sig[0] = sig.w[0];
-        r.sig[1] = sig.w[1];
-        r.sig[2] = sig.w[2];
-        r.sig[3] = sig.w[3];
-        crec[k] = r;
-        if (cown) cown[k] = own;
-        if (v) {
-            const int bit = ((i & 15) << 4) | (j & 15);
-            const unsigned long long m = 1ull << (bit & 63);
+    // the prefix's decodes are loaded 8 at a time (independent loads in
+    // flight together), then folded in order
+    constexpr int kU = 8;
+    for (int64_t j0 = c0; j0 < k; j0 += kU) {
+        uint32_t dd[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) dd[u] = j0 + u < k ? dec[j0 + u] : 0u;
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+        const int64_t j = j0 + u;
+        if (j >= k) break;
+        const uint32_t d = dd[u];
+        const int f = (int)(d >> 26), ci = (int)((d >> 13) & 8191u), cj = (int)(d & 8191u);
+        if (d != kNoDecode) {
+            const int bit = ((ci & 15) << 4) | (cj & 15);
+            const unsigned long long mb = 1ull << (bit & 63);
             const int wi = bit >> 6;  // selects, not an indexed store: keeps sig in registers
-            sig.w[0] |= wi == 0 ? m : 0;
-            sig.w[1] |= wi == 1 ? m : 0;
-            sig.w[2] |= wi == 2 ? m : 0;
-            sig.w[3] |= wi == 3 ? m : 0;
-            if (k == c0) {
+            sig.w[0] |= wi == 0 ? mb : 0;
+            sig.w[1] |= wi == 1 ? mb : 0;
+            sig.w[2] |= wi == 2 ? mb : 0;
+            sig.w[3] |= wi == 3 ? mb : 0;
+            if (j == c0) {
                 pf = f;
-                imin = imax = i;
-                jmin = jmax = j;
+                imin = imax = ci;
+                jmin = jmax = cj;
             } else {
                 if (pf != f) pf = -2;
-                imin = min(imin, i);
-                imax = max(imax, i);
-                jmin = min(jmin, j);
-                jmax = max(jmax, j);
+                imin = min(imin, ci);
+                imax = max(imax, ci);
+                jmin = min(jmin, cj);
+                jmax = max(jmax, cj);
             }
         } else {
             bad = true;
             sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = ~0ull;
         }
+        }
     }
+    const uint32_t dk = dec[k];
+    const int f = (int)(dk >> 26), i = (int)((dk >> 13) & 8191u), jj = (int)(dk & 8191u);
+    const bool v = dk != kNoDecode;
+    const bool compact = v && !bad &&
+                         (k == c0 || (pf == f && imin >= i - 7 && imax <= i + 7 && jmin >= jj - 7 && jmax <= jj + 7));
+    QRec r;
+    r.tlo = tlo;
+    r.thi = thi;
+    r.alo = qv.alo[q];
+    r.ahi = qv.ahi[q];
+    r.qv = q | (k == c0 ? kRank0 : 0u) | (compact ? kCompact : 0u);
+    r.bq0 = bucket_of(tlo < thi ? tlo : thi, a.bk);
+    r.sig[0] = sig.w[0];
+    r.sig[1] = sig.w[1];
+    r.sig[2] = sig.w[2];
+    r.sig[3] = sig.w[3];
+    crec[k] = r;
+    if (cown) cown[k] = qv.owner[q];
 }
 
-__device__ __forceinline__ uint32_t group_of(const IndexView &a, uint64_t key)
+// Record range [gbeg[g], gend[g]) of every group in the sorted keys (groups
+// no query met keep 0, 0).
+__global__ void k_gbounds(int64_t nkeys, const uint32_t *skey, uint32_t *gbeg, uint32_t *gend)
 {
-    const uint32_t slot = (uint32_t)(key >> 6);
-    const int b = (int)(key & 63);
-    return a.s_base[slot] + (uint32_t)__popcll(a.s_mask[slot] & ((1ull << b) - 1ull));
+    const int64_t i = tid64();
+    if (i >= nkeys) return;
+    const uint32_t g = skey[i];
+    if (i == 0 || skey[i - 1] != g) gbeg[g] = (uint32_t)i;
+    if (i == nkeys - 1 || skey[i + 1] != g) gend[g] = (uint32_t)(i + 1);
 }
 
 // Postings per lane in a join unit: a unit covers up to 64 * kSlots postings
@@ -559,64 +603,66 @@ __device__ __forceinline__ uint32_t group_of(const IndexView &a, uint64_t key)
 // and each broadcast record is tested against all of it.
 constexpr int kSlots = 2;
 
-// (2) join units: (run, tile of <= 64 * kSlots postings, kQChunk-record chunk).
-// u_pt = tile | (slots - 1) << 28.
+// (2) join units: (group, tile of <= 64 * kSlots postings, kQChunk-record
+// chunk), one thread per group of the index.  u_pt = tile | (slots - 1) << 28.
+// The unit count stays on the device (uoff[ng]); the persistent join reads it.
 template <int PASS>
-__global__ void k_units(int64_t nruns, IndexView a, const uint64_t *ukey, const int64_t *rstart, int64_t *cnt,
-                        const int64_t *uoff, uint32_t *u_run, uint32_t *u_pt, uint32_t *u_qt)
+__global__ void k_units(int64_t ng, const uint32_t *bk_start, const uint32_t *gbeg, const uint32_t *gend, int64_t *cnt,
+                        const int64_t *uoff, uint32_t *u_grp, uint32_t *u_pt, uint32_t *u_qt)
 {
-    int64_t r = tid64();
-    if (r >= nruns) return;
-    const uint32_t g = group_of(a, ukey[r]);
-    const int64_t np = (int64_t)a.bk_start[g + 1] - a.bk_start[g];
-    const int64_t nq = rstart[r + 1] - rstart[r];
+    const int64_t g = tid64();
+    if (g >= ng) return;
+    const int64_t nrec = (int64_t)gend[g] - gbeg[g];
+    const int64_t np = (int64_t)bk_start[g + 1] - bk_start[g];
     const int64_t k = min((int64_t)kSlots, max((int64_t)1, (np + 63) / 64));
-    const int64_t tp = (np + 64 * k - 1) / (64 * k), tq = (nq + kQChunk - 1) / kQChunk;
+    const int64_t tp = (np + 64 * k - 1) / (64 * k), tq = (nrec + kQChunk - 1) / kQChunk;
     if (!PASS) {
-        cnt[r] = tp * tq;
+        cnt[g] = tp * tq;
         return;
     }
-    int64_t w = uoff[r];
+    int64_t w = uoff[g];
     for (int64_t i = 0; i < tp; i++)
         for (int64_t j = 0; j < tq; j++, w++) {
-            u_run[w] = (uint32_t)r;
+            u_grp[w] = (uint32_t)g;
             u_pt[w] = (uint32_t)i | (uint32_t)(k - 1) << 28;
             u_qt[w] = (uint32_t)j;
         }
 }
 
-// Diagnostics (timing mode): sum over runs of records x tiles (wave
-// iterations before the time pre-filter) and of records x postings (useful
-// lane tests).
-__global__ void k_work_stats(int64_t nruns, IndexView a, const uint64_t *ukey, const int64_t *rstart,
+// Diagnostics (timing mode): groups met, sum over groups of records x tiles
+// (wave iterations before the time pre-filter) and of records x postings
+// (useful lane tests).
+__global__ void k_work_stats(int64_t ng, const uint32_t *bk_start, const uint32_t *gbeg, const uint32_t *gend,
                              unsigned long long *stat)
 {
-    int64_t r = tid64();
-    unsigned long long it = 0, lt = 0;
-    if (r < nruns) {
-        const uint32_t g = group_of(a, ukey[r]);
-        const unsigned long long np = a.bk_start[g + 1] - a.bk_start[g];
-        const unsigned long long nq = (unsigned long long)(rstart[r + 1] - rstart[r]);
+    int64_t g = tid64();
+    unsigned long long it = 0, lt = 0, met = 0;
+    if (g < ng) {
+        const unsigned long long np = bk_start[g + 1] - bk_start[g];
+        const unsigned long long nq = (unsigned long long)(gend[g] - gbeg[g]);
         const unsigned long long k = np > 64 ? kSlots : 1;
         it = nq * ((np + 64 * k - 1) / (64 * k));
         lt = nq * np;
+        met = nq ? 1 : 0;
     }
     for (int o = 32; o > 0; o >>= 1) {
         it += __shfl_xor(it, o);
         lt += __shfl_xor(lt, o);
+        met += __shfl_xor(met, o);
     }
-    if ((threadIdx.x & 63) == 0 && (it || lt)) {
+    if ((threadIdx.x & 63) == 0 && (it || lt || met)) {
         atomicAdd(&stat[0], it);
         atomicAdd(&stat[1], lt);
+        atomicAdd(&stat[2], met);
     }
 }
 
 struct JoinArgs {
     IndexView ix;
     QueryView qv;
-    int64_t nunits;
-    const uint64_t *ukey;
-    const int64_t *rstart;
+    const int64_t *nunits;  // device: written by the unit scan
+    const uint64_t *g_key;  // group -> slot << 6 | bucket
+    const uint32_t *gbeg, *gend;
     int64_t cap;
 };
 
@@ -637,7 +683,7 @@ __device__ __forceinline__ void load_slot(const IndexView &ix, uint32_t p, uint3
     s.first = s.compact = false;
     s.ent = 0;
     s.be0 = 0;
-    s.alt = make_float2(0.f, 0.f);
+    s.alt = make_float2(INFINITY, -INFINITY);    // matches nothing
     s.t = make_longlong2(LLONG_MAX, LLONG_MIN);  // matches nothing
     s.own = 0;
     s.s01 = s.s23 = make_ulonglong2(0, 0);
@@ -694,17 +740,17 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
     // persistent waves: grab kGrab units at a time until the queue drains;
     // the staging buffer carries over between units, so the output counter
     // sees one atomic per kStage pairs
+    const int64_t nunits = *a.nunits;
     for (;;) {
         uint32_t ub = 0;
         if (lane == 0) ub = atomicAdd(work, (uint32_t)kGrab);
         ub = __builtin_amdgcn_readfirstlane(__shfl(ub, 0));
-        if ((int64_t)ub >= a.nunits) break;
-        const uint32_t ue = (uint32_t)min((int64_t)ub + kGrab, a.nunits);
+        if ((int64_t)ub >= nunits) break;
+        const uint32_t ue = (uint32_t)min((int64_t)ub + kGrab, nunits);
         for (uint32_t u = ub; u < ue; u++) {
-            const uint32_t r = u_run[u];
-            const uint64_t key = a.ukey[r];
+            const uint32_t g = u_run[u];
+            const uint64_t key = a.g_key[g];
             const int b = (int)(key & 63);
-            const uint32_t g = group_of(ix, key);
             const uint32_t gs = ix.bk_start[g], ge = ix.bk_start[g + 1];
             const uint32_t pt = u_pt[u];
             const int nslot = (int)(pt >> 28) + 1;
@@ -715,20 +761,26 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
                 if (k < nslot) load_slot(ix, p0 + 64u * k, ge, OWNER, sl[k]);
                 else load_slot(ix, ge, ge, OWNER, sl[k]);
             }
-            // time bounds of the unit: records whose window misses all postings are skipped
+            // time and altitude bounds of the unit: records whose window or
+            // altitude band misses all postings are skipped
             long long tmin = LLONG_MAX, tmax = LLONG_MIN;
+            float amin = INFINITY, amax = -INFINITY;
 #pragma unroll
             for (int k = 0; k < kSlots; k++) {
                 tmin = min(tmin, sl[k].t.x);
                 tmax = max(tmax, sl[k].t.y);
+                amin = fminf(amin, sl[k].alt.x);
+                amax = fmaxf(amax, sl[k].alt.y);
             }
             for (int o = 32; o > 0; o >>= 1) {
                 tmin = min(tmin, __shfl_xor(tmin, o));
                 tmax = max(tmax, __shfl_xor(tmax, o));
+                amin = fminf(amin, __shfl_xor(amin, o));
+                amax = fmaxf(amax, __shfl_xor(amax, o));
             }
             const uint64_t cell = cell_of_slot(ix, (uint32_t)(key >> 6));
-            const int64_t k0 = a.rstart[r] + (int64_t)u_qt[u] * kQChunk;
-            const int64_t k1 = min(a.rstart[r + 1], k0 + kQChunk);
+            const int64_t k0 = (int64_t)a.gbeg[g] + (int64_t)u_qt[u] * kQChunk;
+            const int64_t k1 = min((int64_t)a.gend[g], k0 + kQChunk);
             const int4 *rec4 = reinterpret_cast<const int4 *>(recs);
             for (int64_t base = k0; base < k1; base += 64) {
                 const int64_t kk = base + lane;
@@ -744,7 +796,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
                     if (OWNER) s_own[w][lane] = rown[ci];
                     const long long tlo = ((long long)c0.y << 32) | (uint32_t)c0.x;
                     const long long thi = ((long long)c0.w << 32) | (uint32_t)c0.z;
-                    rel = !(tmax < tlo || tmin > thi);  // else no posting of the unit can match
+                    const float alo = __int_as_float(c1.x), ahi = __int_as_float(c1.y);
+                    rel = !(tmax < tlo || tmin > thi) && !(amax < alo || amin > ahi);  // else no posting can match
                 }
                 __builtin_amdgcn_wave_barrier();
                 unsigned long long todo = __ballot(rel);
@@ -891,8 +944,10 @@ int64_t fetch_i64(const int64_t *p, hipStream_t s)
 // ================================================================== build
 void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, const uint64_t *cells,
                          const float *alt_lo, const float *alt_hi, const int64_t *t0, const int64_t *t1,
-                         const int32_t *owner, hipStream_t s)
+                         const int32_t *owner, uint64_t cell_lo, uint64_t cell_hi, hipStream_t s)
 {
+    idx->cell_lo = cell_lo;
+    idx->cell_hi = cell_hi;
     idx->n_e = n;
     idx->has_owner = owner != nullptr;
     const int64_t P = fetch_i64(cell_offs + n, s);
@@ -908,7 +963,9 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     sort_pairs(ka, kb, va, vb, P, 64, tmp_, s);
     int64_t *keep = c0_.ensure(3 * Pa), *reg = keep + Pa, *irr = reg + Pa;
     int64_t *kpos = c1_.ensure(3 * (Pa + 1)), *rpos = kpos + (Pa + 1), *ipos = rpos + (Pa + 1);
-    if (P) hipLaunchKernelGGL(k_keep_flags, dim3(grid_for(P, kBlock)), dim3(kBlock), 0, s, P, kb, vb, keep, reg, irr);
+    if (P)
+        hipLaunchKernelGGL(k_keep_flags, dim3(grid_for(P, kBlock)), dim3(kBlock), 0, s, P, kb, vb, cell_lo, cell_hi, keep, reg,
+                           irr);
     exclusive_scan_i64(keep, kpos, P, tmp_, s);
     exclusive_scan_i64(reg, rpos, P, tmp_, s);
     exclusive_scan_i64(irr, ipos, P, tmp_, s);
@@ -1068,11 +1125,28 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
         uint32_t *bk_start = idx->bk_start.ensure(ng + 1);
         hipLaunchKernelGGL(k_i64_to_u32, dim3(grid_for(ng + 1, kBlock)), dim3(kBlock), 0, s, ng + 1, gst, bk_start);
         hipLaunchKernelGGL(k_group_mask, dim3(grid_for(ng, kBlock)), dim3(kBlock), 0, s, ng, gkey, s_mask);
+        uint64_t *g_key = idx->g_key.ensure(ng + 1);
+        DSS_HIP(hipMemcpyAsync(g_key, gkey, sizeof(uint64_t) * ng, hipMemcpyDeviceToDevice, s));
+        // join-unit bound inputs: posting tiles per group (k_units)
+        std::vector<uint32_t> hb((size_t)ng + 1);
+        DSS_HIP(hipMemcpyAsync(hb.data(), bk_start, sizeof(uint32_t) * (ng + 1), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipStreamSynchronize(s));
+        idx->tiles_total = 0;
+        idx->tiles_max = 0;
+        for (int64_t g = 0; g < ng; g++) {
+            const int64_t np = (int64_t)hb[g + 1] - hb[g];
+            const int64_t k = std::min((int64_t)kSlots, std::max((int64_t)1, (np + 63) / 64));
+            const int64_t tp = (np + 64 * k - 1) / (64 * k);
+            idx->tiles_total += tp;
+            idx->tiles_max = std::max(idx->tiles_max, tp);
+        }
     } else {
         idx->bk_start.ensure(1);
         DSS_HIP(hipMemsetAsync(idx->bk_start.p, 0, sizeof(uint32_t), s));
+        idx->g_key.ensure(1);
+        idx->tiles_total = idx->tiles_max = 0;
     }
+    idx->n_groups = ng;
     {
         DevBuf<int64_t> pc, po;
         int64_t *pcnt = pc.ensure(n_slots + 1), *poff = po.ensure(n_slots + 2);
@@ -1120,66 +1194,73 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         join_ms_ = 0;
     };
     if (nq <= 0 || idx->n_b == 0) return empty();
-    // (1) keys (slot << 6 | bucket) for every group a query cell meets
-    int64_t *qcnt = c0_.ensure(nq + 1), *qoff = c1_.ensure(nq + 2);
-    hipLaunchKernelGGL(k_qkeys<0>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, ix, qv, qcnt, nullptr, nullptr, nullptr);
-    exclusive_scan_i64(qcnt, qoff, nq, tmp_, s);
-    int64_t hk[2] = {0, 0};
-    DSS_HIP(hipMemcpyAsync(&hk[0], qoff + nq, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    DSS_HIP(hipMemcpyAsync(&hk[1], q_offs + nq, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    const int64_t ng = idx->n_groups;
+    // (1) per query cell: group keys + records; the one host sync before the
+    // join sizes the key buffers (the radix sort takes a host count)
+    int64_t nqc = 0;
+    DSS_HIP(hipMemcpyAsync(&nqc, q_offs + nq, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
-    const int64_t nkeys = hk[0], nqc = hk[1];
+    if (nqc >= (int64_t)0xffffffffll) throw Error(DSSG_ERR_CAPACITY, "search: more than 2^32 query cells per batch");
+    if (nqc == 0) return empty();
+    uint32_t *cq = cq_.ensure(nqc + 1);
+    uint32_t *dec = dec_.ensure(nqc + 1);
+    hipLaunchKernelGGL(k_cell_query, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_offs, cq);
+    hipLaunchKernelGGL(k_qdecode, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, nqc, q_cells, dec);
+    int64_t *kcnt = c0_.ensure(nqc + 1), *koff = c1_.ensure(nqc + 2);
+    hipLaunchKernelGGL(k_qcells<0>, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, ix, qv, nqc, cq, dec, kcnt, nullptr,
+                       nullptr, nullptr, nullptr, nullptr);
+    exclusive_scan_i64(kcnt, koff, nqc, tmp_, s);
+    const int64_t nkeys = fetch_i64(koff + nqc, s);
     keys_ = nkeys;
     if (nkeys == 0) return empty();
     if (nkeys >= (int64_t)0x7fffffff) throw Error(DSSG_ERR_CAPACITY, "search: more than 2^31 (cell, bucket) keys per batch");
-    // query-cell records (independent of the sort)
-    if (nqc >= (int64_t)0xffffffffll) throw Error(DSSG_ERR_CAPACITY, "search: more than 2^32 query cells per batch");
     QRec *recs = (QRec *)rec_.ensure(sizeof(QRec) * (nqc + 1));
     int32_t *rown = q_owner ? (int32_t *)own_.ensure(nqc + 1) : nullptr;
-    hipLaunchKernelGGL(k_qcellrec, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, ix, qv, recs, rown);
-    uint64_t *key = k0_.ensure(nkeys + 1), *skey = k1_.ensure(nkeys + 1);
-    uint32_t *val = v0_.ensure(nkeys + 1), *sval = v1_.ensure(nkeys + 1);
-    hipLaunchKernelGGL(k_qkeys<1>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, ix, qv, nullptr, qoff, key, val);
-    // (2) group by key (stable: query order kept within a group)
-    sort_pairs(key, skey, val, sval, nkeys, bits_for(idx->n_dense + idx->n_irr) + 6, tmp_, s);
-    uint64_t *ukey = uk_.ensure(nkeys + 1);
-    int64_t *rcnt = rc_.ensure(nkeys + 1), *rstart = rs_.ensure(nkeys + 2), *nruns_d = nr_.ensure(2);
-    size_t bytes = 0;
-    DSS_HIP(hipcub::DeviceRunLengthEncode::Encode(nullptr, bytes, skey, ukey, rcnt, nruns_d, (int)nkeys, s));
-    tmp_.ensure(bytes + 16);
-    DSS_HIP(hipcub::DeviceRunLengthEncode::Encode(tmp_.p, bytes, skey, ukey, rcnt, nruns_d, (int)nkeys, s));
-    // query records (independent of the run boundaries)
-    const int64_t nruns = fetch_i64(nruns_d, s);
-    exclusive_scan_i64(rcnt, rstart, nruns, tmp_, s);
-    // (3) join units
-    int64_t *ucnt = uc_.ensure(nruns + 1), *uoff = uo_.ensure(nruns + 2);
-    hipLaunchKernelGGL(k_units<0>, dim3(grid_for(nruns, kBlock)), dim3(kBlock), 0, s, nruns, ix, ukey, rstart, ucnt, nullptr,
-                       nullptr, nullptr, nullptr);
-    exclusive_scan_i64(ucnt, uoff, nruns, tmp_, s);
-    const int64_t nunits = fetch_i64(uoff + nruns, s);
-    units_ = nunits;
+    uint32_t *key = v0_.ensure(nkeys + 1), *skey = v2_.ensure(nkeys + 1);
+    uint32_t *val = v1_.ensure(nkeys + 1), *sval = v3_.ensure(nkeys + 1);
+    hipLaunchKernelGGL(k_qcells<1>, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, ix, qv, nqc, cq, dec, nullptr, koff,
+                       key, val, recs, rown);
+    // (2) group by group id (radix sort over bits_for(ng) bits), then each
+    // group's record range
+    sort_pairs(key, skey, val, sval, nkeys, bits_for(ng), tmp_, s);
+    uint32_t *gbeg = gb_.ensure(ng + 1), *gend = ge_.ensure(ng + 1);
+    DSS_HIP(hipMemsetAsync(gbeg, 0, sizeof(uint32_t) * (ng + 1), s));
+    DSS_HIP(hipMemsetAsync(gend, 0, sizeof(uint32_t) * (ng + 1), s));
+    hipLaunchKernelGGL(k_gbounds, dim3(grid_for(nkeys, kBlock)), dim3(kBlock), 0, s, nkeys, skey, gbeg, gend);
+    // (3) join units over all groups; the total stays on the device.  Bound:
+    // each group contributes tiles x ceil(records / kQChunk) units.
+    int64_t *ucnt = uc_.ensure(ng + 1), *uoff = uo_.ensure(ng + 2);
+    hipLaunchKernelGGL(k_units<0>, dim3(grid_for(ng, kBlock)), dim3(kBlock), 0, s, ng, idx->bk_start.p, gbeg, gend, ucnt,
+                       nullptr, nullptr, nullptr, nullptr);
+    exclusive_scan_i64(ucnt, uoff, ng, tmp_, s);
+    const int64_t ubound = idx->tiles_total + (nkeys / kQChunk + 1) * idx->tiles_max;
+    if (ubound >= (int64_t)0xffffffffll - kGrab) throw Error(DSSG_ERR_CAPACITY, "search: too many join units");
+    uint32_t *u_run = ur_.ensure(ubound + 1), *u_pt = up_.ensure(ubound + 1), *u_qt = uq_.ensure(ubound + 1);
+    hipLaunchKernelGGL(k_units<1>, dim3(grid_for(ng, kBlock)), dim3(kBlock), 0, s, ng, idx->bk_start.p, gbeg, gend, nullptr,
+                       uoff, u_run, u_pt, u_qt);
     if (timing_) {
-        unsigned long long *st = counter_.ensure(4) + 2;
-        DSS_HIP(hipMemsetAsync(st, 0, 2 * sizeof(unsigned long long), s));
-        hipLaunchKernelGGL(k_work_stats, dim3(grid_for(nruns, kBlock)), dim3(kBlock), 0, s, nruns, ix, ukey, rstart, st);
-        unsigned long long h[2];
+        unsigned long long *st = counter_.ensure(8) + 2;
+        DSS_HIP(hipMemsetAsync(st, 0, 3 * sizeof(unsigned long long), s));
+        hipLaunchKernelGGL(k_work_stats, dim3(grid_for(ng, kBlock)), dim3(kBlock), 0, s, ng, idx->bk_start.p, gbeg, gend,
+                           st);
+        unsigned long long h[3];
+        int64_t nu = 0;
         DSS_HIP(hipMemcpyAsync(h, st, sizeof(h), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipMemcpyAsync(&nu, uoff + ng, sizeof(nu), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipStreamSynchronize(s));
         iters_ = (int64_t)h[0];
         tests_ = (int64_t)h[1];
-        runs_ = nruns;
+        runs_ = (int64_t)h[2];
+        units_ = nu;
     }
-    if (nunits >= (int64_t)0xffffffffll - kGrab) throw Error(DSSG_ERR_CAPACITY, "search: too many join units");
-    uint32_t *u_run = ur_.ensure(nunits + 1), *u_pt = up_.ensure(nunits + 1), *u_qt = uq_.ensure(nunits + 1);
-    hipLaunchKernelGGL(k_units<1>, dim3(grid_for(nruns, kBlock)), dim3(kBlock), 0, s, nruns, ix, ukey, rstart, nullptr, uoff,
-                       u_run, u_pt, u_qt);
     // (4) join; grow the output and rerun if the guess was too small
     JoinArgs ja{};
     ja.ix = ix;
     ja.qv = qv;
-    ja.nunits = nunits;
-    ja.ukey = ukey;
-    ja.rstart = rstart;
+    ja.nunits = uoff + ng;
+    ja.g_key = idx->g_key.p;
+    ja.gbeg = gbeg;
+    ja.gend = gend;
     unsigned long long *counter = counter_.ensure(1);
     if (out_cap_ == 0) out_cap_ = (size_t)nq * 16 + 1024;
     // persistent grid: a few workgroups per CU (LDS-limited), units pulled from a queue
@@ -1189,8 +1270,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         DSS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
         n_cu_ = ncu > 0 ? ncu : 256;
     }
-    const int64_t want = (nunits + kWaves - 1) / kWaves;
-    const unsigned nblocks = (unsigned)min(want, (int64_t)n_cu_ * kJoinBlocksPerCU);
+    const unsigned nblocks = (unsigned)n_cu_ * kJoinBlocksPerCU;
     uint32_t *work = work_.ensure(1);
     for (int attempt = 0; attempt < 3; attempt++) {
         uint32_t *oq = oq_.ensure(out_cap_), *oe = oe_.ensure(out_cap_);
@@ -1200,8 +1280,8 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
         if (nblocks && q_owner)
             hipLaunchKernelGGL(k_join<true>, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
-                               (const uint32_t *)sval, (const int32_t *)rown, (const uint32_t *)u_run, (const uint32_t *)u_pt, (const uint32_t *)u_qt,
-                               oq, oe, counter, work);
+                               (const uint32_t *)sval, (const int32_t *)rown, (const uint32_t *)u_run,
+                               (const uint32_t *)u_pt, (const uint32_t *)u_qt, oq, oe, counter, work);
         else if (nblocks)
             hipLaunchKernelGGL(k_join<false>, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
                                (const uint32_t *)sval, (const int32_t *)nullptr, (const uint32_t *)u_run, (const uint32_t *)u_pt,

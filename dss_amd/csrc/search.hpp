@@ -8,6 +8,7 @@ struct dssg_index {
     int64_t n_reg = 0;    // of which on valid level-13 cells (dense lookup)
     int64_t n_cells = 0;  // distinct cells
     int64_t n_b = 0;      // time-bucketed postings (the join's working set)
+    uint64_t cell_lo = 0, cell_hi = ~0ull;  // cell range of the postings held (shards)
     bool has_owner = false;
     // ---- plain postings, sorted by (cell, entity); regular first -------------
     // A cell's "slot" is its dense slot (level-13 cells) or n_dense + its index
@@ -35,6 +36,9 @@ struct dssg_index {
     dss::DevBuf<unsigned long long> s_mask;  // n_slots
     dss::DevBuf<uint32_t> s_base;            // n_slots + 1
     dss::DevBuf<uint32_t> bk_start;          // n_groups + 1
+    dss::DevBuf<uint64_t> g_key;             // n_groups: slot << 6 | bucket
+    int64_t n_groups = 0;
+    int64_t tiles_total = 0, tiles_max = 0;  // join-unit posting tiles (sum, max over groups)
     dss::DevBuf<uint32_t> b_e;               // entity | first bit
     dss::DevBuf<float2> b_alt;               // (alt_lo, alt_hi)
     dss::DevBuf<longlong2> b_t;              // (t0, t1) microseconds
@@ -48,8 +52,12 @@ namespace dss {
 
 class SearchEngine {
    public:
+    // Postings are kept only for cells in [cell_lo, cell_hi] (a cell-range
+    // shard); entity cell lists stay whole, so the smallest-shared-cell rule
+    // emits every pair on exactly one shard.
     void build(dssg_index *idx, int64_t n, const int64_t *cell_offs, const uint64_t *cells, const float *alt_lo,
-               const float *alt_hi, const int64_t *t0, const int64_t *t1, const int32_t *owner, hipStream_t s);
+               const float *alt_hi, const int64_t *t0, const int64_t *t1, const int32_t *owner, uint64_t cell_lo,
+               uint64_t cell_hi, hipStream_t s);
     // q cells must be sorted ascending and unique per query.
     void search(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
                 const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
@@ -73,7 +81,7 @@ class SearchEngine {
    private:
     DevBuf<unsigned char> tmp_;
     DevBuf<uint64_t> k0_, k1_, uk_;
-    DevBuf<uint32_t> v0_, v1_, ur_, up_, uq_;
+    DevBuf<uint32_t> v0_, v1_, v2_, v3_, ur_, up_, uq_, cq_, gb_, ge_, dec_;
     DevBuf<int64_t> c0_, c1_, rc_, rs_, nr_, uc_, uo_;
     DevBuf<unsigned long long> counter_;
     DevBuf<uint32_t> oq_, oe_;

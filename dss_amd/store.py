@@ -60,7 +60,11 @@ class EntityIndex:
     subscriptions): replaces scd_cells_operations / RID cells INT64[] +
     INVERTED INDEX.  NULL conventions as include/dssgpu.h."""
 
-    def __init__(self, cell_offs, cells, alt_lo=None, alt_hi=None, t0=None, t1=None, owner=None, device: int = 0):
+    def __init__(self, cell_offs, cells, alt_lo=None, alt_hi=None, t0=None, t1=None, owner=None, device: int = 0,
+                 cell_range=None):
+        """cell_range=(lo, hi): a cell-range shard (dssg_index_build_range):
+        postings only for cells in [lo, hi] (uint64 order), entity cell lists
+        whole."""
         self.ctx = _lib.context(device)
         offs = np.ascontiguousarray(cell_offs, dtype=np.int64)
         n = len(offs) - 1
@@ -71,19 +75,21 @@ class EntityIndex:
         a1 = np.ascontiguousarray(t1 if t1 is not None else np.full(n, 2**63 - 1), dtype=np.int64)
         own = np.ascontiguousarray(owner, dtype=np.int32) if owner is not None else None
         h = C.c_void_p()
-        rc = self.ctx.L.dssg_index_build(self.ctx.h, n, _p(offs, C.c_int64), _p(cells, C.c_uint64),
-                                         _p(alo, C.c_float), _p(ahi, C.c_float), _p(a0, C.c_int64),
-                                         _p(a1, C.c_int64),
-                                         _p(own, C.c_int32) if own is not None else C.POINTER(C.c_int32)(),
-                                         C.byref(h))
+        lo, hi = cell_range if cell_range is not None else (0, 2**64 - 1)
+        rc = self.ctx.L.dssg_index_build_range(self.ctx.h, n, _p(offs, C.c_int64), _p(cells, C.c_uint64),
+                                               _p(alo, C.c_float), _p(ahi, C.c_float), _p(a0, C.c_int64),
+                                               _p(a1, C.c_int64),
+                                               _p(own, C.c_int32) if own is not None else C.POINTER(C.c_int32)(),
+                                               int(lo), int(hi), C.byref(h))
         self.ctx.check(rc)
         self.h = h
         self.n = n
 
     @classmethod
-    def from_lists(cls, cell_lists, alt_lo=None, alt_hi=None, t0=None, t1=None, owner=None, device=0):
+    def from_lists(cls, cell_lists, alt_lo=None, alt_hi=None, t0=None, t1=None, owner=None, device=0,
+                   cell_range=None):
         offs, cells = _csr(cell_lists)
-        return cls(offs, cells, alt_lo, alt_hi, t0, t1, owner, device)
+        return cls(offs, cells, alt_lo, alt_hi, t0, t1, owner, device, cell_range)
 
     @property
     def num_postings(self) -> int:

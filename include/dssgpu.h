@@ -128,6 +128,19 @@ int dssg_index_build(dssg_ctx *ctx, int64_t n, const int64_t *cell_offs, const u
 int dssg_index_build_device(dssg_ctx *ctx, int64_t n, const int64_t *d_cell_offs, const uint64_t *d_cells,
                             const float *d_alt_lo, const float *d_alt_hi, const int64_t *d_t0, const int64_t *d_t1,
                             const int32_t *d_owner, void *stream, dssg_index **out);
+/* Cell-range shard of the same index (the postings table
+ * scd_cells_operations is range-partitioned by cell_id, store.go:140-147):
+ * postings only for cells in [cell_lo, cell_hi] (uint64 order), entity cell
+ * lists whole, so a (query, entity) pair is emitted by exactly one shard --
+ * the one holding their smallest shared cell.  Searches take the full query
+ * batch. */
+int dssg_index_build_range(dssg_ctx *ctx, int64_t n, const int64_t *cell_offs, const uint64_t *cells,
+                           const float *alt_lo, const float *alt_hi, const int64_t *t0, const int64_t *t1,
+                           const int32_t *owner, uint64_t cell_lo, uint64_t cell_hi, dssg_index **out);
+int dssg_index_build_range_device(dssg_ctx *ctx, int64_t n, const int64_t *d_cell_offs, const uint64_t *d_cells,
+                                  const float *d_alt_lo, const float *d_alt_hi, const int64_t *d_t0, const int64_t *d_t1,
+                                  const int32_t *d_owner, uint64_t cell_lo, uint64_t cell_hi, void *stream,
+                                  dssg_index **out);
 void dssg_index_free(dssg_index *idx);
 int64_t dssg_index_num_postings(const dssg_index *idx);
 int64_t dssg_index_num_cells(const dssg_index *idx);
