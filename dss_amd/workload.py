@@ -120,6 +120,51 @@ def metro_footprints(rng, n, region=METRO, circle_frac=0.3, hotspots=None, hot_f
     return Footprints(kind, voff, lat, lng, radius_m)
 
 
+def _quads(rng, n, clat, clng, a, b, rot, cw):
+    """4-gons centred at (clat, clng): half-extents a (along rot) and b
+    (across), CCW unless cw.  Returns Footprints."""
+    corners = np.array([[-1, -1], [1, -1], [1, 1], [-1, 1]], dtype=np.float64)
+    order = np.where(cw[:, None], np.array([3, 2, 1, 0])[None, :], np.array([0, 1, 2, 3])[None, :])
+    cx = corners[order, 0] * a[:, None]
+    cy = corners[order, 1] * b[:, None]
+    c, s = np.cos(rot)[:, None], np.sin(rot)[:, None]
+    dx = cx * c - cy * s
+    dy = cx * s + cy * c
+    plat, plng = _offset(clat[:, None], clng[:, None], dx, dy)
+    voff = np.arange(n + 1, dtype=np.int64) * 4
+    return Footprints(np.full(n, KIND_POLYGON, np.int32), voff, plat.reshape(-1).copy(), plng.reshape(-1).copy(),
+                      np.zeros(n, np.float32))
+
+
+def city_blocks(rng, n, region=NYC) -> Footprints:
+    """city-block 4-gons, sides U[80, 250] m, rotated
+    U[0, 30] degrees, half of them clockwise (reversal path)."""
+    clat, clng = _centres(rng, n, region)
+    a = rng.uniform(80, 250, n) / 2
+    b = rng.uniform(80, 250, n) / 2
+    rot = np.radians(rng.uniform(0, 30, n))
+    cw = rng.random(n) < 0.5
+    return _quads(rng, n, clat, clng, a, b, rot, cw)
+
+
+CONUS_HOTSPOTS = [(40.71, -74.01), (34.05, -118.24), (41.88, -87.63), (29.76, -95.37), (33.45, -112.07),
+                  (39.95, -75.17), (29.42, -98.49), (32.72, -117.16), (32.78, -96.80), (37.34, -121.89),
+                  (30.27, -97.74), (39.74, -104.99), (47.61, -122.33), (42.36, -71.06), (38.91, -77.04),
+                  (36.17, -86.78), (45.52, -122.68), (25.76, -80.19), (33.75, -84.39), (44.98, -93.27)]
+
+
+def corridors(rng, n, region=CONUS, hotspots=CONUS_HOTSPOTS, hot_frac=0.8, sigma_m=20000.0) -> Footprints:
+    """long thin 4-gon corridors, length logU[5, 100]
+    km, width U[30, 300] m, orientation U[0, pi), 80% around 20 metro
+    hotspots (sigma 20 km), half of them clockwise."""
+    clat, clng = _centres(rng, n, region, hotspots, hot_frac, sigma_m)
+    length = np.exp(rng.uniform(np.log(5000.0), np.log(100000.0), n))
+    width = rng.uniform(30, 300, n)
+    rot = rng.uniform(0, np.pi, n)
+    cw = rng.random(n) < 0.5
+    return _quads(rng, n, clat, clng, length / 2, width / 2, rot, cw)
+
+
 @dataclass
 class Attrs:
     alt_lo: np.ndarray  # float32
@@ -151,23 +196,61 @@ def query_attrs(rng, n) -> Attrs:
     return Attrs(lo, hi, t0.astype(np.int64), t1.astype(np.int64))
 
 
+def rid_attrs(rng, n, query: bool) -> Attrs:
+    """SURVEY s8(d) config 4 (RID): ISAs t0 = T + U[0, 1 h), 30 s long;
+    queries earliest = T + U[0, 1 h), latest = earliest + 30 s.  RID search
+    has no altitude predicate (identification_service_area.go:170-180), so
+    altitudes are the NULL sentinels."""
+    t0 = T0_US + rng.integers(0, HOUR_US, n)
+    t1 = t0 + 30_000_000
+    inf = np.full(n, np.inf, np.float32)
+    return Attrs(-inf, inf, t0.astype(np.int64), t1.astype(np.int64))
+
+
+# BASELINE.json configs: (queries, entities, kind) at scale 1
+CONFIG_SIZES = {0: (10_000, 100_000), 1: (1_000_000, 1_000_000), 2: (1_000_000, 10_000_000),
+                3: (1_000_000, 5_000_000), 4: (1_000_000, 50_000_000)}
+CONFIG_NAMES = {0: "Go CPU ref: SF-Bay metro, circles+polygons",
+                1: "1xMI355X: SF-Bay metro, circles+polygons",
+                2: "8xMI355X: California, 70% around 4 hotspots",
+                3: "RID ISAs: NYC city blocks, 30 s windows",
+                4: "continent stress: CONUS corridors, 80% around 20 hotspots"}
+
+
 def config(i: int, scale: float = 1.0):
     """Return (rng, queries, q_attrs, intents, i_attrs, now_us) for BASELINE config i.
 
-    `scale` shrinks the counts (tests); the shapes and distributions stay."""
+    `scale` shrinks the counts (tests); the shapes and distributions stay.
+    Config 3 is RID (search_isas semantics: no altitude, 30 s windows)."""
     rng = np.random.default_rng(20201015 + i)
-    if i == 0:
-        nq, ni, region, kw = 10_000, 100_000, METRO, {}
-    elif i == 1:
-        nq, ni, region, kw = 1_000_000, 1_000_000, METRO, {}
-    elif i == 2:
-        nq, ni, region, kw = 1_000_000, 10_000_000, CALIFORNIA, dict(hotspots=CA_HOTSPOTS, hot_frac=0.7, sigma_m=15000.0)
-    else:
+    if i not in CONFIG_SIZES:
         raise ValueError(f"config {i} not generated here")
+    nq, ni = CONFIG_SIZES[i]
     nq = max(1, int(nq * scale))
     ni = max(1, int(ni * scale))
-    intents = metro_footprints(rng, ni, region, **kw)
-    ia = intent_attrs(rng, ni)
-    queries = metro_footprints(rng, nq, region, **kw)
-    qa = query_attrs(rng, nq)
+    if i in (0, 1, 2):
+        kw = dict(hotspots=CA_HOTSPOTS, hot_frac=0.7, sigma_m=15000.0) if i == 2 else {}
+        region = CALIFORNIA if i == 2 else METRO
+        intents = metro_footprints(rng, ni, region, **kw)
+        ia = intent_attrs(rng, ni)
+        queries = metro_footprints(rng, nq, region, **kw)
+        qa = query_attrs(rng, nq)
+    elif i == 3:
+        intents = city_blocks(rng, ni)
+        ia = rid_attrs(rng, ni, False)
+        queries = city_blocks(rng, nq)
+        qa = rid_attrs(rng, nq, True)
+    else:
+        intents = corridors(rng, ni)
+        ia = intent_attrs(rng, ni)
+        queries = corridors(rng, nq)
+        qa = query_attrs(rng, nq)
     return rng, queries, qa, intents, ia, T0_US
+
+
+def query_bounds(qa: Attrs, now_us: int):
+    """Query (tlo, thi) as the search kernels take them: SCD
+    `COALESCE(ends_at >= start) AND ends_at >= now` (operations.go:398-402)
+    and the RID app-layer clamp earliest = max(now, earliest) (isa.go:38-45)
+    both fold into tlo = max(t0, now)."""
+    return np.maximum(qa.t0, now_us), qa.t1
