@@ -11,11 +11,17 @@ coverings) -> overlap join against the HBM-resident index -> fused
 altitude/time/now filter -> deduplicated (query, intent) pairs resident in
 HBM.  The index (intent coverings + posting lists) is built before timing.
 
-Multi-GPU (torchrun, one process per GPU): the index fits every GPU's HBM
-many times over (~0.3 GB for 1M intents), so each rank holds a replica and
-owns a disjoint 1M-query slice of the global batch -- no exchange on the data
-path ("scaling": "weak").  Timing: barrier + synchronize on
-both sides of exactly --steps steps, max over ranks.
+Multi-GPU (torchrun, one process per GPU), --mode:
+  sharded (default for N > 1): the intent index is split into
+    N uint64 cell ranges at posting quantiles, one shard per GPU.  Each rank
+    covers its own 1M queries, routes every query (row + whole cell list) to
+    the shards owning its cells (all-to-all over RCCL/xGMI), joins what it
+    receives against its shard, and routes the pairs back to their queries'
+    home ranks (second all-to-all).  "scaling": "weak" (1M queries per GPU).
+  replica: every rank holds the whole index and joins its own slice; no
+    collective on the data path.
+Timing: barrier + synchronize on both sides of exactly --steps steps, max
+over ranks.
 """
 import argparse
 import json
@@ -48,6 +54,11 @@ def main():
     ap.add_argument("--no-verify", action="store_true", help="skip the full-size GPU-vs-oracle parity check")
     ap.add_argument("--survey-model", type=int, default=1, help="also count SURVEY s8(d)'s per-query byte model")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--mode", choices=["sharded", "replica"], default=None,
+                    help="multi-GPU layout (default: sharded for N > 1, replica for N = 1)")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on a multi-GPU node; gloo for rehearsals")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal: every rank on cuda:0 (one-GPU box, gloo backend)")
     args = ap.parse_args()
 
     import torch
@@ -55,10 +66,17 @@ def main():
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", 0))
+    mode = args.mode or ("sharded" if world > 1 else "replica")
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    stage_host = args.dist_backend != "nccl"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")   # single-process sharded runs (no torchrun)
+    os.environ.setdefault("MASTER_PORT", "29533")
+    if world > 1 or mode == "sharded":
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
+        else:
+            dist.init_process_group(args.dist_backend, rank=rank, world_size=world)
 
     from dss_amd import _lib, device as D, workload as W
 
@@ -86,17 +104,35 @@ def main():
     torch.cuda.synchronize()
     tb = time.time()
     icells = D.cover(ctx, d_int)
-    index = D.build_index(ctx, icells, i_alo, i_ahi, i_t0, i_t1)
+    ranges = None
+    if mode == "sharded":
+        from dss_amd import shard
+        # splitters from the intent postings (host), then this rank's shard
+        i_offs_h = D.copy_back(ctx, icells.offs, ni + 1, np.int64)
+        i_cells_h = D.copy_back(ctx, icells.cells, int(i_offs_h[-1]), np.uint64)
+        ranges = shard.cell_splitters(i_cells_h, world)
+        # parity reference: the whole index, built while icells is valid (the
+        # next cover() reuses its buffers)
+        full_index = None if args.no_verify else D.build_index(ctx, icells, i_alo, i_ahi, i_t0, i_t1)
+        tb = time.time()
+        index = D.build_index(ctx, icells, i_alo, i_ahi, i_t0, i_t1, cell_range=ranges[rank])
+    else:
+        index = D.build_index(ctx, icells, i_alo, i_ahi, i_t0, i_t1)
     torch.cuda.synchronize()
     build_s = time.time() - tb
     n_post = int(ctx.L.dssg_index_num_postings(index))
     # keep intent cells for the CPU baseline before the next cover() reuses buffers
     i_offs_h = D.copy_back(ctx, icells.offs, ni + 1, np.int64)
     i_cells_h = D.copy_back(ctx, icells.cells, int(i_offs_h[-1]), np.uint64)
-    log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s, index build {build_s:.2f}s, postings {n_post}")
+    log(f"[rank {rank}] mode {mode}, setup {time.time() - t_setup:.1f}s, index build {build_s:.2f}s, postings {n_post}")
+    sharded = None
+    if mode == "sharded":
+        sharded = shard.ShardedSearch(ctx, index, ranges, stage_host=stage_host)
 
-    def step():
+    def step(timed=False):
         cells = D.cover(ctx, d_q)
+        if sharded is not None:
+            return cells, sharded.step(cells.offs, cells.cells, nq, q_alo, q_ahi, q_tlo, q_thi, timed=timed)
         pairs = D.search(ctx, index, cells, q_alo, q_ahi, q_tlo, q_thi)
         return cells, pairs
 
@@ -121,6 +157,13 @@ def main():
         elapsed = float(tt.item())
     ms_per_step = 1000.0 * elapsed / max(1, args.steps)
     value = world * nq * args.steps / elapsed
+
+    if sharded is not None:
+        sharded_report(args, ctx, D, dist, torch, sharded, step, full_index, i_cells_h, ranges, rank, world, nq, ni,
+                       n_post, build_s, value, ms_per_step, q_alo, q_ahi, q_tlo, q_thi)
+        ctx.L.dssg_index_free(index)
+        dist.destroy_process_group()
+        return
 
     # ------------------------------------------- phase timing + roofline
     import ctypes as C
@@ -206,6 +249,112 @@ def main():
     ctx.L.dssg_index_free(index)
     if world > 1:
         dist.destroy_process_group()
+
+
+def mix64(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finalizer (uint64, wrapping): an order-independent pair-set
+    checksum is sum(mix64(q << 32 | e)) mod 2^64."""
+    with np.errstate(over="ignore"):
+        z = x.astype(np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def pair_checksum(keys: np.ndarray) -> int:
+    tot = np.uint64(0)
+    with np.errstate(over="ignore"):
+        for k in range(0, len(keys), 1 << 24):
+            tot = tot + mix64(keys[k:k + (1 << 24)]).sum(dtype=np.uint64)
+    return int(tot)
+
+
+def sharded_report(args, ctx, D, dist, torch, sh, step, full, i_cells_h, ranges, rank, world, nq, ni, n_post, build_s,
+                   value, ms_per_step, q_alo, q_ahi, q_tlo, q_thi):
+    """Phase breakdown (synchronised passes, max over ranks), the shard join's
+    roofline, and parity: every rank's delivered pair set == a whole-index
+    search of its own queries (count + order-independent checksum)."""
+    import ctypes as C
+    dev = f"cuda:{torch.cuda.current_device()}"
+    ctx.L.dssg_set_timing(ctx.h, 1)
+    sh.times = {}
+    reps = 5
+    cover_ms, kern_ms = [], []
+    for _ in range(reps):
+        cells, out = step(timed=True)
+        ca, cb, cc = C.c_double(), C.c_double(), C.c_double()
+        ctx.L.dssg_phase_times(ctx.h, C.byref(ca), C.byref(cb), C.byref(cc))
+        cover_ms.append(ca.value)
+        kern_ms.append(cc.value)
+    ctx.L.dssg_set_timing(ctx.h, 0)
+    names = ["route", "exchange_queries", "join", "route_pairs", "exchange_pairs"]
+    ph = [float(np.mean(cover_ms))] + [1000.0 * sh.times.get(k, 0.0) / reps for k in names] + [float(np.mean(kern_ms))]
+    tph = torch.tensor(ph, dtype=torch.float64, device=dev)
+    dist.all_reduce(tph, op=dist.ReduceOp.MAX)
+    ph = tph.tolist()
+    phase = dict(zip(["cover"] + names + ["join_kernel"], ph))
+    # shard join roofline (DESIGN.md s5 byte model over what this shard joined)
+    rc = sh.last_recv_cells.cpu().numpy().view(np.uint64)
+    lo, hi = ranges[rank]
+    own = i_cells_h[(i_cells_h >= np.uint64(lo)) & (i_cells_h <= np.uint64(hi))]
+    p_touched = touched_postings(own, rc)
+    jb = 24 * sh.last_rows + 8 * len(rc) + 28 * p_touched + 8 * sh.last_shard_pairs
+    kern = ph[-1]
+    local = torch.tensor([jb / (float(np.mean(kern_ms)) * 1e-3) / 1e9, float(sh.last_rows), float(len(rc)),
+                          float(sh.last_shard_pairs), float(out.numel())], dtype=torch.float64, device=dev)
+    mins = local.clone()
+    dist.all_reduce(mins, op=dist.ReduceOp.MIN)
+    sums = local.clone()
+    dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+    # parity: whole-index search of this rank's own queries
+    parity = None
+    if full is not None:
+        pairs = D.search(ctx, full, cells, q_alo, q_ahi, q_tlo, q_thi)  # cells: the last step's covering
+        torch.cuda.synchronize()
+        fq = D.copy_back(ctx, pairs.q, pairs.n, np.uint32).astype(np.uint64)
+        fe = D.copy_back(ctx, pairs.e, pairs.n, np.uint32).astype(np.uint64)
+        ctx.L.dssg_index_free(full)
+        want = (fq << np.uint64(32)) | fe
+        got = out.cpu().numpy().view(np.uint64)
+        ok = len(want) == len(got) and pair_checksum(want) == pair_checksum(got)
+        t = torch.tensor([1.0 if ok else 0.0, float(len(got))], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        parity = {"check": "per rank: count + sum(splitmix64(q << 32 | e)) of the delivered pairs == a whole-index "
+                           "search of the rank's own queries", "all_ranks_equal": bool(t[0].item() == 1.0)}
+    if rank != 0:
+        return
+    result = {
+        "metric": "4D conflict queries/sec vs N-intent airspace",
+        "value": value,
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded SURVEY s8(d) generator; no datasets)",
+        "config": {"workload": f"configs[{args.config}]: {nq} query footprints/GPU/step (70% polygon, 30% circle)"
+                               f" vs a {ni}-intent index sharded by S2 cell range over {world} GPU(s), SF-Bay metro,"
+                               " S2 level 13",
+                   "queries_per_gpu_step": nq, "intents": ni, "postings_rank0": n_post,
+                   "parallelism": f"cell-range shards x{world}; queries routed to shards and pairs routed home by "
+                                  f"all-to-all ({args.dist_backend})", "scale": args.scale},
+        "coverings_per_s": world * nq / (phase["cover"] * 1e-3),
+        "phase_ms_max_over_ranks": phase,
+        "routed": {"rows_total": sums[1].item(), "rows_min_rank": mins[1].item(), "cells_total": sums[2].item(),
+                   "pairs_total": sums[4].item()},
+        "index_build_s": build_s,
+        "roofline": {"kernel": "k_join on the shard (overlap join + fused altitude/time filter)", "bound": "hbm",
+                     "achieved": local[0].item(), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": local[0].item() / HBM_PEAK_GBS, "traffic": None, "rank": 0,
+                     "algorithmic_bytes": jb, "launch_ms": float(np.mean(kern_ms))},
+        "cpu_baseline": None,
+        "parity": parity,
+    }
+    print(json.dumps(result), flush=True)
 
 
 def touched_postings(i_cells, q_cells):

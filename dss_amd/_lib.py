@@ -51,6 +51,17 @@ class Pairs(C.Structure):
     _fields_ = [("q", C.c_void_p), ("e", C.c_void_p), ("n", C.c_int64)]
 
 
+MAX_PARTS = 64
+ROUTE_ROW_BYTES = 32
+
+
+class Batch(C.Structure):
+    """dssg_batch: a received (unpacked) query batch."""
+    _fields_ = [("n", C.c_int64), ("offs", C.c_void_p), ("cells", C.c_void_p), ("alt_lo", C.c_void_p),
+                ("alt_hi", C.c_void_p), ("tlo", C.c_void_p), ("thi", C.c_void_p), ("home", C.c_void_p),
+                ("qid", C.c_void_p)]
+
+
 _lib = None
 _lock = threading.Lock()
 
@@ -106,6 +117,16 @@ def load():
         L.dssg_search_isas.argtypes = [vp, vp, i64, P(i64), P(u64), P(i64), P(i64), P(u32), P(u32), i64, P(i64)]
         L.dssg_search_subscriptions.argtypes = [vp, vp, i64, P(i64), P(u64), P(i32), i64, P(u32), P(u32), i64,
                                                 P(i64)]
+        L.dssg_index_set_notification_index.argtypes = [vp, vp, P(i64)]
+        L.dssg_index_get_notification_index.argtypes = [vp, vp, P(i64)]
+        L.dssg_notify_subscriptions.argtypes = [vp, vp, i64, P(i64), P(u64), i64, P(u32), P(u32), P(i64), i64, P(i64)]
+        L.dssg_owner_subscriptions.argtypes = [vp, vp, i64, P(i32), i64, P(u32), P(u32), i64, P(i64)]
+        L.dssg_max_subscription_count.argtypes = [vp, vp, i64, P(i64), P(u64), P(i32), i64, P(i64)]
+        L.dssg_route_plan_device.argtypes = [vp, i64, vp, vp, i32, vp, vp, P(i64), P(i64)]
+        L.dssg_route_fill_device.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.dssg_unpack_queries_device.argtypes = [vp, i64, vp, vp, i32, P(i64), vp, P(Batch)]
+        L.dssg_route_pairs_plan_device.argtypes = [vp, P(Batch), P(Pairs), i32, vp, P(i64)]
+        L.dssg_route_pairs_fill_device.argtypes = [vp, P(Batch), P(Pairs), vp, vp]
         L.dssg_phase_times.argtypes = [vp, P(d), P(d), P(d)]
         L.dssg_set_timing.argtypes = [vp, C.c_int]
         L.dssg_set_timing.restype = None

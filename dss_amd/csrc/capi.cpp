@@ -12,13 +12,17 @@
 
 #include "common.hpp"
 #include "cover.hpp"
+#include "route.hpp"
 #include "search.hpp"
+#include "subs.hpp"
 
 struct dssg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     dss::CoverEngine cover;
     dss::SearchEngine search;
+    dss::RouteEngine route;
+    dss::SubsEngine subs;
     std::string last_error;
     bool timing = false;
     double cover_ms = 0, join_ms = 0;
@@ -131,6 +135,26 @@ void sort_pairs_host(uint32_t *q, uint32_t *e, int64_t n)
         q[i] = (uint32_t)(k[i] >> 32);
         e[i] = (uint32_t)k[i];
     }
+}
+
+// Per-query sort + unique of the query cells (CellUnion order; UnionVolumes4D
+// hands the store unsorted cells, quirk Q14), uploaded to the context's
+// staging buffers.
+void stage_query_cells(dssg_ctx *ctx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells, hipStream_t s,
+                       const int64_t **d_offs, const uint64_t **d_cells)
+{
+    std::vector<int64_t> offs((size_t)nq + 1, 0);
+    std::vector<uint64_t> cells;
+    cells.reserve((size_t)q_offs[nq]);
+    for (int64_t q = 0; q < nq; q++) {
+        size_t b = cells.size();
+        cells.insert(cells.end(), q_cells + q_offs[q], q_cells + q_offs[q + 1]);
+        std::sort(cells.begin() + (long)b, cells.end());
+        cells.erase(std::unique(cells.begin() + (long)b, cells.end()), cells.end());
+        offs[(size_t)q + 1] = (int64_t)cells.size();
+    }
+    *d_offs = upload(ctx->d_qoffs, offs.data(), nq + 1, s);
+    *d_cells = upload(ctx->d_cells, cells.data(), (int64_t)cells.size(), s);
 }
 
 }  // namespace
@@ -415,22 +439,12 @@ int dssg_search(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t 
     if (nq > 0 && (!q_alt_lo || !q_alt_hi || !q_tlo || !q_thi)) return DSSG_ERR_INVALID;
     int code = DSSG_OK;
     int rc = guarded(ctx, [&] {
-        // per-query sort + unique (CellUnion order; UnionVolumes4D output is
-        // unsorted, quirk Q14)
-        std::vector<int64_t> offs((size_t)nq + 1, 0);
-        std::vector<uint64_t> cells;
-        cells.reserve((size_t)q_offs[nq]);
-        for (int64_t q = 0; q < nq; q++) {
+        for (int64_t q = 0; q < nq; q++)
             if (q_tlo[q] == INT64_MIN) throw dss::Error(DSSG_ERR_INVALID, "query tlo must not be NULL");
-            size_t b = cells.size();
-            cells.insert(cells.end(), q_cells + q_offs[q], q_cells + q_offs[q + 1]);
-            std::sort(cells.begin() + (long)b, cells.end());
-            cells.erase(std::unique(cells.begin() + (long)b, cells.end()), cells.end());
-            offs[(size_t)q + 1] = (int64_t)cells.size();
-        }
         hipStream_t s = ctx->stream;
-        const int64_t *dqo = upload(ctx->d_qoffs, offs.data(), nq + 1, s);
-        const uint64_t *dqc = upload(ctx->d_cells, cells.data(), (int64_t)cells.size(), s);
+        const int64_t *dqo = nullptr;
+        const uint64_t *dqc = nullptr;
+        stage_query_cells(ctx, nq, q_offs, q_cells, s, &dqo, &dqc);
         const float *dlo = upload(ctx->d_alo, q_alt_lo, nq, s);
         const float *dhi = upload(ctx->d_ahi, q_alt_hi, nq, s);
         const int64_t *dtl = upload(ctx->d_tlo, q_tlo, nq, s);
@@ -493,6 +507,163 @@ int dssg_search_subscriptions(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, 
     std::vector<int64_t> tlo((size_t)nq, now_us), thi((size_t)nq, INT64_MAX);
     return dssg_search(ctx, idx, nq, q_offs, q_cells, lo.data(), hi.data(), tlo.data(), thi.data(), owner, out_q, out_e,
                        cap, needed);
+}
+
+int dssg_route_plan_device(dssg_ctx *ctx, int64_t nq, const int64_t *d_q_offs, const uint64_t *d_q_cells,
+                           int32_t nparts, const uint64_t *d_part_hi, void *stream, int64_t *row_counts,
+                           int64_t *cell_counts)
+{
+    if (!ctx || nq < 0 || !d_part_hi || !row_counts || !cell_counts || nparts < 1 || nparts > DSSG_MAX_PARTS ||
+        (nq > 0 && (!d_q_offs || !d_q_cells)))
+        return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        ctx->route.plan(nq, d_q_offs, d_q_cells, nparts, d_part_hi, s, row_counts, cell_counts);
+    });
+}
+
+int dssg_route_fill_device(dssg_ctx *ctx, int64_t nq, const int64_t *d_q_offs, const uint64_t *d_q_cells,
+                           const float *d_q_alt_lo, const float *d_q_alt_hi, const int64_t *d_q_tlo,
+                           const int64_t *d_q_thi, void *stream, void *d_rows_out, uint64_t *d_cells_out)
+{
+    if (!ctx || nq < 0 || (nq > 0 && (!d_q_offs || !d_q_cells || !d_q_alt_lo || !d_q_alt_hi || !d_q_tlo || !d_q_thi ||
+                                      !d_rows_out || !d_cells_out)))
+        return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        ctx->route.fill(nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo, d_q_thi, s, d_rows_out, d_cells_out);
+    });
+}
+
+int dssg_unpack_queries_device(dssg_ctx *ctx, int64_t nrows, const void *d_rows, const uint64_t *d_cells,
+                               int32_t nparts, const int64_t *src_rows, void *stream, dssg_batch *out)
+{
+    if (!ctx || !out || nrows < 0 || !src_rows || nparts < 1 || nparts > DSSG_MAX_PARTS || (nrows > 0 && !d_rows))
+        return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        ctx->route.unpack(nrows, d_rows, d_cells, nparts, src_rows, s, out);
+    });
+}
+
+int dssg_route_pairs_plan_device(dssg_ctx *ctx, const dssg_batch *batch, const dssg_pairs *pairs, int32_t nparts,
+                                 void *stream, int64_t *counts)
+{
+    if (!ctx || !batch || !pairs || !counts || nparts < 1 || nparts > DSSG_MAX_PARTS || pairs->n < 0)
+        return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        ctx->route.pairs_plan(batch, pairs, nparts, s, counts);
+    });
+}
+
+int dssg_route_pairs_fill_device(dssg_ctx *ctx, const dssg_batch *batch, const dssg_pairs *pairs, void *stream,
+                                 uint64_t *d_out)
+{
+    if (!ctx || !batch || !pairs || pairs->n < 0 || (pairs->n > 0 && !d_out)) return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        ctx->route.pairs_fill(batch, pairs, s, d_out);
+    });
+}
+
+int dssg_index_set_notification_index(dssg_ctx *ctx, dssg_index *idx, const int64_t *values)
+{
+    if (!ctx || !idx || (idx->n_e > 0 && !values)) return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        if (idx->n_e > 0)
+            DSS_HIP(hipMemcpy(idx->e_notify.p, values, sizeof(int64_t) * (size_t)idx->n_e, hipMemcpyHostToDevice));
+    });
+}
+
+int dssg_index_get_notification_index(dssg_ctx *ctx, const dssg_index *idx, int64_t *values)
+{
+    if (!ctx || !idx || (idx->n_e > 0 && !values)) return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        if (idx->n_e > 0)
+            DSS_HIP(hipMemcpy(values, idx->e_notify.p, sizeof(int64_t) * (size_t)idx->n_e, hipMemcpyDeviceToHost));
+    });
+}
+
+int dssg_notify_subscriptions(dssg_ctx *ctx, dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
+                              int64_t now_us, uint32_t *out_q, uint32_t *out_e, int64_t *out_index, int64_t cap,
+                              int64_t *needed)
+{
+    if (!ctx || !idx || !needed || nq < 0 || !q_offs || now_us == INT64_MIN) return DSSG_ERR_INVALID;
+    int code = DSSG_OK;
+    int rc = guarded(ctx, [&] {
+        hipStream_t s = ctx->stream;
+        const int64_t *dqo = nullptr;
+        const uint64_t *dqc = nullptr;
+        stage_query_cells(ctx, nq, q_offs, q_cells, s, &dqo, &dqc);
+        // RID subscriptions.go:207-212 / SCD subscriptions.go:133-170:
+        // cells overlap AND ends_at >= now; no altitude or start predicate
+        std::vector<float> lo((size_t)nq + 1, -INFINITY), hi((size_t)nq + 1, INFINITY);
+        std::vector<int64_t> tlo((size_t)nq + 1, now_us), thi((size_t)nq + 1, INT64_MAX);
+        const float *dlo = upload(ctx->d_alo, lo.data(), nq, s);
+        const float *dhi = upload(ctx->d_ahi, hi.data(), nq, s);
+        const int64_t *dtl = upload(ctx->d_tlo, tlo.data(), nq, s);
+        const int64_t *dth = upload(ctx->d_thi, thi.data(), nq, s);
+        dssg_pairs res;
+        ctx->search.search(idx, nq, dqo, dqc, dlo, dhi, dtl, dth, nullptr, s, &res);
+        *needed = res.n;
+        if (res.n > cap) {  // no counter moves unless the caller can take the rows
+            code = DSSG_ERR_CAPACITY;
+            return;
+        }
+        if (res.n > 0 && (!out_q || !out_e || !out_index)) throw dss::Error(DSSG_ERR_INVALID, "output pointers are NULL");
+        uint32_t *dq, *de;
+        int64_t *dv;
+        ctx->subs.notify(idx, &res, s, &dq, &de, &dv);
+        if (res.n > 0) {
+            DSS_HIP(hipMemcpyAsync(out_q, dq, sizeof(uint32_t) * (size_t)res.n, hipMemcpyDeviceToHost, s));
+            DSS_HIP(hipMemcpyAsync(out_e, de, sizeof(uint32_t) * (size_t)res.n, hipMemcpyDeviceToHost, s));
+            DSS_HIP(hipMemcpyAsync(out_index, dv, sizeof(int64_t) * (size_t)res.n, hipMemcpyDeviceToHost, s));
+        }
+        DSS_HIP(hipStreamSynchronize(s));
+    });
+    return rc ? rc : code;
+}
+
+int dssg_owner_subscriptions(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int32_t *owner, int64_t now_us,
+                             uint32_t *out_q, uint32_t *out_e, int64_t cap, int64_t *needed)
+{
+    if (!ctx || !idx || !needed || nq < 0 || (nq > 0 && !owner) || now_us == INT64_MIN) return DSSG_ERR_INVALID;
+    int code = DSSG_OK;
+    int rc = guarded(ctx, [&] {
+        hipStream_t s = ctx->stream;
+        const int32_t *dow = upload(ctx->d_owner, owner, nq, s);
+        uint32_t *dq, *de;
+        const int64_t n = ctx->subs.owner_subs(idx, nq, dow, now_us, s, &dq, &de);
+        *needed = n;
+        if (n > cap) {
+            code = DSSG_ERR_CAPACITY;
+            return;
+        }
+        if (n > 0) {
+            if (!out_q || !out_e) throw dss::Error(DSSG_ERR_INVALID, "output pointers are NULL");
+            DSS_HIP(hipMemcpyAsync(out_q, dq, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, s));
+            DSS_HIP(hipMemcpyAsync(out_e, de, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, s));
+            DSS_HIP(hipStreamSynchronize(s));
+        }
+    });
+    return rc ? rc : code;
+}
+
+int dssg_max_subscription_count(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *q_offs,
+                                const uint64_t *q_cells, const int32_t *owner, int64_t now_us, int64_t *out_count)
+{
+    if (!ctx || !idx || nq < 0 || !q_offs || (nq > 0 && (!owner || !out_count)) || now_us == INT64_MIN)
+        return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = ctx->stream;
+        const int64_t nqc = q_offs[nq] - q_offs[0];
+        if (nqc < 0 || q_offs[0] != 0) throw dss::Error(DSSG_ERR_INVALID, "q_offs must start at 0 and ascend");
+        const int64_t *dqo = upload(ctx->d_qoffs, q_offs, nq + 1, s);
+        const uint64_t *dqc = upload(ctx->d_cells, q_cells, nqc, s);
+        const int32_t *dow = upload(ctx->d_owner, owner, nq, s);
+        ctx->subs.max_count(idx, nq, dqo, dqc, nqc, dow, now_us, s, out_count);
+    });
 }
 
 int dssg_search_stats_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *d_q_offs,

@@ -1,0 +1,131 @@
+// Device view of a dssg_index (search.hpp) shared by the kernels that read
+// the index: the overlap join (search.hip) and the subscription-store
+// queries (subs.hip).  Layout: DESIGN.md s3.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "search.hpp"
+
+namespace dss {
+namespace {
+
+constexpr uint32_t kFirstBit = 0x80000000u;
+constexpr uint64_t kLsb13 = 1ull << 34;
+
+__device__ __forceinline__ int64_t tid64() { return (int64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+__host__ __device__ __forceinline__ bool is_regular(uint64_t c)
+{
+    return (c & ((kLsb13 << 1) - 1)) == kLsb13 && (c >> 61) < 6;  // level 13, valid face
+}
+__host__ __device__ __forceinline__ unsigned long long order_key(long long t)
+{
+    return (unsigned long long)t ^ 0x8000000000000000ull;  // signed order as unsigned
+}
+
+struct Buckets {
+    long long tbase;
+    int shift;
+    int nb;
+};
+// Monotone in t, so B(max(a, b)) = max(B(a), B(b)).
+__device__ __forceinline__ int bucket_of(long long t, const Buckets &bk)
+{
+    if (t <= bk.tbase) return 0;
+    unsigned long long d = ((unsigned long long)t - (unsigned long long)bk.tbase) >> bk.shift;
+    return d >= (unsigned long long)bk.nb ? bk.nb - 1 : (int)d;
+}
+
+// Device view of a dssg_index.
+struct IndexView {
+    uint64_t kmin;
+    int64_t n_dense;
+    const uint32_t *dense;
+    int64_t n_irr;
+    const uint64_t *irr_cells;
+    const uint32_t *irr_start;
+    const uint32_t *p_e;
+    const int64_t *e_offs;
+    const uint64_t *e_cells;
+    const unsigned long long *s_mask;
+    const uint32_t *s_base;
+    const uint32_t *bk_start;
+    const uint32_t *b_e;
+    const float2 *b_alt;
+    const longlong2 *b_t;
+    const uint8_t *b_meta;
+    const ulonglong2 *b_sig;
+    const int32_t *b_owner;
+    const uint32_t *p_mult;  // multiplicity of (cell, entity) in the stored cell array
+    const int64_t *e_t1;     // entity end time (us)
+    const int32_t *e_owner;  // entity owner (nullptr: built without owners)
+    Buckets bk;
+};
+
+IndexView view_of(const dssg_index *idx)
+{
+    IndexView v{};
+    v.kmin = idx->kmin;
+    v.n_dense = idx->n_dense;
+    v.dense = idx->dense.p;
+    v.n_irr = idx->n_irr;
+    v.irr_cells = idx->irr_cells.p;
+    v.irr_start = idx->irr_start.p;
+    v.p_e = idx->p_e.p;
+    v.e_offs = idx->e_offs.p;
+    v.e_cells = idx->e_cells.p;
+    v.s_mask = idx->s_mask.p;
+    v.s_base = idx->s_base.p;
+    v.bk_start = idx->bk_start.p;
+    v.b_e = idx->b_e.p;
+    v.b_alt = idx->b_alt.p;
+    v.b_t = idx->b_t.p;
+    v.b_meta = idx->b_meta.p;
+    v.b_sig = idx->b_sig.p;
+    v.b_owner = idx->has_owner ? idx->b_owner.p : nullptr;
+    v.p_mult = idx->p_mult.p;
+    v.e_t1 = idx->e_t1.p;
+    v.e_owner = idx->has_owner ? idx->e_owner.p : nullptr;
+    v.bk = Buckets{idx->tbase, idx->shift, idx->nb};
+    return v;
+}
+
+// Slot of cell c, or false if c is in neither table.
+__device__ __forceinline__ bool find_slot(const IndexView &a, uint64_t c, uint32_t &slot)
+{
+    if (is_regular(c)) {
+        uint64_t k = c >> 35;
+        if (k < a.kmin || (int64_t)(k - a.kmin) >= a.n_dense) return false;
+        slot = (uint32_t)(k - a.kmin);
+        return true;
+    }
+    int64_t lo = 0, hi = a.n_irr;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (a.irr_cells[mid] < c) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo < a.n_irr && a.irr_cells[lo] == c) {
+        slot = (uint32_t)(a.n_dense + lo);
+        return true;
+    }
+    return false;
+}
+__device__ __forceinline__ uint64_t cell_of_slot(const IndexView &a, uint32_t slot)
+{
+    if ((int64_t)slot < a.n_dense) return ((a.kmin + slot) << 35) | kLsb13;
+    return a.irr_cells[slot - (uint32_t)a.n_dense];
+}
+__device__ __forceinline__ void plain_range(const IndexView &a, uint32_t slot, uint32_t &s, uint32_t &e)
+{
+    if ((int64_t)slot < a.n_dense) {
+        s = a.dense[slot];
+        e = a.dense[slot + 1];
+    } else {
+        uint32_t k = slot - (uint32_t)a.n_dense;
+        s = a.irr_start[k];
+        e = a.irr_start[k + 1];
+    }
+}
+
+}  // namespace
+}  // namespace dss

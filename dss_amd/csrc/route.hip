@@ -1,0 +1,303 @@
+// Cell-range shard routing on gfx950.
+//
+// The reference partitions its postings table scd_cells_operations by
+// cell_id range inside CockroachDB (pkg/scd/store/cockroach/store.go:140-147)
+// and lets the SQL layer fan a query out to the ranges its cells hit.  Here
+// the fan-out is explicit, one process per GPU:
+//
+//   home rank:  covered query batch --k_route<0>/k_route<1>--> part-major
+//               send buffers (one 32-byte row + the query's whole cell list
+//               per (query, shard that owns >= 1 of its cells));
+//   exchange:   all-to-all (RCCL over xGMI; dss_amd/shard.py);
+//   shard:      k_unpack_rows -> a plain query batch for dssg_search_device
+//               against the shard's cell-range index;
+//   shard:      k_route_pairs<0>/<1> -> the pair set, part-major by the
+//               query's home rank, packed (home-local query << 32 | entity);
+//   exchange:   all-to-all back; each home rank holds its queries' pairs.
+//
+// A shard receives a query's WHOLE cell list, and the shard index keeps every
+// entity's whole cell list, so the smallest-shared-cell rule of the join
+// emits each (query, entity) pair on exactly one shard: no cross-shard dedupe.
+//
+// Slots inside a destination segment come from one 64-bit atomic per wave and
+// destination, packing (rows << 40 | cells): a segment's cell lists are laid
+// out in the order of its rows, which is all the receiver needs to rebuild
+// the CSR offsets.  Row order within a segment is unspecified (result sets
+// are unordered, quirk Q13).
+#include <hip/hip_runtime.h>
+
+#include "route.hpp"
+
+namespace dss {
+namespace {
+
+constexpr unsigned kBlock = 256;
+constexpr int kCellBits = 40;
+constexpr unsigned long long kCellMask = (1ull << kCellBits) - 1ull;
+
+__device__ __forceinline__ int64_t tid64() { return (int64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+
+// First part r with c <= hi[r] (hi ascending, hi[np-1] = UINT64_MAX).
+__device__ __forceinline__ int part_of(uint64_t c, const uint64_t *hi, int np)
+{
+    int lo = 0, h = np - 1;
+    while (lo < h) {
+        const int m = (lo + h) >> 1;
+        if (c <= hi[m]) h = m;
+        else lo = m + 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ unsigned long long wave_or(unsigned long long v)
+{
+    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o);
+    return v;
+}
+
+// Inclusive wave scan of v (64 lanes).
+__device__ __forceinline__ unsigned long long wave_scan(unsigned long long v, int lane)
+{
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// PASS 0: destination mask of every query (parts holding >= 1 of its cells)
+// and per-part totals (rows, cells).  PASS 1: rows and cell lists written
+// into the part-major buffers at row_base[d] / cell_base[d] + cursor.
+template <int PASS>
+__global__ __launch_bounds__(kBlock) void k_route(int64_t nq, const int64_t *offs, const uint64_t *cells, const float *alo,
+                                                  const float *ahi, const int64_t *tlo, const int64_t *thi, int np,
+                                                  const uint64_t *part_hi, unsigned long long *mask,
+                                                  unsigned long long *tot_rows, unsigned long long *tot_cells,
+                                                  const int64_t *row_base, const int64_t *cell_base,
+                                                  unsigned long long *cursor, QRow *rows, uint64_t *out_cells)
+{
+    const int64_t q = tid64();
+    const int lane = threadIdx.x & 63;
+    const bool live = q < nq;
+    unsigned long long m = 0;
+    int64_t c0 = 0, nc = 0;
+    if (live) {
+        c0 = offs[q];
+        nc = offs[q + 1] - c0;
+        if (PASS == 0) {
+            for (int64_t k = 0; k < nc; k++) m |= 1ull << part_of(cells[c0 + k], part_hi, np);
+            mask[q] = m;
+        } else {
+            m = mask[q];
+        }
+    }
+    unsigned long long wm = wave_or(m);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    while (wm) {  // wave-uniform loop over the destinations this wave meets
+        const int d = __builtin_ctzll(wm);
+        wm &= wm - 1;
+        const bool has = (m >> d) & 1ull;
+        const unsigned long long bal = __ballot(has);
+        const unsigned long long v = has ? (unsigned long long)nc : 0ull;
+        const unsigned long long inc = wave_scan(v, lane);
+        const unsigned long long wcells = __shfl(inc, 63);
+        const unsigned long long wrows = (unsigned long long)__popcll(bal);
+        if (PASS == 0) {
+            if (lane == 0) {
+                atomicAdd(&tot_rows[d], wrows);
+                atomicAdd(&tot_cells[d], wcells);
+            }
+            continue;
+        }
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(&cursor[d], (wrows << kCellBits) | wcells);
+        base = __shfl(base, 0);
+        if (!has) continue;
+        const int64_t r = row_base[d] + (int64_t)(base >> kCellBits) + __popcll(bal & below);
+        const int64_t cp = cell_base[d] + (int64_t)(base & kCellMask) + (int64_t)(inc - v);
+        QRow row;
+        row.tlo = tlo[q];
+        row.thi = thi[q];
+        row.alo = alo[q];
+        row.ahi = ahi[q];
+        row.qid = (uint32_t)q;
+        row.ncells = (uint32_t)nc;
+        rows[r] = row;
+        for (int64_t k = 0; k < nc; k++) out_cells[cp + k] = cells[c0 + k];
+    }
+}
+
+// Received rows (source-part-major) -> a plain query batch: SoA attributes,
+// per-row cell counts (scanned into offsets by the host driver), home part
+// and home-local query id.
+__global__ void k_unpack_rows(int64_t n, const QRow *rows, int np, const int64_t *src_base, int64_t *ncells, float *alo,
+                              float *ahi, int64_t *tlo, int64_t *thi, uint32_t *home, uint32_t *qid)
+{
+    const int64_t i = tid64();
+    if (i >= n) return;
+    const QRow r = rows[i];
+    int src = 0;
+    while (src + 1 < np && src_base[src + 1] <= i) src++;
+    ncells[i] = r.ncells;
+    alo[i] = r.alo;
+    ahi[i] = r.ahi;
+    tlo[i] = r.tlo;
+    thi[i] = r.thi;
+    home[i] = (uint32_t)src;
+    qid[i] = r.qid;
+}
+
+// Pairs (batch row, entity) -> part-major by the row's home part, packed
+// (home-local query << 32 | entity).  PASS 0 counts, PASS 1 fills.
+template <int PASS>
+__global__ __launch_bounds__(kBlock) void k_route_pairs(int64_t n, const uint32_t *pq, const uint32_t *pe,
+                                                        const uint32_t *home, const uint32_t *qid,
+                                                        unsigned long long *tot, const int64_t *base_d,
+                                                        unsigned long long *cursor, uint64_t *out)
+{
+    const int64_t i = tid64();
+    const int lane = threadIdx.x & 63;
+    const bool live = i < n;
+    int d = -1;
+    uint32_t q = 0;
+    if (live) {
+        q = pq[i];
+        d = (int)home[q];
+    }
+    unsigned long long wm = wave_or(live ? 1ull << d : 0ull);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    while (wm) {
+        const int t = __builtin_ctzll(wm);
+        wm &= wm - 1;
+        const bool has = d == t;
+        const unsigned long long bal = __ballot(has);
+        const unsigned long long cnt = (unsigned long long)__popcll(bal);
+        unsigned long long b = 0;
+        if (lane == 0) b = atomicAdd(PASS == 0 ? &tot[t] : &cursor[t], cnt);
+        b = __shfl(b, 0);  // all lanes, before any divergence
+        if (PASS == 0 || !has) continue;
+        out[base_d[t] + (int64_t)b + __popcll(bal & below)] = ((uint64_t)qid[q] << 32) | pe[i];
+    }
+}
+
+}  // namespace
+
+void RouteEngine::plan(int64_t nq, const int64_t *offs, const uint64_t *cells, int np, const uint64_t *part_hi,
+                       hipStream_t s, int64_t *row_counts, int64_t *cell_counts)
+{
+    if (np < 1 || np > kMaxParts) throw Error(DSSG_ERR_INVALID, "route: nparts must be in [1, 64]");
+    if (nq >= (1ll << 24)) throw Error(DSSG_ERR_INVALID, "route: more than 2^24 queries per batch");
+    unsigned long long *mask = mask_.ensure(nq + 1);
+    unsigned long long *acc = acc_.ensure(3 * kMaxParts);  // totals rows | totals cells | cursors
+    DSS_HIP(hipMemsetAsync(acc, 0, 3 * kMaxParts * sizeof(unsigned long long), s));
+    if (nq > 0)
+        hipLaunchKernelGGL(k_route<0>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, offs, cells, nullptr, nullptr,
+                           nullptr, nullptr, np, part_hi, mask, acc, acc + kMaxParts, nullptr, nullptr, nullptr, nullptr,
+                           nullptr);
+    unsigned long long h[2 * kMaxParts];
+    DSS_HIP(hipMemcpyAsync(h, acc, sizeof(h), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    int64_t rb[kMaxParts], cb[kMaxParts], R = 0, Cn = 0;
+    for (int d = 0; d < np; d++) {
+        rb[d] = R;
+        cb[d] = Cn;
+        row_counts[d] = (int64_t)h[d];
+        cell_counts[d] = (int64_t)h[kMaxParts + d];
+        R += row_counts[d];
+        Cn += cell_counts[d];
+    }
+    if (Cn >= (int64_t)kCellMask) throw Error(DSSG_ERR_INVALID, "route: more than 2^40 routed cells");
+    int64_t *bases = base_.ensure(2 * kMaxParts);
+    DSS_HIP(hipMemcpyAsync(bases, rb, sizeof(int64_t) * np, hipMemcpyHostToDevice, s));
+    DSS_HIP(hipMemcpyAsync(bases + kMaxParts, cb, sizeof(int64_t) * np, hipMemcpyHostToDevice, s));
+    DSS_HIP(hipStreamSynchronize(s));  // rb/cb are stack arrays
+    plan_nq_ = nq;
+    plan_np_ = np;
+    plan_offs_ = offs;
+    plan_cells_ = cells;
+    plan_part_hi_ = part_hi;
+}
+
+void RouteEngine::fill(int64_t nq, const int64_t *offs, const uint64_t *cells, const float *alo, const float *ahi,
+                       const int64_t *tlo, const int64_t *thi, hipStream_t s, void *rows, uint64_t *out_cells)
+{
+    if (plan_np_ == 0 || nq != plan_nq_ || offs != plan_offs_ || cells != plan_cells_)
+        throw Error(DSSG_ERR_INVALID, "route fill: no matching dssg_route_plan_device on this context");
+    unsigned long long *acc = acc_.p;
+    if (nq > 0)
+        hipLaunchKernelGGL(k_route<1>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, offs, cells, alo, ahi, tlo, thi,
+                           plan_np_, plan_part_hi_, mask_.p, nullptr, nullptr, base_.p, base_.p + kMaxParts,
+                           acc + 2 * kMaxParts, (QRow *)rows, out_cells);
+    plan_np_ = 0;  // one fill per plan (the cursors are spent)
+}
+
+void RouteEngine::unpack(int64_t nrows, const void *rows, const uint64_t *cells, int np, const int64_t *src_rows,
+                         hipStream_t s, dssg_batch *out)
+{
+    if (np < 1 || np > kMaxParts) throw Error(DSSG_ERR_INVALID, "unpack: nparts must be in [1, 64]");
+    int64_t sb[kMaxParts], acc = 0;
+    for (int d = 0; d < np; d++) {
+        sb[d] = acc;
+        acc += src_rows[d];
+    }
+    if (acc != nrows) throw Error(DSSG_ERR_INVALID, "unpack: per-source row counts do not sum to nrows");
+    int64_t *d_sb = sbase_.ensure(kMaxParts);
+    DSS_HIP(hipMemcpyAsync(d_sb, sb, sizeof(int64_t) * np, hipMemcpyHostToDevice, s));
+    DSS_HIP(hipStreamSynchronize(s));  // sb is a stack array
+    int64_t *nc = ncell_.ensure(nrows + 1);
+    float *alo = alo_.ensure(nrows + 1), *ahi = ahi_.ensure(nrows + 1);
+    int64_t *tlo = tlo_.ensure(nrows + 1), *thi = thi_.ensure(nrows + 1);
+    uint32_t *home = home_.ensure(nrows + 1), *qid = qid_.ensure(nrows + 1);
+    int64_t *offs = offs_.ensure(nrows + 2);
+    if (nrows > 0)
+        hipLaunchKernelGGL(k_unpack_rows, dim3(grid_for(nrows, kBlock)), dim3(kBlock), 0, s, nrows, (const QRow *)rows, np,
+                           d_sb, nc, alo, ahi, tlo, thi, home, qid);
+    exclusive_scan_i64(nc, offs, nrows, tmp_, s);
+    out->n = nrows;
+    out->offs = offs;
+    out->cells = cells;
+    out->alt_lo = alo;
+    out->alt_hi = ahi;
+    out->tlo = tlo;
+    out->thi = thi;
+    out->home = home;
+    out->qid = qid;
+}
+
+void RouteEngine::pairs_plan(const dssg_batch *b, const dssg_pairs *p, int np, hipStream_t s, int64_t *counts)
+{
+    if (np < 1 || np > kMaxParts) throw Error(DSSG_ERR_INVALID, "route_pairs: nparts must be in [1, 64]");
+    unsigned long long *acc = pacc_.ensure(2 * kMaxParts);
+    DSS_HIP(hipMemsetAsync(acc, 0, 2 * kMaxParts * sizeof(unsigned long long), s));
+    const int64_t n = p->n;
+    if (n > 0)
+        hipLaunchKernelGGL(k_route_pairs<0>, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, p->q, p->e, b->home, b->qid,
+                           acc, nullptr, nullptr, nullptr);
+    unsigned long long h[kMaxParts];
+    DSS_HIP(hipMemcpyAsync(h, acc, sizeof(h), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    int64_t pb[kMaxParts], tot = 0;
+    for (int d = 0; d < np; d++) {
+        pb[d] = tot;
+        counts[d] = (int64_t)h[d];
+        tot += counts[d];
+    }
+    int64_t *d_pb = pbase_.ensure(kMaxParts);
+    DSS_HIP(hipMemcpyAsync(d_pb, pb, sizeof(int64_t) * np, hipMemcpyHostToDevice, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    pplan_n_ = n;
+    pplan_np_ = np;
+    pplan_q_ = p->q;
+}
+
+void RouteEngine::pairs_fill(const dssg_batch *b, const dssg_pairs *p, hipStream_t s, uint64_t *out)
+{
+    if (pplan_np_ == 0 || p->n != pplan_n_ || p->q != pplan_q_)
+        throw Error(DSSG_ERR_INVALID, "route_pairs fill: no matching dssg_route_pairs_plan_device on this context");
+    if (p->n > 0)
+        hipLaunchKernelGGL(k_route_pairs<1>, dim3(grid_for(p->n, kBlock)), dim3(kBlock), 0, s, p->n, p->q, p->e, b->home,
+                           b->qid, nullptr, pbase_.p, pacc_.p + kMaxParts, out);
+    pplan_np_ = 0;
+}
+
+}  // namespace dss

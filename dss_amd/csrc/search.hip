@@ -32,14 +32,13 @@
 #include <algorithm>
 #include <vector>
 
+#include "index_view.cuh"
 #include "search.hpp"
 
 namespace dss {
 namespace {
 
 constexpr unsigned kBlock = 256;
-constexpr uint32_t kFirstBit = 0x80000000u;
-constexpr uint64_t kLsb13 = 1ull << 34;
 constexpr int kLongBucket = 63;
 constexpr int kLongSpan = 8;     // entities touching more buckets go to kLongBucket
 constexpr int kMaxBuckets = 61;  // regular buckets 0..nb-1
@@ -50,115 +49,6 @@ constexpr int kGrab = 4;         // join units a persistent wave takes per queue
 constexpr int kJoinBlocksPerCU = 5;  // LDS: 32 KiB per workgroup
 constexpr uint32_t kRank0 = 0x80000000u;    // record: the cell is the query's first cell
 constexpr uint32_t kCompact = 0x40000000u;  // record: the query's prefix is compact
-
-__device__ __forceinline__ int64_t tid64() { return (int64_t)blockIdx.x * blockDim.x + threadIdx.x; }
-__host__ __device__ __forceinline__ bool is_regular(uint64_t c)
-{
-    return (c & ((kLsb13 << 1) - 1)) == kLsb13 && (c >> 61) < 6;  // level 13, valid face
-}
-__host__ __device__ __forceinline__ unsigned long long order_key(long long t)
-{
-    return (unsigned long long)t ^ 0x8000000000000000ull;  // signed order as unsigned
-}
-
-struct Buckets {
-    long long tbase;
-    int shift;
-    int nb;
-};
-// Monotone in t, so B(max(a, b)) = max(B(a), B(b)).
-__device__ __forceinline__ int bucket_of(long long t, const Buckets &bk)
-{
-    if (t <= bk.tbase) return 0;
-    unsigned long long d = ((unsigned long long)t - (unsigned long long)bk.tbase) >> bk.shift;
-    return d >= (unsigned long long)bk.nb ? bk.nb - 1 : (int)d;
-}
-
-// Device view of a dssg_index.
-struct IndexView {
-    uint64_t kmin;
-    int64_t n_dense;
-    const uint32_t *dense;
-    int64_t n_irr;
-    const uint64_t *irr_cells;
-    const uint32_t *irr_start;
-    const uint32_t *p_e;
-    const int64_t *e_offs;
-    const uint64_t *e_cells;
-    const unsigned long long *s_mask;
-    const uint32_t *s_base;
-    const uint32_t *bk_start;
-    const uint32_t *b_e;
-    const float2 *b_alt;
-    const longlong2 *b_t;
-    const uint8_t *b_meta;
-    const ulonglong2 *b_sig;
-    const int32_t *b_owner;
-    Buckets bk;
-};
-
-IndexView view_of(const dssg_index *idx)
-{
-    IndexView v{};
-    v.kmin = idx->kmin;
-    v.n_dense = idx->n_dense;
-    v.dense = idx->dense.p;
-    v.n_irr = idx->n_irr;
-    v.irr_cells = idx->irr_cells.p;
-    v.irr_start = idx->irr_start.p;
-    v.p_e = idx->p_e.p;
-    v.e_offs = idx->e_offs.p;
-    v.e_cells = idx->e_cells.p;
-    v.s_mask = idx->s_mask.p;
-    v.s_base = idx->s_base.p;
-    v.bk_start = idx->bk_start.p;
-    v.b_e = idx->b_e.p;
-    v.b_alt = idx->b_alt.p;
-    v.b_t = idx->b_t.p;
-    v.b_meta = idx->b_meta.p;
-    v.b_sig = idx->b_sig.p;
-    v.b_owner = idx->has_owner ? idx->b_owner.p : nullptr;
-    v.bk = Buckets{idx->tbase, idx->shift, idx->nb};
-    return v;
-}
-
-// Slot of cell c, or false if c is in neither table.
-__device__ __forceinline__ bool find_slot(const IndexView &a, uint64_t c, uint32_t &slot)
-{
-    if (is_regular(c)) {
-        uint64_t k = c >> 35;
-        if (k < a.kmin || (int64_t)(k - a.kmin) >= a.n_dense) return false;
-        slot = (uint32_t)(k - a.kmin);
-        return true;
-    }
-    int64_t lo = 0, hi = a.n_irr;
-    while (lo < hi) {
-        int64_t mid = (lo + hi) >> 1;
-        if (a.irr_cells[mid] < c) lo = mid + 1;
-        else hi = mid;
-    }
-    if (lo < a.n_irr && a.irr_cells[lo] == c) {
-        slot = (uint32_t)(a.n_dense + lo);
-        return true;
-    }
-    return false;
-}
-__device__ __forceinline__ uint64_t cell_of_slot(const IndexView &a, uint32_t slot)
-{
-    if ((int64_t)slot < a.n_dense) return ((a.kmin + slot) << 35) | kLsb13;
-    return a.irr_cells[slot - (uint32_t)a.n_dense];
-}
-__device__ __forceinline__ void plain_range(const IndexView &a, uint32_t slot, uint32_t &s, uint32_t &e)
-{
-    if ((int64_t)slot < a.n_dense) {
-        s = a.dense[slot];
-        e = a.dense[slot + 1];
-    } else {
-        uint32_t k = slot - (uint32_t)a.n_dense;
-        s = a.irr_start[k];
-        e = a.irr_start[k + 1];
-    }
-}
 
 // ---- level-13 decode + prefix signatures -----------------------------------
 __device__ __forceinline__ int s2pos_to_ij(int o, int pos) { return (int)((0x874B78B4u >> (8 * o + 2 * pos)) & 3u); }
@@ -268,17 +158,24 @@ __global__ void k_scatter_unique(int64_t P, const uint64_t *key, const uint32_t 
 
 __global__ void k_scatter_part(int64_t P, const uint64_t *key, const uint32_t *val, const int64_t *reg,
                                const int64_t *rpos, const int64_t *irr, const int64_t *ipos, int64_t n_reg,
-                               uint64_t *p_cell, uint32_t *p_e)
+                               uint64_t *p_cell, uint32_t *p_e, uint32_t *p_mult)
 {
     int64_t i = tid64();
-    if (i >= P) return;
-    if (reg[i]) {
-        p_cell[rpos[i]] = key[i];
-        p_e[rpos[i]] = val[i];
-    } else if (irr[i]) {
-        p_cell[n_reg + ipos[i]] = key[i];
-        p_e[n_reg + ipos[i]] = val[i];
-    }
+    if (i >= P || !(reg[i] || irr[i])) return;
+    uint32_t m = 1;  // run length of this (cell, entity) in the sorted input
+    while (i + m < P && key[i + m] == key[i] && val[i + m] == val[i]) m++;
+    const int64_t w = reg[i] ? rpos[i] : n_reg + ipos[i];
+    p_cell[w] = key[i];
+    p_e[w] = val[i];
+    p_mult[w] = m;
+}
+
+__global__ void k_owner_keys(int64_t n, const int32_t *owner, uint32_t *key, uint32_t *val)
+{
+    int64_t e = tid64();
+    if (e >= n) return;
+    key[e] = (uint32_t)owner[e] ^ 0x80000000u;  // signed order as unsigned
+    val[e] = (uint32_t)e;
 }
 
 __global__ void k_count_by_entity(int64_t P, const uint32_t *e, unsigned long long *cnt)
@@ -974,14 +871,18 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     DSS_HIP(hipMemcpyAsync(&counts[1], rpos + P, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipMemcpyAsync(&counts[2], ipos + P, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
+    // Pu: unique (cell, entity) postings (entity cell lists, always whole);
+    // Pin: those in this index's cell range (the postings it serves)
     const int64_t Pu = counts[0], n_reg = counts[1], n_irr_p = counts[2];
-    idx->n_p = Pu;
+    const int64_t Pin = n_reg + n_irr_p;
+    idx->n_p = Pin;
     idx->n_reg = n_reg;
-    uint64_t *p_cell = idx->p_cell.ensure(Pu + 1);
-    uint32_t *p_e = idx->p_e.ensure(Pu + 1);
+    uint64_t *p_cell = idx->p_cell.ensure(Pin + 1);
+    uint32_t *p_e = idx->p_e.ensure(Pin + 1);
+    uint32_t *p_mult = idx->p_mult.ensure(Pin + 1);
     if (P)
         hipLaunchKernelGGL(k_scatter_part, dim3(grid_for(P, kBlock)), dim3(kBlock), 0, s, P, kb, vb, reg, rpos, irr, ipos,
-                           n_reg, p_cell, p_e);
+                           n_reg, p_cell, p_e, p_mult);
     // (2) entity -> sorted unique cell lists: unique postings in cell order,
     // then a stable sort by entity
     if (P)
@@ -997,8 +898,8 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     int64_t *e_offs = idx->e_offs.ensure(n + 1);
     exclusive_scan_i64(ec64, e_offs, n, tmp_, s);
     unsigned long long *ncell = ec + n + 1;  // scratch counter (zeroed above)
-    if (Pu)
-        hipLaunchKernelGGL(k_first_flags, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, p_cell, p_e, e_offs, e_cells,
+    if (Pin)
+        hipLaunchKernelGGL(k_first_flags, dim3(grid_for(Pin, kBlock)), dim3(kBlock), 0, s, Pin, p_cell, p_e, e_offs, e_cells,
                            ncell);
     {
         unsigned long long h = 0;
@@ -1045,7 +946,7 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
         uint32_t *irr_start = idx->irr_start.ensure(nu + 1);
         hipLaunchKernelGGL(k_irr_scatter, dim3(grid_for(n_irr_p, kBlock)), dim3(kBlock), 0, s, n_irr_p, p_cell + n_reg, f, fpo,
                            n_reg, ic, irr_start);
-        uint32_t endv = (uint32_t)Pu;
+        uint32_t endv = (uint32_t)Pin;
         DSS_HIP(hipMemcpyAsync(irr_start + nu, &endv, sizeof(uint32_t), hipMemcpyHostToDevice, s));
         DSS_HIP(hipStreamSynchronize(s));
     } else {
@@ -1082,20 +983,20 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     // (6) bucketed postings
     const IndexView pv = view_of(idx);
     DevBuf<uint32_t> ps_buf;
-    uint32_t *pslot = ps_buf.ensure(Pu + 1);
-    if (Pu) hipLaunchKernelGGL(k_plain_slot, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, p_cell, pv, pslot);
-    int64_t *bcnt = c0_.ensure(Pu + 1), *boff = c1_.ensure(Pu + 2);
-    if (Pu)
-        hipLaunchKernelGGL(k_bucket_copies<0>, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, p_e, pslot, t0, t1, bk,
+    uint32_t *pslot = ps_buf.ensure(Pin + 1);
+    if (Pin) hipLaunchKernelGGL(k_plain_slot, dim3(grid_for(Pin, kBlock)), dim3(kBlock), 0, s, Pin, p_cell, pv, pslot);
+    int64_t *bcnt = c0_.ensure(Pin + 1), *boff = c1_.ensure(Pin + 2);
+    if (Pin)
+        hipLaunchKernelGGL(k_bucket_copies<0>, dim3(grid_for(Pin, kBlock)), dim3(kBlock), 0, s, Pin, p_e, pslot, t0, t1, bk,
                            bcnt, nullptr, nullptr, nullptr);
-    exclusive_scan_i64(bcnt, boff, Pu, tmp_, s);
-    const int64_t NB = fetch_i64(boff + Pu, s);
+    exclusive_scan_i64(bcnt, boff, Pin, tmp_, s);
+    const int64_t NB = fetch_i64(boff + Pin, s);
     if (NB >= (int64_t)0x7fffffff) throw Error(DSSG_ERR_INVALID, "index: more than 2^31 bucketed postings per device");
     idx->n_b = NB;
     uint64_t *bk0 = k0_.ensure(NB + 1), *bk1 = k1_.ensure(NB + 1);
     uint32_t *bv0 = v0_.ensure(NB + 1), *bv1 = v1_.ensure(NB + 1);
-    if (Pu)
-        hipLaunchKernelGGL(k_bucket_copies<1>, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, p_e, pslot, t0, t1, bk,
+    if (Pin)
+        hipLaunchKernelGGL(k_bucket_copies<1>, dim3(grid_for(Pin, kBlock)), dim3(kBlock), 0, s, Pin, p_e, pslot, t0, t1, bk,
                            nullptr, boff, bk0, bv0);
     sort_pairs(bk0, bk1, bv0, bv1, NB, bits_for(n_slots) + 6, tmp_, s);
     uint32_t *b_e = idx->b_e.ensure(NB + 1);
@@ -1157,6 +1058,20 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
         hipLaunchKernelGGL(k_i64_to_u32, dim3(grid_for(n_slots + 1, kBlock)), dim3(kBlock), 0, s, n_slots + 1, poff, s_base);
         DSS_HIP(hipStreamSynchronize(s));
     }
+    // (8) entity-level attributes: ends_at, owner, owner -> entities, counters
+    int64_t *et1 = idx->e_t1.ensure(n + 1);
+    if (n) DSS_HIP(hipMemcpyAsync(et1, t1, sizeof(int64_t) * n, hipMemcpyDeviceToDevice, s));
+    int64_t *notify = idx->e_notify.ensure(n + 1);
+    DSS_HIP(hipMemsetAsync(notify, 0, sizeof(int64_t) * (n + 1), s));
+    if (owner) {
+        int32_t *eo = idx->e_owner.ensure(n + 1);
+        if (n) DSS_HIP(hipMemcpyAsync(eo, owner, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
+        uint32_t *k0 = v0_.ensure(n + 1), *v0 = v1_.ensure(n + 1);
+        uint32_t *ok = idx->o_key.ensure(n + 1), *oe = idx->o_ent.ensure(n + 1);
+        if (n) hipLaunchKernelGGL(k_owner_keys, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, owner, k0, v0);
+        sort_pairs(k0, ok, v0, oe, n, 32, tmp_, s);
+    }
+    DSS_HIP(hipStreamSynchronize(s));
 }
 
 // ================================================================== search

@@ -15,6 +15,8 @@ struct dssg_index {
     // in the irregular side table.
     dss::DevBuf<uint64_t> p_cell;
     dss::DevBuf<uint32_t> p_e;  // bit 31: the cell is the entity's smallest cell
+    dss::DevBuf<uint32_t> p_mult;  // times (cell, entity) occurs in the stored cell array (RID
+                                   // `unnest(cells)` counts repeats, subscriptions.go:94-101)
     uint64_t kmin = 0;          // dense slot k <-> cell (kmin + k) << 35 | 1 << 34
     int64_t n_dense = 0;
     dss::DevBuf<uint32_t> dense;  // n_dense + 1 plain posting offsets
@@ -45,6 +47,12 @@ struct dssg_index {
     dss::DevBuf<uint8_t> b_meta;             // entity's first bucket | compact << 7
     dss::DevBuf<ulonglong2> b_sig;           // 2 per posting: 256-bit prefix signature
     dss::DevBuf<int32_t> b_owner;
+    // ---- entity-level attributes (subscription-store queries, subs.hip) ------
+    dss::DevBuf<int64_t> e_t1;     // ends_at (us)
+    dss::DevBuf<int32_t> e_owner;  // owner id (has_owner)
+    dss::DevBuf<uint32_t> o_key;   // owner ^ 0x80000000, ascending (owner -> entities)
+    dss::DevBuf<uint32_t> o_ent;   // entity ids in o_key order
+    dss::DevBuf<int64_t> e_notify; // notification_index counters
     int device = 0;
 };
 

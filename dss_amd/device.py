@@ -55,13 +55,16 @@ def cover(ctx: _lib.Context, fp: DeviceFootprints) -> _lib.Cells:
     return out
 
 
-def build_index(ctx: _lib.Context, cells: _lib.Cells, alt_lo, alt_hi, t0, t1, owner=None) -> C.c_void_p:
-    """dssg_index_build_device from a device covering (entities = footprints)."""
+def build_index(ctx: _lib.Context, cells: _lib.Cells, alt_lo, alt_hi, t0, t1, owner=None,
+                cell_range=None) -> C.c_void_p:
+    """dssg_index_build_device from a device covering (entities = footprints);
+    cell_range=(lo, hi): a cell-range shard (dssg_index_build_range_device)."""
     h = C.c_void_p()
-    ctx.check(ctx.L.dssg_index_build_device(ctx.h, cells.n, C.c_void_p(cells.offs), C.c_void_p(cells.cells),
-                                            _ptr(alt_lo), _ptr(alt_hi), _ptr(t0), _ptr(t1),
-                                            _ptr(owner) if owner is not None else C.c_void_p(0), _stream_ptr(),
-                                            C.byref(h)))
+    lo, hi = cell_range if cell_range is not None else (0, 2**64 - 1)
+    ctx.check(ctx.L.dssg_index_build_range_device(ctx.h, cells.n, C.c_void_p(cells.offs), C.c_void_p(cells.cells),
+                                                  _ptr(alt_lo), _ptr(alt_hi), _ptr(t0), _ptr(t1),
+                                                  _ptr(owner) if owner is not None else C.c_void_p(0), int(lo),
+                                                  int(hi), _stream_ptr(), C.byref(h)))
     return h
 
 

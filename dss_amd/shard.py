@@ -10,21 +10,27 @@ explicit one-process-per-GPU layout:
     a skewed airspace still balances by postings, not by id span);
   * rank r builds `dssg_index_build_range` over its range: postings only for
     its cells, every entity's cell list whole;
-  * each rank covers its slice of the query batch and `allgather_csr` gives
-    every rank the whole covered batch (RCCL all-gather over xGMI; gloo on
-    CPU in the tests);
-  * each rank joins the whole batch against its shard.  Because the
-    smallest-shared-cell rule sees whole cell lists, every (query, entity)
-    pair is emitted by exactly one rank -- no cross-shard dedupe;
-  * `gather_pairs` collects the pair sets (all-gather of counts, then of the
-    padded buffers).
+  * `ShardedSearch` (the device path, one process per GPU): each rank covers
+    its own query batch; `dssg_route_plan/fill_device` packs, per query, one
+    row + its whole cell list for every shard owning one of its cells; an
+    all-to-all (RCCL over xGMI) delivers them; the shard unpacks them
+    (`dssg_unpack_queries_device`) and joins them against its cell-range
+    index with the single-GPU join kernel; `dssg_route_pairs_*` sends every
+    pair back to its query's home rank (second all-to-all).  Because the
+    smallest-shared-cell rule sees whole cell lists on both sides, every
+    (query, entity) pair is emitted by exactly one shard -- no cross-shard
+    dedupe.  xGMI is point-to-point, so the exchange is a direct all-to-all
+    (one peer per link), never a ring of the whole batch.
+  * `allgather_csr` / `gather_pairs`: the simpler broadcast-style exchange
+    (every rank sees the whole batch), kept for the CPU protocol test.
 
-Only the exchange steps are collectives; the join itself is the same HIP
-kernel as the single-GPU path.  torch.distributed is plumbing: the process
-group and the collectives; the tensors it moves are the C ABI's buffers.
+Only the exchange steps are collectives; every byte they move is packed and
+unpacked by HIP kernels behind the C ABI.  torch.distributed is plumbing: the
+process group and the collectives over caller-owned device tensors.
 """
 from __future__ import annotations
 
+import ctypes as C
 from typing import List, Sequence, Tuple
 
 import numpy as np
@@ -127,3 +133,123 @@ def gather_pairs(q, e, group=None):
     dist.all_gather(outs, pk, group=group)
     allp = torch.cat([outs[r][: ns[r]] for r in range(world)])
     return allp >> 32, allp & 0xFFFFFFFF
+
+
+# ------------------------------------------------------- device sharded path
+def part_his(ranges: Sequence[Tuple[int, int]]) -> np.ndarray:
+    """Inclusive upper bounds of the parts (dssg_route_plan_device's
+    part_hi), uint64, the last one UINT64_MAX."""
+    his = np.array([hi for _, hi in ranges], dtype=np.uint64)
+    if len(his) == 0 or int(his[-1]) != U64_MAX:
+        raise ValueError("ranges must end at UINT64_MAX")
+    return his
+
+
+def all_to_all(send, send_counts: Sequence[int], group=None, stage_host: bool = False):
+    """All-to-all of a part-major 1-D tensor (send_counts[d] elements for rank
+    d).  Returns (received tensor, source-major; per-source counts).  Counts
+    travel first (one all-to-all of world int64s).  stage_host: bounce
+    through host memory (gloo)."""
+    import torch
+    dist = _dist()
+    dev = send.device
+    cdev = "cpu" if stage_host else dev
+    sc = torch.tensor(list(send_counts), dtype=torch.int64, device=cdev)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = [int(x) for x in rc.tolist()]
+    src = send.cpu() if stage_host else send
+    out = torch.empty(sum(recv_counts), dtype=send.dtype, device=cdev)
+    dist.all_to_all_single(out, src, recv_counts, [int(x) for x in send_counts], group=group)
+    return (out.to(dev) if stage_host else out), recv_counts
+
+
+class ShardedSearch:
+    """One rank of the cell-range sharded 4D search.
+
+    `index` is this rank's dssg_index_build_range[_device] shard over
+    `ranges[rank]`; `step` takes this rank's covered query batch (device CSR
+    + attributes, tlo already max(start, now)) and returns, on the same rank,
+    the (query, entity) pairs of its own queries as one int64 tensor packed
+    (query << 32 | entity) -- exactly the pair set a single-GPU search of the
+    batch against the whole index returns."""
+
+    def __init__(self, ctx, index, ranges, group=None, stage_host: bool = False):
+        import torch
+        from . import device as D
+        dist = _dist()
+        self.ctx, self.index, self.group = ctx, index, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if len(ranges) != self.world:
+            raise ValueError("one cell range per rank")
+        self.stage_host = stage_host
+        self.dev = torch.device("cuda", torch.cuda.current_device())
+        self.part_hi = torch.as_tensor(part_his(ranges).view(np.int64), device=self.dev)
+        self._D = D
+        self.times = {}
+
+    def _mark(self, name, t0, sync):
+        import time
+        import torch
+        if sync:
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            self.times[name] = self.times.get(name, 0.0) + (t - t0)
+            return t
+        return t0
+
+    def step(self, offs_ptr, cells_ptr, nq, alo, ahi, tlo, thi, timed: bool = False):
+        import time
+        import torch
+        from . import _lib
+        D, ctx, L = self._D, self.ctx, self.ctx.L
+        W = self.world
+        st = D._stream_ptr()
+        t = time.perf_counter()
+        if timed:
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+        # (1) route this rank's queries to the shards owning their cells
+        rc = (C.c_int64 * _lib.MAX_PARTS)()
+        cc = (C.c_int64 * _lib.MAX_PARTS)()
+        ctx.check(L.dssg_route_plan_device(ctx.h, nq, C.c_void_p(offs_ptr), C.c_void_p(cells_ptr), W,
+                                           D._ptr(self.part_hi), st, rc, cc))
+        rows_n, cells_n = [rc[d] for d in range(W)], [cc[d] for d in range(W)]
+        words = _lib.ROUTE_ROW_BYTES // 8
+        send_rows = torch.empty(sum(rows_n) * words + 1, dtype=torch.int64, device=self.dev)
+        send_cells = torch.empty(sum(cells_n) + 1, dtype=torch.int64, device=self.dev)
+        ctx.check(L.dssg_route_fill_device(ctx.h, nq, C.c_void_p(offs_ptr), C.c_void_p(cells_ptr), D._ptr(alo),
+                                           D._ptr(ahi), D._ptr(tlo), D._ptr(thi), st, D._ptr(send_rows),
+                                           D._ptr(send_cells)))
+        t = self._mark("route", t, timed)
+        # (2) exchange (all-to-all over xGMI)
+        recv_rows, src_words = all_to_all(send_rows[:-1], [r * words for r in rows_n], self.group, self.stage_host)
+        recv_cells, _ = all_to_all(send_cells[:-1], cells_n, self.group, self.stage_host)
+        t = self._mark("exchange_queries", t, timed)
+        # (3) unpack + join against this rank's shard
+        src_rows = (C.c_int64 * _lib.MAX_PARTS)(*[w // words for w in src_words])
+        nrows = sum(src_words) // words
+        batch = _lib.Batch()
+        recv_rows = recv_rows if recv_rows.numel() else torch.empty(1, dtype=torch.int64, device=self.dev)
+        recv_cells = recv_cells if recv_cells.numel() else torch.empty(1, dtype=torch.int64, device=self.dev)
+        ctx.check(L.dssg_unpack_queries_device(ctx.h, nrows, D._ptr(recv_rows), C.c_void_p(recv_cells.data_ptr()), W,
+                                               src_rows, st, C.byref(batch)))
+        pairs = _lib.Pairs()
+        ctx.check(L.dssg_search_device(ctx.h, self.index, batch.n, C.c_void_p(batch.offs), C.c_void_p(batch.cells),
+                                       C.c_void_p(batch.alt_lo), C.c_void_p(batch.alt_hi), C.c_void_p(batch.tlo),
+                                       C.c_void_p(batch.thi), C.c_void_p(0), st, C.byref(pairs)))
+        t = self._mark("join", t, timed)
+        # (4) pairs back to their queries' home ranks
+        pc = (C.c_int64 * _lib.MAX_PARTS)()
+        ctx.check(L.dssg_route_pairs_plan_device(ctx.h, C.byref(batch), C.byref(pairs), W, st, pc))
+        pn = [pc[d] for d in range(W)]
+        send_pairs = torch.empty(sum(pn) + 1, dtype=torch.int64, device=self.dev)
+        ctx.check(L.dssg_route_pairs_fill_device(ctx.h, C.byref(batch), C.byref(pairs), st, D._ptr(send_pairs)))
+        t = self._mark("route_pairs", t, timed)
+        out, _ = all_to_all(send_pairs[:-1], pn, self.group, self.stage_host)
+        self._mark("exchange_pairs", t, timed)
+        self.last_rows = nrows
+        self.last_recv_cells = recv_cells[: int(batch.n and recv_cells.numel())] if nrows else recv_cells[:0]
+        self.last_shard_pairs = int(pairs.n)
+        return out

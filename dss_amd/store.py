@@ -9,6 +9,10 @@
       impl pkg/rid/cockroach/subscriptions.go:222-273
   scdstore.SubscriptionStore.SearchSubscriptions pkg/scd/store/store.go:35
       impl pkg/scd/store/cockroach/subscriptions.go:498-545 (Q7: cells ignored)
+  repos.Subscription.UpdateNotificationIdxsInCells / MaxSubscriptionCountInCellsByOwner
+      impl pkg/rid/cockroach/subscriptions.go:83-116, 204-219
+  SCD fetchSubscriptionsForNotification / fetchMaxSubscriptionCountByCellAndOwner
+      pkg/scd/store/cockroach/subscriptions.go:128-173, 255-283
 
 Stored entities live in a GPU-resident `EntityIndex` (dssg_index).  Entity
 ids are dense 0..n-1 indices that the caller maps to its rows (UUIDs).
@@ -163,6 +167,56 @@ class EntityIndex:
                           _p(ow, C.c_int32) if ow is not None else C.POINTER(C.c_int32)(), int(now_us))
 
 
+    # ------------------------------------------- subscription-store queries
+    def set_notification_index(self, values):
+        v = np.ascontiguousarray(values, dtype=np.int64)
+        if len(v) != self.n:
+            raise ValueError("one notification index per entity")
+        self.ctx.check(self.ctx.L.dssg_index_set_notification_index(self.ctx.h, self.h, _p(v, C.c_int64)))
+
+    def notification_index(self) -> np.ndarray:
+        v = np.zeros(max(self.n, 1), dtype=np.int64)
+        self.ctx.check(self.ctx.L.dssg_index_get_notification_index(self.ctx.h, self.h, _p(v, C.c_int64)))
+        return v[: self.n]
+
+    def notify_batch(self, q_offs, q_cells, now_us):
+        """dssg_notify_subscriptions: (q, e, notification index after the
+        increment), sorted by (e, q); the counters advance."""
+        q_offs = np.ascontiguousarray(q_offs, dtype=np.int64)
+        q_cells = np.ascontiguousarray(q_cells, dtype=np.uint64)
+        nq = len(q_offs) - 1
+        need = C.c_int64(0)
+        cap = max(1024, nq * 8)
+        while True:
+            oq = np.zeros(cap, dtype=np.uint32)
+            oe = np.zeros(cap, dtype=np.uint32)
+            ov = np.zeros(cap, dtype=np.int64)
+            rc = self.ctx.L.dssg_notify_subscriptions(self.ctx.h, self.h, nq, _p(q_offs, C.c_int64),
+                                                      _p(q_cells, C.c_uint64), int(now_us), _p(oq, C.c_uint32),
+                                                      _p(oe, C.c_uint32), _p(ov, C.c_int64), cap, C.byref(need))
+            if rc == _lib.DSSG_ERR_CAPACITY:
+                cap = int(need.value) + 1
+                continue
+            self.ctx.check(rc)
+            n = need.value
+            return oq[:n].copy(), oe[:n].copy(), ov[:n].copy()
+
+    def owner_subscriptions_batch(self, owner, now_us):
+        ow = np.ascontiguousarray(owner, dtype=np.int32)
+        return self._call(self.ctx.L.dssg_owner_subscriptions, len(ow), _p(ow, C.c_int32), int(now_us))
+
+    def max_subscription_count_batch(self, q_offs, q_cells, owner, now_us) -> np.ndarray:
+        q_offs = np.ascontiguousarray(q_offs, dtype=np.int64)
+        q_cells = np.ascontiguousarray(q_cells, dtype=np.uint64)
+        ow = np.ascontiguousarray(owner, dtype=np.int32)
+        nq = len(q_offs) - 1
+        out = np.zeros(max(nq, 1), dtype=np.int64)
+        self.ctx.check(self.ctx.L.dssg_max_subscription_count(self.ctx.h, self.h, nq, _p(q_offs, C.c_int64),
+                                                              _p(q_cells, C.c_uint64), _p(ow, C.c_int32),
+                                                              int(now_us), _p(out, C.c_int64)))
+        return out[:nq]
+
+
 # ------------------------------------------------------------ reference API
 def SearchOperations(index: EntityIndex, v4d: Volume4D, owner=None, now_us: int = 0) -> List[int]:
     """operations.go:374-445 searchOperations; `owner` is ignored (Q6)."""
@@ -217,3 +271,34 @@ def SearchSubscriptionsByOwner(index: EntityIndex, cells: Sequence[int], owner: 
     offs, cc = _csr([cells])
     _, e = index.search_subscriptions_batch(offs, cc, now_us, [owner])
     return [int(x) for x in e]
+
+
+def UpdateNotificationIdxsInCells(index: EntityIndex, cells: Sequence[int], now_us: int) -> List[Tuple[int, int]]:
+    """RID subscriptions.go:204-219: every unexpired subscription sharing a
+    cell gets notification_index + 1; returns (entity, new index) rows."""
+    offs, cc = _csr([cells])
+    _, e, v = index.notify_batch(offs, cc, now_us)
+    return [(int(a), int(b)) for a, b in zip(e, v)]
+
+
+def FetchSubscriptionsForNotification(index: EntityIndex, cells: Sequence[int], now_us: int) -> List[Tuple[int, int]]:
+    """SCD subscriptions.go:128-173 (DISTINCT subscription_id WHERE cell_id =
+    ANY(cells), then the UPDATE ... WHERE ends_at >= now RETURNING): the same
+    fan-out over the SCD cells table."""
+    return UpdateNotificationIdxsInCells(index, cells, now_us)
+
+
+def SCDSearchSubscriptions(index: EntityIndex, cells: Sequence[int], owner: int, now_us: int) -> List[int]:
+    """scdstore.SubscriptionStore.SearchSubscriptions (pkg/scd/store/cockroach/
+    subscriptions.go:497-545): every unexpired subscription of the owner; the
+    cells do not filter (Q7) but an empty covering is still a BadRequest."""
+    if len(cells) == 0:
+        raise BadRequest("no location provided")
+    _, e = index.owner_subscriptions_batch([owner], now_us)
+    return [int(x) for x in e]
+
+
+def MaxSubscriptionCountInCellsByOwner(index: EntityIndex, cells: Sequence[int], owner: int, now_us: int) -> int:
+    """RID subscriptions.go:83-116 / SCD subscriptions.go:255-283."""
+    offs, cc = _csr([cells])
+    return int(index.max_subscription_count_batch(offs, cc, [owner], now_us)[0])

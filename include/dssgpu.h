@@ -180,6 +180,86 @@ int dssg_search_subscriptions(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, 
                               const uint64_t *q_cells, const int32_t *owner, int64_t now_us, uint32_t *out_q,
                               uint32_t *out_e, int64_t cap, int64_t *needed);
 
+/* ---- subscription-store queries -----------------------------------------
+ * Notification fan-out: RID UpdateNotificationIdxsInCells
+ * (pkg/rid/cockroach/subscriptions.go:204-219) and SCD
+ * fetchSubscriptionsForNotification (pkg/scd/store/cockroach/
+ * subscriptions.go:128-173).  For each query q (processed in batch order),
+ * every entity sharing a cell with it and with ends_at >= now has its
+ * notification_index incremented; pair k returns the value after its own
+ * increment (UPDATE ... RETURNING).  Pairs come back sorted by (entity,
+ * query).  On DSSG_ERR_CAPACITY no counter moves.  The counters live in the
+ * index (0 after a build; set/get copy n host int64 values). */
+int dssg_index_set_notification_index(dssg_ctx *ctx, dssg_index *idx, const int64_t *values);
+int dssg_index_get_notification_index(dssg_ctx *ctx, const dssg_index *idx, int64_t *values);
+int dssg_notify_subscriptions(dssg_ctx *ctx, dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
+                              int64_t now_us, uint32_t *out_q, uint32_t *out_e, int64_t *out_index, int64_t cap,
+                              int64_t *needed);
+/* SCD SubscriptionStore.SearchSubscriptions (pkg/scd/store/cockroach/
+ * subscriptions.go:497-545): its LEFT JOIN keeps every row, so the answer is
+ * every entity of owner[q] with ends_at >= now and the cells do not filter
+ * (quirk Q7; the caller still rejects an empty covering with BadRequest("no
+ * location provided")).  Needs an index built with owners.  Pairs sorted by
+ * (query, entity). */
+int dssg_owner_subscriptions(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int32_t *owner, int64_t now_us,
+                             uint32_t *out_q, uint32_t *out_e, int64_t cap, int64_t *needed);
+/* RID MaxSubscriptionCountInCellsByOwner (pkg/rid/cockroach/
+ * subscriptions.go:83-116) and SCD fetchMaxSubscriptionCountByCellAndOwner
+ * (pkg/scd/store/cockroach/subscriptions.go:255-283): out_count[q] = max over
+ * the query's cells c of the number of owner[q]'s entities with
+ * ends_at >= now that hold c (a cell repeated in a stored array counts each
+ * time, as RID's unnest(cells) does), 0 if none (IFNULL).  Query cells may be
+ * unsorted or repeated.  Needs an index built with owners. */
+int dssg_max_subscription_count(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *q_offs,
+                                const uint64_t *q_cells, const int32_t *owner, int64_t now_us, int64_t *out_count);
+
+/* ---- multi-GPU routing (cell-range shards) --------------
+ * The reference range-partitions scd_cells_operations by cell_id inside
+ * CockroachDB (pkg/scd/store/cockroach/store.go:140-147) and the SQL layer
+ * fans `cell_id = ANY($cells)` (operations.go:384-390) out to the ranges.
+ * Here, one process per GPU:
+ *  1. dssg_route_plan_device + dssg_route_fill_device: the home rank's
+ *     covered batch -> part-major send buffers (caller-owned device memory):
+ *     per (query, part owning >= 1 of its cells) one DSSG_ROUTE_ROW_BYTES row
+ *     {i64 tlo, i64 thi, f32 alo, f32 ahi, u32 qid, u32 ncells} and the
+ *     query's whole cell list (a part's cell lists in the order of its rows).
+ *     Part d owns cells c with part_hi[d-1] < c <= part_hi[d] (uint64 order,
+ *     part_hi[nparts-1] = UINT64_MAX; d_part_hi is a device array).  The plan
+ *     returns the per-part row and cell counts (host arrays of nparts).
+ *  2. the caller all-to-alls rows and cells (RCCL over xGMI);
+ *  3. dssg_unpack_queries_device: received rows (source-part-major, src_rows[s]
+ *     rows from part s) -> a query batch for dssg_search_device against the
+ *     part's dssg_index_build_range index (context-owned until the next unpack);
+ *  4. dssg_route_pairs_plan_device + dssg_route_pairs_fill_device: that
+ *     search's pairs -> part-major by home part, packed
+ *     (home-local qid << 32 | entity); the caller all-to-alls them back.
+ * A part sees a query's whole cell list and every entity's whole cell list, so
+ * each (query, entity) pair is emitted by exactly one part (the one owning
+ * their smallest shared cell): no cross-shard dedupe. */
+#define DSSG_MAX_PARTS 64
+#define DSSG_ROUTE_ROW_BYTES 32
+typedef struct {
+    int64_t n;                   /* rows = queries of the batch */
+    const int64_t *offs;         /* device, n+1 */
+    const uint64_t *cells;       /* device (the caller's received cells) */
+    const float *alt_lo, *alt_hi;
+    const int64_t *tlo, *thi;
+    const uint32_t *home;        /* source part of each row */
+    const uint32_t *qid;         /* query index in its home batch */
+} dssg_batch;
+int dssg_route_plan_device(dssg_ctx *ctx, int64_t nq, const int64_t *d_q_offs, const uint64_t *d_q_cells,
+                           int32_t nparts, const uint64_t *d_part_hi, void *stream, int64_t *row_counts,
+                           int64_t *cell_counts);
+int dssg_route_fill_device(dssg_ctx *ctx, int64_t nq, const int64_t *d_q_offs, const uint64_t *d_q_cells,
+                           const float *d_q_alt_lo, const float *d_q_alt_hi, const int64_t *d_q_tlo,
+                           const int64_t *d_q_thi, void *stream, void *d_rows_out, uint64_t *d_cells_out);
+int dssg_unpack_queries_device(dssg_ctx *ctx, int64_t nrows, const void *d_rows, const uint64_t *d_cells,
+                               int32_t nparts, const int64_t *src_rows, void *stream, dssg_batch *out);
+int dssg_route_pairs_plan_device(dssg_ctx *ctx, const dssg_batch *batch, const dssg_pairs *pairs, int32_t nparts,
+                                 void *stream, int64_t *counts);
+int dssg_route_pairs_fill_device(dssg_ctx *ctx, const dssg_batch *batch, const dssg_pairs *pairs, void *stream,
+                                 uint64_t *d_out);
+
 /* ---- diagnostics --------------------------------------------------------
  * Average device time (ms) of the most recent launches of the named kernel
  * phase, measured with HIP events on the launching stream (bench.py). */

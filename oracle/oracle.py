@@ -239,6 +239,61 @@ class Index:
             pass
 
 
+# ------------------------------------------------- subscription-store queries
+# Pure-Python restatements of the SQL (small cases only).
+
+def notify(e_offs, e_cells, e_t1, counters, q_offs, q_cells, now):
+    """RID UpdateNotificationIdxsInCells (pkg/rid/cockroach/subscriptions.go:
+    204-219) / SCD fetchSubscriptionsForNotification (pkg/scd/store/cockroach/
+    subscriptions.go:128-173), one UPDATE per query in batch order:
+    `notification_index += 1 WHERE cells && $q AND ends_at >= now RETURNING`.
+    Returns (q, e, value) sorted by (e, q) and the final counters."""
+    cnt = [int(x) for x in counters]
+    cell_sets = [set(int(c) for c in e_cells[e_offs[e]:e_offs[e + 1]]) for e in range(len(e_offs) - 1)]
+    out = []
+    for q in range(len(q_offs) - 1):
+        qs = set(int(c) for c in q_cells[q_offs[q]:q_offs[q + 1]])
+        for e, cs in enumerate(cell_sets):
+            if int(e_t1[e]) >= now and cs & qs:
+                cnt[e] += 1
+                out.append((e, q, cnt[e]))
+    out.sort()
+    return (np.array([q for _, q, _ in out], np.uint32), np.array([e for e, _, _ in out], np.uint32),
+            np.array([v for _, _, v in out], np.int64), np.array(cnt, np.int64))
+
+
+def owner_subscriptions(e_owner, e_t1, q_owner, now):
+    """SCD SearchSubscriptions (pkg/scd/store/cockroach/subscriptions.go:
+    497-545): LEFT JOIN keeps every row, so `owner = $2 AND ends_at >= $3`
+    alone decides (quirk Q7).  Returns sorted (q, e)."""
+    rq, re = [], []
+    for q, o in enumerate(q_owner):
+        for e in range(len(e_owner)):
+            if int(e_owner[e]) == int(o) and int(e_t1[e]) >= now:
+                rq.append(q)
+                re.append(e)
+    return np.array(rq, np.uint32), np.array(re, np.uint32)
+
+
+def max_subscription_count(e_offs, e_cells, e_owner, e_t1, q_offs, q_cells, q_owner, now):
+    """RID MaxSubscriptionCountInCellsByOwner (pkg/rid/cockroach/
+    subscriptions.go:83-116): unnest(cells) of the owner's unexpired rows,
+    filtered by `cell_id = ANY($3)`, COUNT(*) GROUP BY cell_id, IFNULL(MAX, 0).
+    A stored array's repeats count each time."""
+    out = np.zeros(len(q_offs) - 1, np.int64)
+    for q in range(len(q_offs) - 1):
+        qs = set(int(c) for c in q_cells[q_offs[q]:q_offs[q + 1]])
+        per = {}
+        for e in range(len(e_offs) - 1):
+            if int(e_owner[e]) != int(q_owner[q]) or int(e_t1[e]) < now:
+                continue
+            for c in e_cells[e_offs[e]:e_offs[e + 1]]:
+                if int(c) in qs:
+                    per[int(c)] = per.get(int(c), 0) + 1
+        out[q] = max(per.values()) if per else 0
+    return out
+
+
 def token(cell: int) -> str:
     """s2.CellID.ToToken: hex with trailing zeros stripped."""
     if cell == 0:

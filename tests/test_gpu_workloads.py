@@ -1,0 +1,37 @@
+"""GPU parity on the other BASELINE.json configs, at sizes
+the oracle finishes in seconds: California hotspots (configs[2]), RID
+city-block ISAs with 30 s windows (configs[3], SearchISAs semantics: no
+altitude, identification_service_area.go:170-180) and continent-scale thin
+corridors (configs[4]).  Coverings must be bit-identical and the pair sets
+equal to the oracle's."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _keys(q, e):
+    return np.sort((np.asarray(q, np.uint64) << np.uint64(32)) | np.asarray(e, np.uint64))
+
+
+@pytest.mark.parametrize("cfg,scale", [(2, 0.002), (3, 0.004), (4, 0.0004)])
+def test_config_parity(oracle, cfg, scale):
+    from dss_amd import geo, workload as W
+    from dss_amd.store import EntityIndex
+    _, q, qa, it, ia, now = W.config(cfg, scale=scale)
+    ci = geo.cover_batch(it.kind, it.voff, it.lat, it.lng, it.radius_m)
+    cq = geo.cover_batch(q.kind, q.voff, q.lat, q.lng, q.radius_m)
+    io, ic, ist, _ = oracle.cover_batch(it.kind, it.voff, it.lat, it.lng, it.radius_m)
+    qo, qc, qst, _ = oracle.cover_batch(q.kind, q.voff, q.lat, q.lng, q.radius_m)
+    assert np.array_equal(ci.offs, io) and np.array_equal(ci.cells, ic)
+    assert np.array_equal(cq.offs, qo) and np.array_equal(cq.cells, qc)
+    assert np.array_equal(ci.status, ist) and np.array_equal(cq.status, qst)
+    tlo, thi = W.query_bounds(qa, now)
+    idx = EntityIndex(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1)
+    if cfg == 3:
+        gq, ge = idx.search_isas_batch(cq.offs, cq.cells, tlo, thi)
+    else:
+        gq, ge = idx.search_operations_batch(cq.offs, cq.cells, qa.alt_lo, qa.alt_hi, qa.t0, qa.t1, now)
+    oq, oe = oracle.search(io, ic, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1, None, qo, qc, qa.alt_lo, qa.alt_hi, tlo, thi)
+    assert len(oq) > 0
+    assert np.array_equal(_keys(gq, ge), _keys(oq, oe))

@@ -123,3 +123,52 @@ def test_regular_loop_is_ccw_20gon(oracle):
     for k in range(20):
         a, b = pts[k] - c, pts[(k + 1) % 20] - c
         assert np.dot(np.cross(a, b), c) > 0
+
+
+# ---- subscription-store KATs (pkg/rid/cockroach/subscriptions_test.go,
+# pkg/rid/application/isa_test.go) pinned on the oracle restatements
+POOL_CELL = 12494535935418957824
+OVERFLOW_CELL = 17106221850767130624
+# subscriptionsPool (subscriptions_test.go:19-64): owners myself, myself, me
+POOL_CELLS = [[OVERFLOW_CELL, POOL_CELL], [POOL_CELL], [POOL_CELL]]
+POOL_OWNER = [0, 0, 1]   # "myself" -> 0, "me" -> 1
+
+
+def _pool_csr():
+    import numpy as np
+    offs = np.cumsum([0] + [len(c) for c in POOL_CELLS]).astype(np.int64)
+    cells = np.array([c for cs in POOL_CELLS for c in cs], np.uint64)
+    return offs, cells
+
+
+def test_oracle_max_subscription_count_kat(oracle):
+    # subscriptions_test.go:275-287: MaxSubscriptionCountInCellsByOwner({pool cell}, "myself") == 2
+    import numpy as np
+    offs, cells = _pool_csr()
+    t1 = np.full(3, 10**15, np.int64)
+    got = oracle.max_subscription_count(offs, cells, POOL_OWNER, t1, np.array([0, 1]), np.array([POOL_CELL], np.uint64),
+                                        [0], 0)
+    assert got.tolist() == [2]
+    # repeats inside a stored array count each time (RID unnest(cells))
+    got = oracle.max_subscription_count(np.array([0, 2]), np.array([POOL_CELL, POOL_CELL], np.uint64), [0], [10**15],
+                                        np.array([0, 1]), np.array([POOL_CELL], np.uint64), [0], 0)
+    assert got.tolist() == [2]
+
+
+def test_oracle_notification_fanout_kat(oracle):
+    # isa_test.go:266-324: subscriptions start at 42; inserting an ISA over the
+    # pool cell notifies all three (43), deleting it notifies them again (44)
+    import numpy as np
+    offs, cells = _pool_csr()
+    t1 = np.full(3, 10**15, np.int64)
+    q_offs, q_cells = np.array([0, 1]), np.array([POOL_CELL], np.uint64)
+    _, e, v, cnt = oracle.notify(offs, cells, t1, [42, 42, 42], q_offs, q_cells, 0)
+    assert sorted(e.tolist()) == [0, 1, 2] and v.tolist() == [43, 43, 43]
+    _, e, v, cnt = oracle.notify(offs, cells, t1, cnt, q_offs, q_cells, 0)
+    assert v.tolist() == [44, 44, 44] and cnt.tolist() == [44, 44, 44]
+
+
+def test_oracle_scd_subscription_search_ignores_cells(oracle):
+    # quirk Q7 (pkg/scd/store/cockroach/subscriptions.go:497-545)
+    q, e = oracle.owner_subscriptions([0, 1, 0, 0], [10, 10, 5, 10], [0], 8)
+    assert e.tolist() == [0, 3]
