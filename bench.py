@@ -57,6 +57,8 @@ def main():
     ap.add_argument("--mode", choices=["sharded", "replica"], default=None,
                     help="multi-GPU layout (default: sharded for N > 1, replica for N = 1)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on a multi-GPU node; gloo for rehearsals")
+    ap.add_argument("--pipelines", type=int, default=1,
+                    help="concurrent batch pipelines per GPU (own engine context + stream + host thread each)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank on cuda:0 (one-GPU box, gloo backend)")
     args = ap.parse_args()
@@ -140,13 +142,45 @@ def main():
         step()
     torch.cuda.synchronize()
 
+    # extra pipelines: each its own context (engine scratch), stream and host
+    # thread, so one batch's cover overlaps another's join
+    workers = []
+    if args.pipelines > 1 and sharded is None:
+        import threading
+        for k in range(args.pipelines - 1):
+            wctx = _lib.Context(local)
+            wstream = torch.cuda.Stream(device=dev)
+            workers.append((wctx, wstream))
+
+    def run_steps(wctx, wstream, n):
+        with torch.cuda.stream(wstream):
+            for _ in range(n):
+                c = D.cover(wctx, d_q)
+                D.search(wctx, index, c, q_alo, q_ahi, q_tlo, q_thi)
+            wstream.synchronize()
+
+    for wctx, wstream in workers:  # warm the extra contexts
+        run_steps(wctx, wstream, 1)
+
     # ------------------------------------------------------------ timed steps
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        cells, pairs = step()
+    if workers:
+        share = [args.steps // args.pipelines + (1 if k < args.steps % args.pipelines else 0)
+                 for k in range(args.pipelines)]
+        threads = [threading.Thread(target=run_steps, args=(wctx, wstream, share[k + 1]))
+                   for k, (wctx, wstream) in enumerate(workers)]
+        for th in threads:
+            th.start()
+        for _ in range(share[0]):
+            cells, pairs = step()
+        for th in threads:
+            th.join()
+    else:
+        for _ in range(args.steps):
+            cells, pairs = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
