@@ -214,6 +214,8 @@ def main():
     n_keys, n_units, n_runs, n_iters, n_tests = (C.c_int64() for _ in range(5))
     ctx.check(ctx.L.dssg_search_counters(ctx.h, C.byref(n_keys), C.byref(n_units), C.byref(n_runs), C.byref(n_iters),
                                          C.byref(n_tests)))
+    n_fl, n_mg, n_ml = (C.c_int64() for _ in range(3))
+    ctx.check(ctx.L.dssg_join_events(ctx.h, C.byref(n_fl), C.byref(n_mg), C.byref(n_ml)))
     c_tot = int(cells.total_cells)
     r_tot = int(pairs.n)
     kern_avg_ms = float(np.mean(kern_ms))
@@ -264,7 +266,8 @@ def main():
             "phase_ms": {"cover": cover_avg, "join": join_avg, "join_kernel": kern_avg_ms},
             "pairs_per_step": r_tot,
             "join_work": {"keys": n_keys.value, "units": n_units.value, "runs": n_runs.value,
-                          "wave_iters": n_iters.value, "lane_tests": n_tests.value},
+                          "wave_iters": n_iters.value, "lane_tests": n_tests.value, "flushes": n_fl.value,
+                          "exact_merges": n_mg.value, "exact_merge_lanes": n_ml.value},
             "index_build_s": build_s,
             "roofline": {"kernel": "k_join (overlap join + fused altitude/time filter)", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

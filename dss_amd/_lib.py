@@ -11,7 +11,9 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdss_amd.so")
+# DSS_AMD_LIB: load a differently-tuned build of the same library (kernel
+# tuning experiments, tools/variants.sh); default: the in-tree build.
+LIB_PATH = os.environ.get("DSS_AMD_LIB") or os.path.join(_HERE, "libdss_amd.so")
 
 DSSG_OK = 0
 DSSG_ERR_INVALID = 1
@@ -130,6 +132,7 @@ def load():
         L.dssg_phase_times.argtypes = [vp, P(d), P(d), P(d)]
         L.dssg_set_timing.argtypes = [vp, C.c_int]
         L.dssg_set_timing.restype = None
+        L.dssg_join_events.argtypes = [vp, P(i64), P(i64), P(i64)]
         L.dssg_search_counters.argtypes = [vp, P(i64), P(i64), P(i64), P(i64), P(i64)]
         L.dssg_search_stats_device.argtypes = [vp, vp, i64, vp, vp, vp, P(i64), P(i64)]
         L.dssg_copy_to_host.argtypes = [vp, vp, vp, C.c_size_t]

@@ -237,6 +237,17 @@ int dssg_search_counters(dssg_ctx *ctx, int64_t *keys, int64_t *units, int64_t *
     return DSSG_OK;
 }
 
+int dssg_join_events(dssg_ctx *ctx, int64_t *flushes, int64_t *merges, int64_t *merge_lanes)
+{
+    if (!ctx) return DSSG_ERR_INVALID;
+    int64_t f, m, l;
+    ctx->search.last_join_events(&f, &m, &l);
+    if (flushes) *flushes = f;
+    if (merges) *merges = m;
+    if (merge_lanes) *merge_lanes = l;
+    return DSSG_OK;
+}
+
 int dssg_cover_batch_device(dssg_ctx *ctx, int64_t n, const int32_t *d_kind, const int64_t *d_voff, const double *d_lat,
                             const double *d_lng, const float *d_radius_m, void *stream, dssg_cells *out)
 {

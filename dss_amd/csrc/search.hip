@@ -30,6 +30,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "index_view.cuh"
@@ -44,9 +46,32 @@ constexpr int kLongSpan = 8;     // entities touching more buckets go to kLongBu
 constexpr int kMaxBuckets = 61;  // regular buckets 0..nb-1
 constexpr int kWaves = 4;        // join units per workgroup
 constexpr int kQChunk = 1024;    // query records per join unit
-constexpr int kStage = 512;      // pairs staged per wave in LDS
-constexpr int kGrab = 4;         // join units a persistent wave takes per queue access
-constexpr int kJoinBlocksPerCU = 5;  // LDS: 32 KiB per workgroup
+#ifndef DSS_JOIN_EXPERIMENT
+#define DSS_JOIN_EXPERIMENT 0
+#endif
+#ifndef DSS_JOIN_DIAG
+#define DSS_JOIN_DIAG 0  // 1: count flushes / exact merges (same-address atomics: slows the join)
+#endif
+#ifndef DSS_JOIN_STAGE
+#define DSS_JOIN_STAGE 1024
+#endif
+#ifndef DSS_JOIN_GRAB
+#define DSS_JOIN_GRAB 4
+#endif
+constexpr int kStage = DSS_JOIN_STAGE;  // pairs staged per wave in LDS
+constexpr int kGrab = DSS_JOIN_GRAB;    // join units a persistent wave takes per queue access
+#ifndef DSS_JOIN_BPC
+#define DSS_JOIN_BPC 4
+#endif
+constexpr int kJoinBlocksPerCU = DSS_JOIN_BPC;  // persistent workgroups per CU (LDS: 40 KiB each)
+#ifndef DSS_JOIN_WAVES
+#define DSS_JOIN_WAVES 5
+#endif
+#if DSS_JOIN_WAVES > 0
+#define DSS_JOIN_OCC __attribute__((amdgpu_waves_per_eu(DSS_JOIN_WAVES)))
+#else
+#define DSS_JOIN_OCC
+#endif
 constexpr uint32_t kRank0 = 0x80000000u;    // record: the cell is the query's first cell
 constexpr uint32_t kCompact = 0x40000000u;  // record: the query's prefix is compact
 
@@ -498,7 +523,10 @@ __global__ void k_gbounds(int64_t nkeys, const uint32_t *skey, uint32_t *gbeg, u
 // Postings per lane in a join unit: a unit covers up to 64 * kSlots postings
 // of one group, so a typical group (SURVEY config 1: ~75 postings) is one unit
 // and each broadcast record is tested against all of it.
-constexpr int kSlots = 2;
+#ifndef DSS_JOIN_SLOTS
+#define DSS_JOIN_SLOTS 2
+#endif
+constexpr int kSlots = DSS_JOIN_SLOTS;
 
 // (2) join units: (group, tile of <= 64 * kSlots postings, kQChunk-record
 // chunk), one thread per group of the index.  u_pt = tile | (slots - 1) << 28.
@@ -554,6 +582,15 @@ __global__ void k_work_stats(int64_t ng, const uint32_t *bk_start, const uint32_
     }
 }
 
+// Unit queue: same-address atomics serialise at one L2 channel
+// (MI355X_MICROARCH.md "dequeue"), so the queue has kQShards heads, each over
+// a contiguous range of the unit list; a wave starts on head blockIdx %
+// kQShards (blocks b and b + 8 share an XCD -- speed only) and then steals.
+#ifndef DSS_JOIN_QSHARDS
+#define DSS_JOIN_QSHARDS 1
+#endif
+constexpr int kQShards = DSS_JOIN_QSHARDS;
+
 struct JoinArgs {
     IndexView ix;
     QueryView qv;
@@ -561,6 +598,7 @@ struct JoinArgs {
     const uint64_t *g_key;  // group -> slot << 6 | bucket
     const uint32_t *gbeg, *gend;
     int64_t cap;
+    unsigned long long *counter;  // output pairs
 };
 
 // One posting held by a lane.
@@ -603,28 +641,38 @@ __device__ __forceinline__ void load_slot(const IndexView &ix, uint32_t p, uint3
 // (3) one wavefront per unit: up to 64 * kSlots postings in registers, the
 // unit's query records staged through LDS 64 at a time and broadcast.
 template <bool OWNER>
-__global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__restrict__ recs,
+__global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, const QRec *__restrict__ recs,
                                                       const uint32_t *__restrict__ sval,
                                                       const int32_t *__restrict__ rown, const uint32_t *__restrict__ u_run,
                                                       const uint32_t *__restrict__ u_pt, const uint32_t *__restrict__ u_qt,
                                                       uint32_t *__restrict__ out_q, uint32_t *__restrict__ out_e,
-                                                      unsigned long long *__restrict__ counter,
                                                       uint32_t *__restrict__ work)
 {
-    __shared__ int4 s_rec[kWaves][4][64];  // 64-byte records, split in 16-byte columns
-    __shared__ int32_t s_own[kWaves][OWNER ? 64 : 1];
+    // record heads (time window, altitudes, query, bucket) stay in the
+    // loading lane's VGPRs and are broadcast with v_readlane; only the
+    // prefix signatures (needed for a minority of records) go through LDS
+    __shared__ int4 s_sig[kWaves][2][64];
     __shared__ uint32_t sq[kWaves][kStage];
     __shared__ uint32_t se[kWaves][kStage];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int staged = 0;
+    const int shard = (int)(blockIdx.x & (kQShards - 1));
     auto flush = [&]() {
         __builtin_amdgcn_wave_barrier();
+#if DSS_JOIN_EXPERIMENT == 1  // timing experiment: drop the pairs
+        staged = 0;
+#endif
         unsigned long long base = 0;
-        if (lane == 0 && staged) base = atomicAdd(counter, (unsigned long long)staged);
+        if (lane == 0 && staged) {
+            base = atomicAdd(a.counter, (unsigned long long)staged);
+#if DSS_JOIN_DIAG
+            atomicAdd(&work[kQShards], 1u);  // diagnostics: flushes
+#endif
+        }
         base = __shfl(base, 0);
         for (int k = lane; k < staged; k += 64) {
-            unsigned long long o = base + (unsigned long long)k;
+            const unsigned long long o = base + (unsigned long long)k;
             if ((int64_t)o < a.cap) {
                 out_q[o] = sq[w][k];
                 out_e[o] = se[w][k];
@@ -634,17 +682,21 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
         __builtin_amdgcn_wave_barrier();
     };
     const IndexView &ix = a.ix;
-    // persistent waves: grab kGrab units at a time until the queue drains;
-    // the staging buffer carries over between units, so the output counter
-    // sees one atomic per kStage pairs
+    // persistent waves: grab kGrab units at a time from this shard's range of
+    // the unit list, then from the other shards' (stealing) until all drain;
+    // the staging buffer carries over between units
     const int64_t nunits = *a.nunits;
-    for (;;) {
+    for (int r = 0; r < kQShards; r++) {
+      const int rs = (shard + r) % kQShards;  // this shard's range, then steal
+      const int64_t rbeg = nunits * rs / kQShards, rend = nunits * (rs + 1) / kQShards;
+      for (;;) {
         uint32_t ub = 0;
-        if (lane == 0) ub = atomicAdd(work, (uint32_t)kGrab);
+        if (lane == 0) ub = atomicAdd(&work[rs], (uint32_t)kGrab);
         ub = __builtin_amdgcn_readfirstlane(__shfl(ub, 0));
-        if ((int64_t)ub >= nunits) break;
-        const uint32_t ue = (uint32_t)min((int64_t)ub + kGrab, nunits);
-        for (uint32_t u = ub; u < ue; u++) {
+        if (rbeg + (int64_t)ub >= rend) break;
+        const uint32_t ub0 = (uint32_t)(rbeg + ub);
+        const uint32_t ue = (uint32_t)min(rbeg + (int64_t)ub + kGrab, rend);
+        for (uint32_t u = ub0; u < ue; u++) {
             const uint32_t g = u_run[u];
             const uint64_t key = a.g_key[g];
             const int b = (int)(key & 63);
@@ -682,98 +734,137 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
             for (int64_t base = k0; base < k1; base += 64) {
                 const int64_t kk = base + lane;
                 bool rel = false;
+                int4 r0 = make_int4(0, 0, 0, 0), r1 = make_int4(0, 0, 0, 0);
+                int32_t rown_l = -1;
                 __builtin_amdgcn_wave_barrier();
                 if (kk < k1) {
                     const uint32_t ci = sval[kk];
-                    const int4 c0 = rec4[4 * ci], c1 = rec4[4 * ci + 1], c2 = rec4[4 * ci + 2], c3 = rec4[4 * ci + 3];
-                    s_rec[w][0][lane] = c0;
-                    s_rec[w][1][lane] = c1;
-                    s_rec[w][2][lane] = c2;
-                    s_rec[w][3][lane] = c3;
-                    if (OWNER) s_own[w][lane] = rown[ci];
-                    const long long tlo = ((long long)c0.y << 32) | (uint32_t)c0.x;
-                    const long long thi = ((long long)c0.w << 32) | (uint32_t)c0.z;
-                    const float alo = __int_as_float(c1.x), ahi = __int_as_float(c1.y);
+                    r0 = rec4[4 * ci];
+                    r1 = rec4[4 * ci + 1];
+                    s_sig[w][0][lane] = rec4[4 * ci + 2];
+                    s_sig[w][1][lane] = rec4[4 * ci + 3];
+                    if (OWNER) rown_l = rown[ci];
+                    const long long tlo = ((long long)r0.y << 32) | (uint32_t)r0.x;
+                    const long long thi = ((long long)r0.w << 32) | (uint32_t)r0.z;
+                    const float alo = __int_as_float(r1.x), ahi = __int_as_float(r1.y);
                     rel = !(tmax < tlo || tmin > thi) && !(amax < alo || amin > ahi);  // else no posting can match
                 }
                 __builtin_amdgcn_wave_barrier();
-                unsigned long long todo = __ballot(rel);
-                while (todo) {
-                    const int j = __builtin_ctzll(todo);
-                    todo &= todo - 1;
-                    const int4 c0 = s_rec[w][0][j], c1 = s_rec[w][1][j];
-                    const long long tlo = ((long long)c0.y << 32) | (uint32_t)c0.x;
-                    const long long thi = ((long long)c0.w << 32) | (uint32_t)c0.z;
-                    const float alo = __int_as_float(c1.x), ahi = __int_as_float(c1.y);
-                    const uint32_t qv = (uint32_t)c1.z;
-                    const int bq0 = c1.w;
-                    const int32_t own = OWNER ? s_own[w][j] : -1;
-                    const uint32_t q = qv & ~(kRank0 | kCompact);
-                    bool pass[kSlots];
-                    bool any_need = false;
+                const unsigned long long todo0 = __ballot(rel);
+                // The record loop, specialised on the unit's slot count.  All
+                // decisions are 64-bit wave masks (SALU); VALU work per record
+                // is the four interval compares per slot, plus the signature
+                // overlap for slots holding a candidate that needs it.
+                auto records = [&](auto nsc) {
+                    constexpr int NS = decltype(nsc)::value;
+                    unsigned long long mf[NS], mc[NS], mb[NS];
 #pragma unroll
-                    for (int k = 0; k < kSlots; k++) {
-                        const Slot &s = sl[k];
-                        // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels),
-                        // evaluated branch-free (bitwise &, no short-circuit)
-                        bool p = (s.t.y >= tlo) & (s.t.x <= thi) & (s.alt.y >= alo) & (s.alt.x <= ahi);
-                        if (OWNER) p = p & ((own < 0) | (s.own == own));
-                        // keep the pair only in its first common bucket ...
-                        p = p & ((b == kLongBucket) | (b == max(bq0, s.be0)));
-                        pass[k] = p;
-                        any_need = any_need | (p & !s.first);
+                    for (int k = 0; k < NS; k++) {
+                        mf[k] = __ballot(sl[k].first);
+                        mc[k] = __ballot(sl[k].compact);
+                        mb[k] = __ballot(sl[k].be0 == b);
                     }
-                    // ... and at the smallest shared cell (SQL DISTINCT, Q13)
-                    if (!(qv & kRank0) && __ballot(any_need)) {
-                        const int4 c2 = s_rec[w][2][j], c3 = s_rec[w][3][j];
-                        const unsigned long long q0 = ((unsigned long long)(uint32_t)c2.y << 32) | (uint32_t)c2.x;
-                        const unsigned long long q1 = ((unsigned long long)(uint32_t)c2.w << 32) | (uint32_t)c2.z;
-                        const unsigned long long q2 = ((unsigned long long)(uint32_t)c3.y << 32) | (uint32_t)c3.x;
-                        const unsigned long long q3 = ((unsigned long long)(uint32_t)c3.w << 32) | (uint32_t)c3.z;
-                        const bool qcompact = (qv & kCompact) != 0;
-                        bool ex[kSlots];
-                        bool any_ex = false;
+                    unsigned long long todo = todo0;
+                    while (todo) {
+                        const int j = __builtin_ctzll(todo);
+                        todo &= todo - 1;
+                        const long long tlo = ((long long)__builtin_amdgcn_readlane(r0.y, j) << 32) |
+                                              (uint32_t)__builtin_amdgcn_readlane(r0.x, j);
+                        const long long thi = ((long long)__builtin_amdgcn_readlane(r0.w, j) << 32) |
+                                              (uint32_t)__builtin_amdgcn_readlane(r0.z, j);
+                        const float alo = __int_as_float(__builtin_amdgcn_readlane(r1.x, j));
+                        const float ahi = __int_as_float(__builtin_amdgcn_readlane(r1.y, j));
+                        const uint32_t qv = (uint32_t)__builtin_amdgcn_readlane(r1.z, j);
+                        const int bq0 = __builtin_amdgcn_readlane(r1.w, j);
+                        const int32_t own = OWNER ? __builtin_amdgcn_readlane(rown_l, j) : -1;
+                        const uint32_t q = qv & ~(kRank0 | kCompact);
+                        // keep a pair only in its first common bucket: b == max(bq0, be0),
+                        // i.e. bq0 == b (every lane) or be0 == b (mask mb)
+                        const bool all_b = (b == kLongBucket) | (bq0 == b);
+                        unsigned long long pm[NS];
 #pragma unroll
-                        for (int k = 0; k < kSlots; k++) {
-                            const Slot &s = sl[k];
-                            const bool ov = ((s.s01.x & q0) | (s.s01.y & q1) | (s.s23.x & q2) | (s.s23.y & q3)) != 0;
-                            const bool chk = pass[k] & !s.first & ov;
-                            const bool both = s.compact & qcompact;
-                            pass[k] = pass[k] & !(chk & both);  // equal bits within +-7 cells: a shared smaller cell exists
-                            ex[k] = chk & !both;                // signature inconclusive: merge the cell lists
-                            any_ex = any_ex | ex[k];
+                        for (int k = 0; k < NS; k++) {
+                            const Slot &sk = sl[k];
+                            // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels)
+                            bool p = (sk.t.y >= tlo) & (sk.t.x <= thi) & (sk.alt.y >= alo) & (sk.alt.x <= ahi);
+                            if (OWNER) p = p & ((own < 0) | (sk.own == own));
+                            const unsigned long long m = __ballot(p);
+                            pm[k] = all_b ? m : (m & mb[k]);
                         }
-                        if (__ballot(any_ex)) {
-                            const uint64_t *qc = a.qv.cells + a.qv.offs[q];
-                            const int64_t nqc = a.qv.offs[q + 1] - a.qv.offs[q];
+                        // ... and at the smallest shared cell (SQL DISTINCT, Q13)
+                        if (!(qv & kRank0)) {
+                            unsigned long long need[NS], any = 0;
 #pragma unroll
-                            for (int k = 0; k < kSlots; k++)
-                                if (ex[k]) pass[k] = no_smaller_shared(ix, sl[k].ent, cell, qc, nqc);
+                            for (int k = 0; k < NS; k++) {
+                                need[k] = pm[k] & ~mf[k];
+                                any |= need[k];
+                            }
+                            if (any) {
+                                const int4 c2 = s_sig[w][0][j], c3 = s_sig[w][1][j];
+                                const bool qcompact = (qv & kCompact) != 0;
+#pragma unroll
+                                for (int k = 0; k < NS; k++) {
+                                    if (!need[k]) continue;
+                                    const Slot &sk = sl[k];
+                                    uint32_t acc = (uint32_t)sk.s01.x & (uint32_t)c2.x;
+                                    acc |= (uint32_t)(sk.s01.x >> 32) & (uint32_t)c2.y;
+                                    acc |= (uint32_t)sk.s01.y & (uint32_t)c2.z;
+                                    acc |= (uint32_t)(sk.s01.y >> 32) & (uint32_t)c2.w;
+                                    acc |= (uint32_t)sk.s23.x & (uint32_t)c3.x;
+                                    acc |= (uint32_t)(sk.s23.x >> 32) & (uint32_t)c3.y;
+                                    acc |= (uint32_t)sk.s23.y & (uint32_t)c3.z;
+                                    acc |= (uint32_t)(sk.s23.y >> 32) & (uint32_t)c3.w;
+                                    const unsigned long long chk = need[k] & __ballot(acc != 0u);
+                                    // both prefixes compact: equal bits are equal cells, a
+                                    // smaller shared cell exists -> drop
+                                    const unsigned long long sure = qcompact ? (chk & mc[k]) : 0ull;
+                                    pm[k] &= ~sure;
+                                    const unsigned long long ex = chk & ~sure;  // inconclusive: merge the lists
+                                    if (ex) {
+#if DSS_JOIN_DIAG
+                                        if (lane == 0) {  // diagnostics: merges (events, lanes)
+                                            atomicAdd(&work[kQShards + 1], 1u);
+                                            atomicAdd(&work[kQShards + 2], (uint32_t)__popcll(ex));
+                                        }
+#endif
+                                        bool drop = false;
+                                        if ((ex >> lane) & 1ull) {
+                                            const uint64_t *qc = a.qv.cells + a.qv.offs[q];
+                                            const int64_t nqc = a.qv.offs[q + 1] - a.qv.offs[q];
+                                            drop = !no_smaller_shared(ix, sk.ent, cell, qc, nqc);
+                                        }
+                                        pm[k] &= ~__ballot(drop);
+                                    }
+                                }
+                            }
+                        }
+                        int tot = 0;
+#pragma unroll
+                        for (int k = 0; k < NS; k++) tot += __popcll(pm[k]);
+                        if (tot == 0) continue;
+                        if (staged + tot > kStage) flush();
+                        const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+                        for (int k = 0; k < NS; k++) {
+                            if ((pm[k] >> lane) & 1ull) {
+                                const int rk = staged + __popcll(pm[k] & below);
+                                sq[w][rk] = q;
+                                se[w][rk] = sl[k].ent;
+                            }
+                            staged += __popcll(pm[k]);
                         }
                     }
-                    unsigned long long m[kSlots];
-                    int tot = 0;
-#pragma unroll
-                    for (int k = 0; k < kSlots; k++) {
-                        m[k] = __ballot(pass[k]);
-                        tot += __popcll(m[k]);
-                    }
-                    if (tot == 0) continue;
-                    if (staged + tot > kStage) flush();
-                    const unsigned long long below = (1ull << lane) - 1ull;
-#pragma unroll
-                    for (int k = 0; k < kSlots; k++) {
-                        if (pass[k]) {
-                            const int rk = staged + __popcll(m[k] & below);
-                            sq[w][rk] = q;
-                            se[w][rk] = sl[k].ent;
-                        }
-                        staged += __popcll(m[k]);
-                    }
-                }
+                };
+#if DSS_JOIN_EXPERIMENT == 2  // timing experiment: units and records loaded, no tests
+                if (todo0 == 0x1234567ull) staged += 1;
+#else
+                if (nslot == 1) records(std::integral_constant<int, 1>{});
+                else records(std::integral_constant<int, kSlots>{});
+#endif
             }
 
         }
+      }
     }
     flush();
 }
@@ -1176,7 +1267,6 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     ja.g_key = idx->g_key.p;
     ja.gbeg = gbeg;
     ja.gend = gend;
-    unsigned long long *counter = counter_.ensure(1);
     if (out_cap_ == 0) out_cap_ = (size_t)nq * 16 + 1024;
     // persistent grid: a few workgroups per CU (LDS-limited), units pulled from a queue
     if (n_cu_ == 0) {
@@ -1186,21 +1276,23 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         n_cu_ = ncu > 0 ? ncu : 256;
     }
     const unsigned nblocks = (unsigned)n_cu_ * kJoinBlocksPerCU;
-    uint32_t *work = work_.ensure(1);
+    uint32_t *work = work_.ensure(kQShards + 4);  // [0, kQShards) unit heads, then diagnostics
+    unsigned long long *counter = counter_.ensure(1);
+    ja.counter = counter;
     for (int attempt = 0; attempt < 3; attempt++) {
         uint32_t *oq = oq_.ensure(out_cap_), *oe = oe_.ensure(out_cap_);
         DSS_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned long long), s));
-        DSS_HIP(hipMemsetAsync(work, 0, sizeof(uint32_t), s));
+        DSS_HIP(hipMemsetAsync(work, 0, (kQShards + 4) * sizeof(uint32_t), s));
         ja.cap = (int64_t)out_cap_;
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
         if (nblocks && q_owner)
             hipLaunchKernelGGL(k_join<true>, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
                                (const uint32_t *)sval, (const int32_t *)rown, (const uint32_t *)u_run,
-                               (const uint32_t *)u_pt, (const uint32_t *)u_qt, oq, oe, counter, work);
+                               (const uint32_t *)u_pt, (const uint32_t *)u_qt, oq, oe, work);
         else if (nblocks)
             hipLaunchKernelGGL(k_join<false>, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
                                (const uint32_t *)sval, (const int32_t *)nullptr, (const uint32_t *)u_run, (const uint32_t *)u_pt,
-                               (const uint32_t *)u_qt, oq, oe, counter, work);
+                               (const uint32_t *)u_qt, oq, oe, work);
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
         unsigned long long total = 0;
         DSS_HIP(hipMemcpyAsync(&total, counter, sizeof(total), hipMemcpyDeviceToHost, s));
@@ -1209,6 +1301,11 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             float ms = 0;
             DSS_HIP(hipEventElapsedTime(&ms, ev0_, ev1_));
             join_ms_ = ms;
+            uint32_t hw[kQShards + 4];
+            DSS_HIP(hipMemcpy(hw, work, sizeof(hw), hipMemcpyDeviceToHost));
+            flushes_ = hw[kQShards];
+            merges_ = hw[kQShards + 1];
+            merge_lanes_ = hw[kQShards + 2];
         }
         if (total <= out_cap_) {
             out->q = oq;

@@ -79,6 +79,13 @@ class SearchEngine {
     int64_t last_units() const { return units_; }
     int64_t last_keys() const { return keys_; }
     // timing mode only: runs, wave iterations (records x tiles), useful lane tests
+    // timing mode only: output flushes, exact list merges (events, lanes)
+    void last_join_events(int64_t *flushes, int64_t *merges, int64_t *merge_lanes) const
+    {
+        *flushes = flushes_;
+        *merges = merges_;
+        *merge_lanes = merge_lanes_;
+    }
     void last_work(int64_t *runs, int64_t *iters, int64_t *tests) const
     {
         *runs = runs_;
@@ -101,6 +108,7 @@ class SearchEngine {
     bool timing_ = false;
     double join_ms_ = 0;
     int64_t units_ = 0, keys_ = 0, runs_ = 0, iters_ = 0, tests_ = 0;
+    int64_t flushes_ = 0, merges_ = 0, merge_lanes_ = 0;
     hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
 };
 
