@@ -57,8 +57,9 @@ def main():
     ap.add_argument("--mode", choices=["sharded", "replica"], default=None,
                     help="multi-GPU layout (default: sharded for N > 1, replica for N = 1)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on a multi-GPU node; gloo for rehearsals")
-    ap.add_argument("--pipelines", type=int, default=1,
-                    help="concurrent batch pipelines per GPU (own engine context + stream + host thread each)")
+    ap.add_argument("--pipelines", type=int, default=2,
+                    help="concurrent batch pipelines per GPU (own engine context + stream + host thread each): one "
+                         "batch's FP64 covering overlaps another's join, as concurrent RPCs would (replica mode)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank on cuda:0 (one-GPU box, gloo backend)")
     args = ap.parse_args()
@@ -261,7 +262,8 @@ def main():
             "config": {"workload": f"configs[{args.config}]: {nq} query footprints/GPU/step (70% polygon, 30% circle)"
                                    f" vs {ni}-intent resident index, SF-Bay metro, S2 level 13",
                        "queries_per_gpu_step": nq, "intents": ni, "postings": n_post,
-                       "parallelism": f"query-sharded x{world}, index replicated", "scale": args.scale},
+                       "parallelism": f"query-sharded x{world}, index replicated", "scale": args.scale,
+                       "pipelines_per_gpu": args.pipelines},
             "coverings_per_s": world * nq / (cover_avg * 1e-3),
             "phase_ms": {"cover": cover_avg, "join": join_avg, "join_kernel": kern_avg_ms},
             "pairs_per_step": r_tot,
