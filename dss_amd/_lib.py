@@ -119,6 +119,15 @@ def load():
         L.dssg_search_isas.argtypes = [vp, vp, i64, P(i64), P(u64), P(i64), P(i64), P(u32), P(u32), i64, P(i64)]
         L.dssg_search_subscriptions.argtypes = [vp, vp, i64, P(i64), P(u64), P(i32), i64, P(u32), P(u32), i64,
                                                 P(i64)]
+        L.dssg_store_create.argtypes = [vp, i32, P(vp)]
+        L.dssg_store_free.argtypes = [vp]
+        L.dssg_store_free.restype = None
+        L.dssg_store_upsert.argtypes = [vp, vp, i64, P(u32), P(i64), P(u64), P(f), P(f), P(i64), P(i64), P(i32)]
+        L.dssg_store_delete.argtypes = [vp, vp, i64, P(u32), P(i32)]
+        L.dssg_store_compact.argtypes = [vp, vp]
+        L.dssg_store_stats.argtypes = [vp, P(i64), P(i64), P(i64), P(i64)]
+        L.dssg_store_search.argtypes = [vp, vp, i64, P(i64), P(u64), P(f), P(f), P(i64), P(i64), P(i32), P(u32),
+                                        P(u32), i64, P(i64)]
         L.dssg_index_set_notification_index.argtypes = [vp, vp, P(i64)]
         L.dssg_index_get_notification_index.argtypes = [vp, vp, P(i64)]
         L.dssg_notify_subscriptions.argtypes = [vp, vp, i64, P(i64), P(u64), i64, P(u32), P(u32), P(i64), i64, P(i64)]

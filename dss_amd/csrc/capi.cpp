@@ -14,6 +14,7 @@
 #include "cover.hpp"
 #include "route.hpp"
 #include "search.hpp"
+#include "store.hpp"
 #include "subs.hpp"
 
 struct dssg_ctx {
@@ -675,6 +676,93 @@ int dssg_max_subscription_count(dssg_ctx *ctx, const dssg_index *idx, int64_t nq
         const int32_t *dow = upload(ctx->d_owner, owner, nq, s);
         ctx->subs.max_count(idx, nq, dqo, dqc, nqc, dow, now_us, s, out_count);
     });
+}
+
+struct dssg_store {
+    dss::Store st;
+    dssg_store(int device, bool owner) : st(device, owner) {}
+};
+
+int dssg_store_create(dssg_ctx *ctx, int32_t with_owner, dssg_store **out)
+{
+    if (!ctx || !out) return DSSG_ERR_INVALID;
+    *out = new (std::nothrow) dssg_store(ctx->device, with_owner != 0);
+    return *out ? DSSG_OK : DSSG_ERR_NOMEM;
+}
+
+void dssg_store_free(dssg_store *st)
+{
+    if (!st) return;
+    delete st;
+}
+
+int dssg_store_upsert(dssg_ctx *ctx, dssg_store *st, int64_t n, const uint32_t *ids, const int64_t *cell_offs,
+                      const uint64_t *cells, const float *alt_lo, const float *alt_hi, const int64_t *t0,
+                      const int64_t *t1, const int32_t *owner)
+{
+    if (!ctx || !st || n < 0 || (n > 0 && (!ids || !cell_offs || !alt_lo || !alt_hi || !t0 || !t1)) ||
+        (n > 0 && cell_offs[n] > 0 && !cells))
+        return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        st->st.upsert(ctx->search, n, ids, cell_offs, cells, alt_lo, alt_hi, t0, t1, owner, ctx->stream);
+    });
+}
+
+int dssg_store_delete(dssg_ctx *ctx, dssg_store *st, int64_t n, const uint32_t *ids, int32_t *found)
+{
+    if (!ctx || !st || n < 0 || (n > 0 && !ids)) return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] { st->st.remove(ctx->search, n, ids, found, ctx->stream); });
+}
+
+int dssg_store_compact(dssg_ctx *ctx, dssg_store *st)
+{
+    if (!ctx || !st) return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] { st->st.compact(ctx->search, ctx->stream); });
+}
+
+int dssg_store_stats(const dssg_store *st, int64_t *live, int64_t *base, int64_t *delta, int64_t *compactions)
+{
+    if (!st) return DSSG_ERR_INVALID;
+    if (live) *live = st->st.live();
+    if (base) *base = st->st.base_size();
+    if (delta) *delta = st->st.delta_size();
+    if (compactions) *compactions = st->st.compactions();
+    return DSSG_OK;
+}
+
+int dssg_store_search(dssg_ctx *ctx, dssg_store *st, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
+                      const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
+                      const int32_t *q_owner, uint32_t *out_q, uint32_t *out_id, int64_t cap, int64_t *needed)
+{
+    if (!ctx || !st || !needed || nq < 0 || !q_offs || (nq > 0 && (!q_alt_lo || !q_alt_hi || !q_tlo || !q_thi)))
+        return DSSG_ERR_INVALID;
+    int code = DSSG_OK;
+    int rc = guarded(ctx, [&] {
+        for (int64_t q = 0; q < nq; q++)
+            if (q_tlo[q] == INT64_MIN) throw dss::Error(DSSG_ERR_INVALID, "query tlo must not be NULL");
+        hipStream_t s = ctx->stream;
+        const int64_t *dqo = nullptr;
+        const uint64_t *dqc = nullptr;
+        stage_query_cells(ctx, nq, q_offs, q_cells, s, &dqo, &dqc);
+        const float *dlo = upload(ctx->d_alo, q_alt_lo, nq, s);
+        const float *dhi = upload(ctx->d_ahi, q_alt_hi, nq, s);
+        const int64_t *dtl = upload(ctx->d_tlo, q_tlo, nq, s);
+        const int64_t *dth = upload(ctx->d_thi, q_thi, nq, s);
+        const int32_t *dow = q_owner ? upload(ctx->d_owner, q_owner, nq, s) : nullptr;
+        std::vector<uint64_t> res;
+        const int64_t n = st->st.search(ctx->search, nq, dqo, dqc, dlo, dhi, dtl, dth, dow, s, res);
+        *needed = n;
+        if (n > cap) {
+            code = DSSG_ERR_CAPACITY;
+            return;
+        }
+        if (n > 0 && (!out_q || !out_id)) throw dss::Error(DSSG_ERR_INVALID, "output pointers are NULL");
+        for (int64_t i = 0; i < n; i++) {
+            out_q[i] = (uint32_t)(res[i] >> 32);
+            out_id[i] = (uint32_t)res[i];
+        }
+    });
+    return rc ? rc : code;
 }
 
 int dssg_search_stats_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *d_q_offs,

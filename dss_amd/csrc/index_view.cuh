@@ -58,6 +58,7 @@ struct IndexView {
     const uint32_t *p_mult;  // multiplicity of (cell, entity) in the stored cell array
     const int64_t *e_t1;     // entity end time (us)
     const int32_t *e_owner;  // entity owner (nullptr: built without owners)
+    const uint32_t *dead;    // tombstone bitmap (nullptr: none)
     Buckets bk;
 };
 
@@ -85,6 +86,7 @@ IndexView view_of(const dssg_index *idx)
     v.p_mult = idx->p_mult.p;
     v.e_t1 = idx->e_t1.p;
     v.e_owner = idx->has_owner ? idx->e_owner.p : nullptr;
+    v.dead = idx->has_dead ? idx->dead.p : nullptr;
     v.bk = Buckets{idx->tbase, idx->shift, idx->nb};
     return v;
 }
@@ -125,6 +127,11 @@ __device__ __forceinline__ void plain_range(const IndexView &a, uint32_t slot, u
         s = a.irr_start[k];
         e = a.irr_start[k + 1];
     }
+}
+
+__device__ __forceinline__ bool is_dead(const IndexView &a, uint32_t e)
+{
+    return a.dead && ((a.dead[e >> 5] >> (e & 31)) & 1u);
 }
 
 }  // namespace

@@ -65,7 +65,7 @@ constexpr int kGrab = DSS_JOIN_GRAB;    // join units a persistent wave takes pe
 #endif
 constexpr int kJoinBlocksPerCU = DSS_JOIN_BPC;  // persistent workgroups per CU (LDS: 40 KiB each)
 #ifndef DSS_JOIN_WAVES
-#define DSS_JOIN_WAVES 5
+#define DSS_JOIN_WAVES 4
 #endif
 #if DSS_JOIN_WAVES > 0
 #define DSS_JOIN_OCC __attribute__((amdgpu_waves_per_eu(DSS_JOIN_WAVES)))
@@ -624,6 +624,10 @@ __device__ __forceinline__ void load_slot(const IndexView &ix, uint32_t p, uint3
     s.s01 = s.s23 = make_ulonglong2(0, 0);
     if (!s.valid) return;
     const uint32_t v = ix.b_e[p];
+    if (is_dead(ix, v & ~kFirstBit)) {  // tombstoned by the write path: matches nothing
+        s.valid = false;
+        return;
+    }
     const uint8_t m = ix.b_meta[p];
     s.ent = v & ~kFirstBit;
     s.first = (v & kFirstBit) != 0;

@@ -53,6 +53,10 @@ struct dssg_index {
     dss::DevBuf<uint32_t> o_key;   // owner ^ 0x80000000, ascending (owner -> entities)
     dss::DevBuf<uint32_t> o_ent;   // entity ids in o_key order
     dss::DevBuf<int64_t> e_notify; // notification_index counters
+    // tombstones (write path, store.hip): bit e set = entity e is deleted or
+    // superseded; the join and the subscription queries skip it
+    dss::DevBuf<uint32_t> dead;
+    bool has_dead = false;
     int device = 0;
 };
 

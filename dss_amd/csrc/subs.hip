@@ -53,7 +53,7 @@ __global__ void k_max_count(IndexView a, int64_t nqc, const uint64_t *cells, con
     unsigned long long cnt = 0;
     for (uint32_t p = s; p < e; p++) {
         const uint32_t ent = a.p_e[p] & ~kFirstBit;
-        if (a.e_owner[ent] == own && a.e_t1[ent] >= now) cnt += a.p_mult[p];
+        if (a.e_owner[ent] == own && a.e_t1[ent] >= now && !is_dead(a, ent)) cnt += a.p_mult[p];
     }
     if (cnt) atomicMax(&out[q], cnt);
 }
@@ -73,8 +73,8 @@ __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t *x, uint32_t 
 // counts, PASS 1 writes at off[q].
 template <int PASS>
 __global__ void k_owner_subs(int64_t nq, const int32_t *owner, long long now, const uint32_t *o_key, const uint32_t *o_ent,
-                             uint32_t n, const int64_t *e_t1, int64_t *cnt, const int64_t *off, uint32_t *out_q,
-                             uint32_t *out_e)
+                             uint32_t n, const int64_t *e_t1, const uint32_t *dead, int64_t *cnt, const int64_t *off,
+                             uint32_t *out_q, uint32_t *out_e)
 {
     const int64_t q = tid64();
     if (q >= nq) return;
@@ -84,7 +84,7 @@ __global__ void k_owner_subs(int64_t nq, const int32_t *owner, long long now, co
     int64_t c = 0, w = PASS ? off[q] : 0;
     for (uint32_t i = b; i < e; i++) {
         const uint32_t ent = o_ent[i];
-        if (e_t1[ent] < now) continue;
+        if (e_t1[ent] < now || (dead && ((dead[ent >> 5] >> (ent & 31)) & 1u))) continue;
         if (PASS) {
             out_q[w] = (uint32_t)q;
             out_e[w] = ent;
@@ -171,7 +171,8 @@ int64_t SubsEngine::owner_subs(const dssg_index *idx, int64_t nq, const int32_t 
     const uint32_t n = (uint32_t)idx->n_e;
     if (nq > 0)
         hipLaunchKernelGGL(k_owner_subs<0>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, owner, (long long)now,
-                           idx->o_key.p, idx->o_ent.p, n, idx->e_t1.p, cnt, nullptr, nullptr, nullptr);
+                           idx->o_key.p, idx->o_ent.p, n, idx->e_t1.p, idx->has_dead ? idx->dead.p : nullptr, cnt,
+                           nullptr, nullptr, nullptr);
     exclusive_scan_i64(cnt, off, nq, tmp_, s);
     int64_t total = 0;
     DSS_HIP(hipMemcpyAsync(&total, off + nq, sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -179,7 +180,8 @@ int64_t SubsEngine::owner_subs(const dssg_index *idx, int64_t nq, const int32_t 
     uint32_t *oq = q_.ensure(total + 1), *oe = e_.ensure(total + 1);
     if (nq > 0 && total > 0)
         hipLaunchKernelGGL(k_owner_subs<1>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, owner, (long long)now,
-                           idx->o_key.p, idx->o_ent.p, n, idx->e_t1.p, nullptr, off, oq, oe);
+                           idx->o_key.p, idx->o_ent.p, n, idx->e_t1.p, idx->has_dead ? idx->dead.p : nullptr, nullptr,
+                           off, oq, oe);
     DSS_HIP(hipStreamSynchronize(s));
     *out_q = oq;
     *out_e = oe;

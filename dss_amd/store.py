@@ -302,3 +302,206 @@ def MaxSubscriptionCountInCellsByOwner(index: EntityIndex, cells: Sequence[int],
     """RID subscriptions.go:83-116 / SCD subscriptions.go:255-283."""
     offs, cc = _csr([cells])
     return int(index.max_subscription_count_batch(offs, cc, [owner], now_us)[0])
+
+
+# ------------------------------------------------------------- write path
+class Store:
+    """dssg_store: a mutable entity index keyed by caller ids (uint32).
+    Upserts/deletes are visible to every later search (base + delta index +
+    tombstones on the GPU, include/dssgpu.h)."""
+
+    def __init__(self, with_owner: bool = False, device: int = 0):
+        self.ctx = _lib.context(device)
+        h = C.c_void_p()
+        self.ctx.check(self.ctx.L.dssg_store_create(self.ctx.h, 1 if with_owner else 0, C.byref(h)))
+        self.h = h
+        self.with_owner = with_owner
+
+    def free(self):
+        if getattr(self, "h", None):
+            self.ctx.L.dssg_store_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def upsert(self, ids, cell_lists, alt_lo, alt_hi, t0, t1, owner=None):
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        offs, cells = _csr(cell_lists)
+        lo = np.ascontiguousarray(alt_lo, dtype=np.float32)
+        hi = np.ascontiguousarray(alt_hi, dtype=np.float32)
+        a0 = np.ascontiguousarray(t0, dtype=np.int64)
+        a1 = np.ascontiguousarray(t1, dtype=np.int64)
+        ow = np.ascontiguousarray(owner, dtype=np.int32) if owner is not None else None
+        self.ctx.check(self.ctx.L.dssg_store_upsert(
+            self.ctx.h, self.h, len(ids), _p(ids, C.c_uint32), _p(offs, C.c_int64), _p(cells, C.c_uint64),
+            _p(lo, C.c_float), _p(hi, C.c_float), _p(a0, C.c_int64), _p(a1, C.c_int64),
+            _p(ow, C.c_int32) if ow is not None else C.POINTER(C.c_int32)()))
+
+    def delete(self, ids) -> np.ndarray:
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        found = np.zeros(max(len(ids), 1), dtype=np.int32)
+        self.ctx.check(self.ctx.L.dssg_store_delete(self.ctx.h, self.h, len(ids), _p(ids, C.c_uint32),
+                                                    _p(found, C.c_int32)))
+        return found[: len(ids)].astype(bool)
+
+    def compact(self):
+        self.ctx.check(self.ctx.L.dssg_store_compact(self.ctx.h, self.h))
+
+    def stats(self) -> dict:
+        v = [C.c_int64() for _ in range(4)]
+        self.ctx.check(self.ctx.L.dssg_store_stats(self.h, *[C.byref(x) for x in v]))
+        return dict(zip(["live", "base", "delta", "compactions"], [x.value for x in v]))
+
+    def search_batch(self, q_offs, q_cells, alt_lo, alt_hi, tlo, thi, owner=None):
+        """(query, id) pairs, sorted; the generic predicate of dssg_search."""
+        q_offs = np.ascontiguousarray(q_offs, dtype=np.int64)
+        q_cells = np.ascontiguousarray(q_cells, dtype=np.uint64)
+        nq = len(q_offs) - 1
+        lo = np.ascontiguousarray(alt_lo, dtype=np.float32)
+        hi = np.ascontiguousarray(alt_hi, dtype=np.float32)
+        tl = np.ascontiguousarray(tlo, dtype=np.int64)
+        th = np.ascontiguousarray(thi, dtype=np.int64)
+        ow = np.ascontiguousarray(owner, dtype=np.int32) if owner is not None else None
+        need = C.c_int64(0)
+        cap = max(1024, nq * 8)
+        while True:
+            oq = np.zeros(cap, dtype=np.uint32)
+            oe = np.zeros(cap, dtype=np.uint32)
+            rc = self.ctx.L.dssg_store_search(
+                self.ctx.h, self.h, nq, _p(q_offs, C.c_int64), _p(q_cells, C.c_uint64), _p(lo, C.c_float),
+                _p(hi, C.c_float), _p(tl, C.c_int64), _p(th, C.c_int64),
+                _p(ow, C.c_int32) if ow is not None else C.POINTER(C.c_int32)(), _p(oq, C.c_uint32),
+                _p(oe, C.c_uint32), cap, C.byref(need))
+            if rc == _lib.DSSG_ERR_CAPACITY:
+                cap = int(need.value) + 1
+                continue
+            self.ctx.check(rc)
+            return oq[: need.value].copy(), oe[: need.value].copy()
+
+
+class NotFound(LookupError):
+    """dsserr.NotFound -> codes.NotFound."""
+
+
+class AlreadyExists(ValueError):
+    """dsserr.AlreadyExists -> codes.AlreadyExists."""
+
+
+class VersionMismatch(ValueError):
+    """dsserr.VersionMismatch -> codes.Aborted."""
+
+
+class PermissionDenied(PermissionError):
+    """dsserr.PermissionDenied -> codes.PermissionDenied."""
+
+
+class MissingOVNs(RuntimeError):
+    """scderr.MissingOVNsInternalError: the key lacks the OVN of a conflicting
+    operation; `missing` lists those operations' ids."""
+
+    def __init__(self, missing):
+        super().__init__("missing OVNs")
+        self.missing = missing
+
+
+def ovn_from_time(updated_at_rfc3339: str, salt: str) -> str:
+    """NewOVNFromTime (pkg/scd/models/models.go:35-40):
+    base64(sha256(salt + t.Format(RFC3339)))."""
+    import base64
+    import hashlib
+    return base64.b64encode(hashlib.sha256((salt + updated_at_rfc3339).encode()).digest()).decode()
+
+
+class Operation:
+    """The scdmodels.Operation fields the write path reads (pkg/scd/models/
+    operations.go:27-45); times are int64 us, None = NULL."""
+
+    def __init__(self, id, owner, cells, altitude_lower=None, altitude_upper=None, start=None, end=None,
+                 state="Accepted", version=0):
+        self.ID, self.Owner, self.Cells = id, owner, list(cells)
+        self.AltitudeLower, self.AltitudeUpper = altitude_lower, altitude_upper
+        self.StartTime, self.EndTime = start, end
+        self.State, self.Version = state, version
+        self.OVN = ""
+        self.UpdatedAt = None
+
+
+class MutableOperationStore:
+    """scdstore.OperationStore's write path over a GPU `Store`:
+    UpsertOperation (pkg/scd/store/cockroach/operations.go:304-372),
+    DeleteOperation (:239-301), SearchOperations (:374-445).  Rows and OVNs
+    live here (host); cells + the 4D attributes live in the GPU store.
+    Owners are strings here and small ints on the GPU (interned)."""
+
+    def __init__(self, device: int = 0):
+        self.gpu = Store(with_owner=False, device=device)
+        self.ops = {}      # id -> Operation
+        self.slot = {}     # id -> uint32 GPU id
+        self.by_slot = {}  # GPU id -> op id
+        self._next = 0
+
+    def _slot_of(self, op_id):
+        if op_id not in self.slot:
+            self.slot[op_id] = self._next
+            self.by_slot[self._next] = op_id
+            self._next += 1
+        return self.slot[op_id]
+
+    def SearchOperations(self, cells, alt_lo, alt_hi, start, end, now_us) -> List["Operation"]:
+        """searchOperations over already-covered cells (the store-internal
+        GeometryFunc path, operations.go:337-348)."""
+        if len(cells) == 0:
+            raise BadRequest("missing cell IDs for query")
+        offs, cc = _csr([cells])
+        tlo = max(NULL_START if start is None else start, now_us)
+        thi = NULL_END_Q if end is None else end
+        _, ids = self.gpu.search_batch(offs, cc, [_f32_or(alt_lo, -np.inf)], [_f32_or(alt_hi, np.inf)], [tlo], [thi])
+        return [self.ops[self.by_slot[int(i)]] for i in ids]
+
+    def UpsertOperation(self, op: "Operation", key: Sequence[str], now_us: int, now_rfc3339: str):
+        old = self.ops.get(op.ID)
+        if old is None and op.Version != 0:
+            raise NotFound(op.ID)
+        if old is not None and op.Version == 0:
+            raise AlreadyExists(op.ID)
+        if old is not None and op.Version != old.Version:
+            raise VersionMismatch("old version")
+        if old is not None and old.Owner != op.Owner:
+            raise PermissionDenied(f"Operation is owned by {old.Owner}")
+        # ValidateTimeRange (pkg/scd/models/operations.go:78-94)
+        if op.StartTime is None:
+            raise BadRequest("Operation must have an time_start")
+        if op.EndTime is None:
+            raise BadRequest("Operation must have an time_end")
+        if op.EndTime < op.StartTime:
+            raise BadRequest("Operation time_end must be after time_start")
+        if op.State in ("Accepted", "Activated"):
+            keyset = set(key)
+            found = self.SearchOperations(op.Cells, op.AltitudeLower, op.AltitudeUpper, op.StartTime, op.EndTime,
+                                          now_us)
+            missing = [o.ID for o in found if o.OVN not in keyset]
+            if missing:
+                raise MissingOVNs(missing)
+        # pushOperation: version + 1, updated_at = transaction time, cells replaced
+        op.Version = (old.Version if old is not None else 0) + 1
+        op.UpdatedAt = now_rfc3339
+        op.OVN = ovn_from_time(now_rfc3339, op.ID)
+        s = self._slot_of(op.ID)
+        self.gpu.upsert([s], [op.Cells], [_f32_or(op.AltitudeLower, -np.inf)], [_f32_or(op.AltitudeUpper, np.inf)],
+                        [op.StartTime], [op.EndTime])
+        self.ops[op.ID] = op
+        return op
+
+    def DeleteOperation(self, op_id, owner):
+        old = self.ops.get(op_id)
+        if old is None:
+            raise NotFound(op_id)
+        if old.Owner != owner:
+            raise PermissionDenied(f"Operation is owned by {old.Owner}")
+        self.gpu.delete([self.slot[op_id]])
+        del self.ops[op_id]
+        return old

@@ -180,6 +180,36 @@ int dssg_search_subscriptions(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, 
                               const uint64_t *q_cells, const int32_t *owner, int64_t now_us, uint32_t *out_q,
                               uint32_t *out_e, int64_t cap, int64_t *needed);
 
+/* ---- write path: a mutable store over the index --
+ * Replaces the row + posting rewrites of UpsertOperation / pushOperation /
+ * DeleteOperation (pkg/scd/store/cockroach/operations.go:119-193, 239-372)
+ * and RID InsertISA / DeleteISA (pkg/rid/cockroach/
+ * identification_service_area.go:97-160): entities are keyed by a caller id
+ * (uint32, the Go side's row handle; 0xffffffff reserved).  Upsert replaces an
+ * id's cells and attributes (or inserts it); delete removes it (found[i] = 0
+ * if it was not live).  Every later search sees every earlier write.  Inside:
+ * an immutable base index, a delta index over the entities written since the
+ * base was built (rebuilt per write batch), and a tombstone bitmap that masks
+ * the base copies of rewritten/deleted ids in the join; the delta is folded
+ * into a new base once it exceeds max(4096, base / 16) entities, or on
+ * dssg_store_compact.  Writes must be serialised by the caller (the Go
+ * store's transaction); dssg_store_search returns (query, id) pairs sorted.
+ * The SCD OVN conflict check of UpsertOperation (operations.go:333-360) is
+ * this search with the operation's own volume, minus the ids whose OVN the
+ * caller's key holds (dss_amd.store.MutableOperationStore). */
+typedef struct dssg_store dssg_store;
+int dssg_store_create(dssg_ctx *ctx, int32_t with_owner, dssg_store **out);
+void dssg_store_free(dssg_store *st);
+int dssg_store_upsert(dssg_ctx *ctx, dssg_store *st, int64_t n, const uint32_t *ids, const int64_t *cell_offs,
+                      const uint64_t *cells, const float *alt_lo, const float *alt_hi, const int64_t *t0,
+                      const int64_t *t1, const int32_t *owner);
+int dssg_store_delete(dssg_ctx *ctx, dssg_store *st, int64_t n, const uint32_t *ids, int32_t *found);
+int dssg_store_compact(dssg_ctx *ctx, dssg_store *st);
+int dssg_store_stats(const dssg_store *st, int64_t *live, int64_t *base, int64_t *delta, int64_t *compactions);
+int dssg_store_search(dssg_ctx *ctx, dssg_store *st, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
+                      const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
+                      const int32_t *q_owner, uint32_t *out_q, uint32_t *out_id, int64_t cap, int64_t *needed);
+
 /* ---- subscription-store queries -----------------------------------------
  * Notification fan-out: RID UpdateNotificationIdxsInCells
  * (pkg/rid/cockroach/subscriptions.go:204-219) and SCD

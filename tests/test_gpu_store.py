@@ -1,0 +1,142 @@
+"""GPU write path: a mutable store over the index.
+
+Random upsert / delete / insert batches, with and without compaction, each
+followed by a search whose pair set must equal the oracle's search over the
+live rows; then the reference's UpsertOperation / DeleteOperation semantics
+(pkg/scd/store/cockroach/operations.go:239-372): NotFound, AlreadyExists,
+VersionMismatch, PermissionDenied, ValidateTimeRange and the OVN conflict
+check (MissingOVNs)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _keys(q, e):
+    return np.sort((np.asarray(q, np.uint64) << np.uint64(32)) | np.asarray(e, np.uint64))
+
+
+class Model:
+    """Host copy of the live rows (test bookkeeping)."""
+
+    def __init__(self):
+        self.rows = {}
+
+    def upsert(self, ids, cells, lo, hi, t0, t1):
+        for k, i in enumerate(ids):
+            self.rows[int(i)] = (list(cells[k]), lo[k], hi[k], t0[k], t1[k])
+
+    def delete(self, ids):
+        for i in ids:
+            self.rows.pop(int(i), None)
+
+    def oracle_pairs(self, oracle, q_offs, q_cells, qa_lo, qa_hi, tlo, thi):
+        ids = sorted(self.rows)
+        offs = np.zeros(len(ids) + 1, np.int64)
+        offs[1:] = np.cumsum([len(self.rows[i][0]) for i in ids])
+        cells = np.array([c for i in ids for c in self.rows[i][0]], np.uint64)
+        col = lambda k, t: np.array([self.rows[i][k] for i in ids], t)  # noqa: E731
+        oq, oe = oracle.search(offs, cells, col(1, np.float32), col(2, np.float32), col(3, np.int64),
+                               col(4, np.int64), None, q_offs, q_cells, qa_lo, qa_hi, tlo, thi)
+        return _keys(oq, np.array(ids, np.uint32)[oe] if len(oe) else oe)
+
+
+def _lists(offs, cells):
+    return [cells[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+
+
+def test_store_random_writes_against_oracle(oracle):
+    from dss_amd import geo, workload as W
+    from dss_amd.store import Store
+    rng = np.random.default_rng(3)
+    _, q, qa, it, ia, now = W.config(0, scale=0.06)      # 600 queries, 6000 intents
+    ci = geo.cover_batch(it.kind, it.voff, it.lat, it.lng, it.radius_m)
+    cq = geo.cover_batch(q.kind, q.voff, q.lat, q.lng, q.radius_m)
+    tlo, thi = W.query_bounds(qa, now)
+    lists = _lists(ci.offs, ci.cells)
+    n = it.n
+    st, model = Store(), Model()
+
+    def check():
+        gq, gid = st.search_batch(cq.offs, cq.cells, qa.alt_lo, qa.alt_hi, tlo, thi)
+        want = model.oracle_pairs(oracle, cq.offs, cq.cells, qa.alt_lo, qa.alt_hi, tlo, thi)
+        assert len(want) > 0
+        assert np.array_equal(_keys(gq, gid), want)
+
+    first = np.arange(0, n // 2, dtype=np.uint32)       # ids 0..2999, all in the delta
+    args = ([lists[i] for i in first], ia.alt_lo[first], ia.alt_hi[first], ia.t0[first], ia.t1[first])
+    st.upsert(first, *args)
+    model.upsert(first, *args)
+    assert st.stats()["delta"] == len(first) and st.stats()["base"] == 0
+    check()
+    st.compact()
+    assert st.stats()["base"] == len(first) and st.stats()["delta"] == 0
+    check()
+    for rnd in range(3):
+        # rewrite some rows with other footprints / times, delete some, insert new ids
+        upd = rng.choice(n // 2, 300, replace=False).astype(np.uint32)
+        src = rng.choice(n, 300, replace=False)
+        a = ([lists[j] for j in src], ia.alt_lo[src], ia.alt_hi[src], ia.t0[src], ia.t1[src])
+        st.upsert(upd, *a)
+        model.upsert(upd, *a)
+        dele = rng.choice(n // 2, 100, replace=False).astype(np.uint32)
+        found = st.delete(dele)
+        assert found.tolist() == [int(d) in model.rows for d in dele]
+        model.delete(dele)
+        new = np.arange(n // 2 + 200 * rnd, n // 2 + 200 * (rnd + 1), dtype=np.uint32)
+        a = ([lists[j] for j in new], ia.alt_lo[new], ia.alt_hi[new], ia.t0[new], ia.t1[new])
+        st.upsert(new, *a)
+        model.upsert(new, *a)
+        assert st.stats()["live"] == len(model.rows)
+        check()
+    # a batch bigger than the delta limit folds everything into a new base
+    big = np.arange(0, n, dtype=np.uint32)[::-1].copy()
+    a = ([lists[j] for j in big], ia.alt_lo[big], ia.alt_hi[big], ia.t0[big], ia.t1[big])
+    c0 = st.stats()["compactions"]
+    st.upsert(big, *a)
+    model.upsert(big, *a)
+    assert st.stats()["compactions"] == c0 + 1 and st.stats()["delta"] == 0
+    check()
+    assert st.delete([10**6]).tolist() == [False]
+
+
+def test_operation_write_path_semantics():
+    from dss_amd.store import (AlreadyExists, BadRequest, MissingOVNs, MutableOperationStore, NotFound, Operation,
+                               PermissionDenied, VersionMismatch)
+    T = 1_700_000_000_000_000
+    H = 3600 * 10**6
+    cells = [0x808fb0ac00000000, 0x808fb74400000000]
+    s = MutableOperationStore()
+    a = s.UpsertOperation(Operation("op-a", "uss1", cells, 0.0, 100.0, T, T + H), [], T, "2023-11-14T22:13:20Z")
+    assert a.Version == 1 and a.OVN
+    with pytest.raises(AlreadyExists):
+        s.UpsertOperation(Operation("op-a", "uss1", cells, 0.0, 100.0, T, T + H), [], T, "2023-11-14T22:13:21Z")
+    with pytest.raises(NotFound):
+        s.UpsertOperation(Operation("op-x", "uss1", cells, 0.0, 100.0, T, T + H, version=3), [], T, "z")
+    with pytest.raises(VersionMismatch):
+        s.UpsertOperation(Operation("op-a", "uss1", cells, 0.0, 100.0, T, T + H, version=7), [a.OVN], T, "z")
+    with pytest.raises(PermissionDenied):
+        s.UpsertOperation(Operation("op-a", "uss2", cells, 0.0, 100.0, T, T + H, version=1), [a.OVN], T, "z")
+    with pytest.raises(BadRequest):
+        s.UpsertOperation(Operation("op-b", "uss2", cells, 0.0, 100.0, T + H, T), [], T, "z")
+    # op-b overlaps op-a in 4D: its key must hold op-a's OVN
+    with pytest.raises(MissingOVNs) as e:
+        s.UpsertOperation(Operation("op-b", "uss2", cells[1:], 50.0, 150.0, T, T + H), [], T, "2023-11-14T22:13:22Z")
+    assert e.value.missing == ["op-a"]
+    b = s.UpsertOperation(Operation("op-b", "uss2", cells[1:], 50.0, 150.0, T, T + H), [a.OVN], T,
+                          "2023-11-14T22:13:22Z")
+    # disjoint altitude: no conflict; non-Accepted/Activated states skip the check
+    s.UpsertOperation(Operation("op-c", "uss3", cells, 500.0, 600.0, T, T + H), [], T, "2023-11-14T22:13:23Z")
+    s.UpsertOperation(Operation("op-d", "uss3", cells, 0.0, 100.0, T, T + H, state="Ended"), [], T, "q")
+    # an update of op-a sees op-b (and itself) as conflicts unless keyed
+    with pytest.raises(MissingOVNs) as e:
+        s.UpsertOperation(Operation("op-a", "uss1", cells, 0.0, 100.0, T, T + H, version=1), [a.OVN], T, "w")
+    assert sorted(e.value.missing) == ["op-b", "op-d"]
+    with pytest.raises(PermissionDenied):
+        s.DeleteOperation("op-b", "uss1")
+    s.DeleteOperation("op-b", "uss2")
+    with pytest.raises(NotFound):
+        s.DeleteOperation("op-b", "uss2")
+    found = {o.ID for o in s.SearchOperations(cells, 0.0, 100.0, T, T + H, T)}
+    assert found == {"op-a", "op-d"}
+    assert b.Version == 1
