@@ -57,6 +57,13 @@ MAX_PARTS = 64
 ROUTE_ROW_BYTES = 32
 
 
+class Volumes(C.Structure):
+    """dssg_volumes: UnionVolumes4D results (device)."""
+    _fields_ = [("n", C.c_int64), ("offs", C.c_void_p), ("cells", C.c_void_p), ("status", C.c_void_p),
+                ("area_km2", C.c_void_p), ("alt_lo", C.c_void_p), ("alt_hi", C.c_void_p), ("t0", C.c_void_p),
+                ("t1", C.c_void_p), ("has_footprint", C.c_void_p), ("total_cells", C.c_int64)]
+
+
 class Batch(C.Structure):
     """dssg_batch: a received (unpacked) query batch."""
     _fields_ = [("n", C.c_int64), ("offs", C.c_void_p), ("cells", C.c_void_p), ("alt_lo", C.c_void_p),
@@ -119,6 +126,7 @@ def load():
         L.dssg_search_isas.argtypes = [vp, vp, i64, P(i64), P(u64), P(i64), P(i64), P(u32), P(u32), i64, P(i64)]
         L.dssg_search_subscriptions.argtypes = [vp, vp, i64, P(i64), P(u64), P(i32), i64, P(u32), P(u32), i64,
                                                 P(i64)]
+        L.dssg_union_volumes_device.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, P(Volumes)]
         L.dssg_store_create.argtypes = [vp, i32, P(vp)]
         L.dssg_store_free.argtypes = [vp]
         L.dssg_store_free.restype = None

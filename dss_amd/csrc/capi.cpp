@@ -12,6 +12,7 @@
 
 #include "common.hpp"
 #include "cover.hpp"
+#include "ingress.hpp"
 #include "route.hpp"
 #include "search.hpp"
 #include "store.hpp"
@@ -24,6 +25,7 @@ struct dssg_ctx {
     dss::SearchEngine search;
     dss::RouteEngine route;
     dss::SubsEngine subs;
+    dss::IngressEngine ingress;
     std::string last_error;
     bool timing = false;
     double cover_ms = 0, join_ms = 0;
@@ -304,6 +306,28 @@ int dssg_cover_batch(dssg_ctx *ctx, int64_t n, const int32_t *kind, const int64_
         if (res.total_cells > cells_cap) code = DSSG_ERR_CAPACITY;
     });
     return rc ? rc : code;
+}
+
+int dssg_union_volumes_device(dssg_ctx *ctx, int64_t nvol, const int64_t *d_vol_offs, const int32_t *d_kind,
+                              const int64_t *d_voff, const double *d_lat, const double *d_lng, const float *d_radius_m,
+                              const uint8_t *d_has_fp, const float *d_alt_lo, const float *d_alt_hi,
+                              const int64_t *d_t0, const int64_t *d_t1, void *stream, dssg_volumes *out)
+{
+    if (!ctx || !out || nvol < 0 || (nvol > 0 && !d_vol_offs)) return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        int64_t nx = 0;
+        if (nvol > 0) {
+            DSS_HIP(hipMemcpyAsync(&nx, d_vol_offs + nvol, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+            DSS_HIP(hipStreamSynchronize(s));
+        }
+        if (nx < 0) throw dss::Error(DSSG_ERR_INVALID, "vol_offs must ascend from 0");
+        if (nx > 0 && (!d_kind || !d_voff || !d_lat || !d_lng || !d_radius_m || !d_has_fp || !d_alt_lo || !d_alt_hi ||
+                       !d_t0 || !d_t1))
+            throw dss::Error(DSSG_ERR_INVALID, "extent arrays are NULL");
+        ctx->ingress.union_volumes(ctx->cover, nvol, d_vol_offs, nx, d_kind, d_voff, d_lat, d_lng, d_radius_m, d_has_fp,
+                                   d_alt_lo, d_alt_hi, d_t0, d_t1, s, out);
+    });
 }
 
 int dssg_area_to_cell_ids(dssg_ctx *ctx, const char *area, uint64_t *out_cells, int64_t cap, int64_t *needed,

@@ -288,3 +288,81 @@ def Levelify(cells: Sequence[int]) -> List[int]:
             first = c - lsb + lsb13
             out.extend(first + k * (lsb13 << 1) for k in range(4 ** (13 - level)))
     return out
+
+
+def UnionVolumes4DBatch(requests: Sequence[Sequence[Volume4D]], device: int = 0) -> list:
+    """models.UnionVolumes4D (pkg/models/geo.go:126-190) for a batch of
+    requests on the GPU (dssg_union_volumes_device): one cover launch for
+    every extent of every request, then a per-request union of the cells.
+    Returns, per request, the GeoError UnionVolumes4D would return or the
+    union Volume4D (its Footprint the union cell set, sorted).  Footprints
+    must be GeoPolygon / GeoCircle (GeometryFunc cells are already covered)."""
+    import torch  # plumbing: device buffers
+    from . import device as D
+    vol_offs, kinds, voff, lat, lng, rad, has_fp, alo, ahi, t0, t1, spatial = [0], [], [0], [], [], [], [], [], [], [], [], []
+    for req in requests:
+        sp = False
+        for v in req:
+            sv = v.SpatialVolume
+            sp = sp or sv is not None
+            fp = sv.Footprint if sv is not None else None
+            if isinstance(fp, GeoPolygon):
+                kinds.append(KIND_POLYGON)
+                lat += [p.Lat for p in fp.Vertices]
+                lng += [p.Lng for p in fp.Vertices]
+                rad.append(0.0)
+            elif isinstance(fp, GeoCircle):
+                kinds.append(KIND_CIRCLE)
+                lat.append(fp.Center.Lat)
+                lng.append(fp.Center.Lng)
+                rad.append(float(np.float32(fp.RadiusMeter)))
+            elif fp is None:
+                kinds.append(KIND_POINTS)  # no vertices; ignored (has_fp = 0)
+                rad.append(0.0)
+            else:
+                raise TypeError("UnionVolumes4DBatch: footprints must be GeoPolygon or GeoCircle")
+            voff.append(len(lat))
+            has_fp.append(1 if fp is not None else 0)
+            alo.append(np.nan if sv is None or sv.AltitudeLo is None else np.float32(sv.AltitudeLo))
+            ahi.append(np.nan if sv is None or sv.AltitudeHi is None else np.float32(sv.AltitudeHi))
+            t0.append(_lib.TIME_NULL_START if v.StartTime is None else v.StartTime)
+            t1.append(_lib.TIME_NULL_END_Q if v.EndTime is None else v.EndTime)
+        vol_offs.append(len(kinds))
+        spatial.append(sp)
+    ctx = _lib.context(device)
+    dev = f"cuda:{device}"
+    t = lambda a, dt: torch.as_tensor(np.asarray(a, dtype=dt) if len(a) else np.zeros(1, dt), device=dev)  # noqa: E731
+    bufs = [t(vol_offs, np.int64), t(kinds, np.int32), t(voff, np.int64), t(lat, np.float64), t(lng, np.float64),
+            t(rad, np.float32), t(has_fp, np.uint8), t(alo, np.float32), t(ahi, np.float32), t(t0, np.int64),
+            t(t1, np.int64)]
+    out = _lib.Volumes()
+    ctx.check(ctx.L.dssg_union_volumes_device(ctx.h, len(requests), *[D._ptr(b) for b in bufs], D._stream_ptr(),
+                                              C.byref(out)))
+    n = len(requests)
+    offs = D.copy_back(ctx, out.offs, n + 1, np.int64)
+    cells = D.copy_back(ctx, out.cells, int(offs[-1]), np.uint64)
+    st = D.copy_back(ctx, out.status, n, np.int32)
+    area = D.copy_back(ctx, out.area_km2, n, np.float64)
+    lo = D.copy_back(ctx, out.alt_lo, n, np.float32)
+    hi = D.copy_back(ctx, out.alt_hi, n, np.float32)
+    s0 = D.copy_back(ctx, out.t0, n, np.int64)
+    s1 = D.copy_back(ctx, out.t1, n, np.int64)
+    fp = D.copy_back(ctx, out.has_footprint, n, np.uint8)
+    res = []
+    for i in range(n):
+        err = error_for_status(int(st[i]), float(area[i]))
+        if err is not None:
+            res.append(err)
+            continue
+        v = Volume4D(StartTime=None if s0[i] == _lib.TIME_NULL_START else int(s0[i]),
+                     EndTime=None if s1[i] == _lib.TIME_NULL_END_Q else int(s1[i]))
+        if spatial[i]:
+            v.SpatialVolume = Volume3D(AltitudeLo=None if np.isnan(lo[i]) else float(lo[i]),
+                                       AltitudeHi=None if np.isnan(hi[i]) else float(hi[i]))
+            if fp[i]:
+                g = _PrecomputedCellGeometry()
+                for c in cells[offs[i]:offs[i + 1]]:
+                    g[int(c)] = None
+                v.SpatialVolume.Footprint = g
+        res.append(v)
+    return res

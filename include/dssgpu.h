@@ -115,6 +115,33 @@ int dssg_cover_batch_device(dssg_ctx *ctx, int64_t n, const int32_t *d_kind, con
 int dssg_area_to_cell_ids(dssg_ctx *ctx, const char *area, uint64_t *out_cells, int64_t cap, int64_t *needed,
                           int32_t *status, double *area_km2);
 
+/* ---- batched ingress: models.UnionVolumes4D (pkg/models/geo.go:126-190) --
+ * A batch of multi-extent volumes: extents [vol_offs[v], vol_offs[v+1]) form
+ * volume v (vol_offs on device for the _device form).  Extent x: footprint as
+ * dssg_cover_batch (kind/voff/lat/lng/radius_m) iff has_fp[x] != 0; altitudes
+ * NaN = NULL; t0 = DSSG_TIME_NULL_START / t1 = DSSG_TIME_NULL_END_Q = NULL.
+ * Per volume: the union of the extents' coverings (sorted, unique; the
+ * reference's map order is unspecified, Q14), min start / max end / min
+ * altitude_lower / max altitude_upper over the extents carrying them (NULL if
+ * none), has_footprint, and the first covering error in extent order (status
+ * DSSG_ST_*, area_km2 for DSSG_ST_AREA_TOO_LARGE), where UnionVolumes4D would
+ * return that error. */
+typedef struct {
+    int64_t n;                 /* volumes */
+    const int64_t *offs;       /* device, n+1 */
+    const uint64_t *cells;     /* device, union cells per volume, sorted */
+    const int32_t *status;     /* device, n */
+    const double *area_km2;    /* device, n */
+    const float *alt_lo, *alt_hi;  /* device, n (NaN = NULL) */
+    const int64_t *t0, *t1;    /* device, n (NULL sentinels as above) */
+    const uint8_t *has_footprint;  /* device, n */
+    int64_t total_cells;
+} dssg_volumes;
+int dssg_union_volumes_device(dssg_ctx *ctx, int64_t nvol, const int64_t *d_vol_offs, const int32_t *d_kind,
+                              const int64_t *d_voff, const double *d_lat, const double *d_lng, const float *d_radius_m,
+                              const uint8_t *d_has_fp, const float *d_alt_lo, const float *d_alt_hi,
+                              const int64_t *d_t0, const int64_t *d_t1, void *stream, dssg_volumes *out);
+
 /* ---- entity index (intents / ISAs / subscriptions) ----------------------
  * Replaces the CRDB tables scd_operations + scd_cells_operations
  * (pkg/scd/store/cockroach/store.go:120-147) and the RID INT64[] cells
