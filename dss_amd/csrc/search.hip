@@ -528,12 +528,24 @@ __global__ void k_gbounds(int64_t nkeys, const uint32_t *skey, uint32_t *gbeg, u
 #endif
 constexpr int kSlots = DSS_JOIN_SLOTS;
 
-// (2) join units: (group, tile of <= 64 * kSlots postings, kQChunk-record
-// chunk), one thread per group of the index.  u_pt = tile | (slots - 1) << 28.
-// The unit count stays on the device (uoff[ng]); the persistent join reads it.
+// Join unit: (group, tile of <= 64 * kSlots postings, chunk of <= kQChunk
+// records), described in 32 bytes so the join reads it with one scalar load.
+struct alignas(16) UnitDesc {
+    uint32_t p0;     // first posting of the tile
+    uint32_t pe;     // end of the group's postings
+    uint32_t k0, k1; // the unit's record range in the sorted keys
+    uint64_t key;    // group key: slot << 6 | bucket
+    uint32_t nslot;  // postings per lane (1..kSlots)
+    uint32_t pad;
+};
+static_assert(sizeof(UnitDesc) == 32, "UnitDesc layout");
+
+// (2) join units, one thread per group of the index; PASS 0 counts, PASS 1
+// writes the descriptors at uoff[g].  The unit count stays on the device
+// (uoff[ng]); the persistent join reads it.
 template <int PASS>
-__global__ void k_units(int64_t ng, const uint32_t *bk_start, const uint32_t *gbeg, const uint32_t *gend, int64_t *cnt,
-                        const int64_t *uoff, uint32_t *u_grp, uint32_t *u_pt, uint32_t *u_qt)
+__global__ void k_units(int64_t ng, const uint32_t *bk_start, const uint32_t *gbeg, const uint32_t *gend,
+                        const uint64_t *g_key, int64_t *cnt, const int64_t *uoff, UnitDesc *units)
 {
     const int64_t g = tid64();
     if (g >= ng) return;
@@ -548,9 +560,15 @@ __global__ void k_units(int64_t ng, const uint32_t *bk_start, const uint32_t *gb
     int64_t w = uoff[g];
     for (int64_t i = 0; i < tp; i++)
         for (int64_t j = 0; j < tq; j++, w++) {
-            u_grp[w] = (uint32_t)g;
-            u_pt[w] = (uint32_t)i | (uint32_t)(k - 1) << 28;
-            u_qt[w] = (uint32_t)j;
+            UnitDesc d;
+            d.p0 = bk_start[g] + (uint32_t)(i * 64 * k);
+            d.pe = bk_start[g + 1];
+            d.k0 = gbeg[g] + (uint32_t)(j * kQChunk);
+            d.k1 = (uint32_t)min((int64_t)gend[g], (int64_t)d.k0 + kQChunk);
+            d.key = g_key[g];
+            d.nslot = (uint32_t)k;
+            d.pad = 0;
+            units[w] = d;
         }
 }
 
@@ -581,15 +599,6 @@ __global__ void k_work_stats(int64_t ng, const uint32_t *bk_start, const uint32_
         atomicAdd(&stat[2], met);
     }
 }
-
-// Unit queue: same-address atomics serialise at one L2 channel
-// (MI355X_MICROARCH.md "dequeue"), so the queue has kQShards heads, each over
-// a contiguous range of the unit list; a wave starts on head blockIdx %
-// kQShards (blocks b and b + 8 share an XCD -- speed only) and then steals.
-#ifndef DSS_JOIN_QSHARDS
-#define DSS_JOIN_QSHARDS 1
-#endif
-constexpr int kQShards = DSS_JOIN_QSHARDS;
 
 struct JoinArgs {
     IndexView ix;
@@ -642,13 +651,62 @@ __device__ __forceinline__ void load_slot(const IndexView &ix, uint32_t p, uint3
     }
 }
 
+// A lane's posting as loaded (software pipeline: loads issued one unit
+// ahead, decoded when the unit starts).
+struct RawSlot {
+    uint32_t v;
+    uint32_t m;
+    float2 alt;
+    longlong2 t;
+    int32_t own;
+    ulonglong2 s01, s23;
+    bool valid;
+};
+
+__device__ __forceinline__ void load_raw(const IndexView &ix, uint32_t p, uint32_t pe, bool owner, RawSlot &r)
+{
+    r.valid = p < pe;
+    if (!r.valid) return;
+    r.v = ix.b_e[p];
+    r.m = ix.b_meta[p];
+    r.alt = ix.b_alt[p];
+    r.t = ix.b_t[p];
+    if (owner) r.own = ix.b_owner[p];
+    r.s01 = ix.b_sig[2 * (size_t)p];  // loaded for first postings too: no wait on b_e here
+    r.s23 = ix.b_sig[2 * (size_t)p + 1];
+}
+
+__device__ __forceinline__ void decode_raw(const IndexView &ix, const RawSlot &r, bool owner, Slot &s)
+{
+    s.valid = r.valid && !is_dead(ix, r.v & ~kFirstBit);  // tombstoned (write path): matches nothing
+    s.first = s.compact = false;
+    s.ent = 0;
+    s.be0 = 0;
+    s.alt = make_float2(INFINITY, -INFINITY);    // matches nothing
+    s.t = make_longlong2(LLONG_MAX, LLONG_MIN);  // matches nothing
+    s.own = 0;
+    s.s01 = s.s23 = make_ulonglong2(0, 0);
+    if (!s.valid) return;
+    s.ent = r.v & ~kFirstBit;
+    s.first = (r.v & kFirstBit) != 0;
+    s.be0 = (int)(r.m & 0x3f);
+    s.compact = (r.m & 0x80) != 0;
+    s.alt = r.alt;
+    s.t = r.t;
+    if (owner) s.own = r.own;
+    if (!s.first) {
+        s.s01 = r.s01;
+        s.s23 = r.s23;
+    }
+}
+
 // (3) one wavefront per unit: up to 64 * kSlots postings in registers, the
 // unit's query records staged through LDS 64 at a time and broadcast.
 template <bool OWNER>
 __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, const QRec *__restrict__ recs,
                                                       const uint32_t *__restrict__ sval,
-                                                      const int32_t *__restrict__ rown, const uint32_t *__restrict__ u_run,
-                                                      const uint32_t *__restrict__ u_pt, const uint32_t *__restrict__ u_qt,
+                                                      const int32_t *__restrict__ rown,
+                                                      const UnitDesc *__restrict__ units,
                                                       uint32_t *__restrict__ out_q, uint32_t *__restrict__ out_e,
                                                       uint32_t *__restrict__ work)
 {
@@ -661,7 +719,6 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int staged = 0;
-    const int shard = (int)(blockIdx.x & (kQShards - 1));
     auto flush = [&]() {
         __builtin_amdgcn_wave_barrier();
 #if DSS_JOIN_EXPERIMENT == 1  // timing experiment: drop the pairs
@@ -671,7 +728,7 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
         if (lane == 0 && staged) {
             base = atomicAdd(a.counter, (unsigned long long)staged);
 #if DSS_JOIN_DIAG
-            atomicAdd(&work[kQShards], 1u);  // diagnostics: flushes
+            atomicAdd(&work[1], 1u);  // diagnostics: flushes
 #endif
         }
         base = __shfl(base, 0);
@@ -686,34 +743,48 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
         __builtin_amdgcn_wave_barrier();
     };
     const IndexView &ix = a.ix;
-    // persistent waves: grab kGrab units at a time from this shard's range of
-    // the unit list, then from the other shards' (stealing) until all drain;
-    // the staging buffer carries over between units
+    const int4 *rec4 = reinterpret_cast<const int4 *>(recs);
+    // persistent waves: units come from one queue, kGrab per atomic; the
+    // staging buffer carries over between units.  Software pipeline: the next
+    // unit's descriptor, posting loads and first record indices are issued
+    // before this unit's record gathers, so the two round trips overlap.
     const int64_t nunits = *a.nunits;
-    for (int r = 0; r < kQShards; r++) {
-      const int rs = (shard + r) % kQShards;  // this shard's range, then steal
-      const int64_t rbeg = nunits * rs / kQShards, rend = nunits * (rs + 1) / kQShards;
-      for (;;) {
-        uint32_t ub = 0;
-        if (lane == 0) ub = atomicAdd(&work[rs], (uint32_t)kGrab);
-        ub = __builtin_amdgcn_readfirstlane(__shfl(ub, 0));
-        if (rbeg + (int64_t)ub >= rend) break;
-        const uint32_t ub0 = (uint32_t)(rbeg + ub);
-        const uint32_t ue = (uint32_t)min(rbeg + (int64_t)ub + kGrab, rend);
-        for (uint32_t u = ub0; u < ue; u++) {
-            const uint32_t g = u_run[u];
-            const uint64_t key = a.g_key[g];
-            const int b = (int)(key & 63);
-            const uint32_t gs = ix.bk_start[g], ge = ix.bk_start[g + 1];
-            const uint32_t pt = u_pt[u];
-            const int nslot = (int)(pt >> 28) + 1;
-            const uint32_t p0 = gs + (pt & 0x0fffffffu) * 64u * (uint32_t)nslot + (uint32_t)lane;
-            Slot sl[kSlots];
+    uint32_t ucur = 0, uend = 0;
+    auto next_unit = [&]() -> int64_t {
+        if (ucur >= uend) {
+            uint32_t ub = 0;
+            if (lane == 0) ub = atomicAdd(&work[0], (uint32_t)kGrab);
+            ub = __builtin_amdgcn_readfirstlane(__shfl(ub, 0));
+            if ((int64_t)ub >= nunits) return -1;
+            ucur = ub;
+            uend = (uint32_t)min((int64_t)ub + kGrab, nunits);
+        }
+        return (int64_t)ucur++;
+    };
+    RawSlot raw[kSlots];
+    UnitDesc d{};
+    uint32_t ci_pre = 0;
+    auto prefetch = [&](int64_t un) {
+        d = units[un];
+        const uint32_t p0 = d.p0 + (uint32_t)lane;
 #pragma unroll
-            for (int k = 0; k < kSlots; k++) {
-                if (k < nslot) load_slot(ix, p0 + 64u * k, ge, OWNER, sl[k]);
-                else load_slot(ix, ge, ge, OWNER, sl[k]);
-            }
+        for (int k = 0; k < kSlots; k++) load_raw(ix, k < (int)d.nslot ? p0 + 64u * k : d.pe, d.pe, OWNER, raw[k]);
+        ci_pre = d.k0 + (uint32_t)lane < d.k1 ? sval[d.k0 + lane] : 0u;
+    };
+    int64_t u = next_unit();
+    if (u >= 0) prefetch(u);
+    while (u >= 0) {
+        const UnitDesc cu = d;
+        Slot sl[kSlots];
+#pragma unroll
+        for (int k = 0; k < kSlots; k++) decode_raw(ix, raw[k], OWNER, sl[k]);
+        uint32_t ci_first = ci_pre;
+        const int64_t un = next_unit();
+        if (un >= 0) prefetch(un);
+        {
+            const uint64_t key = cu.key;
+            const int b = (int)(key & 63);
+            const int nslot = (int)cu.nslot;
             // time and altitude bounds of the unit: records whose window or
             // altitude band misses all postings are skipped
             long long tmin = LLONG_MAX, tmax = LLONG_MIN;
@@ -732,9 +803,7 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                 amax = fmaxf(amax, __shfl_xor(amax, o));
             }
             const uint64_t cell = cell_of_slot(ix, (uint32_t)(key >> 6));
-            const int64_t k0 = (int64_t)a.gbeg[g] + (int64_t)u_qt[u] * kQChunk;
-            const int64_t k1 = min((int64_t)a.gend[g], k0 + kQChunk);
-            const int4 *rec4 = reinterpret_cast<const int4 *>(recs);
+            const int64_t k0 = cu.k0, k1 = cu.k1;
             for (int64_t base = k0; base < k1; base += 64) {
                 const int64_t kk = base + lane;
                 bool rel = false;
@@ -742,7 +811,7 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                 int32_t rown_l = -1;
                 __builtin_amdgcn_wave_barrier();
                 if (kk < k1) {
-                    const uint32_t ci = sval[kk];
+                    const uint32_t ci = base == k0 ? ci_first : sval[kk];
                     r0 = rec4[4 * ci];
                     r1 = rec4[4 * ci + 1];
                     s_sig[w][0][lane] = rec4[4 * ci + 2];
@@ -827,8 +896,8 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                                     if (ex) {
 #if DSS_JOIN_DIAG
                                         if (lane == 0) {  // diagnostics: merges (events, lanes)
-                                            atomicAdd(&work[kQShards + 1], 1u);
-                                            atomicAdd(&work[kQShards + 2], (uint32_t)__popcll(ex));
+                                            atomicAdd(&work[2], 1u);
+                                            atomicAdd(&work[3], (uint32_t)__popcll(ex));
                                         }
 #endif
                                         bool drop = false;
@@ -866,9 +935,8 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                 else records(std::integral_constant<int, kSlots>{});
 #endif
             }
-
         }
-      }
+        u = un;
     }
     flush();
 }
@@ -1240,14 +1308,14 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     // (3) join units over all groups; the total stays on the device.  Bound:
     // each group contributes tiles x ceil(records / kQChunk) units.
     int64_t *ucnt = uc_.ensure(ng + 1), *uoff = uo_.ensure(ng + 2);
-    hipLaunchKernelGGL(k_units<0>, dim3(grid_for(ng, kBlock)), dim3(kBlock), 0, s, ng, idx->bk_start.p, gbeg, gend, ucnt,
-                       nullptr, nullptr, nullptr, nullptr);
+    hipLaunchKernelGGL(k_units<0>, dim3(grid_for(ng, kBlock)), dim3(kBlock), 0, s, ng, idx->bk_start.p, gbeg, gend,
+                       idx->g_key.p, ucnt, nullptr, nullptr);
     exclusive_scan_i64(ucnt, uoff, ng, tmp_, s);
     const int64_t ubound = idx->tiles_total + (nkeys / kQChunk + 1) * idx->tiles_max;
     if (ubound >= (int64_t)0xffffffffll - kGrab) throw Error(DSSG_ERR_CAPACITY, "search: too many join units");
-    uint32_t *u_run = ur_.ensure(ubound + 1), *u_pt = up_.ensure(ubound + 1), *u_qt = uq_.ensure(ubound + 1);
-    hipLaunchKernelGGL(k_units<1>, dim3(grid_for(ng, kBlock)), dim3(kBlock), 0, s, ng, idx->bk_start.p, gbeg, gend, nullptr,
-                       uoff, u_run, u_pt, u_qt);
+    UnitDesc *units = (UnitDesc *)units_buf_.ensure(sizeof(UnitDesc) * (ubound + 1));
+    hipLaunchKernelGGL(k_units<1>, dim3(grid_for(ng, kBlock)), dim3(kBlock), 0, s, ng, idx->bk_start.p, gbeg, gend,
+                       idx->g_key.p, nullptr, uoff, units);
     if (timing_) {
         unsigned long long *st = counter_.ensure(8) + 2;
         DSS_HIP(hipMemsetAsync(st, 0, 3 * sizeof(unsigned long long), s));
@@ -1280,23 +1348,21 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         n_cu_ = ncu > 0 ? ncu : 256;
     }
     const unsigned nblocks = (unsigned)n_cu_ * kJoinBlocksPerCU;
-    uint32_t *work = work_.ensure(kQShards + 4);  // [0, kQShards) unit heads, then diagnostics
+    uint32_t *work = work_.ensure(4);  // [0] unit queue head, [1..3] diagnostics
     unsigned long long *counter = counter_.ensure(1);
     ja.counter = counter;
     for (int attempt = 0; attempt < 3; attempt++) {
         uint32_t *oq = oq_.ensure(out_cap_), *oe = oe_.ensure(out_cap_);
         DSS_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned long long), s));
-        DSS_HIP(hipMemsetAsync(work, 0, (kQShards + 4) * sizeof(uint32_t), s));
+        DSS_HIP(hipMemsetAsync(work, 0, 4 * sizeof(uint32_t), s));
         ja.cap = (int64_t)out_cap_;
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
         if (nblocks && q_owner)
             hipLaunchKernelGGL(k_join<true>, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
-                               (const uint32_t *)sval, (const int32_t *)rown, (const uint32_t *)u_run,
-                               (const uint32_t *)u_pt, (const uint32_t *)u_qt, oq, oe, work);
+                               (const uint32_t *)sval, (const int32_t *)rown, (const UnitDesc *)units, oq, oe, work);
         else if (nblocks)
             hipLaunchKernelGGL(k_join<false>, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
-                               (const uint32_t *)sval, (const int32_t *)nullptr, (const uint32_t *)u_run, (const uint32_t *)u_pt,
-                               (const uint32_t *)u_qt, oq, oe, work);
+                               (const uint32_t *)sval, (const int32_t *)nullptr, (const UnitDesc *)units, oq, oe, work);
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
         unsigned long long total = 0;
         DSS_HIP(hipMemcpyAsync(&total, counter, sizeof(total), hipMemcpyDeviceToHost, s));
@@ -1305,11 +1371,11 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             float ms = 0;
             DSS_HIP(hipEventElapsedTime(&ms, ev0_, ev1_));
             join_ms_ = ms;
-            uint32_t hw[kQShards + 4];
+            uint32_t hw[4];
             DSS_HIP(hipMemcpy(hw, work, sizeof(hw), hipMemcpyDeviceToHost));
-            flushes_ = hw[kQShards];
-            merges_ = hw[kQShards + 1];
-            merge_lanes_ = hw[kQShards + 2];
+            flushes_ = hw[1];
+            merges_ = hw[2];
+            merge_lanes_ = hw[3];
         }
         if (total <= out_cap_) {
             out->q = oq;

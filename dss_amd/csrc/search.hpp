@@ -107,6 +107,7 @@ class SearchEngine {
     DevBuf<unsigned char> rec_;
     DevBuf<int32_t> own_;
     DevBuf<uint32_t> work_;
+    DevBuf<unsigned char> units_buf_;  // join unit descriptors
     int n_cu_ = 0;
     size_t out_cap_ = 0;
     bool timing_ = false;
