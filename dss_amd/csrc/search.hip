@@ -30,6 +30,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cmath>
+#include <cstring>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -43,7 +45,11 @@ namespace {
 constexpr unsigned kBlock = 256;
 constexpr int kLongBucket = 63;
 constexpr int kLongSpan = 8;     // entities touching more buckets go to kLongBucket
-constexpr int kMaxBuckets = 61;  // regular buckets 0..nb-1
+#ifndef DSS_MAX_BUCKETS
+#define DSS_MAX_BUCKETS 61
+#endif
+constexpr int kMaxBuckets = DSS_MAX_BUCKETS;  // regular buckets 0..nb-1 (<= 62: bucket 63 is the long one)
+static_assert(kMaxBuckets <= 62, "bucket 63 is reserved");
 constexpr int kWaves = 4;        // join units per workgroup
 constexpr int kQChunk = 1024;    // query records per join unit
 #ifndef DSS_JOIN_EXPERIMENT
@@ -252,24 +258,36 @@ __global__ void k_irr_scatter(int64_t n_irr_p, const uint64_t *cells, const int6
     }
 }
 
-// Time span of the rows that can match (stored NULL ends never do, Q9).
-__global__ void k_time_range(int64_t n, const int64_t *t0, const int64_t *t1, unsigned long long *mm)
+// Time span of the rows that can match (stored NULL ends never do, Q9), and
+// the sum / count of the bounded rows' durations (bucket width, build step 5).
+__global__ void k_time_range(int64_t n, const int64_t *t0, const int64_t *t1, unsigned long long *mm, double *dsum)
 {
-    unsigned long long lo = ~0ull, hi = 0;
+    unsigned long long lo = ~0ull, hi = 0, cnt = 0;
+    double sum = 0;
     for (int64_t e = tid64(); e < n; e += (int64_t)gridDim.x * blockDim.x) {
         long long a = t0[e], b = t1[e];
         if (b == INT64_MIN) continue;
         long long x = a < b ? a : b, y = a < b ? b : a;
-        if (x != INT64_MIN) lo = min(lo, order_key(x));
+        if (x != INT64_MIN) {
+            lo = min(lo, order_key(x));
+            if (y != INT64_MAX) {
+                sum += (double)y - (double)x;
+                cnt++;
+            }
+        }
         hi = max(hi, order_key(y));
     }
     for (int o = 32; o > 0; o >>= 1) {
         lo = min(lo, __shfl_xor(lo, o));
         hi = max(hi, __shfl_xor(hi, o));
+        cnt += __shfl_xor(cnt, o);
+        sum += __shfl_xor(sum, o);
     }
     if ((threadIdx.x & 63) == 0) {
         atomicMin(&mm[0], lo);
         atomicMax(&mm[1], hi);
+        atomicAdd(&mm[2], cnt);
+        atomicAdd(dsum, sum);
     }
 }
 
@@ -1117,17 +1135,26 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
         idx->irr_start.ensure(1);
     }
     const int64_t n_slots = idx->n_dense + idx->n_irr;
-    // (5) time buckets over the span of the rows that can match
+    // (5) time buckets over the span of the rows that can match.  Width: a
+    // power of two >= span / kMaxBuckets and ~ the mean row duration (rounded
+    // in log2): narrower buckets copy each posting into more buckets (more
+    // bytes per join), wider ones put more non-overlapping pairs in a group
+    // (more tests); measured on configs[1]: 36 min 2.47 ms, 72 min 2.08 ms,
+    // 143 min 2.55 ms per join launch, mean intent duration 62 min.
     {
         DevBuf<unsigned long long> mmb;
-        unsigned long long *mm = mmb.ensure(2), hmm[2] = {~0ull, 0ull};
+        unsigned long long *mm = mmb.ensure(4), hmm[4] = {~0ull, 0ull, 0ull, 0ull};
+        double *dsum = (double *)(mm + 3);
         DSS_HIP(hipMemcpyAsync(mm, hmm, sizeof(hmm), hipMemcpyHostToDevice, s));
         if (n) {
             unsigned g = grid_for(n, kBlock);
-            hipLaunchKernelGGL(k_time_range, dim3(g < 1024 ? g : 1024), dim3(kBlock), 0, s, n, t0, t1, mm);
+            hipLaunchKernelGGL(k_time_range, dim3(g < 1024 ? g : 1024), dim3(kBlock), 0, s, n, t0, t1, mm, dsum);
         }
         DSS_HIP(hipMemcpyAsync(hmm, mm, sizeof(hmm), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipStreamSynchronize(s));
+        double dur_sum = 0;
+        std::memcpy(&dur_sum, &hmm[3], sizeof(double));
+        const double mean_dur = hmm[2] ? dur_sum / (double)hmm[2] : 0.0;
         idx->tbase = 0;
         idx->shift = 0;
         idx->nb = 1;
@@ -1137,6 +1164,7 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
             const unsigned long long span = tmax > tmin ? (unsigned long long)tmax - (unsigned long long)tmin : 0;
             int sh = 0;
             while ((span >> sh) >= (unsigned long long)kMaxBuckets) sh++;
+            if (mean_dur >= 2.0) sh = std::max(sh, std::min(62, (int)std::lround(std::log2(mean_dur))));
             idx->tbase = tmin;
             idx->shift = sh;
             idx->nb = (int)(span >> sh) + 1;
