@@ -88,16 +88,9 @@ def main():
 
     # ---------------------------------------------------------------- setup
     t_setup = time.time()
-    rng_i = np.random.default_rng(20201015 + args.config)   # same airspace on every rank
-    cfg_n = {0: (10_000, 100_000), 1: (1_000_000, 1_000_000)}[args.config]
-    nq = max(1, int(cfg_n[0] * args.scale))
-    ni = max(1, int(cfg_n[1] * args.scale))
-    intents = W.metro_footprints(rng_i, ni)
-    ia = W.intent_attrs(rng_i, ni)
-    rng_q = np.random.default_rng(20201015 + args.config + 1000 * (rank + 1))  # rank's query slice
-    queries = W.metro_footprints(rng_q, nq)
-    qa = W.query_attrs(rng_q, nq)
-    now = W.T0_US
+    # same airspace on every rank (config seed), a rank-private query batch
+    queries, qa, intents, ia, now, rid = W.config_split(args.config, rank, args.scale)
+    nq, ni = queries.n, intents.n
     tlo = np.maximum(qa.t0, now)  # operations.go:398-402 COALESCE(ends_at >= start) AND ends_at >= now
     t = lambda a: torch.as_tensor(a, device=dev)  # noqa: E731
     d_int = D.DeviceFootprints.upload(intents, dev)
@@ -215,8 +208,8 @@ def main():
     n_keys, n_units, n_runs, n_iters, n_tests = (C.c_int64() for _ in range(5))
     ctx.check(ctx.L.dssg_search_counters(ctx.h, C.byref(n_keys), C.byref(n_units), C.byref(n_runs), C.byref(n_iters),
                                          C.byref(n_tests)))
-    n_fl, n_mg, n_ml = (C.c_int64() for _ in range(3))
-    ctx.check(ctx.L.dssg_join_events(ctx.h, C.byref(n_fl), C.byref(n_mg), C.byref(n_ml)))
+    n_fl, n_mg, n_ml, n_tg = (C.c_int64() for _ in range(4))
+    ctx.check(ctx.L.dssg_join_events(ctx.h, C.byref(n_fl), C.byref(n_mg), C.byref(n_ml), C.byref(n_tg)))
     c_tot = int(cells.total_cells)
     r_tot = int(pairs.n)
     kern_avg_ms = float(np.mean(kern_ms))
@@ -259,8 +252,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded SURVEY s8(d) generator; no datasets)",
-            "config": {"workload": f"configs[{args.config}]: {nq} query footprints/GPU/step (70% polygon, 30% circle)"
-                                   f" vs {ni}-intent resident index, SF-Bay metro, S2 level 13",
+            "config": {"workload": f"configs[{args.config}]: {nq} query footprints/GPU/step vs {ni}-entity resident "
+                                   f"index, {W.CONFIG_NAMES[args.config]}, S2 level 13"
+                                   + (" (SearchISAs semantics)" if rid else ""),
                        "queries_per_gpu_step": nq, "intents": ni, "postings": n_post,
                        "parallelism": f"query-sharded x{world}, index replicated", "scale": args.scale,
                        "pipelines_per_gpu": args.pipelines},
@@ -269,7 +263,8 @@ def main():
             "pairs_per_step": r_tot,
             "join_work": {"keys": n_keys.value, "units": n_units.value, "runs": n_runs.value,
                           "wave_iters": n_iters.value, "lane_tests": n_tests.value, "flushes": n_fl.value,
-                          "exact_merges": n_mg.value, "exact_merge_lanes": n_ml.value},
+                          "exact_merges": n_mg.value, "exact_merge_lanes": n_ml.value,
+                          "long_pair_occurrences": n_tg.value},
             "index_build_s": build_s,
             "roofline": {"kernel": "k_join (overlap join + fused altitude/time filter)", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -375,9 +370,8 @@ def sharded_report(args, ctx, D, dist, torch, sh, step, full, i_cells_h, ranges,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded SURVEY s8(d) generator; no datasets)",
-        "config": {"workload": f"configs[{args.config}]: {nq} query footprints/GPU/step (70% polygon, 30% circle)"
-                               f" vs a {ni}-intent index sharded by S2 cell range over {world} GPU(s), SF-Bay metro,"
-                               " S2 level 13",
+        "config": {"workload": f"configs[{args.config}]: {nq} query footprints/GPU/step vs a {ni}-entity index "
+                               f"sharded by S2 cell range over {world} GPU(s), {W.CONFIG_NAMES[args.config]}, S2 level 13",
                    "queries_per_gpu_step": nq, "intents": ni, "postings_rank0": n_post,
                    "parallelism": f"cell-range shards x{world}; queries routed to shards and pairs routed home by "
                                   f"all-to-all ({args.dist_backend})", "scale": args.scale},

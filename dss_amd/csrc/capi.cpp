@@ -240,9 +240,10 @@ int dssg_search_counters(dssg_ctx *ctx, int64_t *keys, int64_t *units, int64_t *
     return DSSG_OK;
 }
 
-int dssg_join_events(dssg_ctx *ctx, int64_t *flushes, int64_t *merges, int64_t *merge_lanes)
+int dssg_join_events(dssg_ctx *ctx, int64_t *flushes, int64_t *merges, int64_t *merge_lanes, int64_t *tagged)
 {
     if (!ctx) return DSSG_ERR_INVALID;
+    if (tagged) *tagged = ctx->search.last_tagged();
     int64_t f, m, l;
     ctx->search.last_join_events(&f, &m, &l);
     if (flushes) *flushes = f;

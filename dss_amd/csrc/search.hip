@@ -55,6 +55,18 @@ constexpr int kQChunk = 1024;    // query records per join unit
 #ifndef DSS_JOIN_EXPERIMENT
 #define DSS_JOIN_EXPERIMENT 0
 #endif
+#ifndef DSS_JOIN_LONG
+#define DSS_JOIN_LONG 1  // 0: experiments only (long x long pairs would be deduplicated wrongly)
+#endif
+#ifndef DSS_JOIN_SPECIALISE
+#define DSS_JOIN_SPECIALISE 1  // record loop specialised on the unit's slot count
+#endif
+#ifndef DSS_JOIN_SIG_AHEAD
+#define DSS_JOIN_SIG_AHEAD 0  // 1: posting signatures in the one-unit-ahead prefetch too
+#endif
+#ifndef DSS_JOIN_PREFETCH
+#define DSS_JOIN_PREFETCH 1  // posting heads loaded one unit ahead
+#endif
 #ifndef DSS_JOIN_DIAG
 #define DSS_JOIN_DIAG 0  // 1: count flushes / exact merges (same-address atomics: slows the join)
 #endif
@@ -80,6 +92,9 @@ constexpr int kJoinBlocksPerCU = DSS_JOIN_BPC;  // persistent workgroups per CU 
 #endif
 constexpr uint32_t kRank0 = 0x80000000u;    // record: the cell is the query's first cell
 constexpr uint32_t kCompact = 0x40000000u;  // record: the query's prefix is compact
+constexpr uint32_t kLong = 0x20000000u;     // record: the query is a long footprint (long_cells)
+constexpr uint32_t kQFlags = kRank0 | kCompact | kLong;
+constexpr uint32_t kTag = 0x80000000u;      // output: a long x long pair, deduplicated after the join
 
 // ---- level-13 decode + prefix signatures -----------------------------------
 __device__ __forceinline__ int s2pos_to_ij(int o, int pos) { return (int)((0x874B78B4u >> (8 * o + 2 * pos)) & 3u); }
@@ -104,13 +119,29 @@ __device__ __forceinline__ bool decode13(uint64_t c, int &face, int &i, int &j)
     return true;
 }
 
-// Prefix signature of a sorted cell list: one bit per (i mod 16, j mod 16)
-// for every cell < c; `compact` iff all of them lie within +-7 cells of c on
-// c's face, so that equal bits imply equal cells.  Two lists can share a cell
-// < c only if their signatures overlap.
+// Prefix signature of a sorted cell list at cell c ("near-only"): one bit
+// per (i mod 16, j mod 16) for every cell < c that lies on c's face within
+// +-7 cells of c (mod 16 is injective on that window, so equal bits are
+// equal cells); `compact` iff every cell < c is such a near cell.  For two
+// lists that meet at c:
+//   * near bits overlap           -> they share a cell < c (exact);
+//   * no overlap, one side compact -> they share no cell < c (exact: a shared
+//     cell < c lies in the compact side's window, so in both near sets);
+//   * otherwise both sides are "long" footprints (cells outside an 8 x 8
+//     window, see long_cells), which the join never tests (tagged pairs).
 struct Sig256 {
     unsigned long long w[4];
 };
+__device__ __forceinline__ void sig_set(Sig256 &sig, int i, int j)
+{
+    const int b = ((i & 15) << 4) | (j & 15);
+    const unsigned long long bit = 1ull << (b & 63);
+    const int wi = b >> 6;  // selects, not an indexed store: keeps sig in registers
+    sig.w[0] |= wi == 0 ? bit : 0;
+    sig.w[1] |= wi == 1 ? bit : 0;
+    sig.w[2] |= wi == 2 ? bit : 0;
+    sig.w[3] |= wi == 3 ? bit : 0;
+}
 __device__ __forceinline__ void prefix_sig(const uint64_t *cells, int64_t n, uint64_t c, Sig256 &sig, bool &compact)
 {
     int fc = 0, ic = 0, jc = 0;
@@ -121,35 +152,68 @@ __device__ __forceinline__ void prefix_sig(const uint64_t *cells, int64_t n, uin
         uint64_t x = cells[k];
         if (x >= c) break;
         int f, i, j;
-        if (decode13(x, f, i, j)) {
-            int b = ((i & 15) << 4) | (j & 15);
-            unsigned long long bit = 1ull << (b & 63);
-            int wi = b >> 6;
-            sig.w[0] |= wi == 0 ? bit : 0;
-            sig.w[1] |= wi == 1 ? bit : 0;
-            sig.w[2] |= wi == 2 ? bit : 0;
-            sig.w[3] |= wi == 3 ? bit : 0;
-            int di = i - ic, dj = j - jc;
-            if (f != fc || di < -7 || di > 7 || dj < -7 || dj > 7) compact = false;
+        if (cvalid && decode13(x, f, i, j)) {
+            const int di = i - ic, dj = j - jc;
+            if (f == fc && di >= -7 && di <= 7 && dj >= -7 && dj <= 7) sig_set(sig, i, j);
+            else compact = false;
         } else {
-            sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = ~0ull;  // position unknown: force the exact check
-            compact = false;
+            compact = false;  // position unknown
         }
     }
 }
 
+// A footprint is "long" unless all its cells are valid level-13 cells of one
+// face inside an 8 x 8 window: then every prefix of it is compact at every
+// one of its cells.  Two long footprints' pairs skip the signature test.
+__device__ __forceinline__ bool long_cells(const uint64_t *cells, int64_t n)
+{
+    int f0 = -1, imin = 0, imax = 0, jmin = 0, jmax = 0;
+    for (int64_t k = 0; k < n; k++) {
+        int f, i, j;
+        if (!decode13(cells[k], f, i, j)) return true;
+        if (k == 0) {
+            f0 = f;
+            imin = imax = i;
+            jmin = jmax = j;
+        } else {
+            if (f != f0) return true;
+            imin = min(imin, i);
+            imax = max(imax, i);
+            jmin = min(jmin, j);
+            jmax = max(jmax, j);
+        }
+    }
+    return imax - imin > 7 || jmax - jmin > 7;
+}
+
 // True iff the query (cells qc[0..nq)) and the entity share no cell < c.
+// Block merge: B cells of each list per step (independent loads, all B x B
+// pairs compared in registers), then the block with the smaller last cell
+// advances (both on a tie) -- every common element meets its twin in some
+// step.  Cells >= c never count (padding with c keeps them out).
+template <int B>
 __device__ bool no_smaller_shared(const IndexView &a, uint32_t ent, uint64_t c, const uint64_t *qc, int64_t nq)
 {
     const uint64_t *ec = a.e_cells + a.e_offs[ent];
-    int64_t ne = a.e_offs[ent + 1] - a.e_offs[ent];
+    const int64_t ne = a.e_offs[ent + 1] - a.e_offs[ent];
     int64_t i = 0, j = 0;
     while (i < nq && j < ne) {
-        uint64_t x = qc[i], y = ec[j];
-        if (x >= c || y >= c) break;
-        if (x == y) return false;
-        if (x < y) i++;
-        else j++;
+        uint64_t x[B], y[B];
+#pragma unroll
+        for (int t = 0; t < B; t++) {
+            x[t] = i + t < nq ? qc[i + t] : c;
+            y[t] = j + t < ne ? ec[j + t] : c;
+        }
+        if (x[0] >= c || y[0] >= c) break;
+        bool hit = false;
+#pragma unroll
+        for (int p = 0; p < B; p++)
+#pragma unroll
+            for (int t = 0; t < B; t++) hit |= (x[p] == y[t]) & (x[p] < c);
+        if (hit) return false;
+        const uint64_t xl = x[B - 1], yl = y[B - 1];
+        if (xl <= yl) i += B;
+        if (yl <= xl) j += B;
     }
     return true;
 }
@@ -362,7 +426,8 @@ __global__ void k_bucket_gather(int64_t NB, const uint32_t *sval, const uint64_t
     b_e[j] = pe;
     b_alt[j] = make_float2(alo[e], ahi[e]);
     b_t[j] = make_longlong2(a, b);
-    b_meta[j] = (uint8_t)(lo | (compact ? 0x80 : 0));
+    const bool lng = long_cells(e_cells + e_offs[e], e_offs[e + 1] - e_offs[e]);
+    b_meta[j] = (uint8_t)(lo | (lng ? 0x40 : 0) | (compact ? 0x80 : 0));
     b_sig[2 * j] = make_ulonglong2(sig.w[0], sig.w[1]);
     b_sig[2 * j + 1] = make_ulonglong2(sig.w[2], sig.w[3]);
     if (owner) b_owner[j] = owner[e];
@@ -418,6 +483,35 @@ __global__ void k_qdecode(int64_t nqc, const uint64_t *cells, uint32_t *dec)
     dec[k] = decode13(cells[k], f, i, j) ? ((uint32_t)f << 26 | (uint32_t)i << 13 | (uint32_t)j) : kNoDecode;
 }
 
+// Long flag of every query (long_cells semantics, from the decodes).
+__global__ void k_qlong(int64_t nq, const int64_t *offs, const uint32_t *dec, uint8_t *qlong)
+{
+    const int64_t q = tid64();
+    if (q >= nq) return;
+    bool lng = false;
+    int f0 = -1, imin = 0, imax = 0, jmin = 0, jmax = 0;
+    for (int64_t k = offs[q]; k < offs[q + 1] && !lng; k++) {
+        const uint32_t d = dec[k];
+        if (d == kNoDecode) {
+            lng = true;
+            break;
+        }
+        const int f = (int)(d >> 26), i = (int)((d >> 13) & 8191u), j = (int)(d & 8191u);
+        if (k == offs[q]) {
+            f0 = f;
+            imin = imax = i;
+            jmin = jmax = j;
+        } else {
+            lng = f != f0;
+            imin = min(imin, i);
+            imax = max(imax, i);
+            jmin = min(jmin, j);
+            jmax = max(jmax, j);
+        }
+    }
+    qlong[q] = (lng || imax - imin > 7 || jmax - jmin > 7) ? 1 : 0;
+}
+
 // Groups (non-empty (slot, bucket) runs of the index) query cell k meets:
 // the buckets of [min(tlo,thi), max(tlo,thi)] plus the long bucket.
 __device__ __forceinline__ unsigned long long cell_groups(const IndexView &a, uint64_t cell, long long tlo,
@@ -437,7 +531,8 @@ __device__ __forceinline__ unsigned long long cell_groups(const IndexView &a, ui
 // `compact` = every earlier cell on this cell's face within +-7 cells).
 template <int PASS>
 __global__ void k_qcells(IndexView a, QueryView qv, int64_t nqc, const uint32_t *cq, const uint32_t *dec, int64_t *kcnt,
-                         const int64_t *koff, uint32_t *gkey, uint32_t *gval, QRec *crec, int32_t *cown)
+                         const int64_t *koff, uint32_t *gkey, uint32_t *gval, QRec *crec, int32_t *cown,
+                         const uint8_t *qlong)
 {
     const int64_t k = tid64();
     if (k >= nqc) return;
@@ -462,13 +557,15 @@ __global__ void k_qcells(IndexView a, QueryView qv, int64_t nqc, const uint32_t 
             w++;
         }
     }
-    // query record
+    // query record: near-only prefix signature of the query's cells before
+    // k (prefix_sig semantics), compact flag, long flag (qlong)
     const int64_t c0 = qv.offs[q];
+    const uint32_t dk = dec[k];
+    const int f = (int)(dk >> 26), i = (int)((dk >> 13) & 8191u), jj = (int)(dk & 8191u);
+    const bool v = dk != kNoDecode;
     Sig256 sig;
     sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = 0;
-    bool bad = false;  // an undecodable cell in the prefix
-    int pf = -1;       // face of every prefix cell, -2 if mixed
-    int imin = 0, imax = 0, jmin = 0, jmax = 0;
+    bool compact = v;
     // the prefix's decodes are loaded 8 at a time (independent loads in
     // flight together), then folded in order
     constexpr int kU = 8;
@@ -478,46 +575,20 @@ __global__ void k_qcells(IndexView a, QueryView qv, int64_t nqc, const uint32_t 
         for (int u = 0; u < kU; u++) dd[u] = j0 + u < k ? dec[j0 + u] : 0u;
 #pragma unroll
         for (int u = 0; u < kU; u++) {
-        const int64_t j = j0 + u;
-        if (j >= k) break;
-        const uint32_t d = dd[u];
-        const int f = (int)(d >> 26), ci = (int)((d >> 13) & 8191u), cj = (int)(d & 8191u);
-        if (d != kNoDecode) {
-            const int bit = ((ci & 15) << 4) | (cj & 15);
-            const unsigned long long mb = 1ull << (bit & 63);
-            const int wi = bit >> 6;  // selects, not an indexed store: keeps sig in registers
-            sig.w[0] |= wi == 0 ? mb : 0;
-            sig.w[1] |= wi == 1 ? mb : 0;
-            sig.w[2] |= wi == 2 ? mb : 0;
-            sig.w[3] |= wi == 3 ? mb : 0;
-            if (j == c0) {
-                pf = f;
-                imin = imax = ci;
-                jmin = jmax = cj;
-            } else {
-                if (pf != f) pf = -2;
-                imin = min(imin, ci);
-                imax = max(imax, ci);
-                jmin = min(jmin, cj);
-                jmax = max(jmax, cj);
-            }
-        } else {
-            bad = true;
-            sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = ~0ull;
-        }
+            if (j0 + u >= k) break;
+            const uint32_t d = dd[u];
+            const int pf = (int)(d >> 26), ci = (int)((d >> 13) & 8191u), cj = (int)(d & 8191u);
+            const int di = ci - i, dj = cj - jj;
+            if (v && d != kNoDecode && pf == f && di >= -7 && di <= 7 && dj >= -7 && dj <= 7) sig_set(sig, ci, cj);
+            else compact = false;
         }
     }
-    const uint32_t dk = dec[k];
-    const int f = (int)(dk >> 26), i = (int)((dk >> 13) & 8191u), jj = (int)(dk & 8191u);
-    const bool v = dk != kNoDecode;
-    const bool compact = v && !bad &&
-                         (k == c0 || (pf == f && imin >= i - 7 && imax <= i + 7 && jmin >= jj - 7 && jmax <= jj + 7));
     QRec r;
     r.tlo = tlo;
     r.thi = thi;
     r.alo = qv.alo[q];
     r.ahi = qv.ahi[q];
-    r.qv = q | (k == c0 ? kRank0 : 0u) | (compact ? kCompact : 0u);
+    r.qv = q | (k == c0 ? kRank0 : 0u) | (compact ? kCompact : 0u) | (qlong[q] ? kLong : 0u);
     r.bq0 = bucket_of(tlo < thi ? tlo : thi, a.bk);
     r.sig[0] = sig.w[0];
     r.sig[1] = sig.w[1];
@@ -625,12 +696,12 @@ struct JoinArgs {
     const uint64_t *g_key;  // group -> slot << 6 | bucket
     const uint32_t *gbeg, *gend;
     int64_t cap;
-    unsigned long long *counter;  // output pairs
+    unsigned long long *counter;  // [0] output pairs, [1] of which tagged (q | kTag)
 };
 
 // One posting held by a lane.
 struct Slot {
-    bool valid, first, compact;
+    bool valid, first, compact, lng;
     uint32_t ent;
     int be0;
     float2 alt;
@@ -642,7 +713,7 @@ struct Slot {
 __device__ __forceinline__ void load_slot(const IndexView &ix, uint32_t p, uint32_t pe, bool owner, Slot &s)
 {
     s.valid = p < pe;
-    s.first = s.compact = false;
+    s.first = s.compact = s.lng = false;
     s.ent = 0;
     s.be0 = 0;
     s.alt = make_float2(INFINITY, -INFINITY);    // matches nothing
@@ -672,32 +743,38 @@ __device__ __forceinline__ void load_slot(const IndexView &ix, uint32_t p, uint3
 // A lane's posting as loaded (software pipeline: loads issued one unit
 // ahead, decoded when the unit starts).
 struct RawSlot {
+    uint32_t p;  // posting index
     uint32_t v;
     uint32_t m;
     float2 alt;
     longlong2 t;
     int32_t own;
+#if DSS_JOIN_SIG_AHEAD
     ulonglong2 s01, s23;
+#endif
     bool valid;
 };
 
 __device__ __forceinline__ void load_raw(const IndexView &ix, uint32_t p, uint32_t pe, bool owner, RawSlot &r)
 {
     r.valid = p < pe;
+    r.p = p;
     if (!r.valid) return;
     r.v = ix.b_e[p];
     r.m = ix.b_meta[p];
     r.alt = ix.b_alt[p];
     r.t = ix.b_t[p];
     if (owner) r.own = ix.b_owner[p];
+#if DSS_JOIN_SIG_AHEAD
     r.s01 = ix.b_sig[2 * (size_t)p];  // loaded for first postings too: no wait on b_e here
     r.s23 = ix.b_sig[2 * (size_t)p + 1];
+#endif
 }
 
 __device__ __forceinline__ void decode_raw(const IndexView &ix, const RawSlot &r, bool owner, Slot &s)
 {
     s.valid = r.valid && !is_dead(ix, r.v & ~kFirstBit);  // tombstoned (write path): matches nothing
-    s.first = s.compact = false;
+    s.first = s.compact = s.lng = false;
     s.ent = 0;
     s.be0 = 0;
     s.alt = make_float2(INFINITY, -INFINITY);    // matches nothing
@@ -709,12 +786,18 @@ __device__ __forceinline__ void decode_raw(const IndexView &ix, const RawSlot &r
     s.first = (r.v & kFirstBit) != 0;
     s.be0 = (int)(r.m & 0x3f);
     s.compact = (r.m & 0x80) != 0;
+    s.lng = (r.m & 0x40) != 0;
     s.alt = r.alt;
     s.t = r.t;
     if (owner) s.own = r.own;
     if (!s.first) {
+#if DSS_JOIN_SIG_AHEAD
         s.s01 = r.s01;
         s.s23 = r.s23;
+#else  // issued here, used by the record loop: overlaps the record gathers
+        s.s01 = ix.b_sig[2 * (size_t)r.p];
+        s.s23 = ix.b_sig[2 * (size_t)r.p + 1];
+#endif
     }
 }
 
@@ -737,6 +820,7 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int staged = 0;
+    int staged_tag = 0;  // staged entries carrying kTag (long x long, separated after the join)
     auto flush = [&]() {
         __builtin_amdgcn_wave_barrier();
 #if DSS_JOIN_EXPERIMENT == 1  // timing experiment: drop the pairs
@@ -744,7 +828,8 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
 #endif
         unsigned long long base = 0;
         if (lane == 0 && staged) {
-            base = atomicAdd(a.counter, (unsigned long long)staged);
+            base = atomicAdd(&a.counter[0], (unsigned long long)staged);
+            if (staged_tag) atomicAdd(&a.counter[1], (unsigned long long)staged_tag);
 #if DSS_JOIN_DIAG
             atomicAdd(&work[1], 1u);  // diagnostics: flushes
 #endif
@@ -758,6 +843,7 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
             }
         }
         staged = 0;
+        staged_tag = 0;
         __builtin_amdgcn_wave_barrier();
     };
     const IndexView &ix = a.ix;
@@ -790,15 +876,22 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
         ci_pre = d.k0 + (uint32_t)lane < d.k1 ? sval[d.k0 + lane] : 0u;
     };
     int64_t u = next_unit();
+#if DSS_JOIN_PREFETCH
     if (u >= 0) prefetch(u);
+#endif
     while (u >= 0) {
+#if !DSS_JOIN_PREFETCH
+        prefetch(u);
+#endif
         const UnitDesc cu = d;
         Slot sl[kSlots];
 #pragma unroll
         for (int k = 0; k < kSlots; k++) decode_raw(ix, raw[k], OWNER, sl[k]);
         uint32_t ci_first = ci_pre;
         const int64_t un = next_unit();
+#if DSS_JOIN_PREFETCH
         if (un >= 0) prefetch(un);
+#endif
         {
             const uint64_t key = cu.key;
             const int b = (int)(key & 63);
@@ -848,11 +941,10 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                 // overlap for slots holding a candidate that needs it.
                 auto records = [&](auto nsc) {
                     constexpr int NS = decltype(nsc)::value;
-                    unsigned long long mf[NS], mc[NS], mb[NS];
+                    unsigned long long mf[NS], mb[NS];
 #pragma unroll
                     for (int k = 0; k < NS; k++) {
                         mf[k] = __ballot(sl[k].first);
-                        mc[k] = __ballot(sl[k].compact);
                         mb[k] = __ballot(sl[k].be0 == b);
                     }
                     unsigned long long todo = todo0;
@@ -868,7 +960,7 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                         const uint32_t qv = (uint32_t)__builtin_amdgcn_readlane(r1.z, j);
                         const int bq0 = __builtin_amdgcn_readlane(r1.w, j);
                         const int32_t own = OWNER ? __builtin_amdgcn_readlane(rown_l, j) : -1;
-                        const uint32_t q = qv & ~(kRank0 | kCompact);
+                        const uint32_t q = qv & ~kQFlags;
                         // keep a pair only in its first common bucket: b == max(bq0, be0),
                         // i.e. bq0 == b (every lane) or be0 == b (mask mb)
                         const bool all_b = (b == kLongBucket) | (bq0 == b);
@@ -882,7 +974,19 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                             const unsigned long long m = __ballot(p);
                             pm[k] = all_b ? m : (m & mb[k]);
                         }
-                        // ... and at the smallest shared cell (SQL DISTINCT, Q13)
+                        // long query x long entity: emitted at every shared cell, tagged,
+                        // deduplicated by one sort after the join
+                        unsigned long long tg[NS];
+#pragma unroll
+                        for (int k = 0; k < NS; k++) tg[k] = 0ull;
+                        if (DSS_JOIN_LONG && (qv & kLong)) {  // masks built here: rare, keeps SGPRs free in the loop
+#pragma unroll
+                            for (int k = 0; k < NS; k++) {
+                                tg[k] = pm[k] & __ballot(sl[k].lng);
+                                pm[k] &= ~tg[k];
+                            }
+                        }
+                        // ... the rest at the smallest shared cell (SQL DISTINCT, Q13)
                         if (!(qv & kRank0)) {
                             unsigned long long need[NS], any = 0;
 #pragma unroll
@@ -905,12 +1009,15 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                                     acc |= (uint32_t)(sk.s23.x >> 32) & (uint32_t)c3.y;
                                     acc |= (uint32_t)sk.s23.y & (uint32_t)c3.z;
                                     acc |= (uint32_t)(sk.s23.y >> 32) & (uint32_t)c3.w;
-                                    const unsigned long long chk = need[k] & __ballot(acc != 0u);
-                                    // both prefixes compact: equal bits are equal cells, a
-                                    // smaller shared cell exists -> drop
-                                    const unsigned long long sure = qcompact ? (chk & mc[k]) : 0ull;
-                                    pm[k] &= ~sure;
-                                    const unsigned long long ex = chk & ~sure;  // inconclusive: merge the lists
+                                    const unsigned long long ov = __ballot(acc != 0u);
+                                    // near bits overlap: equal bits are equal cells, a smaller
+                                    // shared cell exists -> drop; no overlap with either prefix
+                                    // compact: none exists -> keep (prefix_sig)
+                                    pm[k] &= ~(need[k] & ov);
+                                    // neither compact means both footprints are long, i.e.
+                                    // tagged above: the merge below is a safety net only
+                                    unsigned long long ex = qcompact ? 0ull : (need[k] & ~ov);
+                                    if (ex) ex &= ~__ballot(sk.compact);
                                     if (ex) {
 #if DSS_JOIN_DIAG
                                         if (lane == 0) {  // diagnostics: merges (events, lanes)
@@ -922,18 +1029,21 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                                         if ((ex >> lane) & 1ull) {
                                             const uint64_t *qc = a.qv.cells + a.qv.offs[q];
                                             const int64_t nqc = a.qv.offs[q + 1] - a.qv.offs[q];
-                                            drop = !no_smaller_shared(ix, sk.ent, cell, qc, nqc);
+                                            drop = !no_smaller_shared<2>(ix, sk.ent, cell, qc, nqc);  // rare: few registers
                                         }
                                         pm[k] &= ~__ballot(drop);
                                     }
                                 }
                             }
                         }
-                        int tot = 0;
+                        int tot = 0, ttot = 0;
 #pragma unroll
-                        for (int k = 0; k < NS; k++) tot += __popcll(pm[k]);
-                        if (tot == 0) continue;
-                        if (staged + tot > kStage) flush();
+                        for (int k = 0; k < NS; k++) {
+                            tot += __popcll(pm[k]);
+                            ttot += __popcll(tg[k]);
+                        }
+                        if (tot + ttot == 0) continue;
+                        if (staged + tot + ttot > kStage) flush();
                         const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
                         for (int k = 0; k < NS; k++) {
@@ -944,19 +1054,70 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                             }
                             staged += __popcll(pm[k]);
                         }
+                        if (ttot) {  // scalar branch: long x long records only
+#pragma unroll
+                            for (int k = 0; k < NS; k++) {
+                                if ((tg[k] >> lane) & 1ull) {
+                                    const int rk = staged + __popcll(tg[k] & below);
+                                    sq[w][rk] = q | kTag;
+                                    se[w][rk] = sl[k].ent;
+                                }
+                                staged += __popcll(tg[k]);
+                            }
+                            staged_tag += ttot;
+                        }
                     }
                 };
 #if DSS_JOIN_EXPERIMENT == 2  // timing experiment: units and records loaded, no tests
                 if (todo0 == 0x1234567ull) staged += 1;
 #else
+#if DSS_JOIN_SPECIALISE
                 if (nslot == 1) records(std::integral_constant<int, 1>{});
                 else records(std::integral_constant<int, kSlots>{});
+#else
+                records(std::integral_constant<int, kSlots>{});
+#endif
 #endif
             }
         }
         u = un;
     }
     flush();
+}
+
+// Tagged (long x long) pairs after the join.  k_tag_split: the join output
+// -> untagged pairs compacted into (q2, e2) and tagged ones as keys
+// (q << 32 | e), by one scan of the tag flags; k_tag_unique then appends the
+// first of each run of the sorted keys after the untagged pairs.
+__global__ void k_tag_mark(int64_t n, const uint32_t *q, int64_t *flag)
+{
+    const int64_t i = tid64();
+    if (i < n) flag[i] = (q[i] & kTag) ? 1 : 0;
+}
+__global__ void k_tag_split(int64_t n, const uint32_t *q, const uint32_t *e, const int64_t *tpos, uint32_t *q2,
+                            uint32_t *e2, unsigned long long *tkey)
+{
+    const int64_t i = tid64();
+    if (i >= n) return;
+    const uint32_t qq = q[i];
+    if (qq & kTag) tkey[tpos[i]] = ((unsigned long long)(qq & ~kTag) << 32) | e[i];
+    else {
+        q2[i - tpos[i]] = qq;
+        e2[i - tpos[i]] = e[i];
+    }
+}
+__global__ void k_tag_flags(int64_t n, const unsigned long long *key, int64_t *flag)
+{
+    const int64_t i = tid64();
+    if (i < n) flag[i] = (i == 0 || key[i] != key[i - 1]) ? 1 : 0;
+}
+__global__ void k_tag_scatter(int64_t n, const unsigned long long *key, const int64_t *flag, const int64_t *pos,
+                              int64_t at, uint32_t *out_q, uint32_t *out_e)
+{
+    const int64_t i = tid64();
+    if (i >= n || !flag[i]) return;
+    out_q[at + pos[i]] = (uint32_t)(key[i] >> 32);
+    out_e[at + pos[i]] = (uint32_t)key[i];
 }
 
 // Roofline accounting over the plain postings, predicate off: M = postings
@@ -979,7 +1140,7 @@ __global__ __launch_bounds__(kBlock) void k_stats(IndexView a, QueryView qv, uns
                 if (p < e) {
                     const uint32_t pe = a.p_e[p];
                     pass = ci == c0 || (pe & kFirstBit) ||
-                           no_smaller_shared(a, pe & ~kFirstBit, c, qv.cells + c0, ci - c0);
+                           no_smaller_shared<8>(a, pe & ~kFirstBit, c, qv.cells + c0, ci - c0);
                 }
                 my_m += (unsigned long long)(e - base < 64 ? e - base : 64);
                 my_d += (unsigned long long)__popcll(__ballot(pass));
@@ -1285,7 +1446,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
                           const int32_t *q_owner, hipStream_t s, dssg_pairs *out)
 {
     if (q_owner && !idx->has_owner) throw Error(DSSG_ERR_INVALID, "search by owner on an index built without owners");
-    if (nq >= (int64_t)kCompact) throw Error(DSSG_ERR_INVALID, "search: more than 2^30 queries per batch");
+    if (nq >= (int64_t)kLong) throw Error(DSSG_ERR_INVALID, "search: more than 2^29 queries per batch");
     if (timing_ && !ev0_) {
         DSS_HIP(hipEventCreate(&ev0_));
         DSS_HIP(hipEventCreate(&ev1_));
@@ -1313,8 +1474,10 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     hipLaunchKernelGGL(k_cell_query, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_offs, cq);
     hipLaunchKernelGGL(k_qdecode, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, nqc, q_cells, dec);
     int64_t *kcnt = c0_.ensure(nqc + 1), *koff = c1_.ensure(nqc + 2);
+    uint8_t *qlong = qlong_.ensure(nq + 1);
+    hipLaunchKernelGGL(k_qlong, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_offs, dec, qlong);
     hipLaunchKernelGGL(k_qcells<0>, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, ix, qv, nqc, cq, dec, kcnt, nullptr,
-                       nullptr, nullptr, nullptr, nullptr);
+                       nullptr, nullptr, nullptr, nullptr, nullptr);
     exclusive_scan_i64(kcnt, koff, nqc, tmp_, s);
     const int64_t nkeys = fetch_i64(koff + nqc, s);
     keys_ = nkeys;
@@ -1325,7 +1488,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     uint32_t *key = v0_.ensure(nkeys + 1), *skey = v2_.ensure(nkeys + 1);
     uint32_t *val = v1_.ensure(nkeys + 1), *sval = v3_.ensure(nkeys + 1);
     hipLaunchKernelGGL(k_qcells<1>, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, ix, qv, nqc, cq, dec, nullptr, koff,
-                       key, val, recs, rown);
+                       key, val, recs, rown, (const uint8_t *)qlong);
     // (2) group by group id (radix sort over bits_for(ng) bits), then each
     // group's record range
     sort_pairs(key, skey, val, sval, nkeys, bits_for(ng), tmp_, s);
@@ -1377,11 +1540,11 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     }
     const unsigned nblocks = (unsigned)n_cu_ * kJoinBlocksPerCU;
     uint32_t *work = work_.ensure(4);  // [0] unit queue head, [1..3] diagnostics
-    unsigned long long *counter = counter_.ensure(1);
+    unsigned long long *counter = counter_.ensure(2);
     ja.counter = counter;
     for (int attempt = 0; attempt < 3; attempt++) {
         uint32_t *oq = oq_.ensure(out_cap_), *oe = oe_.ensure(out_cap_);
-        DSS_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned long long), s));
+        DSS_HIP(hipMemsetAsync(counter, 0, 2 * sizeof(unsigned long long), s));
         DSS_HIP(hipMemsetAsync(work, 0, 4 * sizeof(uint32_t), s));
         ja.cap = (int64_t)out_cap_;
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
@@ -1392,8 +1555,8 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             hipLaunchKernelGGL(k_join<false>, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
                                (const uint32_t *)sval, (const int32_t *)nullptr, (const UnitDesc *)units, oq, oe, work);
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
-        unsigned long long total = 0;
-        DSS_HIP(hipMemcpyAsync(&total, counter, sizeof(total), hipMemcpyDeviceToHost, s));
+        unsigned long long tot[2] = {0, 0};
+        DSS_HIP(hipMemcpyAsync(tot, counter, sizeof(tot), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipStreamSynchronize(s));
         if (timing_) {
             float ms = 0;
@@ -1405,13 +1568,40 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             merges_ = hw[2];
             merge_lanes_ = hw[3];
         }
-        if (total <= out_cap_) {
-            out->q = oq;
-            out->e = oe;
-            out->n = (int64_t)total;
+        const unsigned long long total = tot[0], ntag = tot[1];
+        tagged_ = (int64_t)ntag;
+        if (total > out_cap_) {
+            out_cap_ = (size_t)(total + total / 8 + 1024);
+            continue;
+        }
+        int64_t nout = (int64_t)total;
+        if (ntag > 0) {  // long x long pairs: split off, sort, unique, append
+            const int64_t n = (int64_t)total, nt = (int64_t)ntag;
+            uint32_t *q2 = oq2_.ensure(out_cap_), *e2 = oe2_.ensure(out_cap_);
+            unsigned long long *k1 = tkey_.ensure(nt + 1), *k2 = tkey2_.ensure(nt + 1);
+            int64_t *flag = c0_.ensure(n + 1), *pos = c1_.ensure(n + 2);
+            hipLaunchKernelGGL(k_tag_mark, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, oq, flag);
+            exclusive_scan_i64(flag, pos, n, tmp_, s);
+            hipLaunchKernelGGL(k_tag_split, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, oq, oe, pos, q2, e2, k1);
+            size_t bytes = 0;
+            DSS_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, k1, k2, (int)nt, 0, 64, s));
+            tmp_.ensure(bytes + 16);
+            DSS_HIP(hipcub::DeviceRadixSort::SortKeys(tmp_.p, bytes, k1, k2, (int)nt, 0, 64, s));
+            hipLaunchKernelGGL(k_tag_flags, dim3(grid_for(nt, kBlock)), dim3(kBlock), 0, s, nt, k2, flag);
+            exclusive_scan_i64(flag, pos, nt, tmp_, s);
+            nout = n - nt;
+            hipLaunchKernelGGL(k_tag_scatter, dim3(grid_for(nt, kBlock)), dim3(kBlock), 0, s, nt, k2, flag, pos, nout, q2,
+                               e2);
+            nout += fetch_i64(pos + nt, s);
+            out->q = q2;
+            out->e = e2;
+            out->n = nout;
             return;
         }
-        out_cap_ = (size_t)(total + total / 8 + 1024);
+        out->q = oq;
+        out->e = oe;
+        out->n = nout;
+        return;
     }
     throw Error(DSSG_ERR_DEVICE, "search: output size did not converge");
 }

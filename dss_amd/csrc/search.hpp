@@ -84,6 +84,7 @@ class SearchEngine {
     int64_t last_keys() const { return keys_; }
     // timing mode only: runs, wave iterations (records x tiles), useful lane tests
     // timing mode only: output flushes, exact list merges (events, lanes)
+    int64_t last_tagged() const { return tagged_; }  // long x long pair occurrences before the dedupe
     void last_join_events(int64_t *flushes, int64_t *merges, int64_t *merge_lanes) const
     {
         *flushes = flushes_;
@@ -103,9 +104,11 @@ class SearchEngine {
     DevBuf<uint32_t> v0_, v1_, v2_, v3_, ur_, up_, uq_, cq_, gb_, ge_, dec_;
     DevBuf<int64_t> c0_, c1_, rc_, rs_, nr_, uc_, uo_;
     DevBuf<unsigned long long> counter_;
-    DevBuf<uint32_t> oq_, oe_;
+    DevBuf<uint32_t> oq_, oe_, oq2_, oe2_;
     DevBuf<unsigned char> rec_;
     DevBuf<int32_t> own_;
+    DevBuf<uint8_t> qlong_;
+    DevBuf<unsigned long long> tkey_, tkey2_;  // tagged (long x long) pairs, deduplicated after the join
     DevBuf<uint32_t> work_;
     DevBuf<unsigned char> units_buf_;  // join unit descriptors
     int n_cu_ = 0;
@@ -113,7 +116,7 @@ class SearchEngine {
     bool timing_ = false;
     double join_ms_ = 0;
     int64_t units_ = 0, keys_ = 0, runs_ = 0, iters_ = 0, tests_ = 0;
-    int64_t flushes_ = 0, merges_ = 0, merge_lanes_ = 0;
+    int64_t flushes_ = 0, merges_ = 0, merge_lanes_ = 0, tagged_ = 0;
     hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
 };
 

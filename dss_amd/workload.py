@@ -248,6 +248,36 @@ def config(i: int, scale: float = 1.0):
     return rng, queries, qa, intents, ia, T0_US
 
 
+def _footprints_for(i: int, rng, n: int) -> Footprints:
+    if i in (0, 1):
+        return metro_footprints(rng, n, METRO)
+    if i == 2:
+        return metro_footprints(rng, n, CALIFORNIA, hotspots=CA_HOTSPOTS, hot_frac=0.7, sigma_m=15000.0)
+    if i == 3:
+        return city_blocks(rng, n)
+    return corridors(rng, n)
+
+
+def config_split(i: int, rank: int = 0, scale: float = 1.0, queries_scale: float = 1.0):
+    """bench.py's form of config i: the airspace (entities + attributes) from
+    the config's seed, identical on every rank, and a rank-private query batch
+    (seed 20201015 + i + 1000 * (rank + 1)) of the config's query shape.
+    Returns (queries, q_attrs, entities, e_attrs, now_us, rid)."""
+    if i not in CONFIG_SIZES:
+        raise ValueError(f"config {i} not generated here")
+    nq, ni = CONFIG_SIZES[i]
+    nq = max(1, int(nq * scale * queries_scale))
+    ni = max(1, int(ni * scale))
+    rid = i == 3
+    rng_i = np.random.default_rng(20201015 + i)
+    ents = _footprints_for(i, rng_i, ni)
+    ea = rid_attrs(rng_i, ni, False) if rid else intent_attrs(rng_i, ni)
+    rng_q = np.random.default_rng(20201015 + i + 1000 * (rank + 1))
+    qs = _footprints_for(i, rng_q, nq)
+    qa = rid_attrs(rng_q, nq, True) if rid else query_attrs(rng_q, nq)
+    return qs, qa, ents, ea, T0_US, rid
+
+
 def query_bounds(qa: Attrs, now_us: int):
     """Query (tlo, thi) as the search kernels take them: SCD
     `COALESCE(ends_at >= start) AND ends_at >= now` (operations.go:398-402)

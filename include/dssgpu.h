@@ -329,10 +329,12 @@ void dssg_set_timing(dssg_ctx *ctx, int enabled);
  * pointer may be NULL. */
 int dssg_search_counters(dssg_ctx *ctx, int64_t *keys, int64_t *units, int64_t *runs, int64_t *iters,
                          int64_t *tests);
-/* Join events of the most recent search (timing mode only): output flushes
- * (one atomic each), exact cell-list merges where the prefix signatures were
- * inconclusive (wave events, lanes).  Any pointer may be NULL. */
-int dssg_join_events(dssg_ctx *ctx, int64_t *flushes, int64_t *merges, int64_t *merge_lanes);
+/* Join events of the most recent search: output flushes (one atomic each)
+ * and exact cell-list merges where the prefix signatures were inconclusive
+ * (wave events, lanes) -- these three only in a DSS_JOIN_DIAG build, with
+ * timing on -- and the long x long pair occurrences that were deduplicated
+ * after the join (always).  Any pointer may be NULL. */
+int dssg_join_events(dssg_ctx *ctx, int64_t *flushes, int64_t *merges, int64_t *merge_lanes, int64_t *tagged);
 /* Roofline accounting for a device query batch: total postings the join
  * scans (sum of M_q) and distinct candidate entities before the
  * altitude/time filter (sum of D_q), SURVEY.md s8(d). */
