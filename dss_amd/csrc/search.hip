@@ -974,19 +974,10 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                             const unsigned long long m = __ballot(p);
                             pm[k] = all_b ? m : (m & mb[k]);
                         }
-                        // long query x long entity: emitted at every shared cell, tagged,
-                        // deduplicated by one sort after the join
-                        unsigned long long tg[NS];
-#pragma unroll
-                        for (int k = 0; k < NS; k++) tg[k] = 0ull;
-                        if (DSS_JOIN_LONG && (qv & kLong)) {  // masks built here: rare, keeps SGPRs free in the loop
-#pragma unroll
-                            for (int k = 0; k < NS; k++) {
-                                tg[k] = pm[k] & __ballot(sl[k].lng);
-                                pm[k] &= ~tg[k];
-                            }
-                        }
-                        // ... the rest at the smallest shared cell (SQL DISTINCT, Q13)
+                        // At the smallest shared cell only (SQL DISTINCT, Q13): a lane whose
+                        // query and entity share a cell < c (near prefix bits overlap, an
+                        // exact test) is dropped; with no overlap the lane is kept, which is
+                        // exact when either prefix is compact (prefix_sig).
                         if (!(qv & kRank0)) {
                             unsigned long long need[NS], any = 0;
 #pragma unroll
@@ -1010,14 +1001,12 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                                     acc |= (uint32_t)sk.s23.y & (uint32_t)c3.z;
                                     acc |= (uint32_t)(sk.s23.y >> 32) & (uint32_t)c3.w;
                                     const unsigned long long ov = __ballot(acc != 0u);
-                                    // near bits overlap: equal bits are equal cells, a smaller
-                                    // shared cell exists -> drop; no overlap with either prefix
-                                    // compact: none exists -> keep (prefix_sig)
                                     pm[k] &= ~(need[k] & ov);
-                                    // neither compact means both footprints are long, i.e.
-                                    // tagged above: the merge below is a safety net only
+                                    // neither prefix compact means both footprints are long:
+                                    // those lanes are tagged below, so this merge is a
+                                    // safety net only
                                     unsigned long long ex = qcompact ? 0ull : (need[k] & ~ov);
-                                    if (ex) ex &= ~__ballot(sk.compact);
+                                    if (ex) ex &= ~__ballot(sk.compact) & ~__ballot(DSS_JOIN_LONG && sk.lng);
                                     if (ex) {
 #if DSS_JOIN_DIAG
                                         if (lane == 0) {  // diagnostics: merges (events, lanes)
@@ -1034,6 +1023,20 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                                         pm[k] &= ~__ballot(drop);
                                     }
                                 }
+                            }
+                        }
+                        // long query x long entity: every surviving occurrence is emitted
+                        // tagged (the smallest shared cell always survives: nothing
+                        // smaller is shared) and the tagged set is deduplicated by one
+                        // sort after the join; such a pair is never emitted untagged
+                        unsigned long long tg[NS];
+#pragma unroll
+                        for (int k = 0; k < NS; k++) tg[k] = 0ull;
+                        if (DSS_JOIN_LONG && (qv & kLong)) {  // masks built here: rare, keeps SGPRs free in the loop
+#pragma unroll
+                            for (int k = 0; k < NS; k++) {
+                                tg[k] = pm[k] & __ballot(sl[k].lng);
+                                pm[k] &= ~tg[k];
                             }
                         }
                         int tot = 0, ttot = 0;
