@@ -210,6 +210,8 @@ def main():
                                          C.byref(n_tests)))
     n_fl, n_mg, n_ml, n_tg = (C.c_int64() for _ in range(4))
     ctx.check(ctx.L.dssg_join_events(ctx.h, C.byref(n_fl), C.byref(n_mg), C.byref(n_ml), C.byref(n_tg)))
+    n_lq, n_lp = C.c_int64(), C.c_int64()
+    ctx.check(ctx.L.dssg_join_longs(ctx.h, C.byref(n_lq), C.byref(n_lp)))
     c_tot = int(cells.total_cells)
     r_tot = int(pairs.n)
     kern_avg_ms = float(np.mean(kern_ms))
@@ -264,7 +266,8 @@ def main():
             "join_work": {"keys": n_keys.value, "units": n_units.value, "runs": n_runs.value,
                           "wave_iters": n_iters.value, "lane_tests": n_tests.value, "flushes": n_fl.value,
                           "exact_merges": n_mg.value, "exact_merge_lanes": n_ml.value,
-                          "long_pair_occurrences": n_tg.value},
+                          "long_pair_occurrences": n_tg.value, "long_queries": n_lq.value,
+                          "long_postings": n_lp.value},
             "index_build_s": build_s,
             "roofline": {"kernel": "k_join (overlap join + fused altitude/time filter)", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -150,6 +150,7 @@ def load():
         L.dssg_set_timing.argtypes = [vp, C.c_int]
         L.dssg_set_timing.restype = None
         L.dssg_join_events.argtypes = [vp, P(i64), P(i64), P(i64), P(i64)]
+        L.dssg_join_longs.argtypes = [vp, P(i64), P(i64)]
         L.dssg_search_counters.argtypes = [vp, P(i64), P(i64), P(i64), P(i64), P(i64)]
         L.dssg_search_stats_device.argtypes = [vp, vp, i64, vp, vp, vp, P(i64), P(i64)]
         L.dssg_copy_to_host.argtypes = [vp, vp, vp, C.c_size_t]

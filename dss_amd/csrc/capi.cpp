@@ -252,6 +252,16 @@ int dssg_join_events(dssg_ctx *ctx, int64_t *flushes, int64_t *merges, int64_t *
     return DSSG_OK;
 }
 
+int dssg_join_longs(dssg_ctx *ctx, int64_t *long_queries, int64_t *long_postings)
+{
+    if (!ctx) return DSSG_ERR_INVALID;
+    int64_t lq, lp;
+    ctx->search.last_longs(&lq, &lp);
+    if (long_queries) *long_queries = lq;
+    if (long_postings) *long_postings = lp;
+    return DSSG_OK;
+}
+
 int dssg_cover_batch_device(dssg_ctx *ctx, int64_t n, const int32_t *d_kind, const int64_t *d_voff, const double *d_lat,
                             const double *d_lng, const float *d_radius_m, void *stream, dssg_cells *out)
 {

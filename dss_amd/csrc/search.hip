@@ -58,6 +58,9 @@ constexpr int kQChunk = 1024;    // query records per join unit
 #ifndef DSS_JOIN_LONG
 #define DSS_JOIN_LONG 1  // 0: experiments only (long x long pairs would be deduplicated wrongly)
 #endif
+// k_join<OWNER, LONG>: LONG = false when the batch holds no long query or
+// the index no long posting (no long x long pair can exist): the tagging
+// code is compiled out of the record loop.
 #ifndef DSS_JOIN_SPECIALISE
 #define DSS_JOIN_SPECIALISE 1  // record loop specialised on the unit's slot count
 #endif
@@ -484,7 +487,8 @@ __global__ void k_qdecode(int64_t nqc, const uint64_t *cells, uint32_t *dec)
 }
 
 // Long flag of every query (long_cells semantics, from the decodes).
-__global__ void k_qlong(int64_t nq, const int64_t *offs, const uint32_t *dec, uint8_t *qlong)
+__global__ void k_qlong(int64_t nq, const int64_t *offs, const uint32_t *dec, uint8_t *qlong,
+                        unsigned long long *nlong)
 {
     const int64_t q = tid64();
     if (q >= nq) return;
@@ -509,7 +513,19 @@ __global__ void k_qlong(int64_t nq, const int64_t *offs, const uint32_t *dec, ui
             jmax = max(jmax, j);
         }
     }
-    qlong[q] = (lng || imax - imin > 7 || jmax - jmin > 7) ? 1 : 0;
+    const bool is_long = lng || imax - imin > 7 || jmax - jmin > 7;
+    qlong[q] = is_long ? 1 : 0;
+    const unsigned long long m = __ballot(is_long);
+    if (m && (threadIdx.x & 63) == __builtin_ctzll(m)) atomicAdd(nlong, (unsigned long long)__popcll(m));
+}
+
+// Long postings of the index (b_meta bit 0x40).
+__global__ void k_count_long(int64_t NB, const uint8_t *b_meta, unsigned long long *cnt)
+{
+    const int64_t j = tid64();
+    const bool l = j < NB && (b_meta[j] & 0x40) != 0;
+    const unsigned long long m = __ballot(l);
+    if (m && (threadIdx.x & 63) == __builtin_ctzll(m)) atomicAdd(cnt, (unsigned long long)__popcll(m));
 }
 
 // Groups (non-empty (slot, bucket) runs of the index) query cell k meets:
@@ -803,7 +819,7 @@ __device__ __forceinline__ void decode_raw(const IndexView &ix, const RawSlot &r
 
 // (3) one wavefront per unit: up to 64 * kSlots postings in registers, the
 // unit's query records staged through LDS 64 at a time and broadcast.
-template <bool OWNER>
+template <bool OWNER, bool LONG>
 __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, const QRec *__restrict__ recs,
                                                       const uint32_t *__restrict__ sval,
                                                       const int32_t *__restrict__ rown,
@@ -1006,7 +1022,7 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                                     // those lanes are tagged below, so this merge is a
                                     // safety net only
                                     unsigned long long ex = qcompact ? 0ull : (need[k] & ~ov);
-                                    if (ex) ex &= ~__ballot(sk.compact) & ~__ballot(DSS_JOIN_LONG && sk.lng);
+                                    if (ex) ex &= ~__ballot(sk.compact) & ~__ballot(LONG && DSS_JOIN_LONG && sk.lng);
                                     if (ex) {
 #if DSS_JOIN_DIAG
                                         if (lane == 0) {  // diagnostics: merges (events, lanes)
@@ -1032,7 +1048,7 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                         unsigned long long tg[NS];
 #pragma unroll
                         for (int k = 0; k < NS; k++) tg[k] = 0ull;
-                        if (DSS_JOIN_LONG && (qv & kLong)) {  // masks built here: rare, keeps SGPRs free in the loop
+                        if (LONG && DSS_JOIN_LONG && (qv & kLong)) {  // masks built here: rare, keeps SGPRs free in the loop
 #pragma unroll
                             for (int k = 0; k < NS; k++) {
                                 tg[k] = pm[k] & __ballot(sl[k].lng);
@@ -1363,6 +1379,13 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     if (NB)
         hipLaunchKernelGGL(k_bucket_gather, dim3(grid_for(NB, kBlock)), dim3(kBlock), 0, s, NB, bv1, p_cell, p_e, e_offs,
                            e_cells, alt_lo, alt_hi, t0, t1, owner, bk, b_e, b_alt, b_t, b_meta, b_sig, b_owner);
+    unsigned long long *nlong_d = (unsigned long long *)c1_.ensure(2);
+    DSS_HIP(hipMemsetAsync(nlong_d, 0, sizeof(unsigned long long), s));
+    if (NB) hipLaunchKernelGGL(k_count_long, dim3(grid_for(NB, kBlock)), dim3(kBlock), 0, s, NB, b_meta, nlong_d);
+    unsigned long long nlong_h = 0;
+    DSS_HIP(hipMemcpyAsync(&nlong_h, nlong_d, sizeof(nlong_h), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    idx->n_long_b = (int64_t)nlong_h;
     // (7) groups = runs of equal (slot, bucket)
     unsigned long long *s_mask = idx->s_mask.ensure(n_slots + 1);
     DSS_HIP(hipMemsetAsync(s_mask, 0, sizeof(unsigned long long) * (n_slots + 1), s));
@@ -1478,12 +1501,21 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     hipLaunchKernelGGL(k_qdecode, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, nqc, q_cells, dec);
     int64_t *kcnt = c0_.ensure(nqc + 1), *koff = c1_.ensure(nqc + 2);
     uint8_t *qlong = qlong_.ensure(nq + 1);
-    hipLaunchKernelGGL(k_qlong, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_offs, dec, qlong);
+    unsigned long long *nlongq_d = counter_.ensure(8) + 5;
+    DSS_HIP(hipMemsetAsync(nlongq_d, 0, sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_qlong, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_offs, dec, qlong, nlongq_d);
     hipLaunchKernelGGL(k_qcells<0>, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, ix, qv, nqc, cq, dec, kcnt, nullptr,
                        nullptr, nullptr, nullptr, nullptr, nullptr);
     exclusive_scan_i64(kcnt, koff, nqc, tmp_, s);
-    const int64_t nkeys = fetch_i64(koff + nqc, s);
+    int64_t nkeys = 0;
+    unsigned long long nlongq = 0;
+    DSS_HIP(hipMemcpyAsync(&nkeys, koff + nqc, sizeof(nkeys), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipMemcpyAsync(&nlongq, nlongq_d, sizeof(nlongq), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
     keys_ = nkeys;
+    long_queries_ = (int64_t)nlongq;
+    long_postings_ = idx->n_long_b;
+    const bool any_long = nlongq > 0 && idx->n_long_b > 0;  // else no long x long pair exists
     if (nkeys == 0) return empty();
     if (nkeys >= (int64_t)0x7fffffff) throw Error(DSSG_ERR_CAPACITY, "search: more than 2^31 (cell, bucket) keys per batch");
     QRec *recs = (QRec *)rec_.ensure(sizeof(QRec) * (nqc + 1));
@@ -1551,12 +1583,13 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         DSS_HIP(hipMemsetAsync(work, 0, 4 * sizeof(uint32_t), s));
         ja.cap = (int64_t)out_cap_;
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
-        if (nblocks && q_owner)
-            hipLaunchKernelGGL(k_join<true>, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
-                               (const uint32_t *)sval, (const int32_t *)rown, (const UnitDesc *)units, oq, oe, work);
-        else if (nblocks)
-            hipLaunchKernelGGL(k_join<false>, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
-                               (const uint32_t *)sval, (const int32_t *)nullptr, (const UnitDesc *)units, oq, oe, work);
+        if (nblocks) {
+            auto kern = q_owner ? (any_long ? k_join<true, true> : k_join<true, false>)
+                                : (any_long ? k_join<false, true> : k_join<false, false>);
+            hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
+                               (const uint32_t *)sval, (const int32_t *)(q_owner ? rown : nullptr),
+                               (const UnitDesc *)units, oq, oe, work);
+        }
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
         unsigned long long tot[2] = {0, 0};
         DSS_HIP(hipMemcpyAsync(tot, counter, sizeof(tot), hipMemcpyDeviceToHost, s));

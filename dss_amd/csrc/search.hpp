@@ -8,6 +8,7 @@ struct dssg_index {
     int64_t n_reg = 0;    // of which on valid level-13 cells (dense lookup)
     int64_t n_cells = 0;  // distinct cells
     int64_t n_b = 0;      // time-bucketed postings (the join's working set)
+    int64_t n_long_b = 0; // of which of long footprints (b_meta 0x40)
     uint64_t cell_lo = 0, cell_hi = ~0ull;  // cell range of the postings held (shards)
     bool has_owner = false;
     // ---- plain postings, sorted by (cell, entity); regular first -------------
@@ -85,6 +86,9 @@ class SearchEngine {
     // timing mode only: runs, wave iterations (records x tiles), useful lane tests
     // timing mode only: output flushes, exact list merges (events, lanes)
     int64_t last_tagged() const { return tagged_; }  // long x long pair occurrences before the dedupe
+    // long queries in the last batch, long postings of its index (both > 0:
+    // the join ran its long x long tagging variant)
+    void last_longs(int64_t *lq, int64_t *lp) const { *lq = long_queries_; *lp = long_postings_; }
     void last_join_events(int64_t *flushes, int64_t *merges, int64_t *merge_lanes) const
     {
         *flushes = flushes_;
@@ -116,7 +120,7 @@ class SearchEngine {
     bool timing_ = false;
     double join_ms_ = 0;
     int64_t units_ = 0, keys_ = 0, runs_ = 0, iters_ = 0, tests_ = 0;
-    int64_t flushes_ = 0, merges_ = 0, merge_lanes_ = 0, tagged_ = 0;
+    int64_t flushes_ = 0, merges_ = 0, merge_lanes_ = 0, tagged_ = 0, long_queries_ = 0, long_postings_ = 0;
     hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
 };
 

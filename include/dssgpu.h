@@ -335,6 +335,11 @@ int dssg_search_counters(dssg_ctx *ctx, int64_t *keys, int64_t *units, int64_t *
  * timing on -- and the long x long pair occurrences that were deduplicated
  * after the join (always).  Any pointer may be NULL. */
 int dssg_join_events(dssg_ctx *ctx, int64_t *flushes, int64_t *merges, int64_t *merge_lanes, int64_t *tagged);
+/* Long footprints of the most recent search (cells outside one 8x8 level-13
+ * window): queries of the batch and bucketed postings of the index.  Only
+ * when both are non-zero can a long x long pair exist, and only then does
+ * the join run its tagging variant.  Any pointer may be NULL. */
+int dssg_join_longs(dssg_ctx *ctx, int64_t *long_queries, int64_t *long_postings);
 /* Roofline accounting for a device query batch: total postings the join
  * scans (sum of M_q) and distinct candidate entities before the
  * altitude/time filter (sum of D_q), SURVEY.md s8(d). */
