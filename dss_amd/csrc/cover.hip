@@ -195,20 +195,13 @@ __global__ void k_verts(int64_t nx, const uint32_t *vown, const int32_t *kind, c
     }
 }
 
-// One thread per vertex slot of a loop candidate (n >= 3 slots):
-//  * the (u,v) image of the vertex on the face of vertex 0 (the planar data
-//    k_setup keeps for single-face small loops) and whether edge (i, i+1) lies
-//    inside that face (any edge that does not clears the footprint's inner
-//    flag: not_inner[f] = 1);
-//  * polygons only: the fan triangle terms of loop.go
-//    surfaceIntegralFloat64(SignedArea) for the loop as given (fwd, slot i =
-//    triangle (v0, vi, vi+1)) and for its reversal (rev, triangle (v[n-1],
-//    v[n-1-i], v[n-2-i])), i = 1 .. n-2.  The fan origin never moves for
-//    loops whose vertices all lie within DSS_SURFACE_MAX_LENGTH of v0; any
-//    other loop, or an undecided sign, goes to the exact per-footprint path
-//    (fan_fail).
-__global__ void k_fan(int64_t nx, const uint32_t *vown, const int32_t *kind, const int64_t *nslots, const int64_t *xoff,
-                      const V3 *xyz, double *fwd, double *rev, uint8_t *fan_fail, double2 *uv, uint8_t *not_inner)
+// One thread per vertex slot of a loop candidate (n >= 3 slots): the (u,v)
+// image of the vertex on the face of vertex 0 (the planar data k_setup keeps
+// for single-face small loops) and whether edge (i, i+1) lies inside that
+// face (any edge that does not clears the footprint's inner flag:
+// not_inner[f] = 1).
+__global__ void k_fan(int64_t nx, const uint32_t *vown, const int64_t *nslots, const int64_t *xoff, const V3 *xyz,
+                      double2 *uv, uint8_t *not_inner)
 {
     const int64_t x = tid64();
     if (x >= nx) return;
@@ -222,25 +215,96 @@ __global__ void k_fan(int64_t nx, const uint32_t *vown, const int32_t *kind, con
     valid_face_xyz_to_uv(face0, p[i], u, v);  // = ClipToPaddedFace's same-face fast path
     uv[x] = make_double2(u, v);
     if (!edge_inside_face(p[i], p[i + 1 == n ? 0 : i + 1], face0)) not_inner[f] = 1;
-    if (kind[f] == DSSG_KIND_CIRCLE || i < 1 || i > n - 2) return;
-    bool fail = false;
-    const V3 a = p[0], b = p[i], c = p[i + 1];
-    fail |= angle(c, a) > DSS_SURFACE_MAX_LENGTH;
-    fwd[x] = fastp::signed_area(a, b, c, fail);
-    const V3 ra = p[n - 1], rb = p[n - 1 - i], rc = p[n - 2 - i];
-    fail |= angle(rc, ra) > DSS_SURFACE_MAX_LENGTH;
-    rev[x] = fastp::signed_area(ra, rb, rc, fail);
-    if (fail) fan_fail[f] = 1;
+}
+
+// Fan-term orientation of a non-circle loop (n >= 3 vertices).  loop.go Area
+// sums SignedArea over the fan (v0, vi, vi+1); when that sum is negative the
+// area wraps to ~4 pi, exceeds the cap and the loop is reversed (Q4), so only
+// the reversed fan's terms matter.  Each term is sign(det(a,b,c)) times the
+// triangle's spherical excess E, and tan(E/2) = |det| / (1 + a.b + b.c + c.a):
+// with every vertex within 0.05 rad of v0, E = |det|/2 to 0.2 %.  So
+// D = sum det / 2 predicts the sign of the sum whenever |D| exceeds 5 % of
+// sum |det| / 2 (plus an absolute floor far above rounding):
+//   omode 0: sum > 0 and the area far below the cap -> forward terms only;
+//   omode 1: sum < 0 -> reversed terms only (the forward area is ~4 pi);
+//   omode 2: undecided -> both, as loop.go computes them.
+// tcnt = fan triangles to evaluate (k_fan_area tasks).
+__global__ void k_orient(int64_t n, const int32_t *kind, const int64_t *nslots, const int64_t *xoff, const V3 *xyz,
+                         uint8_t *omode, int64_t *tcnt)
+{
+    const int64_t f = tid64();
+    if (f >= n) return;
+    const int nv = (int)nslots[f];
+    if (kind[f] == DSSG_KIND_CIRCLE || nv < 3) {
+        omode[f] = 2;
+        tcnt[f] = 0;
+        return;
+    }
+    const V3 *p = xyz + xoff[f];
+    const V3 a = p[0];
+    double d = 0, dabs = 0;
+    bool near = true;
+    V3 b = p[1];
+    near &= a.x * b.x + a.y * b.y + a.z * b.z >= 0.99875;  // cos(0.05)
+    for (int i = 1; i + 1 < nv; i++) {
+        const V3 c = p[i + 1];
+        near &= a.x * c.x + a.y * c.y + a.z * c.z >= 0.99875;
+        const double t = a.x * (b.y * c.z - b.z * c.y) + a.y * (b.z * c.x - b.x * c.z) + a.z * (b.x * c.y - b.y * c.x);
+        d += t;
+        dabs += __builtin_fabs(t);
+        b = c;
+    }
+    d *= 0.5;
+    dabs *= 0.5;
+    const double margin = 0.05 * dabs + 1e-13;
+    int m = 2;
+    if (near && d > margin && d * 1.1 * (DSS_EARTH_AREA_KM2 / (4 * DSS_PI)) < DSS_MAX_AREA_KM2) m = 0;
+    else if (near && d < -margin) m = 1;
+    omode[f] = (uint8_t)m;
+    tcnt[f] = (int64_t)(nv - 2) * (m == 2 ? 2 : 1);
+}
+
+// One thread per fan triangle (grid-stride over the T = toff[n] tasks of
+// k_orient): the loop.go surfaceIntegralFloat64(SignedArea) term of the loop
+// as given (fwd, slot i = triangle (v0, vi, vi+1)) or of its reversal (rev,
+// triangle (v[n-1], v[n-1-i], v[n-2-i])), i = 1 .. n-2.  The fan origin never
+// moves for loops whose vertices all lie within DSS_SURFACE_MAX_LENGTH of the
+// origin; any other loop, or an undecided sign, goes to the exact
+// per-footprint path (fan_fail).
+__global__ void k_fan_area(const int64_t *toff_end, const uint32_t *towner, const int64_t *toff, const uint8_t *omode,
+                           const int64_t *nslots, const int64_t *xoff, const V3 *xyz, double *fwd, double *rev,
+                           uint8_t *fan_fail)
+{
+    const int64_t T = *toff_end;
+    for (int64_t t = tid64(); t < T; t += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t f = towner[t];
+        const int n = (int)nslots[f];
+        const int k = n - 2;
+        int j = (int)(t - toff[f]);
+        const int m = omode[f];
+        const bool r = m == 1 || (m == 2 && j >= k);
+        if (m == 2 && j >= k) j -= k;
+        const int i = 1 + j;
+        const V3 *p = xyz + xoff[f];
+        const V3 a = r ? p[n - 1] : p[0], b = r ? p[n - 1 - i] : p[i], c = r ? p[n - 2 - i] : p[i + 1];
+        bool fail = angle(c, a) > DSS_SURFACE_MAX_LENGTH;
+        const double v = fastp::signed_area(a, b, c, fail);
+        (r ? rev : fwd)[xoff[f] + i] = v;
+        if (fail) fan_fail[f] = 1;
+    }
 }
 
 // loop.go Area from the precomputed fan terms (same summation order as
 // surfaceIntegralFloat64), then loopAreaKm2.  Fails over to the exact path
 // in the bands where Area consults IsNormalized.
-__device__ __forceinline__ double fan_area_km2(const double *t, int n, bool &fail)
+__device__ __forceinline__ double fan_area_km2(const double *t, int n, bool &fail, bool rev_only = false)
 {
     double area = 0;
     for (int i = 1; i + 1 < n; i++) area += t[i];
     const double max_error = DSS_TURN_ANGLE_ERR_PER_VERTEX * (double)n;
+    // omode 1 skipped the forward sum (~ -area): its IsNormalized band
+    // (|sum| < max_error) is excluded with a wide margin instead
+    if (rev_only) fail |= area < 100 * max_error;
     if (area < 0) area += 4 * DSS_PI;
     if (area > 4 * DSS_PI) area = 4 * DSS_PI;
     if (area < 0) area = 0;
@@ -273,7 +337,7 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
                                           uint8_t *flags, int32_t *nvx, double2 *uv, uint64_t *st_id, uint32_t *st_i,
                                           uint32_t *st_j, uint32_t *finfo, int64_t *ncand, uint4 *fbox,
                                           const double *fwd, const double *rev, const uint8_t *fan_fail,
-                                          const uint8_t *not_inner)
+                                          const uint8_t *not_inner, const uint8_t *omode)
 {
     bool fail = false;
     auto bail = [&]() {
@@ -333,9 +397,16 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
                 fail |= fan_fail[f] != 0;
             }
             l.n = nv;
-            origin_of<FAST>(l, fail);
-            if constexpr (FAST) area = fan_area_km2(fwd + xoff[f], nv, fail);
-            else area = area_km2_of<FAST>(l, fail);
+            int om = 2;  // k_orient: which fan terms exist (FAST)
+            if constexpr (FAST) om = omode[f];
+            if (om == 1) {
+                area = INFINITY;  // the forward sum is negative: ~4 pi, above the cap
+            } else {
+                origin_of<FAST>(l, fail);
+                if constexpr (FAST) area = fan_area_km2(fwd + xoff[f], nv, fail);
+                else area = area_km2_of<FAST>(l, fail);
+            }
+            if (FAST && om == 0 && area > DSS_MAX_AREA_KM2) fail = true;  // mispredicted: no reversed terms
             if (bail()) return;
             if (area > DSS_MAX_AREA_KM2) {  // Q4: reverse in place and rebuild
                 for (int i = 0, j = nv - 1; i < j; i++, j--) {
@@ -350,7 +421,7 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
                     }
                 }
                 origin_of<FAST>(l, fail);
-                if constexpr (FAST) area = fan_area_km2(rev + xoff[f], nv, fail);
+                if constexpr (FAST) area = fan_area_km2(rev + xoff[f], nv, fail, om == 1);
                 else area = area_km2_of<FAST>(l, fail);
                 if (bail()) return;
             }
@@ -460,7 +531,7 @@ __global__ __launch_bounds__(64) void k_setup(uint32_t *slow_list, unsigned int 
                         uint8_t *mode, uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx, double2 *uv,
                         uint64_t *st_id, uint32_t *st_i, uint32_t *st_j, uint32_t *finfo, int64_t *ncand,
                         uint4 *fbox, const double *fwd, const double *rev, const uint8_t *fan_fail,
-                        const uint8_t *not_inner, const uint32_t *perm)
+                        const uint8_t *not_inner, const uint8_t *omode, const uint32_t *perm)
 {
     int64_t f = tid64();
     if constexpr (FAST) {
@@ -470,11 +541,11 @@ __global__ __launch_bounds__(64) void k_setup(uint32_t *slow_list, unsigned int 
         for (int64_t i = f; i < (int64_t)*slow_n; i += (int64_t)gridDim.x * blockDim.x)
             setup_one<false>(slow_list[i], nullptr, nullptr, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out,
                              mode, origin_in, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, ncand, fbox, nullptr,
-                             nullptr, nullptr, nullptr);
+                             nullptr, nullptr, nullptr, nullptr);
         return;
     }
     setup_one<true>(f, slow_list, slow_n, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out, mode, origin_in,
-                    fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, ncand, fbox, fwd, rev, fan_fail, not_inner);
+                    fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, ncand, fbox, fwd, rev, fan_fail, not_inner, omode);
 }
 
 __device__ __forceinline__ int num_edges(uint8_t md, int nv) { return md == MODE_LOOP ? nv : (md == MODE_POLYLINE ? nv - 1 : 0); }
@@ -853,39 +924,34 @@ __global__ void k_cand_test(int64_t NC, const uint32_t *cand_f, const int64_t *c
     const uint32_t size = 1u << (kMaxLevel - kCoverLevel);
     const double ulo = st_to_uv((double)i / (double)kMaxSize), uhi = st_to_uv((double)(i + size) / (double)kMaxSize);
     const double vlo = st_to_uv((double)j / (double)kMaxSize), vhi = st_to_uv((double)(j + size) / (double)kMaxSize);
-    // loop.go IntersectsCell: padded edge test, else centre containment
+    // loop.go IntersectsCell: padded edge test, else centre containment.
+    // One pass over the edges does both: the padded test (stop at the first
+    // hit) and, for planar footprints, contains_node's ray cast from the
+    // centre on the same (u,v) edge images -- only used when no edge hits.
+    // uc < a.x + (vc - a.y)(b.x - a.x)/(b.y - a.y), multiplied through by
+    // (b.y - a.y): an edge that misses the padded cell crosses v = vc >= half
+    // a cell (1.2e-4) from uc, so the rounding (~1e-16 relative) cannot flip
+    // the comparison.
     const double pm = kFinePad;
-    bool in = false;
-    for (int e = 0; e < nv && !in; e++) {
-        const double2 a = up[e], b = up[e + 1 == nv ? 0 : e + 1];
-        in = edge_intersects_rect(a.x, a.y, b.x, b.y, ulo - pm, uhi + pm, vlo - pm, vhi + pm);
-    }
-    int64_t r = in ? 1 : 0;
-    if (!in) {
-        if (flags[f] & FL_PLANAR) {
-            // contains_node's planar ray cast, on the same (u,v) edge images
-            const double sz = (double)size;
-            const double half = 0.5 / (double)kMaxSize;
-            const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
-            bool par = false;
-            // uc < a.x + (vc - a.y)(b.x - a.x)/(b.y - a.y), multiplied through
-            // by (b.y - a.y): the edge misses the padded cell, so its crossing
-            // with v = vc is >= half a cell (1.2e-4) from uc and the rounding
-            // (~1e-16 relative) cannot flip the comparison
-            for (int e = 0; e < nv; e++) {
-                const double2 a = up[e], b = up[e + 1 == nv ? 0 : e + 1];
-                if ((a.y > vc) != (b.y > vc)) {
-                    const double d = b.y - a.y;
-                    const double lhs = (uc - a.x) * d, rhs = (vc - a.y) * (b.x - a.x);
-                    if (d > 0 ? lhs < rhs : lhs > rhs) par = !par;
-                }
-            }
-            r = ((origin_in[f] != 0) != par) ? 1 : 0;
-        } else {
-            r = 2;
+    const bool planar = (flags[f] & FL_PLANAR) != 0;
+    const double half = 0.5 / (double)kMaxSize, sz = (double)size;
+    const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
+    bool in = false, par = false;
+    double2 a = up[0];
+    for (int e = 0; e < nv; e++) {
+        const double2 b = up[e + 1 == nv ? 0 : e + 1];
+        if (edge_intersects_rect(a.x, a.y, b.x, b.y, ulo - pm, uhi + pm, vlo - pm, vhi + pm)) {
+            in = true;
+            break;
         }
+        if ((a.y > vc) != (b.y > vc)) {
+            const double d = b.y - a.y;
+            const double lhs = (uc - a.x) * d, rhs = (vc - a.y) * (b.x - a.x);
+            if (d > 0 ? lhs < rhs : lhs > rhs) par = !par;
+        }
+        a = b;
     }
-    kept[c] = r;
+    kept[c] = in ? 1 : planar ? (((origin_in[f] != 0) != par) ? 1 : 0) : 2;
 }
 
 // Undecided candidates: exact S2 containment of the cell centre.
@@ -987,6 +1053,9 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     double *fwd = fwd_.ensure(nx + 1), *rev = rev_.ensure(nx + 1);
     uint8_t *not_inner = ninner_.ensure(n + 1);
     uint32_t *perm = perm_.ensure(n + 1);
+    uint8_t *omode = omode_.ensure(n + 1);
+    int64_t *tcnt = tcnt_.ensure(n + 1), *toff = toff_.ensure(n + 2);
+    uint32_t *towner = towner_.ensure(2 * nx + 1);  // <= 2 (n - 2) tasks per loop
     DSS_HIP(hipMemsetAsync(slow_n, 0, sizeof(unsigned int), s));
     DSS_HIP(hipMemsetAsync(fan_fail, 0, n, s));
     DSS_HIP(hipMemsetAsync(not_inner, 0, n, s));
@@ -996,15 +1065,22 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     hipLaunchKernelGGL(k_vowner, dim3(grid_for(n, B)), dim3(B), 0, s, n, xoff, vown);
     if (nx > 0) {
         hipLaunchKernelGGL(k_verts, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, kind, voff, lat, lng, xoff, frames, xyz);
-        hipLaunchKernelGGL(k_fan, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, kind, nv, xoff, xyz,
-                           fwd, rev, fan_fail, uv, not_inner);
+        hipLaunchKernelGGL(k_fan, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, nv, xoff, xyz, uv, not_inner);
     }
+    // fan triangle terms of Loop.Area: orientation first, then one thread per
+    // triangle actually needed (no lanes idle on circles or on the orientation
+    // that is never summed)
+    hipLaunchKernelGGL(k_orient, dim3(grid_for(n, B)), dim3(B), 0, s, n, kind, nv, xoff, xyz, omode, tcnt);
+    exclusive_scan_i64(tcnt, toff, n, tmp_, s);
+    hipLaunchKernelGGL(k_vowner, dim3(grid_for(n, B)), dim3(B), 0, s, n, toff, towner);
+    hipLaunchKernelGGL(k_fan_area, dim3(std::min<int64_t>(grid_for(2 * nx + 1, B), 2048)), dim3(B), 0, s, toff + n,
+                       towner, toff, omode, nv, xoff, xyz, fwd, rev, fan_fail);
     hipLaunchKernelGGL(k_setup<true>, dim3(grid_for(n, 64)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng,
                        radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo,
-                       ncand, fbox, fwd, rev, fan_fail, not_inner, perm);
+                       ncand, fbox, fwd, rev, fan_fail, not_inner, omode, perm);
     hipLaunchKernelGGL(k_setup<false>, dim3(min(grid_for(n, 64), 512u)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat,
                        lng, radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j,
-                       finfo, ncand, fbox, nullptr, nullptr, nullptr, nullptr, nullptr);
+                       finfo, ncand, fbox, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
     int64_t *eoff = eoff_.ensure(n + 1);
     hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv);
     exclusive_scan_i64(nv, eoff, n, tmp_, s);

@@ -31,7 +31,9 @@ class CoverEngine {
     DevBuf<uint8_t> mode_, orig_, fmask_, flags_, cflags_, act_;
     DevBuf<uint32_t> slow_, vown_;
     DevBuf<uint8_t> fanf_, ninner_;
-    DevBuf<uint32_t> perm_;
+    DevBuf<uint32_t> perm_, towner_;
+    DevBuf<uint8_t> omode_;
+    DevBuf<int64_t> tcnt_, toff_;
     DevBuf<double> fwd_, rev_;
     DevBuf<unsigned char> frames_;
     DevBuf<unsigned int> slow_n_;

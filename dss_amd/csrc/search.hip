@@ -572,6 +572,8 @@ __global__ void k_qcells(IndexView a, QueryView qv, int64_t nqc, const uint32_t 
             gval[w] = (uint32_t)k;
             w++;
         }
+    } else {
+        return;  // no group met: no key refers to this record
     }
     // query record: near-only prefix signature of the query's cells before
     // k (prefix_sig semantics), compact flag, long flag (qlong)
