@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--mode", choices=["sharded", "replica"], default=None,
                     help="multi-GPU layout (default: sharded for N > 1, replica for N = 1)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on a multi-GPU node; gloo for rehearsals")
-    ap.add_argument("--pipelines", type=int, default=2,
+    ap.add_argument("--pipelines", type=int, default=3,
                     help="concurrent batch pipelines per GPU (own engine context + stream + host thread each): one "
                          "batch's FP64 covering overlaps another's join, as concurrent RPCs would (replica mode)")
     ap.add_argument("--same-device", action="store_true",

@@ -225,7 +225,7 @@ __global__ void k_fan(int64_t nx, const uint32_t *vown, const int64_t *nslots, c
 // with every vertex within 0.05 rad of v0, E = |det|/2 to 0.2 %.  So
 // D = sum det / 2 predicts the sign of the sum whenever |D| exceeds 5 % of
 // sum |det| / 2 (plus an absolute floor far above rounding):
-//   omode 0: sum > 0 and the area far below the cap -> forward terms only;
+//   omode 0: sum > 0 and the area (loopAreaKm2, Q1) below the cap -> forward terms only;
 //   omode 1: sum < 0 -> reversed terms only (the forward area is ~4 pi);
 //   omode 2: undecided -> both, as loop.go computes them.
 // tcnt = fan triangles to evaluate (k_fan_area tasks).
@@ -258,7 +258,7 @@ __global__ void k_orient(int64_t n, const int32_t *kind, const int64_t *nslots, 
     dabs *= 0.5;
     const double margin = 0.05 * dabs + 1e-13;
     int m = 2;
-    if (near && d > margin && d * 1.1 * (DSS_EARTH_AREA_KM2 / (4 * DSS_PI)) < DSS_MAX_AREA_KM2) m = 0;
+    if (near && d > margin && ((d * 1.1) * DSS_EARTH_AREA_KM2) / 4.0 * DSS_PI < DSS_MAX_AREA_KM2) m = 0;  // = fan_area_km2
     else if (near && d < -margin) m = 1;
     omode[f] = (uint8_t)m;
     tcnt[f] = (int64_t)(nv - 2) * (m == 2 ? 2 : 1);
@@ -315,6 +315,9 @@ __device__ __forceinline__ double fan_area_km2(const double *t, int n, bool &fai
 template <bool FAST>
 __device__ __forceinline__ void origin_of(LoopView &l, bool &fail)
 {
+#ifdef DSS_EXP_NO_ORIGIN  // timing experiment only (wrong coverings)
+    if constexpr (FAST) return;
+#endif
     if constexpr (FAST) fastp::loop_init_origin(l, fail);
     else loop_init_origin(l);
 }

@@ -115,3 +115,45 @@ def test_empty_batch():
     from dss_amd import geo
     res = geo.cover_batch(np.zeros(0, np.int32), np.zeros(1, np.int64), np.zeros(0), np.zeros(0), np.zeros(0))
     assert len(res.cells) == 0 and len(res.offs) == 1
+
+
+def _ring(clat, clng, r_deg, k, cw, jitter=None):
+    th = np.linspace(0, 2 * np.pi, k, endpoint=False)
+    rr = r_deg * (np.ones(k) if jitter is None else jitter)
+    la, lg = clat + rr * np.sin(th), clng + rr * np.cos(th) / np.cos(np.radians(clat))
+    return (la[::-1], lg[::-1]) if cw else (la, lg)
+
+
+def test_fan_orientation_edge_cases(oracle):
+    """k_orient's three cases against the oracle: loops whose fan-sum sign is
+    predicted (forward only / reversed only) and the undecided ones that
+    evaluate both fans -- near the 2500 km2 cap, beyond the 0.05 rad window,
+    bow-ties and spikes whose fan terms cancel, degenerate and repeated
+    vertices, down to metre-sized loops."""
+    from dss_amd import geo
+    rng = np.random.default_rng(404)
+    polys = []
+    for cw in (False, True):
+        for r_deg in (1e-5, 3e-4, 0.01, 0.2, 0.25, 0.27, 0.29, 2.0, 3.5):   # 1 m .. ~390 km
+            for k in (3, 4, 7, 12):
+                polys.append(_ring(37.5, -122.2, r_deg, k, cw))
+        # spiky stars: alternating radii, fan terms of both signs
+        for k in (8, 16, 30):
+            jit = np.where(np.arange(k) % 2 == 0, 1.0, rng.uniform(0.02, 0.2))
+            polys.append(_ring(37.5, -122.2, 0.02, k, cw, jit))
+    # bow-tie (self-intersecting: the fan terms cancel), collinear, repeated vertices
+    polys.append((np.array([37.0, 37.01, 37.0, 37.01]), np.array([-122.0, -121.99, -121.99, -122.0])))
+    polys.append((np.array([37.0, 37.005, 37.01]), np.array([-122.0, -121.995, -121.99])))
+    polys.append((np.array([37.0, 37.0, 37.01, 37.01, 37.0]), np.array([-122.0, -122.0, -121.99, -122.0, -122.0])))
+    polys.append((np.array([37.0, 37.01, 37.0, 37.0]), np.array([-122.0, -121.99, -121.98, -122.0])))
+    kind = np.zeros(len(polys), np.int32)
+    voff = np.zeros(len(polys) + 1, np.int64)
+    voff[1:] = np.cumsum([len(p[0]) for p in polys])
+    lat = np.concatenate([p[0] for p in polys])
+    lng = np.concatenate([p[1] for p in polys])
+    rad = np.zeros(len(polys), np.float32)
+    offs, cells, status, area = oracle.cover_batch(kind, voff, lat, lng, rad)
+    res = geo.cover_batch(kind, voff, lat, lng, rad)
+    _check_batch(dict(status=status, offs=offs, cells=cells, area_km2=area), res)
+    # both outcomes of the cap occur
+    assert (status == 0).any() and (status != 0).any()
