@@ -707,6 +707,9 @@ __global__ void k_work_stats(int64_t ng, const uint32_t *bk_start, const uint32_
     }
 }
 
+// LLVM compare predicates for __builtin_amdgcn_{s,u}icmp / fcmpf (wave masks)
+constexpr int kCmpOGE = 3, kCmpOLE = 5, kCmpEQ = 32, kCmpNE = 33, kCmpSGE = 39, kCmpSLE = 41;
+
 struct JoinArgs {
     IndexView ix;
     QueryView qv;
@@ -986,10 +989,13 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
 #pragma unroll
                         for (int k = 0; k < NS; k++) {
                             const Slot &sk = sl[k];
-                            // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels)
-                            bool p = (sk.t.y >= tlo) & (sk.t.x <= thi) & (sk.alt.y >= alo) & (sk.alt.x <= ahi);
-                            if (OWNER) p = p & ((own < 0) | (sk.own == own));
-                            const unsigned long long m = __ballot(p);
+                            // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels),
+                            // each compare straight to a wave mask (no bool -> VGPR -> ballot trip)
+                            unsigned long long m = __builtin_amdgcn_sicmpl(sk.t.y, tlo, kCmpSGE) &
+                                                   __builtin_amdgcn_sicmpl(sk.t.x, thi, kCmpSLE) &
+                                                   __builtin_amdgcn_fcmpf(sk.alt.y, alo, kCmpOGE) &
+                                                   __builtin_amdgcn_fcmpf(sk.alt.x, ahi, kCmpOLE);
+                            if (OWNER && own >= 0) m &= __builtin_amdgcn_sicmp(sk.own, own, kCmpEQ);
                             pm[k] = all_b ? m : (m & mb[k]);
                         }
                         // At the smallest shared cell only (SQL DISTINCT, Q13): a lane whose
@@ -1018,7 +1024,7 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                                     acc |= (uint32_t)(sk.s23.x >> 32) & (uint32_t)c3.y;
                                     acc |= (uint32_t)sk.s23.y & (uint32_t)c3.z;
                                     acc |= (uint32_t)(sk.s23.y >> 32) & (uint32_t)c3.w;
-                                    const unsigned long long ov = __ballot(acc != 0u);
+                                    const unsigned long long ov = __builtin_amdgcn_uicmp(acc, 0u, kCmpNE);
                                     pm[k] &= ~(need[k] & ov);
                                     // neither prefix compact means both footprints are long:
                                     // those lanes are tagged below, so this merge is a
