@@ -707,6 +707,12 @@ __global__ void k_work_stats(int64_t ng, const uint32_t *bk_start, const uint32_
     }
 }
 
+// Set bits of m below this lane (v_mbcnt_lo/hi: 2 VALU, no 64-bit and + popcounts).
+__device__ __forceinline__ uint32_t mbcnt64(unsigned long long m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // LLVM compare predicates for __builtin_amdgcn_{s,u}icmp / fcmpf (wave masks)
 constexpr int kCmpOGE = 3, kCmpOLE = 5, kCmpEQ = 32, kCmpNE = 33, kCmpSGE = 39, kCmpSLE = 41;
 
@@ -836,8 +842,7 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
     // loading lane's VGPRs and are broadcast with v_readlane; only the
     // prefix signatures (needed for a minority of records) go through LDS
     __shared__ int4 s_sig[kWaves][2][64];
-    __shared__ uint32_t sq[kWaves][kStage];
-    __shared__ uint32_t se[kWaves][kStage];
+    __shared__ uint2 sp[kWaves][kStage];  // staged (query, entity) pairs: one ds_write_b64 each
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int staged = 0;
@@ -859,8 +864,9 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
         for (int k = lane; k < staged; k += 64) {
             const unsigned long long o = base + (unsigned long long)k;
             if ((int64_t)o < a.cap) {
-                out_q[o] = sq[w][k];
-                out_e[o] = se[w][k];
+                const uint2 v = sp[w][k];
+                out_q[o] = v.x;
+                out_e[o] = v.y;
             }
         }
         staged = 0;
@@ -1071,13 +1077,11 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                         }
                         if (tot + ttot == 0) continue;
                         if (staged + tot + ttot > kStage) flush();
-                        const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
                         for (int k = 0; k < NS; k++) {
                             if ((pm[k] >> lane) & 1ull) {
-                                const int rk = staged + __popcll(pm[k] & below);
-                                sq[w][rk] = q;
-                                se[w][rk] = sl[k].ent;
+                                const int rk = staged + (int)mbcnt64(pm[k]);
+                                sp[w][rk] = make_uint2(q, sl[k].ent);
                             }
                             staged += __popcll(pm[k]);
                         }
@@ -1085,9 +1089,8 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
 #pragma unroll
                             for (int k = 0; k < NS; k++) {
                                 if ((tg[k] >> lane) & 1ull) {
-                                    const int rk = staged + __popcll(tg[k] & below);
-                                    sq[w][rk] = q | kTag;
-                                    se[w][rk] = sl[k].ent;
+                                    const int rk = staged + (int)mbcnt64(tg[k]);
+                                    sp[w][rk] = make_uint2(q | kTag, sl[k].ent);
                                 }
                                 staged += __popcll(tg[k]);
                             }
