@@ -13,6 +13,7 @@
 #include "common.hpp"
 #include "cover.hpp"
 #include "ingress.hpp"
+#include "radix.hpp"
 #include "route.hpp"
 #include "search.hpp"
 #include "store.hpp"
@@ -36,6 +37,7 @@ struct dssg_ctx {
     dss::DevBuf<double> d_lat, d_lng;
     dss::DevBuf<float> d_rad, d_alo, d_ahi;
     dss::DevBuf<uint64_t> d_cells;
+    dss::DevBuf<unsigned char> sort_tmp;
 };
 
 namespace {
@@ -815,6 +817,42 @@ int dssg_copy_to_host(dssg_ctx *ctx, void *dst, const void *src, size_t bytes)
     if (!ctx || (bytes && (!dst || !src))) return DSSG_ERR_INVALID;
     return guarded(ctx, [&] {
         if (bytes) DSS_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    });
+}
+
+int dssg_radix_sort_device(dssg_ctx *ctx, int key_bytes, int64_t n, int bits, const void *d_keys_in, void *d_keys_out,
+                           const uint32_t *d_vals_in, uint32_t *d_vals_out, void *stream, double *ms)
+{
+    if (!ctx || n < 0 || (key_bytes != 4 && key_bytes != 8) || bits < 0 || bits > 8 * key_bytes) return DSSG_ERR_INVALID;
+    if (n > 0 && (!d_keys_in || !d_keys_out || d_keys_in == d_keys_out || (!d_vals_in) != (!d_vals_out) ||
+                  (d_vals_in && d_vals_in == d_vals_out)))
+        return DSSG_ERR_INVALID;
+    if (key_bytes == 4 && !d_vals_in) return DSSG_ERR_INVALID;  // 32-bit keys are sorted with values only
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (ms) {
+            DSS_HIP(hipEventCreate(&e0));
+            DSS_HIP(hipEventCreate(&e1));
+            DSS_HIP(hipEventRecord(e0, s));
+        }
+        if (key_bytes == 8 && d_vals_in)
+            dss::radix_sort_pairs((const unsigned long *)d_keys_in, (unsigned long *)d_keys_out, d_vals_in, d_vals_out, n,
+                                  bits, ctx->sort_tmp, s);
+        else if (key_bytes == 8)
+            dss::radix_sort_keys((const unsigned long *)d_keys_in, (unsigned long *)d_keys_out, n, bits, ctx->sort_tmp, s);
+        else
+            dss::radix_sort_pairs((const uint32_t *)d_keys_in, (uint32_t *)d_keys_out, d_vals_in, d_vals_out, n, bits,
+                                  ctx->sort_tmp, s);
+        if (ms) {
+            DSS_HIP(hipEventRecord(e1, s));
+            DSS_HIP(hipEventSynchronize(e1));
+            float f = 0;
+            DSS_HIP(hipEventElapsedTime(&f, e0, e1));
+            *ms = f;
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+        }
     });
 }
 

@@ -12,11 +12,11 @@
 // is unspecified (quirk Q14), and every consumer treats it as a set.
 #include <hip/hip_runtime.h>
 
-#include <hipcub/hipcub.hpp>
 
 #include <cmath>
 
 #include "ingress.hpp"
+#include "radix.hpp"
 
 namespace dss {
 namespace {
@@ -132,10 +132,7 @@ void IngressEngine::union_volumes(CoverEngine &ce, int64_t nvol, const int64_t *
         // ~0 keys of footprint-less extents sort last within that range)
         int bits = 30;
         while (bits < 64 && ((unsigned long long)nvol >> (bits - 29)) != 0) bits++;
-        size_t bytes = 0;
-        DSS_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, k0, k1, (int)C, 0, bits, s));
-        tmp_.ensure(bytes + 16);
-        DSS_HIP(hipcub::DeviceRadixSort::SortKeys(tmp_.p, bytes, k0, k1, (int)C, 0, bits, s));
+        radix_sort_keys(k0, k1, C, bits, tmp_, s);
     }
     int64_t *flag = flag_.ensure(C + 1), *pos = pos_.ensure(C + 2);
     if (C > 0) hipLaunchKernelGGL(k_unique_flags, dim3(grid_for(C, kBlock)), dim3(kBlock), 0, s, C, k1, flag);

@@ -1,0 +1,314 @@
+// LSD radix sort, hand-written for gfx950 (wave64).  Replaces the CockroachDB
+// index ordering of `scd_cells_operations` (PK (cell_id, operation_id),
+// pkg/scd/store/cockroach/store.go:140-147) in the index build, and groups a
+// batch's (cell, bucket) keys before the join.
+//
+// Per pass over `rb` <= 8 digit bits (passes = ceil(bits / 8), digit width
+// balanced across passes), three launches:
+//   k_rs_hist    one 4096-key tile per block: per-wave LDS digit counts,
+//                written digit-major hist[d][tile] (so one row scan gives
+//                every tile its global start per digit);
+//   k_rs_scan    one block per digit: exclusive scan of its row in place,
+//                row total -> dtot[d];
+//   k_rs_scatter the same tile again: each wave ranks its 1024 keys by
+//                ballot match (rb ballots per 64 keys -> the lanes holding the
+//                same digit; rank = popcount of those below the lane) against
+//                a per-wave LDS digit counter, so the order stays stable
+//                (wave, iteration, lane) = input order; the block then places
+//                the keys digit-sorted in LDS and writes them out in tile
+//                order, so every digit's run leaves as a contiguous burst.
+// HBM per pass: 4n key bytes (hist) + (|K| + |V|) n read + (|K| + |V|) n
+// written, plus 4 * 2^rb * tiles of counts.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "radix.hpp"
+
+namespace dss {
+namespace {
+
+constexpr int kRBlock = 256;
+constexpr int kRWaves = kRBlock / 64;
+constexpr int kItems = 16;
+constexpr int kTile = kRBlock * kItems;  // 4096 keys per block
+constexpr int kWaveTile = 64 * kItems;   // 1024 keys per wave, contiguous
+
+template <typename K>
+__device__ __forceinline__ uint32_t digit_of(K k, int shift, uint32_t mask)
+{
+    return (uint32_t)(k >> shift) & mask;
+}
+
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Inclusive block scan of one value per thread; `total` = block sum.  Syncs
+// on entry use of ws and before returning, so ws can be reused at once.
+__device__ __forceinline__ uint32_t block_incl_scan(uint32_t x, uint32_t *ws, uint32_t &total)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) ws[w] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kRWaves; i++) {
+        const uint32_t t = ws[i];
+        pre += i < w ? t : 0u;
+        tot += t;
+    }
+    __syncthreads();
+    total = tot;
+    return x + pre;
+}
+
+template <typename K>
+__global__ __launch_bounds__(kRBlock) void k_rs_hist(const K *__restrict__ keys, int64_t n, int shift, int rbits,
+                                                     uint32_t *__restrict__ hist, int64_t stride)
+{
+    __shared__ uint32_t h[kRWaves][256];
+    const int tid = threadIdx.x, w = tid >> 6;
+    const uint32_t nd = 1u << rbits, mask = nd - 1;
+    for (int i = tid; i < kRWaves * 256; i += kRBlock) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    K k[kItems];
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        const int64_t i = base + j * kRBlock + tid;
+        k[j] = i < n ? keys[i] : K(0);
+    }
+#pragma unroll
+    for (int j = 0; j < kItems; j++)
+        if (base + j * kRBlock + tid < n) atomicAdd(&h[w][digit_of(k[j], shift, mask)], 1u);
+    __syncthreads();
+    for (int d = tid; d < (int)nd; d += kRBlock) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < kRWaves; i++) c += h[i][d];
+        hist[(int64_t)d * stride + blockIdx.x] = c;
+    }
+}
+
+__global__ __launch_bounds__(kRBlock) void k_rs_scan(uint32_t *__restrict__ hist, int64_t stride, int64_t ntiles,
+                                                     uint32_t *__restrict__ dtot)
+{
+    __shared__ uint32_t ws[kRWaves];
+    uint32_t *row = hist + (int64_t)blockIdx.x * stride;
+    uint32_t carry = 0;
+    for (int64_t b0 = 0; b0 < ntiles; b0 += kRBlock * 4) {
+        const int64_t i0 = b0 + (int64_t)threadIdx.x * 4;
+        uint32_t v[4], t = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            v[k] = i0 + k < ntiles ? row[i0 + k] : 0u;
+            t += v[k];
+        }
+        uint32_t total;
+        uint32_t run = carry + block_incl_scan(t, ws, total) - t;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (i0 + k < ntiles) row[i0 + k] = run;
+            run += v[k];
+        }
+        carry += total;
+    }
+    if (threadIdx.x == 0) dtot[blockIdx.x] = carry;
+}
+
+template <typename K, typename V, bool HAS_V>
+__global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki, const V *__restrict__ vi,
+                                                        K *__restrict__ ko, V *__restrict__ vo, int64_t n, int shift,
+                                                        int rbits, const uint32_t *__restrict__ hist, int64_t stride,
+                                                        const uint32_t *__restrict__ dtot)
+{
+    __shared__ uint32_t wh[kRWaves][256];  // per-wave digit counters, then their exclusive prefix over waves
+    __shared__ uint32_t dstart[256];       // tile-local start of each digit
+    __shared__ uint32_t gbase[256];        // global position of tile slot 0 of each digit
+    __shared__ uint32_t ws[kRWaves];
+    __shared__ K sk[kTile];
+    __shared__ V sv[HAS_V ? kTile : 1];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t nd = 1u << rbits, mask = nd - 1;
+    for (int i = tid; i < kRWaves * 256; i += kRBlock) (&wh[0][0])[i] = 0;
+    // global start of digit `tid` in this tile: all smaller digits + this
+    // digit in earlier tiles
+    const uint32_t dt = (uint32_t)tid < nd ? dtot[tid] : 0u;
+    uint32_t unused;
+    const uint32_t dexcl = block_incl_scan(dt, ws, unused) - dt;
+    const uint32_t gstart = (uint32_t)tid < nd ? dexcl + hist[(int64_t)tid * stride + blockIdx.x] : 0u;
+
+    const int64_t sub = (int64_t)blockIdx.x * kTile + (int64_t)w * kWaveTile;
+    K k[kItems];
+    V v[kItems];
+    uint32_t loc[kItems];
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        const int64_t i = sub + j * 64 + lane;
+        const bool ok = i < n;
+        k[j] = ok ? ki[i] : K(0);
+        if (HAS_V) v[j] = ok ? vi[i] : V(0);
+    }
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        const bool ok = sub + j * 64 + lane < n;
+        const uint32_t d = digit_of(k[j], shift, mask);
+        unsigned long long m = __ballot(ok);
+        for (int b = 0; b < rbits; b++) {
+            const unsigned long long bb = __ballot((d >> b) & 1u);
+            m &= ((d >> b) & 1u) ? bb : ~bb;
+        }
+        // every lane reads its digit's counter before the run's last lane
+        // bumps it (one wave, program order)
+        const uint32_t before = wh[w][d];
+        const uint32_t rank = lanes_below(m);
+        const uint32_t cnt = (uint32_t)__popcll(m);
+        if (ok && rank + 1 == cnt) wh[w][d] = before + cnt;
+        loc[j] = before + rank;
+    }
+    __syncthreads();
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int i = 0; i < kRWaves; i++) {
+        const uint32_t t = wh[i][tid];
+        wh[i][tid] = cnt;
+        cnt += t;
+    }
+    const uint32_t st = block_incl_scan(cnt, ws, unused) - cnt;
+    dstart[tid] = st;
+    gbase[tid] = gstart - st;  // modular: gbase + slot lands in [gstart, gstart + cnt)
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        if (sub + j * 64 + lane < n) {
+            const uint32_t d = digit_of(k[j], shift, mask);
+            const uint32_t slot = dstart[d] + wh[w][d] + loc[j];
+            sk[slot] = k[j];
+            if (HAS_V) sv[slot] = v[j];
+        }
+    }
+    __syncthreads();
+    const int64_t rem = n - (int64_t)blockIdx.x * kTile;
+    const int tile_n = rem < kTile ? (int)rem : kTile;
+    for (int i = tid; i < tile_n; i += kRBlock) {
+        const K kk = sk[i];
+        const uint32_t p = gbase[digit_of(kk, shift, mask)] + (uint32_t)i;
+        ko[p] = kk;
+        if (HAS_V) vo[p] = sv[i];
+    }
+}
+
+// OR over all keys of (key ^ keys[0]): the bits that vary.  Bits constant
+// across the batch need no pass (a level-13 cell id varies in bits 35..63
+// only, so a 64-bit (cell, entity) sort runs 4 passes instead of 8).
+template <typename K>
+__global__ __launch_bounds__(kRBlock) void k_rs_varying(const K *__restrict__ keys, int64_t n,
+                                                        unsigned long long *__restrict__ out)
+{
+    const K k0 = keys[0];
+    unsigned long long acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kRBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kRBlock)
+        acc |= (unsigned long long)(keys[i] ^ k0);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc |= __shfl_xor(acc, off, 64);
+    if ((threadIdx.x & 63) == 0 && acc) atomicOr(out, acc);
+}
+
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+template <typename K, typename V, bool HAS_V>
+void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, int bits, DevBuf<unsigned char> &tmp, hipStream_t s)
+{
+    if (n <= 0) return;
+    if (n >= ((int64_t)1 << 31)) throw Error(DSSG_ERR_CAPACITY, "radix sort: more than 2^31 keys");
+    const int kbits = (int)(8 * sizeof(K));
+    if (bits > kbits) bits = kbits;
+    if (bits <= 0) {
+        DSS_HIP(hipMemcpyAsync(ko, ki, sizeof(K) * n, hipMemcpyDeviceToDevice, s));
+        if (HAS_V) DSS_HIP(hipMemcpyAsync(vo, vi, sizeof(V) * n, hipMemcpyDeviceToDevice, s));
+        return;
+    }
+    const int64_t ntiles = (n + kTile - 1) / kTile, stride = (ntiles + 3) & ~(int64_t)3;
+    const size_t hist_b = align256(sizeof(uint32_t) * 256 * stride), dtot_b = align256(sizeof(uint32_t) * 256);
+    // wide keys: sort only the span of bits that vary (one read + one host
+    // sync, against up to 4 passes saved)
+    int lo = 0;
+    if (bits > 24) {
+        unsigned long long *vm = (unsigned long long *)tmp.ensure(hist_b + dtot_b) + 0;
+        DSS_HIP(hipMemsetAsync(vm, 0, sizeof(unsigned long long), s));
+        const int64_t g = std::min<int64_t>(ntiles, 2048);
+        hipLaunchKernelGGL(k_rs_varying<K>, dim3((unsigned)g), dim3(kRBlock), 0, s, ki, n, vm);
+        unsigned long long var = 0;
+        DSS_HIP(hipMemcpyAsync(&var, vm, sizeof(var), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipStreamSynchronize(s));
+        if (bits < 64) var &= (1ull << bits) - 1;
+        if (var == 0) bits = 0;  // every key equal on the sorted bits: stable = identity
+        else {
+            lo = __builtin_ctzll(var);
+            bits = 64 - __builtin_clzll(var);
+        }
+    }
+    if (bits <= lo) {
+        DSS_HIP(hipMemcpyAsync(ko, ki, sizeof(K) * n, hipMemcpyDeviceToDevice, s));
+        if (HAS_V) DSS_HIP(hipMemcpyAsync(vo, vi, sizeof(V) * n, hipMemcpyDeviceToDevice, s));
+        return;
+    }
+    const int span = bits - lo, passes = (span + 7) / 8, rb = (span + passes - 1) / passes;
+    const size_t ka_b = passes > 1 ? align256(sizeof(K) * n) : 0, va_b = passes > 1 && HAS_V ? align256(sizeof(V) * n) : 0;
+    unsigned char *t = tmp.ensure(hist_b + dtot_b + ka_b + va_b);
+    uint32_t *hist = (uint32_t *)t, *dtot = (uint32_t *)(t + hist_b);
+    K *kalt = (K *)(t + hist_b + dtot_b);
+    V *valt = (V *)(t + hist_b + dtot_b + ka_b);
+    const K *src = ki;
+    const V *srcv = vi;
+    for (int p = 0; p < passes; p++) {
+        const int shift = lo + p * rb, r = bits - shift < rb ? bits - shift : rb;
+        // the last pass lands in ko; earlier ones alternate ko / kalt backwards
+        const bool to_out = ((passes - 1 - p) & 1) == 0;
+        K *dst = to_out ? ko : kalt;
+        V *dstv = to_out ? vo : valt;
+        hipLaunchKernelGGL(k_rs_hist<K>, dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src, n, shift, r, hist, stride);
+        hipLaunchKernelGGL(k_rs_scan, dim3(1u << r), dim3(kRBlock), 0, s, hist, stride, ntiles, dtot);
+        hipLaunchKernelGGL((k_rs_scatter<K, V, HAS_V>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src, srcv, dst, dstv,
+                           n, shift, r, hist, stride, dtot);
+        DSS_HIP(hipGetLastError());
+        src = dst;
+        srcv = dstv;
+    }
+}
+
+}  // namespace
+
+template <typename K, typename V>
+void radix_sort_pairs(const K *ki, K *ko, const V *vi, V *vo, int64_t n, int bits, DevBuf<unsigned char> &tmp,
+                      hipStream_t s)
+{
+    radix_sort<K, V, true>(ki, ko, vi, vo, n, bits, tmp, s);
+}
+
+template <typename K>
+void radix_sort_keys(const K *ki, K *ko, int64_t n, int bits, DevBuf<unsigned char> &tmp, hipStream_t s)
+{
+    radix_sort<K, uint32_t, false>(ki, ko, nullptr, nullptr, n, bits, tmp, s);
+}
+
+template void radix_sort_pairs<unsigned long, uint32_t>(const unsigned long *, unsigned long *, const uint32_t *,
+                                                        uint32_t *, int64_t, int, DevBuf<unsigned char> &, hipStream_t);
+template void radix_sort_pairs<uint32_t, uint32_t>(const uint32_t *, uint32_t *, const uint32_t *, uint32_t *, int64_t,
+                                                   int, DevBuf<unsigned char> &, hipStream_t);
+template void radix_sort_pairs<uint32_t, unsigned long>(const uint32_t *, uint32_t *, const unsigned long *,
+                                                        unsigned long *, int64_t, int, DevBuf<unsigned char> &,
+                                                        hipStream_t);
+template void radix_sort_keys<unsigned long long>(const unsigned long long *, unsigned long long *, int64_t, int,
+                                                  DevBuf<unsigned char> &, hipStream_t);
+template void radix_sort_keys<unsigned long>(const unsigned long *, unsigned long *, int64_t, int,
+                                             DevBuf<unsigned char> &, hipStream_t);
+
+}  // namespace dss

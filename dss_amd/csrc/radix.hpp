@@ -1,0 +1,19 @@
+// Hand-written LSD radix sort for the index build and the per-batch key
+// grouping (north_star "LDS-tiled radix sort of 64-bit
+// cell IDs with wavefront ballot/prefix-scan compaction").  Stable, sorts the
+// low `bits` bits of unsigned keys ascending; ki/vi are left untouched and the
+// result lands in ko/vo (hipCUB DeviceRadixSort argument meaning, so the call
+// sites read the same).  n < 2^31.
+#pragma once
+#include "common.hpp"
+
+namespace dss {
+
+template <typename K, typename V>
+void radix_sort_pairs(const K *ki, K *ko, const V *vi, V *vo, int64_t n, int bits, DevBuf<unsigned char> &tmp,
+                      hipStream_t s);
+
+template <typename K>
+void radix_sort_keys(const K *ki, K *ko, int64_t n, int bits, DevBuf<unsigned char> &tmp, hipStream_t s);
+
+}  // namespace dss

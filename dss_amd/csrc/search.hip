@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "index_view.cuh"
+#include "radix.hpp"
 #include "search.hpp"
 
 namespace dss {
@@ -1186,11 +1187,7 @@ __global__ __launch_bounds__(kBlock) void k_stats(IndexView a, QueryView qv, uns
 template <typename K, typename V>
 void sort_pairs(const K *ki, K *ko, const V *vi, V *vo, int64_t n, int bits, DevBuf<unsigned char> &tmp, hipStream_t s)
 {
-    if (n <= 0) return;
-    size_t bytes = 0;
-    DSS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, ki, ko, vi, vo, (int)n, 0, bits, s));
-    tmp.ensure(bytes + 16);
-    DSS_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, bytes, ki, ko, vi, vo, (int)n, 0, bits, s));
+    radix_sort_pairs(ki, ko, vi, vo, n, bits, tmp, s);  // radix.hip
 }
 
 int bits_for(int64_t n)
@@ -1630,10 +1627,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             hipLaunchKernelGGL(k_tag_mark, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, oq, flag);
             exclusive_scan_i64(flag, pos, n, tmp_, s);
             hipLaunchKernelGGL(k_tag_split, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, oq, oe, pos, q2, e2, k1);
-            size_t bytes = 0;
-            DSS_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, k1, k2, (int)nt, 0, 64, s));
-            tmp_.ensure(bytes + 16);
-            DSS_HIP(hipcub::DeviceRadixSort::SortKeys(tmp_.p, bytes, k1, k2, (int)nt, 0, 64, s));
+            radix_sort_keys(k1, k2, nt, 64, tmp_, s);
             hipLaunchKernelGGL(k_tag_flags, dim3(grid_for(nt, kBlock)), dim3(kBlock), 0, s, nt, k2, flag);
             exclusive_scan_i64(flag, pos, nt, tmp_, s);
             nout = n - nt;

@@ -20,9 +20,9 @@
 //    stored array (RID `unnest(cells)`) -- p_mult.
 #include <hip/hip_runtime.h>
 
-#include <hipcub/hipcub.hpp>
 
 #include "index_view.cuh"
+#include "radix.hpp"
 #include "subs.hpp"
 
 namespace dss {
@@ -197,11 +197,7 @@ void SubsEngine::notify(dssg_index *idx, const dssg_pairs *p, hipStream_t s, uin
     int64_t *ov = v_.ensure(n + 1);
     if (n > 0) {
         hipLaunchKernelGGL(k_pair_keys, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, p->q, p->e, k0);
-        size_t bytes = 0;
-        const int bits = 32 + bits_for_n(idx->n_e);
-        DSS_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, k0, k1, (int)n, 0, bits, s));
-        tmp_.ensure(bytes + 16);
-        DSS_HIP(hipcub::DeviceRadixSort::SortKeys(tmp_.p, bytes, k0, k1, (int)n, 0, bits, s));
+        radix_sort_keys(k0, k1, n, 32 + bits_for_n(idx->n_e), tmp_, s);
         hipLaunchKernelGGL(k_notify_values, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, k1, idx->e_notify.p, oq, oe, ov);
         hipLaunchKernelGGL(k_notify_commit, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, k1, ov, idx->e_notify.p);
     }

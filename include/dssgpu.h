@@ -348,6 +348,14 @@ int dssg_search_stats_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, c
 /* Copy `bytes` from an engine-owned device buffer (dssg_cells / dssg_pairs)
  * to host memory, on the context's device. */
 int dssg_copy_to_host(dssg_ctx *ctx, void *dst, const void *src, size_t bytes);
+/* Stable LSD radix sort of n device-resident unsigned keys on their low
+ * `bits` bits (key_bytes 4 or 8), values (u32, or NULL for keys only)
+ * carried along -- the hand-written sort of the index build and the
+ * per-batch key grouping (radix.hip), exported for parity tests and the
+ * sort-phase roofline.  In and out buffers are distinct.  With ms != NULL
+ * the call waits and reports the sort's duration (HIP events on `stream`). */
+int dssg_radix_sort_device(dssg_ctx *ctx, int key_bytes, int64_t n, int bits, const void *d_keys_in, void *d_keys_out,
+                           const uint32_t *d_vals_in, uint32_t *d_vals_out, void *stream, double *ms);
 /* Evaluate the device restatement of a Go math routine on n inputs
  * (op: 0 sin, 1 cos, 2 tan, 3 atan, 4 atan2(x, y), 5 asin, 6 sqrt, 7 x/y,
  * 8 stToUV, 9 uvToST, 10 PointFromLatLng(x, y).X) -- for bit-exact tests. */
