@@ -45,7 +45,7 @@ def log(*a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=1)
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug only; invalid for the metric)")
@@ -121,6 +121,7 @@ def main():
     i_offs_h = D.copy_back(ctx, icells.offs, ni + 1, np.int64)
     i_cells_h = D.copy_back(ctx, icells.cells, int(i_offs_h[-1]), np.uint64)
     log(f"[rank {rank}] mode {mode}, setup {time.time() - t_setup:.1f}s, index build {build_s:.2f}s, postings {n_post}")
+    sort_ph = sort_phase(ctx, torch, dev, i_offs_h, i_cells_h) if rank == 0 and mode != "sharded" else None
     sharded = None
     if mode == "sharded":
         sharded = shard.ShardedSearch(ctx, index, ranges, stage_host=stage_host)
@@ -138,19 +139,32 @@ def main():
 
     # extra pipelines: each its own context (engine scratch), stream and host
     # thread, so one batch's cover overlaps another's join
+    import threading
     workers = []
     if args.pipelines > 1 and sharded is None:
-        import threading
         for k in range(args.pipelines - 1):
             wctx = _lib.Context(local)
             wstream = torch.cuda.Stream(device=dev)
             workers.append((wctx, wstream))
 
-    def run_steps(wctx, wstream, n):
+    tickets = [0]
+    ticket_lock = threading.Lock() if workers else None
+
+    def take_ticket():
+        # the K timed steps are handed out one at a time, so no pipeline idles
+        # while another still has a queue of steps (the tail is <= one step)
+        with ticket_lock:
+            t = tickets[0]
+            tickets[0] += 1
+        return t < args.steps
+
+    def run_steps(wctx, wstream, n=None):
         with torch.cuda.stream(wstream):
-            for _ in range(n):
+            while (take_ticket() if n is None else n > 0):
                 c = D.cover(wctx, d_q)
                 D.search(wctx, index, c, q_alo, q_ahi, q_tlo, q_thi)
+                if n is not None:
+                    n -= 1
             wstream.synchronize()
 
     for wctx, wstream in workers:  # warm the extra contexts
@@ -162,13 +176,10 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if workers:
-        share = [args.steps // args.pipelines + (1 if k < args.steps % args.pipelines else 0)
-                 for k in range(args.pipelines)]
-        threads = [threading.Thread(target=run_steps, args=(wctx, wstream, share[k + 1]))
-                   for k, (wctx, wstream) in enumerate(workers)]
+        threads = [threading.Thread(target=run_steps, args=(wctx, wstream)) for wctx, wstream in workers]
         for th in threads:
             th.start()
-        for _ in range(share[0]):
+        while take_ticket():
             cells, pairs = step()
         for th in threads:
             th.join()
@@ -269,6 +280,7 @@ def main():
                           "long_pair_occurrences": n_tg.value, "long_queries": n_lq.value,
                           "long_postings": n_lp.value},
             "index_build_s": build_s,
+            "sort_phase": sort_ph,
             "roofline": {"kernel": "k_join (overlap join + fused altitude/time filter)", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
@@ -391,6 +403,34 @@ def sharded_report(args, ctx, D, dist, torch, sh, step, full, i_cells_h, ranges,
         "parity": parity,
     }
     print(json.dumps(result), flush=True)
+
+
+def sort_phase(ctx, torch, dev, i_offs, i_cells):
+    """Sort-phase roofline: the index build's (cell, entity)
+    radix sort (radix.hip) on this airspace's own postings, timed with HIP
+    events on the library's stream.  Algorithmic bytes: 24 B per posting
+    (8 B key + 4 B payload, read and written once)."""
+    import ctypes as C
+    P = len(i_cells)
+    if P == 0:
+        return None
+    keys = torch.as_tensor(i_cells.view(np.int64), device=dev)
+    vals = torch.as_tensor(np.repeat(np.arange(len(i_offs) - 1, dtype=np.int32), np.diff(i_offs)), device=dev)
+    ko, vo = torch.empty_like(keys), torch.empty_like(vals)
+    torch.cuda.synchronize()
+    ms = C.c_double(0)
+    times = []
+    for _ in range(6):
+        ctx.check(ctx.L.dssg_radix_sort_device(ctx.h, 8, P, 64, C.c_void_p(keys.data_ptr()), C.c_void_p(ko.data_ptr()),
+                                               C.c_void_p(vals.data_ptr()), C.c_void_p(vo.data_ptr()), None,
+                                               C.byref(ms)))
+        times.append(ms.value)
+    t = float(np.median(times[1:]))
+    alg = 24 * P
+    return {"kernel": "radix sort of (cell, entity) postings (k_rs_hist/k_rs_scan/k_rs_scatter)", "bound": "hbm",
+            "postings": P, "ms": t, "achieved": alg / t / 1e6, "peak": 8000.0, "unit": "GB/s",
+            "frac": alg / t / 1e6 / 8000.0, "algorithmic_bytes": alg,
+            "note": "level-13 ids vary in bits 35..63 only: 4 digit passes of <= 8 bits"}
 
 
 def touched_postings(i_cells, q_cells):

@@ -902,15 +902,14 @@ __device__ __forceinline__ void cand_cell(int64_t c, uint32_t f, const int64_t *
     id = sid - lsb_for_level(L) + lsb13 + (uint64_t)r * (lsb13 << 1);  // cellid.go ChildBeginAtLevel + r steps
 }
 
-// kept: 0 / 1, or 2 = undecided (centre containment needs the exact S2 test,
-// done by k_cand_exact so that this kernel stays register-light).
-__global__ void k_cand_test(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
-                            const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const uint4 *fbox,
-                            const int64_t *xoff, const double2 *uv, const int32_t *nvx, const uint8_t *origin_in,
-                            const uint8_t *flags, int64_t *kept)
+// Candidate c's verdict: 0 / 1, or 2 = undecided (centre containment needs
+// the exact S2 test, done by k_cand_exact so that this one stays
+// register-light).
+__device__ __forceinline__ int cand_decide(int64_t c, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
+                                           const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo,
+                                           const uint4 *fbox, const int64_t *xoff, const double2 *uv, const int32_t *nvx,
+                                           const uint8_t *origin_in, const uint8_t *flags)
 {
-    const int64_t c = tid64();
-    if (c >= NC) return;
     const uint32_t f = cand_f[c];
     int face;
     uint32_t i, j;
@@ -918,10 +917,7 @@ __global__ void k_cand_test(int64_t NC, const uint32_t *cand_f, const int64_t *c
     cand_cell(c, f, coff, st_id, st_i, st_j, finfo, face, i, j, id);
     const uint4 bx = fbox[f];
     const uint32_t i13 = i >> (kMaxLevel - kCoverLevel), j13 = j >> (kMaxLevel - kCoverLevel);
-    if (i13 < bx.x || i13 > bx.y || j13 < bx.z || j13 > bx.w) {
-        kept[c] = 0;
-        return;
-    }
+    if (i13 < bx.x || i13 > bx.y || j13 < bx.z || j13 > bx.w) return 0;
     const int nv = nvx[f];
     const double2 *up = uv + xoff[f];
     const uint32_t size = 1u << (kMaxLevel - kCoverLevel);
@@ -954,48 +950,91 @@ __global__ void k_cand_test(int64_t NC, const uint32_t *cand_f, const int64_t *c
         }
         a = b;
     }
-    kept[c] = in ? 1 : planar ? (((origin_in[f] != 0) != par) ? 1 : 0) : 2;
+    return in ? 1 : planar ? (((origin_in[f] != 0) != par) ? 1 : 0) : 2;
 }
 
-// Undecided candidates: exact S2 containment of the cell centre.
-__global__ __launch_bounds__(256) void k_cand_exact(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
-                             const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const int64_t *xoff,
-                             const V3 *xyz, const int32_t *nvx, const uint8_t *origin_in, int64_t *kept)
+// Verdicts leave as two ballot masks per wave of 64 candidates (kept, and
+// undecided): 16 B per 64 candidates instead of a per-candidate word, and
+// the compaction below ranks by popcount, with no candidate-sized scan.
+__global__ void k_cand_test(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
+                            const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const uint4 *fbox,
+                            const int64_t *xoff, const double2 *uv, const int32_t *nvx, const uint8_t *origin_in,
+                            const uint8_t *flags, unsigned long long *kmask, unsigned long long *umask)
 {
     const int64_t c = tid64();
-    if (c >= NC || kept[c] != 2) return;
-    const uint32_t f = cand_f[c];
-    int face;
-    uint32_t i, j;
-    uint64_t id;
-    cand_cell(c, f, coff, st_id, st_i, st_j, finfo, face, i, j, id);
-    LoopView l{xyz + xoff[f], nvx[f], origin_in[f] != 0};
-    kept[c] = loop_contains(l, node_center(face, i, j, kCoverLevel)) ? 1 : 0;
+    if (c - (threadIdx.x & 63) >= NC) return;  // whole wave past the end
+    const int v = c < NC ? cand_decide(c, cand_f, coff, st_id, st_i, st_j, finfo, fbox, xoff, uv, nvx, origin_in, flags) : 0;
+    const unsigned long long k = __ballot(v == 1), u = __ballot(v == 2);
+    if ((threadIdx.x & 63) == 0) {
+        kmask[c >> 6] = k;
+        umask[c >> 6] = u;
+    }
+}
+
+// Undecided candidates: exact S2 containment of the cell centre; the wave
+// that owns a mask word folds its results into it.
+__global__ __launch_bounds__(256) void k_cand_exact(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
+                             const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const int64_t *xoff,
+                             const V3 *xyz, const int32_t *nvx, const uint8_t *origin_in, unsigned long long *kmask,
+                             const unsigned long long *umask)
+{
+    const int64_t c = tid64();
+    if (c - (threadIdx.x & 63) >= NC) return;
+    const unsigned long long um = umask[c >> 6];
+    if (um == 0) return;  // wave-uniform
+    bool in = false;
+    if ((um >> (threadIdx.x & 63)) & 1ull) {
+        const uint32_t f = cand_f[c];
+        int face;
+        uint32_t i, j;
+        uint64_t id;
+        cand_cell(c, f, coff, st_id, st_i, st_j, finfo, face, i, j, id);
+        LoopView l{xyz + xoff[f], nvx[f], origin_in[f] != 0};
+        in = loop_contains(l, node_center(face, i, j, kCoverLevel));
+    }
+    const unsigned long long m = __ballot(in);
+    if ((threadIdx.x & 63) == 0) kmask[c >> 6] |= m;
+}
+
+__global__ void k_mask_counts(int64_t G, const unsigned long long *kmask, int64_t *gcnt)
+{
+    const int64_t g = tid64();
+    if (g < G) gcnt[g] = __popcll(kmask[g]);
+}
+
+// Kept candidates before candidate c (c <= NC): group prefix + popcount.
+__device__ __forceinline__ int64_t kept_rank(int64_t c, const unsigned long long *kmask, const int64_t *gpos)
+{
+    const int64_t g = c >> 6;
+    const int r = (int)(c & 63);
+    return gpos[g] + (r ? __popcll(kmask[g] & ((1ull << r) - 1)) : 0);
 }
 
 // Per-footprint cell counts: direct-path count from the candidate scan plus
 // the descent count the item atomics left in dcnt.
-__global__ void k_counts(int64_t n, const int64_t *coff, const int64_t *kpos, const unsigned long long *dcnt,
-                         int64_t *total, int64_t *dc64)
+__global__ void k_counts(int64_t n, const int64_t *coff, const unsigned long long *kmask, const int64_t *gpos,
+                         const unsigned long long *dcnt, int64_t *total, int64_t *dc64)
 {
     int64_t f = tid64();
     if (f >= n) return;
-    total[f] = (kpos[coff[f + 1]] - kpos[coff[f]]) + (int64_t)dcnt[f];
+    total[f] = (kept_rank(coff[f + 1], kmask, gpos) - kept_rank(coff[f], kmask, gpos)) + (int64_t)dcnt[f];
     dc64[f] = (int64_t)dcnt[f];
 }
 
 __global__ void k_cand_emit(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
-                            const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const int64_t *kept,
-                            const int64_t *kpos, const int64_t *offs, uint64_t *cells)
+                            const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo,
+                            const unsigned long long *kmask, const int64_t *gpos, const int64_t *offs, uint64_t *cells)
 {
     const int64_t c = tid64();
-    if (c >= NC || !kept[c]) return;
+    if (c >= NC) return;
+    const unsigned long long km = kmask[c >> 6];
+    if (!((km >> (c & 63)) & 1ull)) return;
     const uint32_t f = cand_f[c];
     int face;
     uint32_t i, j;
     uint64_t id;
     cand_cell(c, f, coff, st_id, st_i, st_j, finfo, face, i, j, id);
-    cells[offs[f] + (kpos[c] - kpos[coff[f]])] = id;
+    cells[offs[f] + (kept_rank(c, kmask, gpos) - kept_rank(coff[f], kmask, gpos))] = id;
 }
 
 __global__ void k_u64_to_i64(int64_t n, const unsigned long long *a, int64_t *b)
@@ -1095,15 +1134,20 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     const int64_t ne = h2[0], NC = h2[1];
     // direct candidates (most footprints): test now, compact after the counts
     uint32_t *cand_f = cand_f_.ensure(NC + 1);
-    int64_t *kept = kept_.ensure(NC + 1), *kpos = kpos_.ensure(NC + 2);
+    const int64_t G = (NC + 63) / 64;  // mask words; kept_rank(NC) reads word G
+    unsigned long long *kmask = kmask_.ensure(2 * (G + 1)), *umask = kmask + (G + 1);
+    int64_t *gcnt = gcnt_.ensure(G + 1), *gpos = gpos_.ensure(G + 2);
+    DSS_HIP(hipMemsetAsync(kmask + G, 0, sizeof(unsigned long long), s));
     if (NC > 0) {
         hipLaunchKernelGGL(k_cand_owner, dim3(grid_for(n, B)), dim3(B), 0, s, n, coff, cand_f);
         hipLaunchKernelGGL(k_cand_test, dim3(grid_for(NC, kCandBlock)), dim3(kCandBlock), 0, s, NC, cand_f, coff, st_id,
-                           st_i, st_j, finfo, fbox, xoff, uv, nvx, orig, flags, kept);
+                           st_i, st_j, finfo, fbox, xoff, uv, nvx, orig, flags, kmask, umask);
         hipLaunchKernelGGL(k_cand_exact, dim3(grid_for(NC, B)), dim3(B), 0, s, NC, cand_f, coff, st_id, st_i, st_j, finfo,
-                           xoff, xyz, nvx, orig, kept);
+                           xoff, xyz, nvx, orig, kmask, umask);
+        hipLaunchKernelGGL(k_mask_counts, dim3(grid_for(G, B)), dim3(B), 0, s, G, kmask, gcnt);
     }
-    exclusive_scan_i64(kept, kpos, NC, tmp_, s);
+    exclusive_scan_i64(gcnt, gpos, G, tmp_, s);
+    DSS_HIP(hipMemsetAsync(gpos + G + 1, 0, sizeof(int64_t), s));
     // hierarchical descent for the rest (big, multi-face, polyline footprints)
     double4 *clip_f = clipf_.ensure(ne + 1), *clip_c = clipc_.ensure(ne + 1);
     uint8_t *cflags = cflags_.ensure(ne + 1);
@@ -1153,7 +1197,7 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     if (nn > 0)
         hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nn, B)), dim3(B), 0, s, nn, F->f.p, F->meta.p, icnt, dcnt);
     int64_t *tot64 = fc64_.ensure(n + 1), *dc64 = dc64_.ensure(n + 1), *dpre = dpre_.ensure(n + 1);
-    hipLaunchKernelGGL(k_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, coff, kpos, dcnt, tot64, dc64);
+    hipLaunchKernelGGL(k_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, coff, kmask, gpos, dcnt, tot64, dc64);
     exclusive_scan_i64(tot64, offs, n, tmp_, s);
     int64_t total = 0;
     if (nn > 0) {
@@ -1165,7 +1209,7 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     uint64_t *cells = cells_.ensure(total + 1);
     if (NC > 0)
         hipLaunchKernelGGL(k_cand_emit, dim3(grid_for(NC, B)), dim3(B), 0, s, NC, cand_f, coff, st_id, st_i, st_j, finfo,
-                           kept, kpos, offs, cells);
+                           kmask, gpos, offs, cells);
     if (nn > 0) {
         uint32_t *big = big_.ensure(nn + 1);
         int *nbig = flag_.ensure(1);

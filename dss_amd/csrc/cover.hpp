@@ -48,7 +48,8 @@ class CoverEngine {
     DevBuf<double2> uv_;
     DevBuf<uint64_t> st_id_;
     DevBuf<uint32_t> st_i_, st_j_, finfo_, cand_f_;
-    DevBuf<int64_t> ncand_, coff_, kept_, kpos_, dc64_, dpre_;
+    DevBuf<int64_t> ncand_, coff_, gcnt_, gpos_, dc64_, dpre_;
+    DevBuf<unsigned long long> kmask_;
     DevBuf<uint4> fbox_;
     bool tables_ = false;
 };
