@@ -210,15 +210,41 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
 // only, so a 64-bit (cell, entity) sort runs 4 passes instead of 8).
 template <typename K>
 __global__ __launch_bounds__(kRBlock) void k_rs_varying(const K *__restrict__ keys, int64_t n,
-                                                        unsigned long long *__restrict__ out)
+                                                        unsigned long long *__restrict__ part)
 {
+    __shared__ unsigned long long wacc[kRWaves];
     const K k0 = keys[0];
     unsigned long long acc = 0;
     for (int64_t i = (int64_t)blockIdx.x * kRBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kRBlock)
         acc |= (unsigned long long)(keys[i] ^ k0);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) acc |= __shfl_xor(acc, off, 64);
-    if ((threadIdx.x & 63) == 0 && acc) atomicOr(out, acc);
+    if ((threadIdx.x & 63) == 0) wacc[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long r = 0;
+#pragma unroll
+        for (int i = 0; i < kRWaves; i++) r |= wacc[i];
+        part[blockIdx.x] = r;  // one partial per block: no same-address atomics
+    }
+}
+
+__global__ __launch_bounds__(kRBlock) void k_rs_or_parts(const unsigned long long *__restrict__ part, int np,
+                                                         unsigned long long *__restrict__ out)
+{
+    __shared__ unsigned long long wacc[kRWaves];
+    unsigned long long acc = 0;
+    for (int i = threadIdx.x; i < np; i += kRBlock) acc |= part[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc |= __shfl_xor(acc, off, 64);
+    if ((threadIdx.x & 63) == 0) wacc[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long r = 0;
+#pragma unroll
+        for (int i = 0; i < kRWaves; i++) r |= wacc[i];
+        *out = r;
+    }
 }
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -241,10 +267,11 @@ void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, int bits, Dev
     // sync, against up to 4 passes saved)
     int lo = 0;
     if (bits > 24) {
-        unsigned long long *vm = (unsigned long long *)tmp.ensure(hist_b + dtot_b) + 0;
-        DSS_HIP(hipMemsetAsync(vm, 0, sizeof(unsigned long long), s));
-        const int64_t g = std::min<int64_t>(ntiles, 2048);
-        hipLaunchKernelGGL(k_rs_varying<K>, dim3((unsigned)g), dim3(kRBlock), 0, s, ki, n, vm);
+        const int g = (int)std::min<int64_t>(ntiles, 1024);
+        unsigned long long *vm = (unsigned long long *)tmp.ensure(std::max(hist_b + dtot_b, sizeof(unsigned long long) * (g + 1))),
+                           *part = vm + 1;
+        hipLaunchKernelGGL(k_rs_varying<K>, dim3((unsigned)g), dim3(kRBlock), 0, s, ki, n, part);
+        hipLaunchKernelGGL(k_rs_or_parts, dim3(1), dim3(kRBlock), 0, s, part, g, vm);
         unsigned long long var = 0;
         DSS_HIP(hipMemcpyAsync(&var, vm, sizeof(var), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipStreamSynchronize(s));
