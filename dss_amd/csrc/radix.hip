@@ -3,8 +3,10 @@
 // pkg/scd/store/cockroach/store.go:140-147) in the index build, and groups a
 // batch's (cell, bucket) keys before the join.
 //
-// Per pass over `rb` <= 8 digit bits (passes = ceil(bits / 8), digit width
-// balanced across passes), three launches:
+// Per pass over `rb` <= 8 digit bits (passes = ceil(span / 8), digit width
+// balanced across passes: 18 bits -> 3 x 6, level-13 cell ids -> 4 x 7-8;
+// 9-bit digits measured slower: 0.26 vs 0.20 ms on 11.6M 18-bit keys),
+// three launches:
 //   k_rs_hist    one 4096-key tile per block: per-wave LDS digit counts,
 //                written digit-major hist[d][tile] (so one row scan gives
 //                every tile its global start per digit);
@@ -29,8 +31,17 @@ namespace dss {
 namespace {
 
 constexpr int kRBlock = 256;
+#ifndef DSS_RADIX_BITS
+#define DSS_RADIX_BITS 8
+#endif
+#ifndef DSS_RADIX_ITEMS
+#define DSS_RADIX_ITEMS 16
+#endif
+constexpr int kMaxDigitBits = DSS_RADIX_BITS;    // digit bits per pass (8: 256 digits, one per thread)
+constexpr int kMaxDigits = 1 << kMaxDigitBits;
+constexpr int kDPT = kMaxDigits / kRBlock;       // digits per thread in the per-digit phases
 constexpr int kRWaves = kRBlock / 64;
-constexpr int kItems = 16;
+constexpr int kItems = DSS_RADIX_ITEMS;
 constexpr int kTile = kRBlock * kItems;  // 4096 keys per block
 constexpr int kWaveTile = 64 * kItems;   // 1024 keys per wave, contiguous
 
@@ -73,10 +84,10 @@ template <typename K>
 __global__ __launch_bounds__(kRBlock) void k_rs_hist(const K *__restrict__ keys, int64_t n, int shift, int rbits,
                                                      uint32_t *__restrict__ hist, int64_t stride)
 {
-    __shared__ uint32_t h[kRWaves][256];
+    __shared__ uint32_t h[kRWaves][kMaxDigits];
     const int tid = threadIdx.x, w = tid >> 6;
     const uint32_t nd = 1u << rbits, mask = nd - 1;
-    for (int i = tid; i < kRWaves * 256; i += kRBlock) (&h[0][0])[i] = 0;
+    for (int i = tid; i < kRWaves * kMaxDigits; i += kRBlock) (&h[0][0])[i] = 0;
     __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * kTile;
     K k[kItems];
@@ -129,21 +140,35 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
                                                         int rbits, const uint32_t *__restrict__ hist, int64_t stride,
                                                         const uint32_t *__restrict__ dtot)
 {
-    __shared__ uint32_t wh[kRWaves][256];  // per-wave digit counters, then their exclusive prefix over waves
-    __shared__ uint32_t dstart[256];       // tile-local start of each digit
-    __shared__ uint32_t gbase[256];        // global position of tile slot 0 of each digit
+    __shared__ uint32_t wh[kRWaves][kMaxDigits];  // per-wave digit counters, then their exclusive prefix over waves
+    __shared__ uint32_t dstart[kMaxDigits];       // tile-local start of each digit
+    __shared__ uint32_t gbase[kMaxDigits];        // global position of tile slot 0 of each digit
     __shared__ uint32_t ws[kRWaves];
     __shared__ K sk[kTile];
     __shared__ V sv[HAS_V ? kTile : 1];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t nd = 1u << rbits, mask = nd - 1;
-    for (int i = tid; i < kRWaves * 256; i += kRBlock) (&wh[0][0])[i] = 0;
-    // global start of digit `tid` in this tile: all smaller digits + this
-    // digit in earlier tiles
-    const uint32_t dt = (uint32_t)tid < nd ? dtot[tid] : 0u;
+    for (int i = tid; i < kRWaves * kMaxDigits; i += kRBlock) (&wh[0][0])[i] = 0;
+    // global start of digits kDPT*tid .. +kDPT-1 in this tile: all smaller
+    // digits + the same digit in earlier tiles
+    uint32_t dt[kDPT], dsum = 0;
+#pragma unroll
+    for (int u = 0; u < kDPT; u++) {
+        const uint32_t d = (uint32_t)(kDPT * tid + u);
+        dt[u] = d < nd ? dtot[d] : 0u;
+        dsum += dt[u];
+    }
     uint32_t unused;
-    const uint32_t dexcl = block_incl_scan(dt, ws, unused) - dt;
-    const uint32_t gstart = (uint32_t)tid < nd ? dexcl + hist[(int64_t)tid * stride + blockIdx.x] : 0u;
+    uint32_t gstart[kDPT];
+    {
+        uint32_t run = block_incl_scan(dsum, ws, unused) - dsum;
+#pragma unroll
+        for (int u = 0; u < kDPT; u++) {
+            const uint32_t d = (uint32_t)(kDPT * tid + u);
+            gstart[u] = d < nd ? run + hist[(int64_t)d * stride + blockIdx.x] : 0u;
+            run += dt[u];
+        }
+    }
 
     const int64_t sub = (int64_t)blockIdx.x * kTile + (int64_t)w * kWaveTile;
     K k[kItems];
@@ -174,16 +199,30 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
         loc[j] = before + rank;
     }
     __syncthreads();
-    uint32_t cnt = 0;
+    uint32_t cnt[kDPT], csum = 0;
 #pragma unroll
-    for (int i = 0; i < kRWaves; i++) {
-        const uint32_t t = wh[i][tid];
-        wh[i][tid] = cnt;
-        cnt += t;
+    for (int u = 0; u < kDPT; u++) {
+        const int d = kDPT * tid + u;
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < kRWaves; i++) {
+            const uint32_t t = wh[i][d];
+            wh[i][d] = c;
+            c += t;
+        }
+        cnt[u] = c;
+        csum += c;
     }
-    const uint32_t st = block_incl_scan(cnt, ws, unused) - cnt;
-    dstart[tid] = st;
-    gbase[tid] = gstart - st;  // modular: gbase + slot lands in [gstart, gstart + cnt)
+    {
+        uint32_t st = block_incl_scan(csum, ws, unused) - csum;
+#pragma unroll
+        for (int u = 0; u < kDPT; u++) {
+            const int d = kDPT * tid + u;
+            dstart[d] = st;
+            gbase[d] = gstart[u] - st;  // modular: gbase + slot lands in [gstart, gstart + cnt)
+            st += cnt[u];
+        }
+    }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kItems; j++) {
@@ -262,7 +301,7 @@ void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, int bits, Dev
         return;
     }
     const int64_t ntiles = (n + kTile - 1) / kTile, stride = (ntiles + 3) & ~(int64_t)3;
-    const size_t hist_b = align256(sizeof(uint32_t) * 256 * stride), dtot_b = align256(sizeof(uint32_t) * 256);
+    const size_t hist_b = align256(sizeof(uint32_t) * kMaxDigits * stride), dtot_b = align256(sizeof(uint32_t) * kMaxDigits);
     // wide keys: sort only the span of bits that vary (one read + one host
     // sync, against up to 4 passes saved)
     int lo = 0;
@@ -287,7 +326,7 @@ void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, int bits, Dev
         if (HAS_V) DSS_HIP(hipMemcpyAsync(vo, vi, sizeof(V) * n, hipMemcpyDeviceToDevice, s));
         return;
     }
-    const int span = bits - lo, passes = (span + 7) / 8, rb = (span + passes - 1) / passes;
+    const int span = bits - lo, passes = (span + kMaxDigitBits - 1) / kMaxDigitBits, rb = (span + passes - 1) / passes;
     const size_t ka_b = passes > 1 ? align256(sizeof(K) * n) : 0, va_b = passes > 1 && HAS_V ? align256(sizeof(V) * n) : 0;
     unsigned char *t = tmp.ensure(hist_b + dtot_b + ka_b + va_b);
     uint32_t *hist = (uint32_t *)t, *dtot = (uint32_t *)(t + hist_b);

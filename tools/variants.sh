@@ -11,7 +11,7 @@ mkdir -p $R/dss_amd/variants $R/build/variants
 while [ $# -ge 2 ]; do
   name=$1; defs=$2; shift 2
   O=$R/build/variants/$name; mkdir -p $O
-  for f in cover.hip ingress.hip search.hip subs.hip store.hip route.hip scan.hip selftest.hip capi.cpp; do
+  for f in cover.hip ingress.hip radix.hip search.hip subs.hip store.hip route.hip scan.hip selftest.hip capi.cpp; do
     /opt/rocm/bin/hipcc $FLAGS $defs -c $C/$f -o $O/$f.o &
   done
   wait
