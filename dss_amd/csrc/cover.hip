@@ -937,18 +937,32 @@ __device__ __forceinline__ int cand_decide(int64_t c, const uint32_t *cand_f, co
     const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
     bool in = false, par = false;
     double2 a = up[0];
-    for (int e = 0; e < nv; e++) {
-        const double2 b = up[e + 1 == nv ? 0 : e + 1];
-        if (edge_intersects_rect(a.x, a.y, b.x, b.y, ulo - pm, uhi + pm, vlo - pm, vhi + pm)) {
-            in = true;
-            break;
+    // vertices are loaded kVU at a time (independent loads in flight
+    // together), then the edges are tested in order; indices past the
+    // closing edge read vertex 0 (valid, unused)
+    constexpr int kVU = 4;
+    for (int e0 = 0; e0 < nv && !in; e0 += kVU) {
+        double2 bb[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; u++) {
+            const int e = e0 + u + 1;
+            bb[u] = up[e < nv ? e : 0];
         }
-        if ((a.y > vc) != (b.y > vc)) {
-            const double d = b.y - a.y;
-            const double lhs = (uc - a.x) * d, rhs = (vc - a.y) * (b.x - a.x);
-            if (d > 0 ? lhs < rhs : lhs > rhs) par = !par;
+#pragma unroll
+        for (int u = 0; u < kVU; u++) {
+            if (e0 + u >= nv) break;
+            const double2 b = bb[u];
+            if (edge_intersects_rect(a.x, a.y, b.x, b.y, ulo - pm, uhi + pm, vlo - pm, vhi + pm)) {
+                in = true;
+                break;
+            }
+            if ((a.y > vc) != (b.y > vc)) {
+                const double d = b.y - a.y;
+                const double lhs = (uc - a.x) * d, rhs = (vc - a.y) * (b.x - a.x);
+                if (d > 0 ? lhs < rhs : lhs > rhs) par = !par;
+            }
+            a = b;
         }
-        a = b;
     }
     return in ? 1 : planar ? (((origin_in[f] != 0) != par) ? 1 : 0) : 2;
 }
