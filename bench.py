@@ -324,6 +324,8 @@ def sharded_report(args, ctx, D, dist, torch, sh, step, full, i_cells_h, ranges,
     roofline, and parity: every rank's delivered pair set == a whole-index
     search of its own queries (count + order-independent checksum)."""
     import ctypes as C
+
+    from dss_amd import workload as W
     dev = f"cuda:{torch.cuda.current_device()}"
     ctx.L.dssg_set_timing(ctx.h, 1)
     sh.times = {}

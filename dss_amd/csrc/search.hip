@@ -588,7 +588,11 @@ __global__ void k_qcells(IndexView a, QueryView qv, int64_t nqc, const uint32_t 
     // the prefix's decodes are loaded 8 at a time (independent loads in
     // flight together), then folded in order
     constexpr int kU = 8;
+#if DSS_EXP_QC == 1  // timing experiment only (wrong signatures)
+    for (int64_t j0 = k; j0 < k; j0 += kU) {
+#else
     for (int64_t j0 = c0; j0 < k; j0 += kU) {
+#endif
         uint32_t dd[kU];
 #pragma unroll
         for (int u = 0; u < kU; u++) dd[u] = j0 + u < k ? dec[j0 + u] : 0u;
