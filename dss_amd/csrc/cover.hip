@@ -387,10 +387,22 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
     } else {
         nv = (int)(voff[f + 1] - v0);
         if (k == DSSG_KIND_POLYGON) {  // Q17: range check precedes the count check
-            for (int i = 0; i < nv; i++) {
-                double la = lat[v0 + i], ln = lng[v0 + i];
-                if (la > 90.0 || la < -90.0 || ln > 180.0 || ln < -180.0) { st = DSSG_ST_BAD_COORD_SET; break; }
+            // 4 vertices' loads in flight together; the verdict is the same
+            // whichever out-of-range vertex is seen first
+            bool bad = false;
+            for (int i0 = 0; i0 < nv && !bad; i0 += 4) {
+                double la[4], ln[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int i = i0 + u < nv ? i0 + u : nv - 1;
+                    la[u] = lat[v0 + i];
+                    ln[u] = lng[v0 + i];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    bad |= la[u] > 90.0 || la[u] < -90.0 || ln[u] > 180.0 || ln[u] < -180.0;
             }
+            if (bad) st = DSSG_ST_BAD_COORD_SET;
         }
         if (st == DSSG_ST_OK && nv < 3) st = DSSG_ST_NOT_ENOUGH_POINTS;
         if (st == DSSG_ST_OK) {
@@ -867,11 +879,26 @@ __global__ void k_emit_big(const uint32_t *big, const uint32_t *nf, const uint64
 // are consecutive ids, so enumerating them by index lists the footprint's
 // candidates sorted; each is tested exactly as k_expand_count tests a level-13
 // node, and an order-preserving scan compacts the survivors.
-__global__ void k_cand_owner(int64_t n, const int64_t *coff, uint32_t *cand_f)
+// Candidate -> footprint, one block per 256 footprints: their candidate
+// offsets go to LDS, then the block's whole candidate range is written
+// coalesced, each candidate finding its footprint by binary search in LDS.
+__global__ __launch_bounds__(256) void k_cand_owner(int64_t n, const int64_t *coff, uint32_t *cand_f)
 {
-    int64_t f = tid64();
-    if (f >= n) return;
-    for (int64_t c = coff[f]; c < coff[f + 1]; c++) cand_f[c] = (uint32_t)f;
+    __shared__ int64_t sc[257];
+    const int64_t f0 = (int64_t)blockIdx.x * 256;
+    const int nf = (int)(n - f0 < 256 ? n - f0 : 256);
+    for (int i = threadIdx.x; i <= nf; i += 256) sc[i] = coff[f0 + i];
+    __syncthreads();
+    const int64_t c1 = sc[nf];
+    for (int64_t c = sc[0] + threadIdx.x; c < c1; c += 256) {
+        int lo = 0, hi = nf;  // sc[lo] <= c < sc[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (sc[mid] <= c) lo = mid;
+            else hi = mid;
+        }
+        cand_f[c] = (uint32_t)(f0 + lo);
+    }
 }
 
 // Level-13 (i, j) and id of candidate c of footprint f.
@@ -1153,7 +1180,7 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     int64_t *gcnt = gcnt_.ensure(G + 1), *gpos = gpos_.ensure(G + 2);
     DSS_HIP(hipMemsetAsync(kmask + G, 0, sizeof(unsigned long long), s));
     if (NC > 0) {
-        hipLaunchKernelGGL(k_cand_owner, dim3(grid_for(n, B)), dim3(B), 0, s, n, coff, cand_f);
+        hipLaunchKernelGGL(k_cand_owner, dim3(grid_for(n, 256)), dim3(256), 0, s, n, coff, cand_f);
         hipLaunchKernelGGL(k_cand_test, dim3(grid_for(NC, kCandBlock)), dim3(kCandBlock), 0, s, NC, cand_f, coff, st_id,
                            st_i, st_j, finfo, fbox, xoff, uv, nvx, orig, flags, kmask, umask);
         hipLaunchKernelGGL(k_cand_exact, dim3(grid_for(NC, B)), dim3(B), 0, s, NC, cand_f, coff, st_id, st_i, st_j, finfo,
