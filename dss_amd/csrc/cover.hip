@@ -299,8 +299,17 @@ __global__ void k_fan_area(const int64_t *toff_end, const uint32_t *towner, cons
 // in the bands where Area consults IsNormalized.
 __device__ __forceinline__ double fan_area_km2(const double *t, int n, bool &fail, bool rev_only = false)
 {
+    // terms loaded 4 at a time, summed in index order (the order of
+    // surfaceIntegralFloat64, so the sum is bit-identical)
     double area = 0;
-    for (int i = 1; i + 1 < n; i++) area += t[i];
+    for (int i0 = 1; i0 + 1 < n; i0 += 4) {
+        double x[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) x[u] = t[i0 + u + 1 < n ? i0 + u : i0];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (i0 + u + 1 < n) area += x[u];
+    }
     const double max_error = DSS_TURN_ANGLE_ERR_PER_VERTEX * (double)n;
     // omode 1 skipped the forward sum (~ -area): its IsNormalized band
     // (|sum| < max_error) is excluded with a wide margin instead
@@ -488,6 +497,7 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
         const int face0 = xyz_face(p[0]);
         double2 *uvp = uv + xoff[f];
         double ulo = 1e300, uhi = -1e300, vlo = 1e300, vhi = -1e300;
+#pragma unroll 4
         for (int i = 0; i < nv; i++) {
             double u, v;
             if constexpr (FAST) {  // projected by k_fan
