@@ -947,14 +947,17 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
             }
             const uint64_t cell = cell_of_slot(ix, (uint32_t)(key >> 6));
             const int64_t k0 = cu.k0, k1 = cu.k1;
+            uint32_t ci_cur = ci_first;
             for (int64_t base = k0; base < k1; base += 64) {
                 const int64_t kk = base + lane;
+                // the next batch's record indices are in flight during this batch
+                const uint32_t ci_nx = kk + 64 < k1 ? sval[kk + 64] : 0u;
                 bool rel = false;
                 int4 r0 = make_int4(0, 0, 0, 0), r1 = make_int4(0, 0, 0, 0);
                 int32_t rown_l = -1;
                 __builtin_amdgcn_wave_barrier();
                 if (kk < k1) {
-                    const uint32_t ci = base == k0 ? ci_first : sval[kk];
+                    const uint32_t ci = ci_cur;
                     r0 = rec4[4 * ci];
                     r1 = rec4[4 * ci + 1];
                     s_sig[w][0][lane] = rec4[4 * ci + 2];
@@ -1113,6 +1116,7 @@ __global__ __launch_bounds__(64 * kWaves) DSS_JOIN_OCC void k_join(JoinArgs a, c
                 records(std::integral_constant<int, kSlots>{});
 #endif
 #endif
+                ci_cur = ci_nx;
             }
         }
         u = un;
