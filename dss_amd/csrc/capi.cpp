@@ -864,4 +864,10 @@ int dssg_selftest_math(dssg_ctx *ctx, int op, int64_t n, const double *x, const 
     });
 }
 
+int dssg_selftest_scan(dssg_ctx *ctx, int64_t n, int shift, const int64_t *in, int64_t *out)
+{
+    if (!ctx || n < 0 || shift < 0 || shift > 64 || !out || (n > 0 && !in)) return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] { dss::selftest_scan(n, shift, in, out, ctx->stream); });
+}
+
 }  // extern "C"

@@ -52,8 +52,9 @@ struct DevBuf {
 inline unsigned grid_for(int64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
 // Exclusive prefix sum of n int64 values into out (n+1 entries, out[n] = total),
-// returns nothing; implemented in scan.hip with hipcub.
+// hand-written reduce-then-scan in scan.hip (in != out).
 void selftest_math(int op, int64_t n, const double *x, const double *y, double *out, hipStream_t s);
+void selftest_scan(int64_t n, int shift, const int64_t *in, int64_t *out, hipStream_t s);
 void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, DevBuf<unsigned char> &tmp, hipStream_t s);
 // perm = footprint indices with every non-circle before every circle (order
 // within each part unspecified): per-footprint kernels then run one kind's

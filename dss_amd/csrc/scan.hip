@@ -1,19 +1,125 @@
-// Device-wide scans (hipcub / rocPRIM) used by the covering and search
-// pipelines for order-preserving compaction.
+// Device-wide scans used by the covering and search pipelines for
+// order-preserving compaction: the int64 exclusive scan is hand-written
+// (below); the polygon/circle partition uses hipCUB.
 #include <hipcub/hipcub.hpp>
 
 #include "common.hpp"
 
 namespace dss {
 
+namespace {
+
+// Exclusive int64 prefix sum, reduce-then-scan over 2048-element tiles
+// (256 lanes x 8 consecutive elements):
+//   k_scan_reduce  tile sums -> part[t]            (skipped for one tile)
+//   k_scan_parts   one block: exclusive scan of the tile sums, in place
+//   k_scan_down    tile t again: lane sums, block scan, + part[t] -> out
+// No look-back spin and no library state: 3 launches (1 for n <= 2048),
+// HBM 8n read twice + 8n written.
+constexpr int kSBlock = 256, kSWaves = kSBlock / 64, kSItems = 8, kSTile = kSBlock * kSItems;
+
+__device__ __forceinline__ long long block_incl_scan_i64(long long x, long long *ws, long long &total)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const long long y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) ws[w] = x;
+    __syncthreads();
+    long long pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kSWaves; i++) {
+        const long long t = ws[i];
+        pre += i < w ? t : 0;
+        tot += t;
+    }
+    __syncthreads();
+    total = tot;
+    return x + pre;
+}
+
+__device__ __forceinline__ long long lane_items(const int64_t *in, int64_t n, int64_t i0, long long v[kSItems])
+{
+    long long t = 0;
+    const bool a16 = ((uintptr_t)in & 15) == 0;  // callers pass offsets into shared buffers
+    if (a16 && i0 + kSItems <= n) {
+        const longlong2 *p = reinterpret_cast<const longlong2 *>(in + i0);  // i0 is a multiple of 8
+#pragma unroll
+        for (int u = 0; u < kSItems / 2; u++) {
+            const longlong2 q = p[u];
+            v[2 * u] = q.x;
+            v[2 * u + 1] = q.y;
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < kSItems; u++) v[u] = i0 + u < n ? in[i0 + u] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kSItems; u++) t += v[u];
+    return t;
+}
+
+__global__ __launch_bounds__(kSBlock) void k_scan_reduce(const int64_t *__restrict__ in, int64_t n,
+                                                         long long *__restrict__ part)
+{
+    __shared__ long long ws[kSWaves];
+    long long v[kSItems];
+    const long long t = lane_items(in, n, (int64_t)blockIdx.x * kSTile + (int64_t)threadIdx.x * kSItems, v);
+    long long total;
+    block_incl_scan_i64(t, ws, total);
+    if (threadIdx.x == 0) part[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kSBlock) void k_scan_parts(long long *__restrict__ part, int64_t nt)
+{
+    __shared__ long long ws[kSWaves];
+    long long carry = 0;
+    for (int64_t b0 = 0; b0 < nt; b0 += kSBlock) {
+        const int64_t i = b0 + threadIdx.x;
+        const long long v = i < nt ? part[i] : 0;
+        long long total;
+        const long long incl = block_incl_scan_i64(v, ws, total);
+        if (i < nt) part[i] = carry + incl - v;
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(kSBlock) void k_scan_down(const int64_t *__restrict__ in, int64_t n,
+                                                       const long long *__restrict__ part, int64_t *__restrict__ out)
+{
+    __shared__ long long ws[kSWaves];
+    const int64_t i0 = (int64_t)blockIdx.x * kSTile + (int64_t)threadIdx.x * kSItems;
+    long long v[kSItems];
+    const long long t = lane_items(in, n, i0, v);
+    long long total;
+    long long run = block_incl_scan_i64(t, ws, total) - t + (part ? part[blockIdx.x] : 0);
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[0] = 0;
+#pragma unroll
+    for (int u = 0; u < kSItems; u++) {
+        run += v[u];
+        if (i0 + u < n) out[i0 + u + 1] = run;  // out[k + 1] = in[0] + ... + in[k]
+    }
+}
+
+}  // namespace
+
 void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, DevBuf<unsigned char> &tmp, hipStream_t s)
 {
-    DSS_HIP(hipMemsetAsync(out, 0, sizeof(int64_t), s));
-    if (n <= 0) return;
-    size_t bytes = 0;
-    DSS_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, in, out + 1, (int)n, s));
-    tmp.ensure(bytes + 16);
-    DSS_HIP(hipcub::DeviceScan::InclusiveSum(tmp.p, bytes, in, out + 1, (int)n, s));
+    if (n <= 0) {
+        DSS_HIP(hipMemsetAsync(out, 0, sizeof(int64_t), s));
+        return;
+    }
+    const int64_t nt = (n + kSTile - 1) / kSTile;
+    long long *part = nullptr;
+    if (nt > 1) {
+        part = (long long *)tmp.ensure(sizeof(long long) * nt);
+        hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nt), dim3(kSBlock), 0, s, in, n, part);
+        hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(kSBlock), 0, s, part, nt);
+    }
+    hipLaunchKernelGGL(k_scan_down, dim3((unsigned)nt), dim3(kSBlock), 0, s, in, n, (const long long *)part, out);
+    DSS_HIP(hipGetLastError());
 }
 
 namespace {

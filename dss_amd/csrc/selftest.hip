@@ -42,4 +42,19 @@ void selftest_math(int op, int64_t n, const double *x, const double *y, double *
     DSS_HIP(hipMemcpyAsync(out, po, sizeof(double) * n, hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
 }
+
+// Exclusive scan of n host int64 values through the device scan, with the
+// input placed `shift` elements into its buffer (shift odd: a pointer that is
+// 8- but not 16-byte aligned, as call sites that scan inside shared buffers
+// pass).  out: n + 1 values.
+void selftest_scan(int64_t n, int shift, const int64_t *in, int64_t *out, hipStream_t s)
+{
+    DevBuf<int64_t> din, dout;
+    DevBuf<unsigned char> tmp;
+    int64_t *pi = din.ensure(n + shift + 1) + shift, *po = dout.ensure(n + 1);
+    if (n) DSS_HIP(hipMemcpyAsync(pi, in, sizeof(int64_t) * n, hipMemcpyHostToDevice, s));
+    exclusive_scan_i64(pi, po, n, tmp, s);
+    DSS_HIP(hipMemcpyAsync(out, po, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+}
 }  // namespace dss

@@ -356,6 +356,11 @@ int dssg_copy_to_host(dssg_ctx *ctx, void *dst, const void *src, size_t bytes);
  * the call waits and reports the sort's duration (HIP events on `stream`). */
 int dssg_radix_sort_device(dssg_ctx *ctx, int key_bytes, int64_t n, int bits, const void *d_keys_in, void *d_keys_out,
                            const uint32_t *d_vals_in, uint32_t *d_vals_out, void *stream, double *ms);
+/* Exclusive prefix sum of n host int64 values through the device scan the
+ * covering and search use (scan.hip), the input placed `shift` elements
+ * into its device buffer (0..64; odd = 8- but not 16-byte aligned);
+ * out[0] = 0, out[k + 1] = in[0] + ... + in[k] -- for parity tests. */
+int dssg_selftest_scan(dssg_ctx *ctx, int64_t n, int shift, const int64_t *in, int64_t *out);
 /* Evaluate the device restatement of a Go math routine on n inputs
  * (op: 0 sin, 1 cos, 2 tan, 3 atan, 4 atan2(x, y), 5 asin, 6 sqrt, 7 x/y,
  * 8 stToUV, 9 uvToST, 10 PointFromLatLng(x, y).X) -- for bit-exact tests. */

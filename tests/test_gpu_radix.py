@@ -105,3 +105,20 @@ def test_radix_sort_constant_and_high_bit_keys(key_bytes):
     assert np.array_equal(ko, rk) and np.array_equal(vo, rv)
     ko, vo, _ = gpu_sort(high, vals, top - 3, key_bytes)  # varying bits outside the sorted range
     assert np.array_equal(ko, high) and np.array_equal(vo, vals)
+
+
+@pytest.mark.parametrize("n,shift", [(0, 0), (1, 0), (2047, 1), (2048, 0), (2049, 1), (4096 * 7 + 3, 0),
+                                     (1_000_003, 1), (1_000_003, 0), (6_700_001, 3)])
+def test_exclusive_scan_matches_cumsum(n, shift):
+    """The hand-written int64 exclusive scan (scan.hip) behind every CSR
+    offset array: out[0] = 0, out[k + 1] = sum(in[:k + 1]), aligned and
+    8-byte-misaligned inputs, single and multi-tile sizes."""
+    from dss_amd import _lib
+    ctx = _lib.context()
+    rng = np.random.default_rng(n + shift)
+    x = rng.integers(0, 1 << 20, size=n, dtype=np.int64)
+    out = np.full(n + 1, -1, dtype=np.int64)
+    P = lambda a: a.ctypes.data_as(C.POINTER(C.c_int64))  # noqa: E731
+    ctx.check(ctx.L.dssg_selftest_scan(ctx.h, n, shift, P(x) if n else None, P(out)))
+    ref = np.concatenate([[0], np.cumsum(x)]).astype(np.int64)
+    assert np.array_equal(out, ref)
