@@ -12,14 +12,18 @@ altitude/time/now filter -> deduplicated (query, intent) pairs resident in
 HBM.  The index (intent coverings + posting lists) is built before timing.
 
 Multi-GPU (torchrun, one process per GPU), --mode:
-  sharded (default for N > 1): the intent index is split into
+  replica (default): every rank holds the whole index (a 1M-intent airspace
+    is ~0.5 GB of a GPU's 288 GB; even configs[4]'s 50M fit many times over)
+    and covers + joins its own 1M-query batch.  Queries are independent, so
+    there is no collective on the data path; "scaling": "weak".
+  sharded: the intent index is split into
     N uint64 cell ranges at posting quantiles, one shard per GPU.  Each rank
     covers its own 1M queries, routes every query (row + whole cell list) to
     the shards owning its cells (all-to-all over RCCL/xGMI), joins what it
     receives against its shard, and routes the pairs back to their queries'
     home ranks (second all-to-all).  "scaling": "weak" (1M queries per GPU).
-  replica: every rank holds the whole index and joins its own slice; no
-    collective on the data path.
+    For an index that outgrows one GPU; the pair exchange (~100 pairs x 8 B
+    per query) costs more than the join it distributes.
 Timing: barrier + synchronize on both sides of exactly --steps steps, max
 over ranks.
 """
@@ -54,8 +58,9 @@ def main():
     ap.add_argument("--no-verify", action="store_true", help="skip the full-size GPU-vs-oracle parity check")
     ap.add_argument("--survey-model", type=int, default=1, help="also count SURVEY s8(d)'s per-query byte model")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--mode", choices=["sharded", "replica"], default=None,
-                    help="multi-GPU layout (default: sharded for N > 1, replica for N = 1)")
+    ap.add_argument("--mode", choices=["sharded", "replica"], default="replica",
+                    help="multi-GPU layout: replica (index on every GPU, queries split; default) or sharded (index "
+                         "split by cell range, queries and pairs exchanged by all-to-all)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on a multi-GPU node; gloo for rehearsals")
     ap.add_argument("--pipelines", type=int, default=3,
                     help="concurrent batch pipelines per GPU (own engine context + stream + host thread each): one "
@@ -70,7 +75,7 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", 0))
-    mode = args.mode or ("sharded" if world > 1 else "replica")
+    mode = args.mode
     torch.cuda.set_device(local)
     stage_host = args.dist_backend != "nccl"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")   # single-process sharded runs (no torchrun)
