@@ -286,6 +286,7 @@ def main():
                           "long_postings": n_lp.value},
             "index_build_s": build_s,
             "sort_phase": sort_ph,
+            "cover_fp64": cover_fp64(nq, ni),
             "roofline": {"kernel": "k_join (overlap join + fused altitude/time filter)", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
@@ -461,6 +462,24 @@ def pmc_traffic(kernel, nq, ni):
     if not k or d.get("queries") != nq or d.get("intents") != ni:
         return None
     return {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": d.get("source", path)}
+
+
+def cover_fp64(nq, ni):
+    """FP64 VALU throughput of the covering kernels (the
+    covering is FP64-VALU-bound) from the committed rocprofv3 pass
+    (tools/fp64_summary.py: 64 x (2 FMA + ADD + MUL) F64 wave instructions
+    per launch over the launch's duration), if one exists for this size."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "fp64_cover.json")) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("queries") != nq or d.get("intents") != ni:
+        return None
+    top = max(d["kernels"].items(), key=lambda kv: kv[1]["avg_ms"])
+    return {"kernel": top[0], "bound": "fp64-valu", "achieved": top[1]["tflops"], "peak": d["peak_tflops"],
+            "unit": "TFLOP/s", "frac": top[1]["frac_of_fp64_peak"], "source": d["source"],
+            "all": {k: round(v["tflops"], 2) for k, v in d["kernels"].items() if v["tflops"] > 0.5}}
 
 
 def cpu_baseline(args, ctx, intents, ia, queries, qa, now, i_offs, i_cells, g_cells, g_pairs):
