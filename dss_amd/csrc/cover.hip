@@ -947,7 +947,17 @@ __device__ __forceinline__ int cand_decide(int64_t c, const uint32_t *cand_f, co
                                            const uint4 *fbox, const int64_t *xoff, const double2 *uv, const int32_t *nvx,
                                            const uint8_t *origin_in, const uint8_t *flags)
 {
+    constexpr int kVU = 4;
     const uint32_t f = cand_f[c];
+    // the first vertex batch is loaded before the candidate's cell is known
+    // (speculatively: a candidate outside the bound discards it), so its
+    // round trip overlaps the start-cell loads of cand_cell
+    const int nv = nvx[f];
+    const double2 *up = uv + xoff[f];
+    double2 a = up[0];
+    double2 bb0[kVU];
+#pragma unroll
+    for (int u = 0; u < kVU; u++) bb0[u] = up[u + 1 < nv ? u + 1 : 0];
     int face;
     uint32_t i, j;
     uint64_t id;
@@ -955,8 +965,6 @@ __device__ __forceinline__ int cand_decide(int64_t c, const uint32_t *cand_f, co
     const uint4 bx = fbox[f];
     const uint32_t i13 = i >> (kMaxLevel - kCoverLevel), j13 = j >> (kMaxLevel - kCoverLevel);
     if (i13 < bx.x || i13 > bx.y || j13 < bx.z || j13 > bx.w) return 0;
-    const int nv = nvx[f];
-    const double2 *up = uv + xoff[f];
     const uint32_t size = 1u << (kMaxLevel - kCoverLevel);
     const double ulo = st_to_uv((double)i / (double)kMaxSize), uhi = st_to_uv((double)(i + size) / (double)kMaxSize);
     const double vlo = st_to_uv((double)j / (double)kMaxSize), vhi = st_to_uv((double)(j + size) / (double)kMaxSize);
@@ -973,17 +981,15 @@ __device__ __forceinline__ int cand_decide(int64_t c, const uint32_t *cand_f, co
     const double half = 0.5 / (double)kMaxSize, sz = (double)size;
     const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
     bool in = false, par = false;
-    double2 a = up[0];
     // vertices are loaded kVU at a time (independent loads in flight
     // together), then the edges are tested in order; indices past the
     // closing edge read vertex 0 (valid, unused)
-    constexpr int kVU = 4;
     for (int e0 = 0; e0 < nv && !in; e0 += kVU) {
         double2 bb[kVU];
 #pragma unroll
         for (int u = 0; u < kVU; u++) {
             const int e = e0 + u + 1;
-            bb[u] = up[e < nv ? e : 0];
+            bb[u] = e0 == 0 ? bb0[u] : up[e < nv ? e : 0];
         }
 #pragma unroll
         for (int u = 0; u < kVU; u++) {
