@@ -547,78 +547,102 @@ __device__ __forceinline__ unsigned long long cell_groups(const IndexView &a, ui
 // cells before k (prefix_sig semantics: an undecodable cell saturates it;
 // `compact` = every earlier cell on this cell's face within +-7 cells).
 template <int PASS>
-__global__ void k_qcells(IndexView a, QueryView qv, int64_t nqc, const uint32_t *cq, const uint32_t *dec, int64_t *kcnt,
-                         const int64_t *koff, uint32_t *gkey, uint32_t *gval, QRec *crec, int32_t *cown,
-                         const uint8_t *qlong)
+__global__ __launch_bounds__(kBlock) void k_qcells(IndexView a, QueryView qv, int64_t nqc, const uint32_t *cq,
+                                                   const uint32_t *dec, int64_t *kcnt, const int64_t *koff,
+                                                   uint32_t *gkey, uint32_t *gval, QRec *crec, int32_t *cown,
+                                                   const uint8_t *qlong)
 {
     const int64_t k = tid64();
-    if (k >= nqc) return;
-    const uint32_t q = cq[k];
-    const long long tlo = qv.tlo[q], thi = qv.thi[q];
-    const uint64_t cell = qv.cells[k];
-    uint32_t slot = 0;
-    unsigned long long m = cell_groups(a, cell, tlo, thi, slot);
     if (!PASS) {
-        kcnt[k] = __popcll(m);
+        if (k >= nqc) return;
+        const uint32_t q = cq[k];
+        uint32_t slot = 0;
+        kcnt[k] = __popcll(cell_groups(a, qv.cells[k], qv.tlo[q], qv.thi[q], slot));
         return;
     }
-    int64_t w = koff[k];
-    if (m) {
-        const unsigned long long m0 = a.s_mask[slot];
-        const uint32_t base = a.s_base[slot];
-        while (m) {
-            const int b = __builtin_ctzll(m);
-            m &= m - 1;
-            gkey[w] = base + (uint32_t)__popcll(m0 & ((1ull << b) - 1ull));
-            gval[w] = (uint32_t)k;
-            w++;
-        }
-    } else {
-        return;  // no group met: no key refers to this record
-    }
-    // query record: near-only prefix signature of the query's cells before
-    // k (prefix_sig semantics), compact flag, long flag (qlong)
-    const int64_t c0 = qv.offs[q];
-    const uint32_t dk = dec[k];
-    const int f = (int)(dk >> 26), i = (int)((dk >> 13) & 8191u), jj = (int)(dk & 8191u);
-    const bool v = dk != kNoDecode;
-    Sig256 sig;
-    sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = 0;
-    bool compact = v;
-    // the prefix's decodes are loaded 8 at a time (independent loads in
-    // flight together), then folded in order
-    constexpr int kU = 8;
-#if DSS_EXP_QC == 1  // timing experiment only (wrong signatures)
-    for (int64_t j0 = k; j0 < k; j0 += kU) {
-#else
-    for (int64_t j0 = c0; j0 < k; j0 += kU) {
-#endif
-        uint32_t dd[kU];
-#pragma unroll
-        for (int u = 0; u < kU; u++) dd[u] = j0 + u < k ? dec[j0 + u] : 0u;
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            if (j0 + u >= k) break;
-            const uint32_t d = dd[u];
-            const int pf = (int)(d >> 26), ci = (int)((d >> 13) & 8191u), cj = (int)(d & 8191u);
-            const int di = ci - i, dj = cj - jj;
-            if (v && d != kNoDecode && pf == f && di >= -7 && di <= 7 && dj >= -7 && dj <= 7) sig_set(sig, ci, cj);
-            else compact = false;
-        }
-    }
+    // PASS 1: every lane of a wave stays to the end (the wave's 64 records
+    // leave through LDS as 4 fully coalesced 1 KiB stores); a lane whose
+    // cell meets no group writes a record nobody reads
+    if (k - (threadIdx.x & 63) >= nqc) return;  // whole wave past the end
     QRec r;
-    r.tlo = tlo;
-    r.thi = thi;
-    r.alo = qv.alo[q];
-    r.ahi = qv.ahi[q];
-    r.qv = q | (k == c0 ? kRank0 : 0u) | (compact ? kCompact : 0u) | (qlong[q] ? kLong : 0u);
-    r.bq0 = bucket_of(tlo < thi ? tlo : thi, a.bk);
-    r.sig[0] = sig.w[0];
-    r.sig[1] = sig.w[1];
-    r.sig[2] = sig.w[2];
-    r.sig[3] = sig.w[3];
-    crec[k] = r;
-    if (cown) cown[k] = qv.owner[q];
+    r.tlo = r.thi = 0;
+    r.alo = r.ahi = 0.f;
+    r.qv = 0;
+    r.bq0 = 0;
+    r.sig[0] = r.sig[1] = r.sig[2] = r.sig[3] = 0;
+    if (k < nqc) {
+        const uint32_t q = cq[k];
+        const long long tlo = qv.tlo[q], thi = qv.thi[q];
+        const uint64_t cell = qv.cells[k];
+        uint32_t slot = 0;
+        unsigned long long m = cell_groups(a, cell, tlo, thi, slot);
+        int64_t w = koff[k];
+        if (m) {
+            const unsigned long long m0 = a.s_mask[slot];
+            const uint32_t base = a.s_base[slot];
+            while (m) {
+                const int b = __builtin_ctzll(m);
+                m &= m - 1;
+                gkey[w] = base + (uint32_t)__popcll(m0 & ((1ull << b) - 1ull));
+                gval[w] = (uint32_t)k;
+                w++;
+            }
+            // query record: near-only prefix signature of the query's cells
+            // before k (prefix_sig semantics), compact flag, long flag (qlong)
+            const int64_t c0 = qv.offs[q];
+            const uint32_t dk = dec[k];
+            const int f = (int)(dk >> 26), i = (int)((dk >> 13) & 8191u), jj = (int)(dk & 8191u);
+            const bool v = dk != kNoDecode;
+            Sig256 sig;
+            sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = 0;
+            bool compact = v;
+            // the prefix's decodes are loaded 8 at a time (independent loads
+            // in flight together), then folded in order
+            constexpr int kU = 8;
+#if DSS_EXP_QC == 1  // timing experiment only (wrong signatures)
+            for (int64_t j0 = k; j0 < k; j0 += kU) {
+#else
+            for (int64_t j0 = c0; j0 < k; j0 += kU) {
+#endif
+                uint32_t dd[kU];
+#pragma unroll
+                for (int u = 0; u < kU; u++) dd[u] = j0 + u < k ? dec[j0 + u] : 0u;
+#pragma unroll
+                for (int u = 0; u < kU; u++) {
+                    if (j0 + u >= k) break;
+                    const uint32_t d = dd[u];
+                    const int pf = (int)(d >> 26), ci = (int)((d >> 13) & 8191u), cj = (int)(d & 8191u);
+                    const int di = ci - i, dj = cj - jj;
+                    if (v && d != kNoDecode && pf == f && di >= -7 && di <= 7 && dj >= -7 && dj <= 7) sig_set(sig, ci, cj);
+                    else compact = false;
+                }
+            }
+            r.tlo = tlo;
+            r.thi = thi;
+            r.alo = qv.alo[q];
+            r.ahi = qv.ahi[q];
+            r.qv = q | (k == c0 ? kRank0 : 0u) | (compact ? kCompact : 0u) | (qlong[q] ? kLong : 0u);
+            r.bq0 = bucket_of(tlo < thi ? tlo : thi, a.bk);
+            r.sig[0] = sig.w[0];
+            r.sig[1] = sig.w[1];
+            r.sig[2] = sig.w[2];
+            r.sig[3] = sig.w[3];
+            if (cown) cown[k] = qv.owner[q];
+        }
+    }
+    __shared__ int4 stage[kBlock / 64][64 * 4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int4 *rr = reinterpret_cast<const int4 *>(&r);
+#pragma unroll
+    for (int u = 0; u < 4; u++) stage[wv][4 * lane + u] = rr[u];
+    __builtin_amdgcn_wave_barrier();  // one wave writes and reads its own slice, in order
+    const int64_t kw = k - lane;
+    int4 *dst = reinterpret_cast<int4 *>(crec + kw);
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int c = 64 * u + lane;
+        if (kw + (c >> 2) < nqc) dst[c] = stage[wv][c];
+    }
 }
 
 // Record range [gbeg[g], gend[g]) of every group in the sorted keys (groups
