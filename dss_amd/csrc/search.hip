@@ -468,23 +468,32 @@ struct alignas(64) QRec {
 };
 static_assert(sizeof(QRec) == 64, "QRec layout");
 
-// Owner query of every query cell.
-__global__ void k_cell_query(int64_t nq, const int64_t *offs, uint32_t *cq)
-{
-    const int64_t q = tid64();
-    if (q >= nq) return;
-    for (int64_t k = offs[q]; k < offs[q + 1]; k++) cq[k] = (uint32_t)q;
-}
-
-// Level-13 (face, i, j) of every query cell, packed face << 26 | i << 13 | j,
-// or kNoDecode for ids that are not valid level-13 cells.
+// Owner query and level-13 (face, i, j) of every query cell, the latter
+// packed face << 26 | i << 13 | j, or kNoDecode for ids that are not valid
+// level-13 cells.  One block per 256 queries: their cell offsets go to LDS,
+// then the block's cells are visited coalesced, each finding its query by
+// binary search in LDS.
 constexpr uint32_t kNoDecode = 0xffffffffu;
-__global__ void k_qdecode(int64_t nqc, const uint64_t *cells, uint32_t *dec)
+__global__ __launch_bounds__(kBlock) void k_cell_query(int64_t nq, const int64_t *offs, const uint64_t *cells,
+                                                       uint32_t *cq, uint32_t *dec)
 {
-    const int64_t k = tid64();
-    if (k >= nqc) return;
-    int f = 0, i = 0, j = 0;
-    dec[k] = decode13(cells[k], f, i, j) ? ((uint32_t)f << 26 | (uint32_t)i << 13 | (uint32_t)j) : kNoDecode;
+    __shared__ int64_t so[kBlock + 1];
+    const int64_t q0 = (int64_t)blockIdx.x * kBlock;
+    const int nb = (int)(nq - q0 < (int64_t)kBlock ? nq - q0 : (int64_t)kBlock);
+    for (int i = threadIdx.x; i <= nb; i += kBlock) so[i] = offs[q0 + i];
+    __syncthreads();
+    const int64_t k1 = so[nb];
+    for (int64_t k = so[0] + threadIdx.x; k < k1; k += kBlock) {
+        int lo = 0, hi = nb;  // so[lo] <= k < so[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (so[mid] <= k) lo = mid;
+            else hi = mid;
+        }
+        cq[k] = (uint32_t)(q0 + lo);
+        int f = 0, i = 0, j = 0;
+        dec[k] = decode13(cells[k], f, i, j) ? ((uint32_t)f << 26 | (uint32_t)i << 13 | (uint32_t)j) : kNoDecode;
+    }
 }
 
 // Long flag of every query (long_cells semantics, from the decodes).
@@ -1537,8 +1546,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     if (nqc == 0) return empty();
     uint32_t *cq = cq_.ensure(nqc + 1);
     uint32_t *dec = dec_.ensure(nqc + 1);
-    hipLaunchKernelGGL(k_cell_query, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_offs, cq);
-    hipLaunchKernelGGL(k_qdecode, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, nqc, q_cells, dec);
+    hipLaunchKernelGGL(k_cell_query, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_offs, q_cells, cq, dec);
     int64_t *kcnt = c0_.ensure(nqc + 1), *koff = c1_.ensure(nqc + 2);
     uint8_t *qlong = qlong_.ensure(nq + 1);
     unsigned long long *nlongq_d = counter_.ensure(8) + 5;
