@@ -474,13 +474,22 @@ static_assert(sizeof(QRec) == 64, "QRec layout");
 // then the block's cells are visited coalesced, each finding its query by
 // binary search in LDS.
 constexpr uint32_t kNoDecode = 0xffffffffu;
+// The same pass sets each query's long flag (long_cells semantics): an
+// undecodable cell, cells on more than one face, or an (i, j) span wider than
+// 7 -- from per-query LDS min/max/face-mask reductions.
 __global__ __launch_bounds__(kBlock) void k_cell_query(int64_t nq, const int64_t *offs, const uint64_t *cells,
-                                                       uint32_t *cq, uint32_t *dec)
+                                                       uint32_t *cq, uint32_t *dec, uint8_t *qlong,
+                                                       unsigned long long *nlong)
 {
     __shared__ int64_t so[kBlock + 1];
+    __shared__ int s_imin[kBlock], s_imax[kBlock], s_jmin[kBlock], s_jmax[kBlock];
+    __shared__ uint32_t s_face[kBlock];  // bit f: a cell on face f; bit 8: an undecodable cell
     const int64_t q0 = (int64_t)blockIdx.x * kBlock;
     const int nb = (int)(nq - q0 < (int64_t)kBlock ? nq - q0 : (int64_t)kBlock);
     for (int i = threadIdx.x; i <= nb; i += kBlock) so[i] = offs[q0 + i];
+    s_imin[threadIdx.x] = s_jmin[threadIdx.x] = 1 << 30;
+    s_imax[threadIdx.x] = s_jmax[threadIdx.x] = -1;
+    s_face[threadIdx.x] = 0;
     __syncthreads();
     const int64_t k1 = so[nb];
     for (int64_t k = so[0] + threadIdx.x; k < k1; k += kBlock) {
@@ -492,39 +501,28 @@ __global__ __launch_bounds__(kBlock) void k_cell_query(int64_t nq, const int64_t
         }
         cq[k] = (uint32_t)(q0 + lo);
         int f = 0, i = 0, j = 0;
-        dec[k] = decode13(cells[k], f, i, j) ? ((uint32_t)f << 26 | (uint32_t)i << 13 | (uint32_t)j) : kNoDecode;
-    }
-}
-
-// Long flag of every query (long_cells semantics, from the decodes).
-__global__ void k_qlong(int64_t nq, const int64_t *offs, const uint32_t *dec, uint8_t *qlong,
-                        unsigned long long *nlong)
-{
-    const int64_t q = tid64();
-    if (q >= nq) return;
-    bool lng = false;
-    int f0 = -1, imin = 0, imax = 0, jmin = 0, jmax = 0;
-    for (int64_t k = offs[q]; k < offs[q + 1] && !lng; k++) {
-        const uint32_t d = dec[k];
-        if (d == kNoDecode) {
-            lng = true;
-            break;
-        }
-        const int f = (int)(d >> 26), i = (int)((d >> 13) & 8191u), j = (int)(d & 8191u);
-        if (k == offs[q]) {
-            f0 = f;
-            imin = imax = i;
-            jmin = jmax = j;
+        const bool ok = decode13(cells[k], f, i, j);
+        dec[k] = ok ? ((uint32_t)f << 26 | (uint32_t)i << 13 | (uint32_t)j) : kNoDecode;
+        if (ok) {
+            atomicOr(&s_face[lo], 1u << f);
+            atomicMin(&s_imin[lo], i);
+            atomicMax(&s_imax[lo], i);
+            atomicMin(&s_jmin[lo], j);
+            atomicMax(&s_jmax[lo], j);
         } else {
-            lng = f != f0;
-            imin = min(imin, i);
-            imax = max(imax, i);
-            jmin = min(jmin, j);
-            jmax = max(jmax, j);
+            atomicOr(&s_face[lo], 1u << 8);
         }
     }
-    const bool is_long = lng || imax - imin > 7 || jmax - jmin > 7;
-    qlong[q] = is_long ? 1 : 0;
+    __syncthreads();
+    const int t = threadIdx.x;
+    bool is_long = false;
+    if (t < nb) {
+        const uint32_t fm = s_face[t];
+        // no cells: not long; else undecodable / multi-face / wide span
+        is_long = fm != 0 && ((fm >> 8) != 0 || __popc(fm) > 1 || s_imax[t] - s_imin[t] > 7 ||
+                              s_jmax[t] - s_jmin[t] > 7);
+        qlong[q0 + t] = is_long ? 1 : 0;
+    }
     const unsigned long long m = __ballot(is_long);
     if (m && (threadIdx.x & 63) == __builtin_ctzll(m)) atomicAdd(nlong, (unsigned long long)__popcll(m));
 }
@@ -1546,12 +1544,12 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     if (nqc == 0) return empty();
     uint32_t *cq = cq_.ensure(nqc + 1);
     uint32_t *dec = dec_.ensure(nqc + 1);
-    hipLaunchKernelGGL(k_cell_query, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_offs, q_cells, cq, dec);
     int64_t *kcnt = c0_.ensure(nqc + 1), *koff = c1_.ensure(nqc + 2);
     uint8_t *qlong = qlong_.ensure(nq + 1);
     unsigned long long *nlongq_d = counter_.ensure(8) + 5;
     DSS_HIP(hipMemsetAsync(nlongq_d, 0, sizeof(unsigned long long), s));
-    hipLaunchKernelGGL(k_qlong, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_offs, dec, qlong, nlongq_d);
+    hipLaunchKernelGGL(k_cell_query, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_offs, q_cells, cq, dec, qlong,
+                       nlongq_d);
     hipLaunchKernelGGL(k_qcells<0>, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, ix, qv, nqc, cq, dec, kcnt, nullptr,
                        nullptr, nullptr, nullptr, nullptr, nullptr);
     exclusive_scan_i64(kcnt, koff, nqc, tmp_, s);
