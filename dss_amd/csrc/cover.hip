@@ -1078,9 +1078,19 @@ __global__ void k_counts(int64_t n, const int64_t *coff, const unsigned long lon
     dc64[f] = (int64_t)dcnt[f];
 }
 
+// Per footprint: where its kept candidates start in the output, less their
+// rank among all kept candidates (so an emitted cell lands at ebase[f] +
+// kept_rank(c), one load instead of three).
+__global__ void k_emit_base(int64_t n, const int64_t *coff, const unsigned long long *kmask, const int64_t *gpos,
+                            const int64_t *offs, int64_t *ebase)
+{
+    const int64_t f = tid64();
+    if (f < n) ebase[f] = offs[f] - kept_rank(coff[f], kmask, gpos);
+}
+
 __global__ void k_cand_emit(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
                             const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo,
-                            const unsigned long long *kmask, const int64_t *gpos, const int64_t *offs, uint64_t *cells)
+                            const unsigned long long *kmask, const int64_t *gpos, const int64_t *ebase, uint64_t *cells)
 {
     const int64_t c = tid64();
     if (c >= NC) return;
@@ -1091,7 +1101,7 @@ __global__ void k_cand_emit(int64_t NC, const uint32_t *cand_f, const int64_t *c
     uint32_t i, j;
     uint64_t id;
     cand_cell(c, f, coff, st_id, st_i, st_j, finfo, face, i, j, id);
-    cells[offs[f] + (kept_rank(c, kmask, gpos) - kept_rank(coff[f], kmask, gpos))] = id;
+    cells[ebase[f] + kept_rank(c, kmask, gpos)] = id;
 }
 
 __global__ void k_u64_to_i64(int64_t n, const unsigned long long *a, int64_t *b)
@@ -1264,9 +1274,12 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     DSS_HIP(hipMemcpyAsync(&total, offs + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
     uint64_t *cells = cells_.ensure(total + 1);
-    if (NC > 0)
+    if (NC > 0) {
+        int64_t *ebase = fc64_.ensure(n + 1);  // tot64 is consumed by the scan above
+        hipLaunchKernelGGL(k_emit_base, dim3(grid_for(n, B)), dim3(B), 0, s, n, coff, kmask, gpos, offs, ebase);
         hipLaunchKernelGGL(k_cand_emit, dim3(grid_for(NC, B)), dim3(B), 0, s, NC, cand_f, coff, st_id, st_i, st_j, finfo,
-                           kmask, gpos, offs, cells);
+                           kmask, gpos, ebase, cells);
+    }
     if (nn > 0) {
         uint32_t *big = big_.ensure(nn + 1);
         int *nbig = flag_.ensure(1);
