@@ -53,11 +53,18 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=1)
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug only; invalid for the metric)")
+    ap.add_argument("--query-scale", type=float, default=1.0,
+                    help="queries per step relative to the config's 1M (configs[4] at full size: 0.1, since its output "
+                         "grows with batch x airspace density: ~5.7k pairs per query against 50M corridors)")
     ap.add_argument("--cpu-sample", type=int, default=-1,
-                    help="queries in the CPU-baseline sample (-1: the whole step's batch, 0: skip)")
+                    help="queries in the CPU-baseline sample (-1: auto -- the whole step's batch for configs[0]/[1], a "
+                         "bounded sample of ~10-30 s of CPU work for the larger airspaces; 0: skip).  The sample's "
+                         "cells and pairs are compared with the GPU step's (parity on the sampled queries)")
     ap.add_argument("--no-verify", action="store_true", help="skip the full-size GPU-vs-oracle parity check")
     ap.add_argument("--survey-model", type=int, default=1, help="also count SURVEY s8(d)'s per-query byte model")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0: the process's CPU share -- the affinity mask, capped by "
+                         "OMP_NUM_THREADS, which the GPU box sets to its per-GPU share of 16)")
     ap.add_argument("--mode", choices=["sharded", "replica"], default="replica",
                     help="multi-GPU layout: replica (index on every GPU, queries split; default) or sharded (index "
                          "split by cell range, queries and pairs exchanged by all-to-all)")
@@ -94,7 +101,7 @@ def main():
     # ---------------------------------------------------------------- setup
     t_setup = time.time()
     # same airspace on every rank (config seed), a rank-private query batch
-    queries, qa, intents, ia, now, rid = W.config_split(args.config, rank, args.scale)
+    queries, qa, intents, ia, now, rid = W.config_split(args.config, rank, args.scale, args.query_scale)
     nq, ni = queries.n, intents.n
     tlo = np.maximum(qa.t0, now)  # operations.go:398-402 COALESCE(ends_at >= start) AND ends_at >= now
     t = lambda a: torch.as_tensor(a, device=dev)  # noqa: E731
@@ -482,18 +489,59 @@ def cover_fp64(nq, ni):
             "all": {k: round(v["tflops"], 2) for k, v in d["kernels"].items() if v["tflops"] > 0.5}}
 
 
+def cpu_info():
+    """Host CPU facts for the baseline line: model (lscpu / /proc/cpuinfo),
+    logical CPUs of the machine (nproc) and of this process (affinity)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    return {"model": model, "nproc": os.cpu_count(), "affinity": aff}
+
+
+def cpu_threads(args):
+    if args.cpu_threads > 0:
+        return args.cpu_threads
+    info = cpu_info()
+    share = info["affinity"]
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        share = min(share, int(omp))
+    return max(1, share)
+
+
+# CPU-baseline sample per config when --cpu-sample is -1 (auto): the oracle's
+# cost per query grows with the airspace density, so the bounded samples keep
+# the baseline near 10-30 s of CPU work on 16 cores.
+AUTO_CPU_SAMPLE = {0: None, 1: None, 2: None, 3: None, 4: 20000}
+
+
 def cpu_baseline(args, ctx, intents, ia, queries, qa, now, i_offs, i_cells, g_cells, g_pairs):
-    """The CPU restatement (oracle/, kind "port": pthreads over the box's
-    host cores) timed on the same step: cover the sample's query footprints
-    and search them against the same intent posting list (built untimed).
-    When the sample is the whole batch, the oracle's cell sets and pair set
-    are also compared with the GPU step's (full-size parity)."""
+    """The CPU restatement (oracle/, kind "port": pthreads over the process's
+    CPU share) timed on the same step: cover the sample's query footprints and
+    search them against the same intent posting list (built untimed).  The
+    sample is the first n queries of the batch; their oracle cell sets and
+    pair set are compared with the GPU step's (every cell and every pair of the
+    sampled queries; the whole batch for configs[0]/[1])."""
     from dss_amd import device as D
     from oracle import oracle as O
     O.build()
-    n = queries.n if args.cpu_sample < 0 else min(args.cpu_sample, queries.n)
+    n = args.cpu_sample
+    if n < 0:
+        auto = AUTO_CPU_SAMPLE.get(args.config)
+        n = queries.n if auto is None else auto
+    n = min(n, queries.n)
     sub = queries if n == queries.n else queries.subset(np.arange(n))
-    th = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    th = cpu_threads(args)
     idx = O.Index(i_offs, i_cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1)
     t0 = time.perf_counter()
     qo, qc, _, _ = O.cover_batch(sub.kind, sub.voff, sub.lat, sub.lng, sub.radius_m, nthreads=th)
@@ -501,21 +549,26 @@ def cpu_baseline(args, ctx, intents, ia, queries, qa, now, i_offs, i_cells, g_ce
     tlo = np.maximum(qa.t0[:n], now)
     rq, re = idx.search(qo, qc, qa.alt_lo[:n], qa.alt_hi[:n], tlo, qa.t1[:n], nthreads=th)
     t2 = time.perf_counter()
+    info = cpu_info()
     cpu = {"value": n / (t2 - t0), "unit": "queries/s", "cores": th, "kind": "port",
            "sample": f"{n} of the step's {queries.n} queries (cover + search) vs the full {intents.n}-intent index",
-           "coverings_per_s": n / (t1 - t0), "seconds": t2 - t0}
+           "coverings_per_s": n / (t1 - t0), "seconds": t2 - t0, "cpu_model": info["model"],
+           "nproc": info["nproc"], "affinity_cpus": info["affinity"],
+           "threads_note": "threads = the process's CPU share on the GPU box (OMP_NUM_THREADS / affinity)"}
     parity = None
-    if n == queries.n and not args.no_verify:
+    if not args.no_verify:
         g_offs = D.copy_back(ctx, g_cells.offs, n + 1, np.int64)
         g_c = D.copy_back(ctx, g_cells.cells, int(g_offs[-1]), np.uint64)
         gq = D.copy_back(ctx, g_pairs.q, int(g_pairs.n), np.uint32)
         ge = D.copy_back(ctx, g_pairs.e, int(g_pairs.n), np.uint32)
-        gk = np.sort((gq.astype(np.uint64) << np.uint64(32)) | ge.astype(np.uint64))
+        keep = gq < n
+        gk = np.sort((gq[keep].astype(np.uint64) << np.uint64(32)) | ge[keep].astype(np.uint64))
         ok = (rq.astype(np.uint64) << np.uint64(32)) | re.astype(np.uint64)
         ok.sort()
-        parity = {"queries": n, "cells_equal": bool(np.array_equal(g_offs, qo) and np.array_equal(g_c, qc)),
+        parity = {"queries": n, "of_batch": queries.n, "cells_equal": bool(np.array_equal(g_offs, qo) and
+                                                                            np.array_equal(g_c, qc)),
                   "pairs_equal": bool(np.array_equal(gk, ok)), "gpu_pairs": int(len(gk)), "oracle_pairs": int(len(ok)),
-                  "cells": int(len(qc))}
+                  "cells": int(len(qc)), "unique": bool(len(gk) == 0 or np.all(gk[1:] != gk[:-1]))}
     return cpu, parity
 
 
