@@ -244,8 +244,7 @@ def main():
     # inputs (24 B attributes + 8 B per covering cell), every posting of a
     # cell the batch touches read once (28 B: entity id, alt pair, time
     # pair), and the output pairs (8 B).
-    q_cells_h = D.copy_back(ctx, cells.cells, c_tot, np.uint64)
-    p_touched = touched_postings(i_cells_h, q_cells_h)
+    p_touched = touched_postings(ctx, D, index, cells)
     join_bytes = 24 * nq + 8 * c_tot + 28 * p_touched + 8 * r_tot
     achieved = join_bytes / (kern_avg_ms * 1e-3) / 1e9
     # SURVEY s8(d) per-query model (B_q summed over queries, each query
@@ -280,7 +279,7 @@ def main():
             "config": {"workload": f"configs[{args.config}]: {nq} query footprints/GPU/step vs {ni}-entity resident "
                                    f"index, {W.CONFIG_NAMES[args.config]}, S2 level 13"
                                    + (" (SearchISAs semantics)" if rid else ""),
-                       "queries_per_gpu_step": nq, "intents": ni, "postings": n_post,
+                       "queries_per_gpu_step": nq, "intents": ni, "postings": n_post, "index": index_info(ctx, index),
                        "parallelism": f"query-sharded x{world}, index replicated", "scale": args.scale,
                        "pipelines_per_gpu": args.pipelines},
             "coverings_per_s": world * nq / (cover_avg * 1e-3),
@@ -359,9 +358,7 @@ def sharded_report(args, ctx, D, dist, torch, sh, step, full, i_cells_h, ranges,
     phase = dict(zip(["cover"] + names + ["join_kernel"], ph))
     # shard join roofline (DESIGN.md s5 byte model over what this shard joined)
     rc = sh.last_recv_cells.cpu().numpy().view(np.uint64)
-    lo, hi = ranges[rank]
-    own = i_cells_h[(i_cells_h >= np.uint64(lo)) & (i_cells_h <= np.uint64(hi))]
-    p_touched = touched_postings(own, rc)
+    p_touched = sh.last_touched
     jb = 24 * sh.last_rows + 8 * len(rc) + 28 * p_touched + 8 * sh.last_shard_pairs
     kern = ph[-1]
     local = torch.tensor([jb / (float(np.mean(kern_ms)) * 1e-3) / 1e9, float(sh.last_rows), float(len(rc)),
@@ -448,10 +445,22 @@ def sort_phase(ctx, torch, dev, i_offs, i_cells):
             "note": "level-13 ids vary in bits 35..63 only: 4 digit passes of <= 8 bits"}
 
 
-def touched_postings(i_cells, q_cells):
-    """Postings whose cell is one of the batch's query cells (each counted once)."""
-    u, cnt = np.unique(i_cells, return_counts=True)
-    return int(cnt[np.isin(u, np.unique(q_cells), assume_unique=True)].sum())
+def touched_postings(ctx, D, index, cells):
+    """Postings of the distinct cells the batch's queries cover, each counted
+    once (dssg_search_touched_device)."""
+    import ctypes as C
+    out = C.c_int64()
+    ctx.check(ctx.L.dssg_search_touched_device(ctx.h, index, cells.n, C.c_void_p(cells.offs), C.c_void_p(cells.cells),
+                                               D._stream_ptr(), C.byref(out)))
+    return int(out.value)
+
+
+def index_info(ctx, index):
+    import ctypes as C
+    v = [C.c_int64() for _ in range(6)]
+    ctx.check(ctx.L.dssg_index_info(index, *[C.byref(x) for x in v]))
+    return dict(zip(["postings", "cells", "long_duration_postings", "long_footprint_postings", "max_cell_postings",
+                     "dcap_us"], [x.value for x in v]))
 
 
 def pmc_traffic(kernel, nq, ni):

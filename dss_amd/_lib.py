@@ -50,7 +50,7 @@ class Cells(C.Structure):
 
 
 class Pairs(C.Structure):
-    _fields_ = [("q", C.c_void_p), ("e", C.c_void_p), ("n", C.c_int64)]
+    _fields_ = [("q", C.c_void_p), ("e", C.c_void_p), ("n", C.c_int64), ("n_tagged", C.c_int64)]
 
 
 MAX_PARTS = 64
@@ -153,6 +153,8 @@ def load():
         L.dssg_join_longs.argtypes = [vp, P(i64), P(i64)]
         L.dssg_search_counters.argtypes = [vp, P(i64), P(i64), P(i64), P(i64), P(i64)]
         L.dssg_search_stats_device.argtypes = [vp, vp, i64, vp, vp, vp, P(i64), P(i64)]
+        L.dssg_search_touched_device.argtypes = [vp, vp, i64, vp, vp, vp, P(i64)]
+        L.dssg_index_info.argtypes = [vp, P(i64), P(i64), P(i64), P(i64), P(i64), P(i64)]
         L.dssg_copy_to_host.argtypes = [vp, vp, vp, C.c_size_t]
         L.dssg_radix_sort_device.argtypes = [vp, C.c_int, i64, C.c_int, vp, vp, vp, vp, vp, P(d)]
         L.dssg_selftest_scan.argtypes = [vp, i64, C.c_int, P(i64), P(i64)]

@@ -368,6 +368,7 @@ int dssg_area_to_cell_ids(dssg_ctx *ctx, const char *area, uint64_t *out_cells, 
         counter++;
         if (c == std::string::npos) break;
         pos = c + 1;
+        if (pos == a.size()) break;  // splitAtComma at EOF with no data left: no empty final token
     }
     int32_t kind = DSSG_KIND_POINTS;
     int64_t voff[2] = {0, (int64_t)lat.size()};
@@ -810,6 +811,29 @@ int dssg_search_stats_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, c
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
         ctx->search.stats(idx, nq, d_q_offs, d_q_cells, s, matched, distinct);
     });
+}
+
+int dssg_search_touched_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *d_q_offs,
+                               const uint64_t *d_q_cells, void *stream, int64_t *touched)
+{
+    if (!ctx || !idx || nq < 0 || !touched || (nq > 0 && !d_q_offs)) return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        *touched = ctx->search.touched(idx, nq, d_q_offs, d_q_cells, s);
+    });
+}
+
+int dssg_index_info(const dssg_index *idx, int64_t *postings, int64_t *cells, int64_t *long_duration,
+                    int64_t *long_footprint, int64_t *max_cell_postings, int64_t *dcap_us)
+{
+    if (!idx) return DSSG_ERR_INVALID;
+    if (postings) *postings = idx->n_p;
+    if (cells) *cells = idx->n_cells;
+    if (long_duration) *long_duration = idx->n_long;
+    if (long_footprint) *long_footprint = idx->n_long_fp;
+    if (max_cell_postings) *max_cell_postings = idx->max_cell_postings;
+    if (dcap_us) *dcap_us = idx->dcap;
+    return DSSG_OK;
 }
 
 int dssg_copy_to_host(dssg_ctx *ctx, void *dst, const void *src, size_t bytes)

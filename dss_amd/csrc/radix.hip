@@ -81,9 +81,10 @@ __device__ __forceinline__ uint32_t block_incl_scan(uint32_t x, uint32_t *ws, ui
 }
 
 template <typename K>
-__global__ __launch_bounds__(kRBlock) void k_rs_hist(const K *__restrict__ keys, int64_t n, int shift, int rbits,
-                                                     uint32_t *__restrict__ hist, int64_t stride)
+__global__ __launch_bounds__(kRBlock) void k_rs_hist(const K *__restrict__ keys, int64_t n, const int64_t *__restrict__ dn,
+                                                     int shift, int rbits, uint32_t *__restrict__ hist, int64_t stride)
 {
+    if (dn) n = min(n, *dn);
     __shared__ uint32_t h[kRWaves][kMaxDigits];
     const int tid = threadIdx.x, w = tid >> 6;
     const uint32_t nd = 1u << rbits, mask = nd - 1;
@@ -136,10 +137,12 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scan(uint32_t *__restrict__ hist
 
 template <typename K, typename V, bool HAS_V>
 __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki, const V *__restrict__ vi,
-                                                        K *__restrict__ ko, V *__restrict__ vo, int64_t n, int shift,
-                                                        int rbits, const uint32_t *__restrict__ hist, int64_t stride,
+                                                        K *__restrict__ ko, V *__restrict__ vo, int64_t n,
+                                                        const int64_t *__restrict__ dn, int shift, int rbits,
+                                                        const uint32_t *__restrict__ hist, int64_t stride,
                                                         const uint32_t *__restrict__ dtot)
 {
+    if (dn) n = min(n, *dn);
     __shared__ uint32_t wh[kRWaves][kMaxDigits];  // per-wave digit counters, then their exclusive prefix over waves
     __shared__ uint32_t dstart[kMaxDigits];       // tile-local start of each digit
     __shared__ uint32_t gbase[kMaxDigits];        // global position of tile slot 0 of each digit
@@ -289,10 +292,12 @@ __global__ __launch_bounds__(kRBlock) void k_rs_or_parts(const unsigned long lon
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 template <typename K, typename V, bool HAS_V>
-void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, int bits, DevBuf<unsigned char> &tmp, hipStream_t s)
+void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, const int64_t *dn, int bits, DevBuf<unsigned char> &tmp,
+                hipStream_t s)
 {
     if (n <= 0) return;
-    if (n >= ((int64_t)1 << 31)) throw Error(DSSG_ERR_CAPACITY, "radix sort: more than 2^31 keys");
+    // positions are uint32: the digit offsets of the last tile stay < 2^32
+    if (n >= ((int64_t)1 << 32) - kTile) throw Error(DSSG_ERR_CAPACITY, "radix sort: more than 2^32 - 4096 keys");
     const int kbits = (int)(8 * sizeof(K));
     if (bits > kbits) bits = kbits;
     if (bits <= 0) {
@@ -305,7 +310,7 @@ void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, int bits, Dev
     // wide keys: sort only the span of bits that vary (one read + one host
     // sync, against up to 4 passes saved)
     int lo = 0;
-    if (bits > 24) {
+    if (bits > 24 && !dn) {  // (a device-side count: the caller's exact bit width)
         const int g = (int)std::min<int64_t>(ntiles, 1024);
         unsigned long long *vm = (unsigned long long *)tmp.ensure(std::max(hist_b + dtot_b, sizeof(unsigned long long) * (g + 1))),
                            *part = vm + 1;
@@ -340,10 +345,10 @@ void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, int bits, Dev
         const bool to_out = ((passes - 1 - p) & 1) == 0;
         K *dst = to_out ? ko : kalt;
         V *dstv = to_out ? vo : valt;
-        hipLaunchKernelGGL(k_rs_hist<K>, dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src, n, shift, r, hist, stride);
+        hipLaunchKernelGGL(k_rs_hist<K>, dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src, n, dn, shift, r, hist, stride);
         hipLaunchKernelGGL(k_rs_scan, dim3(1u << r), dim3(kRBlock), 0, s, hist, stride, ntiles, dtot);
         hipLaunchKernelGGL((k_rs_scatter<K, V, HAS_V>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src, srcv, dst, dstv,
-                           n, shift, r, hist, stride, dtot);
+                           n, dn, shift, r, hist, stride, dtot);
         DSS_HIP(hipGetLastError());
         src = dst;
         srcv = dstv;
@@ -356,13 +361,20 @@ template <typename K, typename V>
 void radix_sort_pairs(const K *ki, K *ko, const V *vi, V *vo, int64_t n, int bits, DevBuf<unsigned char> &tmp,
                       hipStream_t s)
 {
-    radix_sort<K, V, true>(ki, ko, vi, vo, n, bits, tmp, s);
+    radix_sort<K, V, true>(ki, ko, vi, vo, n, nullptr, bits, tmp, s);
+}
+
+template <typename K, typename V>
+void radix_sort_pairs_dn(const K *ki, K *ko, const V *vi, V *vo, int64_t n_max, const int64_t *dn, int bits,
+                         DevBuf<unsigned char> &tmp, hipStream_t s)
+{
+    radix_sort<K, V, true>(ki, ko, vi, vo, n_max, dn, bits, tmp, s);
 }
 
 template <typename K>
 void radix_sort_keys(const K *ki, K *ko, int64_t n, int bits, DevBuf<unsigned char> &tmp, hipStream_t s)
 {
-    radix_sort<K, uint32_t, false>(ki, ko, nullptr, nullptr, n, bits, tmp, s);
+    radix_sort<K, uint32_t, false>(ki, ko, nullptr, nullptr, n, nullptr, bits, tmp, s);
 }
 
 template void radix_sort_pairs<unsigned long, uint32_t>(const unsigned long *, unsigned long *, const uint32_t *,
@@ -372,6 +384,11 @@ template void radix_sort_pairs<uint32_t, uint32_t>(const uint32_t *, uint32_t *,
 template void radix_sort_pairs<uint32_t, unsigned long>(const uint32_t *, uint32_t *, const unsigned long *,
                                                         unsigned long *, int64_t, int, DevBuf<unsigned char> &,
                                                         hipStream_t);
+template void radix_sort_pairs<unsigned long long, uint32_t>(const unsigned long long *, unsigned long long *,
+                                                             const uint32_t *, uint32_t *, int64_t, int,
+                                                             DevBuf<unsigned char> &, hipStream_t);
+template void radix_sort_pairs_dn<uint32_t, uint32_t>(const uint32_t *, uint32_t *, const uint32_t *, uint32_t *, int64_t,
+                                                      const int64_t *, int, DevBuf<unsigned char> &, hipStream_t);
 template void radix_sort_keys<unsigned long long>(const unsigned long long *, unsigned long long *, int64_t, int,
                                                   DevBuf<unsigned char> &, hipStream_t);
 template void radix_sort_keys<unsigned long>(const unsigned long *, unsigned long *, int64_t, int,

@@ -2,63 +2,61 @@
 #pragma once
 #include "common.hpp"
 
+// HBM-resident entity index.  One posting per unique (cell,
+// entity) of the cell range this index serves, sorted by
+//   (slot, duration class, m = min(t0, t1)):
+// a cell's postings are contiguous; within a cell the "regular" postings
+// (entity duration |t1 - t0| <= dcap_thr) come first, sorted by start time m,
+// then the long-duration ones.  A query window [tlo, thi] can only meet a
+// regular posting with m in [tlo - dcap, thi] -- one contiguous range per cell
+// (the band join of search.hip) -- and every long posting of the cell.
 struct dssg_index {
-    int64_t n_e = 0;      // entities
-    int64_t n_p = 0;      // unique (cell, entity) postings
-    int64_t n_reg = 0;    // of which on valid level-13 cells (dense lookup)
-    int64_t n_cells = 0;  // distinct cells
-    int64_t n_b = 0;      // time-bucketed postings (the join's working set)
-    int64_t n_long_b = 0; // of which of long footprints (b_meta 0x40)
+    int64_t n_e = 0;        // entities
+    int64_t n_p = 0;        // postings held (unique (cell, entity) in range, ends_at not NULL)
+    int64_t n_cells = 0;    // distinct cells with postings
+    int64_t n_long = 0;     // postings of long-duration entities
+    int64_t n_long_fp = 0;  // postings of long footprints (b_meta kMetaLongFp)
+    int64_t max_cell_postings = 0;
     uint64_t cell_lo = 0, cell_hi = ~0ull;  // cell range of the postings held (shards)
     bool has_owner = false;
-    // ---- plain postings, sorted by (cell, entity); regular first -------------
-    // A cell's "slot" is its dense slot (level-13 cells) or n_dense + its index
-    // in the irregular side table.
-    dss::DevBuf<uint64_t> p_cell;
-    dss::DevBuf<uint32_t> p_e;  // bit 31: the cell is the entity's smallest cell
-    dss::DevBuf<uint32_t> p_mult;  // times (cell, entity) occurs in the stored cell array (RID
-                                   // `unnest(cells)` counts repeats, subscriptions.go:94-101)
-    uint64_t kmin = 0;          // dense slot k <-> cell (kmin + k) << 35 | 1 << 34
+    // ---- cell -> slot ---------------------------------------------------------
+    // valid level-13 ids: slot = (cell >> 35) - kmin when < n_dense; any other
+    // id (the reference tests use invalid face-7 ids as opaque keys, Q12):
+    // n_dense + its index in the sorted irr_cells.
+    uint64_t kmin = 0;
     int64_t n_dense = 0;
-    dss::DevBuf<uint32_t> dense;  // n_dense + 1 plain posting offsets
     int64_t n_irr = 0;
-    dss::DevBuf<uint64_t> irr_cells;  // sorted, n_irr
-    dss::DevBuf<uint32_t> irr_start;  // n_irr + 1, absolute plain offsets
-    // entity -> sorted unique cells (smallest-shared-cell rule)
-    dss::DevBuf<int64_t> e_offs;
+    dss::DevBuf<uint64_t> irr_cells;  // n_irr, sorted
+    dss::DevBuf<uint64_t> s_post;     // n_slots + 1: first posting of each slot
+    dss::DevBuf<uint32_t> s_nreg;     // n_slots: regular-duration postings of the slot
+    // ---- time --------------------------------------------------------------------
+    int64_t dcap = 0;      // max duration of a regular posting's entity (us)
+    int64_t dcap_thr = 0;  // class threshold: duration <= dcap_thr is regular
+    int64_t tbase = 0;     // query-order quantisation: (tlo - tbase) >> qshift
+    int qshift = 0;
+    // ---- postings ----------------------------------------------------------------
+    dss::DevBuf<uint32_t> b_e;      // entity | kFirstBit (the cell is the entity's smallest)
+    dss::DevBuf<uint8_t> b_meta;    // kMetaCompact | kMetaLongFp
+    dss::DevBuf<float2> b_alt;      // (alt_lo, alt_hi)
+    dss::DevBuf<longlong2> b_t;     // (t0, t1) microseconds
+    dss::DevBuf<ulonglong2> b_sig;  // 2 per posting: 256-bit near-prefix signature
+    dss::DevBuf<int32_t> b_owner;   // has_owner
+    dss::DevBuf<uint32_t> b_mult;   // times (cell, entity) occurs in the stored array (has_mult)
+    bool has_mult = false;
+    // ---- entities ------------------------------------------------------------------
+    dss::DevBuf<int64_t> e_offs;    // entity -> sorted unique cells (all of them, any range)
     dss::DevBuf<uint64_t> e_cells;
-    // ---- time buckets ---------------------------------------------------------
-    // bucket(t) = clamp((t - tbase) >> shift, 0, nb - 1), nb <= 61; bucket 63
-    // holds, once, the entities spanning more than kLongSpan buckets.
-    int64_t tbase = 0;
-    int shift = 0;
-    int nb = 1;
-    // ---- bucketed postings, sorted by (slot, bucket, entity) -----------------
-    // Group g = one non-empty (slot, bucket); g = s_base[slot] +
-    // popcount(s_mask[slot] & ((1 << bucket) - 1)); postings [bk_start[g], bk_start[g+1]).
-    dss::DevBuf<unsigned long long> s_mask;  // n_slots
-    dss::DevBuf<uint32_t> s_base;            // n_slots + 1
-    dss::DevBuf<uint32_t> bk_start;          // n_groups + 1
-    dss::DevBuf<uint64_t> g_key;             // n_groups: slot << 6 | bucket
-    int64_t n_groups = 0;
-    int64_t tiles_total = 0, tiles_max = 0;  // join-unit posting tiles (sum, max over groups)
-    dss::DevBuf<uint32_t> b_e;               // entity | first bit
-    dss::DevBuf<float2> b_alt;               // (alt_lo, alt_hi)
-    dss::DevBuf<longlong2> b_t;              // (t0, t1) microseconds
-    dss::DevBuf<uint8_t> b_meta;             // entity's first bucket | compact << 7
-    dss::DevBuf<ulonglong2> b_sig;           // 2 per posting: 256-bit prefix signature
-    dss::DevBuf<int32_t> b_owner;
-    // ---- entity-level attributes (subscription-store queries, subs.hip) ------
-    dss::DevBuf<int64_t> e_t1;     // ends_at (us)
-    dss::DevBuf<int32_t> e_owner;  // owner id (has_owner)
-    dss::DevBuf<uint32_t> o_key;   // owner ^ 0x80000000, ascending (owner -> entities)
-    dss::DevBuf<uint32_t> o_ent;   // entity ids in o_key order
-    dss::DevBuf<int64_t> e_notify; // notification_index counters
+    dss::DevBuf<int64_t> e_t1;      // ends_at (us)
+    dss::DevBuf<int32_t> e_owner;   // owner id (has_owner)
+    dss::DevBuf<uint32_t> o_key;    // owner ^ 0x80000000, ascending (owner -> entities)
+    dss::DevBuf<uint32_t> o_ent;    // entity ids in o_key order
+    dss::DevBuf<int64_t> e_notify;  // notification_index counters
     // tombstones (write path, store.hip): bit e set = entity e is deleted or
     // superseded; the join and the subscription queries skip it
     dss::DevBuf<uint32_t> dead;
     bool has_dead = false;
     int device = 0;
+    int64_t n_slots() const { return n_dense + n_irr; }
 };
 
 namespace dss {
@@ -67,11 +65,14 @@ class SearchEngine {
    public:
     // Postings are kept only for cells in [cell_lo, cell_hi] (a cell-range
     // shard); entity cell lists stay whole, so the smallest-shared-cell rule
-    // emits every pair on exactly one shard.
+    // emits every pair on exactly one shard (long x long pairs: see search()).
     void build(dssg_index *idx, int64_t n, const int64_t *cell_offs, const uint64_t *cells, const float *alt_lo,
                const float *alt_hi, const int64_t *t0, const int64_t *t1, const int32_t *owner, uint64_t cell_lo,
                uint64_t cell_hi, hipStream_t s);
-    // q cells must be sorted ascending and unique per query.
+    // q cells must be sorted ascending and unique per query.  Output: every
+    // matching (query, entity) pair once; out->n_tagged of them (the last
+    // ones) are long x long pairs, deduplicated within this index only (a
+    // cell-range shard can meet such a pair again on another shard).
     void search(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
                 const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
                 const int32_t *q_owner, hipStream_t s, dssg_pairs *out);
@@ -79,22 +80,26 @@ class SearchEngine {
     // (predicate disabled), i.e. sum_q M_q and sum_q D_q of SURVEY s8(d).
     void stats(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells, hipStream_t s,
                int64_t *matched, int64_t *distinct);
+    // Postings of the distinct cells the batch touches, each once.
+    int64_t touched(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells, hipStream_t s);
     void set_timing(bool on) { timing_ = on; }
     double last_join_kernel_ms() const { return join_ms_; }
     int64_t last_units() const { return units_; }
     int64_t last_keys() const { return keys_; }
-    // timing mode only: runs, wave iterations (records x tiles), useful lane tests
-    // timing mode only: output flushes, exact list merges (events, lanes)
     int64_t last_tagged() const { return tagged_; }  // long x long pair occurrences before the dedupe
-    // long queries in the last batch, long postings of its index (both > 0:
-    // the join ran its long x long tagging variant)
-    void last_longs(int64_t *lq, int64_t *lp) const { *lq = long_queries_; *lp = long_postings_; }
+    void last_longs(int64_t *lq, int64_t *lp) const
+    {
+        *lq = long_queries_;
+        *lp = long_postings_;
+    }
     void last_join_events(int64_t *flushes, int64_t *merges, int64_t *merge_lanes) const
     {
         *flushes = flushes_;
         *merges = merges_;
         *merge_lanes = merge_lanes_;
     }
+    // runs = records joined on the sparse (one lane per record) path; iters =
+    // posting broadcasts of the dense path; tests = record x posting lane tests
     void last_work(int64_t *runs, int64_t *iters, int64_t *tests) const
     {
         *runs = runs_;
@@ -103,20 +108,18 @@ class SearchEngine {
     }
 
    private:
-    DevBuf<unsigned char> tmp_;
-    DevBuf<uint64_t> k0_, k1_, uk_;
-    DevBuf<uint32_t> v0_, v1_, v2_, v3_, ur_, up_, uq_, cq_, gb_, ge_, dec_;
-    DevBuf<int64_t> c0_, c1_, rc_, rs_, nr_, uc_, uo_;
-    DevBuf<unsigned long long> counter_;
-    DevBuf<uint32_t> oq_, oe_, oq2_, oe2_;
-    DevBuf<unsigned char> rec_;
-    DevBuf<int32_t> own_;
+    DevBuf<unsigned char> tmp_, tmp2_;
+    // query side
+    DevBuf<uint32_t> cq_, dec_, okey_, okey2_, oval_, perm_, kkey_, kkey2_, kval_, kval2_, rbeg_, bt_;
+    DevBuf<int64_t> qcnt_, qoff_, rcnt_, roff_, ucnt_, uoff_, cnt64_;
     DevBuf<uint8_t> qlong_;
-    DevBuf<unsigned long long> tkey_, tkey2_;  // tagged (long x long) pairs, deduplicated after the join
-    DevBuf<uint32_t> work_;
-    DevBuf<unsigned char> units_buf_;  // join unit descriptors
+    DevBuf<unsigned char> rec_, units_buf_, batch_buf_;
+    DevBuf<unsigned long long> counter_, regcnt_;
+    DevBuf<uint32_t> oq_, oe_, oq2_, oe2_, work_, fills_;
+    DevBuf<unsigned long long> tkey_, tkey2_;
     int n_cu_ = 0;
     size_t out_cap_ = 0;
+    int64_t units_cap_hint_ = 0, sparse_cap_hint_ = 0;
     bool timing_ = false;
     double join_ms_ = 0;
     int64_t units_ = 0, keys_ = 0, runs_ = 0, iters_ = 0, tests_ = 0;

@@ -17,7 +17,7 @@
 //    fetchMaxSubscriptionCountByCellAndOwner (pkg/scd/store/cockroach/
 //    subscriptions.go:255-283): max over the query cells of the owner's
 //    unexpired subscriptions in that cell, counting repeats of the cell in a
-//    stored array (RID `unnest(cells)`) -- p_mult.
+//    stored array (RID `unnest(cells)`) -- b_mult.
 #include <hip/hip_runtime.h>
 
 
@@ -45,15 +45,16 @@ __global__ void k_max_count(IndexView a, int64_t nqc, const uint64_t *cells, con
 {
     const int64_t k = tid64();
     if (k >= nqc) return;
-    uint32_t slot = 0, s = 0, e = 0;
+    uint32_t slot = 0;
+    uint64_t s = 0, e = 0;
     if (!find_slot(a, cells[k], slot)) return;
-    plain_range(a, slot, s, e);
+    slot_range(a, slot, s, e);
     const uint32_t q = cq[k];
     const int32_t own = owner[q];
     unsigned long long cnt = 0;
-    for (uint32_t p = s; p < e; p++) {
-        const uint32_t ent = a.p_e[p] & ~kFirstBit;
-        if (a.e_owner[ent] == own && a.e_t1[ent] >= now && !is_dead(a, ent)) cnt += a.p_mult[p];
+    for (uint64_t p = s; p < e; p++) {
+        const uint32_t ent = a.b_e[p] & ~kFirstBit;
+        if (a.e_owner[ent] == own && a.e_t1[ent] >= now && !is_dead(a, ent)) cnt += a.b_mult ? a.b_mult[p] : 1u;
     }
     if (cnt) atomicMax(&out[q], cnt);
 }

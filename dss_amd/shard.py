@@ -240,6 +240,12 @@ class ShardedSearch:
                                        C.c_void_p(batch.alt_lo), C.c_void_p(batch.alt_hi), C.c_void_p(batch.tlo),
                                        C.c_void_p(batch.thi), C.c_void_p(0), st, C.byref(pairs)))
         t = self._mark("join", t, timed)
+        if timed:  # roofline accounting: postings of the distinct cells this shard was asked for
+            tch = C.c_int64()
+            ctx.check(L.dssg_search_touched_device(ctx.h, self.index, batch.n, C.c_void_p(batch.offs),
+                                                   C.c_void_p(batch.cells), st, C.byref(tch)))
+            self.last_touched = int(tch.value)
+            t = time.perf_counter()
         # (4) pairs back to their queries' home ranks
         pc = (C.c_int64 * _lib.MAX_PARTS)()
         ctx.check(L.dssg_route_pairs_plan_device(ctx.h, C.byref(batch), C.byref(pairs), W, st, pc))

@@ -84,11 +84,16 @@ typedef struct {
 } dssg_cells;
 
 /* Device-resident search result: unordered set of (query, entity) pairs,
- * each pair once (SQL DISTINCT, quirk Q13). */
+ * each pair once (SQL DISTINCT, quirk Q13).  The last n_tagged pairs are
+ * "long x long" pairs (both footprints spread beyond one 8x8-cell window):
+ * unique within this result, but a cell-range shard (dssg_index_build_range)
+ * can meet such a pair on another shard too, so a sharded caller dedupes
+ * those across shards (the route layer carries the tag). */
 typedef struct {
     const uint32_t *q; /* device */
     const uint32_t *e; /* device */
     int64_t n;
+    int64_t n_tagged;
 } dssg_pairs;
 
 /* ---- context ----------------------------------------------------------- */
@@ -322,11 +327,10 @@ int dssg_route_pairs_fill_device(dssg_ctx *ctx, const dssg_batch *batch, const d
  * phase, measured with HIP events on the launching stream (bench.py). */
 int dssg_phase_times(dssg_ctx *ctx, double *cover_ms, double *join_ms, double *join_kernel_ms);
 void dssg_set_timing(dssg_ctx *ctx, int enabled);
-/* Work counters of the most recent search: (cell, time bucket) keys sorted,
- * join units (64 postings x <= 1024 query records) launched, and -- with
- * timing enabled -- runs (non-empty groups met), wave iterations (records x
- * 64-posting tiles) and useful lane tests (records x postings).  Any
- * pointer may be NULL. */
+/* Work counters of the most recent search: query-cell keys (cells of the
+ * batch whose cell holds postings), join units (<= 64 records x a posting
+ * range), (cell, query class) runs, posting broadcasts (wave iterations) and
+ * record x posting lane tests.  Any pointer may be NULL. */
 int dssg_search_counters(dssg_ctx *ctx, int64_t *keys, int64_t *units, int64_t *runs, int64_t *iters,
                          int64_t *tests);
 /* Join events of the most recent search: output flushes (one atomic each)
@@ -345,6 +349,17 @@ int dssg_join_longs(dssg_ctx *ctx, int64_t *long_queries, int64_t *long_postings
  * altitude/time filter (sum of D_q), SURVEY.md s8(d). */
 int dssg_search_stats_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *d_q_offs,
                              const uint64_t *d_q_cells, void *stream, int64_t *matched, int64_t *distinct);
+/* Postings of the distinct cells a device query batch touches, each counted
+ * once (the 28 B/posting term of the join's algorithmic byte model, DESIGN.md
+ * s5). */
+int dssg_search_touched_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *d_q_offs,
+                               const uint64_t *d_q_cells, void *stream, int64_t *touched);
+/* Index shape: postings held, distinct cells, postings of long-duration
+ * entities (scanned by every record of their cell) and of long footprints,
+ * the largest cell, and dcap (the longest regular duration, us).  Any output
+ * pointer may be NULL. */
+int dssg_index_info(const dssg_index *idx, int64_t *postings, int64_t *cells, int64_t *long_duration,
+                    int64_t *long_footprint, int64_t *max_cell_postings, int64_t *dcap_us);
 /* Copy `bytes` from an engine-owned device buffer (dssg_cells / dssg_pairs)
  * to host memory, on the context's device. */
 int dssg_copy_to_host(dssg_ctx *ctx, void *dst, const void *src, size_t bytes);

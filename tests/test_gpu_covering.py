@@ -35,12 +35,26 @@ def test_polygon_covering_kat():
     ("37.427636,-122.170502,37.408799", "OddNumberOfCoordinatesError"),
     ("37.4,-122.1,abc,-122.2,37.5,-122.3", "BadCoordSetError"),
     ("-23,130,-24,130,-24,132,-23,132", "ErrAreaTooLarge"),
+    # Go's splitAtComma gives no empty final token: 7 tokens -> 3 points + a dropped latitude
+    ("37.4047,-122.1474,37.4037,-122.1485,37.4035,-122.1466,1,", None),
+    ("37.4047,-122.1474,37.4037,-122.1485,37.4035,-122.1466,", "OddNumberOfCoordinatesError"),
+    (",37.4047,-122.1474,37.4037,-122.1485,37.4035", "BadCoordSetError"),
+    ("37.4047,-122.1474,,37.4037,-122.1485,37.4035,-122.1466,1", "BadCoordSetError"),
+    ("37.4047,-122.147_4,37.4037,-122.1485,37.4035,-122.1466", "BadCoordSetError"),
+    (" 37.4047 ,-122.1474,\t37.4037,-122.1485,37.4035,-122.1466 ", None),  # TrimSpace
+    ("0x1.2ap5,-122.1474,37.4037,-122.1485,37.4035,-122.1466", None),    # Go hex float syntax
 ])
-def test_area_to_cell_ids(area, exc):
+def test_area_to_cell_ids(oracle, area, exc):
+    """pkg/geo/s2.go:129-166 through the C ABI: the status, and the cells
+    equal to the restatement (tests/test_oracle_kat.py) over the oracle's
+    Covering."""
     from dss_amd import geo
+    from test_oracle_kat import area_to_cell_ids
     if exc is None:
         cells = geo.AreaToCellIDs(area)
-        assert len(cells) > 0
+        rc, want = area_to_cell_ids(oracle, area)
+        assert rc == oracle.OK
+        assert len(cells) > 0 and [int(c) for c in cells] == [int(c) for c in want]
     else:
         with pytest.raises(getattr(geo, exc)):
             geo.AreaToCellIDs(area)
@@ -157,3 +171,79 @@ def test_fan_orientation_edge_cases(oracle):
     _check_batch(dict(status=status, offs=offs, cells=cells, area_km2=area), res)
     # both outcomes of the cap occur
     assert (status == 0).any() and (status != 0).any()
+
+
+# ---- adversarial geometry: cell boundaries, face edges, poles, antimeridian
+def _face_uv_to_latlng(face, u, v):
+    """S2 face (u, v) -> (lat, lng) degrees (s2 stuv.go faceUVToXYZ)."""
+    x, y, z = [(1, u, v), (-u, 1, v), (-u, -v, 1), (-1, -v, -u), (v, -1, -u), (v, u, -1)][face]
+    return np.degrees(np.arctan2(z, np.hypot(x, y))), np.degrees(np.arctan2(y, x))
+
+
+def _st_to_uv(s):
+    return (4 * s * s - 1) / 3 if s >= 0.5 else (1 - 4 * (1 - s) * (1 - s)) / 3
+
+
+def _corner_uv(rng):
+    """(u, v) of a random level-13 cell corner (i, j multiples of 2^17)."""
+    k = 1 << 13
+    return _st_to_uv(rng.integers(1, k) / k), _st_to_uv(rng.integers(1, k) / k)
+
+
+def test_adversarial_cell_boundaries(oracle):
+    """SURVEY s8(c) residual risk: cells within 1e-15..1e-12 (u, v) of a
+    footprint edge.  Footprints with a vertex on a level-13 cell corner, with
+    an edge running along a cell boundary line (a constant-u great circle)
+    and shifted off it by 1e-15..1e-12, on cube-face edges and face corners;
+    GPU == oracle bit for bit (status, cells, area)."""
+    from dss_amd import geo
+    rng = np.random.default_rng(2024)
+    polys = []
+    d = 4e-5  # ~ a level-13 cell in (u, v) is ~1.2e-4 near the face centre
+    for face in range(6):
+        for _ in range(6):
+            u, v = _corner_uv(rng)
+            # a vertex exactly on the corner, two more nearby
+            a = rng.uniform(0, 2 * np.pi)
+            pts = [(u, v), (u + d * np.cos(a), v + d * np.sin(a)), (u + d * np.cos(a + 2), v + d * np.sin(a + 2))]
+            polys.append([_face_uv_to_latlng(face, *p) for p in pts])
+            # an edge along the constant-u boundary line, then shifted off it
+            for off in (0.0, 1e-15, -1e-15, 1e-14, -1e-13, 1e-12, -1e-12):
+                uu = u + off
+                pts = [(uu, v - 2 * d), (uu, v + 2 * d), (uu + (d if off >= 0 else -d), v)]
+                polys.append([_face_uv_to_latlng(face, *p) for p in pts])
+        # face edges and corners (u, v = +-1)
+        for (u, v) in ((1.0, 0.3), (-1.0, -0.2), (0.4, 1.0), (1.0, 1.0), (-1.0, 1.0), (1.0 - 1e-13, -1.0)):
+            for sgn in (1, -1):
+                pts = [(u, v), (u - sgn * d, v), (u, v - sgn * d)]
+                polys.append([_face_uv_to_latlng(face, *p) for p in pts])
+    kind = np.zeros(len(polys), np.int32)
+    voff = np.zeros(len(polys) + 1, np.int64)
+    voff[1:] = np.cumsum([len(p) for p in polys])
+    lat = np.array([q[0] for p in polys for q in p], dtype=np.float64)
+    lng = np.array([q[1] for p in polys for q in p], dtype=np.float64)
+    rad = np.zeros(len(polys), np.float32)
+    offs, cells, status, area = oracle.cover_batch(kind, voff, lat, lng, rad)
+    res = geo.cover_batch(kind, voff, lat, lng, rad)
+    _check_batch(dict(status=status, offs=offs, cells=cells, area_km2=area), res)
+    assert (status == 0).sum() > len(polys) // 2
+
+
+def test_circles_at_poles_and_antimeridian(oracle):
+    """20-gon circles (Q2) of 50 m .. 2 km centred on / next to the poles and
+    on both sides of the antimeridian (the prober's near-pole pins,
+    monitoring/prober/scd/test_operations_simple.py:32,47,100)."""
+    from dss_amd import geo
+    centres = [(90.0, 0.0), (-90.0, 0.0), (89.999, 0.0), (89.999, 180.0), (-89.9995, -45.0), (0.0, 180.0),
+               (0.0, -180.0), (12.0, 179.9999), (-33.0, -179.99995), (51.5, 180.0), (45.0, 45.0), (35.26438968, 45.0)]
+    radii = (50.0, 120.0, 300.0, 800.0, 2000.0)
+    lat = np.array([c[0] for c in centres for _ in radii])
+    lng = np.array([c[1] for c in centres for _ in radii])
+    rad = np.array([r for _ in centres for r in radii], np.float32)
+    n = len(lat)
+    kind = np.ones(n, np.int32)
+    voff = np.arange(n + 1, dtype=np.int64)
+    offs, cells, status, area = oracle.cover_batch(kind, voff, lat, lng, rad)
+    res = geo.cover_batch(kind, voff, lat, lng, rad)
+    _check_batch(dict(status=status, offs=offs, cells=cells, area_km2=area), res)
+    assert (status == 0).all()

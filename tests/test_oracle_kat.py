@@ -4,6 +4,7 @@ Pins the covering restatement on pkg/models/geo_test.go:10-55 (exact 20-cell
 KAT) and the status-level cases of pkg/geo/s2_test.go:12-52 and the prober.
 """
 import math
+import re
 
 import numpy as np
 import pytest
@@ -12,22 +13,65 @@ KAT_TOKENS = ("808fb0ac 808fb744 808fb754 808fb75c 808fb9fc 808fba04 808fba0c 80
               "808fba64 808fba6c 808fba74 808fba8c 808fbad4 808fbadc 808fbae4 808fbaec 808fbaf4 808fbb2c").split()
 
 
+_GO_FLOAT = re.compile(r"[+-]?(?:(?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?"
+                       r"|0[xX](?:[0-9a-fA-F]+\.?[0-9a-fA-F]*|\.[0-9a-fA-F]+)[pP][+-]?\d+"
+                       r"|[iI][nN][fF](?:[iI][nN][iI][tT][yY])?|[nN][aA][nN])")
+
+
+def go_split_at_comma(area: str):
+    """bufio.Scanner with pkg/geo/s2.go:68-82 splitAtComma: tokens between
+    commas; at EOF the rest is one more token unless it is empty (so a
+    trailing comma yields no empty final token)."""
+    toks, pos = [], 0
+    while True:
+        if pos == len(area):  # atEOF && len(data) == 0
+            return toks
+        i = area.find(",", pos)
+        if i < 0:
+            toks.append(area[pos:])
+            return toks
+        toks.append(area[pos:i])
+        pos = i + 1
+
+
+def go_parse_float(tok: str):
+    """strconv.ParseFloat(tok, 64) acceptance (Go syntax: decimal, hex with a
+    p exponent, inf/infinity/nan; no underscores without a base prefix);
+    None = error."""
+    if not _GO_FLOAT.fullmatch(tok):
+        return None
+    if "x" in tok or "X" in tok:
+        return float.fromhex(tok)
+    return float(tok)
+
+
 def area_to_cell_ids(O, area: str):
-    """pkg/geo/s2.go:129-166 restated on top of the oracle's Covering."""
+    """pkg/geo/s2.go:129-166 restated on top of the oracle's Covering: the
+    comma count decides odd / not-enough first, then every token parses
+    (TrimSpace, ParseFloat) and each (lat, lng) pair becomes a point; a
+    trailing lone latitude is dropped."""
     num = area.count(",") + 1
     if num % 2 == 1:
         return O.ERR_ODD_COORDS, None
     if num // 2 < 3:
         return O.ERR_NOT_ENOUGH_POINTS, None
     vals = []
-    for tok in area.split(","):
-        try:
-            vals.append(float(tok.strip()))
-        except ValueError:
+    for tok in go_split_at_comma(area):
+        v = go_parse_float(tok.strip())
+        if v is None:
             return O.ERR_BAD_COORD_SET, None
-    pts = [O.point_from_degrees(vals[i], vals[i + 1]) for i in range(0, len(vals), 2)]
+        vals.append(v)
+    pts = [O.point_from_degrees(vals[i], vals[i + 1]) for i in range(0, len(vals) - 1, 2)]
     rc, cells, _ = O.covering_xyz(np.array(pts))
     return rc, cells
+
+
+def test_go_split_at_comma():
+    assert go_split_at_comma("1,2,3") == ["1", "2", "3"]
+    assert go_split_at_comma("1,2,3,") == ["1", "2", "3"]
+    assert go_split_at_comma(",1") == ["", "1"]
+    assert go_split_at_comma("1,,2") == ["1", "", "2"]
+    assert go_parse_float("1_000") is None and go_parse_float("0x1p-2") == 0.25 and go_parse_float("") is None
 
 
 def test_polygon_covering_kat(oracle):
@@ -45,6 +89,12 @@ def test_polygon_covering_kat(oracle):
     ("", False),                                                                 # :36-40
     ("37.427636,-122.170502,37.408799,-122.064069", False),                     # :42-46 two points
     ("37.427636,-122.170502,37.408799", False),                                  # :48-52 odd coords
+    # trailing comma: no empty final token (splitAtComma at EOF), so 7 tokens -> 3 points + a dropped lat
+    ("37.4047,-122.1474,37.4037,-122.1485,37.4035,-122.1466,1,", True),
+    ("37.4047,-122.1474,37.4037,-122.1485,37.4035,-122.1466,", False),           # 7 coords: odd
+    (",37.4047,-122.1474,37.4037,-122.1485,37.4035", False),                    # empty first token
+    ("37.4047,-122.1474,,37.4037,-122.1485,37.4035,-122.1466,1", False),       # empty middle token
+    ("37.4047,-122.147_4,37.4037,-122.1485,37.4035,-122.1466", False),          # Go rejects underscores
 ])
 def test_area_to_cell_ids_status(oracle, area, ok):
     rc, cells = area_to_cell_ids(oracle, area)
