@@ -103,8 +103,11 @@ __global__ void k_volume_attrs(int64_t nvol, const int64_t *vol_offs, const int3
     }
     status[v] = st;
     area[v] = ar;
-    oalo[v] = lo;
-    oahi[v] = hi;
+    // NULL out as the search's sentinels (dssgpu.h conventions): a union volume
+    // feeds dssg_search* / the index build directly, and the ordered compares
+    // there treat -INF/+INF like COALESCE(..., true) where NaN would match nothing
+    oalo[v] = isnan(lo) ? -INFINITY : lo;
+    oahi[v] = isnan(hi) ? INFINITY : hi;
     ot0[v] = s;
     ot1[v] = e;
     ofp[v] = fp ? 1 : 0;

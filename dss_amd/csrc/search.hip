@@ -44,8 +44,6 @@ namespace dss {
 namespace {
 
 constexpr unsigned kBlock = 256;
-constexpr int kBatch = 64;              // query records per join unit: one per lane
-constexpr int64_t kChunkMax = 4096;     // postings per join unit at most (longer ranges are split)
 constexpr uint32_t kRank0 = 0x80000000u;     // record: the cell is the query's first cell
 constexpr uint32_t kCompactQ = 0x40000000u;  // record: the query's prefix at this cell is compact
 constexpr uint32_t kLongQ = 0x20000000u;     // record: the query footprint is long (long_cells)
@@ -61,11 +59,7 @@ constexpr uint32_t kWideKey = (1u << kOrderBits) - 1u;  // ... wide queries last
 #ifndef DSS_JOIN_BPC
 #define DSS_JOIN_BPC 6
 #endif
-#ifndef DSS_JOIN_GRAB
-#define DSS_JOIN_GRAB 2
-#endif
 constexpr int kJoinBlocksPerCU = DSS_JOIN_BPC;  // persistent workgroups per CU
-constexpr int kGrab = DSS_JOIN_GRAB;            // join units a wave takes per queue access
 constexpr int kWaves = 4;                       // waves per join workgroup
 
 // ---- level-13 decode + prefix signatures -----------------------------------
@@ -512,18 +506,7 @@ struct alignas(16) QRec {
 };
 static_assert(sizeof(QRec) == 64, "QRec layout");
 
-// Join unit: <= 64 records of one cell x a posting range (regular part, then
-// long part), described in 48 bytes (three scalar loads).
-struct alignas(16) Unit {
-    uint64_t p_lo;  // first regular posting
-    uint64_t l_lo;  // first long posting
-    uint32_t n_reg, n_long;
-    uint32_t r_lo;  // first record (position in the sorted keys)
-    uint32_t nrec;  // records (1..64)
-    uint32_t slot;
-    uint32_t pad[3];
-};
-static_assert(sizeof(Unit) == 48, "Unit layout");
+
 
 __host__ __device__ __forceinline__ bool is_wide(long long tlo, long long thi)
 {
@@ -587,20 +570,33 @@ __global__ __launch_bounds__(kBlock) void k_cell_query(IndexView a, int64_t nq, 
     wave_count(is_long, nlong);
 }
 
-// Query order key: quantised tlo (narrow windows), kWideKey (wide ones).
+// Quantised start: (t - tbase) >> qshift, clamped to [0, kWideKey - 1]
+// (monotone, so a search on it brackets every record of a time range).
+__device__ __forceinline__ uint32_t order_q(long long t, long long tbase, int qshift)
+{
+    const unsigned long long d = t <= tbase ? 0ull : ((unsigned long long)t - (unsigned long long)tbase) >> qshift;
+    return d >= (unsigned long long)(kWideKey - 1) ? kWideKey - 1 : (uint32_t)d;
+}
+
+// Query order key: quantised tlo (narrow windows), kWideKey (wide ones); the
+// widest narrow window of the batch -> *dqmax.
 __global__ void k_qorder(int64_t nq, const int64_t *tlo, const int64_t *thi, long long tbase, int qshift, uint32_t *key,
-                         uint32_t *val)
+                         uint32_t *val, unsigned long long *dqmax)
 {
     const int64_t q = tid64();
-    if (q >= nq) return;
-    const long long a = tlo[q], b = thi[q];
-    uint32_t k = kWideKey;
-    if (!is_wide(a, b)) {
-        const unsigned long long d = a <= tbase ? 0ull : ((unsigned long long)a - (unsigned long long)tbase) >> qshift;
-        k = d >= (unsigned long long)(kWideKey - 1) ? kWideKey - 1 : (uint32_t)d;
+    unsigned long long dq = 0;
+    if (q < nq) {
+        const long long a = tlo[q], b = thi[q];
+        uint32_t k = kWideKey;
+        if (!is_wide(a, b)) {
+            k = order_q(a, tbase, qshift);
+            if (b >= a) dq = (unsigned long long)b - (unsigned long long)a;
+        }
+        key[q] = k;
+        val[q] = (uint32_t)q;
     }
-    key[q] = k;
-    val[q] = (uint32_t)q;
+    for (int o = 32; o > 0; o >>= 1) dq = max(dq, __shfl_xor(dq, o));
+    if ((threadIdx.x & 63) == 0 && dq) atomicMax(dqmax, dq);
 }
 
 // Per query (in order rank r): its cells with postings.
@@ -702,20 +698,6 @@ __device__ __forceinline__ uint64_t ub_m(const longlong2 *bt, uint64_t lo, uint6
     return lo;
 }
 
-// Join units, one wave per window of 64 sorted keys (grid-stride over the
-// device key count).  The window's keys split into pieces at run (cell,
-// query class) boundaries and, for narrow windows, where tlo >> wshift
-// changes (wshift: 2^wshift >= dcap), so a piece's records span at most one
-// such time slice.  A piece of fewer than kSparseMin records goes to the
-// sparse list (k_join_sparse: one lane per record); every other piece becomes
-// one or more units: its records' posting range [min tlo - dcap, max thi]
-// (segmented wave min/max, binary search by the piece's leader lane) plus the
-// cell's long part, split into <= kChunkMax postings.  Unit and sparse slots
-// come from one atomic per wave each.  Units beyond `cap` are counted but not
-// written (the host grows and reruns).
-constexpr int kSparseMin = 6;
-constexpr int kSparseL = 128;
-
 // Work lists written from kRegions counters (spread 256 B apart; one
 // same-address counter saturates at ~88 atomics/us, MI355X_MICROARCH.md
 // "dequeue"): region r holds its items at [r * cap, r * cap + count(r)).
@@ -742,99 +724,6 @@ struct Regions {
     }
 };
 
-__global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *skey, const uint32_t *sval,
-                                                  const QRec *recs, const int64_t *dnkeys, int wshift, Regions ur,
-                                                  Unit *units, Regions sr_, uint32_t *sparse)
-{
-    const int lane = threadIdx.x & 63;
-    const uint32_t nkeys = (uint32_t)*dnkeys;
-    const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
-    const int64_t nwin = ((int64_t)nkeys + 63) / 64;
-    for (int64_t win = wave; win < nwin; win += nwaves) {
-        const uint32_t p = (uint32_t)(win * 64) + (uint32_t)lane;
-        const bool valid = p < nkeys;
-        const uint32_t key = valid ? skey[p] : 0xffffffffu;
-        long long tlo = LLONG_MAX, thi = LLONG_MIN;
-        if (valid) {
-            const QRec *r = recs + sval[p];
-            tlo = r->tlo;
-            thi = r->thi;
-        }
-        // time slice of a narrow record (wide ones: one slice)
-        const long long slice = (key & 1u) ? 0 : (tlo >> wshift);
-        const long long prev_slice = __shfl_up(slice, 1, 64);
-        const bool run_first = valid && (p == 0 || skey[p - 1] != key);
-        const bool start = valid && (lane == 0 || run_first || slice != prev_slice);
-        const unsigned long long smask = __ballot(start), vmask = __ballot(valid);
-        // piece = [leader, next leader); leader lanes = start lanes
-        const unsigned long long above = lane == 63 ? 0ull : (smask >> (lane + 1)) << (lane + 1);
-        const int next = above ? __builtin_ctzll(above) : 64;
-        const int pend = min(next, 64 - __builtin_clzll(vmask));  // piece end (lane index, exclusive)
-        // segmented (suffix within the piece) min / max: after the loop the
-        // leader holds its piece's min tlo / max thi
-        for (int o = 1; o < 64; o <<= 1) {
-            const long long a0 = __shfl_down(tlo, o, 64), a1 = __shfl_down(thi, o, 64);
-            if (lane + o < pend) {
-                tlo = min(tlo, a0);
-                thi = max(thi, a1);
-            }
-        }
-        uint32_t nu = 0, nsp = 0;
-        uint64_t plo = 0, phi = 0, sr = 0, s1 = 0;
-        uint32_t slot = 0;
-        if (start) {
-            const int plen = pend - lane;
-            slot = key >> 1;
-            const uint64_t s0 = a.s_post[slot];
-            s1 = a.s_post[slot + 1];
-            sr = s0 + a.s_nreg[slot];
-            // m in [tlo - dcap, thi]; saturating (tlo > INT64_MIN by contract)
-            const long long mlo = tlo < LLONG_MIN + a.dcap ? LLONG_MIN : tlo - a.dcap;
-            plo = lb_m(a.b_t, s0, sr, mlo);
-            phi = thi < mlo ? plo : ub_m(a.b_t, plo, sr, thi);
-            const uint64_t L = (phi - plo) + (s1 - sr);
-            // a few records over a short posting range: cheaper one per lane
-            if (plen < kSparseMin && L <= (uint64_t)kSparseL) nsp = (uint32_t)plen;
-            else nu = (uint32_t)((L + kChunkMax - 1) / kChunkMax);
-        }
-        // wave prefixes of the unit and sparse counts, one atomic each
-        uint32_t xu = nu, xs = nsp;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t yu = __shfl_up(xu, o, 64), ys = __shfl_up(xs, o, 64);
-            if (lane >= o) {
-                xu += yu;
-                xs += ys;
-            }
-        }
-        const uint32_t tu = __shfl(xu, 63), ts = __shfl(xs, 63);
-        const int reg = (int)(blockIdx.x % kRegions);
-        unsigned long long bu = 0, bs = 0;
-        if (lane == 0 && tu) bu = atomicAdd(ur.counter(reg), (unsigned long long)tu);
-        if (lane == 0 && ts) bs = atomicAdd(sr_.counter(reg), (unsigned long long)ts);
-        bu = __shfl(bu, 0) + (xu - nu);
-        bs = __shfl(bs, 0) + (xs - nsp);
-        if (nsp)
-            for (uint32_t k = 0; k < nsp; k++)
-                if ((int64_t)(bs + k) < sr_.cap) sparse[reg * sr_.cap + (int64_t)(bs + k)] = p + k;
-        const uint64_t nreg = phi - plo, nlong = s1 - sr;
-        for (uint32_t c = 0; c < nu; c++) {
-            const uint64_t v0 = (uint64_t)c * kChunkMax, v1 = min(v0 + kChunkMax, nreg + nlong);
-            Unit d;
-            d.p_lo = plo + min(v0, nreg);
-            d.n_reg = (uint32_t)(min(v1, nreg) - min(v0, nreg));
-            d.l_lo = sr + (v0 > nreg ? v0 - nreg : 0);
-            d.n_long = (uint32_t)((v1 - v0) - d.n_reg);
-            d.r_lo = p;
-            d.nrec = (uint32_t)(pend - lane);
-            d.slot = slot;
-            d.pad[0] = d.pad[1] = d.pad[2] = 0;
-            const unsigned long long w = bu + c;
-            if ((int64_t)w < ur.cap) units[reg * ur.cap + (int64_t)w] = d;
-        }
-    }
-}
-
 // Inclusive prefix sum over the 64 lanes with DPP (no LDS round trips):
 // row_shr 1/2/4/8 scan each 16-lane row, row_bcast 15 / 31 carry the row
 // totals into the rows above (CDNA DPP; rows outside row_mask keep `old`=0).
@@ -849,23 +738,155 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
     return x;
 }
 
+// Quantised start of every sorted record (the query-order key of a narrow
+// record): the join searches a cell's narrow records by it.
+__global__ void k_stq(const uint32_t *sval, const QRec *recs, const int64_t *dnkeys, long long tbase, int qshift,
+                      uint32_t *stq)
+{
+    const int64_t i = tid64();
+    if (i >= *dnkeys) return;
+    stq[i] = order_q(recs[sval[i]].tlo, tbase, qshift);
+}
+
+__device__ __forceinline__ uint32_t lb_u32(const uint32_t *x, uint32_t lo, uint32_t hi, uint32_t v)
+{
+    while (lo < hi) {  // first index in [lo, hi) with x[i] >= v
+        const uint32_t m = (lo + hi) >> 1;
+        if (x[m] < v) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
+
+// Join unit: one tile of <= 64 postings of one cell (a run of its regular
+// postings in start order, or of its long-duration ones) x that cell's
+// query records to test (positions in the sorted keys): narrow ones [n0, n1)
+// -- for a regular tile the sub-range whose quantised start can meet the
+// tile (k_unit_ranges) -- and wide ones [w0, w1); a long tile meets every
+// record of the cell.  32 bytes.
+constexpr uint32_t kUnitLong = 0x80000000u;  // np: long-duration tile
+struct alignas(16) Unit {
+    uint64_t p0;     // first posting
+    uint32_t np;     // postings (1..64) | kUnitLong
+    uint32_t slot;
+    uint32_t n0, n1;  // narrow records
+    uint32_t w0, w1;  // wide records
+};
+static_assert(sizeof(Unit) == 32, "Unit layout");
+
+// Join units, one wave per window of 64 sorted keys (grid-stride over the
+// device key count): every lane that starts a cell (a run of equal slot)
+// finds the cell's record ranges (within the window, or by binary search
+// past it) and emits one unit per 64-posting tile of the cell's regular
+// and long parts; slots come from one atomic per wave (region counters).
+__global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *skey, const int64_t *dnkeys, Regions ur,
+                                                  Unit *units)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t nkeys = (uint32_t)*dnkeys;
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
+    const int64_t nwin = ((int64_t)nkeys + 63) / 64;
+    const int reg = (int)(blockIdx.x % kRegions);
+    for (int64_t win = wave; win < nwin; win += nwaves) {
+        const uint32_t w0 = (uint32_t)(win * 64), wend = min(w0 + 64u, nkeys);
+        const uint32_t p = w0 + (uint32_t)lane;
+        const bool valid = p < nkeys;
+        const uint32_t key = valid ? skey[p] : 0xffffffffu;
+        const uint32_t prev = valid && p > 0 ? skey[p - 1] : 0xffffffffu;
+        const bool cstart = valid && (p == 0 || (prev >> 1) != (key >> 1));
+        const bool wstart = valid && (key & 1u) && (p == 0 || prev != key);
+        const unsigned long long cm = __ballot(cstart), wm = __ballot(wstart);
+        uint32_t nu = 0, rw = 0, re = 0, slot = key >> 1, ntr = 0;
+        uint64_t s0 = 0, sr = 0, s1 = 0;
+        if (cstart) {
+            const unsigned long long above = lane == 63 ? 0ull : (cm >> (lane + 1)) << (lane + 1);
+            const uint32_t nxt = above ? w0 + (uint32_t)__builtin_ctzll(above) : 0xffffffffu;
+            re = nxt != 0xffffffffu ? nxt : lb_u32(skey, wend, nkeys, (slot << 1 | 1u) + 1u);
+            // the first wide record of the cell
+            const unsigned long long wl = (wm >> lane) << lane;  // wide starts at or after this lane
+            const uint32_t wpos = wl ? w0 + (uint32_t)__builtin_ctzll(wl) : 0xffffffffu;
+            if (wpos < re) rw = wpos;
+            else if (re <= wend) rw = re;
+            else rw = lb_u32(skey, wend, re, slot << 1 | 1u);
+            s0 = a.s_post[slot];
+            s1 = a.s_post[slot + 1];
+            sr = s0 + a.s_nreg[slot];
+            ntr = (uint32_t)((sr - s0 + 63) / 64);
+            nu = ntr + (uint32_t)((s1 - sr + 63) / 64);
+        }
+        uint32_t x = wave_incl_scan(nu);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+        unsigned long long bu = 0;
+        if (lane == 0 && tot) bu = atomicAdd(ur.counter(reg), (unsigned long long)tot);
+        bu = __shfl(bu, 0) + (x - nu);
+        for (uint32_t t = 0; t < nu; t++) {
+            Unit d;
+            const bool lng = t >= ntr;
+            const uint64_t b = lng ? sr + 64ull * (t - ntr) : s0 + 64ull * t;
+            const uint64_t e = lng ? s1 : sr;
+            d.p0 = b;
+            d.np = (uint32_t)min((uint64_t)64, e - b) | (lng ? kUnitLong : 0u);
+            d.slot = slot;
+            d.n0 = p;
+            d.n1 = lng ? re : rw;  // a long tile meets every record
+            d.w0 = lng ? re : rw;
+            d.w1 = re;
+            const unsigned long long wpos = bu + t;
+            if ((int64_t)wpos < ur.cap) units[reg * ur.cap + (int64_t)wpos] = d;
+        }
+    }
+}
+
+// Narrow record sub-range of every regular tile: a narrow record (window <=
+// dqmax) meets a posting only if tlo in [m - dqmax, max(t0, t1)], and over a
+// start-sorted tile that is [m_first - dqmax, m_last + dcap]; the records'
+// quantised starts (stq) bracket it by binary search.  One thread per unit.
+__global__ void k_unit_ranges(IndexView a, Regions ur, Unit *units, const uint32_t *stq,
+                              const unsigned long long *dqmax, long long tbase, int qshift)
+{
+    int64_t pre[kRegions + 1];
+    const int64_t n = ur.total(pre);
+    const long long dq = (long long)min(*dqmax, 1ull << 62);
+    for (int64_t u = tid64(); u < n; u += nthreads64()) {
+        Unit &d = units[ur.slot_of(pre, u)];
+        if ((d.np & kUnitLong) || d.n1 <= d.n0) continue;
+        const longlong2 f = a.b_t[d.p0], l = a.b_t[d.p0 + d.np - 1];
+        const long long m0 = tmin2(f.x, f.y), m1 = tmin2(l.x, l.y);
+        const long long lo = m0 < LLONG_MIN + dq ? LLONG_MIN : m0 - dq;
+        const long long hi = m1 > LLONG_MAX - a.dcap ? LLONG_MAX : m1 + a.dcap;
+        const uint32_t n0 = lb_u32(stq, d.n0, d.n1, order_q(lo, tbase, qshift));
+        d.n1 = lb_u32(stq, n0, d.n1, order_q(hi, tbase, qshift) + 1u);
+        d.n0 = n0;
+    }
+}
+
+__device__ __forceinline__ long long readlane64(long long v, int lane)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((unsigned long long)v >> 32), lane);
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
 // Set bits of m below this lane.
 __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m)
 {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Output: pairs go straight to HBM in per-wave chunks of kOutChunk slots
-// reserved with one atomic each (a single same-address counter saturates at
-// ~88 atomics/us, MI355X_MICROARCH.md "dequeue"); each retired chunk records
-// its fill, and k_fix_* close the holes the partly filled chunks leave.
+// Output: pairs go straight to HBM in per-wave chunks of kOutChunk slots,
+// each reserved with one atomic on the wave's region counter (kRegions
+// regions of rcap slots: a single same-address counter saturates at ~88
+// atomics/us, MI355X_MICROARCH.md "dequeue"); each retired chunk records its
+// fill, and k_fix_* close the holes that partly filled or unreserved chunks
+// leave below the total.
 constexpr int kOutChunk = 2048;
 struct OutArgs {
     uint32_t *q, *e;
-    int64_t cap;                   // output slots
-    uint32_t *fills;               // per chunk: pairs written
-    int64_t max_chunks;            // fills[] capacity
-    unsigned long long *counter;   // [0] pairs [1] tagged [2] lane tests [3] broadcasts [7] slots reserved
+    int64_t rcap;                  // slots per region (a multiple of kOutChunk)
+    uint32_t *fills;               // per chunk of all regions: pairs written (0 = unreserved)
+    unsigned long long *octr;      // kRegions reservation counters, kRegStride words apart
+    unsigned long long *counter;   // [0] pairs [1] tagged [2] lane tests [3] broadcasts
 };
 
 struct WaveOut {
@@ -873,37 +894,35 @@ struct WaveOut {
     int fill = kOutChunk;  // no chunk yet
     bool have = false;
     unsigned long long pairs = 0, tagged = 0;
-    // wave-uniform call: every lane with `keep` writes its pair
-    __device__ __forceinline__ void emit(const OutArgs &o, bool keep, bool tag, uint32_t q, uint32_t e)
+    // wave-uniform call: every lane of `keep` writes (q, its e)
+    __device__ __forceinline__ void emit(const OutArgs &o, unsigned long long keep, unsigned long long tag, uint32_t q,
+                                         uint32_t e)
     {
-        const unsigned long long m = __ballot(keep);
-        if (!m) return;
-        const int c = __popcll(m);
+        if (!keep) return;
+        const int c = __popcll(keep);
         if (fill + c > kOutChunk) {
             retire(o);
+            const int reg = (int)(blockIdx.x % kRegions);
             unsigned long long b = 0;
-            if ((threadIdx.x & 63) == 0) b = atomicAdd(&o.counter[7], (unsigned long long)kOutChunk);
-            base = __shfl(b, 0);
+            if ((threadIdx.x & 63) == 0) b = atomicAdd(&o.octr[reg * kRegStride], (unsigned long long)kOutChunk);
+            b = __shfl(b, 0);
+            have = (int64_t)b + kOutChunk <= o.rcap;  // else the region is full: counted, not written (rerun)
+            base = have ? (unsigned long long)reg * (unsigned long long)o.rcap + b : 0ull;
             fill = 0;
-            have = true;
         }
-        if (keep) {
-            const unsigned long long pos = base + (unsigned long long)fill + mbcnt64(m);
-            if ((int64_t)pos < o.cap) {
-                o.q[pos] = q | (tag ? kTag : 0u);
-                o.e[pos] = e;
-            }
+        const int lane = threadIdx.x & 63;
+        if (have && ((keep >> lane) & 1ull)) {
+            const unsigned long long pos = base + (unsigned long long)fill + mbcnt64(keep);
+            o.q[pos] = q | (((tag >> lane) & 1ull) ? kTag : 0u);
+            o.e[pos] = e;
         }
         fill += c;
         pairs += (unsigned long long)c;
-        tagged += (unsigned long long)__popcll(__ballot(keep && tag));
+        tagged += (unsigned long long)__popcll(tag);
     }
     __device__ __forceinline__ void retire(const OutArgs &o)
     {
-        if (have && (threadIdx.x & 63) == 0) {
-            const unsigned long long ch = base / kOutChunk;
-            if ((int64_t)ch < o.max_chunks) o.fills[ch] = (uint32_t)fill;
-        }
+        if (have && (threadIdx.x & 63) == 0) o.fills[base / kOutChunk] = (uint32_t)fill;
         have = false;
     }
     __device__ __forceinline__ void finish(const OutArgs &o)
@@ -916,192 +935,188 @@ struct WaveOut {
     }
 };
 
-// The smallest-shared-cell rule (SQL DISTINCT, Q13) for one candidate
-// (record x posting that passed the predicate), given both near-prefix
-// signatures: keep it iff no smaller shared cell exists; long query x long
-// entity occurrences are all kept, tagged (the smallest shared cell always
-// survives; the tagged set is deduplicated after the join).
-template <bool LONG>
-__device__ __forceinline__ bool keep_candidate(const IndexView &ix, const QueryView &qv, uint32_t rqv, uint32_t em_e,
-                                               uint32_t em_meta, ulonglong2 rs01, ulonglong2 rs23, ulonglong2 ps01,
-                                               ulonglong2 ps23, uint32_t slot, bool &tag)
-{
-    const bool first = (em_e & kFirstBit) != 0;
-    const bool sure = (rqv & kRank0) || first;  // no smaller cell on one side
-    const bool ov = !sure && ((ps01.x & rs01.x) | (ps01.y & rs01.y) | (ps23.x & rs23.x) | (ps23.y & rs23.y)) != 0ull;
-    const bool ll = LONG && (rqv & kLongQ) && (em_meta & kMetaLongFp);
-    bool surv = !ov && (sure || (rqv & kCompactQ) || (em_meta & kMetaCompact) || ll);
-    if (!ov && !surv) {  // neither prefix compact, not both long: exact merge (rare)
-        const uint32_t q = rqv & ~kQFlags;
-        surv = no_smaller_shared<2>(ix, em_e & ~kFirstBit, cell_of_slot(ix, slot), qv.cells + qv.offs[q],
-                                    qv.offs[q + 1] - qv.offs[q]);
-    }
-    tag = surv && ll;
-    return surv;
-}
-
 struct JoinArgs {
     IndexView ix;
     QueryView qv;
-    Regions ur;  // units (k_units)
-    Regions sr;  // sparse records (k_units)
+    Regions ur;                        // units (k_units)
     OutArgs out;
+    const uint32_t *stq;               // quantised start of every sorted record
+    const unsigned long long *dqmax;   // device: widest narrow query window (us)
+    long long tbase;                   // query-order quantisation
+    int qshift;
 };
 
-// Dense cells: one wavefront per unit, lane = record; postings staged in LDS
-// 64 at a time and broadcast.  Per 32-posting half: the fused predicate ORs
-// one bit per posting into the lane's mask, the set bits are compacted into
-// an LDS candidate list (lane-major), and full waves then apply the
-// smallest-shared-cell rule to 64 candidates at a time.
+// One wavefront per unit, lane = posting (the tile stays in registers); the
+// cell's relevant query records are staged in LDS 64 at a time and
+// broadcast.  Narrow records: only those whose quantised start lies in
+// [q(min m - widest window), q(max t1)] (64-ary cooperative search over the
+// cell's start-sorted records); wide ones and long tiles: all.  Per record:
+// the fused altitude/time/owner predicate is one wave mask; the
+// smallest-shared-cell rule (SQL DISTINCT, Q13) compares the record's
+// near-prefix signature (broadcast) with each lane's posting signature.
 template <bool OWNER, bool LONG>
 __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__restrict__ recs,
                                                       const uint32_t *__restrict__ sval,
-                                                      const Unit *__restrict__ units, uint32_t *__restrict__ work)
+                                                      const Unit *__restrict__ units,
+                                                      unsigned long long *__restrict__ work)
 {
-    __shared__ longlong2 s_t[kWaves][64];     // posting (t0, t1); (MAX, MIN) = matches nothing
-    __shared__ float2 s_alt[kWaves][64];      // posting (alt_lo, alt_hi)
-    __shared__ uint2 s_em[kWaves][64];        // (entity | first, meta)
-    __shared__ ulonglong2 s_sig[kWaves][2][64];
-    __shared__ int32_t s_own[kWaves][OWNER ? 64 : 1];
-    __shared__ ulonglong2 s_rsig[kWaves][2][64];  // the unit's record signatures
-    __shared__ uint32_t s_rqv[kWaves][64];
-    __shared__ uint16_t s_cand[kWaves][64 * 32];  // candidates of one half: record << 6 | posting
+    __shared__ longlong2 s_rt[kWaves][64];      // record (tlo, thi)
+    __shared__ float4 s_ra[kWaves][64];         // record (alo, ahi, qv, own)
+    __shared__ ulonglong2 s_rs[kWaves][2][64];  // record near-prefix signature
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const IndexView &ix = a.ix;
     WaveOut out;
     unsigned long long n_tests = 0, n_bcast = 0;
-    int64_t upre[kRegions + 1];
-    const int64_t nunits = a.ur.total(upre);
-    uint32_t ucur = 0, uend = 0;
-    for (;;) {
-        if (ucur >= uend) {
-            uint32_t ub = 0;
-            if (lane == 0) ub = atomicAdd(&work[0], (uint32_t)kGrab);
-            ub = __builtin_amdgcn_readfirstlane(__shfl(ub, 0));
-            if ((int64_t)ub >= nunits) break;
-            ucur = ub;
-            uend = (uint32_t)min((int64_t)ub + kGrab, nunits);
-        }
-        const Unit d = units[a.ur.slot_of(upre, ucur++)];
-        // ---- this lane's record
-        const bool rvalid = (uint32_t)lane < d.nrec;
-        long long rtlo = LLONG_MAX, rthi = LLONG_MIN;
-        float ralo = INFINITY, rahi = -INFINITY;
-        uint32_t rqv = 0;
-        int32_t rown = -1;
-        ulonglong2 rs01 = make_ulonglong2(0, 0), rs23 = make_ulonglong2(0, 0);
-        if (rvalid) {
-            const int4 *r4 = reinterpret_cast<const int4 *>(recs + sval[d.r_lo + lane]);
-            const int4 h0 = r4[0], h1 = r4[1];
-            const int4 g0 = r4[2], g1 = r4[3];
-            rtlo = ((long long)h0.y << 32) | (uint32_t)h0.x;
-            rthi = ((long long)h0.w << 32) | (uint32_t)h0.z;
-            ralo = __int_as_float(h1.x);
-            rahi = __int_as_float(h1.y);
-            rqv = (uint32_t)h1.z;
-            rown = h1.w;
-            rs01 = make_ulonglong2(((unsigned long long)(uint32_t)g0.y << 32) | (uint32_t)g0.x,
-                                   ((unsigned long long)(uint32_t)g0.w << 32) | (uint32_t)g0.z);
-            rs23 = make_ulonglong2(((unsigned long long)(uint32_t)g1.y << 32) | (uint32_t)g1.x,
-                                   ((unsigned long long)(uint32_t)g1.w << 32) | (uint32_t)g1.z);
-        }
-        __builtin_amdgcn_wave_barrier();
-        s_rqv[w][lane] = rqv;
-        s_rsig[w][0][lane] = rs01;
-        s_rsig[w][1][lane] = rs23;
-        const int64_t total = (int64_t)d.n_reg + d.n_long;
-        // ---- posting chunks: this lane loads posting v0 + lane
-        auto post_of = [&](int64_t v) -> uint64_t { return v < (int64_t)d.n_reg ? d.p_lo + v : d.l_lo + (v - d.n_reg); };
-        longlong2 pt;
-        float2 pa;
-        uint32_t pe = 0, pmeta = 0;
-        int32_t pown = 0;
-        ulonglong2 ps0, ps1;
-        auto load_chunk = [&](int64_t v0) {
-            const int64_t v = v0 + lane;
-            pt = make_longlong2(LLONG_MAX, LLONG_MIN);
-            pa = make_float2(INFINITY, -INFINITY);
-            pe = 0;
-            pmeta = 0;
-            pown = 0;
-            ps0 = ps1 = make_ulonglong2(0, 0);
-            if (v < total) {
-                const uint64_t p = post_of(v);
-                pe = ix.b_e[p];
-                pmeta = ix.b_meta[p];
-                pt = ix.b_t[p];
-                pa = ix.b_alt[p];
-                ps0 = ix.b_sig[2 * p];
-                ps1 = ix.b_sig[2 * p + 1];
-                if (OWNER) pown = ix.b_owner[p];
+    // units: kRegions queues (the unit regions), a wave starts on its own
+    // region's and moves on when it is drained; grabs of g units per atomic
+    int qreg = (int)(blockIdx.x % kRegions), visited = 0;
+    int64_t qn = min((int64_t)a.ur.cnt[qreg * kRegStride], a.ur.cap);
+    const int64_t wpr = max((int64_t)1, (int64_t)gridDim.x * kWaves / kRegions);  // waves per region
+    int64_t ucur = 0, uend = 0;
+    auto next_unit = [&]() -> int64_t {
+        while (ucur >= uend) {
+            const int64_t g = min((int64_t)32, max((int64_t)1, qn / (wpr * 8)));
+            unsigned long long ub = 0;
+            if (lane == 0) ub = atomicAdd(&work[qreg * kRegStride], (unsigned long long)g);
+            ub = __shfl(ub, 0);
+            if ((int64_t)ub < qn) {
+                ucur = (int64_t)ub;
+                uend = min((int64_t)ub + g, qn);
+                break;
             }
-        };
-        load_chunk(0);
-        for (int64_t v0 = 0; v0 < total; v0 += 64) {
-            // tombstoned (write path) or padding: matches nothing
-            const bool dead = v0 + lane >= total || is_dead(ix, pe & ~kFirstBit);
-            __builtin_amdgcn_wave_barrier();
-            s_t[w][lane] = dead ? make_longlong2(LLONG_MAX, LLONG_MIN) : pt;
-            s_alt[w][lane] = pa;
-            s_em[w][lane] = make_uint2(pe, pmeta);
-            s_sig[w][0][lane] = ps0;
-            s_sig[w][1][lane] = ps1;
-            if (OWNER) s_own[w][lane] = pown;
-            __builtin_amdgcn_wave_barrier();
-            const int nv = (int)min((int64_t)64, total - v0);
-            if (v0 + 64 < total) load_chunk(v0 + 64);  // next chunk in flight during this one
-            n_bcast += (unsigned long long)nv;
-            n_tests += (unsigned long long)nv * d.nrec;
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                if (h * 32 >= nv) break;
-                const int jn = min(32, nv - h * 32);
-                // ---- predicate, shifted in: after the loop bit (jn - 1 - jj) of
-                // m is posting h * 32 + jj (m + m + p: one v_addc with the
-                // compare mask as carry-in)
-                uint32_t m = 0;
-#pragma unroll 4
-                for (int jj = 0; jj < jn; jj++) {
-                    const int j = h * 32 + jj;
-                    const longlong2 t = s_t[w][j];
-                    const float2 al = s_alt[w][j];
+            if (++visited >= kRegions) return -1;
+            qreg = (qreg + 1) % kRegions;
+            qn = min((int64_t)a.ur.cnt[qreg * kRegStride], a.ur.cap);
+        }
+        return (int64_t)qreg * a.ur.cap + ucur++;
+    };
+    // software pipeline: the next unit's descriptor and postings are loaded
+    // while this one's records are joined
+    Unit dn{};
+    longlong2 nt = make_longlong2(LLONG_MAX, LLONG_MIN);
+    float2 na = make_float2(INFINITY, -INFINITY);
+    uint32_t ne = 0, nmeta = 0;
+    int32_t nown = 0;
+    ulonglong2 ns01 = make_ulonglong2(0, 0), ns23 = make_ulonglong2(0, 0);
+    auto prefetch = [&](int64_t u) {
+        dn = units[u];
+        nt = make_longlong2(LLONG_MAX, LLONG_MIN);
+        na = make_float2(INFINITY, -INFINITY);
+        ne = nmeta = 0;
+        nown = 0;
+        ns01 = ns23 = make_ulonglong2(0, 0);
+        const bool any = dn.n1 > dn.n0 || dn.w1 > dn.w0;  // a tile no record can meet is skipped unloaded
+        if (any && (uint32_t)lane < (dn.np & ~kUnitLong)) {
+            const uint64_t p = dn.p0 + lane;
+            ne = ix.b_e[p];
+            nmeta = ix.b_meta[p];
+            nt = ix.b_t[p];
+            na = ix.b_alt[p];
+            ns01 = ix.b_sig[2 * p];
+            ns23 = ix.b_sig[2 * p + 1];
+            if (OWNER) nown = ix.b_owner[p];
+        }
+    };
+    int64_t un = next_unit();
+    if (un >= 0) prefetch(un);
+    while (un >= 0) {
+        const Unit d = dn;
+        const uint32_t np = d.np & ~kUnitLong;
+        // ---- this lane's posting
+        const longlong2 pt = nt;
+        const float2 pa = na;
+        const uint32_t pe = ne, pmeta = nmeta;
+        const int32_t pown = nown;
+        const ulonglong2 ps01 = ns01, ps23 = ns23;
+        const bool pv = (uint32_t)lane < np && !is_dead(ix, pe & ~kFirstBit);  // tombstones match nothing
+        un = next_unit();
+        if (un >= 0) prefetch(un);
+        if (d.n1 <= d.n0 && d.w1 <= d.w0) continue;
+        const uint32_t pent = pe & ~kFirstBit;
+        const unsigned long long vmask = __ballot(pv);
+        if (!vmask) continue;  // (un, the next unit, is already in flight)
+        const unsigned long long fmask = __ballot(pv && (pe & kFirstBit));        // entity's smallest cell
+        const unsigned long long cmask = __ballot(pv && (pmeta & kMetaCompact));  // compact prefix
+        const unsigned long long lmask = LONG ? __ballot(pv && (pmeta & kMetaLongFp)) : 0ull;
+        // tile time bounds (a regular tile is sorted by m = min(t0, t1)):
+        // records whose window misses every posting are skipped (a long
+        // tile: no bound)
+        long long t0min = LLONG_MIN, t1max = LLONG_MAX;
+        if (!(d.np & kUnitLong)) {
+            const long long m = tmin2(pt.x, pt.y);
+            t0min = readlane64(m, 0);  // <= every t0 of the tile
+            long long t1 = (uint32_t)lane < np ? (pt.x > pt.y ? pt.x : pt.y) : LLONG_MIN;
+            for (int o = 32; o > 0; o >>= 1) t1 = max(t1, __shfl_xor(t1, o));
+            t1max = t1;
+        }
+        const uint32_t ra0 = d.n0, ra1 = d.n1, rb0 = d.w0, rb1 = d.w1;
+        for (int part = 0; part < 2; part++) {
+            const uint32_t x0 = part ? rb0 : ra0, x1 = part ? rb1 : ra1;
+            for (uint32_t base = x0; base < x1; base += 64) {
+                const uint32_t r = base + (uint32_t)lane;
+                bool rel = false;
+                __builtin_amdgcn_wave_barrier();
+                if (r < x1) {
+                    const int4 *r4 = reinterpret_cast<const int4 *>(recs + sval[r]);
+                    const int4 h0 = r4[0], h1 = r4[1];
+                    const long long tlo = ((long long)h0.y << 32) | (uint32_t)h0.x;
+                    const long long thi = ((long long)h0.w << 32) | (uint32_t)h0.z;
+                    const float alo = __int_as_float(h1.x), ahi = __int_as_float(h1.y);
+                    s_rt[w][lane] = make_longlong2(tlo, thi);
+                    s_ra[w][lane] = make_float4(alo, ahi, __int_as_float(h1.z), __int_as_float(h1.w));
+                    s_rs[w][0][lane] = reinterpret_cast<const ulonglong2 *>(r4)[2];
+                    s_rs[w][1][lane] = reinterpret_cast<const ulonglong2 *>(r4)[3];
+                    rel = t1max >= tlo && t0min <= thi;
+                }
+                __builtin_amdgcn_wave_barrier();
+                unsigned long long todo = __ballot(rel);
+                n_bcast += (unsigned long long)__popcll(todo);
+                n_tests += (unsigned long long)__popcll(todo) * (unsigned long long)__popcll(vmask);
+                while (todo) {
+                    const int j = __builtin_ctzll(todo);
+                    todo &= todo - 1;
+                    const longlong2 rt = s_rt[w][j];
+                    const float4 ra = s_ra[w][j];
+                    const uint32_t qv = __builtin_amdgcn_readfirstlane(__float_as_int(ra.z));
                     // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels)
-                    bool p = (t.y >= rtlo) & (t.x <= rthi) & (al.y >= ralo) & (al.x <= rahi);
-                    if (OWNER) p &= (rown < 0) | (s_own[w][j] == rown);
-                    m = m + m + (p ? 1u : 0u);
-                }
-                if (!rvalid) m = 0;
-                // ---- candidates -> LDS list (lane-major), then 64 at a time
-                const uint32_t c = (uint32_t)__popc(m);
-                const uint32_t x = wave_incl_scan(c);
-                const int T = __builtin_amdgcn_readlane((int)x, 63);
-                if (T == 0) continue;
-                uint32_t off = x - c;
-                const uint32_t hi = (uint32_t)(h * 32 + jn - 1);  // posting of bit 0
-                while (m) {
-                    const uint32_t b = (uint32_t)__builtin_ctz(m);
-                    m &= m - 1u;
-                    s_cand[w][off++] = (uint16_t)((uint32_t)lane << 6 | (hi - b));
-                }
-                __builtin_amdgcn_wave_barrier();
-                for (int b0 = 0; b0 < T; b0 += 64) {
-                    const bool on = b0 + lane < T;
-                    const uint32_t cd = on ? s_cand[w][b0 + lane] : 0u;
-                    const uint32_t r = cd >> 6, j = cd & 63u;
-                    bool keep = false, tag = false;
-                    uint32_t cq = 0, ce = 0;
-                    if (on) {
-                        const uint32_t qv = s_rqv[w][r];
-                        const uint2 em = s_em[w][j];
-                        keep = keep_candidate<LONG>(ix, a.qv, qv, em.x, em.y, s_rsig[w][0][r], s_rsig[w][1][r],
-                                                    s_sig[w][0][j], s_sig[w][1][j], d.slot, tag);
-                        cq = qv & ~kQFlags;
-                        ce = em.x & ~kFirstBit;
+                    bool pass = pv && (pt.y >= rt.x) & (pt.x <= rt.y) & (pa.y >= ra.x) & (pa.x <= ra.y);
+                    if (OWNER) {
+                        const int32_t own = __builtin_amdgcn_readfirstlane(__float_as_int(ra.w));
+                        if (own >= 0) pass &= pown == own;
                     }
-                    out.emit(a.out, keep, tag, cq, ce);
+                    const unsigned long long pm = __ballot(pass);
+                    if (!pm) continue;
+                    // smallest shared cell only: a rank-0 record (query's first cell) or a
+                    // posting at its entity's first cell has no smaller cell on one side
+                    unsigned long long keep = pm;
+                    unsigned long long need = (qv & kRank0) ? 0ull : (pm & ~fmask);
+                    const bool ll_r = LONG && (qv & kLongQ);
+                    if (need) {
+                        const ulonglong2 c0 = s_rs[w][0][j], c1 = s_rs[w][1][j];
+                        const bool ov =
+                            ((c0.x & ps01.x) | (c0.y & ps01.y) | (c1.x & ps23.x) | (c1.y & ps23.y)) != 0ull;
+                        const unsigned long long ovm = __ballot(ov) & need;
+                        keep &= ~ovm;
+                        need &= ~ovm;
+                        // no overlap: exact when either prefix is compact; both long: tagged
+                        unsigned long long ex = (qv & kCompactQ) ? 0ull : (need & ~cmask & ~(ll_r ? lmask : 0ull));
+                        if (ex) {  // neither prefix compact, not both long: exact merge (rare)
+                            bool drop = false;
+                            if ((ex >> lane) & 1ull) {
+                                const uint32_t q = qv & ~kQFlags;
+                                drop = !no_smaller_shared<2>(ix, pent, cell_of_slot(ix, d.slot), a.qv.cells + a.qv.offs[q],
+                                                             a.qv.offs[q + 1] - a.qv.offs[q]);
+                            }
+                            keep &= ~__ballot(drop);
+                        }
+                    }
+                    // long query x long entity: every surviving occurrence is emitted
+                    // tagged (the smallest shared cell always survives) and the tagged
+                    // set is deduplicated after the join
+                    const unsigned long long tag = ll_r ? (keep & lmask) : 0ull;
+                    out.emit(a.out, keep, tag, qv & ~kQFlags, pent);
                 }
-                __builtin_amdgcn_wave_barrier();
             }
         }
     }
@@ -1110,99 +1125,6 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
         atomicAdd(&a.out.counter[2], n_tests);
         atomicAdd(&a.out.counter[3], n_bcast);
     }
-}
-
-// Sparse cells (runs of < kSparseRun records): one lane per record, each
-// scanning its own posting range [tlo - dcap, thi] of its cell (binary
-// search) plus the cell's long part, the next posting's loads in flight
-// while the current one is tested.
-template <bool OWNER, bool LONG>
-__global__ __launch_bounds__(kBlock) void k_join_sparse(JoinArgs a, const QRec *__restrict__ recs,
-                                                        const uint32_t *__restrict__ skey,
-                                                        const uint32_t *__restrict__ sval,
-                                                        const uint32_t *__restrict__ list)
-{
-    const IndexView &ix = a.ix;
-    int64_t spre[kRegions + 1];
-    const int64_t n = a.sr.total(spre);
-    WaveOut out;
-    unsigned long long n_tests = 0;
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
-    for (int64_t base = wave * 64; base < n; base += nwaves * 64) {
-        const int64_t i = base + lane;
-        const bool valid = i < n;
-        long long rtlo = LLONG_MAX, rthi = LLONG_MIN;
-        float ralo = INFINITY, rahi = -INFINITY;
-        uint32_t rqv = 0, slot = 0;
-        int32_t rown = -1;
-        ulonglong2 rs01 = make_ulonglong2(0, 0), rs23 = make_ulonglong2(0, 0);
-        uint64_t plo = 0, nreg = 0, llo = 0, L = 0;
-        if (valid) {
-            const uint32_t p = list[a.sr.slot_of(spre, i)];
-            slot = skey[p] >> 1;
-            const QRec *r = recs + sval[p];
-            rtlo = r->tlo;
-            rthi = r->thi;
-            ralo = r->alo;
-            rahi = r->ahi;
-            rqv = r->qv;
-            rown = r->own;
-            rs01 = make_ulonglong2(r->sig[0], r->sig[1]);
-            rs23 = make_ulonglong2(r->sig[2], r->sig[3]);
-            const uint64_t s0 = ix.s_post[slot], s1 = ix.s_post[slot + 1], sr = s0 + ix.s_nreg[slot];
-            const long long mlo = rtlo < LLONG_MIN + ix.dcap ? LLONG_MIN : rtlo - ix.dcap;
-            plo = lb_m(ix.b_t, s0, sr, mlo);
-            const uint64_t phi = rthi < mlo ? plo : ub_m(ix.b_t, plo, sr, rthi);
-            nreg = phi - plo;
-            llo = sr;
-            L = nreg + (s1 - sr);
-        }
-        const uint32_t rq = rqv & ~kQFlags;
-        n_tests += L;
-        auto post_of = [&](uint64_t v) -> uint64_t { return v < nreg ? plo + v : llo + (v - nreg); };
-        longlong2 nt = make_longlong2(LLONG_MAX, LLONG_MIN);
-        float2 na = make_float2(INFINITY, -INFINITY);
-        if (L > 0) {
-            nt = ix.b_t[post_of(0)];
-            na = ix.b_alt[post_of(0)];
-        }
-        for (uint64_t v = 0;; v++) {
-            const bool act = v < L;
-            if (!__ballot(act)) break;
-            const longlong2 t = nt;
-            const float2 al = na;
-            const uint64_t p = act ? post_of(v) : 0;
-            if (v + 1 < L) {
-                const uint64_t pn = post_of(v + 1);
-                nt = ix.b_t[pn];
-                na = ix.b_alt[pn];
-            }
-            bool pass = act && (t.y >= rtlo) & (t.x <= rthi) & (al.y >= ralo) & (al.x <= rahi);
-            uint32_t ee = 0;
-            bool keep = false, tag = false;
-            if (pass) {
-                const uint32_t em = ix.b_e[p];
-                if (is_dead(ix, em & ~kFirstBit)) pass = false;
-                if (OWNER && pass && rown >= 0 && ix.b_owner[p] != rown) pass = false;
-                if (pass) {
-                    const uint32_t meta = ix.b_meta[p];
-                    ulonglong2 ps01 = make_ulonglong2(0, 0), ps23 = make_ulonglong2(0, 0);
-                    if (!(em & kFirstBit) && !(rqv & kRank0)) {
-                        ps01 = ix.b_sig[2 * p];
-                        ps23 = ix.b_sig[2 * p + 1];
-                    }
-                    keep = keep_candidate<LONG>(ix, a.qv, rqv, em, meta, rs01, rs23, ps01, ps23, slot, tag);
-                    ee = em & ~kFirstBit;
-                }
-            }
-            out.emit(a.out, keep, tag, rq, ee);
-        }
-    }
-    out.finish(a.out);
-    for (int o = 32; o > 0; o >>= 1) n_tests += __shfl_xor(n_tests, o);
-    if (lane == 0 && n_tests) atomicAdd(&a.out.counter[2], n_tests);
 }
 
 // Closing the output holes: chunk c holds fills[c] pairs at c * kOutChunk;
@@ -1613,7 +1535,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     uint32_t *ok0 = okey_.ensure(nq + 1), *ok1 = okey2_.ensure(nq + 1), *ov0 = oval_.ensure(nq + 1),
              *perm = perm_.ensure(nq + 1);
     hipLaunchKernelGGL(k_qorder, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_tlo, q_thi, (long long)idx->tbase,
-                       idx->qshift, ok0, ov0);
+                       idx->qshift, ok0, ov0, cnt + 10);
     radix_sort_pairs(ok0, ok1, ov0, perm, nq, kOrderBits, tmp_, s);
     // (3) keys (slot << 1 | wide, query cell) in that order; records per cell
     int64_t *qc = qcnt_.ensure(nq + 1), *qo = qoff_.ensure(nq + 2);
@@ -1629,84 +1551,81 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     // order), over the device key count qo[nq] (<= nqc)
     const int64_t *dnkeys = qo + nq;
     radix_sort_pairs_dn(key, skey, val, sval, nqc, dnkeys, bits_for(idx->n_slots()) + 1, tmp_, s);
-    // (5) join units (dense runs) and the sparse-record list, per window of
-    // 64 sorted keys
+    // (5) the sorted records' quantised starts; join units = 64-posting
+    // tiles of every cell the batch meets
     if (n_cu_ == 0) {
         int dev = 0, ncu = 0;
         DSS_HIP(hipGetDevice(&dev));
         DSS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
         n_cu_ = ncu > 0 ? ncu : 256;
     }
-    // per-region capacities (kRegions regions each): units, sparse records
-    int64_t ucap = std::max<int64_t>(units_cap_hint_, nqc / kBatch / kRegions + 1024);
-    int64_t scap = std::max<int64_t>(sparse_cap_hint_, nqc / 4 + 1024);
-    unsigned long long *rc = regcnt_.ensure(2 * kRegions * kRegStride);
+    uint32_t *stq = rbeg_.ensure(nqc + 1);
+    hipLaunchKernelGGL(k_stq, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, sval, recs, dnkeys, (long long)idx->tbase,
+                       idx->qshift, stq);
+    // per-region unit capacity: the tiles of every cell is an upper bound
+    int64_t ucap = std::max<int64_t>(units_cap_hint_, 1024);
+    unsigned long long *rc = regcnt_.ensure(kRegions * kRegStride);
     Unit *units = nullptr;
-    uint32_t *sparse = nullptr;
     const unsigned ugrid = (unsigned)std::min<int64_t>((nqc + 63) / 64 / (kBlock / 64) + 1, (int64_t)n_cu_ * 16);
-    int wshift = 0;  // time slices of 2^wshift >= dcap us
-    while (wshift < 62 && (1ll << wshift) < idx->dcap) wshift++;
     auto build_units = [&]() {
         units = (Unit *)units_buf_.ensure(sizeof(Unit) * (kRegions * ucap + 1));
-        sparse = rbeg_.ensure(kRegions * scap + 1);
-        DSS_HIP(hipMemsetAsync(rc, 0, sizeof(unsigned long long) * 2 * kRegions * kRegStride, s));
-        hipLaunchKernelGGL(k_units, dim3(ugrid), dim3(kBlock), 0, s, ix, skey, sval, recs, dnkeys, wshift,
-                           Regions{rc, ucap}, units, Regions{rc + kRegions * kRegStride, scap}, sparse);
+        DSS_HIP(hipMemsetAsync(rc, 0, sizeof(unsigned long long) * kRegions * kRegStride, s));
+        hipLaunchKernelGGL(k_units, dim3(ugrid), dim3(kBlock), 0, s, ix, skey, dnkeys, Regions{rc, ucap}, units);
+        hipLaunchKernelGGL(k_unit_ranges, dim3((unsigned)n_cu_ * 8), dim3(kBlock), 0, s, ix, Regions{rc, ucap}, units,
+                           (const uint32_t *)stq, (const unsigned long long *)(cnt + 10), (long long)idx->tbase,
+                           idx->qshift);
     };
     build_units();
-    // (6) join (dense units, then the sparse records); grow the output (and
-    // the work lists) and rerun if too small
+    // (6) join; grow the output (and the units) and rerun if too small
     JoinArgs ja{};
     ja.ix = ix;
     ja.qv = qv;
+    ja.stq = stq;
+    ja.dqmax = cnt + 10;
+    ja.tbase = idx->tbase;
+    ja.qshift = idx->qshift;
     const unsigned nblocks = (unsigned)n_cu_ * kJoinBlocksPerCU;
-    const unsigned sgrid = (unsigned)std::min<int64_t>((nqc + kBlock - 1) / kBlock, (int64_t)n_cu_ * 16);
-    uint32_t *work = work_.ensure(4);
-    if (out_cap_ == 0) out_cap_ = (size_t)nq * 16 + 1024 + kOutChunk;
+    // [0, kRegions) unit queue heads, [kRegions, 2 kRegions) output region counters (kRegStride apart)
+    unsigned long long *work = (unsigned long long *)work_.ensure(2 * kRegions * kRegStride * 2);
+    unsigned long long *octr = work + kRegions * kRegStride;
+    if (out_rcap_ == 0) out_rcap_ = ((int64_t)nq * 16 / kRegions / kOutChunk + 2) * kOutChunk;
     const bool any_long = idx->n_long_fp > 0;  // the batch's long flag is only known on the device
     for (int attempt = 0; attempt < 5; attempt++) {
-        uint32_t *oq = oq_.ensure(out_cap_), *oe = oe_.ensure(out_cap_);
-        const int64_t max_chunks = (int64_t)(out_cap_ / kOutChunk) + 2;
-        uint32_t *fills = fills_.ensure(max_chunks + 1);
+        const int64_t cap = kRegions * out_rcap_, nch = cap / kOutChunk;
+        uint32_t *oq = oq_.ensure(cap + 1), *oe = oe_.ensure(cap + 1);
+        uint32_t *fills = fills_.ensure(nch + 1);
+        DSS_HIP(hipMemsetAsync(fills, 0, sizeof(uint32_t) * nch, s));
         DSS_HIP(hipMemsetAsync(cnt, 0, 4 * sizeof(unsigned long long), s));
-        DSS_HIP(hipMemsetAsync(cnt + 7, 0, sizeof(unsigned long long), s));
-        DSS_HIP(hipMemsetAsync(work, 0, 4 * sizeof(uint32_t), s));
+        DSS_HIP(hipMemsetAsync(work, 0, sizeof(unsigned long long) * 2 * kRegions * kRegStride, s));
         ja.ur = Regions{rc, ucap};
-        ja.sr = Regions{rc + kRegions * kRegStride, scap};
-        ja.out = OutArgs{oq, oe, (int64_t)out_cap_, fills, max_chunks, cnt};
+        ja.out = OutArgs{oq, oe, out_rcap_, fills, octr, cnt};
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
         auto kern = q_owner ? (any_long ? k_join<true, true> : k_join<true, false>)
                             : (any_long ? k_join<false, true> : k_join<false, false>);
         hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs, (const uint32_t *)sval,
                            (const Unit *)units, work);
-        auto skern = q_owner ? (any_long ? k_join_sparse<true, true> : k_join_sparse<true, false>)
-                             : (any_long ? k_join_sparse<false, true> : k_join_sparse<false, false>);
-        hipLaunchKernelGGL(skern, dim3(sgrid), dim3(kBlock), 0, s, ja, (const QRec *)recs, (const uint32_t *)skey,
-                           (const uint32_t *)sval, (const uint32_t *)sparse);
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
-        unsigned long long h[12], hr[2 * kRegions * kRegStride];
+        unsigned long long h[12], hr[kRegions * kRegStride], ho[kRegions * kRegStride];
         DSS_HIP(hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipMemcpyAsync(hr, rc, sizeof(hr), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipMemcpyAsync(ho, octr, sizeof(ho), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipStreamSynchronize(s));
-        int64_t nu = 0, ns = 0, umax = 0, smax = 0;
+        int64_t nu = 0, umax = 0, omax = 0;
         for (int r = 0; r < kRegions; r++) {
-            const int64_t u = (int64_t)hr[r * kRegStride], v = (int64_t)hr[(kRegions + r) * kRegStride];
+            const int64_t u = (int64_t)hr[r * kRegStride];
             nu += u;
-            ns += v;
             umax = std::max(umax, u);
-            smax = std::max(smax, v);
+            omax = std::max(omax, (int64_t)ho[r * kRegStride]);
         }
-        if (umax > ucap || smax > scap) {  // a work list did not fit: regrow, rebuild, rerun the join
-            ucap = std::max(ucap, umax + umax / 4 + 1024);
-            scap = std::max(scap, smax + smax / 4 + 1024);
+        if (umax > ucap) {  // the units did not fit: regrow, rebuild them, rerun the join
+            ucap = umax + umax / 4 + 1024;
             build_units();
             continue;
         }
-        sparse_cap_hint_ = std::max<int64_t>(sparse_cap_hint_, smax + smax / 8);
         units_cap_hint_ = std::max<int64_t>(units_cap_hint_, umax + umax / 8);
-        const unsigned long long total = h[0], ntag = h[1], reserved = h[7];
-        if (reserved > out_cap_) {
-            out_cap_ = (size_t)(reserved + reserved / 8 + 4 * (unsigned long long)kOutChunk);
+        const unsigned long long total = h[0], ntag = h[1];
+        if (omax > out_rcap_) {  // an output region filled up: regrow (per region) and rerun
+            out_rcap_ = ((omax + omax / 4) / kOutChunk + 2) * kOutChunk;
             continue;
         }
         if (timing_) {
@@ -1715,7 +1634,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             join_ms_ = ms;
         }
         keys_ = (int64_t)fetch(dnkeys, s);
-        runs_ = ns;  // records joined on the sparse path
+        runs_ = 0;
         units_ = nu;
         tests_ = (int64_t)h[2];
         iters_ = (int64_t)h[3];
@@ -1723,9 +1642,8 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         long_postings_ = idx->n_long_fp;
         tagged_ = (int64_t)ntag;
         const int64_t n = (int64_t)total;
-        // close the holes of partly filled chunks (pairs above n -> holes below n)
-        const int64_t nch = (int64_t)(reserved / kOutChunk);
-        if ((int64_t)reserved > n && nch > 0) {
+        // close the holes of partly filled / unreserved chunks (pairs above n -> holes below n)
+        if (nch > 0) {
             int64_t *hole = cnt64_.ensure(4 * (nch + 2)), *tail = hole + (nch + 2);
             int64_t *hoff = tail + (nch + 2), *toff = hoff + (nch + 2);
             hipLaunchKernelGGL(k_fix_counts, dim3(grid_for(nch, kBlock)), dim3(kBlock), 0, s, nch, fills, n, hole, tail);
@@ -1741,7 +1659,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             return;
         }
         // long x long pairs: split off, sort, unique, append
-        uint32_t *q2 = oq2_.ensure(out_cap_), *e2 = oe2_.ensure(out_cap_);
+        uint32_t *q2 = oq2_.ensure(n + 1), *e2 = oe2_.ensure(n + 1);
         unsigned long long *k1 = tkey_.ensure(ntag + 1), *k2 = tkey2_.ensure(ntag + 1);
         int64_t *dtot = (int64_t *)(cnt + 9);
         int64_t nun = 0, nt = 0, nuq = 0;

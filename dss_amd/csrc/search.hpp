@@ -98,8 +98,8 @@ class SearchEngine {
         *merges = merges_;
         *merge_lanes = merge_lanes_;
     }
-    // runs = records joined on the sparse (one lane per record) path; iters =
-    // posting broadcasts of the dense path; tests = record x posting lane tests
+    // runs = 0 (kept for the ABI); iters = record broadcasts (wave
+    // iterations); tests = record x posting lane tests
     void last_work(int64_t *runs, int64_t *iters, int64_t *tests) const
     {
         *runs = runs_;
@@ -115,11 +115,12 @@ class SearchEngine {
     DevBuf<uint8_t> qlong_;
     DevBuf<unsigned char> rec_, units_buf_, batch_buf_;
     DevBuf<unsigned long long> counter_, regcnt_;
-    DevBuf<uint32_t> oq_, oe_, oq2_, oe2_, work_, fills_;
+    DevBuf<uint32_t> oq_, oe_, oq2_, oe2_, fills_;
+    DevBuf<unsigned long long> work_;
     DevBuf<unsigned long long> tkey_, tkey2_;
     int n_cu_ = 0;
-    size_t out_cap_ = 0;
-    int64_t units_cap_hint_ = 0, sparse_cap_hint_ = 0;
+    int64_t out_rcap_ = 0;  // output slots per region
+    int64_t units_cap_hint_ = 0;
     bool timing_ = false;
     double join_ms_ = 0;
     int64_t units_ = 0, keys_ = 0, runs_ = 0, iters_ = 0, tests_ = 0;

@@ -66,6 +66,7 @@ void Store::upsert(SearchEngine &se, int64_t n, const uint32_t *ids, const int64
         r.t0 = t0[i];
         r.t1 = t1[i];
         r.owner = owner ? owner[i] : 0;
+        if (!r.in_delta) delta_list_.push_back(id);
         r.in_delta = true;
         tomb(id);
     }
@@ -81,8 +82,7 @@ void Store::remove(SearchEngine &se, int64_t n, const uint32_t *ids, int32_t *fo
         if (found) found[i] = f ? 1 : 0;
         if (!f) continue;
         Row &r = rows_[id];
-        r.live = false;
-        r.in_delta = false;
+        r.live = false;  // stays in delta_list_ until the next refresh drops it
         r.cells.clear();
         live_--;
         tomb(id);
@@ -146,9 +146,21 @@ dssg_index *Store::build(SearchEngine &se, const std::vector<uint32_t> &ids, hip
 // has grown past max(kMinDelta, base / kDeltaFrac)), then upload tombstones.
 void Store::refresh(SearchEngine &se, hipStream_t s)
 {
+    // the delta's ids come from the write list (O(delta), not O(max id));
+    // deleted ones leave it here
     std::vector<uint32_t> dids;
-    for (uint32_t id = 0; id < rows_.size(); id++)
-        if (rows_[id].live && rows_[id].in_delta) dids.push_back(id);
+    size_t keep = 0;
+    for (const uint32_t id : delta_list_) {
+        Row &r = rows_[id];
+        if (!r.live) {
+            r.in_delta = false;
+            continue;
+        }
+        delta_list_[keep++] = id;
+        dids.push_back(id);
+    }
+    delta_list_.resize(keep);
+    std::sort(dids.begin(), dids.end());
     const int64_t nbase = base_ ? base_->n_e : 0;
     if ((int64_t)dids.size() > std::max<int64_t>(kMinDelta, nbase / kDeltaFrac)) {
         compact(se, s);
@@ -179,6 +191,7 @@ void Store::compact(SearchEngine &se, hipStream_t s)
     base_pos_.assign(rows_.size(), -1);
     for (size_t i = 0; i < ids.size(); i++) base_pos_[ids[i]] = (int64_t)i;
     for (Row &r : rows_) r.in_delta = false;
+    delta_list_.clear();
     dead_h_.assign(ids.size() / 32 + 1, 0u);
     dead_dirty_ = false;
     if (!ids.empty()) base_ = build(se, ids, s, base_ids_);

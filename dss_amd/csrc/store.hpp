@@ -50,6 +50,7 @@ class Store {
     int device_;
     bool with_owner_;
     std::vector<Row> rows_;   // by caller id
+    std::vector<uint32_t> delta_list_;  // ids written since the base was built (in_delta set when listed)
     int64_t live_ = 0, compactions_ = 0;
     dssg_index *base_ = nullptr, *delta_ = nullptr;
     DevBuf<uint32_t> base_ids_, delta_ids_;  // dense index -> id

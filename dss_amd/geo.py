@@ -357,8 +357,8 @@ def UnionVolumes4DBatch(requests: Sequence[Sequence[Volume4D]], device: int = 0)
         v = Volume4D(StartTime=None if s0[i] == _lib.TIME_NULL_START else int(s0[i]),
                      EndTime=None if s1[i] == _lib.TIME_NULL_END_Q else int(s1[i]))
         if spatial[i]:
-            v.SpatialVolume = Volume3D(AltitudeLo=None if np.isnan(lo[i]) else float(lo[i]),
-                                       AltitudeHi=None if np.isnan(hi[i]) else float(hi[i]))
+            v.SpatialVolume = Volume3D(AltitudeLo=None if lo[i] == -np.inf else float(lo[i]),
+                                       AltitudeHi=None if hi[i] == np.inf else float(hi[i]))
             if fp[i]:
                 g = _PrecomputedCellGeometry()
                 for c in cells[offs[i]:offs[i + 1]]:

@@ -464,9 +464,10 @@ class MutableOperationStore:
 
     def UpsertOperation(self, op: "Operation", key: Sequence[str], now_us: int, now_rfc3339: str):
         old = self.ops.get(op.ID)
-        if old is None and op.Version != 0:
+        # Version.Empty() is v <= 0 (pkg/scd/models/models.go:56-58)
+        if old is None and op.Version > 0:
             raise NotFound(op.ID)
-        if old is not None and op.Version == 0:
+        if old is not None and op.Version <= 0:
             raise AlreadyExists(op.ID)
         if old is not None and op.Version != old.Version:
             raise VersionMismatch("old version")

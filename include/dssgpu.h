@@ -124,11 +124,12 @@ int dssg_area_to_cell_ids(dssg_ctx *ctx, const char *area, uint64_t *out_cells, 
  * A batch of multi-extent volumes: extents [vol_offs[v], vol_offs[v+1]) form
  * volume v (vol_offs on device for the _device form).  Extent x: footprint as
  * dssg_cover_batch (kind/voff/lat/lng/radius_m) iff has_fp[x] != 0; altitudes
- * NaN = NULL; t0 = DSSG_TIME_NULL_START / t1 = DSSG_TIME_NULL_END_Q = NULL.
+ * NaN = NULL on input; t0 = DSSG_TIME_NULL_START / t1 = DSSG_TIME_NULL_END_Q = NULL.
  * Per volume: the union of the extents' coverings (sorted, unique; the
  * reference's map order is unspecified, Q14), min start / max end / min
  * altitude_lower / max altitude_upper over the extents carrying them (NULL if
- * none), has_footprint, and the first covering error in extent order (status
+ * none, returned as -INFINITY / +INFINITY so a union volume can be passed
+ * straight to the index build or a search), has_footprint, and the first covering error in extent order (status
  * DSSG_ST_*, area_km2 for DSSG_ST_AREA_TOO_LARGE), where UnionVolumes4D would
  * return that error. */
 typedef struct {
@@ -137,7 +138,7 @@ typedef struct {
     const uint64_t *cells;     /* device, union cells per volume, sorted */
     const int32_t *status;     /* device, n */
     const double *area_km2;    /* device, n */
-    const float *alt_lo, *alt_hi;  /* device, n (NaN = NULL) */
+    const float *alt_lo, *alt_hi;  /* device, n (NULL -> -INFINITY / +INFINITY, the search sentinels) */
     const int64_t *t0, *t1;    /* device, n (NULL sentinels as above) */
     const uint8_t *has_footprint;  /* device, n */
     int64_t total_cells;

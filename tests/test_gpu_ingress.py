@@ -117,3 +117,36 @@ def test_union_matches_host_mirror():
         assert g.StartTime == h.StartTime and g.EndTime == h.EndTime
         if h.SpatialVolume is not None and h.SpatialVolume.Footprint is not None:
             assert set(g.SpatialVolume.Footprint.keys()) == set(h.SpatialVolume.Footprint.keys())
+
+
+def test_union_null_altitude_feeds_search(oracle):
+    """A union volume whose extents carry no altitude comes back with the
+    search's NULL sentinels (-INF / +INF), so passing dssg_volumes straight to
+    a search matches like the reference's COALESCE(..., true)
+    (pkg/scd/store/cockroach/operations.go:394-397)."""
+    import ctypes as C
+    import torch
+    from dss_amd import _lib, device as D
+    from dss_amd.store import EntityIndex
+    ctx = _lib.context()
+    dev = "cuda:0"
+    # one volume: a circle with no altitude bounds and no times
+    t = lambda a, dt: torch.as_tensor(np.asarray(a, dtype=dt), device=dev)  # noqa: E731
+    bufs = [t([0, 1], np.int64), t([_lib.KIND_CIRCLE], np.int32), t([0, 1], np.int64), t([37.5], np.float64),
+            t([-122.2], np.float64), t([300.0], np.float32), t([1], np.uint8), t([np.nan], np.float32),
+            t([np.nan], np.float32), t([_lib.TIME_NULL_START], np.int64), t([_lib.TIME_NULL_END_Q], np.int64)]
+    out = _lib.Volumes()
+    ctx.check(ctx.L.dssg_union_volumes_device(ctx.h, 1, *[D._ptr(b) for b in bufs], D._stream_ptr(), C.byref(out)))
+    offs = D.copy_back(ctx, out.offs, 2, np.int64)
+    cells = D.copy_back(ctx, out.cells, int(offs[-1]), np.uint64)
+    lo = D.copy_back(ctx, out.alt_lo, 1, np.float32)
+    hi = D.copy_back(ctx, out.alt_hi, 1, np.float32)
+    assert lo[0] == -np.inf and hi[0] == np.inf
+    # an operation in the same place, 1000-1100 m, now .. now + 1 h
+    now = 1_600_000_000_000_000
+    rc, e_cells = oracle.circle_covering(37.5, -122.2, 100.0)
+    idx = EntityIndex(np.array([0, len(e_cells)], np.int64), np.asarray(e_cells, np.uint64),
+                      np.array([1000.0], np.float32), np.array([1100.0], np.float32), np.array([now], np.int64),
+                      np.array([now + 3_600_000_000], np.int64))
+    rq, re = idx.search_operations_batch(offs, cells, lo, hi, [_lib.TIME_NULL_START], [_lib.TIME_NULL_END_Q], now)
+    assert list(rq) == [0] and list(re) == [0]

@@ -164,3 +164,52 @@ def test_device_api_matches_host_api(golden_covering):
     key = np.sort((q.astype(np.uint64) << np.uint64(32)) | e.astype(np.uint64))
     hkey = (hq.astype(np.uint64) << np.uint64(32)) | he.astype(np.uint64)
     assert np.array_equal(key, hkey)
+
+
+@pytest.mark.parametrize("nq,ne,span_h,dur", [
+    (3000, 6000, 24, "mixed"),     # long runs: > 64 records and > 64 postings per cell
+    (64, 4096, 24, "mixed"),       # exactly one 64-record batch
+    (130, 130, 2, "mixed"),        # run lengths around the 64 boundaries
+    (2000, 3000, 1, "short"),      # RID-like 30 s windows, dense in time
+    (500, 3000, 24, "long"),       # many long-duration entities (the long part of a cell)
+])
+def test_hot_cell_band_join(oracle, nq, ne, span_h, dur):
+    """Hot cells: every footprint within a few level-13 cells, so one cell's
+    records and postings span many 64-wide tiles and batches; the band join's
+    record ranges (cooperative 64-ary search over start-sorted records), tile
+    bounds and long-duration postings against the oracle."""
+    from dss_amd.store import EntityIndex
+    rng = np.random.default_rng(nq * 7 + ne)
+    T, H, M = 1_600_000_000_000_000, 3_600_000_000, 60_000_000
+    cells = np.array([oracle.cellid_from_degrees(37.5 + 0.01 * i, -122.2) for i in range(3)], dtype=np.uint64)
+
+    def lists(n):
+        k = rng.integers(1, 4, n)
+        offs = np.zeros(n + 1, np.int64)
+        np.cumsum(k, out=offs[1:])
+        c = np.concatenate([np.sort(rng.choice(cells, int(x), replace=False)) for x in k])
+        return offs, c.astype(np.uint64)
+
+    eo, ec = lists(ne)
+    qo, qc = lists(nq)
+    e_t0 = T + rng.integers(0, span_h * H, ne)
+    if dur == "short":
+        e_t1 = e_t0 + 30_000_000
+    elif dur == "long":
+        e_t1 = e_t0 + np.where(rng.random(ne) < 0.3, rng.integers(10 * H, 30 * H, ne), rng.integers(5 * M, 2 * H, ne))
+    else:
+        e_t1 = e_t0 + rng.integers(5 * M, 2 * H, ne)
+    e_lo = rng.uniform(0, 400, ne).astype(np.float32)
+    e_hi = (e_lo + rng.uniform(10, 200, ne)).astype(np.float32)
+    q_t0 = T + rng.integers(0, span_h * H, nq)
+    q_t1 = q_t0 + (30_000_000 if dur == "short" else rng.integers(1 * M, 30 * M, nq))
+    wide = rng.random(nq) < 0.05  # NULL end -> a wide window
+    q_t1 = np.where(wide, np.iinfo(np.int64).max, q_t1)
+    q_lo = rng.uniform(0, 400, nq).astype(np.float32)
+    q_hi = (q_lo + rng.uniform(10, 200, nq)).astype(np.float32)
+    idx = EntityIndex(eo, ec, e_lo, e_hi, e_t0, e_t1)
+    rq, re = idx.search_operations_batch(qo, qc, q_lo, q_hi, q_t0, q_t1, T)
+    tlo = np.maximum(q_t0, T)
+    oq, oe = oracle.search(eo, ec, e_lo, e_hi, e_t0, e_t1, None, qo, qc, q_lo, q_hi, tlo, q_t1)
+    assert len(oq) > 0
+    assert np.array_equal(rq, oq) and np.array_equal(re, oe)

@@ -113,6 +113,11 @@ def test_operation_write_path_semantics():
         s.UpsertOperation(Operation("op-a", "uss1", cells, 0.0, 100.0, T, T + H), [], T, "2023-11-14T22:13:21Z")
     with pytest.raises(NotFound):
         s.UpsertOperation(Operation("op-x", "uss1", cells, 0.0, 100.0, T, T + H, version=3), [], T, "z")
+    # Version.Empty() is v <= 0 (pkg/scd/models/models.go:56-58): a negative version is "create"
+    with pytest.raises(AlreadyExists):
+        s.UpsertOperation(Operation("op-a", "uss1", cells, 0.0, 100.0, T, T + H, version=-2), [], T, "z")
+    n = s.UpsertOperation(Operation("op-n", "uss9", cells, 900.0, 950.0, T, T + H, version=-1), [], T, "n")
+    assert n.Version == 1
     with pytest.raises(VersionMismatch):
         s.UpsertOperation(Operation("op-a", "uss1", cells, 0.0, 100.0, T, T + H, version=7), [a.OVN], T, "z")
     with pytest.raises(PermissionDenied):
