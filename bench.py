@@ -111,16 +111,21 @@ def main():
     i_alo, i_ahi, i_t0, i_t1 = t(ia.alt_lo), t(ia.alt_hi), t(ia.t0), t(ia.t1)
     torch.cuda.synchronize()
     tb = time.time()
-    icells = D.cover(ctx, d_int)
+    # the intents' coverings, covered in chunks and kept in torch-owned HBM
+    # (the next cover() call reuses the library's own output buffers)
+    i_offs_t, i_cells_t = cover_chunked(ctx, D, torch, intents, dev)
+    icells = _lib.Cells(ni, int(i_offs_t.data_ptr()), int(i_cells_t.data_ptr()), 0, 0, int(i_cells_t.numel()))
+    del d_int
+    cover_i_s = time.time() - tb
+    tb = time.time()
     ranges = None
+    large = i_cells_t.numel() > LARGE_POSTINGS
     if mode == "sharded":
         from dss_amd import shard
         # splitters from the intent postings (host), then this rank's shard
-        i_offs_h = D.copy_back(ctx, icells.offs, ni + 1, np.int64)
-        i_cells_h = D.copy_back(ctx, icells.cells, int(i_offs_h[-1]), np.uint64)
+        i_cells_h = i_cells_t.cpu().numpy().view(np.uint64)
         ranges = shard.cell_splitters(i_cells_h, world)
-        # parity reference: the whole index, built while icells is valid (the
-        # next cover() reuses its buffers)
+        # parity reference: the whole index
         full_index = None if args.no_verify else D.build_index(ctx, icells, i_alo, i_ahi, i_t0, i_t1)
         tb = time.time()
         index = D.build_index(ctx, icells, i_alo, i_ahi, i_t0, i_t1, cell_range=ranges[rank])
@@ -129,11 +134,13 @@ def main():
     torch.cuda.synchronize()
     build_s = time.time() - tb
     n_post = int(ctx.L.dssg_index_num_postings(index))
-    # keep intent cells for the CPU baseline before the next cover() reuses buffers
-    i_offs_h = D.copy_back(ctx, icells.offs, ni + 1, np.int64)
-    i_cells_h = D.copy_back(ctx, icells.cells, int(i_offs_h[-1]), np.uint64)
-    log(f"[rank {rank}] mode {mode}, setup {time.time() - t_setup:.1f}s, index build {build_s:.2f}s, postings {n_post}")
-    sort_ph = sort_phase(ctx, torch, dev, i_offs_h, i_cells_h) if rank == 0 and mode != "sharded" else None
+    log(f"[rank {rank}] mode {mode}, setup {time.time() - t_setup:.1f}s, intent cover {cover_i_s:.2f}s, index build "
+        f"{build_s:.2f}s, postings {n_post}")
+    sort_ph = None
+    if rank == 0 and mode != "sharded":
+        sort_ph = (sort_phase(ctx, torch, dev, i_offs_t, i_cells_t) if not large else
+                   {"skipped": f"{i_cells_t.numel()} postings: the sort's scratch on top of the index would not fit "
+                               f"beside it; the build's sorts are inside index_build_s"})
     sharded = None
     if mode == "sharded":
         sharded = shard.ShardedSearch(ctx, index, ranges, stage_host=stage_host)
@@ -261,7 +268,8 @@ def main():
     if rank == 0:
         cpu = parity = None
         if args.cpu_sample != 0 and world == 1:
-            cpu, parity = cpu_baseline(args, ctx, intents, ia, queries, qa, now, i_offs_h, i_cells_h, cells, pairs)
+            cpu, parity = cpu_baseline(args, ctx, intents, ia, queries, qa, now,
+                                       lambda sc: intent_csr(torch, i_offs_t, i_cells_t, sc), cells, pairs)
         traffic = pmc_traffic("k_join", nq, ni)
         result = {
             "metric": "4D conflict queries/sec vs N-intent airspace",
@@ -417,17 +425,80 @@ def sharded_report(args, ctx, D, dist, torch, sh, step, full, i_cells_h, ranges,
     print(json.dumps(result), flush=True)
 
 
-def sort_phase(ctx, torch, dev, i_offs, i_cells):
+LARGE_POSTINGS = 600_000_000  # above: no host copy of the intents' cells, no standalone sort-phase run
+
+
+def cover_chunked(ctx, D, torch, fp, dev, chunk=4_000_000):
+    """Cover footprints chunk by chunk on the GPU; the CSR lands in torch
+    tensors (offs int64 [n+1], cells int64 bit patterns [P])."""
+    import ctypes as C
+    n = fp.n
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    parts = []
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        sub = fp.subset(np.arange(a, b)) if (a, b) != (0, n) else fp
+        d = D.DeviceFootprints.upload(sub, dev)
+        c = D.cover(ctx, d)
+        o = torch.empty(b - a + 1, dtype=torch.int64, device=dev)
+        x = torch.empty(max(1, int(c.total_cells)), dtype=torch.int64, device=dev)
+        ctx.check(ctx.L.dssg_copy_device(ctx.h, C.c_void_p(o.data_ptr()), C.c_void_p(c.offs), 8 * (b - a + 1),
+                                         D._stream_ptr()))
+        if c.total_cells:
+            ctx.check(ctx.L.dssg_copy_device(ctx.h, C.c_void_p(x.data_ptr()), C.c_void_p(c.cells),
+                                             8 * int(c.total_cells), D._stream_ptr()))
+        parts.append((a, b, o, x[: int(c.total_cells)]))
+        del d
+    torch.cuda.synchronize()
+    total = sum(int(x.numel()) for _, _, _, x in parts)
+    cells = torch.empty(max(1, total), dtype=torch.int64, device=dev)
+    base = 0
+    for a, b, o, x in parts:
+        offs[a + 1: b + 1] = o[1:] + base
+        cells[base: base + x.numel()] = x
+        base += int(x.numel())
+    del parts
+    return offs, cells[:total]
+
+
+def intent_csr(torch, offs_t, cells_t, sample_cells):
+    """Host CSR of the intents the CPU baseline's index needs: all of them,
+    or -- for airspaces past LARGE_POSTINGS -- only those sharing a cell with
+    the sample's queries (the only ones that can pair with them), found on the
+    GPU.  Returns (offs, cells, entity ids)."""
+    if cells_t.numel() <= LARGE_POSTINGS:
+        offs = offs_t.cpu().numpy()
+        return offs, cells_t.cpu().numpy().view(np.uint64), np.arange(len(offs) - 1, dtype=np.int64)
+    sc = torch.as_tensor(np.unique(sample_cells).view(np.int64), device=cells_t.device)
+    hits = []
+    step = 1 << 27
+    for a in range(0, cells_t.numel(), step):  # chunked: bounded scratch
+        x = cells_t[a: a + step]
+        i = torch.searchsorted(sc, x).clamp_(max=sc.numel() - 1)
+        hits.append(torch.nonzero(sc[i] == x).squeeze(1) + a)
+    pos = torch.cat(hits)
+    ents = torch.unique(torch.searchsorted(offs_t, pos, right=True) - 1)
+    starts, ends = offs_t[ents], offs_t[ents + 1]
+    lens = ends - starts
+    new_offs = torch.zeros(ents.numel() + 1, dtype=torch.int64, device=cells_t.device)
+    new_offs[1:] = torch.cumsum(lens, 0)
+    idx = torch.repeat_interleave(starts - new_offs[:-1], lens) + torch.arange(int(new_offs[-1]), device=cells_t.device)
+    sub = cells_t[idx]
+    return new_offs.cpu().numpy(), sub.cpu().numpy().view(np.uint64), ents.cpu().numpy()
+
+
+def sort_phase(ctx, torch, dev, i_offs_t, i_cells_t):
     """Sort-phase roofline: the index build's (cell, entity)
     radix sort (radix.hip) on this airspace's own postings, timed with HIP
     events on the library's stream.  Algorithmic bytes: 24 B per posting
     (8 B key + 4 B payload, read and written once)."""
     import ctypes as C
-    P = len(i_cells)
+    P = int(i_cells_t.numel())
     if P == 0:
         return None
-    keys = torch.as_tensor(i_cells.view(np.int64), device=dev)
-    vals = torch.as_tensor(np.repeat(np.arange(len(i_offs) - 1, dtype=np.int32), np.diff(i_offs)), device=dev)
+    keys = i_cells_t
+    n = i_offs_t.numel() - 1
+    vals = torch.repeat_interleave(torch.arange(n, dtype=torch.int32, device=dev), i_offs_t[1:] - i_offs_t[:-1])
     ko, vo = torch.empty_like(keys), torch.empty_like(vals)
     torch.cuda.synchronize()
     ms = C.c_double(0)
@@ -534,13 +605,15 @@ def cpu_threads(args):
 AUTO_CPU_SAMPLE = {0: None, 1: None, 2: None, 3: None, 4: 20000}
 
 
-def cpu_baseline(args, ctx, intents, ia, queries, qa, now, i_offs, i_cells, g_cells, g_pairs):
+def cpu_baseline(args, ctx, intents, ia, queries, qa, now, intent_csr_fn, g_cells, g_pairs):
     """The CPU restatement (oracle/, kind "port": pthreads over the process's
     CPU share) timed on the same step: cover the sample's query footprints and
-    search them against the same intent posting list (built untimed).  The
-    sample is the first n queries of the batch; their oracle cell sets and
-    pair set are compared with the GPU step's (every cell and every pair of the
-    sampled queries; the whole batch for configs[0]/[1])."""
+    search them against the intents' posting list (built untimed; for the
+    largest airspaces only the intents sharing a cell with the sample, which
+    are the only ones that can pair with it).  The sample is the first n
+    queries of the batch; their oracle cell sets and pair set are compared
+    with the GPU step's (every cell and every pair of the sampled queries; the
+    whole batch for configs[0]..[3])."""
     from dss_amd import device as D
     from oracle import oracle as O
     O.build()
@@ -551,17 +624,23 @@ def cpu_baseline(args, ctx, intents, ia, queries, qa, now, i_offs, i_cells, g_ce
     n = min(n, queries.n)
     sub = queries if n == queries.n else queries.subset(np.arange(n))
     th = cpu_threads(args)
-    idx = O.Index(i_offs, i_cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1)
     t0 = time.perf_counter()
     qo, qc, _, _ = O.cover_batch(sub.kind, sub.voff, sub.lat, sub.lng, sub.radius_m, nthreads=th)
     t1 = time.perf_counter()
+    i_offs, i_cells, ents = intent_csr_fn(qc)
+    sel = lambda a: a[ents] if len(ents) != len(a) else a  # noqa: E731
+    idx = O.Index(i_offs, i_cells, sel(ia.alt_lo), sel(ia.alt_hi), sel(ia.t0), sel(ia.t1))
     tlo = np.maximum(qa.t0[:n], now)
-    rq, re = idx.search(qo, qc, qa.alt_lo[:n], qa.alt_hi[:n], tlo, qa.t1[:n], nthreads=th)
     t2 = time.perf_counter()
+    rq, re = idx.search(qo, qc, qa.alt_lo[:n], qa.alt_hi[:n], tlo, qa.t1[:n], nthreads=th)
+    t3 = time.perf_counter()
+    re = ents[re]
     info = cpu_info()
-    cpu = {"value": n / (t2 - t0), "unit": "queries/s", "cores": th, "kind": "port",
-           "sample": f"{n} of the step's {queries.n} queries (cover + search) vs the full {intents.n}-intent index",
-           "coverings_per_s": n / (t1 - t0), "seconds": t2 - t0, "cpu_model": info["model"],
+    secs = (t1 - t0) + (t3 - t2)
+    cpu = {"value": n / secs, "unit": "queries/s", "cores": th, "kind": "port",
+           "sample": f"{n} of the step's {queries.n} queries (cover + search) vs the {intents.n}-intent index"
+                     + ("" if len(ents) == intents.n else f" (the {len(ents)} intents sharing a cell with the sample)"),
+           "coverings_per_s": n / (t1 - t0), "seconds": secs, "cpu_model": info["model"],
            "nproc": info["nproc"], "affinity_cpus": info["affinity"],
            "threads_note": "threads = the process's CPU share on the GPU box (OMP_NUM_THREADS / affinity)"}
     parity = None

@@ -156,6 +156,7 @@ def load():
         L.dssg_search_touched_device.argtypes = [vp, vp, i64, vp, vp, vp, P(i64)]
         L.dssg_index_info.argtypes = [vp, P(i64), P(i64), P(i64), P(i64), P(i64), P(i64)]
         L.dssg_copy_to_host.argtypes = [vp, vp, vp, C.c_size_t]
+        L.dssg_copy_device.argtypes = [vp, vp, vp, C.c_size_t, vp]
         L.dssg_radix_sort_device.argtypes = [vp, C.c_int, i64, C.c_int, vp, vp, vp, vp, vp, P(d)]
         L.dssg_selftest_scan.argtypes = [vp, i64, C.c_int, P(i64), P(i64)]
         L.dssg_selftest_math.argtypes = [vp, C.c_int, i64, P(d), P(d), P(d)]

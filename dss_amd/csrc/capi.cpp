@@ -836,6 +836,15 @@ int dssg_index_info(const dssg_index *idx, int64_t *postings, int64_t *cells, in
     return DSSG_OK;
 }
 
+int dssg_copy_device(dssg_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream)
+{
+    if (!ctx || (bytes && (!dst || !src))) return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        if (bytes) DSS_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+    });
+}
+
 int dssg_copy_to_host(dssg_ctx *ctx, void *dst, const void *src, size_t bytes)
 {
     if (!ctx || (bytes && (!dst || !src))) return DSSG_ERR_INVALID;

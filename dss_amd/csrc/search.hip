@@ -56,6 +56,33 @@ constexpr uint32_t kNoSlot = 0xffffffffu;
 constexpr unsigned long long kWideWindow = 1ull << 32;
 constexpr int kOrderBits = 23;                          // query order key: quantised tlo
 constexpr uint32_t kWideKey = (1u << kOrderBits) - 1u;  // ... wide queries last
+
+// Work lists written from kRegions counters (spread 256 B apart; one
+// same-address counter saturates at ~88 atomics/us, MI355X_MICROARCH.md
+// "dequeue"): region r holds its items at [r * cap, r * cap + count(r)).
+constexpr int kRegions = 8;
+constexpr int kRegStride = 32;
+struct Regions {
+    unsigned long long *cnt;  // kRegions counters, kRegStride words apart
+    int64_t cap;              // items per region
+    __device__ __forceinline__ unsigned long long *counter(int r) const { return cnt + r * kRegStride; }
+    // total items written and the region of virtual item u (u < total)
+    __device__ __forceinline__ int64_t total(int64_t pre[kRegions + 1]) const
+    {
+        pre[0] = 0;
+#pragma unroll
+        for (int r = 0; r < kRegions; r++) pre[r + 1] = pre[r] + min((int64_t)cnt[r * kRegStride], cap);
+        return pre[kRegions];
+    }
+    __device__ __forceinline__ int64_t slot_of(const int64_t pre[kRegions + 1], int64_t u) const
+    {
+        int r = 0;
+#pragma unroll
+        for (int k = 1; k < kRegions; k++) r += u >= pre[k] ? 1 : 0;
+        return r * cap + (u - pre[r]);
+    }
+};
+
 #ifndef DSS_JOIN_BPC
 #define DSS_JOIN_BPC 6
 #endif
@@ -580,9 +607,10 @@ __device__ __forceinline__ uint32_t order_q(long long t, long long tbase, int qs
 
 // Query order key: quantised tlo (narrow windows), kWideKey (wide ones); the
 // widest narrow window of the batch -> *dqmax.
-__global__ void k_qorder(int64_t nq, const int64_t *tlo, const int64_t *thi, long long tbase, int qshift, uint32_t *key,
-                         uint32_t *val, unsigned long long *dqmax)
+__global__ __launch_bounds__(kBlock) void k_qorder(int64_t nq, const int64_t *tlo, const int64_t *thi, long long tbase,
+                                                   int qshift, uint32_t *key, uint32_t *val, unsigned long long *dqmax)
 {
+    __shared__ unsigned long long wmax[kBlock / 64];
     const int64_t q = tid64();
     unsigned long long dq = 0;
     if (q < nq) {
@@ -596,7 +624,13 @@ __global__ void k_qorder(int64_t nq, const int64_t *tlo, const int64_t *thi, lon
         val[q] = (uint32_t)q;
     }
     for (int o = 32; o > 0; o >>= 1) dq = max(dq, __shfl_xor(dq, o));
-    if ((threadIdx.x & 63) == 0 && dq) atomicMax(dqmax, dq);
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = dq;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // one atomic per block, on one of kRegions slots (readers take the max)
+        unsigned long long m = 0;
+        for (int i = 0; i < kBlock / 64; i++) m = max(m, wmax[i]);
+        if (m) atomicMax(&dqmax[(blockIdx.x % kRegions) * kRegStride], m);
+    }
 }
 
 // Per query (in order rank r): its cells with postings.
@@ -698,32 +732,6 @@ __device__ __forceinline__ uint64_t ub_m(const longlong2 *bt, uint64_t lo, uint6
     return lo;
 }
 
-// Work lists written from kRegions counters (spread 256 B apart; one
-// same-address counter saturates at ~88 atomics/us, MI355X_MICROARCH.md
-// "dequeue"): region r holds its items at [r * cap, r * cap + count(r)).
-constexpr int kRegions = 8;
-constexpr int kRegStride = 32;
-struct Regions {
-    unsigned long long *cnt;  // kRegions counters, kRegStride words apart
-    int64_t cap;              // items per region
-    __device__ __forceinline__ unsigned long long *counter(int r) const { return cnt + r * kRegStride; }
-    // total items written and the region of virtual item u (u < total)
-    __device__ __forceinline__ int64_t total(int64_t pre[kRegions + 1]) const
-    {
-        pre[0] = 0;
-#pragma unroll
-        for (int r = 0; r < kRegions; r++) pre[r + 1] = pre[r] + min((int64_t)cnt[r * kRegStride], cap);
-        return pre[kRegions];
-    }
-    __device__ __forceinline__ int64_t slot_of(const int64_t pre[kRegions + 1], int64_t u) const
-    {
-        int r = 0;
-#pragma unroll
-        for (int k = 1; k < kRegions; k++) r += u >= pre[k] ? 1 : 0;
-        return r * cap + (u - pre[r]);
-    }
-};
-
 // Inclusive prefix sum over the 64 lanes with DPP (no LDS round trips):
 // row_shr 1/2/4/8 scan each 16-lane row, row_bcast 15 / 31 carry the row
 // totals into the rows above (CDNA DPP; rows outside row_mask keep `old`=0).
@@ -736,16 +744,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
     return x;
-}
-
-// Quantised start of every sorted record (the query-order key of a narrow
-// record): the join searches a cell's narrow records by it.
-__global__ void k_stq(const uint32_t *sval, const QRec *recs, const int64_t *dnkeys, long long tbase, int qshift,
-                      uint32_t *stq)
-{
-    const int64_t i = tid64();
-    if (i >= *dnkeys) return;
-    stq[i] = order_q(recs[sval[i]].tlo, tbase, qshift);
 }
 
 __device__ __forceinline__ uint32_t lb_u32(const uint32_t *x, uint32_t lo, uint32_t hi, uint32_t v)
@@ -841,13 +839,27 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
 // Narrow record sub-range of every regular tile: a narrow record (window <=
 // dqmax) meets a posting only if tlo in [m - dqmax, max(t0, t1)], and over a
 // start-sorted tile that is [m_first - dqmax, m_last + dcap]; the records'
-// quantised starts (stq) bracket it by binary search.  One thread per unit.
-__global__ void k_unit_ranges(IndexView a, Regions ur, Unit *units, const uint32_t *stq,
-                              const unsigned long long *dqmax, long long tbase, int qshift)
+// quantised starts (their order) bracket it by binary search.  One thread
+// per unit.
+__device__ __forceinline__ uint32_t lb_rec_q(const uint32_t *sval, const QRec *recs, uint32_t lo, uint32_t hi, uint32_t v,
+                                             long long tbase, int qshift)
+{
+    while (lo < hi) {  // first record in [lo, hi) with order_q(tlo) >= v
+        const uint32_t m = (lo + hi) >> 1;
+        if (order_q(recs[sval[m]].tlo, tbase, qshift) < v) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
+
+__global__ void k_unit_ranges(IndexView a, Regions ur, Unit *units, const uint32_t *sval, const QRec *recs,
+                              const unsigned long long *dqslots, long long tbase, int qshift)
 {
     int64_t pre[kRegions + 1];
     const int64_t n = ur.total(pre);
-    const long long dq = (long long)min(*dqmax, 1ull << 62);
+    unsigned long long dqm = 0;
+    for (int r = 0; r < kRegions; r++) dqm = max(dqm, dqslots[r * kRegStride]);
+    const long long dq = (long long)min(dqm, 1ull << 62);
     for (int64_t u = tid64(); u < n; u += nthreads64()) {
         Unit &d = units[ur.slot_of(pre, u)];
         if ((d.np & kUnitLong) || d.n1 <= d.n0) continue;
@@ -855,8 +867,8 @@ __global__ void k_unit_ranges(IndexView a, Regions ur, Unit *units, const uint32
         const long long m0 = tmin2(f.x, f.y), m1 = tmin2(l.x, l.y);
         const long long lo = m0 < LLONG_MIN + dq ? LLONG_MIN : m0 - dq;
         const long long hi = m1 > LLONG_MAX - a.dcap ? LLONG_MAX : m1 + a.dcap;
-        const uint32_t n0 = lb_u32(stq, d.n0, d.n1, order_q(lo, tbase, qshift));
-        d.n1 = lb_u32(stq, n0, d.n1, order_q(hi, tbase, qshift) + 1u);
+        const uint32_t n0 = lb_rec_q(sval, recs, d.n0, d.n1, order_q(lo, tbase, qshift), tbase, qshift);
+        d.n1 = lb_rec_q(sval, recs, n0, d.n1, order_q(hi, tbase, qshift) + 1u, tbase, qshift);
         d.n0 = n0;
     }
 }
@@ -880,7 +892,7 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m)
 // atomics/us, MI355X_MICROARCH.md "dequeue"); each retired chunk records its
 // fill, and k_fix_* close the holes that partly filled or unreserved chunks
 // leave below the total.
-constexpr int kOutChunk = 2048;
+constexpr int kOutChunk = 1024;
 struct OutArgs {
     uint32_t *q, *e;
     int64_t rcap;                  // slots per region (a multiple of kOutChunk)
@@ -940,10 +952,6 @@ struct JoinArgs {
     QueryView qv;
     Regions ur;                        // units (k_units)
     OutArgs out;
-    const uint32_t *stq;               // quantised start of every sorted record
-    const unsigned long long *dqmax;   // device: widest narrow query window (us)
-    long long tbase;                   // query-order quantisation
-    int qshift;
 };
 
 // One wavefront per unit, lane = posting (the tile stays in registers); the
@@ -1127,36 +1135,40 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
     }
 }
 
-// Closing the output holes: chunk c holds fills[c] pairs at c * kOutChunk;
-// with n pairs in all, the holes below n are filled with the pairs above n.
+// Closing the output holes: chunk c holds fills[c] pairs at c * kOutChunk
+// (0 = never reserved); with n pairs in all, the holes below n are filled
+// with the pairs at or above n, in order.  k_fix_counts: per chunk its holes
+// below n and its pairs at or above n; k_fix_fill: one block per chunk below
+// n walks its holes and finds each source in the (few) chunks at or above n.
 __global__ void k_fix_counts(int64_t nch, const uint32_t *fills, int64_t n, int64_t *hole, int64_t *tail)
 {
     const int64_t c = tid64();
     if (c >= nch) return;
     const int64_t s = c * kOutChunk, f = fills[c];
-    const int64_t h0 = s + f, h1 = min(s + (int64_t)kOutChunk, n);   // holes below n
-    const int64_t t0 = max(s, n), t1 = s + f;                         // pairs at or above n
+    const int64_t h0 = s + f, h1 = min(s + (int64_t)kOutChunk, n);  // holes below n
+    const int64_t t0 = max(s, n), t1 = s + f;                        // pairs at or above n
     hole[c] = h1 > h0 ? h1 - h0 : 0;
     tail[c] = t1 > t0 ? t1 - t0 : 0;
 }
-__global__ void k_fix_move(int64_t nch, const uint32_t *fills, int64_t n, const int64_t *hoff, const int64_t *toff,
-                           uint32_t *q, uint32_t *e)
+__global__ void k_fix_fill(int64_t nch, const uint32_t *fills, int64_t n, const int64_t *hole, const int64_t *hoff,
+                           const int64_t *toff, uint32_t *q, uint32_t *e)
 {
     const int64_t c = blockIdx.x;
-    if (c >= nch) return;
-    const int64_t s = c * kOutChunk, f = fills[c];
-    const int64_t t0 = max(s, n), t1 = s + f;
-    for (int64_t k = t0 + threadIdx.x; k < t1; k += blockDim.x) {
-        const int64_t h = toff[c] + (k - t0);  // global hole index
-        int64_t lo = 0, hi = nch;                // chunk cc with hoff[cc] <= h < hoff[cc + 1]
+    const int64_t h = hole[c];
+    if (h == 0) return;
+    const int64_t clo = n / kOutChunk;  // chunks holding pairs at or above n start here
+    for (int64_t k = threadIdx.x; k < h; k += blockDim.x) {
+        const int64_t t = hoff[c] + k;  // its source: the t-th pair at or above n
+        int64_t lo = clo, hi = nch;     // tail chunk tc with toff[tc] <= t < toff[tc + 1]
         while (hi - lo > 1) {
             const int64_t mid = (lo + hi) >> 1;
-            if (hoff[mid] <= h) lo = mid;
+            if (toff[mid] <= t) lo = mid;
             else hi = mid;
         }
-        const int64_t dst = lo * kOutChunk + fills[lo] + (h - hoff[lo]);
-        q[dst] = q[k];
-        e[dst] = e[k];
+        const int64_t src = max(lo * kOutChunk, n) + (t - toff[lo]);
+        const int64_t dst = c * kOutChunk + fills[c] + k;
+        q[dst] = q[src];
+        e[dst] = e[src];
     }
 }
 
@@ -1522,10 +1534,16 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     const int64_t nqc = fetch(q_offs + nq, s);
     if (nqc >= (int64_t)0xffffffffll) throw Error(DSSG_ERR_CAPACITY, "search: more than 2^32 - 1 query cells per batch");
     if (nqc == 0) return empty();
-    // [0] pairs [1] tagged [2] lane tests [3] broadcasts [5] long queries [6] units [7] output slots reserved
-    // [8] sparse records [9] scratch
-    unsigned long long *cnt = counter_.ensure(12);
-    DSS_HIP(hipMemsetAsync(cnt, 0, 12 * sizeof(unsigned long long), s));
+    // one control block (a single memset to start, one copy back per join):
+    // dqmax slots, unit region counters, misc counters ([0] pairs [1] tagged
+    // [2] lane tests [3] broadcasts [5] long queries [9] scratch), unit queue
+    // heads, output region counters -- kRegStride words between counters
+    constexpr int kR = kRegions * kRegStride;
+    constexpr int kCtlDq = 0, kCtlUnits = kR, kCtlMisc = 2 * kR, kCtlQueue = 2 * kR + 16, kCtlOut = 3 * kR + 16,
+                  kCtlWords = 4 * kR + 16;
+    unsigned long long *ctl = counter_.ensure(kCtlWords);
+    unsigned long long *cnt = ctl + kCtlMisc;
+    DSS_HIP(hipMemsetAsync(ctl, 0, kCtlWords * sizeof(unsigned long long), s));
     // (1) per query cell: query, decode, slot; per query: long flag
     uint32_t *cq = cq_.ensure(nqc + 1), *dec = dec_.ensure(nqc + 1), *cslot = bt_.ensure(nqc + 1);
     uint8_t *qlong = qlong_.ensure(nq + 1);
@@ -1535,7 +1553,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     uint32_t *ok0 = okey_.ensure(nq + 1), *ok1 = okey2_.ensure(nq + 1), *ov0 = oval_.ensure(nq + 1),
              *perm = perm_.ensure(nq + 1);
     hipLaunchKernelGGL(k_qorder, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_tlo, q_thi, (long long)idx->tbase,
-                       idx->qshift, ok0, ov0, cnt + 10);
+                       idx->qshift, ok0, ov0, ctl + kCtlDq);
     radix_sort_pairs(ok0, ok1, ov0, perm, nq, kOrderBits, tmp_, s);
     // (3) keys (slot << 1 | wide, query cell) in that order; records per cell
     int64_t *qc = qcnt_.ensure(nq + 1), *qo = qoff_.ensure(nq + 2);
@@ -1551,43 +1569,32 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     // order), over the device key count qo[nq] (<= nqc)
     const int64_t *dnkeys = qo + nq;
     radix_sort_pairs_dn(key, skey, val, sval, nqc, dnkeys, bits_for(idx->n_slots()) + 1, tmp_, s);
-    // (5) the sorted records' quantised starts; join units = 64-posting
-    // tiles of every cell the batch meets
+    // (5) join units = 64-posting tiles of every cell the batch meets, each
+    // with the records it can meet
     if (n_cu_ == 0) {
         int dev = 0, ncu = 0;
         DSS_HIP(hipGetDevice(&dev));
         DSS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
         n_cu_ = ncu > 0 ? ncu : 256;
     }
-    uint32_t *stq = rbeg_.ensure(nqc + 1);
-    hipLaunchKernelGGL(k_stq, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, sval, recs, dnkeys, (long long)idx->tbase,
-                       idx->qshift, stq);
-    // per-region unit capacity: the tiles of every cell is an upper bound
-    int64_t ucap = std::max<int64_t>(units_cap_hint_, 1024);
-    unsigned long long *rc = regcnt_.ensure(kRegions * kRegStride);
+    int64_t ucap = std::max<int64_t>(units_cap_hint_, 1024);  // per region
     Unit *units = nullptr;
     const unsigned ugrid = (unsigned)std::min<int64_t>((nqc + 63) / 64 / (kBlock / 64) + 1, (int64_t)n_cu_ * 16);
     auto build_units = [&]() {
         units = (Unit *)units_buf_.ensure(sizeof(Unit) * (kRegions * ucap + 1));
-        DSS_HIP(hipMemsetAsync(rc, 0, sizeof(unsigned long long) * kRegions * kRegStride, s));
-        hipLaunchKernelGGL(k_units, dim3(ugrid), dim3(kBlock), 0, s, ix, skey, dnkeys, Regions{rc, ucap}, units);
-        hipLaunchKernelGGL(k_unit_ranges, dim3((unsigned)n_cu_ * 8), dim3(kBlock), 0, s, ix, Regions{rc, ucap}, units,
-                           (const uint32_t *)stq, (const unsigned long long *)(cnt + 10), (long long)idx->tbase,
-                           idx->qshift);
+        DSS_HIP(hipMemsetAsync(ctl + kCtlUnits, 0, kR * sizeof(unsigned long long), s));
+        hipLaunchKernelGGL(k_units, dim3(ugrid), dim3(kBlock), 0, s, ix, skey, dnkeys, Regions{ctl + kCtlUnits, ucap},
+                           units);
+        hipLaunchKernelGGL(k_unit_ranges, dim3((unsigned)n_cu_ * 8), dim3(kBlock), 0, s, ix,
+                           Regions{ctl + kCtlUnits, ucap}, units, (const uint32_t *)sval, (const QRec *)recs,
+                           (const unsigned long long *)(ctl + kCtlDq), (long long)idx->tbase, idx->qshift);
     };
     build_units();
     // (6) join; grow the output (and the units) and rerun if too small
     JoinArgs ja{};
     ja.ix = ix;
     ja.qv = qv;
-    ja.stq = stq;
-    ja.dqmax = cnt + 10;
-    ja.tbase = idx->tbase;
-    ja.qshift = idx->qshift;
     const unsigned nblocks = (unsigned)n_cu_ * kJoinBlocksPerCU;
-    // [0, kRegions) unit queue heads, [kRegions, 2 kRegions) output region counters (kRegStride apart)
-    unsigned long long *work = (unsigned long long *)work_.ensure(2 * kRegions * kRegStride * 2);
-    unsigned long long *octr = work + kRegions * kRegStride;
     if (out_rcap_ == 0) out_rcap_ = ((int64_t)nq * 16 / kRegions / kOutChunk + 2) * kOutChunk;
     const bool any_long = idx->n_long_fp > 0;  // the batch's long flag is only known on the device
     for (int attempt = 0; attempt < 5; attempt++) {
@@ -1595,27 +1602,24 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         uint32_t *oq = oq_.ensure(cap + 1), *oe = oe_.ensure(cap + 1);
         uint32_t *fills = fills_.ensure(nch + 1);
         DSS_HIP(hipMemsetAsync(fills, 0, sizeof(uint32_t) * nch, s));
-        DSS_HIP(hipMemsetAsync(cnt, 0, 4 * sizeof(unsigned long long), s));
-        DSS_HIP(hipMemsetAsync(work, 0, sizeof(unsigned long long) * 2 * kRegions * kRegStride, s));
-        ja.ur = Regions{rc, ucap};
-        ja.out = OutArgs{oq, oe, out_rcap_, fills, octr, cnt};
+        DSS_HIP(hipMemsetAsync(ctl + kCtlMisc, 0, (kCtlWords - kCtlMisc) * sizeof(unsigned long long), s));
+        ja.ur = Regions{ctl + kCtlUnits, ucap};
+        ja.out = OutArgs{oq, oe, out_rcap_, fills, ctl + kCtlOut, cnt};
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
         auto kern = q_owner ? (any_long ? k_join<true, true> : k_join<true, false>)
                             : (any_long ? k_join<false, true> : k_join<false, false>);
         hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs, (const uint32_t *)sval,
-                           (const Unit *)units, work);
+                           (const Unit *)units, ctl + kCtlQueue);
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
-        unsigned long long h[12], hr[kRegions * kRegStride], ho[kRegions * kRegStride];
-        DSS_HIP(hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, s));
-        DSS_HIP(hipMemcpyAsync(hr, rc, sizeof(hr), hipMemcpyDeviceToHost, s));
-        DSS_HIP(hipMemcpyAsync(ho, octr, sizeof(ho), hipMemcpyDeviceToHost, s));
+        unsigned long long h[kCtlWords];
+        DSS_HIP(hipMemcpyAsync(h, ctl, sizeof(h), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipStreamSynchronize(s));
         int64_t nu = 0, umax = 0, omax = 0;
         for (int r = 0; r < kRegions; r++) {
-            const int64_t u = (int64_t)hr[r * kRegStride];
+            const int64_t u = (int64_t)h[kCtlUnits + r * kRegStride];
             nu += u;
             umax = std::max(umax, u);
-            omax = std::max(omax, (int64_t)ho[r * kRegStride]);
+            omax = std::max(omax, (int64_t)h[kCtlOut + r * kRegStride]);
         }
         if (umax > ucap) {  // the units did not fit: regrow, rebuild them, rerun the join
             ucap = umax + umax / 4 + 1024;
@@ -1623,33 +1627,37 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             continue;
         }
         units_cap_hint_ = std::max<int64_t>(units_cap_hint_, umax + umax / 8);
-        const unsigned long long total = h[0], ntag = h[1];
         if (omax > out_rcap_) {  // an output region filled up: regrow (per region) and rerun
-            out_rcap_ = ((omax + omax / 4) / kOutChunk + 2) * kOutChunk;
+            out_rcap_ = ((omax + omax / 8) / kOutChunk + 2) * kOutChunk;
             continue;
         }
+        const unsigned long long total = h[kCtlMisc + 0], ntag = h[kCtlMisc + 1];
         if (timing_) {
             float ms = 0;
             DSS_HIP(hipEventElapsedTime(&ms, ev0_, ev1_));
             join_ms_ = ms;
+            keys_ = (int64_t)fetch(dnkeys, s);
         }
-        keys_ = (int64_t)fetch(dnkeys, s);
         runs_ = 0;
         units_ = nu;
-        tests_ = (int64_t)h[2];
-        iters_ = (int64_t)h[3];
-        long_queries_ = (int64_t)h[5];
+        tests_ = (int64_t)h[kCtlMisc + 2];
+        iters_ = (int64_t)h[kCtlMisc + 3];
+        long_queries_ = (int64_t)h[kCtlMisc + 5];
         long_postings_ = idx->n_long_fp;
         tagged_ = (int64_t)ntag;
         const int64_t n = (int64_t)total;
-        // close the holes of partly filled / unreserved chunks (pairs above n -> holes below n)
-        if (nch > 0) {
+        // close the holes of partly filled / unreserved chunks below n with
+        // the pairs at or above n
+        {
+            const int64_t nbelow = std::min<int64_t>(nch, (n + kOutChunk - 1) / kOutChunk);
             int64_t *hole = cnt64_.ensure(4 * (nch + 2)), *tail = hole + (nch + 2);
             int64_t *hoff = tail + (nch + 2), *toff = hoff + (nch + 2);
             hipLaunchKernelGGL(k_fix_counts, dim3(grid_for(nch, kBlock)), dim3(kBlock), 0, s, nch, fills, n, hole, tail);
             exclusive_scan_i64(hole, hoff, nch, tmp2_, s);
             exclusive_scan_i64(tail, toff, nch, tmp2_, s);
-            hipLaunchKernelGGL(k_fix_move, dim3((unsigned)nch), dim3(kBlock), 0, s, nch, fills, n, hoff, toff, oq, oe);
+            if (nbelow > 0)
+                hipLaunchKernelGGL(k_fix_fill, dim3((unsigned)nbelow), dim3(kBlock), 0, s, nch, fills, n, hole, hoff, toff,
+                                   oq, oe);
         }
         if (ntag == 0) {
             out->q = oq;

@@ -361,6 +361,9 @@ int dssg_search_touched_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq,
  * pointer may be NULL. */
 int dssg_index_info(const dssg_index *idx, int64_t *postings, int64_t *cells, int64_t *long_duration,
                     int64_t *long_footprint, int64_t *max_cell_postings, int64_t *dcap_us);
+/* Device-to-device copy on `stream` (e.g. an engine-owned dssg_cells buffer
+ * into caller memory before the next call reuses it). */
+int dssg_copy_device(dssg_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
 /* Copy `bytes` from an engine-owned device buffer (dssg_cells / dssg_pairs)
  * to host memory, on the context's device. */
 int dssg_copy_to_host(dssg_ctx *ctx, void *dst, const void *src, size_t bytes);
