@@ -46,6 +46,27 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+_STAGE = ["start"]
+
+
+def stage(name):
+    """Name the current stage (the heartbeat reports it)."""
+    _STAGE[0] = name
+    log(f"[bench] {name}")
+
+
+def heartbeat(every=30.0):
+    """A stderr line every `every` s while the process runs (long configs)."""
+    import threading
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(every)
+            log(f"[bench] alive {time.time() - t0:.0f}s, stage: {_STAGE[0]}")
+    threading.Thread(target=run, daemon=True).start()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -76,6 +97,7 @@ def main():
                     help="rehearsal: every rank on cuda:0 (one-GPU box, gloo backend)")
     args = ap.parse_args()
 
+    heartbeat()
     import torch
     import torch.distributed as dist
 
@@ -190,6 +212,7 @@ def main():
         run_steps(wctx, wstream, 1)
 
     # ------------------------------------------------------------ timed steps
+    stage("timed steps")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -224,6 +247,7 @@ def main():
         return
 
     # ------------------------------------------- phase timing + roofline
+    stage(f"phase timing ({value:.4g} queries/s over the timed steps)")
     import ctypes as C
     ctx.L.dssg_set_timing(ctx.h, 1)
     cover_ms, join_ms, kern_ms = [], [], []
@@ -251,6 +275,7 @@ def main():
     # inputs (24 B attributes + 8 B per covering cell), every posting of a
     # cell the batch touches read once (28 B: entity id, alt pair, time
     # pair), and the output pairs (8 B).
+    stage("touched postings")
     p_touched = touched_postings(ctx, D, index, cells)
     join_bytes = 24 * nq + 8 * c_tot + 28 * p_touched + 8 * r_tot
     achieved = join_bytes / (kern_avg_ms * 1e-3) / 1e9
@@ -259,6 +284,7 @@ def main():
     # would move; reported for reference, not as the roofline.
     m_tot, d_tot = C.c_int64(), C.c_int64()
     if args.survey_model:
+        stage("survey model counts")
         ctx.check(ctx.L.dssg_search_stats_device(ctx.h, index, cells.n, C.c_void_p(cells.offs),
                                                  C.c_void_p(cells.cells), D._stream_ptr(), C.byref(m_tot),
                                                  C.byref(d_tot)))
@@ -268,6 +294,7 @@ def main():
     if rank == 0:
         cpu = parity = None
         if args.cpu_sample != 0 and world == 1:
+            stage("cpu baseline")
             cpu, parity = cpu_baseline(args, ctx, intents, ia, queries, qa, now,
                                        lambda sc: intent_csr(torch, i_offs_t, i_cells_t, sc), cells, pairs)
         traffic = pmc_traffic("k_join", nq, ni)
@@ -437,7 +464,7 @@ def cover_chunked(ctx, D, torch, fp, dev, chunk=4_000_000):
     parts = []
     for a in range(0, n, chunk):
         b = min(n, a + chunk)
-        sub = fp.subset(np.arange(a, b)) if (a, b) != (0, n) else fp
+        sub = fp.slice(a, b) if (a, b) != (0, n) else fp
         d = D.DeviceFootprints.upload(sub, dev)
         c = D.cover(ctx, d)
         o = torch.empty(b - a + 1, dtype=torch.int64, device=dev)
@@ -457,7 +484,9 @@ def cover_chunked(ctx, D, torch, fp, dev, chunk=4_000_000):
         offs[a + 1: b + 1] = o[1:] + base
         cells[base: base + x.numel()] = x
         base += int(x.numel())
-    del parts
+    parts = x = o = None
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()  # the chunk copies' memory back to the device for the index build
     return offs, cells[:total]
 
 
@@ -469,22 +498,30 @@ def intent_csr(torch, offs_t, cells_t, sample_cells):
     if cells_t.numel() <= LARGE_POSTINGS:
         offs = offs_t.cpu().numpy()
         return offs, cells_t.cpu().numpy().view(np.uint64), np.arange(len(offs) - 1, dtype=np.int64)
-    sc = torch.as_tensor(np.unique(sample_cells).view(np.int64), device=cells_t.device)
-    hits = []
-    step = 1 << 27
-    for a in range(0, cells_t.numel(), step):  # chunked: bounded scratch
+    dev = cells_t.device
+    # int64 order (cell ids of faces 4, 5 are negative as int64): searchsorted needs it
+    sc = torch.as_tensor(np.unique(np.asarray(sample_cells, np.uint64).view(np.int64)), device=dev)
+    hit = torch.zeros(offs_t.numel() - 1, dtype=torch.bool, device=dev)
+    step = 1 << 26  # chunked: a few GB of scratch beside the resident index
+    for a in range(0, cells_t.numel(), step):
         x = cells_t[a: a + step]
         i = torch.searchsorted(sc, x).clamp_(max=sc.numel() - 1)
-        hits.append(torch.nonzero(sc[i] == x).squeeze(1) + a)
-    pos = torch.cat(hits)
-    ents = torch.unique(torch.searchsorted(offs_t, pos, right=True) - 1)
-    starts, ends = offs_t[ents], offs_t[ents + 1]
-    lens = ends - starts
-    new_offs = torch.zeros(ents.numel() + 1, dtype=torch.int64, device=cells_t.device)
-    new_offs[1:] = torch.cumsum(lens, 0)
-    idx = torch.repeat_interleave(starts - new_offs[:-1], lens) + torch.arange(int(new_offs[-1]), device=cells_t.device)
-    sub = cells_t[idx]
-    return new_offs.cpu().numpy(), sub.cpu().numpy().view(np.uint64), ents.cpu().numpy()
+        pos = torch.nonzero(sc[i] == x).squeeze(1) + a
+        del i
+        hit[torch.searchsorted(offs_t, pos, right=True) - 1] = True
+        del pos
+    ents = torch.nonzero(hit).squeeze(1)
+    del hit
+    offs_parts, cell_parts, base = [np.zeros(1, np.int64)], [], 0
+    for a in range(0, ents.numel(), 1 << 20):  # the selected entities' cells, block by block to the host
+        en = ents[a: a + (1 << 20)]
+        starts, lens = offs_t[en], offs_t[en + 1] - offs_t[en]
+        o = torch.cumsum(lens, 0)
+        idx = torch.repeat_interleave(starts - (o - lens), lens) + torch.arange(int(o[-1]), device=dev)
+        cell_parts.append(cells_t[idx].cpu().numpy().view(np.uint64))
+        offs_parts.append(o.cpu().numpy() + base)
+        base += int(o[-1])
+    return np.concatenate(offs_parts), np.concatenate(cell_parts), ents.cpu().numpy()
 
 
 def sort_phase(ctx, torch, dev, i_offs_t, i_cells_t):
@@ -627,13 +664,17 @@ def cpu_baseline(args, ctx, intents, ia, queries, qa, now, intent_csr_fn, g_cell
     t0 = time.perf_counter()
     qo, qc, _, _ = O.cover_batch(sub.kind, sub.voff, sub.lat, sub.lng, sub.radius_m, nthreads=th)
     t1 = time.perf_counter()
+    stage(f"cpu baseline: {n} queries covered in {t1 - t0:.1f}s; intents for the oracle index")
     i_offs, i_cells, ents = intent_csr_fn(qc)
+    stage(f"cpu baseline: oracle index over {len(ents)} intents, {len(i_cells)} postings")
     sel = lambda a: a[ents] if len(ents) != len(a) else a  # noqa: E731
     idx = O.Index(i_offs, i_cells, sel(ia.alt_lo), sel(ia.alt_hi), sel(ia.t0), sel(ia.t1))
     tlo = np.maximum(qa.t0[:n], now)
     t2 = time.perf_counter()
+    stage("cpu baseline: oracle search")
     rq, re = idx.search(qo, qc, qa.alt_lo[:n], qa.alt_hi[:n], tlo, qa.t1[:n], nthreads=th)
     t3 = time.perf_counter()
+    stage(f"cpu baseline: search {t3 - t2:.1f}s; parity")
     re = ents[re]
     info = cpu_info()
     secs = (t1 - t0) + (t3 - t2)

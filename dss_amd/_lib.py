@@ -149,6 +149,7 @@ def load():
         L.dssg_phase_times.argtypes = [vp, P(d), P(d), P(d)]
         L.dssg_set_timing.argtypes = [vp, C.c_int]
         L.dssg_set_timing.restype = None
+        L.dssg_set_tuning.argtypes = [vp, C.c_char_p, C.c_int64]
         L.dssg_join_events.argtypes = [vp, P(i64), P(i64), P(i64), P(i64)]
         L.dssg_join_longs.argtypes = [vp, P(i64), P(i64)]
         L.dssg_search_counters.argtypes = [vp, P(i64), P(i64), P(i64), P(i64), P(i64)]
@@ -180,6 +181,10 @@ class Context:
     def check(self, rc: int):
         if rc not in (DSSG_OK,):
             raise DssgError(rc, self.L.dssg_last_error(self.h).decode() or self.L.dssg_strerror(rc).decode())
+
+    def set_tuning(self, key: str, value: int):
+        """dssg_set_tuning (e.g. "tag_bucket_avg")."""
+        self.check(self.L.dssg_set_tuning(self.h, key.encode(), int(value)))
 
     def close(self):
         if getattr(self, "h", None):

@@ -220,6 +220,16 @@ void dssg_set_timing(dssg_ctx *ctx, int enabled)
     ctx->search.set_timing(ctx->timing);
 }
 
+int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value)
+{
+    if (!ctx || !key) return DSSG_ERR_INVALID;
+    if (std::string(key) == "tag_bucket_avg") {
+        ctx->search.set_tag_bucket_avg(value);
+        return DSSG_OK;
+    }
+    return DSSG_ERR_INVALID;
+}
+
 int dssg_phase_times(dssg_ctx *ctx, double *cover_ms, double *join_ms, double *join_kernel_ms)
 {
     if (!ctx) return DSSG_ERR_INVALID;
@@ -841,7 +851,7 @@ int dssg_copy_device(dssg_ctx *ctx, void *dst, const void *src, size_t bytes, vo
     if (!ctx || (bytes && (!dst || !src))) return DSSG_ERR_INVALID;
     return guarded(ctx, [&] {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-        if (bytes) DSS_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+        dss::device_copy(dst, src, bytes, s);
     });
 }
 

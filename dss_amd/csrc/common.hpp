@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -42,7 +43,20 @@ struct DevBuf {
     {
         if (n <= cap && p) return p;
         release();
-        size_t c = n < 16 ? 16 : n + n / 4;
+        // 25 % growth slack, at most 256 MiB of it
+        const size_t slack = std::min(n / 4, ((size_t)256 << 20) / sizeof(T));
+        size_t c = n < 16 ? 16 : n + slack;
+        DSS_HIP(hipMalloc(&p, c * sizeof(T)));
+        cap = c;
+        return p;
+    }
+    // no growth slack: for the long-lived index arrays (tens of GB at the
+    // largest airspaces)
+    T *ensure_exact(size_t n)
+    {
+        if (n <= cap && p) return p;
+        release();
+        const size_t c = n < 16 ? 16 : n;
         DSS_HIP(hipMalloc(&p, c * sizeof(T)));
         cap = c;
         return p;
@@ -50,6 +64,14 @@ struct DevBuf {
 };
 
 inline unsigned grid_for(int64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
+
+// Device-to-device copy by a kernel (16-byte vectors when both ends allow),
+// any size: the runtime's blit path is not relied on for multi-GB copies.
+void device_copy(void *dst, const void *src, size_t bytes, hipStream_t s);
+
+// With DSSG_SYNC_CHECK=1 in the environment: synchronize and raise with the
+// stage's name on any device error (localizes a fault to a build stage).
+void stage_check(hipStream_t s, const char *stage);
 
 // Exclusive prefix sum of n int64 values into out (n+1 entries, out[n] = total),
 // hand-written reduce-then-scan in scan.hip (in != out).
@@ -60,6 +82,6 @@ void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, DevBuf<unsig
 // within each part unspecified): per-footprint kernels then run one kind's
 // code path per wave.
 void partition_polygons_first(const int32_t *kind, uint32_t *perm, unsigned long long *nsel, int64_t n,
-                              DevBuf<unsigned char> &tmp, hipStream_t s);
+                              DevBuf<unsigned char> &tmp, DevBuf<unsigned char> &tmp2, hipStream_t s);
 
 }  // namespace dss

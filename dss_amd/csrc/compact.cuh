@@ -2,7 +2,8 @@
 //
 // compact_if(n, pred, emit): emit(i, rank) for every i in [0, n) with
 // pred(i), rank = number of earlier i with pred -- without materialising a
-// flag array (the predicate is evaluated twice, once per pass):
+// flag array (the predicate is evaluated twice, once per pass); split_if
+// also places the failing elements (rank i - passing before i):
 //   k_cmp_count  one 4096-element tile per block: count -> cnt[tile]
 //   exclusive_scan_i64 over the tile counts (scan.hip)
 //   k_cmp_emit   the tile again: per 256-element row a ballot per wave, the
@@ -15,6 +16,8 @@
 // Emit: __device__ void operator()(int64_t i, int64_t rank) const
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -50,9 +53,17 @@ __global__ __launch_bounds__(kBlock) void k_cmp_count(int64_t n, Pred pred, int6
     }
 }
 
-template <class Pred, class Emit>
-__global__ __launch_bounds__(kBlock) void k_cmp_emit(int64_t n, Pred pred, Emit emit, const int64_t *__restrict__ off)
+struct NoEmit {
+    __device__ void operator()(int64_t, int64_t) const {}
+};
+
+// EmitF: also place the elements failing pred (rank among those = i - the
+// passing ones before i); NoEmit: compaction only.
+template <class Pred, class Emit, class EmitF>
+__global__ __launch_bounds__(kBlock) void k_cmp_emit(int64_t n, Pred pred, Emit emit, EmitF emit_f,
+                                                     const int64_t *__restrict__ off)
 {
+    constexpr bool kSplit = !std::is_same<EmitF, NoEmit>::value;
     __shared__ uint32_t rc[kRows * kWaves];  // (row, wave) counts, then their exclusive prefix
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t base = (int64_t)blockIdx.x * kTile;
@@ -81,10 +92,12 @@ __global__ __launch_bounds__(kBlock) void k_cmp_emit(int64_t n, Pred pred, Emit 
     const int64_t tb = off[blockIdx.x];
 #pragma unroll
     for (int r = 0; r < kRows; r++) {
-        if ((pm >> r) & 1u) {
-            const int64_t i = base + (int64_t)r * kBlock + threadIdx.x;
-            emit(i, tb + (int64_t)rc[r * kWaves + w] + (int64_t)lanes_below(bal[r]));
-        }
+        const int64_t i = base + (int64_t)r * kBlock + threadIdx.x;
+        const int64_t rank = tb + (int64_t)rc[r * kWaves + w] + (int64_t)lanes_below(bal[r]);
+        if ((pm >> r) & 1u)
+            emit(i, rank);
+        else if (kSplit && i < n)
+            emit_f(i, i - rank);
     }
 }
 
@@ -93,11 +106,13 @@ inline int64_t tiles_for(int64_t n) { return (n + kTile - 1) / kTile; }
 
 }  // namespace cmpct
 
-// Order-preserving compaction; the total lands in *d_total (device, int64)
-// and, when `h_total` is non-null, on the host (one stream sync).
-template <class Pred, class Emit>
-void compact_if(int64_t n, Pred pred, Emit emit, DevBuf<unsigned char> &tmp, DevBuf<unsigned char> &scan_tmp,
-                hipStream_t s, int64_t *d_total, int64_t *h_total)
+// Order-preserving split: emit(i, rank) for the elements passing pred,
+// emit_f(i, rank) for the others (each rank within its side); the passing
+// count lands in *d_total (device, int64) and, when `h_total` is non-null, on
+// the host (one stream sync).  EmitF = cmpct::NoEmit: plain compaction.
+template <class Pred, class Emit, class EmitF>
+void split_if(int64_t n, Pred pred, Emit emit, EmitF emit_f, DevBuf<unsigned char> &tmp,
+              DevBuf<unsigned char> &scan_tmp, hipStream_t s, int64_t *d_total, int64_t *h_total)
 {
     const int64_t nt = cmpct::tiles_for(n);
     if (n <= 0) {
@@ -111,14 +126,22 @@ void compact_if(int64_t n, Pred pred, Emit emit, DevBuf<unsigned char> &tmp, Dev
     int64_t *off = cnt + nt;
     hipLaunchKernelGGL(cmpct::k_cmp_count<Pred>, dim3((unsigned)nt), dim3(cmpct::kBlock), 0, s, n, pred, cnt);
     exclusive_scan_i64(cnt, off, nt, scan_tmp, s);
-    hipLaunchKernelGGL((cmpct::k_cmp_emit<Pred, Emit>), dim3((unsigned)nt), dim3(cmpct::kBlock), 0, s, n, pred, emit,
-                       (const int64_t *)off);
+    hipLaunchKernelGGL((cmpct::k_cmp_emit<Pred, Emit, EmitF>), dim3((unsigned)nt), dim3(cmpct::kBlock), 0, s, n, pred,
+                       emit, emit_f, (const int64_t *)off);
     DSS_HIP(hipMemcpyAsync(d_total, off + nt, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
     DSS_HIP(hipGetLastError());
     if (h_total) {
         DSS_HIP(hipMemcpyAsync(h_total, off + nt, sizeof(int64_t), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipStreamSynchronize(s));
     }
+}
+
+// Order-preserving compaction (split_if without the failing side).
+template <class Pred, class Emit>
+void compact_if(int64_t n, Pred pred, Emit emit, DevBuf<unsigned char> &tmp, DevBuf<unsigned char> &scan_tmp,
+                hipStream_t s, int64_t *d_total, int64_t *h_total)
+{
+    split_if(n, pred, emit, cmpct::NoEmit{}, tmp, scan_tmp, s, d_total, h_total);
 }
 
 }  // namespace dss

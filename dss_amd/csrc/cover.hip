@@ -1168,7 +1168,7 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     DSS_HIP(hipMemsetAsync(slow_n, 0, sizeof(unsigned int), s));
     DSS_HIP(hipMemsetAsync(fan_fail, 0, n, s));
     DSS_HIP(hipMemsetAsync(not_inner, 0, n, s));
-    partition_polygons_first(kind, perm, fcnt_.ensure(n + 1), n, tmp_, s);
+    partition_polygons_first(kind, perm, fcnt_.ensure(n + 2), n, tmp_, tmp2_, s);
     // per-vertex pre-pass: frames, owners, S2 points, fan terms
     hipLaunchKernelGGL(k_circle_frames, dim3(grid_for(n, B)), dim3(B), 0, s, n, kind, voff, lat, lng, radius_m, frames);
     hipLaunchKernelGGL(k_vowner, dim3(grid_for(n, B)), dim3(B), 0, s, n, xoff, vown);

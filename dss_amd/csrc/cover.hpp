@@ -38,7 +38,7 @@ class CoverEngine {
     DevBuf<unsigned char> frames_;
     DevBuf<unsigned int> slow_n_;
     DevBuf<double4> clipf_, clipc_;
-    DevBuf<unsigned char> tmp_;
+    DevBuf<unsigned char> tmp_, tmp2_;
     DevBuf<int> flag_;
     DevBuf<unsigned long long> fcnt_;
     DevBuf<uint64_t> cells_;

@@ -301,8 +301,8 @@ void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, const int64_t
     const int kbits = (int)(8 * sizeof(K));
     if (bits > kbits) bits = kbits;
     if (bits <= 0) {
-        DSS_HIP(hipMemcpyAsync(ko, ki, sizeof(K) * n, hipMemcpyDeviceToDevice, s));
-        if (HAS_V) DSS_HIP(hipMemcpyAsync(vo, vi, sizeof(V) * n, hipMemcpyDeviceToDevice, s));
+        device_copy(ko, ki, sizeof(K) * n, s);
+        if (HAS_V) device_copy(vo, vi, sizeof(V) * n, s);
         return;
     }
     const int64_t ntiles = (n + kTile - 1) / kTile, stride = (ntiles + 3) & ~(int64_t)3;
@@ -327,8 +327,8 @@ void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, const int64_t
         }
     }
     if (bits <= lo) {
-        DSS_HIP(hipMemcpyAsync(ko, ki, sizeof(K) * n, hipMemcpyDeviceToDevice, s));
-        if (HAS_V) DSS_HIP(hipMemcpyAsync(vo, vi, sizeof(V) * n, hipMemcpyDeviceToDevice, s));
+        device_copy(ko, ki, sizeof(K) * n, s);
+        if (HAS_V) device_copy(vo, vi, sizeof(V) * n, s);
         return;
     }
     const int span = bits - lo, passes = (span + kMaxDigitBits - 1) / kMaxDigitBits, rb = (span + passes - 1) / passes;

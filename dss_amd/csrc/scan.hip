@@ -1,13 +1,17 @@
 // Device-wide scans used by the covering and search pipelines for
-// order-preserving compaction: the int64 exclusive scan is hand-written
-// (below); the polygon/circle partition uses hipCUB.
-#include <hipcub/hipcub.hpp>
+// order-preserving compaction (the int64 exclusive scan below, the
+// polygon/circle partition over compact.cuh), plus the device copy.
+#include <cstdlib>
+#include <string>
 
 #include "common.hpp"
+#include "compact.cuh"
 
 namespace dss {
 
 namespace {
+
+__device__ __forceinline__ int64_t tid64_s() { return (int64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 
 // Exclusive int64 prefix sum, reduce-then-scan over 2048-element tiles
 // (256 lanes x 8 consecutive elements):
@@ -123,21 +127,59 @@ void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, DevBuf<unsig
 }
 
 namespace {
-struct NotCircle {
-    __host__ __device__ bool operator()(int32_t k) const { return k != DSSG_KIND_CIRCLE; }
+struct IsCircle {
+    const int32_t *kind;
+    bool want;
+    __device__ bool operator()(int64_t i) const { return (kind[i] == DSSG_KIND_CIRCLE) == want; }
 };
+struct PlaceAt {
+    uint32_t *perm;
+    const int64_t *base;  // device: the first part's size (nullptr: 0)
+    __device__ void operator()(int64_t i, int64_t r) const { perm[(base ? *base : 0) + r] = (uint32_t)i; }
+};
+
+__global__ void k_copy16(int64_t n16, const uint4 *__restrict__ src, uint4 *__restrict__ dst)
+{
+    for (int64_t i = tid64_s(); i < n16; i += (int64_t)gridDim.x * blockDim.x) dst[i] = src[i];
+}
+__global__ void k_copy1(int64_t n, const unsigned char *__restrict__ src, unsigned char *__restrict__ dst)
+{
+    for (int64_t i = tid64_s(); i < n; i += (int64_t)gridDim.x * blockDim.x) dst[i] = src[i];
+}
 }  // namespace
 
 void partition_polygons_first(const int32_t *kind, uint32_t *perm, unsigned long long *nsel, int64_t n,
-                              DevBuf<unsigned char> &tmp, hipStream_t s)
+                              DevBuf<unsigned char> &tmp, DevBuf<unsigned char> &tmp2, hipStream_t s)
 {
     if (n <= 0) return;
-    hipcub::CountingInputIterator<uint32_t> idx(0);
-    hipcub::TransformInputIterator<bool, NotCircle, const int32_t *> flags(kind, NotCircle());
-    size_t bytes = 0;
-    DSS_HIP(hipcub::DevicePartition::Flagged(nullptr, bytes, idx, flags, perm, nsel, (int)n, s));
-    tmp.ensure(bytes + 16);
-    DSS_HIP(hipcub::DevicePartition::Flagged(tmp.p, bytes, idx, flags, perm, nsel, (int)n, s));
+    // non-circles first (their count -> nsel[0]), then circles after them
+    int64_t *npoly = (int64_t *)nsel, *ncirc = (int64_t *)(nsel + 1);
+    compact_if(n, IsCircle{kind, false}, PlaceAt{perm, nullptr}, tmp, tmp2, s, npoly, nullptr);
+    compact_if(n, IsCircle{kind, true}, PlaceAt{perm, npoly}, tmp, tmp2, s, ncirc, nullptr);
+}
+
+void device_copy(void *dst, const void *src, size_t bytes, hipStream_t s)
+{
+    if (!bytes) return;
+    const bool a16 = (((uintptr_t)dst | (uintptr_t)src) & 15) == 0;
+    const int64_t n16 = a16 ? (int64_t)(bytes / 16) : 0, done = n16 * 16;
+    const unsigned g = 8192;  // grid-stride: any size, work items < 2^32
+    if (n16) hipLaunchKernelGGL(k_copy16, dim3(g), dim3(256), 0, s, n16, (const uint4 *)src, (uint4 *)dst);
+    if ((int64_t)bytes > done)
+        hipLaunchKernelGGL(k_copy1, dim3(g), dim3(256), 0, s, (int64_t)bytes - done, (const unsigned char *)src + done,
+                           (unsigned char *)dst + done);
+    DSS_HIP(hipGetLastError());
+}
+
+void stage_check(hipStream_t s, const char *stage)
+{
+    static const bool on = [] {
+        const char *e = std::getenv("DSSG_SYNC_CHECK");
+        return e && *e && *e != '0';
+    }();
+    if (!on) return;
+    const hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) throw Error(DSSG_ERR_DEVICE, std::string("after ") + stage + ": " + hipGetErrorString(e));
 }
 
 }  // namespace dss

@@ -1172,9 +1172,27 @@ __global__ void k_fix_fill(int64_t nch, const uint32_t *fills, int64_t n, const 
     }
 }
 
-// Tagged (long x long) pairs after the join: untagged pairs compacted into
-// (q2, e2), tagged ones into 64-bit keys (q << 32 | e); the keys are sorted
-// and the first of each run appended after the untagged pairs.
+// Tagged (long x long) pairs after the join.  One split pass sends the
+// untagged pairs to (q2, e2) and the tagged ones to 64-bit keys
+// ((q << eb | e) << hb | bucket), bucket = hb hash bits of the pair; a radix
+// sort over the hb bucket bits only (ceil(hb / 8) passes instead of a full
+// 40+-bit sort) groups equal pairs in one bucket of ~1024 keys (tunable), and
+// one block per bucket removes the duplicates in an LDS hash set.  A bucket
+// too large for the LDS set (never at the average) falls back to a full sort
+// of its keys.
+constexpr int kDedupBlock = 256, kDedupSlots = 4096;  // 32 KB of LDS: several blocks per CU
+constexpr int64_t kDedupMax = kDedupSlots * 3 / 4;
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x)
+{
+    x ^= x >> 31;
+    x *= 0x7fb5d329728ea185ull;
+    x ^= x >> 27;
+    x *= 0x81dadef4bc2dd44dull;
+    x ^= x >> 33;
+    return x;
+}
+
 struct PredTag {
     const uint32_t *q;
     bool tagged;
@@ -1189,27 +1207,129 @@ struct EmitUntagged {
         e2[r] = e[i];
     }
 };
-struct EmitTagKey {
+struct EmitTagKey {  // hb == 0: the plain (q << 32 | e) key of the full-sort path
     const uint32_t *q, *e;
     unsigned long long *key;
+    int eb, hb;
     __device__ void operator()(int64_t i, int64_t r) const
     {
-        key[r] = ((unsigned long long)(q[i] & ~kTag) << 32) | e[i];
+        if (hb == 0) {
+            key[r] = ((unsigned long long)(q[i] & ~kTag) << 32) | e[i];
+            return;
+        }
+        const unsigned long long pk = ((unsigned long long)(q[i] & ~kTag) << eb) | e[i];
+        key[r] = (pk << hb) | (mix64(pk) >> (64 - hb));
     }
 };
 struct PredRunU64 {
     const unsigned long long *k;
     __device__ bool operator()(int64_t i) const { return i == 0 || k[i] != k[i - 1]; }
 };
-struct EmitPairFromKey {
+struct EmitPairFromKey {  // key = q << eb | e
     const unsigned long long *k;
     uint32_t *q, *e;
     int64_t at;
+    int eb;
     __device__ void operator()(int64_t i, int64_t r) const
     {
-        q[at + r] = (uint32_t)(k[i] >> 32);
-        e[at + r] = (uint32_t)k[i];
+        q[at + r] = (uint32_t)(k[i] >> eb);
+        e[at + r] = (uint32_t)(k[i] & ((1ull << eb) - 1));
     }
+};
+
+// bucket b's keys are [bs[b], be[b]) of the bucket-sorted keys (0, 0 if none)
+__global__ void k_tag_bounds(int64_t n, const unsigned long long *__restrict__ k, int hb, int64_t *__restrict__ bs,
+                             int64_t *__restrict__ be)
+{
+    const int64_t i = tid64();
+    if (i >= n) return;
+    const unsigned long long m = (1ull << hb) - 1, b = k[i] & m;
+    if (i == 0 || (k[i - 1] & m) != b) bs[b] = i;
+    if (i == n - 1 || (k[i + 1] & m) != b) be[b] = i + 1;
+}
+
+// One block per bucket: its distinct pairs (keys >> hb) into stage[bs[b] ..),
+// their count into cnt[b]; a bucket over kDedupMax keys is flagged instead.
+__global__ __launch_bounds__(kDedupBlock) void k_tag_dedupe(const unsigned long long *__restrict__ k,
+                                                             const int64_t *__restrict__ bs,
+                                                             const int64_t *__restrict__ be, int hb,
+                                                             unsigned long long *__restrict__ stage,
+                                                             int64_t *__restrict__ cnt, uint8_t *__restrict__ ovf,
+                                                             unsigned long long *__restrict__ novf)
+{
+    __shared__ unsigned long long tab[kDedupSlots];
+    __shared__ uint32_t nout;
+    const int64_t b = blockIdx.x, lo = bs[b], hi = be[b];
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (hi - lo > kDedupMax) {  // block-uniform
+        if (tid == 0) {
+            cnt[b] = 0;
+            ovf[b] = 1;
+            atomicAdd(novf, 1ull);
+        }
+        return;
+    }
+    if (tid == 0) ovf[b] = 0;
+    if (hi == lo) {
+        if (tid == 0) cnt[b] = 0;
+        return;
+    }
+    // table: the smallest power of two >= 2x the bucket's keys (load <= 1/2)
+    uint32_t slots = 256;
+    while ((int64_t)slots < 2 * (hi - lo) && slots < (uint32_t)kDedupSlots) slots <<= 1;
+    const uint32_t smask = slots - 1;
+    constexpr unsigned long long kEmpty = ~0ull;
+    for (uint32_t i = tid; i < slots; i += kDedupBlock) tab[i] = kEmpty;
+    if (tid == 0) nout = 0;
+    __syncthreads();
+    for (int64_t i = lo + tid; i < hi; i += kDedupBlock) {
+        const unsigned long long pk = k[i] >> hb;
+        uint32_t h = (uint32_t)mix64(pk ^ 0x9e3779b97f4a7c15ull) & smask;
+        while (true) {  // fewer distinct keys than slots: a free slot always exists
+            const unsigned long long prev = atomicCAS(&tab[h], kEmpty, pk);
+            if (prev == kEmpty || prev == pk) break;
+            h = (h + 1) & smask;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < slots; i0 += kDedupBlock) {
+        const unsigned long long v = i0 + tid < slots ? tab[i0 + tid] : kEmpty;
+        const bool has = v != kEmpty;
+        const unsigned long long m = __ballot(has);
+        uint32_t base = 0;
+        if (lane == 0 && m) base = atomicAdd(&nout, (uint32_t)__popcll(m));
+        base = __shfl(base, 0);
+        if (has) stage[lo + base + mbcnt64(m)] = v;
+    }
+    __syncthreads();
+    if (tid == 0) cnt[b] = nout;
+}
+
+// bucket b's distinct pairs -> (q, e) at off[b]
+__global__ void k_tag_emit(const unsigned long long *__restrict__ stage, const int64_t *__restrict__ bs,
+                           const int64_t *__restrict__ cnt, const int64_t *__restrict__ off, int eb,
+                           uint32_t *__restrict__ q, uint32_t *__restrict__ e)
+{
+    const int64_t b = blockIdx.x, c = cnt[b], lo = bs[b], o = off[b];
+    const unsigned long long em = (1ull << eb) - 1;
+    for (int64_t j = threadIdx.x; j < c; j += blockDim.x) {
+        const unsigned long long pk = stage[lo + j];
+        q[o + j] = (uint32_t)(pk >> eb);
+        e[o + j] = (uint32_t)(pk & em);
+    }
+}
+
+struct PredOvf {  // keys of the flagged buckets
+    const unsigned long long *k;
+    const uint8_t *ovf;
+    int hb;
+    __device__ bool operator()(int64_t i) const { return ovf[k[i] & ((1ull << hb) - 1)] != 0; }
+};
+struct EmitShift {
+    const unsigned long long *k;
+    unsigned long long *out;
+    int hb;
+    __device__ void operator()(int64_t i, int64_t r) const { out[r] = k[i] >> hb; }
 };
 
 // Roofline accounting, predicate off: M = postings scanned query-cell by
@@ -1310,13 +1430,14 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     if (n) hipLaunchKernelGGL(k_expand, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, cell_offs, pent);
     unsigned int *bad = (unsigned int *)(stat + 79);
     if (P) hipLaunchKernelGGL(k_check_sorted, dim3(grid_for(P, kBlock)), dim3(kBlock), 0, s, P, pent, cells, bad);
+    stage_check(s, "index build: expand");
     const bool general = P > 0 && fetch(bad, s) != 0;
-    int64_t *e_offs = idx->e_offs.ensure(n + 1);
-    uint64_t *e_cells = idx->e_cells.ensure(P + 1);
+    int64_t *e_offs = idx->e_offs.ensure_exact(n + 1);
+    uint64_t *e_cells = idx->e_cells.ensure_exact(P + 1);
     const uint32_t *mult = nullptr;
     if (!general) {
-        DSS_HIP(hipMemcpyAsync(e_offs, cell_offs, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToDevice, s));
-        if (P) DSS_HIP(hipMemcpyAsync(e_cells, cells, sizeof(uint64_t) * P, hipMemcpyDeviceToDevice, s));
+        device_copy(e_offs, cell_offs, sizeof(int64_t) * (n + 1), s);
+        device_copy(e_cells, cells, sizeof(uint64_t) * P, s);
     } else {  // sort by cell, then stably by entity; unique (entity, cell) runs with multiplicity
         DevBuf<uint64_t> ka, kb;
         DevBuf<uint32_t> va, vb;
@@ -1331,6 +1452,7 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
         if (Pu == 0) DSS_HIP(hipMemsetAsync(e_offs, 0, sizeof(int64_t) * (n + 1), s));
         mult = m;
     }
+    stage_check(s, "index build: entity cells");
     idx->has_mult = general;
     // (2) decodes, per-entity long flags, duration classes, time range
     DevBuf<uint32_t> dec_b;
@@ -1341,6 +1463,7 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     if (n)
         hipLaunchKernelGGL(k_entity_info, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, e_offs, dec, t0, t1, elong,
                            stat, stat + 65);
+    stage_check(s, "index build: entity info");
     unsigned long long h[80];
     DSS_HIP(hipMemcpyAsync(h, stat, sizeof(h), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
@@ -1385,11 +1508,11 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
         int64_t *dtot = (int64_t *)(stat + 78), nirr_p = 0, nu = 0;
         compact_if(Pu, PredIrr{bc}, EmitIrr{e_cells, i0}, tmp_, tmp2_, s, dtot, &nirr_p);
         radix_sort_keys(i0, i1, nirr_p, 64, tmp_, s);
-        uint64_t *irr = idx->irr_cells.ensure(nirr_p + 1);
+        uint64_t *irr = idx->irr_cells.ensure_exact(nirr_p + 1);
         compact_if(nirr_p, PredRunStart64{i1}, EmitCopy64{i1, irr}, tmp_, tmp2_, s, dtot, &nu);
         idx->n_irr = nu;
     } else {
-        idx->irr_cells.ensure(1);
+        idx->irr_cells.ensure_exact(1);
     }
     const int64_t ns = idx->n_slots();
     if (ns >= (int64_t)0x7fffffff) throw Error(DSSG_ERR_INVALID, "index: more than 2^31 - 1 cell slots");
@@ -1408,6 +1531,7 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
         compact_if(Pu, PredPosting{bc}, EmitPostingKey{bc, k0, v0}, tmp_, tmp2_, s, dtot, &NP);
         radix_sort_pairs(k0, k1, v0, pos, NP, 64, tmp_, s);
     }
+    stage_check(s, "index build: posting sort");
     idx->n_p = NP;
     IndexView pv = view_of(idx);  // slots only (postings not built yet)
     DevBuf<uint32_t> key_b, key2_b, pos2_b;
@@ -1420,17 +1544,18 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     pos_b.release();
     tmp_.release();  // the sort's alternate buffers
     // (5) posting attributes in final order
-    uint32_t *b_e = idx->b_e.ensure(NP + 1);
-    uint8_t *b_meta = idx->b_meta.ensure(NP + 1);
-    float2 *b_alt = idx->b_alt.ensure(NP + 1);
-    longlong2 *b_t = idx->b_t.ensure(NP + 1);
-    ulonglong2 *b_sig = idx->b_sig.ensure(2 * (NP + 1));
-    int32_t *b_owner = idx->b_owner.ensure(owner ? NP + 1 : 1);
-    uint32_t *b_mult = idx->b_mult.ensure(mult ? NP + 1 : 1);
+    uint32_t *b_e = idx->b_e.ensure_exact(NP + 1);
+    uint8_t *b_meta = idx->b_meta.ensure_exact(NP + 1);
+    float2 *b_alt = idx->b_alt.ensure_exact(NP + 1);
+    longlong2 *b_t = idx->b_t.ensure_exact(NP + 1);
+    ulonglong2 *b_sig = idx->b_sig.ensure_exact(2 * (NP + 1));
+    int32_t *b_owner = idx->b_owner.ensure_exact(owner ? NP + 1 : 1);
+    uint32_t *b_mult = idx->b_mult.ensure_exact(mult ? NP + 1 : 1);
     if (NP)
         hipLaunchKernelGGL(k_gather, dim3(grid_for(NP, kBlock)), dim3(kBlock), 0, s, NP, pos2, pent, e_offs, dec, elong,
                            alt_lo, alt_hi, t0, t1, owner, mult, b_e, b_meta, b_alt, b_t, b_sig, b_owner, b_mult,
                            stat + 71);
+    stage_check(s, "index build: gather");
     pos2_b.release();
     dec_b.release();
     // (6) slot table: s_post (first posting per slot, scan of counts), s_nreg
@@ -1445,25 +1570,26 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
                                stat + 72);
         DevBuf<int64_t> c_b, o_b;
         int64_t *cnt = c_b.ensure(ns + 1), *off = o_b.ensure(ns + 2);
-        uint32_t *nreg = idx->s_nreg.ensure(ns + 1);
+        uint32_t *nreg = idx->s_nreg.ensure_exact(ns + 1);
         if (ns)
             hipLaunchKernelGGL(k_slot_counts, dim3(grid_for(ns, kBlock)), dim3(kBlock), 0, s, ns, sf, se, sr, cnt, nreg,
                                stat + 74);
         exclusive_scan_i64(cnt, off, ns, tmp2_, s);
-        uint64_t *sp = idx->s_post.ensure(ns + 1);
+        uint64_t *sp = idx->s_post.ensure_exact(ns + 1);
         hipLaunchKernelGGL(k_u64_store, dim3(grid_for(ns + 1, kBlock)), dim3(kBlock), 0, s, ns + 1, off, sp);
     }
+    stage_check(s, "index build: slot table");
     // (7) entity-level attributes: ends_at, owner, owner -> entities, counters
-    int64_t *et1 = idx->e_t1.ensure(n + 1);
-    if (n) DSS_HIP(hipMemcpyAsync(et1, t1, sizeof(int64_t) * n, hipMemcpyDeviceToDevice, s));
-    int64_t *notify = idx->e_notify.ensure(n + 1);
+    int64_t *et1 = idx->e_t1.ensure_exact(n + 1);
+    device_copy(et1, t1, sizeof(int64_t) * n, s);
+    int64_t *notify = idx->e_notify.ensure_exact(n + 1);
     DSS_HIP(hipMemsetAsync(notify, 0, sizeof(int64_t) * (n + 1), s));
     if (owner) {
-        int32_t *eo = idx->e_owner.ensure(n + 1);
-        if (n) DSS_HIP(hipMemcpyAsync(eo, owner, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
+        int32_t *eo = idx->e_owner.ensure_exact(n + 1);
+        device_copy(eo, owner, sizeof(int32_t) * n, s);
         DevBuf<uint32_t> kb, vb;
         uint32_t *k0 = kb.ensure(n + 1), *v0 = vb.ensure(n + 1);
-        uint32_t *ok = idx->o_key.ensure(n + 1), *oe = idx->o_ent.ensure(n + 1);
+        uint32_t *ok = idx->o_key.ensure_exact(n + 1), *oe = idx->o_ent.ensure_exact(n + 1);
         if (n) hipLaunchKernelGGL(k_owner_keys, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, owner, k0, v0);
         radix_sort_pairs(k0, ok, v0, oe, n, 32, tmp_, s);
     }
@@ -1666,15 +1792,46 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             out->n_tagged = 0;
             return;
         }
-        // long x long pairs: split off, sort, unique, append
+        // long x long pairs: split off, group by hash bucket, unique, append
         uint32_t *q2 = oq2_.ensure(n + 1), *e2 = oe2_.ensure(n + 1);
         unsigned long long *k1 = tkey_.ensure(ntag + 1), *k2 = tkey2_.ensure(ntag + 1);
         int64_t *dtot = (int64_t *)(cnt + 9);
-        int64_t nun = 0, nt = 0, nuq = 0;
-        compact_if(n, PredTag{oq, false}, EmitUntagged{oq, oe, q2, e2}, tmp_, tmp2_, s, dtot, &nun);
-        compact_if(n, PredTag{oq, true}, EmitTagKey{oq, oe, k1}, tmp_, tmp2_, s, dtot, &nt);
-        radix_sort_keys(k1, k2, nt, 64, tmp_, s);
-        compact_if(nt, PredRunU64{k2}, EmitPairFromKey{k2, q2, e2, nun}, tmp_, tmp2_, s, dtot, &nuq);
+        int64_t nun = 0, nuq = 0;
+        const int qb = bits_for(nq), eb = bits_for(idx->n_e);
+        int hb = 1;
+        while (hb < 24 && ((int64_t)ntag >> hb) > tag_bucket_avg_) hb++;
+        const bool hashed = tag_bucket_avg_ > 0 && qb + eb + hb <= 64;
+        if (!hashed) hb = 0;
+        split_if(n, PredTag{oq, false}, EmitUntagged{oq, oe, q2, e2}, EmitTagKey{oq, oe, k1, hashed ? eb : 32, hb},
+                 tmp_, tmp2_, s, dtot, &nun);
+        const int64_t nt = n - nun;
+        if (!hashed) {
+            radix_sort_keys(k1, k2, nt, 64, tmp_, s);
+            compact_if(nt, PredRunU64{k2}, EmitPairFromKey{k2, q2, e2, nun, 32}, tmp_, tmp2_, s, dtot, &nuq);
+        } else {
+            radix_sort_keys(k1, k2, nt, hb, tmp_, s);
+            const int64_t nb = (int64_t)1 << hb;
+            int64_t *bs = tb_.ensure(4 * nb + 2), *be = bs + nb, *bc = be + nb, *bo = bc + nb;
+            uint8_t *ovf = tovf_.ensure(nb + 1);
+            DSS_HIP(hipMemsetAsync(bs, 0, 2 * nb * sizeof(int64_t), s));
+            hipLaunchKernelGGL(k_tag_bounds, dim3(grid_for(nt, kBlock)), dim3(kBlock), 0, s, nt, k2, hb, bs, be);
+            hipLaunchKernelGGL(k_tag_dedupe, dim3((unsigned)nb), dim3(kDedupBlock), 0, s, k2, bs, be, hb, k1, bc, ovf,
+                               cnt + 10);
+            exclusive_scan_i64(bc, bo, nb, tmp2_, s);
+            hipLaunchKernelGGL(k_tag_emit, dim3((unsigned)nb), dim3(256), 0, s, k1, bs, bc, bo, eb, q2 + nun, e2 + nun);
+            unsigned long long tail[2];  // distinct pairs of the regular buckets, flagged buckets
+            device_copy(cnt + 11, bo + nb, sizeof(int64_t), s);
+            DSS_HIP(hipMemcpyAsync(tail, cnt + 10, sizeof(tail), hipMemcpyDeviceToHost, s));
+            DSS_HIP(hipStreamSynchronize(s));
+            nuq = (int64_t)tail[1];
+            if (tail[0]) {  // flagged buckets: full sort of their keys
+                int64_t no = 0, nov = 0;
+                compact_if(nt, PredOvf{k2, ovf, hb}, EmitShift{k2, k1, hb}, tmp_, tmp2_, s, dtot, &no);
+                radix_sort_keys(k1, k2, no, 64, tmp_, s);
+                compact_if(no, PredRunU64{k2}, EmitPairFromKey{k2, q2, e2, nun + nuq, eb}, tmp_, tmp2_, s, dtot, &nov);
+                nuq += nov;
+            }
+        }
         out->q = q2;
         out->e = e2;
         out->n = nun + nuq;

@@ -83,6 +83,8 @@ class SearchEngine {
     // Postings of the distinct cells the batch touches, each once.
     int64_t touched(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells, hipStream_t s);
     void set_timing(bool on) { timing_ = on; }
+    // tuning: average tagged pairs per dedupe bucket (<= 0: the full-sort path)
+    void set_tag_bucket_avg(int64_t v) { tag_bucket_avg_ = v; }
     double last_join_kernel_ms() const { return join_ms_; }
     int64_t last_units() const { return units_; }
     int64_t last_keys() const { return keys_; }
@@ -118,10 +120,13 @@ class SearchEngine {
     DevBuf<uint32_t> oq_, oe_, oq2_, oe2_, fills_;
     DevBuf<unsigned long long> work_;
     DevBuf<unsigned long long> tkey_, tkey2_;
+    DevBuf<int64_t> tb_;   // tag buckets: starts, ends, distinct counts, offsets
+    DevBuf<uint8_t> tovf_;  // tag buckets too large for the LDS set
     int n_cu_ = 0;
     int64_t out_rcap_ = 0;  // output slots per region
     int64_t units_cap_hint_ = 0;
     bool timing_ = false;
+    int64_t tag_bucket_avg_ = 1024;
     double join_ms_ = 0;
     int64_t units_ = 0, keys_ = 0, runs_ = 0, iters_ = 0, tests_ = 0;
     int64_t flushes_ = 0, merges_ = 0, merge_lanes_ = 0, tagged_ = 0, long_queries_ = 0, long_postings_ = 0;

@@ -36,6 +36,12 @@ class Footprints:
     def n(self) -> int:
         return len(self.kind)
 
+    def slice(self, a: int, b: int) -> "Footprints":
+        """Footprints [a, b) (vertex offsets rebased to 0)."""
+        v0, v1 = int(self.voff[a]), int(self.voff[b])
+        return Footprints(self.kind[a:b], self.voff[a:b + 1] - v0, self.lat[v0:v1], self.lng[v0:v1],
+                          self.radius_m[a:b])
+
     def subset(self, idx: np.ndarray) -> "Footprints":
         idx = np.asarray(idx)
         counts = self.voff[idx + 1] - self.voff[idx]

@@ -35,3 +35,36 @@ def test_config_parity(oracle, cfg, scale):
     oq, oe = oracle.search(io, ic, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1, None, qo, qc, qa.alt_lo, qa.alt_hi, tlo, thi)
     assert len(oq) > 0
     assert np.array_equal(_keys(gq, ge), _keys(oq, oe))
+
+
+@pytest.fixture(scope="module")
+def corridors_case(oracle):
+    """configs[4] corridors at a scale with ~45k long x long occurrences."""
+    from dss_amd import geo, workload as W
+    _, q, qa, it, ia, now = W.config(4, scale=0.003)
+    ci = geo.cover_batch(it.kind, it.voff, it.lat, it.lng, it.radius_m)
+    cq = geo.cover_batch(q.kind, q.voff, q.lat, q.lng, q.radius_m)
+    tlo, thi = W.query_bounds(qa, now)
+    oq, oe = oracle.search(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1, None, cq.offs, cq.cells, qa.alt_lo,
+                           qa.alt_hi, tlo, thi)
+    return ci, cq, qa, ia, now, _keys(oq, oe)
+
+
+# tag_bucket_avg: 1024 (default buckets), 1 (hb capped by the pair count: tiny
+# buckets), 2^40 (two buckets, each over the LDS set: the full-sort fallback
+# for flagged buckets), 0 (the full-sort path)
+@pytest.mark.parametrize("avg", [1024, 1, 1 << 40, 0])
+def test_long_pair_dedupe_paths(corridors_case, avg):
+    from dss_amd import _lib
+    from dss_amd.store import EntityIndex
+    ci, cq, qa, ia, now, want = corridors_case
+    ctx = _lib.context(0)
+    ctx.set_tuning("tag_bucket_avg", avg)
+    try:
+        idx = EntityIndex(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1)
+        gq, ge = idx.search_operations_batch(cq.offs, cq.cells, qa.alt_lo, qa.alt_hi, qa.t0, qa.t1, now)
+    finally:
+        ctx.set_tuning("tag_bucket_avg", 1024)
+    got = _keys(gq, ge)
+    assert len(got) > 0 and np.all(got[1:] != got[:-1])
+    assert np.array_equal(got, want)

@@ -9,7 +9,7 @@ STEPS=${STEPS:-3}
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/prof/$TAG
 mkdir -p "$OUT"
-B="$R/bench.py --steps $STEPS --warmup 1 --cpu-sample 0 --survey-model 0 --pipelines 1"
+B="$R/bench.py --steps $STEPS --warmup 1 --cpu-sample 0 --survey-model 0 --pipelines 1 $BENCH_ARGS"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT" -o kt --output-format csv -- python3 $B > "$OUT/kt.log" 2>&1
 [ -n "$KT_ONLY" ] || timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT" -o pmc_fetch --output-format csv -- python3 $B > "$OUT/pmc_fetch.log" 2>&1
