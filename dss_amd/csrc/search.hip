@@ -746,6 +746,41 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
     return x;
 }
 
+// 64-bit wave maximum by DPP (no LDS round trips): lanes a step does not
+// feed see the identity (LLONG_MIN).
+template <int ctl, int rmask>
+__device__ __forceinline__ long long dpp_i64(long long x)
+{
+    const int lo = (int)(uint32_t)(unsigned long long)x, hi = (int)(uint32_t)((unsigned long long)x >> 32);
+    const uint32_t l = (uint32_t)__builtin_amdgcn_update_dpp(0, lo, ctl, rmask, 0xf, false);
+    const uint32_t h = (uint32_t)__builtin_amdgcn_update_dpp((int)0x80000000, hi, ctl, rmask, 0xf, false);
+    return (long long)(((unsigned long long)h << 32) | l);
+}
+__device__ __forceinline__ long long wave_max_i64(long long x)
+{
+    x = max(x, dpp_i64<0x111, 0xf>(x));  // row_shr:1
+    x = max(x, dpp_i64<0x112, 0xf>(x));  // row_shr:2
+    x = max(x, dpp_i64<0x114, 0xf>(x));  // row_shr:4
+    x = max(x, dpp_i64<0x118, 0xf>(x));  // row_shr:8
+    x = max(x, dpp_i64<0x142, 0xa>(x));  // row_bcast:15
+    x = max(x, dpp_i64<0x143, 0xc>(x));  // row_bcast:31
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(unsigned long long)x, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((unsigned long long)x >> 32), 63);
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
+// Wave maximum (lane 63 of a DPP max-scan; no LDS round trips).
+__device__ __forceinline__ uint32_t wave_max(uint32_t x)
+{
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));  // row_shr:1
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));  // row_shr:2
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));  // row_shr:4
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));  // row_shr:8
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
 __device__ __forceinline__ uint32_t lb_u32(const uint32_t *x, uint32_t lo, uint32_t hi, uint32_t v)
 {
     while (lo < hi) {  // first index in [lo, hi) with x[i] >= v
@@ -901,48 +936,77 @@ struct OutArgs {
     unsigned long long *counter;   // [0] pairs [1] tagged [2] lane tests [3] broadcasts
 };
 
+__device__ __forceinline__ int uni32(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ unsigned long long uni64(unsigned long long x)
+{
+    return ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
+
+// Per-wave output state, wave-uniform by construction (readfirstlane keeps
+// it in scalar registers: no exec-mask traffic around the chunk test).
 struct WaveOut {
     unsigned long long base = 0;
     int fill = kOutChunk;  // no chunk yet
-    bool have = false;
-    unsigned long long pairs = 0, tagged = 0;
-    // wave-uniform call: every lane of `keep` writes (q, its e)
-    __device__ __forceinline__ void emit(const OutArgs &o, unsigned long long keep, unsigned long long tag, uint32_t q,
-                                         uint32_t e)
+    int have = 0;
+    unsigned long long pairs = 0;  // wave-uniform
+    unsigned long long tagged = 0;  // per lane
+    // wave-uniform call: room for `total` (> 0) pairs.  The batch first fills
+    // what is left of the current chunk, the rest goes to ceil(rest /
+    // kOutChunk) fresh chunks; pair i of the batch lands at at(i).
+    struct Span {
+        unsigned long long a0, a1;  // a0 + i for i < n0, else a1 + i
+        int n0;
+        __device__ __forceinline__ unsigned long long at(unsigned long long i) const
+        {
+            return (i < (unsigned long long)n0 ? a0 : a1) + i;
+        }
+    };
+    __device__ __forceinline__ Span reserve(const OutArgs &o, int total)
     {
-        if (!keep) return;
-        const int c = __popcll(keep);
-        if (fill + c > kOutChunk) {
-            retire(o);
-            const int reg = (int)(blockIdx.x % kRegions);
-            unsigned long long b = 0;
-            if ((threadIdx.x & 63) == 0) b = atomicAdd(&o.octr[reg * kRegStride], (unsigned long long)kOutChunk);
-            b = __shfl(b, 0);
-            have = (int64_t)b + kOutChunk <= o.rcap;  // else the region is full: counted, not written (rerun)
-            base = have ? (unsigned long long)reg * (unsigned long long)o.rcap + b : 0ull;
-            fill = 0;
+        pairs += (unsigned long long)total;
+        Span sp;
+        sp.a0 = base + (unsigned long long)fill;
+        if (fill + total <= kOutChunk) {
+            sp.n0 = total;
+            sp.a1 = sp.a0;
+            fill = uni32(fill + total);
+            return sp;
         }
-        const int lane = threadIdx.x & 63;
-        if (have && ((keep >> lane) & 1ull)) {
-            const unsigned long long pos = base + (unsigned long long)fill + mbcnt64(keep);
-            o.q[pos] = q | (((tag >> lane) & 1ull) ? kTag : 0u);
-            o.e[pos] = e;
-        }
-        fill += c;
-        pairs += (unsigned long long)c;
-        tagged += (unsigned long long)__popcll(tag);
+        sp.n0 = have ? kOutChunk - fill : 0;
+        fill = kOutChunk;  // the current chunk is now full
+        retire(o);
+        const int rest = total - sp.n0;
+        const int nch = (rest + kOutChunk - 1) / kOutChunk;
+        const int reg = (int)(blockIdx.x % kRegions);
+        unsigned long long b = 0;
+        if ((threadIdx.x & 63) == 0)
+            b = atomicAdd(&o.octr[reg * kRegStride], (unsigned long long)nch * (unsigned long long)kOutChunk);
+        b = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 0) << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 0);
+        // else the region is full: counted, not written (rerun)
+        have = uni32((int64_t)b + (int64_t)nch * kOutChunk <= o.rcap);
+        const unsigned long long st = uni64(have ? (unsigned long long)reg * (unsigned long long)o.rcap + b : 0ull);
+        if (have)  // the chunks before the last are full
+            for (int c = threadIdx.x & 63; c < nch - 1; c += 64) o.fills[st / kOutChunk + c] = (uint32_t)kOutChunk;
+        sp.a1 = st - (unsigned long long)sp.n0;
+        base = uni64(st + (unsigned long long)(nch - 1) * kOutChunk);
+        fill = uni32(rest - (nch - 1) * kOutChunk);
+        return sp;
     }
     __device__ __forceinline__ void retire(const OutArgs &o)
     {
         if (have && (threadIdx.x & 63) == 0) o.fills[base / kOutChunk] = (uint32_t)fill;
-        have = false;
+        have = 0;
     }
     __device__ __forceinline__ void finish(const OutArgs &o)
     {
         retire(o);
+        unsigned long long t = tagged;  // per lane: sum over the wave
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
         if ((threadIdx.x & 63) == 0 && pairs) {
             atomicAdd(&o.counter[0], pairs);
-            if (tagged) atomicAdd(&o.counter[1], tagged);
+            if (t) atomicAdd(&o.counter[1], t);
         }
     }
 };
@@ -987,7 +1051,11 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
             const int64_t g = min((int64_t)32, max((int64_t)1, qn / (wpr * 8)));
             unsigned long long ub = 0;
             if (lane == 0) ub = atomicAdd(&work[qreg * kRegStride], (unsigned long long)g);
-            ub = __shfl(ub, 0);
+            // lane 0's grab into scalar registers: the unit loop's exits stay
+            // wave-uniform, so its loop-carried state (output chunk, counters)
+            // stays scalar too
+            ub = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ub >> 32), 0) << 32) |
+                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ub, 0);
             if ((int64_t)ub < qn) {
                 ucur = (int64_t)ub;
                 uend = min((int64_t)ub + g, qn);
@@ -1029,7 +1097,13 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
     int64_t un = next_unit();
     if (un >= 0) prefetch(un);
     while (un >= 0) {
-        const Unit d = dn;
+        Unit d = dn;  // (a uniform load; made explicit for the compiler)
+        d.np = (uint32_t)uni32((int)d.np);
+        d.slot = (uint32_t)uni32((int)d.slot);
+        d.n0 = (uint32_t)uni32((int)d.n0);
+        d.n1 = (uint32_t)uni32((int)d.n1);
+        d.w0 = (uint32_t)uni32((int)d.w0);
+        d.w1 = (uint32_t)uni32((int)d.w1);
         const uint32_t np = d.np & ~kUnitLong;
         // ---- this lane's posting
         const longlong2 pt = nt;
@@ -1044,9 +1118,6 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
         const uint32_t pent = pe & ~kFirstBit;
         const unsigned long long vmask = __ballot(pv);
         if (!vmask) continue;  // (un, the next unit, is already in flight)
-        const unsigned long long fmask = __ballot(pv && (pe & kFirstBit));        // entity's smallest cell
-        const unsigned long long cmask = __ballot(pv && (pmeta & kMetaCompact));  // compact prefix
-        const unsigned long long lmask = LONG ? __ballot(pv && (pmeta & kMetaLongFp)) : 0ull;
         // tile time bounds (a regular tile is sorted by m = min(t0, t1)):
         // records whose window misses every posting are skipped (a long
         // tile: no bound)
@@ -1054,76 +1125,165 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
         if (!(d.np & kUnitLong)) {
             const long long m = tmin2(pt.x, pt.y);
             t0min = readlane64(m, 0);  // <= every t0 of the tile
-            long long t1 = (uint32_t)lane < np ? (pt.x > pt.y ? pt.x : pt.y) : LLONG_MIN;
-            for (int o = 32; o > 0; o >>= 1) t1 = max(t1, __shfl_xor(t1, o));
-            t1max = t1;
+            t1max = wave_max_i64((uint32_t)lane < np ? (pt.x > pt.y ? pt.x : pt.y) : LLONG_MIN);
         }
         const uint32_t ra0 = d.n0, ra1 = d.n1, rb0 = d.w0, rb1 = d.w1;
+        const bool pfirst = (pe & kFirstBit) != 0;                  // entity's smallest cell
+        const bool pcompact = (pmeta & kMetaCompact) != 0;          // compact prefix
+        const bool plong = LONG && (pmeta & kMetaLongFp) != 0;      // long footprint
         for (int part = 0; part < 2; part++) {
             const uint32_t x0 = part ? rb0 : ra0, x1 = part ? rb1 : ra1;
             for (uint32_t base = x0; base < x1; base += 64) {
+                // stage the batch's records whose window meets the tile's time
+                // hull, compacted to slots [0, nrel)
                 const uint32_t r = base + (uint32_t)lane;
                 bool rel = false;
-                __builtin_amdgcn_wave_barrier();
+                int4 h0 = make_int4(0, 0, 0, 0), h1 = h0;
+                ulonglong2 g0 = make_ulonglong2(0, 0), g1 = g0;
                 if (r < x1) {
                     const int4 *r4 = reinterpret_cast<const int4 *>(recs + sval[r]);
-                    const int4 h0 = r4[0], h1 = r4[1];
+                    h0 = r4[0];
+                    h1 = r4[1];
                     const long long tlo = ((long long)h0.y << 32) | (uint32_t)h0.x;
                     const long long thi = ((long long)h0.w << 32) | (uint32_t)h0.z;
-                    const float alo = __int_as_float(h1.x), ahi = __int_as_float(h1.y);
-                    s_rt[w][lane] = make_longlong2(tlo, thi);
-                    s_ra[w][lane] = make_float4(alo, ahi, __int_as_float(h1.z), __int_as_float(h1.w));
-                    s_rs[w][0][lane] = reinterpret_cast<const ulonglong2 *>(r4)[2];
-                    s_rs[w][1][lane] = reinterpret_cast<const ulonglong2 *>(r4)[3];
                     rel = t1max >= tlo && t0min <= thi;
+                    if (rel) {
+                        g0 = reinterpret_cast<const ulonglong2 *>(r4)[2];
+                        g1 = reinterpret_cast<const ulonglong2 *>(r4)[3];
+                    }
+                }
+                const unsigned long long relm = __ballot(rel);
+                const int nrel = uni32(__popcll(relm));
+                if (!nrel) continue;
+                const uint32_t slot = mbcnt64(relm);
+                __builtin_amdgcn_wave_barrier();
+                if (rel) {
+                    s_rt[w][slot] = make_longlong2(((long long)h0.y << 32) | (uint32_t)h0.x,
+                                                   ((long long)h0.w << 32) | (uint32_t)h0.z);
+                    s_ra[w][slot] = make_float4(__int_as_float(h1.x), __int_as_float(h1.y), __int_as_float(h1.z),
+                                                __int_as_float(h1.w));
+                    s_rs[w][0][slot] = g0;
+                    s_rs[w][1][slot] = g1;
                 }
                 __builtin_amdgcn_wave_barrier();
-                unsigned long long todo = __ballot(rel);
-                n_bcast += (unsigned long long)__popcll(todo);
-                n_tests += (unsigned long long)__popcll(todo) * (unsigned long long)__popcll(vmask);
-                while (todo) {
-                    const int j = __builtin_ctzll(todo);
-                    todo &= todo - 1;
+                // record flags by slot, as wave-uniform masks
+                const uint32_t qslot = (lane < nrel) ? (uint32_t)__float_as_int(s_ra[w][lane].z) : 0u;
+                const unsigned long long R0 = __ballot((qslot & kRank0) != 0);
+                const unsigned long long RC = __ballot((qslot & kCompactQ) != 0);
+                const unsigned long long RL = LONG ? __ballot((qslot & kLongQ) != 0) : 0ull;
+                n_bcast += (unsigned long long)nrel;
+                n_tests += (unsigned long long)nrel * (unsigned long long)__popcll(vmask);
+                // (1) this lane's posting against every staged record: a bit per
+                // passing record.  COALESCE'd predicates of operations.go:394-402
+                // (NULL -> sentinels).
+                uint32_t mlo = 0, mhi = 0;
+                const int nlo = nrel < 32 ? nrel : 32;
+#pragma unroll 4
+                for (int j = 0; j < nlo; j++) {
                     const longlong2 rt = s_rt[w][j];
                     const float4 ra = s_ra[w][j];
-                    const uint32_t qv = __builtin_amdgcn_readfirstlane(__float_as_int(ra.z));
-                    // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels)
-                    bool pass = pv && (pt.y >= rt.x) & (pt.x <= rt.y) & (pa.y >= ra.x) & (pa.x <= ra.y);
+                    bool pass = (pt.y >= rt.x) & (pt.x <= rt.y) & (pa.y >= ra.x) & (pa.x <= ra.y);
                     if (OWNER) {
-                        const int32_t own = __builtin_amdgcn_readfirstlane(__float_as_int(ra.w));
-                        if (own >= 0) pass &= pown == own;
+                        const int32_t own = __float_as_int(ra.w);
+                        pass &= (own < 0) | (pown == own);
                     }
-                    const unsigned long long pm = __ballot(pass);
-                    if (!pm) continue;
-                    // smallest shared cell only: a rank-0 record (query's first cell) or a
-                    // posting at its entity's first cell has no smaller cell on one side
-                    unsigned long long keep = pm;
-                    unsigned long long need = (qv & kRank0) ? 0ull : (pm & ~fmask);
-                    const bool ll_r = LONG && (qv & kLongQ);
-                    if (need) {
+                    mlo |= (uint32_t)pass << j;
+                }
+#pragma unroll 4
+                for (int j = 32; j < nrel; j++) {
+                    const longlong2 rt = s_rt[w][j];
+                    const float4 ra = s_ra[w][j];
+                    bool pass = (pt.y >= rt.x) & (pt.x <= rt.y) & (pa.y >= ra.x) & (pa.x <= ra.y);
+                    if (OWNER) {
+                        const int32_t own = __float_as_int(ra.w);
+                        pass &= (own < 0) | (pown == own);
+                    }
+                    mhi |= (uint32_t)pass << (j - 32);
+                }
+                const unsigned long long m = pv ? (((unsigned long long)mhi << 32) | mlo) : 0ull;
+                // (2) smallest shared cell only (SQL DISTINCT, Q13): a rank-0 record
+                // (the query's first cell) or a posting at its entity's first cell
+                // has no smaller cell on one side; otherwise the near-prefix
+                // signatures decide -- overlap: drop; none and either prefix
+                // compact: keep (exact); both footprints long: keep, tagged (the
+                // tagged set is deduplicated after the join); else exact merge.
+                unsigned long long keep = pfirst ? m : (m & R0);
+                unsigned long long need = m & ~keep;
+                // lane-major (each lane walks its own checks) for full batches;
+                // record-major (one broadcast signature per record) for small ones
+                if (nrel > 16) {
+                    while (need) {
+                        const int j = __builtin_ctzll(need);
+                        need &= need - 1;
                         const ulonglong2 c0 = s_rs[w][0][j], c1 = s_rs[w][1][j];
-                        const bool ov =
-                            ((c0.x & ps01.x) | (c0.y & ps01.y) | (c1.x & ps23.x) | (c1.y & ps23.y)) != 0ull;
-                        const unsigned long long ovm = __ballot(ov) & need;
-                        keep &= ~ovm;
-                        need &= ~ovm;
-                        // no overlap: exact when either prefix is compact; both long: tagged
-                        unsigned long long ex = (qv & kCompactQ) ? 0ull : (need & ~cmask & ~(ll_r ? lmask : 0ull));
-                        if (ex) {  // neither prefix compact, not both long: exact merge (rare)
-                            bool drop = false;
-                            if ((ex >> lane) & 1ull) {
-                                const uint32_t q = qv & ~kQFlags;
-                                drop = !no_smaller_shared<2>(ix, pent, cell_of_slot(ix, d.slot), a.qv.cells + a.qv.offs[q],
-                                                             a.qv.offs[q + 1] - a.qv.offs[q]);
-                            }
-                            keep &= ~__ballot(drop);
+                        if (((c0.x & ps01.x) | (c0.y & ps01.y) | (c1.x & ps23.x) | (c1.y & ps23.y)) != 0ull) continue;
+                        bool k = pcompact || ((RC >> j) & 1ull) || (plong && ((RL >> j) & 1ull));
+                        if (!k) {  // neither prefix compact, not both long (rare)
+                            const uint32_t q = (uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags;
+                            k = no_smaller_shared<2>(ix, pent, cell_of_slot(ix, d.slot), a.qv.cells + a.qv.offs[q],
+                                                     a.qv.offs[q + 1] - a.qv.offs[q]);
                         }
+                        if (k) keep |= 1ull << j;
                     }
-                    // long query x long entity: every surviving occurrence is emitted
-                    // tagged (the smallest shared cell always survives) and the tagged
-                    // set is deduplicated after the join
-                    const unsigned long long tag = ll_r ? (keep & lmask) : 0ull;
-                    out.emit(a.out, keep, tag, qv & ~kQFlags, pent);
+                } else {
+                    const unsigned long long cm = __ballot(pcompact), lm = __ballot(plong);
+                    for (int j = 0; j < nrel; j++) {
+                        const unsigned long long nj = __ballot((need >> j) & 1ull);
+                        if (!nj) continue;
+                        const ulonglong2 c0 = s_rs[w][0][j], c1 = s_rs[w][1][j];
+                        const bool ov = ((c0.x & ps01.x) | (c0.y & ps01.y) | (c1.x & ps23.x) | (c1.y & ps23.y)) != 0ull;
+                        const unsigned long long ok = nj & ~__ballot(ov);
+                        unsigned long long kj =
+                            ((RC >> j) & 1ull) ? ok : (ok & (cm | (((RL >> j) & 1ull) ? lm : 0ull)));
+                        const unsigned long long ex = ok & ~kj;
+                        if (ex) {  // neither prefix compact, not both long (rare)
+                            bool k = false;
+                            if ((ex >> lane) & 1ull) {
+                                const uint32_t q = (uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags;
+                                k = no_smaller_shared<2>(ix, pent, cell_of_slot(ix, d.slot), a.qv.cells + a.qv.offs[q],
+                                                         a.qv.offs[q + 1] - a.qv.offs[q]);
+                            }
+                            kj |= __ballot(k);
+                        }
+                        if ((kj >> lane) & 1ull) keep |= 1ull << j;
+                    }
+                }
+                // (3) emission, the batch's pairs contiguous: lane-major (each lane's
+                // pairs after the lanes before it; iterations = the largest lane
+                // count) at low pass density, else record-major (one coalesced row
+                // per record: dense batches would scatter too many lane stores)
+                const uint32_t cnt = (uint32_t)__popcll(keep);
+                const uint32_t incl = wave_incl_scan(cnt);
+                const int total = uni32(__builtin_amdgcn_readlane((int)incl, 63));
+                if (!total) continue;
+                const WaveOut::Span sp = out.reserve(a.out, total);
+                if (LONG && plong) out.tagged += (unsigned long long)__popcll(keep & RL);
+                if (!out.have) continue;
+                if ((int64_t)total * 4 <= (int64_t)nrel * __popcll(vmask)) {  // pass density <= 1/4
+                    unsigned long long i = incl - cnt;
+                    unsigned long long kk = keep;
+                    while (kk) {
+                        const int j = __builtin_ctzll(kk);
+                        kk &= kk - 1;
+                        const uint32_t q = (uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags;
+                        const unsigned long long pos = sp.at(i++);
+                        a.out.q[pos] = q | ((plong && ((RL >> j) & 1ull)) ? kTag : 0u);
+                        a.out.e[pos] = pent;
+                    }
+                } else {
+                    unsigned long long off = 0;
+                    for (int j = 0; j < nrel; j++) {
+                        const unsigned long long kj = __ballot((keep >> j) & 1ull);
+                        if (!kj) continue;
+                        const uint32_t q =
+                            (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s_ra[w][j].z)) & ~kQFlags;
+                        if ((kj >> lane) & 1ull) {
+                            const unsigned long long pos = sp.at(off + mbcnt64(kj));
+                            a.out.q[pos] = q | ((plong && ((RL >> j) & 1ull)) ? kTag : 0u);
+                            a.out.e[pos] = pent;
+                        }
+                        off += (unsigned long long)__popcll(kj);
+                    }
                 }
             }
         }
