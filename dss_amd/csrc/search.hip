@@ -545,46 +545,79 @@ __host__ __device__ __forceinline__ bool is_wide(long long tlo, long long thi)
 // (long_cells) from per-query LDS min/max/face-mask reductions.  One block
 // per 256 queries: their cell offsets go to LDS, the block's cells are then
 // visited coalesced, each finding its query by binary search in LDS.
+// Per query cell: its query, decode and slot (kNoSlot if the cell holds no
+// postings), and its rank among its query's cells with postings (vpre[k] -
+// qvb[q]); per query: the long flag and the count of cells with postings.
+// One block per 256 queries, their cells in kBlock-wide steps.
 __global__ __launch_bounds__(kBlock) void k_cell_query(IndexView a, int64_t nq, const int64_t *offs,
                                                        const uint64_t *cells, uint32_t *cq, uint32_t *dec,
-                                                       uint32_t *cslot, uint8_t *qlong, unsigned long long *nlong)
+                                                       uint32_t *cslot, uint8_t *qlong, uint32_t *vpre,
+                                                       uint32_t *qvb, uint32_t *qvalid, unsigned long long *nlong)
 {
     __shared__ int64_t so[kBlock + 1];
     __shared__ int s_imin[kBlock], s_imax[kBlock], s_jmin[kBlock], s_jmax[kBlock];
     __shared__ uint32_t s_face[kBlock];  // bit f: a cell on face f; bit 8: an undecodable cell
+    __shared__ uint32_t s_cnt[kBlock];   // cells with postings per query
+    __shared__ uint32_t s_wsum[kBlock / 64];
     const int64_t q0 = (int64_t)blockIdx.x * kBlock;
     const int nb = (int)(nq - q0 < (int64_t)kBlock ? nq - q0 : (int64_t)kBlock);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int i = threadIdx.x; i <= nb; i += kBlock) so[i] = offs[q0 + i];
     s_imin[threadIdx.x] = s_jmin[threadIdx.x] = 1 << 30;
     s_imax[threadIdx.x] = s_jmax[threadIdx.x] = -1;
     s_face[threadIdx.x] = 0;
+    s_cnt[threadIdx.x] = 0;
     __syncthreads();
     const int64_t k1 = so[nb];
-    for (int64_t k = so[0] + threadIdx.x; k < k1; k += kBlock) {
-        int lo = 0, hi = nb;  // so[lo] <= k < so[hi]
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (so[mid] <= k) lo = mid;
-            else hi = mid;
+    uint32_t carry = 0;  // cells with postings before this step (block-relative)
+    for (int64_t base = so[0]; base < k1; base += kBlock) {
+        const int64_t k = base + threadIdx.x;
+        bool valid = false;
+        int lo = 0;
+        if (k < k1) {
+            int hi = nb;  // so[lo] <= k < so[hi]
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (so[mid] <= k) lo = mid;
+                else hi = mid;
+            }
+            cq[k] = (uint32_t)(q0 + lo);
+            const uint64_t c = cells[k];
+            const uint32_t d = decode13(c);
+            dec[k] = d;
+            uint32_t sl = kNoSlot;
+            if (find_slot(a, c, sl) && a.s_post[sl + 1] == a.s_post[sl]) sl = kNoSlot;
+            cslot[k] = sl;
+            valid = sl != kNoSlot;
+            if (valid) atomicAdd(&s_cnt[lo], 1u);
+            if (d != kNoDecode) {
+                atomicOr(&s_face[lo], 1u << (d >> 26));
+                atomicMin(&s_imin[lo], (int)((d >> 13) & 8191u));
+                atomicMax(&s_imax[lo], (int)((d >> 13) & 8191u));
+                atomicMin(&s_jmin[lo], (int)(d & 8191u));
+                atomicMax(&s_jmax[lo], (int)(d & 8191u));
+            } else {
+                atomicOr(&s_face[lo], 1u << 8);
+            }
         }
-        cq[k] = (uint32_t)(q0 + lo);
-        const uint64_t c = cells[k];
-        const uint32_t d = decode13(c);
-        dec[k] = d;
-        uint32_t s = kNoSlot;
-        if (find_slot(a, c, s) && a.s_post[s + 1] == a.s_post[s]) s = kNoSlot;
-        cslot[k] = s;
-        if (d != kNoDecode) {
-            atomicOr(&s_face[lo], 1u << (d >> 26));
-            atomicMin(&s_imin[lo], (int)((d >> 13) & 8191u));
-            atomicMax(&s_imax[lo], (int)((d >> 13) & 8191u));
-            atomicMin(&s_jmin[lo], (int)(d & 8191u));
-            atomicMax(&s_jmax[lo], (int)(d & 8191u));
-        } else {
-            atomicOr(&s_face[lo], 1u << 8);
+        // block exclusive scan of the valid flags
+        const unsigned long long m = __ballot(valid);
+        if (lane == 0) s_wsum[wv] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t pre = carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)),
+                 tot = 0;
+#pragma unroll
+        for (int i = 0; i < kBlock / 64; i++) {
+            pre += i < wv ? s_wsum[i] : 0u;
+            tot += s_wsum[i];
         }
+        if (k < k1) {
+            vpre[k] = pre;
+            if (k == so[lo]) qvb[q0 + lo] = pre;
+        }
+        carry += tot;
+        __syncthreads();
     }
-    __syncthreads();
     const int t = threadIdx.x;
     bool is_long = false;
     if (t < nb) {
@@ -593,6 +626,7 @@ __global__ __launch_bounds__(kBlock) void k_cell_query(IndexView a, int64_t nq, 
         is_long = fm != 0 && ((fm >> 8) != 0 || __popc(fm) > 1 || s_imax[t] - s_imin[t] > 7 ||
                               s_jmax[t] - s_jmin[t] > 7);
         qlong[q0 + t] = is_long ? 1 : 0;
+        qvalid[q0 + t] = s_cnt[t];
     }
     wave_count(is_long, nlong);
 }
@@ -634,33 +668,31 @@ __global__ __launch_bounds__(kBlock) void k_qorder(int64_t nq, const int64_t *tl
 }
 
 // Per query (in order rank r): its cells with postings.
-__global__ void k_qcount(int64_t nq, const int64_t *offs, const uint32_t *perm, const uint32_t *cslot, int64_t *cnt)
+__global__ void k_qcount(int64_t nq, const uint32_t *perm, const uint32_t *qvalid, int64_t *cnt, uint32_t *rank)
 {
     const int64_t r = tid64();
     if (r >= nq) return;
     const uint32_t q = perm[r];
-    int64_t c = 0;
-    for (int64_t k = offs[q]; k < offs[q + 1]; k++) c += cslot[k] != kNoSlot;
-    cnt[r] = c;
+    cnt[r] = qvalid[q];
+    rank[q] = (uint32_t)r;
 }
 
-// Per query (in order rank r): one key (slot << 1 | wide) per cell with
-// postings, value = the query cell, written at off[r].
-__global__ void k_qemit(int64_t nq, const int64_t *offs, const uint32_t *perm, const uint32_t *okey,
-                        const uint32_t *cslot, const int64_t *off, uint32_t *key, uint32_t *val)
+// Per query cell with postings: its key (slot << 1 | wide) and value (the
+// query cell) at off[rank of its query] + its rank among the query's cells
+// with postings -- the queries in order, each query's cells in cell order.
+__global__ void k_qemit(int64_t nqc, const uint32_t *cq, const uint32_t *cslot, const uint32_t *vpre,
+                        const uint32_t *qvb, const uint32_t *rank, const uint32_t *okey, const int64_t *off,
+                        uint32_t *key, uint32_t *val)
 {
-    const int64_t r = tid64();
-    if (r >= nq) return;
-    const uint32_t q = perm[r];
+    const int64_t k = tid64();
+    if (k >= nqc) return;
+    const uint32_t s = cslot[k];
+    if (s == kNoSlot) return;
+    const uint32_t q = cq[k], r = rank[q];
     const uint32_t wide = okey[r] == kWideKey ? 1u : 0u;
-    int64_t w = off[r];
-    for (int64_t k = offs[q]; k < offs[q + 1]; k++) {
-        const uint32_t s = cslot[k];
-        if (s == kNoSlot) continue;
-        key[w] = s << 1 | wide;
-        val[w] = (uint32_t)k;
-        w++;
-    }
+    const int64_t w = off[r] + (int64_t)(vpre[k] - qvb[q]);
+    key[w] = s << 1 | wide;
+    val[w] = (uint32_t)k;
 }
 
 // One record per query cell: time window, altitudes, owner, flags and the
@@ -1316,10 +1348,31 @@ __global__ void k_fix_fill(int64_t nch, const uint32_t *fills, int64_t n, const 
     const int64_t c = blockIdx.x;
     const int64_t h = hole[c];
     if (h == 0) return;
-    const int64_t clo = n / kOutChunk;  // chunks holding pairs at or above n start here
+    // the tail chunk of this block's first source, found once (thread 0); each
+    // thread gallops forward from it to its own source's chunk
+    __shared__ int64_t s_lo;
+    if (threadIdx.x == 0) {
+        int64_t lo = n / kOutChunk, hi = nch;  // tail chunk tc with toff[tc] <= t < toff[tc + 1]
+        const int64_t t0 = hoff[c];
+        while (hi - lo > 1) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (toff[mid] <= t0) lo = mid;
+            else hi = mid;
+        }
+        s_lo = lo;
+    }
+    __syncthreads();
+    const int64_t lo0 = s_lo;
     for (int64_t k = threadIdx.x; k < h; k += blockDim.x) {
         const int64_t t = hoff[c] + k;  // its source: the t-th pair at or above n
-        int64_t lo = clo, hi = nch;     // tail chunk tc with toff[tc] <= t < toff[tc + 1]
+        // galloping from the block's first source chunk (runs of empty tail
+        // chunks -- unreserved region space -- are skipped in O(log) steps)
+        int64_t lo = lo0, step = 1;
+        while (lo + step < nch && toff[lo + step] <= t) {
+            lo += step;
+            step <<= 1;
+        }
+        int64_t hi = lo + step < nch ? lo + step : nch;
         while (hi - lo > 1) {
             const int64_t mid = (lo + hi) >> 1;
             if (toff[mid] <= t) lo = mid;
@@ -1832,9 +1885,11 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     DSS_HIP(hipMemsetAsync(ctl, 0, kCtlWords * sizeof(unsigned long long), s));
     // (1) per query cell: query, decode, slot; per query: long flag
     uint32_t *cq = cq_.ensure(nqc + 1), *dec = dec_.ensure(nqc + 1), *cslot = bt_.ensure(nqc + 1);
+    uint32_t *vpre = vpre_.ensure(nqc + 1), *qaux = qaux_.ensure(3 * (nq + 1));
+    uint32_t *qvb = qaux, *qvalid = qaux + (nq + 1), *qrank = qaux + 2 * (nq + 1);
     uint8_t *qlong = qlong_.ensure(nq + 1);
     hipLaunchKernelGGL(k_cell_query, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, ix, nq, q_offs, q_cells, cq, dec,
-                       cslot, qlong, cnt + 5);
+                       cslot, qlong, vpre, qvb, qvalid, cnt + 5);
     // (2) query order: narrow windows by start time, wide ones last
     uint32_t *ok0 = okey_.ensure(nq + 1), *ok1 = okey2_.ensure(nq + 1), *ov0 = oval_.ensure(nq + 1),
              *perm = perm_.ensure(nq + 1);
@@ -1843,12 +1898,12 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     radix_sort_pairs(ok0, ok1, ov0, perm, nq, kOrderBits, tmp_, s);
     // (3) keys (slot << 1 | wide, query cell) in that order; records per cell
     int64_t *qc = qcnt_.ensure(nq + 1), *qo = qoff_.ensure(nq + 2);
-    hipLaunchKernelGGL(k_qcount, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_offs, perm, cslot, qc);
+    hipLaunchKernelGGL(k_qcount, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, perm, qvalid, qc, qrank);
     exclusive_scan_i64(qc, qo, nq, tmp2_, s);
     uint32_t *key = kkey_.ensure(nqc + 1), *skey = kkey2_.ensure(nqc + 1), *val = kval_.ensure(nqc + 1),
              *sval = kval2_.ensure(nqc + 1);
-    hipLaunchKernelGGL(k_qemit, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_offs, perm, ok1, cslot, qo, key,
-                       val);
+    hipLaunchKernelGGL(k_qemit, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, nqc, cq, cslot, vpre, qvb, qrank, ok1,
+                       qo, key, val);
     QRec *recs = (QRec *)rec_.ensure(sizeof(QRec) * (nqc + 1));
     hipLaunchKernelGGL(k_qrecs, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, qv, nqc, cq, dec, qlong, recs);
     // (4) group the keys by cell (stable: each cell's records stay in query

@@ -120,6 +120,7 @@ class SearchEngine {
     DevBuf<uint32_t> oq_, oe_, oq2_, oe2_, fills_;
     DevBuf<unsigned long long> work_;
     DevBuf<unsigned long long> tkey_, tkey2_;
+    DevBuf<uint32_t> vpre_, qaux_;  // query cells: rank among the query's cells with postings; per query aux
     DevBuf<int64_t> tb_;   // tag buckets: starts, ends, distinct counts, offsets
     DevBuf<uint8_t> tovf_;  // tag buckets too large for the LDS set
     int n_cu_ = 0;

@@ -1,0 +1,244 @@
+package gpu
+
+/*
+#include "dssgpu.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"sync"
+	"unsafe"
+
+	"github.com/golang/geo/s2"
+)
+
+// Row is the 4D part of one stored entity (an operation, ISA or
+// subscription): what the CRDB schema keeps in the cells / altitude / time /
+// owner columns (pkg/scd/store/cockroach/store.go:120-147,
+// pkg/rid/cockroach/store.go:122-151).
+type Row struct {
+	Key          string // the entity id
+	Cells        s2.CellUnion
+	AltLo, AltHi float32 // NULL: -Inf / +Inf
+	T0, T1       int64   // unix us; NULL start: math.MinInt64, NULL ends_at: math.MinInt64 (never matches)
+	Owner        string
+}
+
+// Query is one search volume, already folded into the ABI's bounds
+// (e.t1 >= TLo AND e.t0 <= THi AND the altitude overlap AND owner).
+type Query struct {
+	Cells        s2.CellUnion
+	AltLo, AltHi float32
+	TLo, THi     int64
+	Owner        string // "" = any owner
+}
+
+// Mirror is the GPU-resident copy of one table's 4D columns, behind
+// dssg_store (base + delta indexes with tombstones, dssgpu.h).  Writes are
+// serialised by the mirror; searches run concurrently, each on its own
+// context from the pool.
+type Mirror struct {
+	mu        sync.RWMutex
+	st        *C.dssg_store
+	withOwner bool
+	ids       map[string]uint32 // key -> dense id
+	keys      []string          // dense id -> key ("" = free)
+	free      []uint32
+	owners    map[string]int32
+}
+
+// NewMirror creates an empty mirror; withOwner keeps owner ids for
+// owner-filtered searches (RID SearchSubscriptionsByOwner).
+func NewMirror(withOwner bool) (*Mirror, error) {
+	c, err := getCtx()
+	if err != nil {
+		return nil, err
+	}
+	defer putCtx(c)
+	m := &Mirror{withOwner: withOwner, ids: map[string]uint32{}, owners: map[string]int32{}}
+	wo := C.int32_t(0)
+	if withOwner {
+		wo = 1
+	}
+	if rc := C.dssg_store_create(c.c, wo, &m.st); rc != C.DSSG_OK {
+		return nil, c.err("dssg_store_create", rc)
+	}
+	return m, nil
+}
+
+// Close frees the device copy.
+func (m *Mirror) Close() {
+	m.mu.Lock()
+	defer m.mu.Unlock()
+	if m.st != nil {
+		C.dssg_store_free(m.st)
+		m.st = nil
+	}
+}
+
+func (m *Mirror) ownerID(o string) int32 {
+	if o == "" {
+		return -1
+	}
+	id, ok := m.owners[o]
+	if !ok {
+		id = int32(len(m.owners))
+		m.owners[o] = id
+	}
+	return id
+}
+
+// Upsert writes rows (insert or replace by key), as one dssg_store_upsert.
+func (m *Mirror) Upsert(rows []Row) error {
+	if len(rows) == 0 {
+		return nil
+	}
+	m.mu.Lock()
+	defer m.mu.Unlock()
+	c, err := getCtx()
+	if err != nil {
+		return err
+	}
+	defer putCtx(c)
+	n := len(rows)
+	ids := make([]C.uint32_t, n)
+	offs := make([]C.int64_t, n+1)
+	lo, hi := make([]C.float, n), make([]C.float, n)
+	t0, t1 := make([]C.int64_t, n), make([]C.int64_t, n)
+	own := make([]C.int32_t, n)
+	for i, r := range rows {
+		id, ok := m.ids[r.Key]
+		if !ok {
+			if k := len(m.free); k > 0 {
+				id = m.free[k-1]
+				m.free = m.free[:k-1]
+				m.keys[id] = r.Key
+			} else {
+				id = uint32(len(m.keys))
+				m.keys = append(m.keys, r.Key)
+			}
+			m.ids[r.Key] = id
+		}
+		ids[i] = C.uint32_t(id)
+		offs[i+1] = offs[i] + C.int64_t(len(r.Cells))
+		lo[i], hi[i] = C.float(r.AltLo), C.float(r.AltHi)
+		t0[i], t1[i] = C.int64_t(r.T0), C.int64_t(r.T1)
+		own[i] = C.int32_t(m.ownerID(r.Owner))
+	}
+	cells := make([]uint64, int(offs[n])+1)
+	for i, r := range rows {
+		for k, cid := range r.Cells {
+			cells[int(offs[i])+k] = uint64(cid)
+		}
+	}
+	var ownp *C.int32_t
+	if m.withOwner {
+		ownp = &own[0]
+	}
+	if rc := C.dssg_store_upsert(c.c, m.st, C.int64_t(n), &ids[0], &offs[0], (*C.uint64_t)(unsafe.Pointer(&cells[0])),
+		&lo[0], &hi[0], &t0[0], &t1[0], ownp); rc != C.DSSG_OK {
+		return c.err("dssg_store_upsert", rc)
+	}
+	return nil
+}
+
+// Delete removes keys (unknown keys are ignored).
+func (m *Mirror) Delete(keys []string) error {
+	m.mu.Lock()
+	defer m.mu.Unlock()
+	ids := make([]C.uint32_t, 0, len(keys))
+	for _, k := range keys {
+		if id, ok := m.ids[k]; ok {
+			ids = append(ids, C.uint32_t(id))
+			delete(m.ids, k)
+			m.keys[id] = ""
+			m.free = append(m.free, id)
+		}
+	}
+	if len(ids) == 0 {
+		return nil
+	}
+	c, err := getCtx()
+	if err != nil {
+		return err
+	}
+	defer putCtx(c)
+	found := make([]C.int32_t, len(ids))
+	if rc := C.dssg_store_delete(c.c, m.st, C.int64_t(len(ids)), &ids[0], &found[0]); rc != C.DSSG_OK {
+		return c.err("dssg_store_delete", rc)
+	}
+	return nil
+}
+
+// Search runs a batch of queries; result i holds the keys matching query i
+// (each once: the SQL DISTINCT / && semantics), in key-id order.
+func (m *Mirror) Search(qs []Query) ([][]string, error) {
+	out := make([][]string, len(qs))
+	if len(qs) == 0 {
+		return out, nil
+	}
+	m.mu.RLock()
+	defer m.mu.RUnlock()
+	c, err := getCtx()
+	if err != nil {
+		return nil, err
+	}
+	defer putCtx(c)
+	n := len(qs)
+	offs := make([]C.int64_t, n+1)
+	lo, hi := make([]C.float, n), make([]C.float, n)
+	tlo, thi := make([]C.int64_t, n), make([]C.int64_t, n)
+	own := make([]C.int32_t, n)
+	for i, q := range qs {
+		offs[i+1] = offs[i] + C.int64_t(len(q.Cells))
+		lo[i], hi[i] = C.float(q.AltLo), C.float(q.AltHi)
+		tlo[i], thi[i] = C.int64_t(q.TLo), C.int64_t(q.THi)
+		own[i] = -1
+		if q.Owner != "" {
+			id, ok := m.owners[q.Owner]
+			if !ok {
+				id = -2 // an owner with no rows matches nothing
+			}
+			own[i] = C.int32_t(id)
+		}
+	}
+	cells := make([]uint64, int(offs[n])+1)
+	for i, q := range qs {
+		for k, cid := range q.Cells {
+			cells[int(offs[i])+k] = uint64(cid)
+		}
+	}
+	var ownp *C.int32_t
+	if m.withOwner {
+		ownp = &own[0]
+	}
+	pq, pe := make([]uint32, 1024), make([]uint32, 1024)
+	for {
+		var needed C.int64_t
+		rc := C.dssg_store_search(c.c, m.st, C.int64_t(n), &offs[0], (*C.uint64_t)(unsafe.Pointer(&cells[0])), &lo[0],
+			&hi[0], &tlo[0], &thi[0], ownp, (*C.uint32_t)(unsafe.Pointer(&pq[0])),
+			(*C.uint32_t)(unsafe.Pointer(&pe[0])), C.int64_t(len(pq)), &needed)
+		if rc == C.DSSG_ERR_CAPACITY {
+			pq, pe = make([]uint32, int(needed)+1), make([]uint32, int(needed)+1)
+			continue
+		}
+		if rc != C.DSSG_OK {
+			return nil, c.err("dssg_store_search", rc)
+		}
+		for k := 0; k < int(needed); k++ {
+			if int(pe[k]) >= len(m.keys) || m.keys[pe[k]] == "" {
+				return nil, fmt.Errorf("dssg_store_search: id %d not live", pe[k])
+			}
+			out[pq[k]] = append(out[pq[k]], m.keys[pe[k]])
+		}
+		return out, nil
+	}
+}
+
+// Len is the number of live rows.
+func (m *Mirror) Len() int {
+	m.mu.RLock()
+	defer m.mu.RUnlock()
+	return len(m.ids)
+}
