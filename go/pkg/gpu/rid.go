@@ -1,0 +1,332 @@
+package gpu
+
+import (
+	"context"
+	"sync"
+	"time"
+
+	"github.com/golang/geo/s2"
+	dsserr "github.com/interuss/dss/pkg/errors"
+	dssmodels "github.com/interuss/dss/pkg/models"
+	ridmodels "github.com/interuss/dss/pkg/rid/models"
+	"github.com/interuss/dss/pkg/rid/repos"
+)
+
+// RIDTransactor decorates the reference's CockroachDB repos.Transactor
+// (pkg/rid/cockroach/store.go): writes and point reads go to CRDB, while
+// SearchISAs, SearchSubscriptions and SearchSubscriptionsByOwner run on GPU
+// mirrors of the identification_service_areas / subscriptions tables'
+// cells, time and owner columns.  Writes made inside InTxnRetrier reach the
+// mirrors once the transaction has committed; inside it, searches go to CRDB
+// so a transaction sees its own writes.
+type RIDTransactor struct {
+	repos.Transactor
+	// Now is the store clock (cockroach.DefaultClock in the reference).
+	Now func() time.Time
+
+	isas, subs *Mirror
+	mu         sync.RWMutex
+	isaRows    map[dssmodels.ID]*ridmodels.IdentificationServiceArea
+	subRows    map[dssmodels.ID]*ridmodels.Subscription
+}
+
+// NewRIDTransactor builds the mirrors from the tables' current rows.
+func NewRIDTransactor(inner repos.Transactor, isas []*ridmodels.IdentificationServiceArea, subs []*ridmodels.Subscription) (*RIDTransactor, error) {
+	t := &RIDTransactor{Transactor: inner, Now: time.Now,
+		isaRows: map[dssmodels.ID]*ridmodels.IdentificationServiceArea{}, subRows: map[dssmodels.ID]*ridmodels.Subscription{}}
+	var err error
+	if t.isas, err = NewMirror(false); err != nil {
+		return nil, err
+	}
+	if t.subs, err = NewMirror(true); err != nil {
+		return nil, err
+	}
+	w := newRIDWrites()
+	for _, i := range isas {
+		w.isas[i.ID] = i
+	}
+	for _, s := range subs {
+		w.subs[s.ID] = s
+	}
+	if err := t.apply(w); err != nil {
+		return nil, err
+	}
+	return t, nil
+}
+
+// RID rows have no altitude filter in any search (identification_service_area.go:166-197).
+func isaRow(i *ridmodels.IdentificationServiceArea) Row {
+	return Row{Key: i.ID.String(), Cells: i.Cells, AltLo: negInf, AltHi: posInf,
+		T0: usOrNull(i.StartTime, timeNullStart), T1: usOrNull(i.EndTime, timeNullStored), Owner: i.Owner.String()}
+}
+
+func ridSubRow(s *ridmodels.Subscription) Row {
+	return Row{Key: s.ID.String(), Cells: s.Cells, AltLo: negInf, AltHi: posInf,
+		T0: usOrNull(s.StartTime, timeNullStart), T1: usOrNull(s.EndTime, timeNullStored), Owner: s.Owner.String()}
+}
+
+// ridWrites is a set of committed row changes (nil value: deleted).
+type ridWrites struct {
+	isas map[dssmodels.ID]*ridmodels.IdentificationServiceArea
+	subs map[dssmodels.ID]*ridmodels.Subscription
+}
+
+func newRIDWrites() *ridWrites {
+	return &ridWrites{isas: map[dssmodels.ID]*ridmodels.IdentificationServiceArea{},
+		subs: map[dssmodels.ID]*ridmodels.Subscription{}}
+}
+
+func (t *RIDTransactor) apply(w *ridWrites) error {
+	t.mu.Lock()
+	defer t.mu.Unlock()
+	var rows []Row
+	var dels []string
+	for id, i := range w.isas {
+		if i == nil {
+			dels = append(dels, id.String())
+			delete(t.isaRows, id)
+		} else {
+			rows = append(rows, isaRow(i))
+			t.isaRows[id] = i
+		}
+	}
+	if err := t.isas.Upsert(rows); err != nil {
+		return err
+	}
+	if err := t.isas.Delete(dels); err != nil {
+		return err
+	}
+	rows, dels = rows[:0], dels[:0]
+	for id, s := range w.subs {
+		if s == nil {
+			dels = append(dels, id.String())
+			delete(t.subRows, id)
+		} else {
+			rows = append(rows, ridSubRow(s))
+			t.subRows[id] = s
+		}
+	}
+	if err := t.subs.Upsert(rows); err != nil {
+		return err
+	}
+	return t.subs.Delete(dels)
+}
+
+// InTxnRetrier runs f on a recording repo; the last attempt's writes are
+// mirrored once the inner retrier reports the transaction committed.
+func (t *RIDTransactor) InTxnRetrier(ctx context.Context, f func(repo repos.Repository) error) error {
+	var w *ridWrites
+	err := t.Transactor.InTxnRetrier(ctx, func(repo repos.Repository) error {
+		w = newRIDWrites() // a retried attempt starts over
+		return f(&ridRepo{Repository: repo, w: w})
+	})
+	if err != nil || w == nil {
+		return err
+	}
+	return t.apply(w)
+}
+
+// ---- the transactor's own (autocommit) repository methods ---------------
+
+func (t *RIDTransactor) InsertISA(ctx context.Context, isa *ridmodels.IdentificationServiceArea) (*ridmodels.IdentificationServiceArea, error) {
+	res, err := t.Transactor.InsertISA(ctx, isa)
+	if err == nil && res != nil {
+		w := newRIDWrites()
+		w.isas[res.ID] = res
+		err = t.apply(w)
+	}
+	return res, err
+}
+
+func (t *RIDTransactor) UpdateISA(ctx context.Context, isa *ridmodels.IdentificationServiceArea) (*ridmodels.IdentificationServiceArea, error) {
+	res, err := t.Transactor.UpdateISA(ctx, isa)
+	if err == nil && res != nil {
+		w := newRIDWrites()
+		w.isas[res.ID] = res
+		err = t.apply(w)
+	}
+	return res, err
+}
+
+func (t *RIDTransactor) DeleteISA(ctx context.Context, isa *ridmodels.IdentificationServiceArea) (*ridmodels.IdentificationServiceArea, error) {
+	res, err := t.Transactor.DeleteISA(ctx, isa)
+	if err == nil {
+		w := newRIDWrites()
+		w.isas[isa.ID] = nil
+		err = t.apply(w)
+	}
+	return res, err
+}
+
+func (t *RIDTransactor) InsertSubscription(ctx context.Context, sub *ridmodels.Subscription) (*ridmodels.Subscription, error) {
+	res, err := t.Transactor.InsertSubscription(ctx, sub)
+	if err == nil && res != nil {
+		w := newRIDWrites()
+		w.subs[res.ID] = res
+		err = t.apply(w)
+	}
+	return res, err
+}
+
+func (t *RIDTransactor) UpdateSubscription(ctx context.Context, sub *ridmodels.Subscription) (*ridmodels.Subscription, error) {
+	res, err := t.Transactor.UpdateSubscription(ctx, sub)
+	if err == nil && res != nil {
+		w := newRIDWrites()
+		w.subs[res.ID] = res
+		err = t.apply(w)
+	}
+	return res, err
+}
+
+func (t *RIDTransactor) DeleteSubscription(ctx context.Context, sub *ridmodels.Subscription) (*ridmodels.Subscription, error) {
+	res, err := t.Transactor.DeleteSubscription(ctx, sub)
+	if err == nil {
+		w := newRIDWrites()
+		w.subs[sub.ID] = nil
+		err = t.apply(w)
+	}
+	return res, err
+}
+
+// UpdateNotificationIdxsInCells stays on CRDB (it is an UPDATE ... RETURNING
+// of the rows' counters); the returned rows refresh the cache.
+func (t *RIDTransactor) UpdateNotificationIdxsInCells(ctx context.Context, cells s2.CellUnion) ([]*ridmodels.Subscription, error) {
+	res, err := t.Transactor.UpdateNotificationIdxsInCells(ctx, cells)
+	if err == nil && len(res) > 0 {
+		w := newRIDWrites()
+		for _, s := range res {
+			w.subs[s.ID] = s
+		}
+		err = t.apply(w)
+	}
+	return res, err
+}
+
+// SearchISAs replaces (*ISAStore).SearchISAs
+// (pkg/rid/cockroach/identification_service_area.go:166-197):
+//   ends_at >= earliest AND COALESCE(starts_at <= latest, true) AND cells && cells.
+func (t *RIDTransactor) SearchISAs(ctx context.Context, cells s2.CellUnion, earliest *time.Time, latest *time.Time) ([]*ridmodels.IdentificationServiceArea, error) {
+	if len(cells) == 0 {
+		return nil, dsserr.BadRequest("missing cell IDs for query")
+	}
+	if earliest == nil {
+		return nil, dsserr.Internal("must call with an earliest start time.")
+	}
+	q := Query{Cells: cells, AltLo: negInf, AltHi: posInf, TLo: earliest.UnixNano() / 1000,
+		THi: usOrNull(latest, timeNullEndQ)}
+	keys, err := t.isas.Search([]Query{q})
+	if err != nil {
+		return nil, err
+	}
+	t.mu.RLock()
+	defer t.mu.RUnlock()
+	out := make([]*ridmodels.IdentificationServiceArea, 0, len(keys[0]))
+	for _, k := range keys[0] {
+		if i, ok := t.isaRows[dssmodels.ID(k)]; ok {
+			c := *i
+			out = append(out, &c)
+		}
+	}
+	return out, nil
+}
+
+func (t *RIDTransactor) searchSubs(cells s2.CellUnion, owner string) ([]*ridmodels.Subscription, error) {
+	if len(cells) == 0 {
+		return nil, dsserr.BadRequest("no location provided")
+	}
+	q := Query{Cells: cells, AltLo: negInf, AltHi: posInf, TLo: t.Now().UnixNano() / 1000, THi: timeNullEndQ,
+		Owner: owner}
+	keys, err := t.subs.Search([]Query{q})
+	if err != nil {
+		return nil, err
+	}
+	t.mu.RLock()
+	defer t.mu.RUnlock()
+	out := make([]*ridmodels.Subscription, 0, len(keys[0]))
+	for _, k := range keys[0] {
+		if s, ok := t.subRows[dssmodels.ID(k)]; ok {
+			c := *s
+			out = append(out, &c)
+		}
+	}
+	return out, nil
+}
+
+// SearchSubscriptions replaces (*SubscriptionStore).SearchSubscriptions
+// (pkg/rid/cockroach/subscriptions.go:222-244): cells && cells AND ends_at >= now.
+func (t *RIDTransactor) SearchSubscriptions(ctx context.Context, cells s2.CellUnion) ([]*ridmodels.Subscription, error) {
+	return t.searchSubs(cells, "")
+}
+
+// SearchSubscriptionsByOwner replaces (*SubscriptionStore).SearchSubscriptionsByOwner
+// (pkg/rid/cockroach/subscriptions.go:247-273): the same AND owner = $owner.
+func (t *RIDTransactor) SearchSubscriptionsByOwner(ctx context.Context, cells s2.CellUnion, owner dssmodels.Owner) ([]*ridmodels.Subscription, error) {
+	return t.searchSubs(cells, owner.String())
+}
+
+// ridRepo is the repository InTxnRetrier hands to f: CRDB in the
+// transaction, with writes recorded for the mirrors.
+type ridRepo struct {
+	repos.Repository
+	w *ridWrites
+}
+
+func (r *ridRepo) dirty() bool { return len(r.w.isas) > 0 || len(r.w.subs) > 0 }
+
+func (r *ridRepo) InsertISA(ctx context.Context, isa *ridmodels.IdentificationServiceArea) (*ridmodels.IdentificationServiceArea, error) {
+	res, err := r.Repository.InsertISA(ctx, isa)
+	if err == nil && res != nil {
+		r.w.isas[res.ID] = res
+	}
+	return res, err
+}
+
+func (r *ridRepo) UpdateISA(ctx context.Context, isa *ridmodels.IdentificationServiceArea) (*ridmodels.IdentificationServiceArea, error) {
+	res, err := r.Repository.UpdateISA(ctx, isa)
+	if err == nil && res != nil {
+		r.w.isas[res.ID] = res
+	}
+	return res, err
+}
+
+func (r *ridRepo) DeleteISA(ctx context.Context, isa *ridmodels.IdentificationServiceArea) (*ridmodels.IdentificationServiceArea, error) {
+	res, err := r.Repository.DeleteISA(ctx, isa)
+	if err == nil {
+		r.w.isas[isa.ID] = nil
+	}
+	return res, err
+}
+
+func (r *ridRepo) InsertSubscription(ctx context.Context, sub *ridmodels.Subscription) (*ridmodels.Subscription, error) {
+	res, err := r.Repository.InsertSubscription(ctx, sub)
+	if err == nil && res != nil {
+		r.w.subs[res.ID] = res
+	}
+	return res, err
+}
+
+func (r *ridRepo) UpdateSubscription(ctx context.Context, sub *ridmodels.Subscription) (*ridmodels.Subscription, error) {
+	res, err := r.Repository.UpdateSubscription(ctx, sub)
+	if err == nil && res != nil {
+		r.w.subs[res.ID] = res
+	}
+	return res, err
+}
+
+func (r *ridRepo) DeleteSubscription(ctx context.Context, sub *ridmodels.Subscription) (*ridmodels.Subscription, error) {
+	res, err := r.Repository.DeleteSubscription(ctx, sub)
+	if err == nil {
+		r.w.subs[sub.ID] = nil
+	}
+	return res, err
+}
+
+func (r *ridRepo) UpdateNotificationIdxsInCells(ctx context.Context, cells s2.CellUnion) ([]*ridmodels.Subscription, error) {
+	res, err := r.Repository.UpdateNotificationIdxsInCells(ctx, cells)
+	if err == nil {
+		for _, s := range res {
+			r.w.subs[s.ID] = s
+		}
+	}
+	return res, err
+}
