@@ -55,6 +55,7 @@ class Pairs(C.Structure):
 
 MAX_PARTS = 64
 ROUTE_ROW_BYTES = 32
+COMM_ID_BYTES = 128
 
 
 class Volumes(C.Structure):
@@ -158,6 +159,12 @@ def load():
         L.dssg_index_info.argtypes = [vp, P(i64), P(i64), P(i64), P(i64), P(i64), P(i64)]
         L.dssg_copy_to_host.argtypes = [vp, vp, vp, C.c_size_t]
         L.dssg_copy_device.argtypes = [vp, vp, vp, C.c_size_t, vp]
+        L.dssg_comm_unique_id.argtypes = [vp]
+        L.dssg_comm_init.argtypes = [vp, C.c_int32, C.c_int32, vp, P(vp)]
+        L.dssg_comm_free.argtypes = [vp]
+        L.dssg_comm_free.restype = None
+        L.dssg_comm_alltoallv_device.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.dssg_sharded_search_device.argtypes = [vp, vp, vp, vp, C.c_int64, vp, vp, vp, vp, vp, vp, vp, P(Pairs)]
         L.dssg_radix_sort_device.argtypes = [vp, C.c_int, i64, C.c_int, vp, vp, vp, vp, vp, P(d)]
         L.dssg_selftest_scan.argtypes = [vp, i64, C.c_int, P(i64), P(i64)]
         L.dssg_selftest_math.argtypes = [vp, C.c_int, i64, P(d), P(d), P(d)]

@@ -1,5 +1,7 @@
 // C ABI (include/dssgpu.h) over the gfx950 covering and search engines.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: the library is opened at dssg_comm_init (dlopen, RTLD_LOCAL)
 
 #include <algorithm>
 #include <cctype>
@@ -7,7 +9,9 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "common.hpp"
@@ -914,3 +918,243 @@ int dssg_selftest_scan(dssg_ctx *ctx, int64_t n, int shift, const int64_t *in, i
 }
 
 }  // extern "C"
+
+/* ======================================================================
+ * Native multi-GPU exchange over RCCL (the range partition
+ * of scd_cells_operations, pkg/scd/store/cockroach/store.go:140-147).
+ * RCCL is opened with dlopen(RTLD_LOCAL) on first use, so the library loads
+ * without it and never shares symbols with another RCCL in the process
+ * (PyTorch bundles its own).
+ * ====================================================================== */
+namespace {
+
+struct Rccl {
+    bool tried = false, ok = false;
+    std::string err;
+    decltype(&ncclGetUniqueId) getUniqueId = nullptr;
+    decltype(&ncclCommInitRank) commInitRank = nullptr;
+    decltype(&ncclCommDestroy) commDestroy = nullptr;
+    decltype(&ncclAllGather) allGather = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) groupStart = nullptr;
+    decltype(&ncclGroupEnd) groupEnd = nullptr;
+    decltype(&ncclGetErrorString) errorString = nullptr;
+};
+
+Rccl &rccl()
+{
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *h = nullptr;
+        for (const char *name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"}) {
+            h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+            if (h) break;
+        }
+        if (!h) {
+            const char *e = dlerror();
+            r.err = std::string("cannot open librccl: ") + (e ? e : "?");
+            return;
+        }
+        bool all = true;
+        auto sym = [&](auto &fn, const char *name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+            if (!fn) all = false;
+        };
+        sym(r.getUniqueId, "ncclGetUniqueId");
+        sym(r.commInitRank, "ncclCommInitRank");
+        sym(r.commDestroy, "ncclCommDestroy");
+        sym(r.allGather, "ncclAllGather");
+        sym(r.send, "ncclSend");
+        sym(r.recv, "ncclRecv");
+        sym(r.groupStart, "ncclGroupStart");
+        sym(r.groupEnd, "ncclGroupEnd");
+        sym(r.errorString, "ncclGetErrorString");
+        r.ok = all;
+        if (!all) r.err = "librccl lacks an expected symbol";
+    });
+    return r;
+}
+
+void nccl_check(ncclResult_t rc, const char *what)
+{
+    if (rc != ncclSuccess)
+        throw dss::Error(DSSG_ERR_DEVICE, std::string(what) + ": " + rccl().errorString(rc));
+}
+
+}  // namespace
+
+struct dssg_comm {
+    ncclComm_t comm = nullptr;
+    int nranks = 0, rank = 0, device = 0;
+    dss::DevBuf<int64_t> d_counts;                 // allgathered count vectors
+    dss::DevBuf<unsigned char> send_rows, recv_rows, recv_cells_b;
+    dss::DevBuf<uint64_t> send_cells, send_pairs, recv_pairs;
+    dss::DevBuf<uint32_t> out_q, out_e;
+};
+
+namespace {
+
+// Every rank's k-vector of int64 counts -> counts[s * k + j] = rank s's j-th (host).
+void allgather_counts(dssg_comm *c, const int64_t *mine, int k, std::vector<int64_t> &all, hipStream_t s)
+{
+    int64_t *d = c->d_counts.ensure((size_t)k * (c->nranks + 1));
+    DSS_HIP(hipMemcpyAsync(d + (size_t)k * c->nranks, mine, sizeof(int64_t) * k, hipMemcpyHostToDevice, s));
+    nccl_check(rccl().allGather(d + (size_t)k * c->nranks, d, (size_t)k * sizeof(int64_t), ncclChar, c->comm, s),
+               "ncclAllGather");
+    all.resize((size_t)k * c->nranks);
+    DSS_HIP(hipMemcpyAsync(all.data(), d, sizeof(int64_t) * all.size(), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+}
+
+// Grouped point-to-point all-to-all of byte blocks (part-major buffers).
+void alltoallv(dssg_comm *c, const void *send, const int64_t *sbytes, void *recv, const int64_t *rbytes, hipStream_t s)
+{
+    Rccl &r = rccl();
+    nccl_check(r.groupStart(), "ncclGroupStart");
+    int64_t so = 0, ro = 0;
+    for (int p = 0; p < c->nranks; p++) {
+        if (sbytes[p] > 0)
+            nccl_check(r.send((const char *)send + so, (size_t)sbytes[p], ncclChar, p, c->comm, s), "ncclSend");
+        if (rbytes[p] > 0)
+            nccl_check(r.recv((char *)recv + ro, (size_t)rbytes[p], ncclChar, p, c->comm, s), "ncclRecv");
+        so += sbytes[p];
+        ro += rbytes[p];
+    }
+    nccl_check(r.groupEnd(), "ncclGroupEnd");
+}
+
+}  // namespace
+
+int dssg_comm_unique_id(uint8_t *id)
+{
+    if (!id) return DSSG_ERR_INVALID;
+    Rccl &r = rccl();
+    if (!r.ok) return DSSG_ERR_DEVICE;
+    ncclUniqueId u;
+    if (r.getUniqueId(&u) != ncclSuccess) return DSSG_ERR_DEVICE;
+    static_assert(sizeof(u) == DSSG_COMM_ID_BYTES, "ncclUniqueId size");
+    std::memcpy(id, &u, sizeof(u));
+    return DSSG_OK;
+}
+
+int dssg_comm_init(dssg_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t *id, dssg_comm **out)
+{
+    if (!ctx || !id || !out || nranks < 1 || nranks > DSSG_MAX_PARTS || rank < 0 || rank >= nranks)
+        return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        Rccl &r = rccl();
+        if (!r.ok) throw dss::Error(DSSG_ERR_DEVICE, r.err);
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof(u));
+        auto *c = new dssg_comm();
+        c->nranks = nranks;
+        c->rank = rank;
+        c->device = ctx->device;
+        const ncclResult_t rc = r.commInitRank(&c->comm, nranks, u, rank);
+        if (rc != ncclSuccess) {
+            delete c;
+            nccl_check(rc, "ncclCommInitRank");
+        }
+        *out = c;
+    });
+}
+
+void dssg_comm_free(dssg_comm *comm)
+{
+    if (!comm) return;
+    (void)hipSetDevice(comm->device);
+    if (comm->comm) rccl().commDestroy(comm->comm);
+    delete comm;
+}
+
+int dssg_comm_alltoallv_device(dssg_ctx *ctx, dssg_comm *comm, const void *d_send, const int64_t *send_bytes,
+                               void *d_recv, const int64_t *recv_bytes, void *stream)
+{
+    if (!ctx || !comm || !send_bytes || !recv_bytes) return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        alltoallv(comm, d_send, send_bytes, d_recv, recv_bytes, s);
+    });
+}
+
+int dssg_sharded_search_device(dssg_ctx *ctx, dssg_comm *comm, const dssg_index *shard, const uint64_t *d_part_hi,
+                               int64_t nq, const int64_t *d_q_offs, const uint64_t *d_q_cells,
+                               const float *d_q_alt_lo, const float *d_q_alt_hi, const int64_t *d_q_tlo,
+                               const int64_t *d_q_thi, void *stream, dssg_pairs *out)
+{
+    if (!ctx || !comm || !shard || !d_part_hi || !out || nq < 0 ||
+        (nq > 0 && (!d_q_offs || !d_q_cells || !d_q_alt_lo || !d_q_alt_hi || !d_q_tlo || !d_q_thi)))
+        return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        const int W = comm->nranks, me = comm->rank;
+        // (1) route this rank's queries to the shards owning their cells
+        int64_t rows_n[DSSG_MAX_PARTS], cells_n[DSSG_MAX_PARTS];
+        ctx->route.plan(nq, d_q_offs, d_q_cells, W, d_part_hi, s, rows_n, cells_n);
+        int64_t nrow = 0, ncell = 0;
+        for (int p = 0; p < W; p++) {
+            nrow += rows_n[p];
+            ncell += cells_n[p];
+        }
+        unsigned char *srows = comm->send_rows.ensure((size_t)nrow * DSSG_ROUTE_ROW_BYTES + 1);
+        uint64_t *scells = comm->send_cells.ensure((size_t)ncell + 1);
+        ctx->route.fill(nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo, d_q_thi, s, srows, scells);
+        // (2) exchange the query rows and their cell lists
+        std::vector<int64_t> cnt;
+        int64_t mine[2 * DSSG_MAX_PARTS];
+        for (int p = 0; p < W; p++) {
+            mine[p] = rows_n[p];
+            mine[W + p] = cells_n[p];
+        }
+        allgather_counts(comm, mine, 2 * W, cnt, s);
+        int64_t sb[DSSG_MAX_PARTS], rb[DSSG_MAX_PARTS], src_rows[DSSG_MAX_PARTS], rrow = 0, rcell = 0;
+        for (int p = 0; p < W; p++) {
+            src_rows[p] = cnt[(size_t)p * 2 * W + me];
+            rrow += src_rows[p];
+            rcell += cnt[(size_t)p * 2 * W + W + me];
+        }
+        unsigned char *rrows = comm->recv_rows.ensure((size_t)rrow * DSSG_ROUTE_ROW_BYTES + 1);
+        uint64_t *rcells = (uint64_t *)comm->recv_cells_b.ensure(sizeof(uint64_t) * ((size_t)rcell + 1));
+        for (int p = 0; p < W; p++) {
+            sb[p] = rows_n[p] * DSSG_ROUTE_ROW_BYTES;
+            rb[p] = src_rows[p] * DSSG_ROUTE_ROW_BYTES;
+        }
+        alltoallv(comm, srows, sb, rrows, rb, s);
+        for (int p = 0; p < W; p++) {
+            sb[p] = cells_n[p] * (int64_t)sizeof(uint64_t);
+            rb[p] = cnt[(size_t)p * 2 * W + W + me] * (int64_t)sizeof(uint64_t);
+        }
+        alltoallv(comm, scells, sb, rcells, rb, s);
+        // (3) the received queries against this rank's shard
+        dssg_batch batch{};
+        ctx->route.unpack(rrow, rrows, rcells, W, src_rows, s, &batch);
+        dssg_pairs pairs{};
+        ctx->search.search(shard, batch.n, batch.offs, batch.cells, batch.alt_lo, batch.alt_hi, batch.tlo, batch.thi,
+                           nullptr, s, &pairs);
+        // (4) pairs back to their queries' home ranks
+        int64_t pn[DSSG_MAX_PARTS];
+        ctx->route.pairs_plan(&batch, &pairs, W, s, pn);
+        int64_t npair = 0;
+        for (int p = 0; p < W; p++) npair += pn[p];
+        uint64_t *spairs = comm->send_pairs.ensure((size_t)npair + 1);
+        ctx->route.pairs_fill(&batch, &pairs, s, spairs);
+        allgather_counts(comm, pn, W, cnt, s);
+        int64_t rpair = 0;
+        for (int p = 0; p < W; p++) {
+            sb[p] = pn[p] * (int64_t)sizeof(uint64_t);
+            rb[p] = cnt[(size_t)p * W + me] * (int64_t)sizeof(uint64_t);
+            rpair += cnt[(size_t)p * W + me];
+        }
+        uint64_t *rpairs = comm->recv_pairs.ensure((size_t)rpair + 1);
+        alltoallv(comm, spairs, sb, rpairs, rb, s);
+        uint32_t *q = comm->out_q.ensure((size_t)rpair + 1), *e = comm->out_e.ensure((size_t)rpair + 1);
+        dss::RouteEngine::split_pairs(rpair, rpairs, q, e, s);
+        DSS_HIP(hipStreamSynchronize(s));
+        out->q = q;
+        out->e = e;
+        out->n = rpair;
+        out->n_tagged = 0;
+    });
+}

@@ -26,6 +26,8 @@
 // are unordered, quirk Q13).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "route.hpp"
 
 namespace dss {
@@ -298,6 +300,26 @@ void RouteEngine::pairs_fill(const dssg_batch *b, const dssg_pairs *p, hipStream
         hipLaunchKernelGGL(k_route_pairs<1>, dim3(grid_for(p->n, kBlock)), dim3(kBlock), 0, s, p->n, p->q, p->e, b->home,
                            b->qid, nullptr, pbase_.p, pacc_.p + kMaxParts, out);
     pplan_np_ = 0;
+}
+
+namespace {
+__global__ void k_split_pairs(int64_t n, const uint64_t *__restrict__ in, uint32_t *__restrict__ q,
+                              uint32_t *__restrict__ e)
+{
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = in[i];
+        q[i] = (uint32_t)(k >> 32);
+        e[i] = (uint32_t)k;
+    }
+}
+}  // namespace
+
+void RouteEngine::split_pairs(int64_t n, const uint64_t *in, uint32_t *q, uint32_t *e, hipStream_t s)
+{
+    if (n <= 0) return;
+    const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_split_pairs, dim3(g), dim3(256), 0, s, n, in, q, e);
+    DSS_HIP(hipGetLastError());
 }
 
 }  // namespace dss

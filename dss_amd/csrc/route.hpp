@@ -27,6 +27,8 @@ class RouteEngine {
                 dssg_batch *out);
     void pairs_plan(const dssg_batch *b, const dssg_pairs *p, int np, hipStream_t s, int64_t *counts);
     void pairs_fill(const dssg_batch *b, const dssg_pairs *p, hipStream_t s, uint64_t *out);
+    // routed pairs (home-local qid << 32 | entity) -> (q, e) arrays
+    static void split_pairs(int64_t n, const uint64_t *in, uint32_t *q, uint32_t *e, hipStream_t s);
 
    private:
     DevBuf<unsigned char> tmp_;

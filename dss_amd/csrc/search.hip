@@ -1532,6 +1532,48 @@ __global__ void k_tag_emit(const unsigned long long *__restrict__ stage, const i
     }
 }
 
+// Cell-range shards (dssg_index_build_range): a long x long pair can meet
+// on several shards, and each keeps its own copy after the dedupe.  Only the
+// shard owning the pair's smallest shared cell keeps it: a shard starting at
+// cell_lo > 0 drops the pairs that also share a cell below cell_lo (a
+// two-pointer walk over the two sorted lists' cells below cell_lo; both lists
+// are whole on every shard).
+__global__ void k_tag_shard_keep(int64_t n, const uint32_t *__restrict__ q, const uint32_t *__restrict__ e,
+                                 QueryView qv, IndexView ix, uint64_t cell_lo, uint8_t *__restrict__ keep)
+{
+    const int64_t i = tid64();
+    if (i >= n) return;
+    const uint32_t qq = q[i], ee = e[i];
+    const uint64_t *a = qv.cells + qv.offs[qq], *b = ix.e_cells + ix.e_offs[ee];
+    const int64_t na = qv.offs[qq + 1] - qv.offs[qq], nb = ix.e_offs[ee + 1] - ix.e_offs[ee];
+    int64_t x = 0, y = 0;
+    bool shared = false;
+    while (x < na && y < nb) {
+        const uint64_t ca = a[x], cb = b[y];
+        if (ca >= cell_lo || cb >= cell_lo) break;
+        if (ca == cb) {
+            shared = true;
+            break;
+        }
+        if (ca < cb) x++;
+        else y++;
+    }
+    keep[i] = shared ? 0 : 1;
+}
+struct PredFlag8 {
+    const uint8_t *f;
+    __device__ bool operator()(int64_t i) const { return f[i] != 0; }
+};
+struct EmitPairCopy {
+    const uint32_t *q, *e;
+    uint32_t *q2, *e2;
+    __device__ void operator()(int64_t i, int64_t r) const
+    {
+        q2[r] = q[i];
+        e2[r] = e[i];
+    }
+};
+
 struct PredOvf {  // keys of the flagged buckets
     const unsigned long long *k;
     const uint8_t *ovf;
@@ -2046,6 +2088,16 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
                 compact_if(no, PredRunU64{k2}, EmitPairFromKey{k2, q2, e2, nun + nuq, eb}, tmp_, tmp2_, s, dtot, &nov);
                 nuq += nov;
             }
+        }
+        if (idx->cell_lo > 0 && nuq > 0) {  // a cell-range shard past the first: exactly-once across shards
+            uint8_t *keep = tovf_.ensure(nuq + 1);  // (the bucket flags are consumed)
+            hipLaunchKernelGGL(k_tag_shard_keep, dim3(grid_for(nuq, kBlock)), dim3(kBlock), 0, s, nuq, q2 + nun,
+                               e2 + nun, qv, ix, (uint64_t)idx->cell_lo, keep);
+            int64_t nk = 0;
+            compact_if(nuq, PredFlag8{keep}, EmitPairCopy{q2 + nun, e2 + nun, oq, oe}, tmp_, tmp2_, s, dtot, &nk);
+            device_copy(q2 + nun, oq, sizeof(uint32_t) * nk, s);
+            device_copy(e2 + nun, oe, sizeof(uint32_t) * nk, s);
+            nuq = nk;
         }
         out->q = q2;
         out->e = e2;

@@ -71,8 +71,9 @@ class SearchEngine {
                uint64_t cell_hi, hipStream_t s);
     // q cells must be sorted ascending and unique per query.  Output: every
     // matching (query, entity) pair once; out->n_tagged of them (the last
-    // ones) are long x long pairs, deduplicated within this index only (a
-    // cell-range shard can meet such a pair again on another shard).
+    // ones) are long x long pairs, deduplicated after the join (on a
+    // cell-range shard: kept only by the shard of their smallest shared cell,
+    // so each comes back once across shards).
     void search(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
                 const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
                 const int32_t *q_owner, hipStream_t s, dssg_pairs *out);

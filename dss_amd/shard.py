@@ -259,3 +259,63 @@ class ShardedSearch:
         self.last_recv_cells = recv_cells[: int(batch.n and recv_cells.numel())] if nrows else recv_cells[:0]
         self.last_shard_pairs = int(pairs.n)
         return out
+
+
+class NativeComm:
+    """A dssg_comm: the library's own RCCL communicator (no torch in the
+    exchange).  `unique_id()` on one rank, shared out of band, then
+    `NativeComm(ctx, nranks, rank, uid)` on every rank."""
+
+    def __init__(self, ctx, nranks: int, rank: int, uid: bytes):
+        from . import _lib
+        if len(uid) != _lib.COMM_ID_BYTES:
+            raise ValueError("a dssg_comm id is %d bytes" % _lib.COMM_ID_BYTES)
+        self.ctx = ctx
+        self.nranks, self.rank = nranks, rank
+        buf = (C.c_uint8 * len(uid)).from_buffer_copy(uid)
+        h = C.c_void_p()
+        ctx.check(ctx.L.dssg_comm_init(ctx.h, nranks, rank, buf, C.byref(h)))
+        self.h = h
+
+    @staticmethod
+    def unique_id(ctx) -> bytes:
+        from . import _lib
+        buf = (C.c_uint8 * _lib.COMM_ID_BYTES)()
+        ctx.check(ctx.L.dssg_comm_unique_id(buf))
+        return bytes(buf)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx.L.dssg_comm_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class NativeShardedSearch:
+    """`ShardedSearch` with the whole step in the library
+    (dssg_sharded_search_device: route, RCCL all-to-alls, shard join, pairs
+    home).  step() returns this rank's (query, entity) pairs as device
+    pointers (a _lib.Pairs, valid until the next step)."""
+
+    def __init__(self, ctx, comm: NativeComm, index, ranges: Sequence[Tuple[int, int]]):
+        import torch
+        if len(ranges) != comm.nranks:
+            raise ValueError("one cell range per rank")
+        self.ctx, self.comm, self.index = ctx, comm, index
+        self.part_hi = torch.as_tensor(part_his(ranges).view(np.int64),
+                                       device=torch.device("cuda", torch.cuda.current_device()))
+
+    def step(self, offs_ptr, cells_ptr, nq, alo, ahi, tlo, thi):
+        from . import _lib, device as D
+        ctx = self.ctx
+        out = _lib.Pairs()
+        ctx.check(ctx.L.dssg_sharded_search_device(ctx.h, self.comm.h, self.index, D._ptr(self.part_hi), nq,
+                                                   C.c_void_p(offs_ptr), C.c_void_p(cells_ptr), D._ptr(alo),
+                                                   D._ptr(ahi), D._ptr(tlo), D._ptr(thi), D._stream_ptr(),
+                                                   C.byref(out)))
+        return out

@@ -298,7 +298,9 @@ int dssg_max_subscription_count(dssg_ctx *ctx, const dssg_index *idx, int64_t nq
  *     (home-local qid << 32 | entity); the caller all-to-alls them back.
  * A part sees a query's whole cell list and every entity's whole cell list, so
  * each (query, entity) pair is emitted by exactly one part (the one owning
- * their smallest shared cell): no cross-shard dedupe. */
+ * their smallest shared cell; long x long pairs, met on every shard they
+ * share a cell with, are dropped by the shards past the smallest): no
+ * cross-shard dedupe. */
 #define DSSG_MAX_PARTS 64
 #define DSSG_ROUTE_ROW_BYTES 32
 typedef struct {
@@ -322,6 +324,32 @@ int dssg_route_pairs_plan_device(dssg_ctx *ctx, const dssg_batch *batch, const d
                                  void *stream, int64_t *counts);
 int dssg_route_pairs_fill_device(dssg_ctx *ctx, const dssg_batch *batch, const dssg_pairs *pairs, void *stream,
                                  uint64_t *d_out);
+
+/* ---- native exchange over RCCL (xGMI) -----------------------------------
+ * The sharded step without any framework: one process per GPU, one
+ * communicator per process.  Rank 0 makes an id (dssg_comm_unique_id), the
+ * processes share it out of band (the Go binding: over its own transport),
+ * each calls dssg_comm_init.  RCCL is opened on first use (dlopen, local
+ * symbols); without it these calls return DSSG_ERR_DEVICE.
+ * dssg_sharded_search_device runs steps 1-4 of the routing protocol above:
+ * route the rank's covered batch, all-to-all the query rows and cell lists
+ * (grouped ncclSend/ncclRecv; counts by ncclAllGather), join them against
+ * this rank's dssg_index_build_range shard, route the pairs home and
+ * all-to-all them back.  Output: this rank's pairs (query index in its own
+ * batch, entity), each exactly once, in device memory owned by the
+ * communicator until its next call.  Collective: every rank calls it. */
+#define DSSG_COMM_ID_BYTES 128
+typedef struct dssg_comm dssg_comm;
+int dssg_comm_unique_id(uint8_t *id);
+int dssg_comm_init(dssg_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t *id, dssg_comm **out);
+void dssg_comm_free(dssg_comm *comm);
+/* Byte blocks, part-major: send_bytes[d] to rank d, recv_bytes[s] from rank s. */
+int dssg_comm_alltoallv_device(dssg_ctx *ctx, dssg_comm *comm, const void *d_send, const int64_t *send_bytes,
+                               void *d_recv, const int64_t *recv_bytes, void *stream);
+int dssg_sharded_search_device(dssg_ctx *ctx, dssg_comm *comm, const dssg_index *shard, const uint64_t *d_part_hi,
+                               int64_t nq, const int64_t *d_q_offs, const uint64_t *d_q_cells,
+                               const float *d_q_alt_lo, const float *d_q_alt_hi, const int64_t *d_q_tlo,
+                               const int64_t *d_q_thi, void *stream, dssg_pairs *out);
 
 /* ---- diagnostics --------------------------------------------------------
  * Average device time (ms) of the most recent launches of the named kernel

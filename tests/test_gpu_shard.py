@@ -21,22 +21,24 @@ def _keys(q, e):
     return np.sort((np.asarray(q, np.uint64) << np.uint64(32)) | np.asarray(e, np.uint64))
 
 
-def _covered(scale):
+def _covered(scale, cfg=0):
     from dss_amd import geo, workload as W
-    _, q, qa, it, ia, now = W.config(0, scale=scale)
+    _, q, qa, it, ia, now = W.config(cfg, scale=scale)
     ci = geo.cover_batch(it.kind, it.voff, it.lat, it.lng, it.radius_m)
     cq = geo.cover_batch(q.kind, q.voff, q.lat, q.lng, q.radius_m)
     tlo, thi = W.query_bounds(qa, now)
     return ci, cq, qa, ia, tlo, thi
 
 
-@pytest.mark.parametrize("nparts", [1, 3, 8])
-def test_routed_shards_equal_full_search(nparts):
+# configs[0] (compact footprints) and configs[4] (corridors: long x long pairs
+# meet on several shards and must still come back exactly once)
+@pytest.mark.parametrize("cfg,scale,nparts", [(0, 0.05, 1), (0, 0.05, 3), (0, 0.05, 8), (4, 0.0004, 3), (4, 0.0004, 8)])
+def test_routed_shards_equal_full_search(cfg, scale, nparts):
     import ctypes as C
     import torch
     from dss_amd import _lib, device as D, shard
     from dss_amd.store import EntityIndex
-    ci, cq, qa, ia, tlo, thi = _covered(0.05)
+    ci, cq, qa, ia, tlo, thi = _covered(scale, cfg)
     full = EntityIndex(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1)
     fq, fe = full.search_batch(cq.offs, cq.cells, qa.alt_lo, qa.alt_hi, tlo, thi)
     assert len(fq) > 0
@@ -178,3 +180,31 @@ def test_sharded_search_two_ranks_gloo():
     assert all(n > 0 for _, _, n, _, _ in res)
     # pairs computed on the shards == pairs delivered home
     assert sum(r[4] for r in res) == sum(r[2] for r in res)
+
+
+def test_native_rccl_one_rank_equals_full_search():
+    """The library's own RCCL exchange (dssg_comm_*, dssg_sharded_search_device)
+    on a one-rank communicator: route -> grouped send/recv to itself -> join
+    -> pairs home, equal to the whole-index search.  (More ranks need more
+    GPUs: the multi-GPU node at round end.)"""
+    import torch
+    from dss_amd import _lib, device as D, shard
+    from dss_amd.store import EntityIndex
+    ci, cq, qa, ia, tlo, thi = _covered(0.05)
+    full = EntityIndex(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1)
+    fq, fe = full.search_batch(cq.offs, cq.cells, qa.alt_lo, qa.alt_hi, tlo, thi)
+    ctx = _lib.context()
+    uid = shard.NativeComm.unique_id(ctx)
+    comm = shard.NativeComm(ctx, 1, 0, uid)
+    ranges = shard.cell_splitters(ci.cells, 1)
+    idx = EntityIndex(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1, cell_range=ranges[0])
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")  # noqa: E731
+    offs, cells = t(cq.offs), t(cq.cells.view(np.int64))
+    ns = shard.NativeShardedSearch(ctx, comm, idx.h, ranges)
+    for _ in range(2):  # a second step reuses the communicator's buffers
+        p = ns.step(offs.data_ptr(), cells.data_ptr(), len(cq.offs) - 1, t(qa.alt_lo), t(qa.alt_hi), t(tlo), t(thi))
+        gq = D.copy_back(ctx, p.q, int(p.n), np.uint32)
+        ge = D.copy_back(ctx, p.e, int(p.n), np.uint32)
+        assert np.array_equal(_keys(gq, ge), _keys(fq, fe))
+    comm.close()
+    idx.free()
