@@ -47,6 +47,25 @@ def log(*a):
 
 
 _STAGE = ["start"]
+_JSON_FD = [None]
+
+
+def keep_stdout_for_json():
+    """Only the result line goes to stdout: native libraries (RCCL's init
+    banner) write to fd 1 directly, so fd 1 is pointed at stderr and the
+    original stdout is kept for emit()."""
+    sys.stdout.flush()
+    _JSON_FD[0] = os.dup(1)
+    os.dup2(2, 1)
+
+
+def emit(result):
+    line = (json.dumps(result) + "\n").encode()
+    if _JSON_FD[0] is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_JSON_FD[0], line)
 
 
 def stage(name):
@@ -86,9 +105,14 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0: the process's CPU share -- the affinity mask, capped by "
                          "OMP_NUM_THREADS, which the GPU box sets to its per-GPU share of 16)")
-    ap.add_argument("--mode", choices=["sharded", "replica"], default="replica",
-                    help="multi-GPU layout: replica (index on every GPU, queries split; default) or sharded (index "
-                         "split by cell range, queries and pairs exchanged by all-to-all)")
+    ap.add_argument("--mode", choices=["sharded", "replica"], default=None,
+                    help="multi-GPU layout: replica (index on every GPU, queries split) or sharded (index split by "
+                         "cell range, queries and pairs exchanged by all-to-all).  Default: sharded for configs[2] "
+                         "on N > 1 GPUs (its BASELINE layout; the replica rate is reported beside it), else replica")
+    ap.add_argument("--exchange", choices=["native", "torch"], default=None,
+                    help="sharded mode's all-to-alls: native (the library's own RCCL communicator, "
+                         "dssg_sharded_search_device) or torch (torch.distributed; the instrumented path).  Default: "
+                         "native with --dist-backend nccl, torch otherwise")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on a multi-GPU node; gloo for rehearsals")
     ap.add_argument("--pipelines", type=int, default=3,
                     help="concurrent batch pipelines per GPU (own engine context + stream + host thread each): one "
@@ -98,13 +122,15 @@ def main():
     args = ap.parse_args()
 
     heartbeat()
+    keep_stdout_for_json()
     import torch
     import torch.distributed as dist
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", 0))
-    mode = args.mode
+    mode = args.mode or ("sharded" if args.config == 2 and world > 1 else "replica")
+    exchange = args.exchange or ("native" if args.dist_backend == "nccl" else "torch")
     torch.cuda.set_device(local)
     stage_host = args.dist_backend != "nccl"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")   # single-process sharded runs (no torchrun)
@@ -163,12 +189,23 @@ def main():
         sort_ph = (sort_phase(ctx, torch, dev, i_offs_t, i_cells_t) if not large else
                    {"skipped": f"{i_cells_t.numel()} postings: the sort's scratch on top of the index would not fit "
                                f"beside it; the build's sorts are inside index_build_s"})
-    sharded = None
+    sharded = native = None
     if mode == "sharded":
+        # the instrumented torch-exchange path always exists (phase breakdown);
+        # the timed steps use the library's own RCCL exchange when native
         sharded = shard.ShardedSearch(ctx, index, ranges, stage_host=stage_host)
+        if exchange == "native":
+            uid = torch.zeros(_lib.COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+            if rank == 0:
+                uid.copy_(torch.frombuffer(bytearray(shard.NativeComm.unique_id(ctx)), dtype=torch.uint8))
+            dist.broadcast(uid, 0)  # bootstrap only: the id travels once
+            native = shard.NativeShardedSearch(ctx, shard.NativeComm(ctx, world, rank, bytes(uid.cpu().numpy())),
+                                               index, ranges)
 
     def step(timed=False):
         cells = D.cover(ctx, d_q)
+        if native is not None and not timed:
+            return cells, native.step(cells.offs, cells.cells, nq, q_alo, q_ahi, q_tlo, q_thi)
         if sharded is not None:
             return cells, sharded.step(cells.offs, cells.cells, nq, q_alo, q_ahi, q_tlo, q_thi, timed=timed)
         pairs = D.search(ctx, index, cells, q_alo, q_ahi, q_tlo, q_thi)
@@ -240,8 +277,37 @@ def main():
     value = world * nq * args.steps / elapsed
 
     if sharded is not None:
+        replica = None
+        if full_index is not None and args.config == 2:
+            # the replica layout beside it (BASELINE configs[2] asks for the
+            # sharded one): every rank joins its own batch against the whole index
+            def rstep():
+                c = D.cover(ctx, d_q)
+                D.search(ctx, full_index, c, q_alo, q_ahi, q_tlo, q_thi)
+            for _ in range(args.warmup):
+                rstep()
+            dist.barrier()
+            torch.cuda.synchronize()
+            r0 = time.perf_counter()
+            for _ in range(args.steps):
+                rstep()
+            torch.cuda.synchronize()
+            dist.barrier()
+            rt = torch.tensor([time.perf_counter() - r0], device=dev, dtype=torch.float64)
+            dist.all_reduce(rt, op=dist.ReduceOp.MAX)
+            replica = {"value": world * nq * args.steps / float(rt.item()),
+                       "ms_per_step": 1000.0 * float(rt.item()) / max(1, args.steps),
+                       "note": "whole index on every GPU, each rank's batch joined locally (no exchange), one pipeline"}
+        native_pairs = None
+        if native is not None:  # the timed path's own output, checked below beside the torch path's
+            c = D.cover(ctx, d_q)
+            p = native.step(c.offs, c.cells, nq, q_alo, q_ahi, q_tlo, q_thi)
+            nq_ = D.copy_back(ctx, p.q, int(p.n), np.uint32).astype(np.uint64)
+            ne_ = D.copy_back(ctx, p.e, int(p.n), np.uint32).astype(np.uint64)
+            native_pairs = (nq_ << np.uint64(32)) | ne_
         sharded_report(args, ctx, D, dist, torch, sharded, step, full_index, i_cells_h, ranges, rank, world, nq, ni,
-                       n_post, build_s, value, ms_per_step, q_alo, q_ahi, q_tlo, q_thi)
+                       n_post, build_s, value, ms_per_step, q_alo, q_ahi, q_tlo, q_thi, exchange, replica,
+                       native_pairs)
         ctx.L.dssg_index_free(index)
         dist.destroy_process_group()
         return
@@ -341,7 +407,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
         }
-        print(json.dumps(result), flush=True)
+        emit(result)
     ctx.L.dssg_index_free(index)
     if world > 1:
         dist.destroy_process_group()
@@ -366,7 +432,8 @@ def pair_checksum(keys: np.ndarray) -> int:
 
 
 def sharded_report(args, ctx, D, dist, torch, sh, step, full, i_cells_h, ranges, rank, world, nq, ni, n_post, build_s,
-                   value, ms_per_step, q_alo, q_ahi, q_tlo, q_thi):
+                   value, ms_per_step, q_alo, q_ahi, q_tlo, q_thi, exchange="torch", replica=None,
+                   native_pairs=None):
     """Phase breakdown (synchronised passes, max over ranks), the shard join's
     roofline, and parity: every rank's delivered pair set == a whole-index
     search of its own queries (count + order-independent checksum)."""
@@ -413,10 +480,14 @@ def sharded_report(args, ctx, D, dist, torch, sh, step, full, i_cells_h, ranges,
         want = (fq << np.uint64(32)) | fe
         got = out.cpu().numpy().view(np.uint64)
         ok = len(want) == len(got) and pair_checksum(want) == pair_checksum(got)
-        t = torch.tensor([1.0 if ok else 0.0, float(len(got))], dtype=torch.float64, device=dev)
+        nok = native_pairs is None or (len(want) == len(native_pairs) and
+                                       pair_checksum(want) == pair_checksum(native_pairs))
+        t = torch.tensor([1.0 if ok else 0.0, 1.0 if nok else 0.0, float(len(got))], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         parity = {"check": "per rank: count + sum(splitmix64(q << 32 | e)) of the delivered pairs == a whole-index "
                            "search of the rank's own queries", "all_ranks_equal": bool(t[0].item() == 1.0)}
+        if native_pairs is not None:
+            parity["native_exchange_equal"] = bool(t[1].item() == 1.0)
     if rank != 0:
         return
     result = {
@@ -436,7 +507,9 @@ def sharded_report(args, ctx, D, dist, torch, sh, step, full, i_cells_h, ranges,
                                f"sharded by S2 cell range over {world} GPU(s), {W.CONFIG_NAMES[args.config]}, S2 level 13",
                    "queries_per_gpu_step": nq, "intents": ni, "postings_rank0": n_post,
                    "parallelism": f"cell-range shards x{world}; queries routed to shards and pairs routed home by "
-                                  f"all-to-all ({args.dist_backend})", "scale": args.scale},
+                                  f"all-to-all ({'the library RCCL communicator' if exchange == 'native' else args.dist_backend})",
+                   "exchange": exchange, "scale": args.scale},
+        "replica": replica,
         "coverings_per_s": world * nq / (phase["cover"] * 1e-3),
         "phase_ms_max_over_ranks": phase,
         "routed": {"rows_total": sums[1].item(), "rows_min_rank": mins[1].item(), "cells_total": sums[2].item(),
@@ -449,7 +522,7 @@ def sharded_report(args, ctx, D, dist, torch, sh, step, full, i_cells_h, ranges,
         "cpu_baseline": None,
         "parity": parity,
     }
-    print(json.dumps(result), flush=True)
+    emit(result)
 
 
 LARGE_POSTINGS = 600_000_000  # above: no host copy of the intents' cells, no standalone sort-phase run
