@@ -341,6 +341,10 @@ def main():
     # inputs (24 B attributes + 8 B per covering cell), every posting of a
     # cell the batch touches read once (28 B: entity id, alt pair, time
     # pair), and the output pairs (8 B).
+    stage("cover roofline counts")
+    c_offs_h = D.copy_back(ctx, cells.offs, nq + 1, np.int64)
+    cover_rl = cover_roofline(queries, c_offs_h, D.copy_back(ctx, cells.cells, int(c_offs_h[-1]), np.uint64),
+                              cover_avg)
     stage("touched postings")
     p_touched = touched_postings(ctx, D, index, cells)
     join_bytes = 24 * nq + 8 * c_tot + 28 * p_touched + 8 * r_tot
@@ -394,6 +398,7 @@ def main():
             "index_build_s": build_s,
             "sort_phase": sort_ph,
             "cover_fp64": cover_fp64(nq, ni),
+            "cover_roofline": cover_rl,
             "roofline": {"kernel": "k_join (overlap join + fused altitude/time filter)", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
@@ -659,6 +664,68 @@ def pmc_traffic(kernel, nq, ni):
     if not k or d.get("queries") != nq or d.get("intents") != ni:
         return None
     return {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": d.get("source", path)}
+
+
+_POS_IJ = np.array([[(0x874B78B4 >> (8 * o + 2 * p)) & 3 for p in range(4)] for o in range(4)], np.uint64)
+_POS_OR = np.array([(0xC1 >> (2 * p)) & 3 for p in range(4)], np.uint64)
+
+
+def decode13(cells):
+    """Level-13 S2 cell ids -> (face, i, j) (cellid.go faceIJOrientation,
+    one level at a time; the same walk as search.hip decode13)."""
+    c = np.asarray(cells, np.uint64)
+    face = (c >> np.uint64(61)).astype(np.int64)
+    o = (face & 1).astype(np.uint64)
+    i = np.zeros(len(c), np.int64)
+    j = np.zeros(len(c), np.int64)
+    for lvl in range(13):
+        pos = (c >> np.uint64(59 - 2 * lvl)) & np.uint64(3)
+        ij = _POS_IJ[o, pos]
+        i = (i << 1) | (ij >> np.uint64(1)).astype(np.int64)
+        j = (j << 1) | (ij & np.uint64(1)).astype(np.int64)
+        o = o ^ _POS_OR[pos]
+    return face, i, j
+
+
+def cover_roofline(fp, offs, cells, cover_ms):
+    """SURVEY.md s8(d)'s covering model: F_p = 48 E_p (|C_p| + |R_p|) + 40 V_p
+    summed over the step's footprints, against the FP64 vector peak.  E_p =
+    V_p = the loop's vertices (a circle's RegularLoop has 20; the closing
+    edge included), C_p = its output cells, R_p = the level-13 edge
+    neighbours of C_p outside C_p (a neighbour across a cube face is counted
+    as rejected: exact within a face, an over-count of at most the cells
+    that touch a face edge)."""
+    n = len(offs) - 1
+    if n == 0 or len(cells) == 0:
+        return None
+    nv = np.where(fp.kind == 1, 20, np.diff(fp.voff)).astype(np.int64)
+    cp = np.diff(offs).astype(np.int64)
+    owner = np.repeat(np.arange(n, dtype=np.int64), cp)
+    face, i, j = decode13(cells)
+    key = (owner << 30) | (face << 26) | (i << 13) | j
+    own = np.sort(key)
+    nb = []
+    for di, dj in ((1, 0), (-1, 0), (0, 1), (0, -1)):
+        ii, jj = i + di, j + dj
+        inside = (ii >= 0) & (ii < 8192) & (jj >= 0) & (jj < 8192)
+        k = (owner << 30) | (face << 26) | (np.clip(ii, 0, 8191) << 13) | np.clip(jj, 0, 8191)
+        nb.append(np.where(inside, k, -1 - np.arange(len(k), dtype=np.int64) * 4 - len(nb)))  # cross-face: unique
+    nb = np.unique(np.concatenate(nb))
+    pos = np.searchsorted(own, nb)
+    hit = (pos < len(own)) & (own[np.minimum(pos, len(own) - 1)] == nb)
+    rej = nb[~hit]
+    rp = np.zeros(n, np.int64)
+    inface = rej >= 0
+    np.add.at(rp, rej[inface] >> 30, 1)
+    # cross-face neighbours: attribute to their cells' footprints
+    xf = (-1 - rej[~inface]) // 4
+    np.add.at(rp, owner[xf], 1)
+    flops = float(np.sum(48 * nv * (cp + rp) + 40 * nv))
+    achieved = flops / (cover_ms * 1e-3) / 1e12
+    return {"model": "SURVEY s8(d): F_p = 48 E_p (|C_p| + |R_p|) + 40 V_p", "bound": "fp64-valu",
+            "flops": flops, "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / FP64_PEAK_TFLOPS, "cover_ms": cover_ms,
+            "counts": {"footprints": n, "E": int(nv.sum()), "C": int(cp.sum()), "R": int(rp.sum())}}
 
 
 def cover_fp64(nq, ni):
