@@ -117,6 +117,9 @@ def main():
     ap.add_argument("--pipelines", type=int, default=3,
                     help="concurrent batch pipelines per GPU (own engine context + stream + host thread each): one "
                          "batch's FP64 covering overlaps another's join, as concurrent RPCs would (replica mode)")
+    ap.add_argument("--latency", type=int, default=1,
+                    help="also time single requests (cover + search of one footprint): alone, and 64 concurrent "
+                         "callers through the micro-batcher (dssg_batcher)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank on cuda:0 (one-GPU box, gloo backend)")
     args = ap.parse_args()
@@ -341,6 +344,8 @@ def main():
     # inputs (24 B attributes + 8 B per covering cell), every posting of a
     # cell the batch touches read once (28 B: entity id, alt pair, time
     # pair), and the output pairs (8 B).
+    stage("single-request latency")
+    latency = request_latency(ctx, D, index, queries, qa, now) if args.latency else None
     stage("cover roofline counts")
     c_offs_h = D.copy_back(ctx, cells.offs, nq + 1, np.int64)
     cover_rl = cover_roofline(queries, c_offs_h, D.copy_back(ctx, cells.cells, int(c_offs_h[-1]), np.uint64),
@@ -399,6 +404,7 @@ def main():
             "sort_phase": sort_ph,
             "cover_fp64": cover_fp64(nq, ni),
             "cover_roofline": cover_rl,
+            "request_latency": latency,
             "roofline": {"kernel": "k_join (overlap join + fused altitude/time filter)", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
@@ -726,6 +732,80 @@ def cover_roofline(fp, offs, cells, cover_ms):
             "flops": flops, "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / FP64_PEAK_TFLOPS, "cover_ms": cover_ms,
             "counts": {"footprints": n, "E": int(nv.sum()), "C": int(cp.sum()), "R": int(rp.sum())}}
+
+
+def request_latency(ctx, D, index, queries, qa, now, n_alone=500, callers=64, seconds=2.0):
+    """The per-RPC path the reference runs (one covering + one SQL search per
+    request): (a) one request at a time through the host ABI
+    (dssg_cover_batch + dssg_search_operations, each a host round trip);
+    (b) `callers` threads each issuing requests back to back through the
+    micro-batcher (dssg_batcher), which coalesces them into shared cover +
+    join launches.  p50 / p99 request latency in ms and requests/s."""
+    import ctypes as C
+    import threading
+    from dss_amd.store import Batcher, _p
+    L = ctx.L
+    lat_ms = []
+    cap = 1 << 16
+    cells = np.empty(cap, np.uint64)
+    oq, oe = np.empty(cap, np.uint32), np.empty(cap, np.uint32)
+    for k in range(n_alone):
+        i = k % queries.n
+        v0, v1 = queries.voff[i], queries.voff[i + 1]
+        kind = np.array([queries.kind[i]], np.int32)
+        voff = np.array([0, v1 - v0], np.int64)
+        la, lg = np.ascontiguousarray(queries.lat[v0:v1]), np.ascontiguousarray(queries.lng[v0:v1])
+        rad = np.array([queries.radius_m[i]], np.float32)
+        offs = np.zeros(2, np.int64)
+        st, area, need = np.zeros(1, np.int32), np.zeros(1), C.c_int64()
+        lo, hi = np.array([qa.alt_lo[i]], np.float32), np.array([qa.alt_hi[i]], np.float32)
+        s0, e0 = np.array([qa.t0[i]], np.int64), np.array([qa.t1[i]], np.int64)
+        t0 = time.perf_counter()
+        ctx.check(L.dssg_cover_batch(ctx.h, 1, _p(kind, C.c_int32), _p(voff, C.c_int64), _p(la, C.c_double),
+                                     _p(lg, C.c_double), _p(rad, C.c_float), _p(offs, C.c_int64),
+                                     _p(cells, C.c_uint64), cap, C.byref(need), _p(st, C.c_int32),
+                                     _p(area, C.c_double)))
+        ctx.check(L.dssg_search_operations(ctx.h, index, 1, _p(offs, C.c_int64), _p(cells, C.c_uint64),
+                                           _p(lo, C.c_float), _p(hi, C.c_float), _p(s0, C.c_int64),
+                                           _p(e0, C.c_int64), int(now), _p(oq, C.c_uint32), _p(oe, C.c_uint32), cap,
+                                           C.byref(need)))
+        lat_ms.append(1000.0 * (time.perf_counter() - t0))
+    alone = np.array(lat_ms[20:])
+
+    import types
+    b = Batcher(types.SimpleNamespace(h=index), max_batch=4096, max_wait_us=100)  # (an index handle holder)
+    stop = [False]
+    rec = [[] for _ in range(callers)]
+
+    def caller(k):
+        i = k
+        while not stop[0]:
+            v0, v1 = queries.voff[i], queries.voff[i + 1]
+            t0 = time.perf_counter()
+            b.search_operations(queries.kind[i], queries.lat[v0:v1], queries.lng[v0:v1], queries.radius_m[i],
+                                qa.alt_lo[i], qa.alt_hi[i], qa.t0[i], qa.t1[i], now)
+            rec[k].append(1000.0 * (time.perf_counter() - t0))
+            i = (i + callers) % queries.n
+
+    ths = [threading.Thread(target=caller, args=(k,)) for k in range(callers)]
+    t_start = time.perf_counter()
+    for t in ths:
+        t.start()
+    time.sleep(seconds)
+    stop[0] = True
+    for t in ths:
+        t.join()
+    wall = time.perf_counter() - t_start
+    nreq, nbatch = b.stats()
+    b.close()
+    allr = np.concatenate([np.array(r) for r in rec if r]) if any(rec) else np.zeros(1)
+    return {"alone": {"requests": len(alone), "p50_ms": float(np.percentile(alone, 50)),
+                      "p99_ms": float(np.percentile(alone, 99)), "requests_per_s": float(1000.0 / alone.mean())},
+            "batched": {"callers": callers, "requests": int(nreq), "batches": int(nbatch),
+                        "mean_batch": float(nreq / max(1, nbatch)), "p50_ms": float(np.percentile(allr, 50)),
+                        "p99_ms": float(np.percentile(allr, 99)), "requests_per_s": float(nreq / wall)},
+            "note": "one request = cover 1 footprint + searchOperations, host buffers in and out (the RPC path); "
+                    "batched: Python caller threads through dssg_batcher (max_wait 100 us)"}
 
 
 def cover_fp64(nq, ni):

@@ -164,6 +164,13 @@ def load():
         L.dssg_comm_free.argtypes = [vp]
         L.dssg_comm_free.restype = None
         L.dssg_comm_alltoallv_device.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.dssg_batcher_create.argtypes = [C.c_int, vp, C.c_int32, C.c_int32, P(vp)]
+        L.dssg_batcher_free.argtypes = [vp]
+        L.dssg_batcher_free.restype = None
+        L.dssg_batcher_search_operations.argtypes = [vp, C.c_int32, C.c_int64, vp, vp, C.c_float, C.c_float, C.c_float,
+                                                      C.c_int64, C.c_int64, C.c_int64, vp, C.c_int64, P(C.c_int64),
+                                                      P(C.c_int32), P(C.c_double)]
+        L.dssg_batcher_stats.argtypes = [vp, P(C.c_int64), P(C.c_int64)]
         L.dssg_sharded_search_device.argtypes = [vp, vp, vp, vp, C.c_int64, vp, vp, vp, vp, vp, vp, vp, P(Pairs)]
         L.dssg_radix_sort_device.argtypes = [vp, C.c_int, i64, C.c_int, vp, vp, vp, vp, vp, P(d)]
         L.dssg_selftest_scan.argtypes = [vp, i64, C.c_int, P(i64), P(i64)]

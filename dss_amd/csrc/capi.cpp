@@ -9,7 +9,11 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -1157,4 +1161,195 @@ int dssg_sharded_search_device(dssg_ctx *ctx, dssg_comm *comm, const dssg_index 
         out->n = rpair;
         out->n_tagged = 0;
     });
+}
+
+/* ======================================================================
+ * Micro-batcher: the per-RPC path.  The reference runs one covering and one
+ * SQL search per request (pkg/scd/operations_handler.go:118-168,
+ * pkg/rid/server/isa_handler.go:153-207); here concurrent single requests
+ * are coalesced by a worker thread into one cover launch and one join per
+ * batch (up to max_batch requests, waiting at most max_wait_us after the
+ * first), and each caller gets its own answer back.
+ * ====================================================================== */
+struct dssg_batcher {
+    struct Req {
+        int32_t kind = 0;
+        std::vector<double> lat, lng;
+        float radius = 0, alo = 0, ahi = 0;
+        int64_t tlo = 0, thi = 0;
+        std::vector<uint32_t> ids;
+        int32_t status = 0;
+        double area = 0;
+        int rc = DSSG_OK;
+        std::string err;
+        bool done = false;
+    };
+    dssg_ctx *ctx = nullptr;
+    const dssg_index *idx = nullptr;
+    int max_batch = 1024, max_wait_us = 200;
+    std::mutex mu;
+    std::condition_variable cv, done_cv;
+    std::deque<Req *> queue;
+    bool stop = false;
+    int64_t n_requests = 0, n_batches = 0;
+    std::thread worker;
+
+    void run_batch(std::vector<Req *> &b)
+    {
+        const int64_t n = (int64_t)b.size();
+        std::vector<int32_t> kind(n);
+        std::vector<int64_t> voff(n + 1, 0), tlo(n), thi(n);
+        std::vector<float> rad(n), alo(n), ahi(n);
+        std::vector<double> lat, lng;
+        for (int64_t i = 0; i < n; i++) {
+            Req *r = b[i];
+            kind[i] = r->kind;
+            voff[i + 1] = voff[i] + (int64_t)r->lat.size();
+            lat.insert(lat.end(), r->lat.begin(), r->lat.end());
+            lng.insert(lng.end(), r->lng.begin(), r->lng.end());
+            rad[i] = r->radius;
+            alo[i] = r->alo;
+            ahi[i] = r->ahi;
+            tlo[i] = r->tlo;
+            thi[i] = r->thi;
+        }
+        std::vector<int32_t> status(n);
+        std::vector<double> area(n);
+        std::vector<uint32_t> pq, pe;
+        const int rc = guarded(ctx, [&] {
+            hipStream_t s = ctx->stream;
+            const int64_t nv = voff[n];
+            const int32_t *dk = upload(ctx->d_kind, kind.data(), n, s);
+            const int64_t *dv = upload(ctx->d_voff, voff.data(), n + 1, s);
+            const double *dla = upload(ctx->d_lat, lat.data(), nv, s);
+            const double *dln = upload(ctx->d_lng, lng.data(), nv, s);
+            const float *dr = upload(ctx->d_rad, rad.data(), n, s);
+            dssg_cells cov;
+            ctx->cover.run(n, dk, dv, dla, dln, dr, s, &cov);
+            DSS_HIP(hipMemcpyAsync(status.data(), cov.status, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, s));
+            DSS_HIP(hipMemcpyAsync(area.data(), cov.area_km2, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, s));
+            const float *dlo = upload(ctx->d_alo, alo.data(), n, s);
+            const float *dhi = upload(ctx->d_ahi, ahi.data(), n, s);
+            const int64_t *dtl = upload(ctx->d_tlo, tlo.data(), n, s);
+            const int64_t *dth = upload(ctx->d_thi, thi.data(), n, s);
+            dssg_pairs res{};
+            if (cov.total_cells > 0) ctx->search.search(idx, n, cov.offs, cov.cells, dlo, dhi, dtl, dth, nullptr, s, &res);
+            pq.resize((size_t)res.n);
+            pe.resize((size_t)res.n);
+            if (res.n > 0) {
+                DSS_HIP(hipMemcpyAsync(pq.data(), res.q, sizeof(uint32_t) * (size_t)res.n, hipMemcpyDeviceToHost, s));
+                DSS_HIP(hipMemcpyAsync(pe.data(), res.e, sizeof(uint32_t) * (size_t)res.n, hipMemcpyDeviceToHost, s));
+            }
+            DSS_HIP(hipStreamSynchronize(s));
+            if (res.n > 0) sort_pairs_host(pq.data(), pe.data(), res.n);
+        });
+        std::lock_guard<std::mutex> lk(mu);
+        size_t k = 0;
+        for (int64_t i = 0; i < n; i++) {
+            Req *r = b[i];
+            r->rc = rc;
+            if (rc != DSSG_OK) r->err = ctx->last_error;
+            r->status = status[i];
+            r->area = area[i];
+            while (k < pq.size() && (int64_t)pq[k] == i) r->ids.push_back(pe[k++]);
+            r->done = true;
+        }
+        n_batches++;
+        n_requests += n;
+        done_cv.notify_all();
+    }
+
+    void loop()
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        while (true) {
+            cv.wait(lk, [&] { return stop || !queue.empty(); });
+            if (queue.empty() && stop) return;
+            // coalesce: until max_batch requests or max_wait_us after the first
+            const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(max_wait_us);
+            cv.wait_until(lk, until, [&] { return stop || (int)queue.size() >= max_batch; });
+            std::vector<Req *> b;
+            while (!queue.empty() && (int)b.size() < max_batch) {
+                b.push_back(queue.front());
+                queue.pop_front();
+            }
+            lk.unlock();
+            run_batch(b);
+            lk.lock();
+        }
+    }
+};
+
+int dssg_batcher_create(int device, const dssg_index *idx, int32_t max_batch, int32_t max_wait_us, dssg_batcher **out)
+{
+    if (!idx || !out || max_batch < 1 || max_wait_us < 0) return DSSG_ERR_INVALID;
+    dssg_ctx *ctx = nullptr;
+    const int rc = dssg_create(device, &ctx);
+    if (rc != DSSG_OK) return rc;
+    auto *b = new dssg_batcher();
+    b->ctx = ctx;
+    b->idx = idx;
+    b->max_batch = max_batch;
+    b->max_wait_us = max_wait_us;
+    b->worker = std::thread([b] { b->loop(); });
+    *out = b;
+    return DSSG_OK;
+}
+
+void dssg_batcher_free(dssg_batcher *b)
+{
+    if (!b) return;
+    {
+        std::lock_guard<std::mutex> lk(b->mu);
+        b->stop = true;
+    }
+    b->cv.notify_all();
+    if (b->worker.joinable()) b->worker.join();
+    dssg_destroy(b->ctx);
+    delete b;
+}
+
+int dssg_batcher_search_operations(dssg_batcher *b, int32_t kind, int64_t nv, const double *lat, const double *lng,
+                                   float radius_m, float alt_lo, float alt_hi, int64_t start, int64_t end,
+                                   int64_t now_us, uint32_t *out_e, int64_t cap, int64_t *needed, int32_t *status,
+                                   double *area_km2)
+{
+    if (!b || !needed || !status || nv < 0 || (nv > 0 && (!lat || !lng)) || now_us == INT64_MIN ||
+        (kind != DSSG_KIND_POLYGON && kind != DSSG_KIND_CIRCLE && kind != DSSG_KIND_POINTS))
+        return DSSG_ERR_INVALID;
+    dssg_batcher::Req r;
+    r.kind = kind;
+    if (nv > 0) {
+        r.lat.assign(lat, lat + nv);
+        r.lng.assign(lng, lng + nv);
+    }
+    r.radius = radius_m;
+    r.alo = alt_lo;
+    r.ahi = alt_hi;
+    r.tlo = std::max(start, now_us);  // operations.go:398-402
+    r.thi = end;
+    std::unique_lock<std::mutex> lk(b->mu);
+    b->queue.push_back(&r);
+    b->cv.notify_all();
+    b->done_cv.wait(lk, [&] { return r.done; });
+    lk.unlock();
+    *status = r.status;
+    if (area_km2) *area_km2 = r.area;
+    if (r.rc != DSSG_OK) return r.rc;
+    *needed = (int64_t)r.ids.size();
+    if ((int64_t)r.ids.size() > cap) return DSSG_ERR_CAPACITY;
+    if (!r.ids.empty()) {
+        if (!out_e) return DSSG_ERR_INVALID;
+        std::memcpy(out_e, r.ids.data(), sizeof(uint32_t) * r.ids.size());
+    }
+    return DSSG_OK;
+}
+
+int dssg_batcher_stats(dssg_batcher *b, int64_t *requests, int64_t *batches)
+{
+    if (!b) return DSSG_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (requests) *requests = b->n_requests;
+    if (batches) *batches = b->n_batches;
+    return DSSG_OK;
 }

@@ -506,3 +506,57 @@ class MutableOperationStore:
         self.gpu.delete([self.slot[op_id]])
         del self.ops[op_id]
         return old
+
+
+class Batcher:
+    """dssg_batcher: concurrent single SCD searchOperations requests (an
+    uncovered footprint each) coalesced into one cover launch + one join per
+    batch by the library's worker thread.  `search_operations` blocks the
+    calling thread only (ctypes releases the GIL), so many Python threads --
+    or Go goroutines through the same C call -- share batches."""
+
+    def __init__(self, index: "EntityIndex", max_batch: int = 1024, max_wait_us: int = 200, device: int = 0):
+        self.index = index  # the index must outlive the batcher
+        self.L = _lib.load()
+        h = C.c_void_p()
+        rc = self.L.dssg_batcher_create(device, index.h, int(max_batch), int(max_wait_us), C.byref(h))
+        if rc != _lib.DSSG_OK:
+            raise _lib.DssgError(rc, self.L.dssg_strerror(rc).decode())
+        self.h = h
+
+    def search_operations(self, kind: int, lat, lng, radius_m: float, alt_lo: float, alt_hi: float, start: int,
+                          end: int, now_us: int):
+        """-> (status, entity ids); status DSSG_ST_* of the covering."""
+        lat = np.ascontiguousarray(lat, dtype=np.float64)
+        lng = np.ascontiguousarray(lng, dtype=np.float64)
+        cap = 256
+        while True:
+            out = np.empty(cap, dtype=np.uint32)
+            needed, st, area = C.c_int64(), C.c_int32(), C.c_double()
+            rc = self.L.dssg_batcher_search_operations(self.h, int(kind), len(lat), _p(lat, C.c_double),
+                                                       _p(lng, C.c_double), float(radius_m), float(alt_lo),
+                                                       float(alt_hi), int(start), int(end), int(now_us),
+                                                       _p(out, C.c_uint32), cap, C.byref(needed), C.byref(st),
+                                                       C.byref(area))
+            if rc == _lib.DSSG_ERR_CAPACITY:
+                cap = int(needed.value) + 1
+                continue
+            if rc != _lib.DSSG_OK:
+                raise _lib.DssgError(rc, self.L.dssg_strerror(rc).decode())
+            return int(st.value), out[: needed.value].copy()
+
+    def stats(self):
+        r, b = C.c_int64(), C.c_int64()
+        self.L.dssg_batcher_stats(self.h, C.byref(r), C.byref(b))
+        return int(r.value), int(b.value)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.dssg_batcher_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -351,6 +351,26 @@ int dssg_sharded_search_device(dssg_ctx *ctx, dssg_comm *comm, const dssg_index 
                                const float *d_q_alt_lo, const float *d_q_alt_hi, const int64_t *d_q_tlo,
                                const int64_t *d_q_thi, void *stream, dssg_pairs *out);
 
+/* ---- per-request path: micro-batcher -------------------------------------
+ * The reference covers and searches once per RPC (pkg/scd/operations_handler
+ * .go:118-168).  A batcher owns a context and a worker thread; concurrent
+ * callers each submit one SCD searchOperations request (an uncovered
+ * footprint as dssg_cover_batch takes it, altitudes, start/end, now) and
+ * block until the worker has run the batch it joined -- up to max_batch
+ * requests, waiting at most max_wait_us after the first -- as one cover
+ * launch and one join.  Result: the entity ids (sorted), the covering status
+ * (DSSG_ST_*; the caller maps an error or an empty covering to its
+ * BadRequest as searchOperations does), area_km2.  The index must outlive
+ * the batcher; it is read concurrently, never written. */
+typedef struct dssg_batcher dssg_batcher;
+int dssg_batcher_create(int device, const dssg_index *idx, int32_t max_batch, int32_t max_wait_us, dssg_batcher **out);
+void dssg_batcher_free(dssg_batcher *b);
+int dssg_batcher_search_operations(dssg_batcher *b, int32_t kind, int64_t nv, const double *lat, const double *lng,
+                                   float radius_m, float alt_lo, float alt_hi, int64_t start, int64_t end,
+                                   int64_t now_us, uint32_t *out_e, int64_t cap, int64_t *needed, int32_t *status,
+                                   double *area_km2);
+int dssg_batcher_stats(dssg_batcher *b, int64_t *requests, int64_t *batches);
+
 /* ---- diagnostics --------------------------------------------------------
  * Average device time (ms) of the most recent launches of the named kernel
  * phase, measured with HIP events on the launching stream (bench.py). */
