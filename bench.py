@@ -344,8 +344,6 @@ def main():
     # inputs (24 B attributes + 8 B per covering cell), every posting of a
     # cell the batch touches read once (28 B: entity id, alt pair, time
     # pair), and the output pairs (8 B).
-    stage("single-request latency")
-    latency = request_latency(ctx, D, index, queries, qa, now) if args.latency else None
     stage("cover roofline counts")
     c_offs_h = D.copy_back(ctx, cells.offs, nq + 1, np.int64)
     cover_rl = cover_roofline(queries, c_offs_h, D.copy_back(ctx, cells.cells, int(c_offs_h[-1]), np.uint64),
@@ -372,6 +370,12 @@ def main():
             stage("cpu baseline")
             cpu, parity = cpu_baseline(args, ctx, intents, ia, queries, qa, now,
                                        lambda sc: intent_csr(torch, i_offs_t, i_cells_t, sc), cells, pairs)
+        # last: the per-request calls reuse the context's cover / search
+        # buffers that `cells` and `pairs` point into
+        latency = None
+        if args.latency:
+            stage("single-request latency")
+            latency = request_latency(ctx, D, index, queries, qa, now)
         traffic = pmc_traffic("k_join", nq, ni)
         result = {
             "metric": "4D conflict queries/sec vs N-intent airspace",

@@ -955,16 +955,19 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m)
 
 // Output: pairs go straight to HBM in per-wave chunks of kOutChunk slots,
 // each reserved with one atomic on the wave's region counter (kRegions
-// regions of rcap slots: a single same-address counter saturates at ~88
-// atomics/us, MI355X_MICROARCH.md "dequeue"); each retired chunk records its
-// fill, and k_fix_* close the holes that partly filled or unreserved chunks
-// leave below the total.
-constexpr int kOutChunk = 1024;
+// counters: a single same-address counter saturates at ~88 atomics/us,
+// MI355X_MICROARCH.md "dequeue").  The regions interleave at chunk
+// granularity -- local chunk l of region r is global chunk l * kRegions + r
+// -- so every region fills the bottom of the buffer: the holes below the
+// total are only the waves' last, partly filled chunks and the few chunks of
+// the regions' imbalance, which k_fix_* close.
+constexpr int kOutChunk = 1024, kOutChunkLog = 10, kRegionsLog = 3;
+static_assert((1 << kOutChunkLog) == kOutChunk && (1 << kRegionsLog) == kRegions, "output layout");
 struct OutArgs {
     uint32_t *q, *e;
     int64_t rcap;                  // slots per region (a multiple of kOutChunk)
-    uint32_t *fills;               // per chunk of all regions: pairs written (0 = unreserved)
-    unsigned long long *octr;      // kRegions reservation counters, kRegStride words apart
+    uint32_t *fills;               // per global chunk: pairs written (0 = unreserved)
+    unsigned long long *octr;      // kRegions reservation counters (local slots), kRegStride words apart
     unsigned long long *counter;   // [0] pairs [1] tagged [2] lane tests [3] broadcasts
 };
 
@@ -978,20 +981,23 @@ __device__ __forceinline__ unsigned long long uni64(unsigned long long x)
 // Per-wave output state, wave-uniform by construction (readfirstlane keeps
 // it in scalar registers: no exec-mask traffic around the chunk test).
 struct WaveOut {
-    unsigned long long base = 0;
+    unsigned long long base = 0;  // global slot of the current chunk
     int fill = kOutChunk;  // no chunk yet
     int have = 0;
     unsigned long long pairs = 0;  // wave-uniform
     unsigned long long tagged = 0;  // per lane
     // wave-uniform call: room for `total` (> 0) pairs.  The batch first fills
     // what is left of the current chunk, the rest goes to ceil(rest /
-    // kOutChunk) fresh chunks; pair i of the batch lands at at(i).
+    // kOutChunk) fresh chunks of the region (kRegions global chunks apart);
+    // pair i of the batch lands at at(i).
     struct Span {
-        unsigned long long a0, a1;  // a0 + i for i < n0, else a1 + i
+        unsigned long long a0, g0;  // a0 + i for i < n0; else chunk-strided from g0
         int n0;
         __device__ __forceinline__ unsigned long long at(unsigned long long i) const
         {
-            return (i < (unsigned long long)n0 ? a0 : a1) + i;
+            if (i < (unsigned long long)n0) return a0 + i;
+            const unsigned long long j = i - (unsigned long long)n0;
+            return g0 + ((j >> kOutChunkLog) << (kOutChunkLog + kRegionsLog)) + (j & (kOutChunk - 1));
         }
     };
     __device__ __forceinline__ Span reserve(const OutArgs &o, int total)
@@ -1001,7 +1007,7 @@ struct WaveOut {
         sp.a0 = base + (unsigned long long)fill;
         if (fill + total <= kOutChunk) {
             sp.n0 = total;
-            sp.a1 = sp.a0;
+            sp.g0 = sp.a0;
             fill = uni32(fill + total);
             return sp;
         }
@@ -1018,17 +1024,18 @@ struct WaveOut {
             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 0);
         // else the region is full: counted, not written (rerun)
         have = uni32((int64_t)b + (int64_t)nch * kOutChunk <= o.rcap);
-        const unsigned long long st = uni64(have ? (unsigned long long)reg * (unsigned long long)o.rcap + b : 0ull);
+        const unsigned long long lc = b >> kOutChunkLog;  // first local chunk
         if (have)  // the chunks before the last are full
-            for (int c = threadIdx.x & 63; c < nch - 1; c += 64) o.fills[st / kOutChunk + c] = (uint32_t)kOutChunk;
-        sp.a1 = st - (unsigned long long)sp.n0;
-        base = uni64(st + (unsigned long long)(nch - 1) * kOutChunk);
+            for (int c = threadIdx.x & 63; c < nch - 1; c += 64)
+                o.fills[((lc + (unsigned long long)c) << kRegionsLog) | (unsigned long long)reg] = (uint32_t)kOutChunk;
+        sp.g0 = uni64(((lc << kRegionsLog) | (unsigned long long)reg) << kOutChunkLog);
+        base = uni64((((lc + (unsigned long long)(nch - 1)) << kRegionsLog) | (unsigned long long)reg) << kOutChunkLog);
         fill = uni32(rest - (nch - 1) * kOutChunk);
         return sp;
     }
     __device__ __forceinline__ void retire(const OutArgs &o)
     {
-        if (have && (threadIdx.x & 63) == 0) o.fills[base / kOutChunk] = (uint32_t)fill;
+        if (have && (threadIdx.x & 63) == 0) o.fills[base >> kOutChunkLog] = (uint32_t)fill;
         have = 0;
     }
     __device__ __forceinline__ void finish(const OutArgs &o)
@@ -1330,7 +1337,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
 // Closing the output holes: chunk c holds fills[c] pairs at c * kOutChunk
 // (0 = never reserved); with n pairs in all, the holes below n are filled
 // with the pairs at or above n, in order.  k_fix_counts: per chunk its holes
-// below n and its pairs at or above n; k_fix_fill: one block per chunk below
+// below n and its pairs at or above n; k_fix_fill: a block per chunk below
 // n walks its holes and finds each source in the (few) chunks at or above n.
 __global__ void k_fix_counts(int64_t nch, const uint32_t *fills, int64_t n, int64_t *hole, int64_t *tail)
 {
@@ -1342,46 +1349,49 @@ __global__ void k_fix_counts(int64_t nch, const uint32_t *fills, int64_t n, int6
     hole[c] = h1 > h0 ? h1 - h0 : 0;
     tail[c] = t1 > t0 ? t1 - t0 : 0;
 }
-__global__ void k_fix_fill(int64_t nch, const uint32_t *fills, int64_t n, const int64_t *hole, const int64_t *hoff,
-                           const int64_t *toff, uint32_t *q, uint32_t *e)
+__global__ void k_fix_fill(int64_t nch, int64_t nbelow, const uint32_t *fills, int64_t n, const int64_t *hole,
+                           const int64_t *hoff, const int64_t *toff, uint32_t *q, uint32_t *e)
 {
-    const int64_t c = blockIdx.x;
-    const int64_t h = hole[c];
-    if (h == 0) return;
-    // the tail chunk of this block's first source, found once (thread 0); each
-    // thread gallops forward from it to its own source's chunk
+    // a fixed grid strides over the chunks below n; full ones are skipped
     __shared__ int64_t s_lo;
-    if (threadIdx.x == 0) {
-        int64_t lo = n / kOutChunk, hi = nch;  // tail chunk tc with toff[tc] <= t < toff[tc + 1]
-        const int64_t t0 = hoff[c];
-        while (hi - lo > 1) {
-            const int64_t mid = (lo + hi) >> 1;
-            if (toff[mid] <= t0) lo = mid;
-            else hi = mid;
+    for (int64_t c = blockIdx.x; c < nbelow; c += gridDim.x) {
+        const int64_t h = hole[c];
+        if (h == 0) continue;
+        // the tail chunk of this chunk's first source, found once (thread 0);
+        // each thread gallops forward from it to its own source's chunk
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t lo = n / kOutChunk, hi = nch;  // tail chunk tc with toff[tc] <= t < toff[tc + 1]
+            const int64_t t0 = hoff[c];
+            while (hi - lo > 1) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (toff[mid] <= t0) lo = mid;
+                else hi = mid;
+            }
+            s_lo = lo;
         }
-        s_lo = lo;
-    }
-    __syncthreads();
-    const int64_t lo0 = s_lo;
-    for (int64_t k = threadIdx.x; k < h; k += blockDim.x) {
-        const int64_t t = hoff[c] + k;  // its source: the t-th pair at or above n
-        // galloping from the block's first source chunk (runs of empty tail
-        // chunks -- unreserved region space -- are skipped in O(log) steps)
-        int64_t lo = lo0, step = 1;
-        while (lo + step < nch && toff[lo + step] <= t) {
-            lo += step;
-            step <<= 1;
+        __syncthreads();
+        const int64_t lo0 = s_lo;
+        for (int64_t k = threadIdx.x; k < h; k += blockDim.x) {
+            const int64_t t = hoff[c] + k;  // its source: the t-th pair at or above n
+            // galloping from the chunk's first source chunk (runs of empty
+            // tail chunks -- unreserved space -- are skipped in O(log) steps)
+            int64_t lo = lo0, step = 1;
+            while (lo + step < nch && toff[lo + step] <= t) {
+                lo += step;
+                step <<= 1;
+            }
+            int64_t hi = lo + step < nch ? lo + step : nch;
+            while (hi - lo > 1) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (toff[mid] <= t) lo = mid;
+                else hi = mid;
+            }
+            const int64_t src = max(lo * kOutChunk, n) + (t - toff[lo]);
+            const int64_t dst = c * kOutChunk + fills[c] + k;
+            q[dst] = q[src];
+            e[dst] = e[src];
         }
-        int64_t hi = lo + step < nch ? lo + step : nch;
-        while (hi - lo > 1) {
-            const int64_t mid = (lo + hi) >> 1;
-            if (toff[mid] <= t) lo = mid;
-            else hi = mid;
-        }
-        const int64_t src = max(lo * kOutChunk, n) + (t - toff[lo]);
-        const int64_t dst = c * kOutChunk + fills[c] + k;
-        q[dst] = q[src];
-        e[dst] = e[src];
     }
 }
 
@@ -2039,8 +2049,8 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             exclusive_scan_i64(hole, hoff, nch, tmp2_, s);
             exclusive_scan_i64(tail, toff, nch, tmp2_, s);
             if (nbelow > 0)
-                hipLaunchKernelGGL(k_fix_fill, dim3((unsigned)nbelow), dim3(kBlock), 0, s, nch, fills, n, hole, hoff, toff,
-                                   oq, oe);
+                hipLaunchKernelGGL(k_fix_fill, dim3((unsigned)std::min<int64_t>(nbelow, (int64_t)n_cu_ * 4)),
+                                   dim3(kBlock), 0, s, nch, nbelow, fills, n, hole, hoff, toff, oq, oe);
         }
         if (ntag == 0) {
             out->q = oq;
