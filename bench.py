@@ -114,6 +114,8 @@ def main():
                          "dssg_sharded_search_device) or torch (torch.distributed; the instrumented path).  Default: "
                          "native with --dist-backend nccl, torch otherwise")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on a multi-GPU node; gloo for rehearsals")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="dssg_set_tuning knob for every pipeline's context (e.g. lazy_sig_recs=0)")
     ap.add_argument("--pipelines", type=int, default=3,
                     help="concurrent batch pipelines per GPU (own engine context + stream + host thread each): one "
                          "batch's FP64 covering overlaps another's join, as concurrent RPCs would (replica mode)")
@@ -148,6 +150,9 @@ def main():
 
     ctx = _lib.context(local)
     dev = f"cuda:{local}"
+    tunes = [(kv.split("=", 1)[0], int(kv.split("=", 1)[1])) for kv in args.tune]
+    for k, v in tunes:
+        ctx.set_tuning(k, v)
 
     # ---------------------------------------------------------------- setup
     t_setup = time.time()
@@ -225,6 +230,8 @@ def main():
     if args.pipelines > 1 and sharded is None:
         for k in range(args.pipelines - 1):
             wctx = _lib.Context(local)
+            for k, v in tunes:
+                wctx.set_tuning(k, v)
             wstream = torch.cuda.Stream(device=dev)
             workers.append((wctx, wstream))
 

@@ -235,6 +235,10 @@ int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value)
         ctx->search.set_tag_bucket_avg(value);
         return DSSG_OK;
     }
+    if (std::string(key) == "lazy_sig_recs") {
+        ctx->search.set_lazy_sig_recs(value);
+        return DSSG_OK;
+    }
     return DSSG_ERR_INVALID;
 }
 

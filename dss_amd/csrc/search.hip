@@ -48,7 +48,6 @@ constexpr uint32_t kRank0 = 0x80000000u;     // record: the cell is the query's 
 constexpr uint32_t kCompactQ = 0x40000000u;  // record: the query's prefix at this cell is compact
 constexpr uint32_t kLongQ = 0x20000000u;     // record: the query footprint is long (long_cells)
 constexpr uint32_t kQFlags = kRank0 | kCompactQ | kLongQ;
-constexpr uint32_t kTag = 0x80000000u;  // output: a long x long pair, deduplicated after the join
 constexpr uint32_t kNoDecode = 0xffffffffu;
 constexpr uint32_t kNoSlot = 0xffffffffu;
 // Query windows wider than this (us, ~72 min) form their own per-cell runs:
@@ -963,12 +962,21 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m)
 // the regions' imbalance, which k_fix_* close.
 constexpr int kOutChunk = 1024, kOutChunkLog = 10, kRegionsLog = 3;
 static_assert((1 << kOutChunkLog) == kOutChunk && (1 << kRegionsLog) == kRegions, "output layout");
+struct OutStream {
+    int64_t rcap;                  // slots per region (a multiple of kOutChunk)
+    uint32_t *fills;               // per global chunk: entries written (0 = unreserved)
+    unsigned long long *octr;      // kRegions reservation counters (local slots), kRegStride words apart
+};
+// Two streams: the pairs (q, e), final as written, and the long x long pairs
+// the signatures cannot decide, as 64-bit keys (q << eb | e) << hbm | hbm
+// hash bits of the pair, deduplicated after the join.
 struct OutArgs {
     uint32_t *q, *e;
-    int64_t rcap;                  // slots per region (a multiple of kOutChunk)
-    uint32_t *fills;               // per global chunk: pairs written (0 = unreserved)
-    unsigned long long *octr;      // kRegions reservation counters (local slots), kRegStride words apart
-    unsigned long long *counter;   // [0] pairs [1] tagged [2] lane tests [3] broadcasts
+    OutStream ps;
+    unsigned long long *tk;
+    OutStream ts;
+    int eb, hbm;
+    unsigned long long *counter;   // [0] pairs [1] tagged keys [2] lane tests [3] broadcasts
 };
 
 __device__ __forceinline__ int uni32(int x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -985,7 +993,6 @@ struct WaveOut {
     int fill = kOutChunk;  // no chunk yet
     int have = 0;
     unsigned long long pairs = 0;  // wave-uniform
-    unsigned long long tagged = 0;  // per lane
     // wave-uniform call: room for `total` (> 0) pairs.  The batch first fills
     // what is left of the current chunk, the rest goes to ceil(rest /
     // kOutChunk) fresh chunks of the region (kRegions global chunks apart);
@@ -1000,7 +1007,7 @@ struct WaveOut {
             return g0 + ((j >> kOutChunkLog) << (kOutChunkLog + kRegionsLog)) + (j & (kOutChunk - 1));
         }
     };
-    __device__ __forceinline__ Span reserve(const OutArgs &o, int total)
+    __device__ __forceinline__ Span reserve(const OutStream &o, int total)
     {
         pairs += (unsigned long long)total;
         Span sp;
@@ -1033,28 +1040,43 @@ struct WaveOut {
         fill = uni32(rest - (nch - 1) * kOutChunk);
         return sp;
     }
-    __device__ __forceinline__ void retire(const OutArgs &o)
+    __device__ __forceinline__ void retire(const OutStream &o)
     {
         if (have && (threadIdx.x & 63) == 0) o.fills[base >> kOutChunkLog] = (uint32_t)fill;
         have = 0;
     }
-    __device__ __forceinline__ void finish(const OutArgs &o)
+    __device__ __forceinline__ void finish(const OutStream &o, unsigned long long *counter)
     {
         retire(o);
-        unsigned long long t = tagged;  // per lane: sum over the wave
-        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
-        if ((threadIdx.x & 63) == 0 && pairs) {
-            atomicAdd(&o.counter[0], pairs);
-            if (t) atomicAdd(&o.counter[1], t);
-        }
+        if ((threadIdx.x & 63) == 0 && pairs) atomicAdd(counter, pairs);
     }
 };
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x)
+{
+    x ^= x >> 31;
+    x *= 0x7fb5d329728ea185ull;
+    x ^= x >> 27;
+    x *= 0x81dadef4bc2dd44dull;
+    x ^= x >> 33;
+    return x;
+}
+
+// tagged-stream key of (q, e): the pair over hbm (3..24) bits of a cheap
+// two-multiply hash of it (only bucketing: equal pairs, equal buckets)
+__device__ __forceinline__ unsigned long long tag_key(uint32_t q, uint32_t e, int eb, int hbm)
+{
+    const unsigned long long pk = ((unsigned long long)q << eb) | e;
+    const uint32_t h = (q * 0x9e3779b1u) ^ (e * 0x85ebca77u);
+    return (pk << hbm) | (h >> (32 - hbm));
+}
 
 struct JoinArgs {
     IndexView ix;
     QueryView qv;
     Regions ur;                        // units (k_units)
     OutArgs out;
+    uint32_t lazy_sig_recs;            // units with more records prefetch the posting signatures
 };
 
 // One wavefront per unit, lane = posting (the tile stays in registers); the
@@ -1077,7 +1099,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const IndexView &ix = a.ix;
-    WaveOut out;
+    WaveOut out, tout;  // pairs, tagged keys
     unsigned long long n_tests = 0, n_bcast = 0;
     // units: kRegions queues (the unit regions), a wave starts on its own
     // region's and moves on when it is drained; grabs of g units per atomic
@@ -1114,6 +1136,10 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
     uint32_t ne = 0, nmeta = 0;
     int32_t nown = 0;
     ulonglong2 ns01 = make_ulonglong2(0, 0), ns23 = make_ulonglong2(0, 0);
+    bool nsig = false;
+    // A unit with few records (the sparse case: a cell scanned for a handful
+    // of queries) leaves the posting signatures (32 of the 61 bytes) to be
+    // loaded later, only by the lanes that need the smallest-shared-cell test.
     auto prefetch = [&](int64_t u) {
         dn = units[u];
         nt = make_longlong2(LLONG_MAX, LLONG_MIN);
@@ -1121,15 +1147,18 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
         ne = nmeta = 0;
         nown = 0;
         ns01 = ns23 = make_ulonglong2(0, 0);
-        const bool any = dn.n1 > dn.n0 || dn.w1 > dn.w0;  // a tile no record can meet is skipped unloaded
-        if (any && (uint32_t)lane < (dn.np & ~kUnitLong)) {
+        const uint32_t nrec = (dn.n1 > dn.n0 ? dn.n1 - dn.n0 : 0u) + (dn.w1 > dn.w0 ? dn.w1 - dn.w0 : 0u);
+        nsig = nrec > a.lazy_sig_recs;
+        if (nrec && (uint32_t)lane < (dn.np & ~kUnitLong)) {  // a tile no record can meet is skipped unloaded
             const uint64_t p = dn.p0 + lane;
             ne = ix.b_e[p];
             nmeta = ix.b_meta[p];
             nt = ix.b_t[p];
             na = ix.b_alt[p];
-            ns01 = ix.b_sig[2 * p];
-            ns23 = ix.b_sig[2 * p + 1];
+            if (nsig) {
+                ns01 = ix.b_sig[2 * p];
+                ns23 = ix.b_sig[2 * p + 1];
+            }
             if (OWNER) nown = ix.b_owner[p];
         }
     };
@@ -1149,7 +1178,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
         const float2 pa = na;
         const uint32_t pe = ne, pmeta = nmeta;
         const int32_t pown = nown;
-        const ulonglong2 ps01 = ns01, ps23 = ns23;
+        ulonglong2 ps01 = ns01, ps23 = ns23;
+        const bool usig = nsig;  // the signatures are loaded (else: per lane, on first need)
+        bool lsig = false;
         const bool pv = (uint32_t)lane < np && !is_dead(ix, pe & ~kFirstBit);  // tombstones match nothing
         un = next_unit();
         if (un >= 0) prefetch(un);
@@ -1164,7 +1195,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
         if (!(d.np & kUnitLong)) {
             const long long m = tmin2(pt.x, pt.y);
             t0min = readlane64(m, 0);  // <= every t0 of the tile
+#ifndef DSS_XP_NOHULL
             t1max = wave_max_i64((uint32_t)lane < np ? (pt.x > pt.y ? pt.x : pt.y) : LLONG_MIN);
+#endif
         }
         const uint32_t ra0 = d.n0, ra1 = d.n1, rb0 = d.w0, rb1 = d.w1;
         const bool pfirst = (pe & kFirstBit) != 0;                  // entity's smallest cell
@@ -1248,6 +1281,21 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
                 // tagged set is deduplicated after the join); else exact merge.
                 unsigned long long keep = pfirst ? m : (m & R0);
                 unsigned long long need = m & ~keep;
+#ifdef DSS_XP_NOSIG  // timing experiment only: no smallest-shared-cell test
+                keep = m;
+                need = 0;
+#endif
+                if (!usig) {  // lazy signatures: the lanes that need them now
+                    const bool want = need != 0ull && !lsig;
+                    if (__ballot(want)) {
+                        if (want) {
+                            const uint64_t p = d.p0 + (uint64_t)lane;
+                            ps01 = ix.b_sig[2 * p];
+                            ps23 = ix.b_sig[2 * p + 1];
+                            lsig = true;
+                        }
+                    }
+                }
                 // lane-major (each lane walks its own checks) for full batches;
                 // record-major (one broadcast signature per record) for small ones
                 if (nrel > 16) {
@@ -1287,47 +1335,76 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
                         if ((kj >> lane) & 1ull) keep |= 1ull << j;
                     }
                 }
-                // (3) emission, the batch's pairs contiguous: lane-major (each lane's
-                // pairs after the lanes before it; iterations = the largest lane
-                // count) at low pass density, else record-major (one coalesced row
-                // per record: dense batches would scatter too many lane stores)
-                const uint32_t cnt = (uint32_t)__popcll(keep);
-                const uint32_t incl = wave_incl_scan(cnt);
-                const int total = uni32(__builtin_amdgcn_readlane((int)incl, 63));
-                if (!total) continue;
-                const WaveOut::Span sp = out.reserve(a.out, total);
-                if (LONG && plong) out.tagged += (unsigned long long)__popcll(keep & RL);
-                if (!out.have) continue;
-                if ((int64_t)total * 4 <= (int64_t)nrel * __popcll(vmask)) {  // pass density <= 1/4
-                    unsigned long long i = incl - cnt;
-                    unsigned long long kk = keep;
-                    while (kk) {
-                        const int j = __builtin_ctzll(kk);
-                        kk &= kk - 1;
-                        const uint32_t q = (uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags;
-                        const unsigned long long pos = sp.at(i++);
-                        a.out.q[pos] = q | ((plong && ((RL >> j) & 1ull)) ? kTag : 0u);
-                        a.out.e[pos] = pent;
+                // (3) emission, the batch's pairs contiguous per stream (pairs;
+                // long x long keys): lane-major (each lane's pairs after the
+                // lanes before it; iterations = the largest lane count) at low
+                // pass density, else record-major (one coalesced row per record:
+                // dense batches would scatter too many lane stores).  Both
+                // streams' counts ride one scan (16-bit halves: <= 64 x 64).
+                const unsigned long long tagm = (LONG && plong) ? (keep & RL) : 0ull;
+                const uint32_t cu = (uint32_t)__popcll(keep & ~tagm), ct = (uint32_t)__popcll(tagm);
+                const uint32_t incl = wave_incl_scan(cu | (ct << 16));
+                const uint32_t tot = (uint32_t)uni32(__builtin_amdgcn_readlane((int)incl, 63));
+                const int total_u = (int)(tot & 0xffffu), total_t = LONG ? (int)(tot >> 16) : 0;
+                if (!(total_u | total_t)) continue;
+                WaveOut::Span su{}, st{};
+                if (total_u) su = out.reserve(a.out.ps, total_u);
+                if (LONG && total_t) st = tout.reserve(a.out.ts, total_t);
+#ifdef DSS_XP_NOEMIT  // timing experiment only: reserved, not written
+                continue;
+#endif
+                const bool wu = out.have != 0, wt = LONG && tout.have != 0;  // else counted only (rerun)
+                if ((int64_t)(total_u + total_t) * 4 <= (int64_t)nrel * __popcll(vmask)) {  // pass density <= 1/4
+                    // (one loop per stream: no divergent double bodies)
+                    if (wu) {
+                        unsigned long long iu = (incl & 0xffffu) - cu, kk = keep & ~tagm;
+                        while (kk) {
+                            const int j = __builtin_ctzll(kk);
+                            kk &= kk - 1;
+                            const uint32_t q = (uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags;
+                            const unsigned long long pos = su.at(iu++);
+                            a.out.q[pos] = q;
+                            a.out.e[pos] = pent;
+                        }
+                    }
+                    if (LONG && wt) {
+                        unsigned long long it = (incl >> 16) - ct, kk = tagm;
+                        while (kk) {
+                            const int j = __builtin_ctzll(kk);
+                            kk &= kk - 1;
+                            const uint32_t q = (uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags;
+                            a.out.tk[st.at(it++)] = tag_key(q, pent, a.out.eb, a.out.hbm);
+                        }
                     }
                 } else {
-                    unsigned long long off = 0;
+                    const unsigned long long lm = LONG ? __ballot(plong) : 0ull;
+                    unsigned long long ou = 0, ot = 0;
                     for (int j = 0; j < nrel; j++) {
                         const unsigned long long kj = __ballot((keep >> j) & 1ull);
                         if (!kj) continue;
+                        const unsigned long long kt = (LONG && ((RL >> j) & 1ull)) ? (kj & lm) : 0ull, ku = kj & ~kt;
                         const uint32_t q =
                             (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s_ra[w][j].z)) & ~kQFlags;
-                        if ((kj >> lane) & 1ull) {
-                            const unsigned long long pos = sp.at(off + mbcnt64(kj));
-                            a.out.q[pos] = q | ((plong && ((RL >> j) & 1ull)) ? kTag : 0u);
-                            a.out.e[pos] = pent;
+                        if ((ku >> lane) & 1ull) {
+                            const unsigned long long pos = su.at(ou + mbcnt64(ku));
+                            if (wu) {
+                                a.out.q[pos] = q;
+                                a.out.e[pos] = pent;
+                            }
                         }
-                        off += (unsigned long long)__popcll(kj);
+                        if (LONG && ((kt >> lane) & 1ull)) {
+                            const unsigned long long pos = st.at(ot + mbcnt64(kt));
+                            if (wt) a.out.tk[pos] = tag_key(q, pent, a.out.eb, a.out.hbm);
+                        }
+                        ou += (unsigned long long)__popcll(ku);
+                        ot += (unsigned long long)__popcll(kt);
                     }
                 }
             }
         }
     }
-    out.finish(a.out);
+    out.finish(a.out.ps, &a.out.counter[0]);
+    if (LONG) tout.finish(a.out.ts, &a.out.counter[1]);
     if (lane == 0) {
         atomicAdd(&a.out.counter[2], n_tests);
         atomicAdd(&a.out.counter[3], n_bcast);
@@ -1349,8 +1426,21 @@ __global__ void k_fix_counts(int64_t nch, const uint32_t *fills, int64_t n, int6
     hole[c] = h1 > h0 ? h1 - h0 : 0;
     tail[c] = t1 > t0 ? t1 - t0 : 0;
 }
+struct MovePairs {
+    uint32_t *q, *e;
+    __device__ void operator()(int64_t dst, int64_t src) const
+    {
+        q[dst] = q[src];
+        e[dst] = e[src];
+    }
+};
+struct MoveKeys {
+    unsigned long long *k;
+    __device__ void operator()(int64_t dst, int64_t src) const { k[dst] = k[src]; }
+};
+template <typename Move>
 __global__ void k_fix_fill(int64_t nch, int64_t nbelow, const uint32_t *fills, int64_t n, const int64_t *hole,
-                           const int64_t *hoff, const int64_t *toff, uint32_t *q, uint32_t *e)
+                           const int64_t *hoff, const int64_t *toff, Move mv)
 {
     // a fixed grid strides over the chunks below n; full ones are skipped
     __shared__ int64_t s_lo;
@@ -1388,75 +1478,36 @@ __global__ void k_fix_fill(int64_t nch, int64_t nbelow, const uint32_t *fills, i
                 else hi = mid;
             }
             const int64_t src = max(lo * kOutChunk, n) + (t - toff[lo]);
-            const int64_t dst = c * kOutChunk + fills[c] + k;
-            q[dst] = q[src];
-            e[dst] = e[src];
+            mv(c * kOutChunk + fills[c] + k, src);
         }
     }
 }
 
-// Tagged (long x long) pairs after the join.  One split pass sends the
-// untagged pairs to (q2, e2) and the tagged ones to 64-bit keys
-// ((q << eb | e) << hb | bucket), bucket = hb hash bits of the pair; a radix
-// sort over the hb bucket bits only (ceil(hb / 8) passes instead of a full
-// 40+-bit sort) groups equal pairs in one bucket of ~1024 keys (tunable), and
+// Tagged (long x long) pairs after the join, which writes them as 64-bit keys
+// ((q << eb | e) << hbm | hbm hash bits of the pair) to their own stream; a
+// radix sort over hb <= hbm low hash bits only (ceil(hb / 8) passes instead
+// of a full 40+-bit sort) groups equal pairs in one bucket of ~1024 keys
+// (tunable), and
 // one block per bucket removes the duplicates in an LDS hash set.  A bucket
 // too large for the LDS set (never at the average) falls back to a full sort
 // of its keys.
 constexpr int kDedupBlock = 256, kDedupSlots = 4096;  // 32 KB of LDS: several blocks per CU
 constexpr int64_t kDedupMax = kDedupSlots * 3 / 4;
 
-__device__ __forceinline__ unsigned long long mix64(unsigned long long x)
-{
-    x ^= x >> 31;
-    x *= 0x7fb5d329728ea185ull;
-    x ^= x >> 27;
-    x *= 0x81dadef4bc2dd44dull;
-    x ^= x >> 33;
-    return x;
-}
-
-struct PredTag {
-    const uint32_t *q;
-    bool tagged;
-    __device__ bool operator()(int64_t i) const { return ((q[i] & kTag) != 0) == tagged; }
-};
-struct EmitUntagged {
-    const uint32_t *q, *e;
-    uint32_t *q2, *e2;
-    __device__ void operator()(int64_t i, int64_t r) const
-    {
-        q2[r] = q[i];
-        e2[r] = e[i];
-    }
-};
-struct EmitTagKey {  // hb == 0: the plain (q << 32 | e) key of the full-sort path
-    const uint32_t *q, *e;
-    unsigned long long *key;
-    int eb, hb;
-    __device__ void operator()(int64_t i, int64_t r) const
-    {
-        if (hb == 0) {
-            key[r] = ((unsigned long long)(q[i] & ~kTag) << 32) | e[i];
-            return;
-        }
-        const unsigned long long pk = ((unsigned long long)(q[i] & ~kTag) << eb) | e[i];
-        key[r] = (pk << hb) | (mix64(pk) >> (64 - hb));
-    }
-};
 struct PredRunU64 {
     const unsigned long long *k;
     __device__ bool operator()(int64_t i) const { return i == 0 || k[i] != k[i - 1]; }
 };
-struct EmitPairFromKey {  // key = q << eb | e
+struct EmitPairFromKey {  // key >> sh = q << eb | e
     const unsigned long long *k;
     uint32_t *q, *e;
     int64_t at;
-    int eb;
+    int eb, sh;
     __device__ void operator()(int64_t i, int64_t r) const
     {
-        q[at + r] = (uint32_t)(k[i] >> eb);
-        e[at + r] = (uint32_t)(k[i] & ((1ull << eb) - 1));
+        const unsigned long long pk = k[i] >> sh;
+        q[at + r] = (uint32_t)(pk >> eb);
+        e[at + r] = (uint32_t)(pk & ((1ull << eb) - 1));
     }
 };
 
@@ -1471,11 +1522,11 @@ __global__ void k_tag_bounds(int64_t n, const unsigned long long *__restrict__ k
     if (i == n - 1 || (k[i + 1] & m) != b) be[b] = i + 1;
 }
 
-// One block per bucket: its distinct pairs (keys >> hb) into stage[bs[b] ..),
+// One block per bucket: its distinct pairs (keys >> hbm) into stage[bs[b] ..),
 // their count into cnt[b]; a bucket over kDedupMax keys is flagged instead.
 __global__ __launch_bounds__(kDedupBlock) void k_tag_dedupe(const unsigned long long *__restrict__ k,
                                                              const int64_t *__restrict__ bs,
-                                                             const int64_t *__restrict__ be, int hb,
+                                                             const int64_t *__restrict__ be, int hbm,
                                                              unsigned long long *__restrict__ stage,
                                                              int64_t *__restrict__ cnt, uint8_t *__restrict__ ovf,
                                                              unsigned long long *__restrict__ novf)
@@ -1506,7 +1557,7 @@ __global__ __launch_bounds__(kDedupBlock) void k_tag_dedupe(const unsigned long 
     if (tid == 0) nout = 0;
     __syncthreads();
     for (int64_t i = lo + tid; i < hi; i += kDedupBlock) {
-        const unsigned long long pk = k[i] >> hb;
+        const unsigned long long pk = k[i] >> hbm;
         uint32_t h = (uint32_t)mix64(pk ^ 0x9e3779b97f4a7c15ull) & smask;
         while (true) {  // fewer distinct keys than slots: a free slot always exists
             const unsigned long long prev = atomicCAS(&tab[h], kEmpty, pk);
@@ -1593,8 +1644,8 @@ struct PredOvf {  // keys of the flagged buckets
 struct EmitShift {
     const unsigned long long *k;
     unsigned long long *out;
-    int hb;
-    __device__ void operator()(int64_t i, int64_t r) const { out[r] = k[i] >> hb; }
+    int sh;
+    __device__ void operator()(int64_t i, int64_t r) const { out[r] = k[i] >> sh; }
 };
 
 // Roofline accounting, predicate off: M = postings scanned query-cell by
@@ -1931,7 +1982,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     // heads, output region counters -- kRegStride words between counters
     constexpr int kR = kRegions * kRegStride;
     constexpr int kCtlDq = 0, kCtlUnits = kR, kCtlMisc = 2 * kR, kCtlQueue = 2 * kR + 16, kCtlOut = 3 * kR + 16,
-                  kCtlWords = 4 * kR + 16;
+                  kCtlTOut = 4 * kR + 16, kCtlWords = 5 * kR + 16;
     unsigned long long *ctl = counter_.ensure(kCtlWords);
     unsigned long long *cnt = ctl + kCtlMisc;
     DSS_HIP(hipMemsetAsync(ctl, 0, kCtlWords * sizeof(unsigned long long), s));
@@ -1987,17 +2038,39 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     JoinArgs ja{};
     ja.ix = ix;
     ja.qv = qv;
+    ja.lazy_sig_recs = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(lazy_sig_recs_, 0xffffffffll));
     const unsigned nblocks = (unsigned)n_cu_ * kJoinBlocksPerCU;
     if (out_rcap_ == 0) out_rcap_ = ((int64_t)nq * 16 / kRegions / kOutChunk + 2) * kOutChunk;
     const bool any_long = idx->n_long_fp > 0;  // the batch's long flag is only known on the device
-    for (int attempt = 0; attempt < 5; attempt++) {
+    if (any_long && tag_rcap_ == 0) tag_rcap_ = ((int64_t)nq * 4 / kRegions / kOutChunk + 2) * kOutChunk;
+    const int qb = bits_for(nq), eb = bits_for(idx->n_e);
+    const int hbm = std::min(24, 64 - qb - eb);  // qb <= 29, eb <= 32: 3 <= hbm <= 24
+    // closing the holes of partly filled / unreserved chunks below n with the
+    // entries at or above n
+    auto close_holes = [&](int64_t nch, const uint32_t *fills, int64_t n, auto mover) {
+        const int64_t nbelow = std::min<int64_t>(nch, (n + kOutChunk - 1) / kOutChunk);
+        int64_t *hole = cnt64_.ensure(4 * (nch + 2)), *tail = hole + (nch + 2);
+        int64_t *hoff = tail + (nch + 2), *toff = hoff + (nch + 2);
+        hipLaunchKernelGGL(k_fix_counts, dim3(grid_for(nch, kBlock)), dim3(kBlock), 0, s, nch, fills, n, hole, tail);
+        exclusive_scan_i64(hole, hoff, nch, tmp2_, s);
+        exclusive_scan_i64(tail, toff, nch, tmp2_, s);
+        if (nbelow > 0)
+            hipLaunchKernelGGL(k_fix_fill<decltype(mover)>, dim3((unsigned)std::min<int64_t>(nbelow, (int64_t)n_cu_ * 4)),
+                               dim3(kBlock), 0, s, nch, nbelow, fills, n, hole, hoff, toff, mover);
+    };
+    for (int attempt = 0; attempt < 6; attempt++) {
         const int64_t cap = kRegions * out_rcap_, nch = cap / kOutChunk;
         uint32_t *oq = oq_.ensure(cap + 1), *oe = oe_.ensure(cap + 1);
-        uint32_t *fills = fills_.ensure(nch + 1);
-        DSS_HIP(hipMemsetAsync(fills, 0, sizeof(uint32_t) * nch, s));
-        DSS_HIP(hipMemsetAsync(ctl + kCtlMisc, 0, (kCtlWords - kCtlMisc) * sizeof(unsigned long long), s));
+        const int64_t tcap = any_long ? kRegions * tag_rcap_ : 0, tnch = tcap / kOutChunk;
+        uint32_t *fills = fills_.ensure(nch + tnch + 1), *tfills = fills + nch;
+        unsigned long long *tk = any_long ? tkey_.ensure(tcap + 1) : nullptr;
+        DSS_HIP(hipMemsetAsync(fills, 0, sizeof(uint32_t) * (nch + tnch), s));
+        // (misc word 5, the long-query count of k_cell_query, survives)
+        DSS_HIP(hipMemsetAsync(ctl + kCtlMisc, 0, 5 * sizeof(unsigned long long), s));
+        DSS_HIP(hipMemsetAsync(ctl + kCtlMisc + 6, 0, (kCtlWords - kCtlMisc - 6) * sizeof(unsigned long long), s));
         ja.ur = Regions{ctl + kCtlUnits, ucap};
-        ja.out = OutArgs{oq, oe, out_rcap_, fills, ctl + kCtlOut, cnt};
+        ja.out = OutArgs{oq, oe, OutStream{out_rcap_, fills, ctl + kCtlOut}, tk, OutStream{tag_rcap_, tfills, ctl + kCtlTOut},
+                         eb, hbm, cnt};
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
         auto kern = q_owner ? (any_long ? k_join<true, true> : k_join<true, false>)
                             : (any_long ? k_join<false, true> : k_join<false, false>);
@@ -2007,12 +2080,13 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         unsigned long long h[kCtlWords];
         DSS_HIP(hipMemcpyAsync(h, ctl, sizeof(h), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipStreamSynchronize(s));
-        int64_t nu = 0, umax = 0, omax = 0;
+        int64_t nu = 0, umax = 0, omax = 0, tmax = 0;
         for (int r = 0; r < kRegions; r++) {
             const int64_t u = (int64_t)h[kCtlUnits + r * kRegStride];
             nu += u;
             umax = std::max(umax, u);
             omax = std::max(omax, (int64_t)h[kCtlOut + r * kRegStride]);
+            tmax = std::max(tmax, (int64_t)h[kCtlTOut + r * kRegStride]);
         }
         if (umax > ucap) {  // the units did not fit: regrow, rebuild them, rerun the join
             ucap = umax + umax / 4 + 1024;
@@ -2020,11 +2094,17 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             continue;
         }
         units_cap_hint_ = std::max<int64_t>(units_cap_hint_, umax + umax / 8);
+        bool rerun = false;
         if (omax > out_rcap_) {  // an output region filled up: regrow (per region) and rerun
             out_rcap_ = ((omax + omax / 8) / kOutChunk + 2) * kOutChunk;
-            continue;
+            rerun = true;
         }
-        const unsigned long long total = h[kCtlMisc + 0], ntag = h[kCtlMisc + 1];
+        if (any_long && tmax > tag_rcap_) {  // the same for the tagged keys
+            tag_rcap_ = ((tmax + tmax / 8) / kOutChunk + 2) * kOutChunk;
+            rerun = true;
+        }
+        if (rerun) continue;
+        const int64_t n = (int64_t)h[kCtlMisc + 0], nt = (int64_t)h[kCtlMisc + 1];
         if (timing_) {
             float ms = 0;
             DSS_HIP(hipEventElapsedTime(&ms, ev0_, ev1_));
@@ -2037,55 +2117,46 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         iters_ = (int64_t)h[kCtlMisc + 3];
         long_queries_ = (int64_t)h[kCtlMisc + 5];
         long_postings_ = idx->n_long_fp;
-        tagged_ = (int64_t)ntag;
-        const int64_t n = (int64_t)total;
-        // close the holes of partly filled / unreserved chunks below n with
-        // the pairs at or above n
-        {
-            const int64_t nbelow = std::min<int64_t>(nch, (n + kOutChunk - 1) / kOutChunk);
-            int64_t *hole = cnt64_.ensure(4 * (nch + 2)), *tail = hole + (nch + 2);
-            int64_t *hoff = tail + (nch + 2), *toff = hoff + (nch + 2);
-            hipLaunchKernelGGL(k_fix_counts, dim3(grid_for(nch, kBlock)), dim3(kBlock), 0, s, nch, fills, n, hole, tail);
-            exclusive_scan_i64(hole, hoff, nch, tmp2_, s);
-            exclusive_scan_i64(tail, toff, nch, tmp2_, s);
-            if (nbelow > 0)
-                hipLaunchKernelGGL(k_fix_fill, dim3((unsigned)std::min<int64_t>(nbelow, (int64_t)n_cu_ * 4)),
-                                   dim3(kBlock), 0, s, nch, nbelow, fills, n, hole, hoff, toff, oq, oe);
-        }
-        if (ntag == 0) {
+        tagged_ = nt;
+        close_holes(nch, fills, n, MovePairs{oq, oe});
+        if (nt == 0) {
             out->q = oq;
             out->e = oe;
             out->n = n;
             out->n_tagged = 0;
             return;
         }
-        // long x long pairs: split off, group by hash bucket, unique, append
-        uint32_t *q2 = oq2_.ensure(n + 1), *e2 = oe2_.ensure(n + 1);
-        unsigned long long *k1 = tkey_.ensure(ntag + 1), *k2 = tkey2_.ensure(ntag + 1);
+        // long x long keys: contiguous, grouped by hash bucket, unique,
+        // appended after the pairs (in place when the pair buffer has room;
+        // the next batch's buffer is sized for it)
+        close_holes(tnch, tfills, nt, MoveKeys{tk});
+        uint32_t *fq = oq, *fe = oe;
+        if (n + nt > cap) {
+            fq = oq2_.ensure(n + nt + 1);
+            fe = oe2_.ensure(n + nt + 1);
+            device_copy(fq, oq, sizeof(uint32_t) * n, s);
+            device_copy(fe, oe, sizeof(uint32_t) * n, s);
+            out_rcap_ = std::max<int64_t>(out_rcap_, ((n + nt) / kRegions / kOutChunk + 2) * kOutChunk);
+        }
+        unsigned long long *k1 = tk, *k2 = tkey2_.ensure(nt + 1);
         int64_t *dtot = (int64_t *)(cnt + 9);
-        int64_t nun = 0, nuq = 0;
-        const int qb = bits_for(nq), eb = bits_for(idx->n_e);
-        int hb = 1;
-        while (hb < 24 && ((int64_t)ntag >> hb) > tag_bucket_avg_) hb++;
-        const bool hashed = tag_bucket_avg_ > 0 && qb + eb + hb <= 64;
-        if (!hashed) hb = 0;
-        split_if(n, PredTag{oq, false}, EmitUntagged{oq, oe, q2, e2}, EmitTagKey{oq, oe, k1, hashed ? eb : 32, hb},
-                 tmp_, tmp2_, s, dtot, &nun);
-        const int64_t nt = n - nun;
-        if (!hashed) {
+        int64_t nuq = 0;
+        if (tag_bucket_avg_ <= 0) {  // one full sort of the keys
             radix_sort_keys(k1, k2, nt, 64, tmp_, s);
-            compact_if(nt, PredRunU64{k2}, EmitPairFromKey{k2, q2, e2, nun, 32}, tmp_, tmp2_, s, dtot, &nuq);
+            compact_if(nt, PredRunU64{k2}, EmitPairFromKey{k2, fq, fe, n, eb, hbm}, tmp_, tmp2_, s, dtot, &nuq);
         } else {
+            int hb = 1;
+            while (hb < hbm && (nt >> hb) > tag_bucket_avg_) hb++;
             radix_sort_keys(k1, k2, nt, hb, tmp_, s);
             const int64_t nb = (int64_t)1 << hb;
             int64_t *bs = tb_.ensure(4 * nb + 2), *be = bs + nb, *bc = be + nb, *bo = bc + nb;
             uint8_t *ovf = tovf_.ensure(nb + 1);
             DSS_HIP(hipMemsetAsync(bs, 0, 2 * nb * sizeof(int64_t), s));
             hipLaunchKernelGGL(k_tag_bounds, dim3(grid_for(nt, kBlock)), dim3(kBlock), 0, s, nt, k2, hb, bs, be);
-            hipLaunchKernelGGL(k_tag_dedupe, dim3((unsigned)nb), dim3(kDedupBlock), 0, s, k2, bs, be, hb, k1, bc, ovf,
+            hipLaunchKernelGGL(k_tag_dedupe, dim3((unsigned)nb), dim3(kDedupBlock), 0, s, k2, bs, be, hbm, k1, bc, ovf,
                                cnt + 10);
             exclusive_scan_i64(bc, bo, nb, tmp2_, s);
-            hipLaunchKernelGGL(k_tag_emit, dim3((unsigned)nb), dim3(256), 0, s, k1, bs, bc, bo, eb, q2 + nun, e2 + nun);
+            hipLaunchKernelGGL(k_tag_emit, dim3((unsigned)nb), dim3(256), 0, s, k1, bs, bc, bo, eb, fq + n, fe + n);
             unsigned long long tail[2];  // distinct pairs of the regular buckets, flagged buckets
             device_copy(cnt + 11, bo + nb, sizeof(int64_t), s);
             DSS_HIP(hipMemcpyAsync(tail, cnt + 10, sizeof(tail), hipMemcpyDeviceToHost, s));
@@ -2093,25 +2164,26 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             nuq = (int64_t)tail[1];
             if (tail[0]) {  // flagged buckets: full sort of their keys
                 int64_t no = 0, nov = 0;
-                compact_if(nt, PredOvf{k2, ovf, hb}, EmitShift{k2, k1, hb}, tmp_, tmp2_, s, dtot, &no);
-                radix_sort_keys(k1, k2, no, 64, tmp_, s);
-                compact_if(no, PredRunU64{k2}, EmitPairFromKey{k2, q2, e2, nun + nuq, eb}, tmp_, tmp2_, s, dtot, &nov);
+                compact_if(nt, PredOvf{k2, ovf, hb}, EmitShift{k2, k1, hbm}, tmp_, tmp2_, s, dtot, &no);
+                radix_sort_keys(k1, k2, no, qb + eb, tmp_, s);
+                compact_if(no, PredRunU64{k2}, EmitPairFromKey{k2, fq, fe, n + nuq, eb, 0}, tmp_, tmp2_, s, dtot, &nov);
                 nuq += nov;
             }
         }
         if (idx->cell_lo > 0 && nuq > 0) {  // a cell-range shard past the first: exactly-once across shards
             uint8_t *keep = tovf_.ensure(nuq + 1);  // (the bucket flags are consumed)
-            hipLaunchKernelGGL(k_tag_shard_keep, dim3(grid_for(nuq, kBlock)), dim3(kBlock), 0, s, nuq, q2 + nun,
-                               e2 + nun, qv, ix, (uint64_t)idx->cell_lo, keep);
+            hipLaunchKernelGGL(k_tag_shard_keep, dim3(grid_for(nuq, kBlock)), dim3(kBlock), 0, s, nuq, fq + n, fe + n,
+                               qv, ix, (uint64_t)idx->cell_lo, keep);
+            uint32_t *tq = reinterpret_cast<uint32_t *>(k2), *te = tq + nuq;  // k2 holds >= 2 nuq words
             int64_t nk = 0;
-            compact_if(nuq, PredFlag8{keep}, EmitPairCopy{q2 + nun, e2 + nun, oq, oe}, tmp_, tmp2_, s, dtot, &nk);
-            device_copy(q2 + nun, oq, sizeof(uint32_t) * nk, s);
-            device_copy(e2 + nun, oe, sizeof(uint32_t) * nk, s);
+            compact_if(nuq, PredFlag8{keep}, EmitPairCopy{fq + n, fe + n, tq, te}, tmp_, tmp2_, s, dtot, &nk);
+            device_copy(fq + n, tq, sizeof(uint32_t) * nk, s);
+            device_copy(fe + n, te, sizeof(uint32_t) * nk, s);
             nuq = nk;
         }
-        out->q = q2;
-        out->e = e2;
-        out->n = nun + nuq;
+        out->q = fq;
+        out->e = fe;
+        out->n = n + nuq;
         out->n_tagged = nuq;
         return;
     }

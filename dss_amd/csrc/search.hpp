@@ -86,6 +86,9 @@ class SearchEngine {
     void set_timing(bool on) { timing_ = on; }
     // tuning: average tagged pairs per dedupe bucket (<= 0: the full-sort path)
     void set_tag_bucket_avg(int64_t v) { tag_bucket_avg_ = v; }
+    // join units with at most this many records load the posting signatures
+    // only for the lanes that need them (0: always prefetched)
+    void set_lazy_sig_recs(int64_t v) { lazy_sig_recs_ = v; }
     double last_join_kernel_ms() const { return join_ms_; }
     int64_t last_units() const { return units_; }
     int64_t last_keys() const { return keys_; }
@@ -126,9 +129,11 @@ class SearchEngine {
     DevBuf<uint8_t> tovf_;  // tag buckets too large for the LDS set
     int n_cu_ = 0;
     int64_t out_rcap_ = 0;  // output slots per region
+    int64_t tag_rcap_ = 0;  // tagged-key slots per region
     int64_t units_cap_hint_ = 0;
     bool timing_ = false;
     int64_t tag_bucket_avg_ = 1024;
+    int64_t lazy_sig_recs_ = 0;
     double join_ms_ = 0;
     int64_t units_ = 0, keys_ = 0, runs_ = 0, iters_ = 0, tests_ = 0;
     int64_t flushes_ = 0, merges_ = 0, merge_lanes_ = 0, tagged_ = 0, long_queries_ = 0, long_postings_ = 0;

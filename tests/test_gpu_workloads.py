@@ -68,3 +68,22 @@ def test_long_pair_dedupe_paths(corridors_case, avg):
     got = _keys(gq, ge)
     assert len(got) > 0 and np.all(got[1:] != got[:-1])
     assert np.array_equal(got, want)
+
+
+# lazy_sig_recs: 0 (every unit prefetches the posting signatures), 2^30 (every
+# unit loads them per lane on first need) -- the same pairs either way
+@pytest.mark.parametrize("lazy", [0, 1 << 30])
+def test_lazy_signature_paths(corridors_case, lazy):
+    from dss_amd import _lib
+    from dss_amd.store import EntityIndex
+    ci, cq, qa, ia, now, want = corridors_case
+    ctx = _lib.context(0)
+    ctx.set_tuning("lazy_sig_recs", lazy)
+    try:
+        idx = EntityIndex(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1)
+        gq, ge = idx.search_operations_batch(cq.offs, cq.cells, qa.alt_lo, qa.alt_hi, qa.t0, qa.t1, now)
+    finally:
+        ctx.set_tuning("lazy_sig_recs", 0)
+    got = _keys(gq, ge)
+    assert len(got) > 0 and np.all(got[1:] != got[:-1])
+    assert np.array_equal(got, want)
