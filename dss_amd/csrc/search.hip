@@ -87,7 +87,10 @@ struct Regions {
 #endif
 constexpr int kJoinBlocksPerCU = DSS_JOIN_BPC;  // persistent workgroups per CU
 constexpr int kWaves = 4;                       // waves per join workgroup
-
+#ifndef DSS_EMIT_DENSITY
+#define DSS_EMIT_DENSITY 4
+#endif
+constexpr int kEmitDensity = DSS_EMIT_DENSITY;  // record-major emission above 1 / kEmitDensity pass density
 // ---- level-13 decode + prefix signatures -----------------------------------
 __device__ __forceinline__ int s2pos_to_ij(int o, int pos) { return (int)((0x874B78B4u >> (8 * o + 2 * pos)) & 3u); }
 __device__ __forceinline__ int s2pos_to_orientation(int pos) { return (int)((0xC1u >> (2 * pos)) & 3u); }
@@ -191,7 +194,7 @@ __device__ __forceinline__ bool long_cells_dec(const uint32_t *dec, int64_t n)
 // registers, then the block with the smaller last cell advances (both on a
 // tie).  Cells >= c never count.
 template <int B>
-__device__ bool no_smaller_shared(const IndexView &a, uint32_t ent, uint64_t c, const uint64_t *qc, int64_t nq)
+__device__ __attribute__((noinline)) bool no_smaller_shared(const IndexView &a, uint32_t ent, uint64_t c, const uint64_t *qc, int64_t nq)
 {
     const uint64_t *ec = a.e_cells + a.e_offs[ent];
     const int64_t ne = a.e_offs[ent + 1] - a.e_offs[ent];
@@ -1296,44 +1299,19 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
                         }
                     }
                 }
-                // lane-major (each lane walks its own checks) for full batches;
-                // record-major (one broadcast signature per record) for small ones
-                if (nrel > 16) {
-                    while (need) {
-                        const int j = __builtin_ctzll(need);
-                        need &= need - 1;
-                        const ulonglong2 c0 = s_rs[w][0][j], c1 = s_rs[w][1][j];
-                        if (((c0.x & ps01.x) | (c0.y & ps01.y) | (c1.x & ps23.x) | (c1.y & ps23.y)) != 0ull) continue;
-                        bool k = pcompact || ((RC >> j) & 1ull) || (plong && ((RL >> j) & 1ull));
-                        if (!k) {  // neither prefix compact, not both long (rare)
-                            const uint32_t q = (uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags;
-                            k = no_smaller_shared<2>(ix, pent, cell_of_slot(ix, d.slot), a.qv.cells + a.qv.offs[q],
-                                                     a.qv.offs[q + 1] - a.qv.offs[q]);
-                        }
-                        if (k) keep |= 1ull << j;
+                // lane-major (each lane walks its own checks): full batches
+                while (need) {
+                    const int j = __builtin_ctzll(need);
+                    need &= need - 1;
+                    const ulonglong2 c0 = s_rs[w][0][j], c1 = s_rs[w][1][j];
+                    if (((c0.x & ps01.x) | (c0.y & ps01.y) | (c1.x & ps23.x) | (c1.y & ps23.y)) != 0ull) continue;
+                    bool k = pcompact || ((RC >> j) & 1ull) || (plong && ((RL >> j) & 1ull));
+                    if (LONG && !k) {  // neither prefix compact, not both long (rare; needs long postings)
+                        const uint32_t q = (uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags;
+                        k = no_smaller_shared<2>(ix, pent, cell_of_slot(ix, d.slot), a.qv.cells + a.qv.offs[q],
+                                                 a.qv.offs[q + 1] - a.qv.offs[q]);
                     }
-                } else {
-                    const unsigned long long cm = __ballot(pcompact), lm = __ballot(plong);
-                    for (int j = 0; j < nrel; j++) {
-                        const unsigned long long nj = __ballot((need >> j) & 1ull);
-                        if (!nj) continue;
-                        const ulonglong2 c0 = s_rs[w][0][j], c1 = s_rs[w][1][j];
-                        const bool ov = ((c0.x & ps01.x) | (c0.y & ps01.y) | (c1.x & ps23.x) | (c1.y & ps23.y)) != 0ull;
-                        const unsigned long long ok = nj & ~__ballot(ov);
-                        unsigned long long kj =
-                            ((RC >> j) & 1ull) ? ok : (ok & (cm | (((RL >> j) & 1ull) ? lm : 0ull)));
-                        const unsigned long long ex = ok & ~kj;
-                        if (ex) {  // neither prefix compact, not both long (rare)
-                            bool k = false;
-                            if ((ex >> lane) & 1ull) {
-                                const uint32_t q = (uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags;
-                                k = no_smaller_shared<2>(ix, pent, cell_of_slot(ix, d.slot), a.qv.cells + a.qv.offs[q],
-                                                         a.qv.offs[q + 1] - a.qv.offs[q]);
-                            }
-                            kj |= __ballot(k);
-                        }
-                        if ((kj >> lane) & 1ull) keep |= 1ull << j;
-                    }
+                    if (k) keep |= 1ull << j;
                 }
                 // (3) emission, the batch's pairs contiguous per stream (pairs;
                 // long x long keys): lane-major (each lane's pairs after the
@@ -1354,7 +1332,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
                 continue;
 #endif
                 const bool wu = out.have != 0, wt = LONG && tout.have != 0;  // else counted only (rerun)
-                if ((int64_t)(total_u + total_t) * 4 <= (int64_t)nrel * __popcll(vmask)) {  // pass density <= 1/4
+                if ((int64_t)(total_u + total_t) * kEmitDensity <= (int64_t)nrel * __popcll(vmask)) {
                     // (one loop per stream: no divergent double bodies)
                     if (wu) {
                         unsigned long long iu = (incl & 0xffffu) - cu, kk = keep & ~tagm;
