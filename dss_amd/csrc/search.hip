@@ -53,7 +53,7 @@ constexpr uint32_t kNoSlot = 0xffffffffu;
 // Query windows wider than this (us, ~72 min) form their own per-cell runs:
 // a narrow batch's posting range stays [min tlo - dcap, max tlo + 72 min].
 constexpr unsigned long long kWideWindow = 1ull << 32;
-constexpr int kOrderBits = 23;                          // query order key: quantised tlo
+constexpr int kOrderBits = 16;                          // query order key: quantised tlo (2 radix passes)
 constexpr uint32_t kWideKey = (1u << kOrderBits) - 1u;  // ... wide queries last
 
 // Work lists written from kRegions counters (spread 256 B apart; one
