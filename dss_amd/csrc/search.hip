@@ -1248,6 +1248,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
                 const unsigned long long RL = LONG ? __ballot((qslot & kLongQ) != 0) : 0ull;
                 n_bcast += (unsigned long long)nrel;
                 n_tests += (unsigned long long)nrel * (unsigned long long)__popcll(vmask);
+#ifdef DSS_XP_NOTEST  // timing experiment only: records staged, never tested
+                if (R0 | RC | RL) continue;
+#endif
                 // (1) this lane's posting against every staged record: a bit per
                 // passing record.  COALESCE'd predicates of operations.go:394-402
                 // (NULL -> sentinels).
@@ -1392,17 +1395,30 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
 // Closing the output holes: chunk c holds fills[c] pairs at c * kOutChunk
 // (0 = never reserved); with n pairs in all, the holes below n are filled
 // with the pairs at or above n, in order.  k_fix_counts: per chunk its holes
-// below n and its pairs at or above n; k_fix_fill: a block per chunk below
-// n walks its holes and finds each source in the (few) chunks at or above n.
-__global__ void k_fix_counts(int64_t nch, const uint32_t *fills, int64_t n, int64_t *hole, int64_t *tail)
+// below n and its pairs at or above n, and the list of chunks below n with
+// holes (one ballot-aggregated atomic per wave; the order of the list is
+// free: each chunk's sources follow from hoff alone).  k_fix_fill: a block
+// per listed chunk, the sources found in an LDS window of the tail offsets.
+__global__ void k_fix_counts(int64_t nch, const uint32_t *fills, int64_t n, int64_t *hole, int64_t *tail,
+                             uint32_t *list, unsigned int *nlist)
 {
     const int64_t c = tid64();
-    if (c >= nch) return;
-    const int64_t s = c * kOutChunk, f = fills[c];
-    const int64_t h0 = s + f, h1 = min(s + (int64_t)kOutChunk, n);  // holes below n
-    const int64_t t0 = max(s, n), t1 = s + f;                        // pairs at or above n
-    hole[c] = h1 > h0 ? h1 - h0 : 0;
-    tail[c] = t1 > t0 ? t1 - t0 : 0;
+    bool listed = false;
+    if (c < nch) {
+        const int64_t s = c * kOutChunk, f = fills[c];
+        const int64_t h0 = s + f, h1 = min(s + (int64_t)kOutChunk, n);  // holes below n
+        const int64_t t0 = max(s, n), t1 = s + f;                        // pairs at or above n
+        hole[c] = h1 > h0 ? h1 - h0 : 0;
+        tail[c] = t1 > t0 ? t1 - t0 : 0;
+        listed = h1 > h0;
+    }
+    const unsigned long long m = __ballot(listed);
+    if (!m) return;
+    const int lane = threadIdx.x & 63, leader = __builtin_ctzll(m);
+    unsigned int b = 0;
+    if (lane == leader) b = atomicAdd(nlist, (unsigned int)__popcll(m));
+    b = (unsigned int)__shfl((int)b, leader);
+    if (listed) list[b + mbcnt64(m)] = (uint32_t)c;
 }
 struct MovePairs {
     uint32_t *q, *e;
@@ -1416,21 +1432,20 @@ struct MoveKeys {
     unsigned long long *k;
     __device__ void operator()(int64_t dst, int64_t src) const { k[dst] = k[src]; }
 };
+constexpr int kFixBlock = 256;
 template <typename Move>
-__global__ void k_fix_fill(int64_t nch, int64_t nbelow, const uint32_t *fills, int64_t n, const int64_t *hole,
-                           const int64_t *hoff, const int64_t *toff, Move mv)
+__global__ __launch_bounds__(kFixBlock) void k_fix_fill(int64_t nch, const uint32_t *list, const unsigned int *nlist,
+                                                        const uint32_t *fills, int64_t n, const int64_t *hole,
+                                                        const int64_t *hoff, const int64_t *toff, Move mv)
 {
-    // a fixed grid strides over the chunks below n; full ones are skipped
     __shared__ int64_t s_lo;
-    for (int64_t c = blockIdx.x; c < nbelow; c += gridDim.x) {
-        const int64_t h = hole[c];
-        if (h == 0) continue;
-        // the tail chunk of this chunk's first source, found once (thread 0);
-        // each thread gallops forward from it to its own source's chunk
+    __shared__ int64_t s_toff[kFixBlock + 1];  // toff[lo0 .. lo0 + kFixBlock]
+    const int64_t nl = *nlist;
+    for (int64_t i = blockIdx.x; i < nl; i += gridDim.x) {
+        const int64_t c = list[i], h = hole[c], t0 = hoff[c];
         __syncthreads();
-        if (threadIdx.x == 0) {
-            int64_t lo = n / kOutChunk, hi = nch;  // tail chunk tc with toff[tc] <= t < toff[tc + 1]
-            const int64_t t0 = hoff[c];
+        if (threadIdx.x == 0) {  // tail chunk lo0 of the first source: toff[lo0] <= t0 < toff[lo0 + 1]
+            int64_t lo = n / kOutChunk, hi = nch;
             while (hi - lo > 1) {
                 const int64_t mid = (lo + hi) >> 1;
                 if (toff[mid] <= t0) lo = mid;
@@ -1440,20 +1455,33 @@ __global__ void k_fix_fill(int64_t nch, int64_t nbelow, const uint32_t *fills, i
         }
         __syncthreads();
         const int64_t lo0 = s_lo;
-        for (int64_t k = threadIdx.x; k < h; k += blockDim.x) {
-            const int64_t t = hoff[c] + k;  // its source: the t-th pair at or above n
-            // galloping from the chunk's first source chunk (runs of empty
-            // tail chunks -- unreserved space -- are skipped in O(log) steps)
-            int64_t lo = lo0, step = 1;
-            while (lo + step < nch && toff[lo + step] <= t) {
-                lo += step;
-                step <<= 1;
-            }
-            int64_t hi = lo + step < nch ? lo + step : nch;
-            while (hi - lo > 1) {
-                const int64_t mid = (lo + hi) >> 1;
-                if (toff[mid] <= t) lo = mid;
-                else hi = mid;
+        for (int j = threadIdx.x; j <= kFixBlock; j += kFixBlock)
+            s_toff[j] = lo0 + j < nch ? toff[lo0 + j] : INT64_MAX;
+        __syncthreads();
+        for (int64_t k = threadIdx.x; k < h; k += kFixBlock) {
+            const int64_t t = t0 + k;  // its source: the t-th pair at or above n
+            int64_t lo;
+            if (t < s_toff[kFixBlock]) {  // inside the window (the usual case)
+                int a = 0, b = kFixBlock;  // s_toff[a] <= t < s_toff[b]
+                while (b - a > 1) {
+                    const int mid = (a + b) >> 1;
+                    if (s_toff[mid] <= t) a = mid;
+                    else b = mid;
+                }
+                lo = lo0 + a;
+            } else {  // past it: galloping in global memory
+                int64_t step = 1;
+                lo = lo0 + kFixBlock;
+                while (lo + step < nch && toff[lo + step] <= t) {
+                    lo += step;
+                    step <<= 1;
+                }
+                int64_t hi = lo + step < nch ? lo + step : nch;
+                while (hi - lo > 1) {
+                    const int64_t mid = (lo + hi) >> 1;
+                    if (toff[mid] <= t) lo = mid;
+                    else hi = mid;
+                }
             }
             const int64_t src = max(lo * kOutChunk, n) + (t - toff[lo]);
             mv(c * kOutChunk + fills[c] + k, src);
@@ -2027,14 +2055,19 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     // entries at or above n
     auto close_holes = [&](int64_t nch, const uint32_t *fills, int64_t n, auto mover) {
         const int64_t nbelow = std::min<int64_t>(nch, (n + kOutChunk - 1) / kOutChunk);
-        int64_t *hole = cnt64_.ensure(4 * (nch + 2)), *tail = hole + (nch + 2);
+        int64_t *hole = cnt64_.ensure(5 * (nch + 2)), *tail = hole + (nch + 2);
         int64_t *hoff = tail + (nch + 2), *toff = hoff + (nch + 2);
-        hipLaunchKernelGGL(k_fix_counts, dim3(grid_for(nch, kBlock)), dim3(kBlock), 0, s, nch, fills, n, hole, tail);
+        uint32_t *list = reinterpret_cast<uint32_t *>(toff + (nch + 2));
+        unsigned int *nlist = reinterpret_cast<unsigned int *>(cnt + 12);  // (zeroed with the control block)
+        DSS_HIP(hipMemsetAsync(nlist, 0, sizeof(unsigned int), s));
+        hipLaunchKernelGGL(k_fix_counts, dim3(grid_for(nch, kBlock)), dim3(kBlock), 0, s, nch, fills, n, hole, tail,
+                           list, nlist);
         exclusive_scan_i64(hole, hoff, nch, tmp2_, s);
         exclusive_scan_i64(tail, toff, nch, tmp2_, s);
         if (nbelow > 0)
-            hipLaunchKernelGGL(k_fix_fill<decltype(mover)>, dim3((unsigned)std::min<int64_t>(nbelow, (int64_t)n_cu_ * 4)),
-                               dim3(kBlock), 0, s, nch, nbelow, fills, n, hole, hoff, toff, mover);
+            hipLaunchKernelGGL(k_fix_fill<decltype(mover)>, dim3((unsigned)std::min<int64_t>(nbelow, (int64_t)n_cu_ * 8)),
+                               dim3(kFixBlock), 0, s, nch, (const uint32_t *)list, (const unsigned int *)nlist, fills, n,
+                               hole, hoff, toff, mover);
     };
     for (int attempt = 0; attempt < 6; attempt++) {
         const int64_t cap = kRegions * out_rcap_, nch = cap / kOutChunk;
