@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -1104,6 +1105,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
     const IndexView &ix = a.ix;
     WaveOut out, tout;  // pairs, tagged keys
     unsigned long long n_tests = 0, n_bcast = 0;
+#ifdef DSS_XP_COUNT  // timing experiment only: wave-iteration counts of the join's loops
+    unsigned long long x_batches = 0, x_nonempty = 0, x_sig = 0, x_emit = 0, x_need = 0;
+#endif
     // units: kRegions queues (the unit regions), a wave starts on its own
     // region's and moves on when it is drained; grabs of g units per atomic
     int qreg = (int)(blockIdx.x % kRegions), visited = 0;
@@ -1215,7 +1219,11 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
                 bool rel = false;
                 int4 h0 = make_int4(0, 0, 0, 0), h1 = h0;
                 ulonglong2 g0 = make_ulonglong2(0, 0), g1 = g0;
+#ifdef DSS_XP_NOSTAGE  // timing experiment only: no record loads, nothing staged
+                if (r < x1 && r == 0xffffffffu) {
+#else
                 if (r < x1) {
+#endif
                     const int4 *r4 = reinterpret_cast<const int4 *>(recs + sval[r]);
                     h0 = r4[0];
                     h1 = r4[1];
@@ -1229,6 +1237,14 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
                 }
                 const unsigned long long relm = __ballot(rel);
                 const int nrel = uni32(__popcll(relm));
+#ifdef DSS_XP_NOLDS  // timing experiment only: records loaded and hull-tested, not staged
+                n_bcast += (unsigned long long)nrel;
+                continue;
+#endif
+#ifdef DSS_XP_COUNT
+                x_batches++;
+                x_nonempty += nrel ? 1 : 0;
+#endif
                 if (!nrel) continue;
                 const uint32_t slot = mbcnt64(relm);
                 __builtin_amdgcn_wave_barrier();
@@ -1302,6 +1318,10 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
                         }
                     }
                 }
+#ifdef DSS_XP_COUNT
+                x_sig += wave_max((uint32_t)__popcll(need));
+                x_need += __builtin_amdgcn_readlane((int)wave_incl_scan((uint32_t)__popcll(need)), 63);
+#endif
                 // lane-major (each lane walks its own checks): full batches
                 while (need) {
                     const int j = __builtin_ctzll(need);
@@ -1335,6 +1355,11 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
                 continue;
 #endif
                 const bool wu = out.have != 0, wt = LONG && tout.have != 0;  // else counted only (rerun)
+#ifdef DSS_XP_COUNT
+                x_emit += (int64_t)(total_u + total_t) * kEmitDensity <= (int64_t)nrel * __popcll(vmask)
+                              ? wave_max((uint32_t)__popcll(keep))
+                              : (unsigned long long)nrel;
+#endif
                 if ((int64_t)(total_u + total_t) * kEmitDensity <= (int64_t)nrel * __popcll(vmask)) {
                     // (one loop per stream: no divergent double bodies)
                     if (wu) {
@@ -1389,6 +1414,13 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
     if (lane == 0) {
         atomicAdd(&a.out.counter[2], n_tests);
         atomicAdd(&a.out.counter[3], n_bcast);
+#ifdef DSS_XP_COUNT
+        atomicAdd(&a.out.counter[6], x_batches);
+        atomicAdd(&a.out.counter[7], x_nonempty);
+        atomicAdd(&a.out.counter[8], x_sig);
+        atomicAdd(&a.out.counter[13], x_emit);
+        atomicAdd(&a.out.counter[14], x_need);
+#endif
     }
 }
 
@@ -2127,6 +2159,11 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         tests_ = (int64_t)h[kCtlMisc + 2];
         iters_ = (int64_t)h[kCtlMisc + 3];
         long_queries_ = (int64_t)h[kCtlMisc + 5];
+#ifdef DSS_XP_COUNT
+        fprintf(stderr, "[xp] batches %llu nonempty %llu sig_iters %llu need %llu emit_iters %llu bcast %llu tests %llu\n",
+                h[kCtlMisc + 6], h[kCtlMisc + 7], h[kCtlMisc + 8], h[kCtlMisc + 14], h[kCtlMisc + 13], h[kCtlMisc + 3],
+                h[kCtlMisc + 2]);
+#endif
         long_postings_ = idx->n_long_fp;
         tagged_ = nt;
         close_holes(nch, fills, n, MovePairs{oq, oe});
