@@ -755,6 +755,7 @@ def request_latency(ctx, D, index, queries, qa, now, n_alone=500, callers=64, se
     import ctypes as C
     import threading
     from dss_amd.store import Batcher, _p
+    from dss_amd._lib import DSSG_ERR_CAPACITY
     L = ctx.L
     lat_ms = []
     cap = 1 << 16
@@ -772,14 +773,26 @@ def request_latency(ctx, D, index, queries, qa, now, n_alone=500, callers=64, se
         lo, hi = np.array([qa.alt_lo[i]], np.float32), np.array([qa.alt_hi[i]], np.float32)
         s0, e0 = np.array([qa.t0[i]], np.int64), np.array([qa.t1[i]], np.int64)
         t0 = time.perf_counter()
-        ctx.check(L.dssg_cover_batch(ctx.h, 1, _p(kind, C.c_int32), _p(voff, C.c_int64), _p(la, C.c_double),
-                                     _p(lg, C.c_double), _p(rad, C.c_float), _p(offs, C.c_int64),
-                                     _p(cells, C.c_uint64), cap, C.byref(need), _p(st, C.c_int32),
-                                     _p(area, C.c_double)))
-        ctx.check(L.dssg_search_operations(ctx.h, index, 1, _p(offs, C.c_int64), _p(cells, C.c_uint64),
-                                           _p(lo, C.c_float), _p(hi, C.c_float), _p(s0, C.c_int64),
-                                           _p(e0, C.c_int64), int(now), _p(oq, C.c_uint32), _p(oe, C.c_uint32), cap,
-                                           C.byref(need)))
+        # the ABI's capacity protocol, as a caller follows it: DSSG_ERR_CAPACITY
+        # -> grow to *needed and call again (counted in the request's latency)
+        while True:
+            rc = L.dssg_cover_batch(ctx.h, 1, _p(kind, C.c_int32), _p(voff, C.c_int64), _p(la, C.c_double),
+                                    _p(lg, C.c_double), _p(rad, C.c_float), _p(offs, C.c_int64),
+                                    _p(cells, C.c_uint64), len(cells), C.byref(need), _p(st, C.c_int32),
+                                    _p(area, C.c_double))
+            if rc != DSSG_ERR_CAPACITY:
+                break
+            cells = np.empty(int(need.value) + 1, np.uint64)
+        ctx.check(rc)
+        while True:
+            rc = L.dssg_search_operations(ctx.h, index, 1, _p(offs, C.c_int64), _p(cells, C.c_uint64),
+                                          _p(lo, C.c_float), _p(hi, C.c_float), _p(s0, C.c_int64),
+                                          _p(e0, C.c_int64), int(now), _p(oq, C.c_uint32), _p(oe, C.c_uint32),
+                                          len(oq), C.byref(need))
+            if rc != DSSG_ERR_CAPACITY:
+                break
+            oq, oe = np.empty(int(need.value) + 1, np.uint32), np.empty(int(need.value) + 1, np.uint32)
+        ctx.check(rc)
         lat_ms.append(1000.0 * (time.perf_counter() - t0))
     alone = np.array(lat_ms[20:])
 

@@ -551,7 +551,10 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
 }
 
 template <bool FAST>
-__global__ __launch_bounds__(64) void k_setup(uint32_t *slow_list, unsigned int *slow_n, int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
+#ifndef DSS_SETUP_WPE
+#define DSS_SETUP_WPE 1
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAST ? DSS_SETUP_WPE : 1))) void k_setup(uint32_t *slow_list, unsigned int *slow_n, int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
                         const float *radius_m, const int64_t *xoff, V3 *xyz, int32_t *status, double *area_out,
                         uint8_t *mode, uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx, double2 *uv,
                         uint64_t *st_id, uint32_t *st_i, uint32_t *st_j, uint32_t *finfo, int64_t *ncand,
