@@ -835,15 +835,31 @@ __global__ void k_expand_write(int64_t nn, const uint32_t *nf, const uint64_t *n
     *any_open = 1;
 }
 
-// Final items -> per-footprint counts.
-__global__ void k_item_counts(int64_t nn, const uint32_t *nf, const uint32_t *nmeta, int64_t *icnt, unsigned long long *fcnt)
+// Final items -> per-footprint counts.  A long footprint (a corridor) owns
+// thousands of consecutive items, and same-address global atomics serialise
+// (~88 per us): the block sums its items per footprint in LDS first (slot
+// f - the block's first footprint; items out of that window go straight to
+// HBM) and adds each sum with one global atomic.
+constexpr int kItemBlock = 256;
+__global__ __launch_bounds__(kItemBlock) void k_item_counts(int64_t nn, const uint32_t *nf, const uint32_t *nmeta,
+                                                            int64_t *icnt, unsigned long long *fcnt)
 {
-    int64_t k = tid64();
-    if (k >= nn) return;
-    int level = meta_level(nmeta[k]);
-    int64_t c = (int64_t)1 << (2 * (kCoverLevel - level));
-    icnt[k] = c;
-    atomicAdd(&fcnt[nf[k]], (unsigned long long)c);
+    __shared__ unsigned long long s_sum[kItemBlock];
+    const int64_t k0 = (int64_t)blockIdx.x * kItemBlock, k = k0 + threadIdx.x;
+    const uint32_t f0 = nf[k0];
+    s_sum[threadIdx.x] = 0;
+    __syncthreads();
+    if (k < nn) {
+        const int level = meta_level(nmeta[k]);
+        const int64_t c = (int64_t)1 << (2 * (kCoverLevel - level));
+        icnt[k] = c;
+        const uint32_t f = nf[k], d = f - f0;
+        if (d < (uint32_t)kItemBlock) atomicAdd(&s_sum[d], (unsigned long long)c);
+        else atomicAdd(&fcnt[f], (unsigned long long)c);
+    }
+    __syncthreads();
+    const unsigned long long v = s_sum[threadIdx.x];
+    if (v) atomicAdd(&fcnt[f0 + threadIdx.x], v);
 }
 
 // Descent items are numbered among themselves (ipos); dpre[f] = descent cells
@@ -1265,7 +1281,8 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     DSS_HIP(hipMemsetAsync(dcnt, 0, sizeof(unsigned long long) * (n + 1), s));
     int64_t *icnt = ncnt_.ensure(nn + 1), *ipos = npos_.ensure(nn + 1);
     if (nn > 0)
-        hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nn, B)), dim3(B), 0, s, nn, F->f.p, F->meta.p, icnt, dcnt);
+        hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nn, kItemBlock)), dim3(kItemBlock), 0, s, nn, F->f.p, F->meta.p,
+                           icnt, dcnt);
     int64_t *tot64 = fc64_.ensure(n + 1), *dc64 = dc64_.ensure(n + 1), *dpre = dpre_.ensure(n + 1);
     hipLaunchKernelGGL(k_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, coff, kmask, gpos, dcnt, tot64, dc64);
     exclusive_scan_i64(tot64, offs, n, tmp_, s);
