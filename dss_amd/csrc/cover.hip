@@ -1029,9 +1029,111 @@ __device__ __forceinline__ int cand_decide(int64_t c, const uint32_t *cand_f, co
     return in ? 1 : planar ? (((origin_in[f] != 0) != par) ? 1 : 0) : 2;
 }
 
+// The edge / centre test of candidate c of footprint f at level-13 (i, j)
+// inside the footprint's bound (cand_decide past its bound check).
+__device__ __forceinline__ int cand_edges(uint32_t f, uint32_t i, uint32_t j, const int64_t *xoff, const double2 *uv,
+                                          const int32_t *nvx, const uint8_t *origin_in, const uint8_t *flags)
+{
+    constexpr int kVU = 4;
+    const int nv = nvx[f];
+    const double2 *up = uv + xoff[f];
+    double2 a = up[0];
+    const uint32_t size = 1u << (kMaxLevel - kCoverLevel);
+    const double ulo = st_to_uv((double)i / (double)kMaxSize), uhi = st_to_uv((double)(i + size) / (double)kMaxSize);
+    const double vlo = st_to_uv((double)j / (double)kMaxSize), vhi = st_to_uv((double)(j + size) / (double)kMaxSize);
+    const double pm = kFinePad;
+    const bool planar = (flags[f] & FL_PLANAR) != 0;
+    const double half = 0.5 / (double)kMaxSize, sz = (double)size;
+    const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
+    bool in = false, par = false;
+    for (int e0 = 0; e0 < nv && !in; e0 += kVU) {
+        double2 bb[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; u++) {
+            const int e = e0 + u + 1;
+            bb[u] = up[e < nv ? e : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < kVU; u++) {
+            if (e0 + u >= nv) break;
+            const double2 b = bb[u];
+            if (edge_intersects_rect(a.x, a.y, b.x, b.y, ulo - pm, uhi + pm, vlo - pm, vhi + pm)) {
+                in = true;
+                break;
+            }
+            if ((a.y > vc) != (b.y > vc)) {
+                const double d = b.y - a.y;
+                const double lhs = (uc - a.x) * d, rhs = (vc - a.y) * (b.x - a.x);
+                if (d > 0 ? lhs < rhs : lhs > rhs) par = !par;
+            }
+            a = b;
+        }
+    }
+    return in ? 1 : planar ? (((origin_in[f] != 0) != par) ? 1 : 0) : 2;
+}
+
 // Verdicts leave as two ballot masks per wave of 64 candidates (kept, and
 // undecided): 16 B per 64 candidates instead of a per-candidate word, and
 // the compaction below ranks by popcount, with no candidate-sized scan.
+// The block first tests its 256 candidates against their footprints' level-13
+// bounds, compacts the ones inside to its first threads (LDS), and only those
+// run the edge loop: the out-of-bound lanes no longer idle through it.
+#ifndef DSS_CAND_COMPACT
+#define DSS_CAND_COMPACT 1
+#endif
+__global__ __launch_bounds__(kCandBlock) void k_cand_test_c(int64_t NC, const uint32_t *cand_f, const int64_t *coff,
+                                                            const uint64_t *st_id, const uint32_t *st_i,
+                                                            const uint32_t *st_j, const uint32_t *finfo,
+                                                            const uint4 *fbox, const int64_t *xoff, const double2 *uv,
+                                                            const int32_t *nvx, const uint8_t *origin_in,
+                                                            const uint8_t *flags, unsigned long long *kmask,
+                                                            unsigned long long *umask)
+{
+    __shared__ uint32_t s_lt[kCandBlock], s_ci[kCandBlock], s_cj[kCandBlock], s_f[kCandBlock];
+    __shared__ unsigned int s_n;
+    __shared__ unsigned long long s_k[kCandBlock / 64], s_u[kCandBlock / 64];
+    const int t = threadIdx.x, lane = t & 63;
+    const int64_t c0 = (int64_t)blockIdx.x * kCandBlock, c = c0 + t;
+    if (t == 0) s_n = 0;
+    if (t < kCandBlock / 64) s_k[t] = s_u[t] = 0;
+    __syncthreads();
+    bool inb = false;
+    uint32_t i = 0, j = 0, f = 0;
+    if (c < NC) {
+        f = cand_f[c];
+        int face;
+        uint64_t id;
+        cand_cell(c, f, coff, st_id, st_i, st_j, finfo, face, i, j, id);
+        const uint4 bx = fbox[f];
+        const uint32_t i13 = i >> (kMaxLevel - kCoverLevel), j13 = j >> (kMaxLevel - kCoverLevel);
+        inb = !(i13 < bx.x || i13 > bx.y || j13 < bx.z || j13 > bx.w);
+    }
+    const unsigned long long m = __ballot(inb);
+    unsigned int base = 0;
+    if (lane == 0 && m) base = atomicAdd(&s_n, (unsigned int)__popcll(m));
+    base = (unsigned int)__shfl((int)base, 0);
+    if (inb) {
+        const unsigned int p = base + (unsigned int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        s_lt[p] = (uint32_t)t;
+        s_ci[p] = i;
+        s_cj[p] = j;
+        s_f[p] = f;
+    }
+    __syncthreads();
+    if ((unsigned int)t < s_n) {
+        const uint32_t lt = s_lt[t];
+        const int v = cand_edges(s_f[t], s_ci[t], s_cj[t], xoff, uv, nvx, origin_in, flags);
+        if (v == 1) atomicOr(&s_k[lt >> 6], 1ull << (lt & 63));
+        else if (v == 2) atomicOr(&s_u[lt >> 6], 1ull << (lt & 63));
+    }
+    __syncthreads();
+    if (t < kCandBlock / 64 && c0 + 64 * t < NC) {
+        kmask[(c0 >> 6) + t] = s_k[t];
+        umask[(c0 >> 6) + t] = s_u[t];
+    }
+}
+
 __global__ void k_cand_test(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
                             const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const uint4 *fbox,
                             const int64_t *xoff, const double2 *uv, const int32_t *nvx, const uint8_t *origin_in,
@@ -1226,8 +1328,9 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     DSS_HIP(hipMemsetAsync(kmask + G, 0, sizeof(unsigned long long), s));
     if (NC > 0) {
         hipLaunchKernelGGL(k_cand_owner, dim3(grid_for(n, 256)), dim3(256), 0, s, n, coff, cand_f);
-        hipLaunchKernelGGL(k_cand_test, dim3(grid_for(NC, kCandBlock)), dim3(kCandBlock), 0, s, NC, cand_f, coff, st_id,
-                           st_i, st_j, finfo, fbox, xoff, uv, nvx, orig, flags, kmask, umask);
+        hipLaunchKernelGGL(DSS_CAND_COMPACT ? k_cand_test_c : k_cand_test, dim3(grid_for(NC, kCandBlock)),
+                           dim3(kCandBlock), 0, s, NC, cand_f, coff, st_id, st_i, st_j, finfo, fbox, xoff, uv, nvx, orig,
+                           flags, kmask, umask);
         hipLaunchKernelGGL(k_cand_exact, dim3(grid_for(NC, B)), dim3(B), 0, s, NC, cand_f, coff, st_id, st_i, st_j, finfo,
                            xoff, xyz, nvx, orig, kmask, umask);
         hipLaunchKernelGGL(k_mask_counts, dim3(grid_for(G, B)), dim3(B), 0, s, G, kmask, gcnt);
