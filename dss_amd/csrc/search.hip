@@ -91,7 +91,11 @@ constexpr int kWaves = 4;                       // waves per join workgroup
 #ifndef DSS_EMIT_DENSITY
 #define DSS_EMIT_DENSITY 4
 #endif
-constexpr int kEmitDensity = DSS_EMIT_DENSITY;  // record-major emission above 1 / kEmitDensity pass density
+constexpr int kEmitDensity = DSS_EMIT_DENSITY;
+#ifndef DSS_OUT_STAGE
+#define DSS_OUT_STAGE 256
+#endif
+constexpr int kOutStage = DSS_OUT_STAGE;  // pairs per wave staged in LDS before the stores (0: direct stores)  // record-major emission above 1 / kEmitDensity pass density
 // ---- level-13 decode + prefix signatures -----------------------------------
 __device__ __forceinline__ int s2pos_to_ij(int o, int pos) { return (int)((0x874B78B4u >> (8 * o + 2 * pos)) & 3u); }
 __device__ __forceinline__ int s2pos_to_orientation(int pos) { return (int)((0xC1u >> (2 * pos)) & 3u); }
@@ -1092,7 +1096,7 @@ struct JoinArgs {
 // smallest-shared-cell rule (SQL DISTINCT, Q13) compares the record's
 // near-prefix signature (broadcast) with each lane's posting signature.
 template <bool OWNER, bool LONG>
-__global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__restrict__ recs,
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LONG ? 1 : kJoinBlocksPerCU))) void k_join(JoinArgs a, const QRec *__restrict__ recs,
                                                       const uint32_t *__restrict__ sval,
                                                       const Unit *__restrict__ units,
                                                       unsigned long long *__restrict__ work)
@@ -1100,6 +1104,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
     __shared__ longlong2 s_rt[kWaves][64];      // record (tlo, thi)
     __shared__ float4 s_ra[kWaves][64];         // record (alo, ahi, qv, own)
     __shared__ ulonglong2 s_rs[kWaves][2][64];  // record near-prefix signature
+    __shared__ uint2 s_out[kWaves][kOutStage];   // a sparse batch's pairs, staged for coalesced stores
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const IndexView &ix = a.ix;
@@ -1362,7 +1367,27 @@ __global__ __launch_bounds__(64 * kWaves) void k_join(JoinArgs a, const QRec *__
 #endif
                 if ((int64_t)(total_u + total_t) * kEmitDensity <= (int64_t)nrel * __popcll(vmask)) {
                     // (one loop per stream: no divergent double bodies)
-                    if (wu) {
+                    if (!LONG && kOutStage && wu && total_u <= kOutStage) {  // (long variants: direct, no VGPR headroom)
+                        // each lane's pairs into the wave's LDS stage (one 8-B
+                        // LDS store per pair), then the batch leaves as runs of
+                        // consecutive slots: full-width coalesced global stores
+                        // instead of one scattered 4-B store per pair and array
+                        uint32_t iu = (incl & 0xffffu) - cu;
+                        unsigned long long kk = keep & ~tagm;
+                        while (kk) {
+                            const int j = __builtin_ctzll(kk);
+                            kk &= kk - 1;
+                            s_out[w][iu++] = make_uint2((uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags, pent);
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        for (int p = lane; p < total_u; p += 64) {
+                            const uint2 v = s_out[w][p];
+                            const unsigned long long pos = su.at((unsigned long long)p);
+                            a.out.q[pos] = v.x;
+                            a.out.e[pos] = v.y;
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                    } else if (wu) {
                         unsigned long long iu = (incl & 0xffffu) - cu, kk = keep & ~tagm;
                         while (kk) {
                             const int j = __builtin_ctzll(kk);
