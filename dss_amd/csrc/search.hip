@@ -1333,7 +1333,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                     need &= need - 1;
                     const ulonglong2 c0 = s_rs[w][0][j], c1 = s_rs[w][1][j];
                     if (((c0.x & ps01.x) | (c0.y & ps01.y) | (c1.x & ps23.x) | (c1.y & ps23.y)) != 0ull) continue;
-                    bool k = pcompact || ((RC >> j) & 1ull) || (plong && ((RL >> j) & 1ull));
+                    // (without long postings every posting's prefix is compact:
+                    // all of its entity's cells lie in an 8 x 8 window)
+                    bool k = !LONG || pcompact || ((RC >> j) & 1ull) || (plong && ((RL >> j) & 1ull));
                     if (LONG && !k) {  // neither prefix compact, not both long (rare; needs long postings)
                         const uint32_t q = (uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags;
                         k = no_smaller_shared<2>(ix, pent, cell_of_slot(ix, d.slot), a.qv.cells + a.qv.offs[q],

@@ -13,7 +13,7 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 tail -2 "$OUT/gpu_tests.log"
 timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo BENCH_FAILED; tail "$OUT/bench.err"; exit 1; }
 cut -c1-400 "$OUT/bench.json"
-BENCH_ARGS="--latency 0" bash tools/profile.sh "$TAG" > "$OUT/profile.log" 2>&1 || { echo PROF_FAILED; tail "$OUT/profile.log"; exit 1; }
+BENCH_ARGS="--latency 0 --pipelines 3" bash tools/profile.sh "$TAG" > "$OUT/profile.log" 2>&1 || { echo PROF_FAILED; tail "$OUT/profile.log"; exit 1; }
 P=gpurun_out/prof/$TAG
 cp "$P/summary.csv" "$OUT/pmc_summary.csv"
 cp "$P"/kt_kernel_stats.csv "$OUT/kernel_stats.csv" 2>/dev/null || cp "$(ls "$P"/*kernel_stats.csv | head -1)" "$OUT/kernel_stats.csv"
