@@ -2,28 +2,29 @@
 """Benchmark: 4D conflict queries/s against a resident N-intent airspace.
 
 BASELINE.json metric "4D conflict queries/sec vs N-intent airspace
-(1/2/4/8 GPU); coverings/sec", workload configs[1]: 1M polygon/circle query
-footprints per GPU step against a 1M-intent index, SF-Bay metro region
-(seeded synthetic data, SURVEY.md s8(d) generator).
+(1/2/4/8 GPU); coverings/sec".  Default workload configs[2], the north-star
+airspace: 1M polygon/circle query footprints per GPU step against a
+10M-intent index over California (70 % around 4 hotspots), seeded synthetic
+data (SURVEY.md s8(d) generator).  --config 1 is the 1M x 1M metro config.
 
 One step = cover the rank's 1M query footprints on the GPU (level-13 S2
 coverings) -> overlap join against the HBM-resident index -> fused
 altitude/time/now filter -> deduplicated (query, intent) pairs resident in
 HBM.  The index (intent coverings + posting lists) is built before timing.
 
-Multi-GPU (torchrun, one process per GPU), --mode:
-  replica (default): every rank holds the whole index (a 1M-intent airspace
-    is ~0.5 GB of a GPU's 288 GB; even configs[4]'s 50M fit many times over)
-    and covers + joins its own 1M-query batch.  Queries are independent, so
-    there is no collective on the data path; "scaling": "weak".
-  sharded: the intent index is split into
-    N uint64 cell ranges at posting quantiles, one shard per GPU.  Each rank
-    covers its own 1M queries, routes every query (row + whole cell list) to
-    the shards owning its cells (all-to-all over RCCL/xGMI), joins what it
-    receives against its shard, and routes the pairs back to their queries'
-    home ranks (second all-to-all).  "scaling": "weak" (1M queries per GPU).
-    For an index that outgrows one GPU; the pair exchange (~100 pairs x 8 B
-    per query) costs more than the join it distributes.
+Ranks: one process per GPU.  Under torchrun (WORLD_SIZE set) each process is
+one rank; `--gpus N` without a launcher starts the N rank processes itself
+(self_launch) before anything touches a GPU.  --mode:
+  sharded (default on N > 1; BASELINE's layout): the intent
+    index is split into N uint64 cell ranges at posting quantiles, one shard
+    per GPU.  Each rank covers its own 1M queries, routes every query (row +
+    whole cell list) to the shards owning its cells (all-to-all over
+    RCCL/xGMI, the library's own communicator), joins what it receives
+    against its shard, and routes the pairs back to their queries' home ranks
+    (second all-to-all).  "scaling": "weak" (1M queries per GPU).  The
+    replica rate (same pipelines, no exchange) is reported beside it.
+  replica (default on one GPU): the rank holds the whole index and covers +
+    joins its own batch; no collective on the data path.
 Timing: barrier + synchronize on both sides of exactly --steps steps, max
 over ranks.
 """
@@ -86,19 +87,24 @@ def heartbeat(every=30.0):
     threading.Thread(target=run, daemon=True).start()
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (ranks) of one node.  Under a launcher (torchrun: WORLD_SIZE set) each process is one "
+                         "rank; without one, N > 1 starts N rank processes itself (before any GPU call here) and "
+                         "relays rank 0's result line")
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", type=int, default=1)
+    ap.add_argument("--config", type=int, default=2,
+                    help="BASELINE.json configs[i]; default 2: the north-star airspace (10M intents, 1M-query batches "
+                         "per GPU), the layout BASELINE's 1/2/4/8-GPU metric is quoted on")
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug only; invalid for the metric)")
     ap.add_argument("--query-scale", type=float, default=1.0,
                     help="queries per step relative to the config's 1M (configs[4] at full size: 0.1, since its output "
                          "grows with batch x airspace density: ~5.7k pairs per query against 50M corridors)")
     ap.add_argument("--cpu-sample", type=int, default=-1,
-                    help="queries in the CPU-baseline sample (-1: auto -- the whole step's batch for configs[0]/[1], a "
-                         "bounded sample of ~10-30 s of CPU work for the larger airspaces; 0: skip).  The sample's "
+                    help="queries in the CPU-baseline sample (-1: auto -- the whole step's batch for configs[0]..[3], a "
+                         "bounded sample of ~10-30 s of CPU work for configs[4]; 0: skip).  The sample's "
                          "cells and pairs are compared with the GPU step's (parity on the sampled queries)")
     ap.add_argument("--no-verify", action="store_true", help="skip the full-size GPU-vs-oracle parity check")
     ap.add_argument("--survey-model", type=int, default=1, help="also count SURVEY s8(d)'s per-query byte model")
@@ -106,9 +112,9 @@ def main():
                     help="CPU-baseline threads (0: the process's CPU share -- the affinity mask, capped by "
                          "OMP_NUM_THREADS, which the GPU box sets to its per-GPU share of 16)")
     ap.add_argument("--mode", choices=["sharded", "replica"], default=None,
-                    help="multi-GPU layout: replica (index on every GPU, queries split) or sharded (index split by "
-                         "cell range, queries and pairs exchanged by all-to-all).  Default: sharded for configs[2] "
-                         "on N > 1 GPUs (its BASELINE layout; the replica rate is reported beside it), else replica")
+                    help="multi-GPU layout: sharded (index split by S2 cell range, queries and pairs exchanged by "
+                         "all-to-all; the default on N > 1 GPUs, BASELINE's layout, with the replica rate reported "
+                         "beside it) or replica (index on every GPU, queries split; the default on one GPU)")
     ap.add_argument("--exchange", choices=["native", "torch"], default=None,
                     help="sharded mode's all-to-alls: native (the library's own RCCL communicator, "
                          "dssg_sharded_search_device) or torch (torch.distributed; the instrumented path).  Default: "
@@ -117,14 +123,193 @@ def main():
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="dssg_set_tuning knob for every pipeline's context (e.g. lazy_sig_recs=0)")
     ap.add_argument("--pipelines", type=int, default=3,
-                    help="concurrent batch pipelines per GPU (own engine context + stream + host thread each): one "
-                         "batch's FP64 covering overlaps another's join, as concurrent RPCs would (replica mode)")
+                    help="batch pipelines per GPU, each its own engine context + stream + host thread.  replica: P "
+                         "independent cover+join pipelines (one batch's FP64 covering overlaps another's join, as "
+                         "concurrent RPCs would); sharded: P-1 contexts cover the next batches ahead while the "
+                         "exchange + shard join runs the batches in step order on one communicator")
     ap.add_argument("--latency", type=int, default=1,
                     help="also time single requests (cover + search of one footprint): alone, and 64 concurrent "
                          "callers through the micro-batcher (dssg_batcher)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank on cuda:0 (one-GPU box, gloo backend)")
-    args = ap.parse_args()
+    ap.add_argument("--launch-probe", default=None, metavar="DIR",
+                    help="test hook: each rank writes its launch environment to DIR/rank<r>.json and exits before "
+                         "importing torch (checks the self-launch on a machine without GPUs)")
+    return ap.parse_args(argv)
+
+
+def self_launch(args, argv):
+    """`--gpus N` (N > 1) with no launcher around this process: start N rank
+    processes of this same command line, one per GPU (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* in their environment, rendezvous on 127.0.0.1), the
+    way torchrun would.  Nothing here touches the GPU: the children own the
+    devices.  Rank 0's stdout (the result line) is relayed; if a rank fails,
+    the others are stopped (their exact PIDs) and its exit status returned."""
+    import socket
+    import subprocess
+    import threading
+    n = args.gpus
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    log(f"[bench] self-launch: {n} ranks, rendezvous 127.0.0.1:{port}")
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "bench.py")] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else None))
+
+    def relay():
+        for line in procs[0].stdout:
+            sys.stdout.write(line.decode(errors="replace"))
+            sys.stdout.flush()
+    th = threading.Thread(target=relay, daemon=True)
+    th.start()
+    rc, alive, deadline = 0, set(range(n)), None
+    while alive:
+        for r in sorted(alive):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            alive.discard(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                log(f"[bench] rank {r} exited with status {c}; stopping the other ranks")
+                for q in alive:
+                    procs[q].terminate()
+                deadline = time.time() + 30
+        if deadline is not None and time.time() > deadline:
+            for q in alive:
+                procs[q].kill()
+            deadline = None
+        time.sleep(0.1)
+    th.join(timeout=10)
+    return rc
+
+
+def launch_probe(path):
+    """--launch-probe: record this rank's launch environment (no torch, no GPU)."""
+    os.makedirs(path, exist_ok=True)
+    rank = int(os.environ.get("RANK", 0))
+    rec = {k.lower(): os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    rec["pid"] = os.getpid()
+    rec["torch_imported"] = "torch" in sys.modules
+    with open(os.path.join(path, f"rank{rank}.json"), "w") as f:
+        json.dump(rec, f)
+    if rank == 0:
+        print(json.dumps({"launch_probe": rec}), flush=True)
+
+
+def timed(torch, dist, dev, world, fn):
+    """Barrier + synchronize on both sides of fn(); the max over ranks (s)."""
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    return elapsed
+
+
+def replica_steps(torch, D, ctx, workers, d_q, index, qargs, steps):
+    """`steps` replica steps (cover + join against the whole index) over the
+    main context and the worker pipelines; the steps are handed out one at a
+    time, so no pipeline idles while another still has a queue (the tail is
+    at most one step)."""
+    import threading
+    tickets = [0]
+    lock = threading.Lock()
+
+    def take():
+        with lock:
+            t = tickets[0]
+            tickets[0] += 1
+        return t < steps
+
+    def run(wctx, wstream):
+        with torch.cuda.stream(wstream):
+            while take():
+                D.search(wctx, index, D.cover(wctx, d_q), *qargs)
+            wstream.synchronize()
+
+    threads = [threading.Thread(target=run, args=w) for w in workers]
+    for th in threads:
+        th.start()
+    run(ctx, torch.cuda.current_stream())
+    for th in threads:
+        th.join()
+
+
+def cover_ahead_steps(torch, D, ctx, covers, d_q, steps, search_fn):
+    """`steps` sharded steps: step k's batch is covered by covers[k % P] (own
+    context, stream and host thread) ahead of time, and the exchange + shard
+    join (`search_fn(cells)`) runs on the calling thread in step order -- one
+    communicator, so every rank issues its collectives in the same order.  A
+    cover context re-covers only after the search that read its last batch
+    (host semaphore + a stream wait on that search's event)."""
+    import queue
+    import threading
+    P = len(covers)
+    if P == 0:  # one pipeline: cover inline on the main context
+        for _ in range(steps):
+            search_fn(D.cover(ctx, d_q))
+        return
+    ready = [queue.Queue() for _ in range(P)]
+    free = [threading.Semaphore(1) for _ in range(P)]
+    done = [None] * P
+    err = []
+
+    def cover_loop(p):
+        wctx, ws = covers[p]
+        try:
+            with torch.cuda.stream(ws):
+                for _ in range(p, steps, P):
+                    free[p].acquire()
+                    if done[p] is not None:
+                        ws.wait_event(done[p])
+                    c = D.cover(wctx, d_q)
+                    ev = torch.cuda.Event()
+                    ev.record(ws)
+                    ready[p].put((c, ev))
+        except BaseException as e:  # handed to the search thread
+            err.append(e)
+            ready[p].put(None)
+
+    threads = [threading.Thread(target=cover_loop, args=(p,), daemon=True) for p in range(P)]
+    for th in threads:
+        th.start()
+    main = torch.cuda.current_stream()
+    for k in range(steps):
+        item = ready[k % P].get()
+        if item is None:
+            raise err[0]
+        c, ev = item
+        main.wait_event(ev)
+        search_fn(c)
+        ev_done = torch.cuda.Event()
+        ev_done.record(main)
+        done[k % P] = ev_done
+        free[k % P].release()
+    for th in threads:
+        th.join()
+
+
+def main():
+    argv = sys.argv[1:]
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args, argv))
+    if args.launch_probe:
+        launch_probe(args.launch_probe)
+        return
 
     heartbeat()
     keep_stdout_for_json()
@@ -133,12 +318,14 @@ def main():
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
+    if world != args.gpus:
+        log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}; the line reports n_gpus = WORLD_SIZE")
     local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", 0))
-    mode = args.mode or ("sharded" if args.config == 2 and world > 1 else "replica")
+    mode = args.mode or ("sharded" if world > 1 else "replica")
     exchange = args.exchange or ("native" if args.dist_backend == "nccl" else "torch")
     torch.cuda.set_device(local)
     stage_host = args.dist_backend != "nccl"
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")   # single-process sharded runs (no torchrun)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")   # single-process sharded runs (no launcher)
     os.environ.setdefault("MASTER_PORT", "29533")
     if world > 1 or mode == "sharded":
         if args.dist_backend == "nccl":
@@ -164,6 +351,7 @@ def main():
     d_int = D.DeviceFootprints.upload(intents, dev)
     d_q = D.DeviceFootprints.upload(queries, dev)
     q_alo, q_ahi, q_tlo, q_thi = t(qa.alt_lo), t(qa.alt_hi), t(tlo), t(qa.t1)
+    qargs = (q_alo, q_ahi, q_tlo, q_thi)
     i_alo, i_ahi, i_t0, i_t1 = t(ia.alt_lo), t(ia.alt_hi), t(ia.t0), t(ia.t1)
     torch.cuda.synchronize()
     tb = time.time()
@@ -174,15 +362,15 @@ def main():
     del d_int
     cover_i_s = time.time() - tb
     tb = time.time()
-    ranges = None
+    ranges = full_index = None
     large = i_cells_t.numel() > LARGE_POSTINGS
     if mode == "sharded":
         from dss_amd import shard
         # splitters from the intent postings (host), then this rank's shard
         i_cells_h = i_cells_t.cpu().numpy().view(np.uint64)
         ranges = shard.cell_splitters(i_cells_h, world)
-        # parity reference: the whole index
-        full_index = None if args.no_verify else D.build_index(ctx, icells, i_alo, i_ahi, i_t0, i_t1)
+        # the whole index beside the shard: the replica rate and the parity reference
+        full_index = D.build_index(ctx, icells, i_alo, i_ahi, i_t0, i_t1)
         tb = time.time()
         index = D.build_index(ctx, icells, i_alo, i_ahi, i_t0, i_t1, cell_range=ranges[rank])
     else:
@@ -210,117 +398,75 @@ def main():
             native = shard.NativeShardedSearch(ctx, shard.NativeComm(ctx, world, rank, bytes(uid.cpu().numpy())),
                                                index, ranges)
 
+    def shard_search(cells, timed_phases=False):
+        if native is not None and not timed_phases:
+            return native.step(cells.offs, cells.cells, nq, *qargs)
+        return sharded.step(cells.offs, cells.cells, nq, *qargs, timed=timed_phases)
+
     def step(timed=False):
         cells = D.cover(ctx, d_q)
-        if native is not None and not timed:
-            return cells, native.step(cells.offs, cells.cells, nq, q_alo, q_ahi, q_tlo, q_thi)
         if sharded is not None:
-            return cells, sharded.step(cells.offs, cells.cells, nq, q_alo, q_ahi, q_tlo, q_thi, timed=timed)
-        pairs = D.search(ctx, index, cells, q_alo, q_ahi, q_tlo, q_thi)
-        return cells, pairs
+            return cells, shard_search(cells, timed)
+        return cells, D.search(ctx, index, cells, *qargs)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
-    # extra pipelines: each its own context (engine scratch), stream and host
-    # thread, so one batch's cover overlaps another's join
-    import threading
+    # extra pipelines: each its own context (engine scratch), stream and host thread
     workers = []
-    if args.pipelines > 1 and sharded is None:
-        for k in range(args.pipelines - 1):
-            wctx = _lib.Context(local)
-            for k, v in tunes:
-                wctx.set_tuning(k, v)
-            wstream = torch.cuda.Stream(device=dev)
-            workers.append((wctx, wstream))
-
-    tickets = [0]
-    ticket_lock = threading.Lock() if workers else None
-
-    def take_ticket():
-        # the K timed steps are handed out one at a time, so no pipeline idles
-        # while another still has a queue of steps (the tail is <= one step)
-        with ticket_lock:
-            t = tickets[0]
-            tickets[0] += 1
-        return t < args.steps
-
-    def run_steps(wctx, wstream, n=None):
-        with torch.cuda.stream(wstream):
-            while (take_ticket() if n is None else n > 0):
-                c = D.cover(wctx, d_q)
-                D.search(wctx, index, c, q_alo, q_ahi, q_tlo, q_thi)
-                if n is not None:
-                    n -= 1
-            wstream.synchronize()
-
-    for wctx, wstream in workers:  # warm the extra contexts
-        run_steps(wctx, wstream, 1)
+    for _ in range(max(0, args.pipelines - 1)):
+        wctx = _lib.Context(local)
+        for k, v in tunes:
+            wctx.set_tuning(k, v)
+        workers.append((wctx, torch.cuda.Stream(device=dev)))
+    for wctx, ws in workers:  # warm the extra contexts (buffers at steady-state size)
+        with torch.cuda.stream(ws):
+            c = D.cover(wctx, d_q)
+            if sharded is None:
+                D.search(wctx, index, c, *qargs)
+            ws.synchronize()
 
     # ------------------------------------------------------------ timed steps
     stage("timed steps")
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    if workers:
-        threads = [threading.Thread(target=run_steps, args=(wctx, wstream)) for wctx, wstream in workers]
-        for th in threads:
-            th.start()
-        while take_ticket():
-            cells, pairs = step()
-        for th in threads:
-            th.join()
+    if sharded is not None:
+        elapsed = timed(torch, dist, dev, world,
+                        lambda: cover_ahead_steps(torch, D, ctx, workers, d_q, args.steps, shard_search))
     else:
-        for _ in range(args.steps):
-            cells, pairs = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed = timed(torch, dist, dev, world,
+                        lambda: replica_steps(torch, D, ctx, workers, d_q, index, qargs, args.steps))
     ms_per_step = 1000.0 * elapsed / max(1, args.steps)
     value = world * nq * args.steps / elapsed
 
     if sharded is not None:
-        replica = None
-        if full_index is not None and args.config == 2:
-            # the replica layout beside it (BASELINE configs[2] asks for the
-            # sharded one): every rank joins its own batch against the whole index
-            def rstep():
-                c = D.cover(ctx, d_q)
-                D.search(ctx, full_index, c, q_alo, q_ahi, q_tlo, q_thi)
-            for _ in range(args.warmup):
-                rstep()
-            dist.barrier()
-            torch.cuda.synchronize()
-            r0 = time.perf_counter()
-            for _ in range(args.steps):
-                rstep()
-            torch.cuda.synchronize()
-            dist.barrier()
-            rt = torch.tensor([time.perf_counter() - r0], device=dev, dtype=torch.float64)
-            dist.all_reduce(rt, op=dist.ReduceOp.MAX)
-            replica = {"value": world * nq * args.steps / float(rt.item()),
-                       "ms_per_step": 1000.0 * float(rt.item()) / max(1, args.steps),
-                       "note": "whole index on every GPU, each rank's batch joined locally (no exchange), one pipeline"}
+        # the replica layout beside it: every rank joins its own batch against
+        # the whole index, same pipelines, no exchange
+        stage("replica rate beside the sharded one")
+        replica_steps(torch, D, ctx, workers, d_q, full_index, qargs, max(1, args.warmup))
+        rt = timed(torch, dist, dev, world,
+                   lambda: replica_steps(torch, D, ctx, workers, d_q, full_index, qargs, args.steps))
+        replica = {"value": world * nq * args.steps / rt, "ms_per_step": 1000.0 * rt / max(1, args.steps),
+                   "pipelines_per_gpu": args.pipelines,
+                   "note": "whole index on every GPU, each rank's batch joined locally (no exchange)"}
         native_pairs = None
         if native is not None:  # the timed path's own output, checked below beside the torch path's
             c = D.cover(ctx, d_q)
-            p = native.step(c.offs, c.cells, nq, q_alo, q_ahi, q_tlo, q_thi)
+            p = native.step(c.offs, c.cells, nq, *qargs)
             nq_ = D.copy_back(ctx, p.q, int(p.n), np.uint32).astype(np.uint64)
             ne_ = D.copy_back(ctx, p.e, int(p.n), np.uint32).astype(np.uint64)
             native_pairs = (nq_ << np.uint64(32)) | ne_
-        sharded_report(args, ctx, D, dist, torch, sharded, step, full_index, i_cells_h, ranges, rank, world, nq, ni,
-                       n_post, build_s, value, ms_per_step, q_alo, q_ahi, q_tlo, q_thi, exchange, replica,
-                       native_pairs)
+        for wctx, _ in workers:
+            wctx.close()
+        sharded_report(args, ctx, D, dist, torch, sharded, step, None if args.no_verify else full_index,
+                       i_cells_h, ranges, rank, world, nq, ni, n_post, build_s, value, ms_per_step, *qargs,
+                       exchange=exchange, replica=replica, native_pairs=native_pairs)
+        if args.no_verify:
+            ctx.L.dssg_index_free(full_index)
         ctx.L.dssg_index_free(index)
         dist.destroy_process_group()
         return
+    for wctx, _ in workers:
+        wctx.close()
 
     # ------------------------------------------- phase timing + roofline
     stage(f"phase timing ({value:.4g} queries/s over the timed steps)")

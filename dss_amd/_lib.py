@@ -213,13 +213,15 @@ class Context:
 
 
 _ctx = {}
+_ctx_lock = threading.Lock()  # not _lock: Context() -> load() takes that one
 
 
 def context(device: int = 0) -> Context:
-    with _lock:
-        pass
-    c = _ctx.get(device)
-    if c is None:
-        c = Context(device)
-        _ctx[device] = c
-    return c
+    """The process's shared context for `device` (created once, under a lock,
+    so concurrent first callers get the same one)."""
+    with _ctx_lock:
+        c = _ctx.get(device)
+        if c is None:
+            c = Context(device)
+            _ctx[device] = c
+        return c

@@ -324,9 +324,6 @@ __device__ __forceinline__ double fan_area_km2(const double *t, int n, bool &fai
 template <bool FAST>
 __device__ __forceinline__ void origin_of(LoopView &l, bool &fail)
 {
-#ifdef DSS_EXP_NO_ORIGIN  // timing experiment only (wrong coverings)
-    if constexpr (FAST) return;
-#endif
     if constexpr (FAST) fastp::loop_init_origin(l, fail);
     else loop_init_origin(l);
 }

@@ -1110,9 +1110,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
     const IndexView &ix = a.ix;
     WaveOut out, tout;  // pairs, tagged keys
     unsigned long long n_tests = 0, n_bcast = 0;
-#ifdef DSS_XP_COUNT  // timing experiment only: wave-iteration counts of the join's loops
-    unsigned long long x_batches = 0, x_nonempty = 0, x_sig = 0, x_emit = 0, x_need = 0;
-#endif
     // units: kRegions queues (the unit regions), a wave starts on its own
     // region's and moves on when it is drained; grabs of g units per atomic
     int qreg = (int)(blockIdx.x % kRegions), visited = 0;
@@ -1207,9 +1204,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
         if (!(d.np & kUnitLong)) {
             const long long m = tmin2(pt.x, pt.y);
             t0min = readlane64(m, 0);  // <= every t0 of the tile
-#ifndef DSS_XP_NOHULL
             t1max = wave_max_i64((uint32_t)lane < np ? (pt.x > pt.y ? pt.x : pt.y) : LLONG_MIN);
-#endif
         }
         const uint32_t ra0 = d.n0, ra1 = d.n1, rb0 = d.w0, rb1 = d.w1;
         const bool pfirst = (pe & kFirstBit) != 0;                  // entity's smallest cell
@@ -1224,11 +1219,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 bool rel = false;
                 int4 h0 = make_int4(0, 0, 0, 0), h1 = h0;
                 ulonglong2 g0 = make_ulonglong2(0, 0), g1 = g0;
-#ifdef DSS_XP_NOSTAGE  // timing experiment only: no record loads, nothing staged
-                if (r < x1 && r == 0xffffffffu) {
-#else
                 if (r < x1) {
-#endif
                     const int4 *r4 = reinterpret_cast<const int4 *>(recs + sval[r]);
                     h0 = r4[0];
                     h1 = r4[1];
@@ -1242,14 +1233,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 }
                 const unsigned long long relm = __ballot(rel);
                 const int nrel = uni32(__popcll(relm));
-#ifdef DSS_XP_NOLDS  // timing experiment only: records loaded and hull-tested, not staged
-                n_bcast += (unsigned long long)nrel;
-                continue;
-#endif
-#ifdef DSS_XP_COUNT
-                x_batches++;
-                x_nonempty += nrel ? 1 : 0;
-#endif
                 if (!nrel) continue;
                 const uint32_t slot = mbcnt64(relm);
                 __builtin_amdgcn_wave_barrier();
@@ -1269,9 +1252,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 const unsigned long long RL = LONG ? __ballot((qslot & kLongQ) != 0) : 0ull;
                 n_bcast += (unsigned long long)nrel;
                 n_tests += (unsigned long long)nrel * (unsigned long long)__popcll(vmask);
-#ifdef DSS_XP_NOTEST  // timing experiment only: records staged, never tested
-                if (R0 | RC | RL) continue;
-#endif
                 // (1) this lane's posting against every staged record: a bit per
                 // passing record.  COALESCE'd predicates of operations.go:394-402
                 // (NULL -> sentinels).
@@ -1308,10 +1288,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 // tagged set is deduplicated after the join); else exact merge.
                 unsigned long long keep = pfirst ? m : (m & R0);
                 unsigned long long need = m & ~keep;
-#ifdef DSS_XP_NOSIG  // timing experiment only: no smallest-shared-cell test
-                keep = m;
-                need = 0;
-#endif
                 if (!usig) {  // lazy signatures: the lanes that need them now
                     const bool want = need != 0ull && !lsig;
                     if (__ballot(want)) {
@@ -1323,10 +1299,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                         }
                     }
                 }
-#ifdef DSS_XP_COUNT
-                x_sig += wave_max((uint32_t)__popcll(need));
-                x_need += __builtin_amdgcn_readlane((int)wave_incl_scan((uint32_t)__popcll(need)), 63);
-#endif
                 // lane-major (each lane walks its own checks): full batches
                 while (need) {
                     const int j = __builtin_ctzll(need);
@@ -1358,15 +1330,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 WaveOut::Span su{}, st{};
                 if (total_u) su = out.reserve(a.out.ps, total_u);
                 if (LONG && total_t) st = tout.reserve(a.out.ts, total_t);
-#ifdef DSS_XP_NOEMIT  // timing experiment only: reserved, not written
-                continue;
-#endif
                 const bool wu = out.have != 0, wt = LONG && tout.have != 0;  // else counted only (rerun)
-#ifdef DSS_XP_COUNT
-                x_emit += (int64_t)(total_u + total_t) * kEmitDensity <= (int64_t)nrel * __popcll(vmask)
-                              ? wave_max((uint32_t)__popcll(keep))
-                              : (unsigned long long)nrel;
-#endif
                 if ((int64_t)(total_u + total_t) * kEmitDensity <= (int64_t)nrel * __popcll(vmask)) {
                     // (one loop per stream: no divergent double bodies)
                     if (!LONG && kOutStage && wu && total_u <= kOutStage) {  // (long variants: direct, no VGPR headroom)
@@ -1441,13 +1405,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
     if (lane == 0) {
         atomicAdd(&a.out.counter[2], n_tests);
         atomicAdd(&a.out.counter[3], n_bcast);
-#ifdef DSS_XP_COUNT
-        atomicAdd(&a.out.counter[6], x_batches);
-        atomicAdd(&a.out.counter[7], x_nonempty);
-        atomicAdd(&a.out.counter[8], x_sig);
-        atomicAdd(&a.out.counter[13], x_emit);
-        atomicAdd(&a.out.counter[14], x_need);
-#endif
     }
 }
 
@@ -2186,11 +2143,6 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         tests_ = (int64_t)h[kCtlMisc + 2];
         iters_ = (int64_t)h[kCtlMisc + 3];
         long_queries_ = (int64_t)h[kCtlMisc + 5];
-#ifdef DSS_XP_COUNT
-        fprintf(stderr, "[xp] batches %llu nonempty %llu sig_iters %llu need %llu emit_iters %llu bcast %llu tests %llu\n",
-                h[kCtlMisc + 6], h[kCtlMisc + 7], h[kCtlMisc + 8], h[kCtlMisc + 14], h[kCtlMisc + 13], h[kCtlMisc + 3],
-                h[kCtlMisc + 2]);
-#endif
         long_postings_ = idx->n_long_fp;
         tagged_ = nt;
         close_holes(nch, fills, n, MovePairs{oq, oe});

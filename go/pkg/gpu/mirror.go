@@ -172,7 +172,11 @@ func (m *Mirror) Delete(keys []string) error {
 }
 
 // Search runs a batch of queries; result i holds the keys matching query i
-// (each once: the SQL DISTINCT / && semantics), in key-id order.
+// (each once: the SQL DISTINCT / && semantics), in key-id order.  A query
+// filtered by an owner that has no row in the mirror matches nothing
+// (`subscriptions.owner = $2`, pkg/rid/cockroach/subscriptions.go:245-273)
+// and is answered here, never sent: the engine reads a negative owner as
+// "any owner" (dssgpu.h), so no sentinel id may stand for it.
 func (m *Mirror) Search(qs []Query) ([][]string, error) {
 	out := make([][]string, len(qs))
 	if len(qs) == 0 {
@@ -180,33 +184,42 @@ func (m *Mirror) Search(qs []Query) ([][]string, error) {
 	}
 	m.mu.RLock()
 	defer m.mu.RUnlock()
+	sent := make([]int, 0, len(qs)) // engine query k = qs[sent[k]]
+	own := make([]C.int32_t, 0, len(qs))
+	for i, q := range qs {
+		o := C.int32_t(-1)
+		if q.Owner != "" {
+			id, ok := m.owners[q.Owner]
+			if !ok {
+				continue // no rows of this owner: empty result
+			}
+			o = C.int32_t(id)
+		}
+		sent = append(sent, i)
+		own = append(own, o)
+	}
+	n := len(sent)
+	if n == 0 {
+		return out, nil
+	}
 	c, err := getCtx()
 	if err != nil {
 		return nil, err
 	}
 	defer putCtx(c)
-	n := len(qs)
 	offs := make([]C.int64_t, n+1)
 	lo, hi := make([]C.float, n), make([]C.float, n)
 	tlo, thi := make([]C.int64_t, n), make([]C.int64_t, n)
-	own := make([]C.int32_t, n)
-	for i, q := range qs {
-		offs[i+1] = offs[i] + C.int64_t(len(q.Cells))
-		lo[i], hi[i] = C.float(q.AltLo), C.float(q.AltHi)
-		tlo[i], thi[i] = C.int64_t(q.TLo), C.int64_t(q.THi)
-		own[i] = -1
-		if q.Owner != "" {
-			id, ok := m.owners[q.Owner]
-			if !ok {
-				id = -2 // an owner with no rows matches nothing
-			}
-			own[i] = C.int32_t(id)
-		}
+	for k, i := range sent {
+		q := qs[i]
+		offs[k+1] = offs[k] + C.int64_t(len(q.Cells))
+		lo[k], hi[k] = C.float(q.AltLo), C.float(q.AltHi)
+		tlo[k], thi[k] = C.int64_t(q.TLo), C.int64_t(q.THi)
 	}
 	cells := make([]uint64, int(offs[n])+1)
-	for i, q := range qs {
-		for k, cid := range q.Cells {
-			cells[int(offs[i])+k] = uint64(cid)
+	for k, i := range sent {
+		for j, cid := range qs[i].Cells {
+			cells[int(offs[k])+j] = uint64(cid)
 		}
 	}
 	var ownp *C.int32_t
@@ -230,7 +243,8 @@ func (m *Mirror) Search(qs []Query) ([][]string, error) {
 			if int(pe[k]) >= len(m.keys) || m.keys[pe[k]] == "" {
 				return nil, fmt.Errorf("dssg_store_search: id %d not live", pe[k])
 			}
-			out[pq[k]] = append(out[pq[k]], m.keys[pe[k]])
+			i := sent[pq[k]]
+			out[i] = append(out[i], m.keys[pe[k]])
 		}
 		return out, nil
 	}

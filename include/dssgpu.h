@@ -84,11 +84,13 @@ typedef struct {
 } dssg_cells;
 
 /* Device-resident search result: unordered set of (query, entity) pairs,
- * each pair once (SQL DISTINCT, quirk Q13).  The last n_tagged pairs are
- * "long x long" pairs (both footprints spread beyond one 8x8-cell window):
- * unique within this result, but a cell-range shard (dssg_index_build_range)
- * can meet such a pair on another shard too, so a sharded caller dedupes
- * those across shards (the route layer carries the tag). */
+ * each pair once (SQL DISTINCT, quirk Q13).  n_tagged is informational: the
+ * last n_tagged pairs are the "long x long" ones (both footprints spread
+ * beyond one 8x8-cell window) that the join deduplicated after the fact.
+ * Cell-range shards (dssg_index_build_range) already return those exactly
+ * once across shards (a shard past the first drops the ones whose smallest
+ * shared cell lies below its range), so a sharded caller needs no dedupe;
+ * dssg_sharded_search_device reports n_tagged = 0. */
 typedef struct {
     const uint32_t *q; /* device */
     const uint32_t *e; /* device */
