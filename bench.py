@@ -891,91 +891,60 @@ def cover_roofline(fp, offs, cells, cover_ms):
             "counts": {"footprints": n, "E": int(nv.sum()), "C": int(cp.sum()), "R": int(rp.sum())}}
 
 
-def request_latency(ctx, D, index, queries, qa, now, n_alone=500, callers=64, seconds=2.0):
+def request_latency(ctx, D, index, queries, qa, now, n_alone=3000, callers=64, seconds=2.0):
     """The per-RPC path the reference runs (one covering + one SQL search per
-    request): (a) one request at a time through the host ABI
-    (dssg_cover_batch + dssg_search_operations, each a host round trip);
-    (b) `callers` threads each issuing requests back to back through the
-    micro-batcher (dssg_batcher), which coalesces them into shared cover +
-    join launches.  p50 / p99 request latency in ms and requests/s."""
+    request, pkg/scd/operations_handler.go:118-168), driven by native caller
+    threads (tools/loadgen.c; Python threads could not issue the calls at
+    this rate):
+      alone:  one request at a time through the unbatched ABI
+              (dssg_cover_batch, then dssg_search_operations: host buffers in
+              and out, the capacity protocol), as the Go binding calls it;
+      single: one caller through the micro-batcher (dssg_batcher);
+      batched: `callers` threads issuing requests back to back through the
+              batcher (2 workers, each its own context and stream).
+    p50 / p99 request latency in ms and requests/s."""
     import ctypes as C
-    import threading
-    from dss_amd.store import Batcher, _p
-    from dss_amd._lib import DSSG_ERR_CAPACITY
-    L = ctx.L
-    lat_ms = []
-    cap = 1 << 16
-    cells = np.empty(cap, np.uint64)
-    oq, oe = np.empty(cap, np.uint32), np.empty(cap, np.uint32)
-    for k in range(n_alone):
-        i = k % queries.n
-        v0, v1 = queries.voff[i], queries.voff[i + 1]
-        kind = np.array([queries.kind[i]], np.int32)
-        voff = np.array([0, v1 - v0], np.int64)
-        la, lg = np.ascontiguousarray(queries.lat[v0:v1]), np.ascontiguousarray(queries.lng[v0:v1])
-        rad = np.array([queries.radius_m[i]], np.float32)
-        offs = np.zeros(2, np.int64)
-        st, area, need = np.zeros(1, np.int32), np.zeros(1), C.c_int64()
-        lo, hi = np.array([qa.alt_lo[i]], np.float32), np.array([qa.alt_hi[i]], np.float32)
-        s0, e0 = np.array([qa.t0[i]], np.int64), np.array([qa.t1[i]], np.int64)
-        t0 = time.perf_counter()
-        # the ABI's capacity protocol, as a caller follows it: DSSG_ERR_CAPACITY
-        # -> grow to *needed and call again (counted in the request's latency)
-        while True:
-            rc = L.dssg_cover_batch(ctx.h, 1, _p(kind, C.c_int32), _p(voff, C.c_int64), _p(la, C.c_double),
-                                    _p(lg, C.c_double), _p(rad, C.c_float), _p(offs, C.c_int64),
-                                    _p(cells, C.c_uint64), len(cells), C.byref(need), _p(st, C.c_int32),
-                                    _p(area, C.c_double))
-            if rc != DSSG_ERR_CAPACITY:
-                break
-            cells = np.empty(int(need.value) + 1, np.uint64)
-        ctx.check(rc)
-        while True:
-            rc = L.dssg_search_operations(ctx.h, index, 1, _p(offs, C.c_int64), _p(cells, C.c_uint64),
-                                          _p(lo, C.c_float), _p(hi, C.c_float), _p(s0, C.c_int64),
-                                          _p(e0, C.c_int64), int(now), _p(oq, C.c_uint32), _p(oe, C.c_uint32),
-                                          len(oq), C.byref(need))
-            if rc != DSSG_ERR_CAPACITY:
-                break
-            oq, oe = np.empty(int(need.value) + 1, np.uint32), np.empty(int(need.value) + 1, np.uint32)
-        ctx.check(rc)
-        lat_ms.append(1000.0 * (time.perf_counter() - t0))
-    alone = np.array(lat_ms[20:])
-
+    from dss_amd.store import Batcher
+    lg = C.CDLL(os.path.join(ROOT, "tools", "libloadgen.so"))
+    vp = C.c_void_p
+    n = queries.n
+    a = lambda x, t: np.ascontiguousarray(x, dtype=t)  # noqa: E731
+    kind, voff = a(queries.kind, np.int32), a(queries.voff, np.int64)
+    la, ln, rad = a(queries.lat, np.float64), a(queries.lng, np.float64), a(queries.radius_m, np.float32)
+    alo, ahi, t0, t1 = a(qa.alt_lo, np.float32), a(qa.alt_hi, np.float32), a(qa.t0, np.int64), a(qa.t1, np.int64)
+    work = [n] + [x.ctypes.data_as(vp) for x in (kind, voff, la, ln, rad, alo, ahi, t0, t1)] + [int(now)]
+    lg.dssl_alone.argtypes = [vp, vp, C.c_int64, C.c_int64] + [vp] * 9 + [C.c_int64, vp, vp]
+    lg.dssl_batched.argtypes = [vp, C.c_int, C.c_double, C.c_int64] + [vp] * 9 + [C.c_int64, C.c_int64, vp, vp, vp,
+                                                                                    vp, vp]
+    lat_a = np.zeros(n_alone)
+    nerr = C.c_int64()
+    ctx.check(lg.dssl_alone(ctx.h, index, n_alone, *work, lat_a.ctypes.data_as(vp), C.byref(nerr)))
+    alone = lat_a[min(200, n_alone // 4):]
     import types
-    b = Batcher(types.SimpleNamespace(h=index), max_batch=4096, max_wait_us=100)  # (an index handle holder)
-    stop = [False]
-    rec = [[] for _ in range(callers)]
+    b = Batcher(types.SimpleNamespace(h=index), max_batch=4096, max_wait_us=0)  # (an index handle holder)
 
-    def caller(k):
-        i = k
-        while not stop[0]:
-            v0, v1 = queries.voff[i], queries.voff[i + 1]
-            t0 = time.perf_counter()
-            b.search_operations(queries.kind[i], queries.lat[v0:v1], queries.lng[v0:v1], queries.radius_m[i],
-                                qa.alt_lo[i], qa.alt_hi[i], qa.t0[i], qa.t1[i], now)
-            rec[k].append(1000.0 * (time.perf_counter() - t0))
-            i = (i + callers) % queries.n
-
-    ths = [threading.Thread(target=caller, args=(k,)) for k in range(callers)]
-    t_start = time.perf_counter()
-    for t in ths:
-        t.start()
-    time.sleep(seconds)
-    stop[0] = True
-    for t in ths:
-        t.join()
-    wall = time.perf_counter() - t_start
-    nreq, nbatch = b.stats()
+    def run(threads, secs):
+        cap = 1 << 22
+        lat = np.zeros(cap)
+        ns, nr, ne, wall = C.c_int64(), C.c_int64(), C.c_int64(), C.c_double()
+        nreq0, nb0 = b.stats()
+        ctx.check(lg.dssl_batched(b.h, threads, secs, *work, cap, lat.ctypes.data_as(vp), C.byref(ns), C.byref(nr),
+                                  C.byref(ne), C.byref(wall)))
+        nreq1, nb1 = b.stats()
+        lat = lat[: ns.value]
+        return {"callers": threads, "requests": int(nr.value), "errors": int(ne.value),
+                "batches": int(nb1 - nb0), "mean_batch": float((nreq1 - nreq0) / max(1, nb1 - nb0)),
+                "p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
+                "requests_per_s": float(nr.value / wall.value)}
+    run(1, 0.3)  # warm the workers' contexts
+    single = run(1, 1.0)
+    batched = run(callers, seconds)
     b.close()
-    allr = np.concatenate([np.array(r) for r in rec if r]) if any(rec) else np.zeros(1)
-    return {"alone": {"requests": len(alone), "p50_ms": float(np.percentile(alone, 50)),
+    return {"alone": {"requests": len(alone), "errors": int(nerr.value), "p50_ms": float(np.percentile(alone, 50)),
                       "p99_ms": float(np.percentile(alone, 99)), "requests_per_s": float(1000.0 / alone.mean())},
-            "batched": {"callers": callers, "requests": int(nreq), "batches": int(nbatch),
-                        "mean_batch": float(nreq / max(1, nbatch)), "p50_ms": float(np.percentile(allr, 50)),
-                        "p99_ms": float(np.percentile(allr, 99)), "requests_per_s": float(nreq / wall)},
+            "single": single, "batched": batched,
             "note": "one request = cover 1 footprint + searchOperations, host buffers in and out (the RPC path); "
-                    "batched: Python caller threads through dssg_batcher (max_wait 100 us)"}
+                    "native caller threads (tools/loadgen.c); batched: dssg_batcher, 2 workers, no fixed wait"}
 
 
 def cover_fp64(nq, ni):
@@ -1066,12 +1035,24 @@ def cpu_baseline(args, ctx, intents, ia, queries, qa, now, intent_csr_fn, g_cell
     t3 = time.perf_counter()
     stage(f"cpu baseline: search {t3 - t2:.1f}s; parity")
     re = ents[re]
+    # the reference's per-request shape on the CPU: one covering + one search
+    # per request, one thread (ctypes call overhead included, ~10 us)
+    req_ms = []
+    for k in range(min(400, n)):
+        v0, v1 = int(sub.voff[k]), int(sub.voff[k + 1])
+        tr = time.perf_counter()
+        o1, c1, _, _ = O.cover_batch(sub.kind[k:k + 1], np.array([0, v1 - v0]), sub.lat[v0:v1], sub.lng[v0:v1],
+                                     sub.radius_m[k:k + 1], nthreads=1)
+        idx.search(o1, c1, qa.alt_lo[k:k + 1], qa.alt_hi[k:k + 1], tlo[k:k + 1], qa.t1[k:k + 1], nthreads=1)
+        req_ms.append(1000.0 * (time.perf_counter() - tr))
     info = cpu_info()
     secs = (t1 - t0) + (t3 - t2)
     cpu = {"value": n / secs, "unit": "queries/s", "cores": th, "kind": "port",
            "sample": f"{n} of the step's {queries.n} queries (cover + search) vs the {intents.n}-intent index"
                      + ("" if len(ents) == intents.n else f" (the {len(ents)} intents sharing a cell with the sample)"),
            "coverings_per_s": n / (t1 - t0), "seconds": secs, "cpu_model": info["model"],
+           "single_request": {"requests": len(req_ms), "p50_ms": float(np.percentile(req_ms, 50)),
+                              "p99_ms": float(np.percentile(req_ms, 99)), "threads": 1},
            "nproc": info["nproc"], "affinity_cpus": info["affinity"],
            "threads_note": "threads = the process's CPU share on the GPU box (OMP_NUM_THREADS / affinity)"}
     parity = None

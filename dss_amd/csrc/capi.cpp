@@ -239,6 +239,14 @@ int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value)
         ctx->search.set_lazy_sig_recs(value);
         return DSSG_OK;
     }
+    if (std::string(key) == "small_search") {  // max queries of the one-launch small-batch join (0: never)
+        ctx->search.set_small_max_q(value);
+        return DSSG_OK;
+    }
+    if (std::string(key) == "cover_wave") {  // 0: every footprint through the general covering pipeline
+        ctx->cover.set_wave_path(value != 0);
+        return DSSG_OK;
+    }
     return DSSG_ERR_INVALID;
 }
 
@@ -1171,14 +1179,19 @@ int dssg_sharded_search_device(dssg_ctx *ctx, dssg_comm *comm, const dssg_index 
  * Micro-batcher: the per-RPC path.  The reference runs one covering and one
  * SQL search per request (pkg/scd/operations_handler.go:118-168,
  * pkg/rid/server/isa_handler.go:153-207); here concurrent single requests
- * are coalesced by a worker thread into one cover launch and one join per
- * batch (up to max_batch requests, waiting at most max_wait_us after the
- * first), and each caller gets its own answer back.
+ * are coalesced into one cover launch and one join per batch, and each
+ * caller gets its own answer back.  Several workers, each with its own
+ * context, stream and pinned staging, run batches concurrently: while one
+ * batch is on the GPU the next one is collected and started by another
+ * worker, so batches form from whatever queued meanwhile (no fixed delay
+ * when a worker is idle).  Small batches take the wave-path covering and
+ * the one-launch small join (k_small_join).
  * ====================================================================== */
 struct dssg_batcher {
     struct Req {
         int32_t kind = 0;
-        std::vector<double> lat, lng;
+        const double *lat = nullptr, *lng = nullptr;  // the caller's arrays (it blocks until done)
+        int64_t nv = 0;
         float radius = 0, alo = 0, ahi = 0;
         int64_t tlo = 0, thi = 0;
         std::vector<uint32_t> ids;
@@ -1188,74 +1201,116 @@ struct dssg_batcher {
         std::string err;
         bool done = false;
     };
-    dssg_ctx *ctx = nullptr;
+    struct Worker {
+        dssg_ctx *ctx = nullptr;
+        std::thread th;
+        unsigned char *h_in = nullptr, *h_out = nullptr;  // pinned staging
+        size_t in_cap = 0, out_cap = 0;
+        dss::DevBuf<unsigned char> d_in;
+        std::vector<int64_t> cnt;
+    };
     const dssg_index *idx = nullptr;
-    int max_batch = 1024, max_wait_us = 200;
+    int max_batch = 1024, max_wait_us = 0;
     std::mutex mu;
     std::condition_variable cv, done_cv;
     std::deque<Req *> queue;
     bool stop = false;
+    int busy = 0;
     int64_t n_requests = 0, n_batches = 0;
-    std::thread worker;
+    std::vector<Worker *> workers;
+    // answers a caller could not take (DSSG_ERR_CAPACITY): kept for its retry
+    std::mutex cache_mu;
+    std::deque<std::pair<uint64_t, std::pair<double, std::vector<uint32_t>>>> cache;
 
-    void run_batch(std::vector<Req *> &b)
+    static size_t al8(size_t x) { return (x + 7) & ~(size_t)7; }
+
+    static void pinned(unsigned char *&p, size_t &cap, size_t need)
+    {
+        if (need <= cap) return;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t n = std::max(need + need / 2, (size_t)1 << 16);
+        DSS_HIP(hipHostMalloc((void **)&p, n, hipHostMallocDefault));
+        cap = n;
+    }
+
+    void run_batch(Worker &w, std::vector<Req *> &b)
     {
         const int64_t n = (int64_t)b.size();
-        std::vector<int32_t> kind(n);
-        std::vector<int64_t> voff(n + 1, 0), tlo(n), thi(n);
-        std::vector<float> rad(n), alo(n), ahi(n);
-        std::vector<double> lat, lng;
-        for (int64_t i = 0; i < n; i++) {
-            Req *r = b[i];
-            kind[i] = r->kind;
-            voff[i + 1] = voff[i] + (int64_t)r->lat.size();
-            lat.insert(lat.end(), r->lat.begin(), r->lat.end());
-            lng.insert(lng.end(), r->lng.begin(), r->lng.end());
-            rad[i] = r->radius;
-            alo[i] = r->alo;
-            ahi[i] = r->ahi;
-            tlo[i] = r->tlo;
-            thi[i] = r->thi;
-        }
-        std::vector<int32_t> status(n);
-        std::vector<double> area(n);
-        std::vector<uint32_t> pq, pe;
-        const int rc = guarded(ctx, [&] {
-            hipStream_t s = ctx->stream;
-            const int64_t nv = voff[n];
-            const int32_t *dk = upload(ctx->d_kind, kind.data(), n, s);
-            const int64_t *dv = upload(ctx->d_voff, voff.data(), n + 1, s);
-            const double *dla = upload(ctx->d_lat, lat.data(), nv, s);
-            const double *dln = upload(ctx->d_lng, lng.data(), nv, s);
-            const float *dr = upload(ctx->d_rad, rad.data(), n, s);
+        int64_t nv = 0;
+        for (Req *r : b) nv += r->nv;
+        // packed input layout (8-byte aligned sections), one H2D copy
+        const size_t o_kind = 0, o_voff = al8(o_kind + 4 * n), o_lat = al8(o_voff + 8 * (n + 1)),
+                     o_lng = o_lat + 8 * nv, o_rad = o_lng + 8 * nv, o_alo = al8(o_rad + 4 * n),
+                     o_ahi = al8(o_alo + 4 * n), o_tlo = al8(o_ahi + 4 * n), o_thi = o_tlo + 8 * n,
+                     in_bytes = o_thi + 8 * n;
+        int64_t npairs = 0;
+        const int rc = guarded(w.ctx, [&] {
+            hipStream_t s = w.ctx->stream;
+            pinned(w.h_in, w.in_cap, in_bytes);
+            unsigned char *h = w.h_in;
+            int32_t *kind = (int32_t *)(h + o_kind);
+            int64_t *voff = (int64_t *)(h + o_voff);
+            double *lat = (double *)(h + o_lat), *lng = (double *)(h + o_lng);
+            float *rad = (float *)(h + o_rad), *alo = (float *)(h + o_alo), *ahi = (float *)(h + o_ahi);
+            int64_t *tlo = (int64_t *)(h + o_tlo), *thi = (int64_t *)(h + o_thi);
+            voff[0] = 0;
+            for (int64_t i = 0; i < n; i++) {
+                const Req *r = b[i];
+                kind[i] = r->kind;
+                if (r->nv > 0) {
+                    std::memcpy(lat + voff[i], r->lat, sizeof(double) * (size_t)r->nv);
+                    std::memcpy(lng + voff[i], r->lng, sizeof(double) * (size_t)r->nv);
+                }
+                voff[i + 1] = voff[i] + r->nv;
+                rad[i] = r->radius;
+                alo[i] = r->alo;
+                ahi[i] = r->ahi;
+                tlo[i] = r->tlo;
+                thi[i] = r->thi;
+            }
+            unsigned char *d = w.d_in.ensure(in_bytes + 8);
+            DSS_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s));
             dssg_cells cov;
-            ctx->cover.run(n, dk, dv, dla, dln, dr, s, &cov);
-            DSS_HIP(hipMemcpyAsync(status.data(), cov.status, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, s));
-            DSS_HIP(hipMemcpyAsync(area.data(), cov.area_km2, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, s));
-            const float *dlo = upload(ctx->d_alo, alo.data(), n, s);
-            const float *dhi = upload(ctx->d_ahi, ahi.data(), n, s);
-            const int64_t *dtl = upload(ctx->d_tlo, tlo.data(), n, s);
-            const int64_t *dth = upload(ctx->d_thi, thi.data(), n, s);
+            w.ctx->cover.run(n, (const int32_t *)(d + o_kind), (const int64_t *)(d + o_voff), (const double *)(d + o_lat),
+                             (const double *)(d + o_lng), (const float *)(d + o_rad), s, &cov);
             dssg_pairs res{};
-            if (cov.total_cells > 0) ctx->search.search(idx, n, cov.offs, cov.cells, dlo, dhi, dtl, dth, nullptr, s, &res);
-            pq.resize((size_t)res.n);
-            pe.resize((size_t)res.n);
-            if (res.n > 0) {
-                DSS_HIP(hipMemcpyAsync(pq.data(), res.q, sizeof(uint32_t) * (size_t)res.n, hipMemcpyDeviceToHost, s));
-                DSS_HIP(hipMemcpyAsync(pe.data(), res.e, sizeof(uint32_t) * (size_t)res.n, hipMemcpyDeviceToHost, s));
+            if (cov.total_cells > 0)
+                w.ctx->search.search(idx, n, cov.offs, cov.cells, (const float *)(d + o_alo), (const float *)(d + o_ahi),
+                                     (const int64_t *)(d + o_tlo), (const int64_t *)(d + o_thi), nullptr, s, &res);
+            npairs = res.n;
+            const size_t r_area = 0, r_stat = 8 * n, r_q = al8(r_stat + 4 * n), r_e = r_q + 4 * npairs,
+                         out_bytes = r_e + 4 * npairs;
+            pinned(w.h_out, w.out_cap, out_bytes + 8);
+            DSS_HIP(hipMemcpyAsync(w.h_out + r_area, cov.area_km2, 8 * n, hipMemcpyDeviceToHost, s));
+            DSS_HIP(hipMemcpyAsync(w.h_out + r_stat, cov.status, 4 * n, hipMemcpyDeviceToHost, s));
+            if (npairs > 0) {
+                DSS_HIP(hipMemcpyAsync(w.h_out + r_q, res.q, 4 * npairs, hipMemcpyDeviceToHost, s));
+                DSS_HIP(hipMemcpyAsync(w.h_out + r_e, res.e, 4 * npairs, hipMemcpyDeviceToHost, s));
             }
             DSS_HIP(hipStreamSynchronize(s));
-            if (res.n > 0) sort_pairs_host(pq.data(), pe.data(), res.n);
+            // each request's ids (unsorted here; the caller sorts its own)
+            const uint32_t *pq = (const uint32_t *)(w.h_out + r_q), *pe = (const uint32_t *)(w.h_out + r_e);
+            w.cnt.assign((size_t)n, 0);
+            for (int64_t k = 0; k < npairs; k++) w.cnt[pq[k]]++;
+            for (int64_t i = 0; i < n; i++) b[i]->ids.reserve((size_t)w.cnt[i]);
+            for (int64_t k = 0; k < npairs; k++) b[pq[k]]->ids.push_back(pe[k]);
+            const double *area = (const double *)(w.h_out + r_area);
+            const int32_t *st = (const int32_t *)(w.h_out + r_stat);
+            for (int64_t i = 0; i < n; i++) {
+                b[i]->status = st[i];
+                b[i]->area = area[i];
+            }
         });
         std::lock_guard<std::mutex> lk(mu);
-        size_t k = 0;
         for (int64_t i = 0; i < n; i++) {
             Req *r = b[i];
             r->rc = rc;
-            if (rc != DSSG_OK) r->err = ctx->last_error;
-            r->status = status[i];
-            r->area = area[i];
-            while (k < pq.size() && (int64_t)pq[k] == i) r->ids.push_back(pe[k++]);
+            if (rc != DSSG_OK) {
+                r->err = w.ctx->last_error;
+                r->ids.clear();
+            }
             r->done = true;
         }
         n_batches++;
@@ -1263,39 +1318,83 @@ struct dssg_batcher {
         done_cv.notify_all();
     }
 
-    void loop()
+    void loop(Worker &w)
     {
         std::unique_lock<std::mutex> lk(mu);
         while (true) {
             cv.wait(lk, [&] { return stop || !queue.empty(); });
-            if (queue.empty() && stop) return;
-            // coalesce: until max_batch requests or max_wait_us after the first
-            const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(max_wait_us);
-            cv.wait_until(lk, until, [&] { return stop || (int)queue.size() >= max_batch; });
+            if (queue.empty()) {
+                if (stop) return;
+                continue;
+            }
+            // another batch in flight: collect a little longer (bounded), else go now
+            if (busy > 0 && max_wait_us > 0 && (int)queue.size() < max_batch) {
+                const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(max_wait_us);
+                cv.wait_until(lk, until, [&] { return stop || (int)queue.size() >= max_batch; });
+                if (queue.empty()) continue;
+            }
             std::vector<Req *> b;
             while (!queue.empty() && (int)b.size() < max_batch) {
                 b.push_back(queue.front());
                 queue.pop_front();
             }
+            busy++;
             lk.unlock();
-            run_batch(b);
+            run_batch(w, b);
             lk.lock();
+            busy--;
         }
     }
 };
 
+namespace {
+// FNV-1a over a request's inputs: the key of an answer kept for a retry.
+uint64_t request_key(int32_t kind, int64_t nv, const double *lat, const double *lng, float radius_m, float alt_lo,
+                     float alt_hi, int64_t start, int64_t end, int64_t now_us)
+{
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void *p, size_t n) {
+        const unsigned char *c = (const unsigned char *)p;
+        for (size_t i = 0; i < n; i++) h = (h ^ c[i]) * 1099511628211ull;
+    };
+    mix(&kind, sizeof(kind));
+    mix(&nv, sizeof(nv));
+    if (nv > 0) {
+        mix(lat, sizeof(double) * (size_t)nv);
+        mix(lng, sizeof(double) * (size_t)nv);
+    }
+    mix(&radius_m, 4);
+    mix(&alt_lo, 4);
+    mix(&alt_hi, 4);
+    mix(&start, 8);
+    mix(&end, 8);
+    mix(&now_us, 8);
+    return h;
+}
+}  // namespace
+
 int dssg_batcher_create(int device, const dssg_index *idx, int32_t max_batch, int32_t max_wait_us, dssg_batcher **out)
 {
     if (!idx || !out || max_batch < 1 || max_wait_us < 0) return DSSG_ERR_INVALID;
-    dssg_ctx *ctx = nullptr;
-    const int rc = dssg_create(device, &ctx);
-    if (rc != DSSG_OK) return rc;
+    if (device != idx->device) return DSSG_ERR_INVALID;  // the workers join against this device's index
+    int nw = 2;
+    if (const char *e = std::getenv("DSSG_BATCHER_WORKERS")) nw = std::max(1, std::min(16, std::atoi(e)));
     auto *b = new dssg_batcher();
-    b->ctx = ctx;
     b->idx = idx;
     b->max_batch = max_batch;
     b->max_wait_us = max_wait_us;
-    b->worker = std::thread([b] { b->loop(); });
+    for (int k = 0; k < nw; k++) {
+        auto *w = new dssg_batcher::Worker();
+        const int rc = dssg_create(device, &w->ctx);
+        if (rc != DSSG_OK) {
+            delete w;
+            b->stop = true;
+            dssg_batcher_free(b);
+            return rc;
+        }
+        b->workers.push_back(w);
+    }
+    for (auto *w : b->workers) w->th = std::thread([b, w] { b->loop(*w); });
     *out = b;
     return DSSG_OK;
 }
@@ -1308,8 +1407,16 @@ void dssg_batcher_free(dssg_batcher *b)
         b->stop = true;
     }
     b->cv.notify_all();
-    if (b->worker.joinable()) b->worker.join();
-    dssg_destroy(b->ctx);
+    for (auto *w : b->workers) {
+        if (w->th.joinable()) w->th.join();
+        if (w->ctx) {
+            (void)hipSetDevice(w->ctx->device);
+            if (w->h_in) (void)hipHostFree(w->h_in);
+            if (w->h_out) (void)hipHostFree(w->h_out);
+        }
+        dssg_destroy(w->ctx);
+        delete w;
+    }
     delete b;
 }
 
@@ -1322,26 +1429,50 @@ int dssg_batcher_search_operations(dssg_batcher *b, int32_t kind, int64_t nv, co
         (kind != DSSG_KIND_POLYGON && kind != DSSG_KIND_CIRCLE && kind != DSSG_KIND_POINTS))
         return DSSG_ERR_INVALID;
     dssg_batcher::Req r;
-    r.kind = kind;
-    if (nv > 0) {
-        r.lat.assign(lat, lat + nv);
-        r.lng.assign(lng, lng + nv);
+    const uint64_t key = request_key(kind, nv, lat, lng, radius_m, alt_lo, alt_hi, start, end, now_us);
+    bool cached = false;
+    {  // the retry of a request whose answer did not fit: no second cover + join
+        std::lock_guard<std::mutex> lk(b->cache_mu);
+        for (auto it = b->cache.begin(); it != b->cache.end(); ++it)
+            if (it->first == key && (int64_t)it->second.second.size() <= cap) {
+                r.area = it->second.first;
+                r.ids = std::move(it->second.second);
+                b->cache.erase(it);
+                cached = true;
+                break;
+            }
     }
-    r.radius = radius_m;
-    r.alo = alt_lo;
-    r.ahi = alt_hi;
-    r.tlo = std::max(start, now_us);  // operations.go:398-402
-    r.thi = end;
-    std::unique_lock<std::mutex> lk(b->mu);
-    b->queue.push_back(&r);
-    b->cv.notify_all();
-    b->done_cv.wait(lk, [&] { return r.done; });
-    lk.unlock();
-    *status = r.status;
-    if (area_km2) *area_km2 = r.area;
-    if (r.rc != DSSG_OK) return r.rc;
+    if (cached) {
+        // the covering succeeded the first time (a capacity answer implies status OK)
+        *status = DSSG_ST_OK;
+        if (area_km2) *area_km2 = r.area;
+    } else {
+        r.kind = kind;
+        r.nv = nv;
+        r.lat = lat;
+        r.lng = lng;
+        r.radius = radius_m;
+        r.alo = alt_lo;
+        r.ahi = alt_hi;
+        r.tlo = std::max(start, now_us);  // operations.go:398-402
+        r.thi = end;
+        std::unique_lock<std::mutex> lk(b->mu);
+        b->queue.push_back(&r);
+        b->cv.notify_one();
+        b->done_cv.wait(lk, [&] { return r.done; });
+        lk.unlock();
+        *status = r.status;
+        if (area_km2) *area_km2 = r.area;
+        if (r.rc != DSSG_OK) return r.rc;
+        std::sort(r.ids.begin(), r.ids.end());
+    }
     *needed = (int64_t)r.ids.size();
-    if ((int64_t)r.ids.size() > cap) return DSSG_ERR_CAPACITY;
+    if ((int64_t)r.ids.size() > cap) {
+        std::lock_guard<std::mutex> lk(b->cache_mu);
+        b->cache.emplace_back(key, std::make_pair(r.area, std::move(r.ids)));
+        while (b->cache.size() > 1024) b->cache.pop_front();
+        return DSSG_ERR_CAPACITY;
+    }
     if (!r.ids.empty()) {
         if (!out_e) return DSSG_ERR_INVALID;
         std::memcpy(out_e, r.ids.data(), sizeof(uint32_t) * r.ids.size());

@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include "common.hpp"
+#include "compact.cuh"
 #include "cover.hpp"
 #include "loopdev.cuh"
 
@@ -1228,26 +1229,497 @@ __global__ void k_u64_to_i64(int64_t n, const unsigned long long *a, int64_t *b)
     if (k < n) b[k] = (int64_t)a[k];
 }
 
+// ===========================================================================
+// Wave path: one wavefront per footprint (north_star "one wavefront per
+// footprint, LDS-staged polygon vertices").  The per-thread pipeline above
+// spreads a footprint over ~15 launches and re-reads its vertices from L2 per
+// candidate; here one wave does the whole covering of a footprint the triage
+// decides, with the loop staged in LDS:
+//   lanes = vertices   S2 points (Go Cephes trig), RegularLoop vertices,
+//                      (u,v) images on the face of vertex 0, the inner test;
+//   lanes = triangles  k_orient's determinants, then Loop.Area's fan terms
+//                      (fastp::signed_area) -- summed in surfaceIntegral order
+//                      by every lane from LDS (bit-identical area);
+//   lanes = edges      loop.go initOriginAndBound's crossing count
+//                      (EdgeCrosser chain, each edge from its own restart);
+//   lanes = candidates the level-13 descendants of the <= 4 start cells, each
+//                      tested against every (u,v) edge in LDS (broadcast reads).
+// Every decision is the one setup_one<true> / k_cand_test_c would make; what
+// they would send to the exact path (triage fails, undecided orientation,
+// polylines, multi-face / big / near-origin loops, > kWaveV vertices) is
+// flagged `slow` and covered by run_general as one compacted sub-batch.
+constexpr int kWaveV = 128;   // vertex cap of the wave path (LDS: 48 B per vertex)
+constexpr int kWaveFp = 4;    // footprints (waves) per block
+struct WaveRec {              // a wave-path footprint's kept candidates
+    uint64_t st_id[4];        // start cells (sorted), level L
+    unsigned long long mask[4];  // kept bits over the <= 256 candidates, in id order
+    uint32_t info;            // L | k << 5
+    uint32_t pad;
+};
+
+__device__ __forceinline__ double wave_min_d(double x)
+{
+    for (int o = 32; o > 0; o >>= 1) x = fmin(x, __shfl_xor(x, o));
+    return x;
+}
+__device__ __forceinline__ double wave_max_d(double x)
+{
+    for (int o = 32; o > 0; o >>= 1) x = fmax(x, __shfl_xor(x, o));
+    return x;
+}
+
+__global__ __launch_bounds__(64 * kWaveFp) void k_cover_wave(int64_t n, const int32_t *kind, const int64_t *voff,
+                                                            const double *lat, const double *lng,
+                                                            const float *radius_m, int32_t *status, double *area_out,
+                                                            int64_t *cnt, WaveRec *rec, uint8_t *slow)
+{
+    __shared__ V3 s_p[kWaveFp][kWaveV];
+    __shared__ double2 s_uv[kWaveFp][kWaveV];
+    __shared__ double s_t[kWaveFp][kWaveV];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t f = (int64_t)blockIdx.x * kWaveFp + w;
+    if (f >= n) return;  // wave-uniform
+    V3 *p = s_p[w];
+    double2 *uvp = s_uv[w];
+    double *tt = s_t[w];
+    const int k = kind[f];
+    const int64_t v0 = voff[f];
+    int st = DSSG_ST_OK, nv = 0;
+    bool go_slow = false;
+    double area = 0;
+    auto finish = [&](int64_t c) {
+        if (lane == 0) {
+            status[f] = st;
+            area_out[f] = area;
+            cnt[f] = go_slow ? 0 : c;
+            slow[f] = go_slow ? 1 : 0;
+        }
+    };
+    // ---- inputs: range / count / radius checks (pkg/models/geo.go:224-268, Q17), S2 points
+    if (k == DSSG_KIND_CIRCLE) {
+        const double la = lat[v0], ln = lng[v0];
+        const float r = radius_m[f];
+        if (la > 90.0 || la < -90.0 || ln > 180.0 || ln < -180.0) st = DSSG_ST_BAD_COORD_SET;
+        else if (!(r > 0)) st = DSSG_ST_RADIUS;
+        else {
+            nv = 20;
+            const double radius = (double)r / DSS_RADIUS_EARTH_M;
+            if (!(radius < 0.5)) {
+                go_slow = true;  // not a small loop
+            } else if (lane < 20) {  // k_circle_frames + k_verts, per lane
+                const V3 c = point_from_degrees(la, ln);
+                const V3 c1 = ortho(c), c0 = cross(c1, c);
+                const double z = go_cos(radius), rr = go_sin(radius);
+                const double px = rr * c_circle_cos[lane], py = rr * c_circle_sin[lane], pz = z;
+                p[lane] = normalize(v3(c0.x * px + c1.x * py + c.x * pz, c0.y * px + c1.y * py + c.y * pz,
+                                       c0.z * px + c1.z * py + c.z * pz));
+            }
+        }
+    } else {
+        nv = (int)(voff[f + 1] - v0);
+        if (k == DSSG_KIND_POLYGON) {
+            bool bad = false;
+            for (int i = lane; i < nv; i += 64) {
+                const double la = lat[v0 + i], ln = lng[v0 + i];
+                bad |= la > 90.0 || la < -90.0 || ln > 180.0 || ln < -180.0;
+            }
+            if (__ballot(bad)) st = DSSG_ST_BAD_COORD_SET;
+        }
+        if (st == DSSG_ST_OK && nv < 3) st = DSSG_ST_NOT_ENOUGH_POINTS;
+        if (st == DSSG_ST_OK) {
+            if (nv > kWaveV) go_slow = true;
+            else
+                for (int i = lane; i < nv; i += 64) p[i] = point_from_degrees(lat[v0 + i], lng[v0 + i]);
+        }
+    }
+    if (st != DSSG_ST_OK || go_slow) {
+        finish(0);
+        return;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- (u,v) on the face of vertex 0; every edge inside that face (k_fan)
+    const int face0 = xyz_face(p[0]);
+    bool outer = false;
+    for (int i = lane; i < nv; i += 64) {
+        double u, v;
+        valid_face_xyz_to_uv(face0, p[i], u, v);
+        uvp[i] = make_double2(u, v);
+        outer |= !edge_inside_face(p[i], p[i + 1 == nv ? 0 : i + 1], face0);
+    }
+    if (__ballot(outer)) {
+        go_slow = true;
+        finish(0);
+        return;
+    }
+    bool fail = false;
+    if (k != DSSG_KIND_CIRCLE) {
+        // ---- k_orient: fan determinants per lane, summed in order by every lane
+        const V3 a = p[0];
+        bool far = false;
+        for (int i = 1 + lane; i < nv; i += 64) {
+            const V3 c = p[i];
+            far |= !(a.x * c.x + a.y * c.y + a.z * c.z >= 0.99875);  // cos(0.05)
+            if (i + 1 < nv) {
+                const V3 b = c, cc = p[i + 1];
+                tt[i] = a.x * (b.y * cc.z - b.z * cc.y) + a.y * (b.z * cc.x - b.x * cc.z) + a.z * (b.x * cc.y - b.y * cc.x);
+            }
+        }
+        const bool near = __ballot(far) == 0ull;
+        __builtin_amdgcn_wave_barrier();
+        double d = 0, dabs = 0;
+        for (int i = 1; i + 1 < nv; i++) {
+            const double t = tt[i];
+            d += t;
+            dabs += __builtin_fabs(t);
+        }
+        d *= 0.5;
+        dabs *= 0.5;
+        const double margin = 0.05 * dabs + 1e-13;
+        int om = 2;
+        if (near && d > margin && ((d * 1.1) * DSS_EARTH_AREA_KM2) / 4.0 * DSS_PI < DSS_MAX_AREA_KM2) om = 0;
+        else if (near && d < -margin) om = 1;
+        if (om == 2) {  // both orientations' terms would be needed: the general path
+            go_slow = true;
+            finish(0);
+            return;
+        }
+        __builtin_amdgcn_wave_barrier();
+        // ---- k_fan_area: the needed orientation's terms, one lane per triangle
+        bool fl = false;
+        for (int j = lane; j < nv - 2; j += 64) {
+            const int i = 1 + j;
+            const V3 ta = om == 1 ? p[nv - 1] : p[0], tb = om == 1 ? p[nv - 1 - i] : p[i],
+                     tc = om == 1 ? p[nv - 2 - i] : p[i + 1];
+            bool f1 = angle(tc, ta) > DSS_SURFACE_MAX_LENGTH;
+            const double v = fastp::signed_area(ta, tb, tc, f1);
+            tt[i] = v;
+            fl |= f1;
+        }
+        fail = __ballot(fl) != 0ull;
+        __builtin_amdgcn_wave_barrier();
+        if (om == 0) {
+            area = fan_area_km2(tt, nv, fail);
+            if (area > DSS_MAX_AREA_KM2) fail = true;  // mispredicted: no reversed terms
+        } else {
+            area = INFINITY;  // the forward sum is negative: ~4 pi, above the cap
+        }
+        if (fail) {
+            go_slow = true;
+            finish(0);
+            return;
+        }
+        if (area > DSS_MAX_AREA_KM2) {  // Q4: reverse in place (points and their (u,v) images)
+            for (int i = lane; i < nv / 2; i += 64) {
+                const int j = nv - 1 - i;
+                const V3 x = p[i];
+                p[i] = p[j];
+                p[j] = x;
+                const double2 y = uvp[i];
+                uvp[i] = uvp[j];
+                uvp[j] = y;
+            }
+            __builtin_amdgcn_wave_barrier();
+            area = fan_area_km2(tt, nv, fail, true);
+            if (fail) {
+                go_slow = true;
+                finish(0);
+                return;
+            }
+        }
+        if (area > DSS_MAX_AREA_KM2) {
+            st = DSSG_ST_AREA_TOO_LARGE;
+            finish(0);
+            return;
+        }
+        if (area <= 0) {  // Q3: open polyline (general path)
+            go_slow = true;
+            finish(0);
+            return;
+        }
+    }
+    // ---- loop.go initOriginAndBound on the final loop: v1's wedge vs the
+    // crossings of OriginPoint -> v1 with every edge (one lane per edge)
+    const V3 P0 = p[0], P1 = p[1], P2 = p[2];
+    const bool v1_inside = !eq(P0, P1) && !eq(P2, P1) && fastp::angle_contains_vertex(P0, P1, P2, fail);
+    EdgeCrosser ex;
+    ex.init(origin_point(), P1);
+    bool par = false, fl = false;
+    for (int i = 1 + lane; i <= nv; i += 64) {
+        EdgeCrosser y = ex;
+        y.c = p[i - 1];
+        y.acb = -triage_sign(y.a, y.b, y.c);  // restart_at(v[i-1])
+        par ^= fastp::edge_or_vertex_chain_crossing(y, p[i == nv ? 0 : i], fl);
+    }
+    fail |= __ballot(fl) != 0ull;
+    const bool contains_v1 = (__popcll(__ballot(par)) & 1) != 0;
+    const bool origin_in = v1_inside != contains_v1;
+    if (fail) {
+        go_slow = true;
+        finish(0);
+        return;
+    }
+    // ---- (u,v) bound, planar test, start cells (setup_one's FL_FAST block)
+    double ulo = 1e300, uhi = -1e300, vlo = 1e300, vhi = -1e300;
+    for (int i = lane; i < nv; i += 64) {
+        const double2 q = uvp[i];
+        ulo = fmin(ulo, q.x);
+        uhi = fmax(uhi, q.x);
+        vlo = fmin(vlo, q.y);
+        vhi = fmax(vhi, q.y);
+    }
+    ulo = wave_min_d(ulo);
+    uhi = wave_max_d(uhi);
+    vlo = wave_min_d(vlo);
+    vhi = wave_max_d(vhi);
+    bool near_origin = false;
+    if (face0 == xyz_face(origin_point())) {
+        double ou, ov;
+        valid_face_xyz_to_uv(face0, origin_point(), ou, ov);
+        near_origin = ou >= ulo - 1e-6 && ou <= uhi + 1e-6 && ov >= vlo - 1e-6 && ov <= vhi + 1e-6;
+    }
+    const double m = 1e-7;
+    const FaceBox b{ulo - m, uhi + m, vlo - m, vhi + m};
+    uint64_t sid[4];
+    uint32_t si[4], sj[4], smt[4];
+    const int kc = start_cells(b, face0, sid, si, sj, smt);
+    const int L = kc > 0 ? meta_level(smt[0]) : 0;
+    if (near_origin || kc == 0 || L < kFastMinLevel) {
+        go_slow = true;
+        finish(0);
+        return;
+    }
+    const int sh13 = kMaxLevel - kCoverLevel;
+    const uint32_t bx0 = (uint32_t)(st_to_ij(uv_to_st(fmax(b.ulo, -1.0))) >> sh13),
+                   bx1 = (uint32_t)(st_to_ij(uv_to_st(fmin(b.uhi, 1.0))) >> sh13),
+                   by0 = (uint32_t)(st_to_ij(uv_to_st(fmax(b.vlo, -1.0))) >> sh13),
+                   by1 = (uint32_t)(st_to_ij(uv_to_st(fmin(b.vhi, 1.0))) >> sh13);
+    // ---- candidates, one per lane: bound, then the padded edge test and the
+    // planar centre ray cast over the LDS edges (cand_edges)
+    const int sh = 2 * (kCoverLevel - L);
+    const int nc = kc << sh;
+    unsigned long long km[4] = {0, 0, 0, 0};
+    const uint32_t size = 1u << (kMaxLevel - kCoverLevel);
+    const double pm = kFinePad;
+    const double half = 0.5 / (double)kMaxSize, sz = (double)size;
+    for (int c0 = 0; c0 < nc; c0 += 64) {
+        const int c = c0 + lane;
+        bool keep = false;
+        if (c < nc) {
+            const int s = c >> sh;
+            const uint32_t r = (uint32_t)(c & ((1 << sh) - 1));
+            int o = meta_orient(smt[s]);
+            uint32_t i = si[s], j = sj[s];
+            for (int l = L + 1; l <= kCoverLevel; l++) {
+                const int digit = (int)((r >> (2 * (kCoverLevel - l))) & 3u);
+                const int ij = pos_to_ij(o, digit);
+                const uint32_t hf = 1u << (kMaxLevel - l);
+                if (ij >> 1) i += hf;
+                if (ij & 1) j += hf;
+                o ^= pos_to_orientation(digit);
+            }
+            const uint32_t i13 = i >> sh13, j13 = j >> sh13;
+            if (!(i13 < bx0 || i13 > bx1 || j13 < by0 || j13 > by1)) {
+                const double culo = st_to_uv((double)i / (double)kMaxSize),
+                             cuhi = st_to_uv((double)(i + size) / (double)kMaxSize);
+                const double cvlo = st_to_uv((double)j / (double)kMaxSize),
+                             cvhi = st_to_uv((double)(j + size) / (double)kMaxSize);
+                const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
+                bool in = false, pr = false;
+                double2 a = uvp[0];
+                for (int e = 0; e < nv; e++) {
+                    const double2 q = uvp[e + 1 < nv ? e + 1 : 0];
+                    if (edge_intersects_rect(a.x, a.y, q.x, q.y, culo - pm, cuhi + pm, cvlo - pm, cvhi + pm)) {
+                        in = true;
+                        break;
+                    }
+                    if ((a.y > vc) != (q.y > vc)) {
+                        const double dd = q.y - a.y;
+                        const double lhs = (uc - a.x) * dd, rhs = (vc - a.y) * (q.x - a.x);
+                        if (dd > 0 ? lhs < rhs : lhs > rhs) pr = !pr;
+                    }
+                    a = q;
+                }
+                keep = in || (origin_in != pr);
+            }
+        }
+        const unsigned long long bm = __ballot(keep);
+        km[0] = (c0 >> 6) == 0 ? bm : km[0];
+        km[1] = (c0 >> 6) == 1 ? bm : km[1];
+        km[2] = (c0 >> 6) == 2 ? bm : km[2];
+        km[3] = (c0 >> 6) == 3 ? bm : km[3];
+    }
+    const int64_t total = __popcll(km[0]) + __popcll(km[1]) + __popcll(km[2]) + __popcll(km[3]);
+    if (lane < 4) {
+        WaveRec &R = rec[f];
+        R.st_id[lane] = lane < kc ? sid[lane] : 0;
+        R.mask[lane] = lane == 0 ? km[0] : lane == 1 ? km[1] : lane == 2 ? km[2] : km[3];
+        if (lane == 0) {
+            R.info = (uint32_t)L | ((uint32_t)kc << 5);
+            R.pad = 0;
+        }
+    }
+    finish(total);
+}
+
+// Wave-path footprints' cells at their CSR offsets (one thread per footprint,
+// kept candidates in id order).
+__global__ void k_emit_wave(int64_t n, const uint8_t *slow, const WaveRec *rec, const int64_t *offs, uint64_t *cells)
+{
+    const int64_t f = tid64();
+    if (f >= n || slow[f]) return;
+    int64_t w = offs[f];
+    if (offs[f + 1] == w) return;
+    const WaveRec R = rec[f];
+    const int L = (int)(R.info & 31u);
+    const int sh = 2 * (kCoverLevel - L);
+    const uint64_t lsbL = lsb_for_level(L), lsb13 = lsb_for_level(kCoverLevel);
+    for (int q = 0; q < 4; q++) {
+        unsigned long long mk = R.mask[q];
+        while (mk) {
+            const int c = 64 * q + __builtin_ctzll(mk);
+            mk &= mk - 1;
+            const int s = c >> sh;
+            const uint64_t r = (uint64_t)(c & ((1 << sh) - 1));
+            cells[w++] = R.st_id[s] - lsbL + lsb13 + r * (lsb13 << 1);  // cellid.go ChildBeginAtLevel + r steps
+        }
+    }
+}
+
+// The slow footprints as their own batch (kind, radius, vertex counts) ...
+__global__ void k_slow_gather(int64_t ns, const uint32_t *list, const int32_t *kind, const int64_t *voff,
+                              const float *radius_m, int32_t *skind, float *srad, int64_t *snv)
+{
+    const int64_t k = tid64();
+    if (k >= ns) return;
+    const uint32_t f = list[k];
+    skind[k] = kind[f];
+    srad[k] = radius_m[f];
+    snv[k] = voff[f + 1] - voff[f];
+}
+// ... and their vertices (one wave per slow footprint).
+__global__ void k_slow_verts(int64_t ns, const uint32_t *list, const int64_t *voff, const double *lat, const double *lng,
+                             const int64_t *svoff, double *slat, double *slng)
+{
+    const int64_t k = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (k >= ns) return;
+    const uint32_t f = list[k];
+    const int64_t a = voff[f], nv = voff[f + 1] - a, b = svoff[k];
+    for (int64_t i = threadIdx.x & 63; i < nv; i += 64) {
+        slat[b + i] = lat[a + i];
+        slng[b + i] = lng[a + i];
+    }
+}
+// The general pipeline's answers back to their footprints.
+__global__ void k_slow_scatter(int64_t ns, const uint32_t *list, const int32_t *sstat, const double *sarea,
+                               const int64_t *soffs, int32_t *status, double *area, int64_t *cnt)
+{
+    const int64_t k = tid64();
+    if (k >= ns) return;
+    const uint32_t f = list[k];
+    status[f] = sstat[k];
+    area[f] = sarea[k];
+    cnt[f] = soffs[k + 1] - soffs[k];
+}
+// The slow footprints' cells into the merged CSR (one wave per footprint).
+__global__ void k_slow_cells(int64_t ns, const uint32_t *list, const int64_t *soffs, const uint64_t *scells,
+                             const int64_t *offs, uint64_t *cells)
+{
+    const int64_t k = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (k >= ns) return;
+    const int64_t a = soffs[k], c = soffs[k + 1] - a, b = offs[list[k]];
+    for (int64_t i = threadIdx.x & 63; i < c; i += 64) cells[b + i] = scells[a + i];
+}
+
+struct PredSlow {
+    const uint8_t *slow;
+    __device__ bool operator()(int64_t i) const { return slow[i] != 0; }
+};
+struct EmitSlow {
+    uint32_t *list;
+    __device__ void operator()(int64_t i, int64_t r) const { list[r] = (uint32_t)i; }
+};
+
 }  // namespace
 
 // ---------------------------------------------------------------- host side
 void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
                       const float *radius_m, hipStream_t s, dssg_cells *out)
 {
+    if (!wave_ || n == 0) {
+        last_slow_ = n;
+        run_general(n, kind, voff, lat, lng, radius_m, s, out);
+        return;
+    }
+    init_tables(s);
+    int32_t *status = w_status_.ensure(n + 1);
+    double *area = w_area_.ensure(n + 1);
+    int64_t *cnt = w_cnt_.ensure(n + 1), *offs = w_offs_.ensure(n + 1), *dtot = w_tot_.ensure(2);
+    WaveRec *rec = (WaveRec *)w_rec_.ensure(sizeof(WaveRec) * (size_t)(n + 1));
+    uint8_t *slow = w_slow_.ensure(n + 1);
+    hipLaunchKernelGGL(k_cover_wave, dim3(grid_for(n, kWaveFp)), dim3(64 * kWaveFp), 0, s, n, kind, voff, lat, lng,
+                       radius_m, status, area, cnt, rec, slow);
+    // the footprints the wave path left: one sub-batch through the general pipeline
+    uint32_t *list = s_list_.ensure(n + 1);
+    int64_t ns = 0;
+    compact_if(n, PredSlow{slow}, EmitSlow{list}, tmp_, tmp2_, s, dtot, &ns);
+    last_slow_ = ns;
+    dssg_cells sub{};
+    if (ns > 0) {
+        int32_t *skind = s_kind_.ensure(ns + 1);
+        float *srad = s_rad_.ensure(ns + 1);
+        int64_t *snv = s_nv_.ensure(ns + 1), *svoff = s_voff_.ensure(ns + 1);
+        hipLaunchKernelGGL(k_slow_gather, dim3(grid_for(ns, kBlock)), dim3(kBlock), 0, s, ns, list, kind, voff, radius_m,
+                           skind, srad, snv);
+        exclusive_scan_i64(snv, svoff, ns, tmp_, s);
+        int64_t snx = 0;
+        DSS_HIP(hipMemcpyAsync(&snx, svoff + ns, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipStreamSynchronize(s));
+        double *slat = s_lat_.ensure(snx + 1), *slng = s_lng_.ensure(snx + 1);
+        hipLaunchKernelGGL(k_slow_verts, dim3(grid_for(ns, kBlock / 64)), dim3(kBlock), 0, s, ns, list, voff, lat, lng,
+                           svoff, slat, slng);
+        run_general(ns, skind, svoff, slat, slng, srad, s, &sub);
+        hipLaunchKernelGGL(k_slow_scatter, dim3(grid_for(ns, kBlock)), dim3(kBlock), 0, s, ns, list, sub.status,
+                           sub.area_km2, sub.offs, status, area, cnt);
+    }
+    exclusive_scan_i64(cnt, offs, n, tmp_, s);
+    int64_t total = 0;
+    DSS_HIP(hipMemcpyAsync(&total, offs + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    uint64_t *cells = w_cells_.ensure(total + 1);
+    hipLaunchKernelGGL(k_emit_wave, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, slow, rec, offs, cells);
+    if (ns > 0)
+        hipLaunchKernelGGL(k_slow_cells, dim3(grid_for(ns, kBlock / 64)), dim3(kBlock), 0, s, ns, list, sub.offs,
+                           sub.cells, offs, cells);
+    out->n = n;
+    out->offs = offs;
+    out->cells = cells;
+    out->status = status;
+    out->area_km2 = area;
+    out->total_cells = total;
+}
+
+void CoverEngine::init_tables(hipStream_t s)
+{
+    if (tables_) return;
+    // RegularLoop angles, bit-identical host evaluation of the Go math
+    double cs[20], sn[20];
+    const double step = 2 * DSS_PI / 20.0;
+    for (int i = 0; i < 20; i++) {
+        const double ang = (double)i * step;
+        cs[i] = go_cos(ang);
+        sn[i] = go_sin(ang);
+    }
+    DSS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_circle_cos), cs, sizeof(cs), 0, hipMemcpyHostToDevice, s));
+    DSS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_circle_sin), sn, sizeof(sn), 0, hipMemcpyHostToDevice, s));
+    tables_ = true;
+}
+
+void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat,
+                              const double *lng, const float *radius_m, hipStream_t s, dssg_cells *out)
+{
     const unsigned B = kBlock;
     out->n = n;
-    if (!tables_) {  // RegularLoop angles, bit-identical host evaluation of the Go math
-        double cs[20], sn[20];
-        const double step = 2 * DSS_PI / 20.0;
-        for (int i = 0; i < 20; i++) {
-            const double ang = (double)i * step;
-            cs[i] = go_cos(ang);
-            sn[i] = go_sin(ang);
-        }
-        DSS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_circle_cos), cs, sizeof(cs), 0, hipMemcpyHostToDevice, s));
-        DSS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_circle_sin), sn, sizeof(sn), 0, hipMemcpyHostToDevice, s));
-        tables_ = true;
-    }
+    init_tables(s);
     int64_t *nv = cnt_.ensure(n + 1);
     int64_t *xoff = xoff_.ensure(n + 1);
     int32_t *status = status_.ensure(n + 1);

@@ -21,10 +21,30 @@ struct Frontier {
 class CoverEngine {
    public:
     // Device pointers in, context-owned device buffers out (see dssg_cells).
+    // The wave path (one wavefront per footprint) covers every footprint it
+    // can decide; the rest go through the general pipeline (run_general) as
+    // one compacted sub-batch.
     void run(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
              const float *radius_m, hipStream_t s, dssg_cells *out);
+    // 0: every footprint through the general pipeline (A/B and tests)
+    void set_wave_path(bool on) { wave_ = on; }
+    int64_t last_slow() const { return last_slow_; }
 
    private:
+    void run_general(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
+                     const float *radius_m, hipStream_t s, dssg_cells *out);
+    void init_tables(hipStream_t s);
+    bool wave_ = true;
+    int64_t last_slow_ = 0;
+    // wave path: per-footprint outputs, the slow sub-batch, the merged CSR
+    DevBuf<int32_t> w_status_, s_kind_;
+    DevBuf<double> w_area_, s_lat_, s_lng_;
+    DevBuf<int64_t> w_cnt_, w_offs_, s_nv_, s_voff_, w_tot_;
+    DevBuf<unsigned char> w_rec_;
+    DevBuf<uint8_t> w_slow_;
+    DevBuf<uint32_t> s_list_;
+    DevBuf<float> s_rad_;
+    DevBuf<uint64_t> w_cells_;
     DevBuf<int64_t> cnt_, xoff_, eoff_, soff_, offs_, ncnt_, npos_, fc64_;
     DevBuf<int32_t> status_, nvx_;
     DevBuf<double> area_, xyz_;

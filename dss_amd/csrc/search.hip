@@ -988,6 +988,11 @@ struct OutArgs {
 };
 
 __device__ __forceinline__ int uni32(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ unsigned long long uni64_lane0(unsigned long long x)
+{
+    return ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 0) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 0);
+}
 __device__ __forceinline__ unsigned long long uni64(unsigned long long x)
 {
     return ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32) |
@@ -1704,6 +1709,71 @@ __global__ __launch_bounds__(kBlock) void k_stats(IndexView a, QueryView qv, uns
     }
 }
 
+// Small batches (the per-RPC path, pkg/scd/operations_handler.go:118-168:
+// one covering and one search per request): one wave per query cell, lanes
+// over the cell's postings in the band [tlo - dcap, thi] plus its long
+// postings, the fused altitude/time/owner filter, and the smallest-shared-cell
+// rule (SQL DISTINCT, Q13) decided exactly by a merge of the two sorted cell
+// lists below the cell -- no query ordering, units or dedupe pass: one
+// launch, its pairs through one wave-aggregated atomic per 64 postings.
+constexpr int kSmallBlock = 256;
+__global__ __launch_bounds__(kSmallBlock) void k_small_join(IndexView ix, QueryView qv, int64_t nqc, int64_t cap,
+                                                             uint32_t *__restrict__ oq, uint32_t *__restrict__ oe,
+                                                             unsigned long long *__restrict__ count)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t k = (int64_t)blockIdx.x * (kSmallBlock / 64) + (threadIdx.x >> 6);
+    if (k >= nqc) return;  // wave-uniform
+    int64_t lo = 0, hi = qv.nq;  // the cell's query: offs[lo] <= k < offs[hi]
+    while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (qv.offs[mid] <= k) lo = mid;
+        else hi = mid;
+    }
+    const uint32_t q = (uint32_t)lo;
+    const int64_t c0 = qv.offs[q];
+    const uint64_t c = qv.cells[k];
+    uint32_t slot;
+    if (!find_slot(ix, c, slot)) return;
+    const uint64_t s0 = ix.s_post[slot], s1 = ix.s_post[slot + 1], sr = s0 + ix.s_nreg[slot];
+    const long long tlo = qv.tlo[q], thi = qv.thi[q];
+    const float alo = qv.alo[q], ahi = qv.ahi[q];
+    const int32_t own = qv.owner ? qv.owner[q] : -1;
+    // a regular posting (|t1 - t0| <= dcap) meets [tlo, thi] only if its start m is in [tlo - dcap, thi]
+    const long long mlo = tlo < LLONG_MIN + ix.dcap ? LLONG_MIN : tlo - ix.dcap;
+    const uint64_t r0 = lb_m(ix.b_t, s0, sr, mlo), r1 = ub_m(ix.b_t, r0, sr, thi);
+    const uint64_t nreg = r1 - r0, ntot = nreg + (s1 - sr);
+    for (uint64_t b = 0; b < ntot; b += 64) {
+        const uint64_t t = b + (uint64_t)lane;
+        bool keep = false;
+        uint32_t ent = 0;
+        if (t < ntot) {
+            const uint64_t p = t < nreg ? r0 + t : sr + (t - nreg);
+            const longlong2 pt = ix.b_t[p];
+            const float2 pa = ix.b_alt[p];
+            const uint32_t pe = ix.b_e[p];
+            ent = pe & ~kFirstBit;
+            // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels)
+            bool pass = (pt.y >= tlo) & (pt.x <= thi) & (pa.y >= alo) & (pa.x <= ahi);
+            if (own >= 0) pass &= ix.b_owner[p] == own;
+            if (pass && !is_dead(ix, ent))
+                keep = k == c0 || (pe & kFirstBit) || no_smaller_shared<2>(ix, ent, c, qv.cells + c0, k - c0);
+        }
+        const unsigned long long m = __ballot(keep);
+        if (!m) continue;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(count, (unsigned long long)__popcll(m));
+        base = uni64_lane0(base);
+        if (keep) {
+            const unsigned long long pos = base + mbcnt64(m);
+            if ((int64_t)pos < cap) {  // else counted only: the host regrows and reruns
+                oq[pos] = q;
+                oe[pos] = ent;
+            }
+        }
+    }
+}
+
 // Postings of the distinct cells a batch touches: mark, then sum.
 __global__ void k_touch_mark(IndexView a, int64_t nqc, const uint64_t *cells, uint8_t *mark)
 {
@@ -1738,6 +1808,44 @@ T fetch(const T *p, hipStream_t s)
 }
 
 }  // namespace
+
+// ============================================================ small batches
+void SearchEngine::search_small(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
+                                const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo,
+                                const int64_t *q_thi, const int32_t *q_owner, int64_t nqc, hipStream_t s,
+                                dssg_pairs *out)
+{
+    const IndexView ix = view_of(idx);
+    const QueryView qv{nq, q_offs, q_cells, q_alt_lo, q_alt_hi, q_tlo, q_thi, q_owner};
+    unsigned long long *count = small_cnt_.ensure(1);
+    if (small_cap_ == 0) small_cap_ = std::max<int64_t>(1 << 16, 64 * qv.nq);
+    for (int attempt = 0; attempt < 4; attempt++) {
+        uint32_t *oq = oq_.ensure(small_cap_ + 1), *oe = oe_.ensure(small_cap_ + 1);
+        DSS_HIP(hipMemsetAsync(count, 0, sizeof(unsigned long long), s));
+        if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
+        hipLaunchKernelGGL(k_small_join, dim3(grid_for(nqc, kSmallBlock / 64)), dim3(kSmallBlock), 0, s, ix, qv, nqc,
+                           small_cap_, oq, oe, count);
+        if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
+        const int64_t n = (int64_t)fetch(count, s);
+        if (n > small_cap_) {  // counted, not all written: regrow and rerun
+            small_cap_ = n + n / 4 + 1024;
+            continue;
+        }
+        if (timing_) {
+            float ms = 0;
+            DSS_HIP(hipEventElapsedTime(&ms, ev0_, ev1_));
+            join_ms_ = ms;
+        }
+        out->q = oq;
+        out->e = oe;
+        out->n = n;
+        out->n_tagged = 0;
+        units_ = keys_ = runs_ = iters_ = tests_ = tagged_ = long_queries_ = 0;
+        long_postings_ = idx->n_long_fp;
+        return;
+    }
+    throw Error(DSSG_ERR_DEVICE, "search: output size did not converge");
+}
 
 // ================================================================== build
 void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, const uint64_t *cells,
@@ -1998,6 +2106,8 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     const int64_t nqc = fetch(q_offs + nq, s);
     if (nqc >= (int64_t)0xffffffffll) throw Error(DSSG_ERR_CAPACITY, "search: more than 2^32 - 1 query cells per batch");
     if (nqc == 0) return empty();
+    if (nq <= small_max_q_ && nqc <= 16 * small_max_q_)
+        return search_small(idx, nq, q_offs, q_cells, q_alt_lo, q_alt_hi, q_tlo, q_thi, q_owner, nqc, s, out);
     // one control block (a single memset to start, one copy back per join):
     // dqmax slots, unit region counters, misc counters ([0] pairs [1] tagged
     // [2] lane tests [3] broadcasts [5] long queries [9] scratch), unit queue

@@ -113,7 +113,16 @@ class SearchEngine {
         *tests = tests_;
     }
 
+    // batches of at most this many queries (and 16x as many cells) take the
+    // one-launch small path (k_small_join); 0: never
+    void set_small_max_q(int64_t v) { small_max_q_ = v; }
+
    private:
+    void search_small(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
+                      const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
+                      const int32_t *q_owner, int64_t nqc, hipStream_t s, dssg_pairs *out);
+    int64_t small_max_q_ = 4096, small_cap_ = 0;
+    DevBuf<unsigned long long> small_cnt_;
     DevBuf<unsigned char> tmp_, tmp2_;
     // query side
     DevBuf<uint32_t> cq_, dec_, okey_, okey2_, oval_, perm_, kkey_, kkey2_, kval_, kval2_, rbeg_, bt_;

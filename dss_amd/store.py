@@ -529,7 +529,7 @@ class Batcher:
         """-> (status, entity ids); status DSSG_ST_* of the covering."""
         lat = np.ascontiguousarray(lat, dtype=np.float64)
         lng = np.ascontiguousarray(lng, dtype=np.float64)
-        cap = 256
+        cap = 4096
         while True:
             out = np.empty(cap, dtype=np.uint32)
             needed, st, area = C.c_int64(), C.c_int32(), C.c_double()

@@ -29,3 +29,17 @@ def golden_covering():
 def golden_search():
     import numpy as np
     return dict(np.load(os.path.join(ROOT, "tests", "golden", "search.npz"), allow_pickle=False))
+
+
+@pytest.fixture(params=["units", "small"])
+def join_path(request):
+    """Run a search test through both joins of the shared context: "units"
+    (the tiled band join, k_join; small_search = 0) and "small" (the
+    one-launch small-batch join, k_small_join, forced for every batch)."""
+    from dss_amd import _lib
+    ctx = _lib.context(0)
+    ctx.set_tuning("small_search", 0 if request.param == "units" else 1 << 24)
+    try:
+        yield request.param
+    finally:
+        ctx.set_tuning("small_search", 4096)

@@ -29,7 +29,7 @@ def isa_index(start, end):
     ("search with non-matching time span", CELLS, lambda s, e: (e + 100 * 1_000_000, e + 200 * 1_000_000), 0),
     ("search with expanded time span", CELLS, lambda s, e: (s - 100 * 1_000_000, e + 100 * 1_000_000), 1),
 ])
-def test_store_search_isas(name, cells, mut, expected):
+def test_store_search_isas(name, cells, mut, expected, join_path):
     # identification_service_area_test.go:33-136 (start = now-1min, end = now+1h)
     from dss_amd.store import SearchISAs
     now = 1_600_000_000_000_000
@@ -61,7 +61,7 @@ def test_search_errors():
         SearchSubscriptions(idx, [], 0)
 
 
-def test_subscriptions_by_owner():
+def test_subscriptions_by_owner(join_path):
     # subscriptions_test.go:172-216: 3 owners, subscription i covers cells[:i+1]
     # (the list holds a duplicate and a face-7 "overflow" id, Q12)
     from dss_amd.store import EntityIndex, SearchSubscriptions, SearchSubscriptionsByOwner
@@ -74,7 +74,7 @@ def test_subscriptions_by_owner():
         assert SearchSubscriptionsByOwner(idx, cells, o, now) == [o]
 
 
-def test_expired_subscription():
+def test_expired_subscription(join_path):
     # subscriptions_test.go:218-255: end = now + 24h; found at +23h, gone at +25h
     from dss_amd.store import EntityIndex, SearchSubscriptionsByOwner
     now = 1_600_000_000_000_000
@@ -84,7 +84,7 @@ def test_expired_subscription():
     assert SearchSubscriptionsByOwner(idx, [12494535866699481088], 7, now + 25 * hour) == []
 
 
-def test_golden_operations(golden_search):
+def test_golden_operations(golden_search, join_path):
     from dss_amd.store import EntityIndex
     g = golden_search
     idx = EntityIndex(g["e_offs"], g["e_cells"], g["e_alt_lo"], g["e_alt_hi"], g["e_t0"], g["e_t1"], g["e_owner"])
@@ -95,7 +95,7 @@ def test_golden_operations(golden_search):
     assert np.array_equal(sq, g["subs_q"]) and np.array_equal(se, g["subs_e"])
 
 
-def test_random_end_to_end(oracle):
+def test_random_end_to_end(oracle, join_path):
     """Cover intents and queries on the GPU, build the index, join; compare
     with the oracle's covering + join on the same seeded inputs."""
     from dss_amd import geo, workload as W
@@ -114,7 +114,7 @@ def test_random_end_to_end(oracle):
     assert np.array_equal(rq, oq) and np.array_equal(re, oe)
 
 
-def test_unsorted_duplicate_query_cells(oracle, golden_search):
+def test_unsorted_duplicate_query_cells(oracle, golden_search, join_path):
     """UnionVolumes4D hands the store unsorted cells (Q14); duplicates too."""
     from dss_amd.store import EntityIndex
     g = golden_search
@@ -173,7 +173,7 @@ def test_device_api_matches_host_api(golden_covering):
     (2000, 3000, 1, "short"),      # RID-like 30 s windows, dense in time
     (500, 3000, 24, "long"),       # many long-duration entities (the long part of a cell)
 ])
-def test_hot_cell_band_join(oracle, nq, ne, span_h, dur):
+def test_hot_cell_band_join(oracle, nq, ne, span_h, dur, join_path):
     """Hot cells: every footprint within a few level-13 cells, so one cell's
     records and postings span many 64-wide tiles and batches; the band join's
     record ranges (cooperative 64-ary search over start-sorted records), tile

@@ -45,7 +45,7 @@ def _lists(offs, cells):
     return [cells[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
 
 
-def test_store_random_writes_against_oracle(oracle):
+def test_store_random_writes_against_oracle(oracle, join_path):
     from dss_amd import geo, workload as W
     from dss_amd.store import Store
     rng = np.random.default_rng(3)

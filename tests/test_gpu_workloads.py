@@ -15,7 +15,7 @@ def _keys(q, e):
 
 
 @pytest.mark.parametrize("cfg,scale", [(2, 0.002), (3, 0.004), (4, 0.0004)])
-def test_config_parity(oracle, cfg, scale):
+def test_config_parity(oracle, cfg, scale, join_path):
     from dss_amd import geo, workload as W
     from dss_amd.store import EntityIndex
     _, q, qa, it, ia, now = W.config(cfg, scale=scale)
@@ -54,7 +54,7 @@ def corridors_case(oracle):
 # buckets), 2^40 (two buckets, each over the LDS set: the full-sort fallback
 # for flagged buckets), 0 (the full-sort path)
 @pytest.mark.parametrize("avg", [1024, 1, 1 << 40, 0])
-def test_long_pair_dedupe_paths(corridors_case, avg):
+def test_long_pair_dedupe_paths(corridors_case, avg, join_path):
     from dss_amd import _lib
     from dss_amd.store import EntityIndex
     ci, cq, qa, ia, now, want = corridors_case
