@@ -256,3 +256,25 @@ func (m *Mirror) Len() int {
 	defer m.mu.RUnlock()
 	return len(m.ids)
 }
+
+// Matches reports whether row r satisfies query q on the host: the ABI's
+// predicate (dssgpu.h dssg_search) with the same NULL sentinels -- for the few
+// rows a transaction has written but not committed (read-your-writes).
+func (r Row) Matches(q Query) bool {
+	if !(r.T1 >= q.TLo && r.T0 <= q.THi && r.AltHi >= q.AltLo && r.AltLo <= q.AltHi) {
+		return false
+	}
+	if q.Owner != "" && r.Owner != q.Owner {
+		return false
+	}
+	set := make(map[s2.CellID]struct{}, len(r.Cells))
+	for _, c := range r.Cells {
+		set[c] = struct{}{}
+	}
+	for _, c := range q.Cells {
+		if _, ok := set[c]; ok {
+			return true
+		}
+	}
+	return false
+}

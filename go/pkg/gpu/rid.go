@@ -3,6 +3,7 @@ package gpu
 import (
 	"context"
 	"sync"
+	"sync/atomic"
 	"time"
 
 	"github.com/golang/geo/s2"
@@ -28,6 +29,18 @@ type RIDTransactor struct {
 	mu         sync.RWMutex
 	isaRows    map[dssmodels.ID]*ridmodels.IdentificationServiceArea
 	subRows    map[dssmodels.ID]*ridmodels.Subscription
+	invalid    int32 // atomic: 1 after a failed apply of committed writes (searches then run on CRDB)
+}
+
+// Invalid reports whether the mirrors fell behind CRDB.
+func (t *RIDTransactor) Invalid() bool { return atomic.LoadInt32(&t.invalid) != 0 }
+
+// applyCommitted mirrors writes CRDB has already committed: a failure cannot
+// undo them, so it marks the mirrors invalid instead of failing the call.
+func (t *RIDTransactor) applyCommitted(w *ridWrites) {
+	if err := t.apply(w); err != nil {
+		atomic.StoreInt32(&t.invalid, 1)
+	}
 }
 
 // NewRIDTransactor builds the mirrors from the tables' current rows.
@@ -123,7 +136,8 @@ func (t *RIDTransactor) InTxnRetrier(ctx context.Context, f func(repo repos.Repo
 	if err != nil || w == nil {
 		return err
 	}
-	return t.apply(w)
+	t.applyCommitted(w)
+	return nil
 }
 
 // ---- the transactor's own (autocommit) repository methods ---------------
@@ -133,7 +147,7 @@ func (t *RIDTransactor) InsertISA(ctx context.Context, isa *ridmodels.Identifica
 	if err == nil && res != nil {
 		w := newRIDWrites()
 		w.isas[res.ID] = res
-		err = t.apply(w)
+		t.applyCommitted(w)
 	}
 	return res, err
 }
@@ -143,7 +157,7 @@ func (t *RIDTransactor) UpdateISA(ctx context.Context, isa *ridmodels.Identifica
 	if err == nil && res != nil {
 		w := newRIDWrites()
 		w.isas[res.ID] = res
-		err = t.apply(w)
+		t.applyCommitted(w)
 	}
 	return res, err
 }
@@ -153,7 +167,7 @@ func (t *RIDTransactor) DeleteISA(ctx context.Context, isa *ridmodels.Identifica
 	if err == nil {
 		w := newRIDWrites()
 		w.isas[isa.ID] = nil
-		err = t.apply(w)
+		t.applyCommitted(w)
 	}
 	return res, err
 }
@@ -163,7 +177,7 @@ func (t *RIDTransactor) InsertSubscription(ctx context.Context, sub *ridmodels.S
 	if err == nil && res != nil {
 		w := newRIDWrites()
 		w.subs[res.ID] = res
-		err = t.apply(w)
+		t.applyCommitted(w)
 	}
 	return res, err
 }
@@ -173,7 +187,7 @@ func (t *RIDTransactor) UpdateSubscription(ctx context.Context, sub *ridmodels.S
 	if err == nil && res != nil {
 		w := newRIDWrites()
 		w.subs[res.ID] = res
-		err = t.apply(w)
+		t.applyCommitted(w)
 	}
 	return res, err
 }
@@ -183,7 +197,7 @@ func (t *RIDTransactor) DeleteSubscription(ctx context.Context, sub *ridmodels.S
 	if err == nil {
 		w := newRIDWrites()
 		w.subs[sub.ID] = nil
-		err = t.apply(w)
+		t.applyCommitted(w)
 	}
 	return res, err
 }
@@ -197,7 +211,7 @@ func (t *RIDTransactor) UpdateNotificationIdxsInCells(ctx context.Context, cells
 		for _, s := range res {
 			w.subs[s.ID] = s
 		}
-		err = t.apply(w)
+		t.applyCommitted(w)
 	}
 	return res, err
 }
@@ -212,14 +226,17 @@ func (t *RIDTransactor) SearchISAs(ctx context.Context, cells s2.CellUnion, earl
 	if earliest == nil {
 		return nil, dsserr.Internal("must call with an earliest start time.")
 	}
+	if t.Invalid() {
+		return t.Transactor.SearchISAs(ctx, cells, earliest, latest)
+	}
 	q := Query{Cells: cells, AltLo: negInf, AltHi: posInf, TLo: earliest.UnixNano() / 1000,
 		THi: usOrNull(latest, timeNullEndQ)}
+	t.mu.RLock() // across the search and the lookup: no apply lands in between
+	defer t.mu.RUnlock()
 	keys, err := t.isas.Search([]Query{q})
 	if err != nil {
 		return nil, err
 	}
-	t.mu.RLock()
-	defer t.mu.RUnlock()
 	out := make([]*ridmodels.IdentificationServiceArea, 0, len(keys[0]))
 	for _, k := range keys[0] {
 		if i, ok := t.isaRows[dssmodels.ID(k)]; ok {
@@ -236,12 +253,12 @@ func (t *RIDTransactor) searchSubs(cells s2.CellUnion, owner string) ([]*ridmode
 	}
 	q := Query{Cells: cells, AltLo: negInf, AltHi: posInf, TLo: t.Now().UnixNano() / 1000, THi: timeNullEndQ,
 		Owner: owner}
+	t.mu.RLock() // across the search and the lookup: no apply lands in between
+	defer t.mu.RUnlock()
 	keys, err := t.subs.Search([]Query{q})
 	if err != nil {
 		return nil, err
 	}
-	t.mu.RLock()
-	defer t.mu.RUnlock()
 	out := make([]*ridmodels.Subscription, 0, len(keys[0]))
 	for _, k := range keys[0] {
 		if s, ok := t.subRows[dssmodels.ID(k)]; ok {
@@ -255,12 +272,18 @@ func (t *RIDTransactor) searchSubs(cells s2.CellUnion, owner string) ([]*ridmode
 // SearchSubscriptions replaces (*SubscriptionStore).SearchSubscriptions
 // (pkg/rid/cockroach/subscriptions.go:222-244): cells && cells AND ends_at >= now.
 func (t *RIDTransactor) SearchSubscriptions(ctx context.Context, cells s2.CellUnion) ([]*ridmodels.Subscription, error) {
+	if t.Invalid() {
+		return t.Transactor.SearchSubscriptions(ctx, cells)
+	}
 	return t.searchSubs(cells, "")
 }
 
 // SearchSubscriptionsByOwner replaces (*SubscriptionStore).SearchSubscriptionsByOwner
 // (pkg/rid/cockroach/subscriptions.go:247-273): the same AND owner = $owner.
 func (t *RIDTransactor) SearchSubscriptionsByOwner(ctx context.Context, cells s2.CellUnion, owner dssmodels.Owner) ([]*ridmodels.Subscription, error) {
+	if t.Invalid() {
+		return t.Transactor.SearchSubscriptionsByOwner(ctx, cells, owner)
+	}
 	return t.searchSubs(cells, owner.String())
 }
 
@@ -270,8 +293,6 @@ type ridRepo struct {
 	repos.Repository
 	w *ridWrites
 }
-
-func (r *ridRepo) dirty() bool { return len(r.w.isas) > 0 || len(r.w.subs) > 0 }
 
 func (r *ridRepo) InsertISA(ctx context.Context, isa *ridmodels.IdentificationServiceArea) (*ridmodels.IdentificationServiceArea, error) {
 	res, err := r.Repository.InsertISA(ctx, isa)

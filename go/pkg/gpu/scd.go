@@ -3,6 +3,7 @@ package gpu
 import (
 	"context"
 	"sync"
+	"sync/atomic"
 	"time"
 
 	"github.com/golang/geo/s2"
@@ -13,12 +14,22 @@ import (
 )
 
 // SCDTransactor decorates the reference's CockroachDB transactor
-// (pkg/scd/store/cockroach, selected in cmds/grpc-backend/main.go): every
-// write and point read still goes to CRDB, the source of truth, while
-// SearchOperations and SearchSubscriptions run on GPU mirrors of the
-// scd_operations / scd_subscriptions 4D columns.  A transaction's writes
-// reach the mirrors when it commits; a transaction that has written runs its
-// own searches on CRDB, so it sees its own writes exactly as SQL does.
+// (pkg/scd/store/cockroach, selected in cmds/grpc-backend/main.go).  CRDB
+// stays the source of truth for every row write and point read; the 4D
+// searches run on GPU mirrors of the scd_operations / scd_subscriptions
+// columns:
+//   - SearchOperations and SearchSubscriptions;
+//   - UpsertOperation's conflict search and OVN set difference
+//     (operations.go:304-372), through the store hook of
+//     go/patches/0002 (UpsertOperationWithConflictSearch), so the
+//     transaction's SQL does only the row writes and the notification;
+//   - inside a transaction, the searches see its own uncommitted writes
+//     (read-your-writes): the mirror's answer minus the rows the transaction
+//     has written, plus those of its written rows that match.
+// A transaction's writes reach the mirrors when it commits.  The mirrors see
+// only this process's writes (single writer per CRDB cluster, INTEGRATION.md);
+// if applying a committed transaction to them fails, they are marked invalid
+// and every search goes to CRDB from then on.
 type SCDTransactor struct {
 	Inner scdstore.Transactor
 	// Now is the store clock (the reference's cockroach.DefaultClock).
@@ -28,7 +39,11 @@ type SCDTransactor struct {
 	mu        sync.RWMutex
 	opRows    map[scdmodels.ID]*scdmodels.Operation
 	subRows   map[scdmodels.ID]*scdmodels.Subscription
+	invalid   int32 // atomic: 1 after a failed apply of a committed transaction
 }
+
+// Invalid reports whether the mirrors fell behind CRDB (searches then run on CRDB).
+func (t *SCDTransactor) Invalid() bool { return atomic.LoadInt32(&t.invalid) != 0 }
 
 // NewSCDTransactor builds the mirrors from the tables' current rows (read
 // once at start-up, e.g. SELECT * FROM scd_operations / scd_subscriptions).
@@ -126,7 +141,11 @@ func (x *scdTx) Commit() error {
 	if err := x.inner.Commit(); err != nil {
 		return err
 	}
-	return x.flush()
+	if err := x.flush(); err != nil {
+		// the transaction did commit: report success, stop trusting the mirrors
+		atomic.StoreInt32(&x.t.invalid, 1)
+	}
+	return nil
 }
 
 func (x *scdTx) flush() error {
@@ -157,8 +176,6 @@ func (x *scdTx) Rollback() error {
 	return x.inner.Rollback()
 }
 
-func (x *scdTx) dirty() bool { return len(x.ops) > 0 || len(x.subs) > 0 }
-
 // scdStore is the store a transaction hands out: the CRDB store with the
 // searches replaced.
 type scdStore struct {
@@ -181,13 +198,37 @@ func (s *scdStore) refreshSub(ctx context.Context, id scdmodels.ID, owner dssmod
 	}
 }
 
+// conflictSearchStore is the reference store with the hook of
+// go/patches/0002-scd-rid-gpu-store-hooks.patch.
+type conflictSearchStore interface {
+	UpsertOperationWithConflictSearch(ctx context.Context, operation *scdmodels.Operation, key []scdmodels.OVN,
+		search func(ctx context.Context, op *scdmodels.Operation) ([]*scdmodels.Operation, error)) (*scdmodels.Operation, []*scdmodels.Subscription, error)
+}
+
 func (s *scdStore) UpsertOperation(ctx context.Context, op *scdmodels.Operation, key []scdmodels.OVN) (*scdmodels.Operation, []*scdmodels.Subscription, error) {
-	res, subs, err := s.Store.UpsertOperation(ctx, op, key)
+	var (
+		res  *scdmodels.Operation
+		subs []*scdmodels.Subscription
+		err  error
+	)
+	if cs, ok := s.Store.(conflictSearchStore); ok && !s.tx.t.Invalid() {
+		res, subs, err = cs.UpsertOperationWithConflictSearch(ctx, op, key, s.conflicts)
+	} else {
+		res, subs, err = s.Store.UpsertOperation(ctx, op, key)
+	}
 	if err == nil && res != nil {
 		s.tx.ops[res.ID] = res
 		s.refreshSub(ctx, res.SubscriptionID, res.Owner)
 	}
 	return res, subs, err
+}
+
+// conflicts is UpsertOperation's search (operations.go:337-348: the
+// operation's own cells, altitudes and times, ends_at >= now) on the GPU
+// mirror, with this transaction's writes overlaid.
+func (s *scdStore) conflicts(ctx context.Context, op *scdmodels.Operation) ([]*scdmodels.Operation, error) {
+	q := opQuery(op.Cells, op.AltitudeLower, op.AltitudeUpper, op.StartTime, op.EndTime, s.tx.t.Now())
+	return s.searchOps(q)
 }
 
 func (s *scdStore) DeleteOperation(ctx context.Context, id scdmodels.ID, owner dssmodels.Owner) (*scdmodels.Operation, []*scdmodels.Subscription, error) {
@@ -217,6 +258,54 @@ func (s *scdStore) DeleteSubscription(ctx context.Context, id scdmodels.ID, owne
 	return res, err
 }
 
+// opQuery folds searchOperations' bounds (operations.go:394-402) into a
+// mirror query: tlo = max(start, now) (COALESCE(ends_at >= start) AND
+// ends_at >= now), NULL end -> open.
+func opQuery(cells s2.CellUnion, lo, hi *float32, start, end *time.Time, now time.Time) Query {
+	tlo := now.UnixNano() / 1000
+	if start != nil {
+		if st := start.UnixNano() / 1000; st > tlo {
+			tlo = st
+		}
+	}
+	return Query{Cells: cells, AltLo: altOr(lo, negInf), AltHi: altOr(hi, posInf), TLo: tlo,
+		THi: usOrNull(end, timeNullEndQ)}
+}
+
+// searchOps runs q on the operations mirror and maps the keys to rows under
+// one read lock (no apply can land between the search and the lookup), with
+// the transaction's own writes overlaid.  Results carry no cells, as
+// searchOperations' rows do not.
+func (s *scdStore) searchOps(q Query) ([]*scdmodels.Operation, error) {
+	t := s.tx.t
+	t.mu.RLock()
+	defer t.mu.RUnlock()
+	keys, err := t.ops.Search([]Query{q})
+	if err != nil {
+		return nil, err
+	}
+	out := make([]*scdmodels.Operation, 0, len(keys[0]))
+	for _, k := range keys[0] {
+		id := scdmodels.ID(k)
+		if _, written := s.tx.ops[id]; written {
+			continue // this transaction's version decides
+		}
+		if o, ok := t.opRows[id]; ok {
+			c := *o
+			c.Cells = nil
+			out = append(out, &c)
+		}
+	}
+	for _, o := range s.tx.ops {
+		if o != nil && opRow(o).Matches(q) {
+			c := *o
+			c.Cells = nil
+			out = append(out, &c)
+		}
+	}
+	return out, nil
+}
+
 // SearchOperations replaces searchOperations
 // (pkg/scd/store/cockroach/operations.go:374-435): the same argument checks
 // and error messages, then
@@ -225,7 +314,7 @@ func (s *scdStore) DeleteSubscription(ctx context.Context, id scdmodels.ID, owne
 //   AND COALESCE(starts_at <= end, true) AND ends_at >= now
 // on the GPU mirror.  The owner argument is unused, as in the reference.
 func (s *scdStore) SearchOperations(ctx context.Context, v4d *dssmodels.Volume4D, owner dssmodels.Owner) ([]*scdmodels.Operation, error) {
-	if s.tx.dirty() {
+	if s.tx.t.Invalid() {
 		return s.Store.SearchOperations(ctx, v4d, owner)
 	}
 	if v4d.SpatialVolume == nil || v4d.SpatialVolume.Footprint == nil {
@@ -238,30 +327,8 @@ func (s *scdStore) SearchOperations(ctx context.Context, v4d *dssmodels.Volume4D
 	if len(cells) == 0 {
 		return nil, dsserr.BadRequest("missing cell IDs for query")
 	}
-	t := s.tx.t
-	now := t.Now().UnixNano() / 1000
-	tlo := now // ends_at >= now, and ends_at >= start when start is set
-	if v4d.StartTime != nil {
-		if st := v4d.StartTime.UnixNano() / 1000; st > tlo {
-			tlo = st
-		}
-	}
-	q := Query{Cells: cells, AltLo: altOr(v4d.SpatialVolume.AltitudeLo, negInf),
-		AltHi: altOr(v4d.SpatialVolume.AltitudeHi, posInf), TLo: tlo, THi: usOrNull(v4d.EndTime, timeNullEndQ)}
-	keys, err := t.ops.Search([]Query{q})
-	if err != nil {
-		return nil, err
-	}
-	t.mu.RLock()
-	defer t.mu.RUnlock()
-	out := make([]*scdmodels.Operation, 0, len(keys[0]))
-	for _, k := range keys[0] {
-		if o, ok := t.opRows[scdmodels.ID(k)]; ok {
-			c := *o
-			out = append(out, &c)
-		}
-	}
-	return out, nil
+	return s.searchOps(opQuery(cells, v4d.SpatialVolume.AltitudeLo, v4d.SpatialVolume.AltitudeHi, v4d.StartTime,
+		v4d.EndTime, s.tx.t.Now()))
 }
 
 // SearchSubscriptions replaces the SCD SubscriptionStore.SearchSubscriptions
@@ -269,7 +336,7 @@ func (s *scdStore) SearchOperations(ctx context.Context, v4d *dssmodels.Volume4D
 // every row of the owner, so the cells only have to be non-empty (quirk Q7):
 // the answer is the owner's subscriptions with ends_at >= now.
 func (s *scdStore) SearchSubscriptions(ctx context.Context, cells s2.CellUnion, owner dssmodels.Owner) ([]*scdmodels.Subscription, error) {
-	if s.tx.dirty() {
+	if s.tx.t.Invalid() {
 		return s.Store.SearchSubscriptions(ctx, cells, owner)
 	}
 	if len(cells) == 0 {
@@ -277,14 +344,25 @@ func (s *scdStore) SearchSubscriptions(ctx context.Context, cells s2.CellUnion, 
 	}
 	t := s.tx.t
 	now := t.Now()
+	live := func(sub *scdmodels.Subscription) bool {
+		return sub.Owner == owner && sub.EndTime != nil && !sub.EndTime.Before(now)
+	}
 	t.mu.RLock()
 	defer t.mu.RUnlock()
 	var out []*scdmodels.Subscription
-	for _, sub := range t.subRows {
-		if sub.Owner == owner && sub.EndTime != nil && !sub.EndTime.Before(now) {
+	for id, sub := range t.subRows {
+		if _, written := s.tx.subs[id]; !written && live(sub) {
 			c := *sub
 			out = append(out, &c)
 		}
 	}
+	for _, sub := range s.tx.subs { // read-your-writes
+		if sub != nil && live(sub) {
+			c := *sub
+			out = append(out, &c)
+		}
+	}
+	// the reference commits this read-only transaction (subscriptions.go:540);
+	// here the caller's transaction is left to the caller
 	return out, nil
 }

@@ -183,6 +183,63 @@ int main(void)
         CHECK(rc == DSSG_OK && needed == 0, "after move n=%lld", (long long)needed);
         dssg_store_free(store);
     }
+    /* ---- UpsertOperation replayed as go/pkg/gpu runs it --------------------
+     * (operations.go:304-372 through UpsertOperationWithConflictSearch): the
+     * conflict search on the store with the transaction's pending writes
+     * overlaid on the host (Row.Matches), the OVN set difference, the write at
+     * commit, the re-search. */
+    {
+        dssg_store *ms = NULL;
+        rc = dssg_store_create(ctx, 0, &ms);
+        CHECK(rc == DSSG_OK && ms, "mirror create rc=%d", rc);
+        const int64_t now = 1000;
+        /* committed: op A (id 1) over the KAT cells, [1000, 5000], alt [0, 100]; OVN "A" */
+        const uint32_t idA = 1;
+        const int64_t offsA[2] = {0, 20}, t0A = 1000, t1A = 5000;
+        const float loA = 0.f, hiA = 100.f;
+        rc = dssg_store_upsert(ctx, ms, 1, &idA, offsA, kat, &loA, &hiA, &t0A, &t1A, NULL);
+        CHECK(rc == DSSG_OK, "mirror upsert A rc=%d", rc);
+        /* the transaction writes op B (id 2): same cells, [2000, 3000], alt [50, 150] */
+        const float loB = 50.f, hiB = 150.f;
+        const int64_t t0B = 2000, t1B = 3000;
+        uint32_t oq[8], oid[8];
+        const int64_t qoffs[2] = {0, 20};
+        int64_t tlo = t0B > now ? t0B : now, thi = t1B;
+        /* conflict search of B's volume, key = {} -> A is missing (409) */
+        rc = dssg_store_search(ctx, ms, 1, qoffs, kat, &loB, &hiB, &tlo, &thi, NULL, oq, oid, 8, &needed);
+        CHECK(rc == DSSG_OK && needed == 1 && oid[0] == idA, "conflict search n=%lld", (long long)needed);
+        /* key = {A's OVN}: nothing missing, B is written in the transaction (pending, not in the mirror) */
+        /* re-search inside the transaction (read-your-writes): the mirror's {A} plus pending B if it matches */
+        const float qlo = 0.f, qhi = 500.f;
+        int64_t qtlo = 2500, qthi = 2600;
+        rc = dssg_store_search(ctx, ms, 1, qoffs, kat, &qlo, &qhi, &qtlo, &qthi, NULL, oq, oid, 8, &needed);
+        const int b_matches = t1B >= qtlo && t0B <= qthi && hiB >= qlo && loB <= qhi; /* Row.Matches, cells shared */
+        CHECK(rc == DSSG_OK && needed == 1 && oid[0] == idA && b_matches, "read-your-writes n=%lld", (long long)needed);
+        /* commit: B reaches the mirror */
+        const uint32_t idB = 2;
+        rc = dssg_store_upsert(ctx, ms, 1, &idB, qoffs, kat, &loB, &hiB, &t0B, &t1B, NULL);
+        CHECK(rc == DSSG_OK, "mirror upsert B rc=%d", rc);
+        rc = dssg_store_search(ctx, ms, 1, qoffs, kat, &qlo, &qhi, &qtlo, &qthi, NULL, oq, oid, 8, &needed);
+        CHECK(rc == DSSG_OK && needed == 2 && oid[0] == idA && oid[1] == idB, "after commit n=%lld", (long long)needed);
+        /* op C over both with key = {A}: B is missing */
+        int64_t ctlo = 2000, cthi = 4000;
+        rc = dssg_store_search(ctx, ms, 1, qoffs, kat, &qlo, &qhi, &ctlo, &cthi, NULL, oq, oid, 8, &needed);
+        int missing = 0;
+        for (int64_t k = 0; k < needed; k++) missing += oid[k] != idA;
+        CHECK(rc == DSSG_OK && needed == 2 && missing == 1, "C conflicts n=%lld missing=%d", (long long)needed, missing);
+        /* B's end before C's start: no conflict with B (COALESCE(ends_at >= start)) */
+        ctlo = 3001;
+        rc = dssg_store_search(ctx, ms, 1, qoffs, kat, &qlo, &qhi, &ctlo, &cthi, NULL, oq, oid, 8, &needed);
+        CHECK(rc == DSSG_OK && needed == 1 && oid[0] == idA, "time-disjoint n=%lld", (long long)needed);
+        /* DeleteOperation of A, committed: only B remains */
+        int32_t found = 0;
+        rc = dssg_store_delete(ctx, ms, 1, &idA, &found);
+        CHECK(rc == DSSG_OK && found == 1, "mirror delete rc=%d", rc);
+        ctlo = 2000;
+        rc = dssg_store_search(ctx, ms, 1, qoffs, kat, &qlo, &qhi, &ctlo, &cthi, NULL, oq, oid, 8, &needed);
+        CHECK(rc == DSSG_OK && needed == 1 && oid[0] == idB, "after delete A n=%lld", (long long)needed);
+        dssg_store_free(ms);
+    }
     free(ecells);
     dssg_destroy(ctx);
     if (failures) {

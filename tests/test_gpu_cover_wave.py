@@ -72,8 +72,10 @@ def test_wave_path_reversal_and_errors(oracle):
         lng += [b for _, b in pts]
         voff.append(len(lat))
         rad.append(0.0)
-    for la, ln, r in ((37.4, -122.1, 300.0), (89.999, 180.0, 300.0), (-56, 178, 50.0), (0, 0, 4.0e6),
-                      (37.4, -122.1, 0.0), (12.0, -34.0, 300.0)):
+    # (0, 0, 3.3e6 m): 0.52 rad, not a small loop (general path); ~30M cells, past the oracle's
+    # 2^24-cell limit, so it is compared wave path vs general path only
+    for la, ln, r in ((37.4, -122.1, 300.0), (89.999, 180.0, 300.0), (-56, 178, 50.0), (0, 0, 3.3e6),
+                      (37.4, -122.1, 0.0), (12.0, -34.0, 300.0), (0, 0, 1.0e6)):
         kinds.append(1)
         lat.append(la)
         lng.append(ln)
@@ -83,6 +85,14 @@ def test_wave_path_reversal_and_errors(oracle):
                          lng=np.array(lng), radius_m=np.array(rad, np.float32))
     wave, gen = _both_paths(fp)
     _same(wave, gen)
-    o_offs, o_cells, o_st, o_area = oracle.cover_batch(fp.kind, fp.voff, fp.lat, fp.lng, fp.radius_m)
-    assert np.array_equal(wave.offs, o_offs) and np.array_equal(wave.cells, o_cells)
+    big = len(polys) + 3
+    keep = np.array([i for i in range(len(kinds)) if i != big])
+    sub = SimpleNamespace(kind=fp.kind[keep], voff=np.concatenate([[0], np.cumsum(np.diff(fp.voff)[keep])]),
+                          lat=np.concatenate([fp.lat[fp.voff[i]:fp.voff[i + 1]] for i in keep]),
+                          lng=np.concatenate([fp.lng[fp.voff[i]:fp.voff[i + 1]] for i in keep]),
+                          radius_m=fp.radius_m[keep])
+    wave, _ = _both_paths(sub)
+    o_offs, o_cells, o_st, o_area = oracle.cover_batch(sub.kind, sub.voff, sub.lat, sub.lng, sub.radius_m)
     assert np.array_equal(wave.status, o_st)
+    assert np.array_equal(wave.offs, o_offs) and np.array_equal(wave.cells, o_cells)
+    assert np.array_equal(wave.area_km2.view(np.uint64), np.asarray(o_area, np.float64).view(np.uint64))

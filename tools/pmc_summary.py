@@ -24,17 +24,30 @@ def short(name):
     return m.group(1) if m else name[:40]
 
 
-def collect(d):
+def collect(d, skip_first=0):
+    """Per kernel: durations (ms) and counter values per dispatch, in dispatch
+    order, without each kernel's first `skip_first` dispatches (the intents'
+    covering / index build and the first search's capacity growth: what is
+    left is one steady-state search per dispatch)."""
     dur = defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
         if not os.path.basename(f).startswith("kt"):
             continue
-        for r in csv.DictReader(open(f)):
+        rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r.get("Dispatch_Id") or r["Start_Timestamp"]))
+        for r in rows:
             dur[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     ctr = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
+        rows = list(csv.DictReader(open(f)))
+        if rows and "Dispatch_Id" in rows[0]:
+            rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        for r in rows:
             ctr[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    if skip_first:
+        dur = defaultdict(list, {k: v[skip_first:] for k, v in dur.items()})
+        for k in ctr:
+            for c in ctr[k]:
+                ctr[k][c] = ctr[k][c][skip_first:]
     return dur, ctr
 
 
@@ -45,8 +58,10 @@ def main():
     ap.add_argument("--queries", type=int)
     ap.add_argument("--intents", type=int)
     ap.add_argument("--source", default="")
+    ap.add_argument("--skip-first", type=int, default=0,
+                    help="drop each kernel's first N dispatches (setup + the first search's capacity growth)")
     a = ap.parse_args()
-    dur, ctr = collect(a.dir)
+    dur, ctr = collect(a.dir, a.skip_first)
     names = sorted(set(dur) | set(ctr), key=lambda k: -sum(dur.get(k, [0])))
     cols = sorted({c for k in ctr for c in ctr[k]})
     print("kernel,dispatches,avg_ms,total_ms," + ",".join(cols) + ",hbm_bytes_per_launch")
@@ -64,7 +79,7 @@ def main():
                   "fetch_kib": f, "write_kib": w, "hbm_bytes_per_launch": hbm}
     if a.json:
         with open(a.json, "w") as fh:
-            json.dump({"source": a.source, "queries": a.queries, "intents": a.intents,
+            json.dump({"source": a.source, "queries": a.queries, "intents": a.intents, "skip_first": a.skip_first,
                        "correction": "hbm = 2*1024*FETCH_SIZE + 1024*WRITE_SIZE (MI355X_MICROARCH.md s HBM)",
                        "kernels": {k: v for k, v in out.items() if v["hbm_bytes_per_launch"] is not None}},
                       fh, indent=1)

@@ -9,7 +9,7 @@ STEPS=${STEPS:-3}
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/prof/$TAG
 mkdir -p "$OUT"
-B="$R/bench.py --steps $STEPS --warmup 1 --cpu-sample 0 --survey-model 0 --pipelines 1 $BENCH_ARGS"
+B="$R/bench.py --steps $STEPS --warmup 1 --cpu-sample 0 --survey-model 0 --pipelines 1 --latency 0 --no-verify $BENCH_ARGS"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT" -o kt --output-format csv -- python3 $B > "$OUT/kt.log" 2>&1
 [ -n "$KT_ONLY" ] || timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT" -o pmc_fetch --output-format csv -- python3 $B > "$OUT/pmc_fetch.log" 2>&1
@@ -23,5 +23,5 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INST
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE -d "$OUT" -o pmc_cyc --output-format csv -- python3 $B > "$OUT/pmc_cyc.log" 2>&1
 fi
 cd "$R"
-python3 tools/pmc_summary.py "$OUT" --json "$OUT/pmc_traffic.json" --queries 1000000 --intents 1000000 --source "profiles/$TAG" > "$OUT/summary.csv"
+python3 tools/pmc_summary.py "$OUT" --skip-first ${SKIP:-2} --json "$OUT/pmc_traffic.json" --queries ${NQ:-1000000} --intents ${NI:-10000000} --source "profiles/$TAG" > "$OUT/summary.csv"
 cat "$OUT/summary.csv" | head -30
