@@ -243,13 +243,8 @@ int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value)
         ctx->search.set_small_max_q(value);
         return DSSG_OK;
     }
-    if (std::string(key) == "join_tiles") {  // 1: k_join (a wave per 64-posting tile); 4: k_join_blk
-        if (value != 1 && value != 4) return DSSG_ERR_INVALID;
-        ctx->search.set_join_tiles(value);
-        return DSSG_OK;
-    }
-    if (std::string(key) == "cover_wave") {  // 0: every footprint through the general covering pipeline
-        ctx->cover.set_wave_path(value != 0);
+    if (std::string(key) == "cover_wave") {  // max batch of the wave-path covering (0: general pipeline only)
+        ctx->cover.set_wave_max(value);
         return DSSG_OK;
     }
     return DSSG_ERR_INVALID;

@@ -45,6 +45,7 @@ enum : uint8_t { FL_SMALL = 1, FL_PLANAR = 2, FL_FAST = 4 };
 // level >= kFastMinLevel (<= 4 * 4^(13 - L) level-13 candidates).
 constexpr int kFastMinLevel = 10;
 constexpr int kCandBlock = 256;
+constexpr int kCandStageV = 1024;  // (u,v) vertices a k_cand_test_c block stages in LDS (16 KiB)
 // node meta: level (bits 0-4), orientation (5-6), done (7), face (8-10)
 __device__ __forceinline__ uint32_t pack_meta(int level, int orient, int done, int face)
 {
@@ -1070,30 +1071,67 @@ __device__ __forceinline__ int cand_edges(uint32_t f, uint32_t i, uint32_t j, co
     return in ? 1 : planar ? (((origin_in[f] != 0) != par) ? 1 : 0) : 2;
 }
 
+// cand_edges over vertices already at `up` (the block's LDS stage).
+__device__ __forceinline__ int cand_edges_at(uint32_t f, uint32_t i, uint32_t j, const double2 *up, const int32_t *nvx,
+                                             const uint8_t *origin_in, const uint8_t *flags)
+{
+    const int nv = nvx[f];
+    double2 a = up[0];
+    const uint32_t size = 1u << (kMaxLevel - kCoverLevel);
+    const double ulo = st_to_uv((double)i / (double)kMaxSize), uhi = st_to_uv((double)(i + size) / (double)kMaxSize);
+    const double vlo = st_to_uv((double)j / (double)kMaxSize), vhi = st_to_uv((double)(j + size) / (double)kMaxSize);
+    const double pm = kFinePad;
+    const bool planar = (flags[f] & FL_PLANAR) != 0;
+    const double half = 0.5 / (double)kMaxSize, sz = (double)size;
+    const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
+    bool in = false, par = false;
+    for (int e = 0; e < nv; e++) {
+        const double2 b = up[e + 1 < nv ? e + 1 : 0];
+        if (edge_intersects_rect(a.x, a.y, b.x, b.y, ulo - pm, uhi + pm, vlo - pm, vhi + pm)) {
+            in = true;
+            break;
+        }
+        if ((a.y > vc) != (b.y > vc)) {
+            const double d = b.y - a.y;
+            const double lhs = (uc - a.x) * d, rhs = (vc - a.y) * (b.x - a.x);
+            if (d > 0 ? lhs < rhs : lhs > rhs) par = !par;
+        }
+        a = b;
+    }
+    return in ? 1 : planar ? (((origin_in[f] != 0) != par) ? 1 : 0) : 2;
+}
+
 // Verdicts leave as two ballot masks per wave of 64 candidates (kept, and
 // undecided): 16 B per 64 candidates instead of a per-candidate word, and
 // the compaction below ranks by popcount, with no candidate-sized scan.
 // The block first tests its 256 candidates against their footprints' level-13
 // bounds, compacts the ones inside to its first threads (LDS), and only those
 // run the edge loop: the out-of-bound lanes no longer idle through it.
-#ifndef DSS_CAND_COMPACT
-#define DSS_CAND_COMPACT 1
-#endif
 __global__ __launch_bounds__(kCandBlock) void k_cand_test_c(int64_t NC, const uint32_t *cand_f, const int64_t *coff,
                                                             const uint64_t *st_id, const uint32_t *st_i,
                                                             const uint32_t *st_j, const uint32_t *finfo,
                                                             const uint4 *fbox, const int64_t *xoff, const double2 *uv,
                                                             const int32_t *nvx, const uint8_t *origin_in,
                                                             const uint8_t *flags, unsigned long long *kmask,
-                                                            unsigned long long *umask)
+                                                            unsigned long long *umask, uint32_t *ulist,
+                                                            unsigned int *ulist_n)
 {
     __shared__ uint32_t s_lt[kCandBlock], s_ci[kCandBlock], s_cj[kCandBlock], s_f[kCandBlock];
     __shared__ unsigned int s_n;
     __shared__ unsigned long long s_k[kCandBlock / 64], s_u[kCandBlock / 64];
+    __shared__ double2 s_uv[kCandStageV];  // the block's footprints' (u,v) vertices, when they fit
     const int t = threadIdx.x, lane = t & 63;
     const int64_t c0 = (int64_t)blockIdx.x * kCandBlock, c = c0 + t;
     if (t == 0) s_n = 0;
     if (t < kCandBlock / 64) s_k[t] = s_u[t] = 0;
+    // candidates are grouped by footprint: the block's footprints are
+    // [cand_f[c0], cand_f[last]], their vertices one contiguous range
+    const int64_t clast = min(c0 + kCandBlock, NC) - 1;
+    const uint32_t f_first = cand_f[c0], f_last = cand_f[clast];
+    const int64_t vb = xoff[f_first], ve = xoff[f_last] + nvx[f_last];
+    const bool staged = ve - vb <= kCandStageV;
+    if (staged)
+        for (int64_t v = vb + t; v < ve; v += kCandBlock) s_uv[v - vb] = uv[v];
     __syncthreads();
     bool inb = false;
     uint32_t i = 0, j = 0, f = 0;
@@ -1121,7 +1159,8 @@ __global__ __launch_bounds__(kCandBlock) void k_cand_test_c(int64_t NC, const ui
     __syncthreads();
     if ((unsigned int)t < s_n) {
         const uint32_t lt = s_lt[t];
-        const int v = cand_edges(s_f[t], s_ci[t], s_cj[t], xoff, uv, nvx, origin_in, flags);
+        const int v = staged ? cand_edges_at(s_f[t], s_ci[t], s_cj[t], s_uv + (xoff[s_f[t]] - vb), nvx, origin_in, flags)
+                             : cand_edges(s_f[t], s_ci[t], s_cj[t], xoff, uv, nvx, origin_in, flags);
         if (v == 1) atomicOr(&s_k[lt >> 6], 1ull << (lt & 63));
         else if (v == 2) atomicOr(&s_u[lt >> 6], 1ull << (lt & 63));
     }
@@ -1129,37 +1168,24 @@ __global__ __launch_bounds__(kCandBlock) void k_cand_test_c(int64_t NC, const ui
     if (t < kCandBlock / 64 && c0 + 64 * t < NC) {
         kmask[(c0 >> 6) + t] = s_k[t];
         umask[(c0 >> 6) + t] = s_u[t];
+        if (s_u[t]) ulist[atomicAdd(ulist_n, 1u)] = (uint32_t)((c0 >> 6) + t);  // words k_cand_exact must finish
     }
 }
 
-__global__ void k_cand_test(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
-                            const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const uint4 *fbox,
-                            const int64_t *xoff, const double2 *uv, const int32_t *nvx, const uint8_t *origin_in,
-                            const uint8_t *flags, unsigned long long *kmask, unsigned long long *umask)
+// Undecided candidates: exact S2 containment of the cell centre.  One wave
+// per listed mask word (k_cand_test_c lists the words with undecided bits;
+// a fixed grid strides over the list, so a batch with none costs one small
+// launch); the wave folds its results into the word.
+__device__ __forceinline__ void cand_exact_word(uint32_t g, int64_t NC, const uint32_t *cand_f, const int64_t *coff,
+                                                const uint64_t *st_id, const uint32_t *st_i, const uint32_t *st_j,
+                                                const uint32_t *finfo, const int64_t *xoff, const V3 *xyz,
+                                                const int32_t *nvx, const uint8_t *origin_in, unsigned long long *kmask,
+                                                const unsigned long long *umask)
 {
-    const int64_t c = tid64();
-    if (c - (threadIdx.x & 63) >= NC) return;  // whole wave past the end
-    const int v = c < NC ? cand_decide(c, cand_f, coff, st_id, st_i, st_j, finfo, fbox, xoff, uv, nvx, origin_in, flags) : 0;
-    const unsigned long long k = __ballot(v == 1), u = __ballot(v == 2);
-    if ((threadIdx.x & 63) == 0) {
-        kmask[c >> 6] = k;
-        umask[c >> 6] = u;
-    }
-}
-
-// Undecided candidates: exact S2 containment of the cell centre; the wave
-// that owns a mask word folds its results into it.
-__global__ __launch_bounds__(256) void k_cand_exact(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
-                             const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const int64_t *xoff,
-                             const V3 *xyz, const int32_t *nvx, const uint8_t *origin_in, unsigned long long *kmask,
-                             const unsigned long long *umask)
-{
-    const int64_t c = tid64();
-    if (c - (threadIdx.x & 63) >= NC) return;
-    const unsigned long long um = umask[c >> 6];
-    if (um == 0) return;  // wave-uniform
+    const int64_t c = ((int64_t)g << 6) + (threadIdx.x & 63);
+    const unsigned long long um = umask[g];
     bool in = false;
-    if ((um >> (threadIdx.x & 63)) & 1ull) {
+    if (c < NC && ((um >> (threadIdx.x & 63)) & 1ull)) {
         const uint32_t f = cand_f[c];
         int face;
         uint32_t i, j;
@@ -1169,7 +1195,18 @@ __global__ __launch_bounds__(256) void k_cand_exact(int64_t NC, const uint32_t *
         in = loop_contains(l, node_center(face, i, j, kCoverLevel));
     }
     const unsigned long long m = __ballot(in);
-    if ((threadIdx.x & 63) == 0) kmask[c >> 6] |= m;
+    if ((threadIdx.x & 63) == 0) kmask[g] |= m;
+}
+
+__global__ __launch_bounds__(256) void k_cand_exact(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
+                             const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const int64_t *xoff,
+                             const V3 *xyz, const int32_t *nvx, const uint8_t *origin_in, unsigned long long *kmask,
+                             const unsigned long long *umask, const uint32_t *ulist, const unsigned int *ulist_n)
+{
+    const unsigned int nl = *ulist_n;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
+    for (int64_t wi = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); wi < (int64_t)nl; wi += nw)
+        cand_exact_word(ulist[wi], NC, cand_f, coff, st_id, st_i, st_j, finfo, xoff, xyz, nvx, origin_in, kmask, umask);
 }
 
 __global__ void k_mask_counts(int64_t G, const unsigned long long *kmask, int64_t *gcnt)
@@ -1645,7 +1682,11 @@ struct EmitSlow {
 void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
                       const float *radius_m, hipStream_t s, dssg_cells *out)
 {
-    if (!wave_ || n == 0) {
+    // the wave path is one launch with few host syncs, but a wave per
+    // footprint runs the per-footprint (uniform) work on all 64 lanes: at 1M
+    // footprints it took 6.5 ms against the general pipeline's 2.1 ms, so it
+    // serves the small, launch-bound batches of the per-request path only
+    if (!wave_ || n == 0 || n > wave_max_) {
         last_slow_ = n;
         run_general(n, kind, voff, lat, lng, radius_m, s, out);
         return;
@@ -1797,11 +1838,13 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     DSS_HIP(hipMemsetAsync(kmask + G, 0, sizeof(unsigned long long), s));
     if (NC > 0) {
         hipLaunchKernelGGL(k_cand_owner, dim3(grid_for(n, 256)), dim3(256), 0, s, n, coff, cand_f);
-        hipLaunchKernelGGL(DSS_CAND_COMPACT ? k_cand_test_c : k_cand_test, dim3(grid_for(NC, kCandBlock)),
-                           dim3(kCandBlock), 0, s, NC, cand_f, coff, st_id, st_i, st_j, finfo, fbox, xoff, uv, nvx, orig,
-                           flags, kmask, umask);
-        hipLaunchKernelGGL(k_cand_exact, dim3(grid_for(NC, B)), dim3(B), 0, s, NC, cand_f, coff, st_id, st_i, st_j, finfo,
-                           xoff, xyz, nvx, orig, kmask, umask);
+        uint32_t *ulist = ulist_.ensure(G + 1);
+        unsigned int *ulist_n = ulist_n_.ensure(1);
+        DSS_HIP(hipMemsetAsync(ulist_n, 0, sizeof(unsigned int), s));
+        hipLaunchKernelGGL(k_cand_test_c, dim3(grid_for(NC, kCandBlock)), dim3(kCandBlock), 0, s, NC, cand_f, coff, st_id,
+                           st_i, st_j, finfo, fbox, xoff, uv, nvx, orig, flags, kmask, umask, ulist, ulist_n);
+        hipLaunchKernelGGL(k_cand_exact, dim3((unsigned)std::min<int64_t>(grid_for(G, B / 64), 1024)), dim3(B), 0, s, NC,
+                           cand_f, coff, st_id, st_i, st_j, finfo, xoff, xyz, nvx, orig, kmask, umask, ulist, ulist_n);
         hipLaunchKernelGGL(k_mask_counts, dim3(grid_for(G, B)), dim3(B), 0, s, G, kmask, gcnt);
     }
     exclusive_scan_i64(gcnt, gpos, G, tmp_, s);

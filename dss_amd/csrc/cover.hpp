@@ -26,8 +26,9 @@ class CoverEngine {
     // one compacted sub-batch.
     void run(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
              const float *radius_m, hipStream_t s, dssg_cells *out);
-    // 0: every footprint through the general pipeline (A/B and tests)
-    void set_wave_path(bool on) { wave_ = on; }
+    // batches of at most `n` footprints take the wave path (0: never; tests
+    // force it for every batch)
+    void set_wave_max(int64_t n) { wave_ = n > 0; wave_max_ = n; }
     int64_t last_slow() const { return last_slow_; }
 
    private:
@@ -35,6 +36,7 @@ class CoverEngine {
                      const float *radius_m, hipStream_t s, dssg_cells *out);
     void init_tables(hipStream_t s);
     bool wave_ = true;
+    int64_t wave_max_ = 16384;
     int64_t last_slow_ = 0;
     // wave path: per-footprint outputs, the slow sub-batch, the merged CSR
     DevBuf<int32_t> w_status_, s_kind_;
@@ -70,6 +72,8 @@ class CoverEngine {
     DevBuf<uint32_t> st_i_, st_j_, finfo_, cand_f_;
     DevBuf<int64_t> ncand_, coff_, gcnt_, gpos_, dc64_, dpre_;
     DevBuf<unsigned long long> kmask_;
+    DevBuf<uint32_t> ulist_;          // mask words with undecided candidates
+    DevBuf<unsigned int> ulist_n_;
     DevBuf<uint4> fbox_;
     bool tables_ = false;
 };

@@ -150,35 +150,50 @@ __global__ void k_unpack_rows(int64_t n, const QRow *rows, int np, const int64_t
 }
 
 // Pairs (batch row, entity) -> part-major by the row's home part, packed
-// (home-local query << 32 | entity).  PASS 0 counts, PASS 1 fills.
+// (home-local query << 32 | entity).  PASS 0 counts, PASS 1 fills.  A block
+// takes a tile of kPairTile pairs: per-destination counts (and each pair's
+// rank among its destination's) come from LDS atomics, and the block adds to
+// / reserves from each destination's global counter once -- one global
+// atomic per (block, destination), not per (wave, destination): with 10^8
+// pairs per step the same-address atomics would otherwise serialise.
+constexpr int kPairItems = 16, kPairTile = kBlock * kPairItems;
 template <int PASS>
-__global__ __launch_bounds__(kBlock) void k_route_pairs(int64_t n, const uint32_t *pq, const uint32_t *pe,
-                                                        const uint32_t *home, const uint32_t *qid,
+__global__ __launch_bounds__(kBlock) void k_route_pairs(int64_t n, const uint32_t *__restrict__ pq,
+                                                        const uint32_t *__restrict__ pe, const uint32_t *__restrict__ home,
+                                                        const uint32_t *__restrict__ qid, int np,
                                                         unsigned long long *tot, const int64_t *base_d,
                                                         unsigned long long *cursor, uint64_t *out)
 {
-    const int64_t i = tid64();
-    const int lane = threadIdx.x & 63;
-    const bool live = i < n;
-    int d = -1;
-    uint32_t q = 0;
-    if (live) {
-        q = pq[i];
-        d = (int)home[q];
+    __shared__ uint32_t s_cnt[DSSG_MAX_PARTS];
+    __shared__ unsigned long long s_base[DSSG_MAX_PARTS];
+    for (int d = threadIdx.x; d < np; d += kBlock) s_cnt[d] = 0;
+    __syncthreads();
+    const int64_t t0 = (int64_t)blockIdx.x * kPairTile;
+    int dst[kPairItems];
+    uint32_t rank[kPairItems];
+#pragma unroll
+    for (int j = 0; j < kPairItems; j++) {
+        const int64_t i = t0 + (int64_t)j * kBlock + threadIdx.x;
+        dst[j] = -1;
+        if (i < n) {
+            dst[j] = (int)home[pq[i]];
+            rank[j] = atomicAdd(&s_cnt[dst[j]], 1u);
+        }
     }
-    unsigned long long wm = wave_or(live ? 1ull << d : 0ull);
-    const unsigned long long below = (1ull << lane) - 1ull;
-    while (wm) {
-        const int t = __builtin_ctzll(wm);
-        wm &= wm - 1;
-        const bool has = d == t;
-        const unsigned long long bal = __ballot(has);
-        const unsigned long long cnt = (unsigned long long)__popcll(bal);
-        unsigned long long b = 0;
-        if (lane == 0) b = atomicAdd(PASS == 0 ? &tot[t] : &cursor[t], cnt);
-        b = __shfl(b, 0);  // all lanes, before any divergence
-        if (PASS == 0 || !has) continue;
-        out[base_d[t] + (int64_t)b + __popcll(bal & below)] = ((uint64_t)qid[q] << 32) | pe[i];
+    __syncthreads();
+    if (PASS == 0) {
+        for (int d = threadIdx.x; d < np; d += kBlock)
+            if (s_cnt[d]) atomicAdd(&tot[d], (unsigned long long)s_cnt[d]);
+        return;
+    }
+    for (int d = threadIdx.x; d < np; d += kBlock)
+        s_base[d] = s_cnt[d] ? atomicAdd(&cursor[d], (unsigned long long)s_cnt[d]) : 0ull;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPairItems; j++) {
+        if (dst[j] < 0) continue;
+        const int64_t i = t0 + (int64_t)j * kBlock + threadIdx.x;
+        out[base_d[dst[j]] + (int64_t)(s_base[dst[j]] + rank[j])] = ((uint64_t)qid[pq[i]] << 32) | pe[i];
     }
 }
 
@@ -273,8 +288,8 @@ void RouteEngine::pairs_plan(const dssg_batch *b, const dssg_pairs *p, int np, h
     DSS_HIP(hipMemsetAsync(acc, 0, 2 * kMaxParts * sizeof(unsigned long long), s));
     const int64_t n = p->n;
     if (n > 0)
-        hipLaunchKernelGGL(k_route_pairs<0>, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, p->q, p->e, b->home, b->qid,
-                           acc, nullptr, nullptr, nullptr);
+        hipLaunchKernelGGL(k_route_pairs<0>, dim3(grid_for(n, kPairTile)), dim3(kBlock), 0, s, n, p->q, p->e, b->home,
+                           b->qid, np, acc, nullptr, nullptr, nullptr);
     unsigned long long h[kMaxParts];
     DSS_HIP(hipMemcpyAsync(h, acc, sizeof(h), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
@@ -297,8 +312,8 @@ void RouteEngine::pairs_fill(const dssg_batch *b, const dssg_pairs *p, hipStream
     if (pplan_np_ == 0 || p->n != pplan_n_ || p->q != pplan_q_)
         throw Error(DSSG_ERR_INVALID, "route_pairs fill: no matching dssg_route_pairs_plan_device on this context");
     if (p->n > 0)
-        hipLaunchKernelGGL(k_route_pairs<1>, dim3(grid_for(p->n, kBlock)), dim3(kBlock), 0, s, p->n, p->q, p->e, b->home,
-                           b->qid, nullptr, pbase_.p, pacc_.p + kMaxParts, out);
+        hipLaunchKernelGGL(k_route_pairs<1>, dim3(grid_for(p->n, kPairTile)), dim3(kBlock), 0, s, p->n, p->q, p->e,
+                           b->home, b->qid, pplan_np_, nullptr, pbase_.p, pacc_.p + kMaxParts, out);
     pplan_np_ = 0;
 }
 

@@ -1413,288 +1413,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
     }
 }
 
-// Block join: one workgroup per unit of up to kBlkTiles consecutive 64-posting
-// tiles of one cell (wave w holds tile w, lane = posting, in registers).  The
-// records of the group's time band are staged ONCE for the whole group --
-// 256 at a time, one per thread (sval gather), hull-tested against the
-// group's [first start, latest end], compacted block-wide into LDS -- and
-// every wave tests its own tile against them 64 at a time.  A record that
-// meets several tiles of a hot cell is loaded once per group instead of once
-// per tile (k_join re-stages it for every tile whose band it meets).  The
-// per-record tests, the smallest-shared-cell rule and the emission are
-// k_join's.
-constexpr int kBlkTiles = kWaves;
-constexpr int kBlkRecs = 64 * kWaves;
-template <bool OWNER, bool LONG>
-__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LONG ? 1 : kJoinBlocksPerCU))) void k_join_blk(JoinArgs a, const QRec *__restrict__ recs,
-                                                          const uint32_t *__restrict__ sval,
-                                                          const Unit *__restrict__ units,
-                                                          unsigned long long *__restrict__ work)
-{
-    __shared__ longlong2 s_rt[kBlkRecs];      // record (tlo, thi)
-    __shared__ float4 s_ra[kBlkRecs];         // record (alo, ahi, qv, own)
-    __shared__ ulonglong2 s_rs[2][kBlkRecs];  // record near-prefix signature
-    __shared__ uint2 s_out[kWaves][kOutStage];
-    __shared__ uint32_t s_wc[kWaves];
-    __shared__ long long s_hull[kWaves];
-    __shared__ long long s_unit;
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const IndexView &ix = a.ix;
-    WaveOut out, tout;
-    unsigned long long n_tests = 0, n_bcast = 0;
-    int qreg = (int)(blockIdx.x % kRegions), visited = 0;
-    int64_t qn = min((int64_t)a.ur.cnt[qreg * kRegStride], a.ur.cap);
-    // one unit per grab, by thread 0 for the block
-    auto grab = [&]() -> long long {
-        while (true) {
-            const unsigned long long ub = atomicAdd(&work[qreg * kRegStride], 1ull);
-            if ((int64_t)ub < qn) return (long long)qreg * a.ur.cap + (long long)ub;
-            if (++visited >= kRegions) return -1;
-            qreg = (qreg + 1) % kRegions;
-            qn = min((int64_t)a.ur.cnt[qreg * kRegStride], a.ur.cap);
-        }
-    };
-    while (true) {
-        if (threadIdx.x == 0) s_unit = grab();
-        __syncthreads();
-        const long long un = s_unit;
-        if (un < 0) break;  // block-uniform
-        Unit d = units[un];
-        d.np = (uint32_t)uni32((int)d.np);
-        d.slot = (uint32_t)uni32((int)d.slot);
-        d.n0 = (uint32_t)uni32((int)d.n0);
-        d.n1 = (uint32_t)uni32((int)d.n1);
-        d.w0 = (uint32_t)uni32((int)d.w0);
-        d.w1 = (uint32_t)uni32((int)d.w1);
-        const bool longu = (d.np & kUnitLong) != 0;
-        const uint32_t npall = d.np & ~kUnitLong;
-        // ---- this lane's posting (tile w)
-        const uint32_t pi = (uint32_t)(64 * w + lane);
-        const bool have = pi < npall;
-        longlong2 pt = make_longlong2(LLONG_MAX, LLONG_MIN);
-        float2 pa = make_float2(INFINITY, -INFINITY);
-        uint32_t pe = 0, pmeta = 0;
-        int32_t pown = 0;
-        ulonglong2 ps01 = make_ulonglong2(0, 0), ps23 = ps01;
-        const uint32_t nrec = (d.n1 > d.n0 ? d.n1 - d.n0 : 0u) + (d.w1 > d.w0 ? d.w1 - d.w0 : 0u);
-        const bool usig = nrec > a.lazy_sig_recs;
-        bool lsig = false;
-        if (have && nrec) {
-            const uint64_t p = d.p0 + pi;
-            pe = ix.b_e[p];
-            pmeta = ix.b_meta[p];
-            pt = ix.b_t[p];
-            pa = ix.b_alt[p];
-            if (usig) {
-                ps01 = ix.b_sig[2 * p];
-                ps23 = ix.b_sig[2 * p + 1];
-            }
-            if (OWNER) pown = ix.b_owner[p];
-        }
-        const bool pv = have && nrec && !is_dead(ix, pe & ~kFirstBit);
-        const unsigned long long vmask = __ballot(pv);
-        const uint32_t pent = pe & ~kFirstBit;
-        // group time hull (a regular group is sorted by m = min(t0, t1))
-        long long t0min = LLONG_MIN, t1max = LLONG_MAX;
-        if (!longu && nrec) {
-            const longlong2 f = ix.b_t[d.p0];
-            t0min = tmin2(f.x, f.y);
-            const long long wm = wave_max_i64(have ? (pt.x > pt.y ? pt.x : pt.y) : LLONG_MIN);
-            if (lane == 0) s_hull[w] = wm;
-            __syncthreads();
-            t1max = s_hull[0];
-#pragma unroll
-            for (int k = 1; k < kWaves; k++) t1max = max(t1max, s_hull[k]);
-        }
-        const bool pfirst = (pe & kFirstBit) != 0;
-        const bool pcompact = (pmeta & kMetaCompact) != 0;
-        const bool plong = LONG && (pmeta & kMetaLongFp) != 0;
-        for (int part = 0; part < 2; part++) {
-            const uint32_t x0 = part ? d.w0 : d.n0, x1 = part ? d.w1 : d.n1;
-            for (uint32_t base = x0; base < x1; base += kBlkRecs) {
-                // ---- stage: one record per thread, hull test, block compaction
-                const uint32_t r = base + threadIdx.x;
-                bool rel = false;
-                int4 h0 = make_int4(0, 0, 0, 0), h1 = h0;
-                const int4 *r4 = nullptr;
-                if (r < x1) {
-                    r4 = reinterpret_cast<const int4 *>(recs + sval[r]);
-                    h0 = r4[0];
-                    h1 = r4[1];
-                    const long long tlo = ((long long)h0.y << 32) | (uint32_t)h0.x;
-                    const long long thi = ((long long)h0.w << 32) | (uint32_t)h0.z;
-                    rel = t1max >= tlo && t0min <= thi;
-                }
-                const unsigned long long relm = __ballot(rel);
-                if (lane == 0) s_wc[w] = (uint32_t)__popcll(relm);
-                __syncthreads();
-                uint32_t pre = 0, nrel = 0;
-#pragma unroll
-                for (int k = 0; k < kWaves; k++) {
-                    const uint32_t c = s_wc[k];
-                    pre += k < w ? c : 0u;
-                    nrel += c;
-                }
-                nrel = (uint32_t)uni32((int)nrel);
-                if (rel) {
-                    const uint32_t slot = pre + mbcnt64(relm);
-                    s_rt[slot] = make_longlong2(((long long)h0.y << 32) | (uint32_t)h0.x,
-                                                ((long long)h0.w << 32) | (uint32_t)h0.z);
-                    s_ra[slot] = make_float4(__int_as_float(h1.x), __int_as_float(h1.y), __int_as_float(h1.z),
-                                             __int_as_float(h1.w));
-                    s_rs[0][slot] = reinterpret_cast<const ulonglong2 *>(r4)[2];
-                    s_rs[1][slot] = reinterpret_cast<const ulonglong2 *>(r4)[3];
-                }
-                __syncthreads();
-                // ---- this wave's tile against the staged records, 64 at a time
-                for (uint32_t sb = 0; vmask && sb < nrel; sb += 64) {
-                    const int nb = (int)min(64u, nrel - sb);
-                    const longlong2 *rt_ = s_rt + sb;
-                    const float4 *ra_ = s_ra + sb;
-                    const ulonglong2 *rs0 = s_rs[0] + sb, *rs1 = s_rs[1] + sb;
-                    const uint32_t qslot = lane < nb ? (uint32_t)__float_as_int(ra_[lane].z) : 0u;
-                    const unsigned long long R0 = __ballot((qslot & kRank0) != 0);
-                    const unsigned long long RC = __ballot((qslot & kCompactQ) != 0);
-                    const unsigned long long RL = LONG ? __ballot((qslot & kLongQ) != 0) : 0ull;
-                    n_bcast += (unsigned long long)nb;
-                    n_tests += (unsigned long long)nb * (unsigned long long)__popcll(vmask);
-                    uint32_t mlo = 0, mhi = 0;
-                    const int nlo = nb < 32 ? nb : 32;
-#pragma unroll 4
-                    for (int j = 0; j < nlo; j++) {
-                        const longlong2 rt = rt_[j];
-                        const float4 ra = ra_[j];
-                        bool pass = (pt.y >= rt.x) & (pt.x <= rt.y) & (pa.y >= ra.x) & (pa.x <= ra.y);
-                        if (OWNER) {
-                            const int32_t own = __float_as_int(ra.w);
-                            pass &= (own < 0) | (pown == own);
-                        }
-                        mlo |= (uint32_t)pass << j;
-                    }
-#pragma unroll 4
-                    for (int j = 32; j < nb; j++) {
-                        const longlong2 rt = rt_[j];
-                        const float4 ra = ra_[j];
-                        bool pass = (pt.y >= rt.x) & (pt.x <= rt.y) & (pa.y >= ra.x) & (pa.x <= ra.y);
-                        if (OWNER) {
-                            const int32_t own = __float_as_int(ra.w);
-                            pass &= (own < 0) | (pown == own);
-                        }
-                        mhi |= (uint32_t)pass << (j - 32);
-                    }
-                    const unsigned long long m = pv ? (((unsigned long long)mhi << 32) | mlo) : 0ull;
-                    if (!__ballot(m != 0ull)) continue;
-                    unsigned long long keep = pfirst ? m : (m & R0);
-                    unsigned long long need = m & ~keep;
-                    if (!usig) {
-                        const bool want = need != 0ull && !lsig;
-                        if (__ballot(want)) {
-                            if (want) {
-                                const uint64_t p = d.p0 + pi;
-                                ps01 = ix.b_sig[2 * p];
-                                ps23 = ix.b_sig[2 * p + 1];
-                                lsig = true;
-                            }
-                        }
-                    }
-                    while (need) {
-                        const int j = __builtin_ctzll(need);
-                        need &= need - 1;
-                        const ulonglong2 c0 = rs0[j], c1 = rs1[j];
-                        if (((c0.x & ps01.x) | (c0.y & ps01.y) | (c1.x & ps23.x) | (c1.y & ps23.y)) != 0ull) continue;
-                        bool k = !LONG || pcompact || ((RC >> j) & 1ull) || (plong && ((RL >> j) & 1ull));
-                        if (LONG && !k) {
-                            const uint32_t q = (uint32_t)__float_as_int(ra_[j].z) & ~kQFlags;
-                            k = no_smaller_shared<2>(ix, pent, cell_of_slot(ix, d.slot), a.qv.cells + a.qv.offs[q],
-                                                     a.qv.offs[q + 1] - a.qv.offs[q]);
-                        }
-                        if (k) keep |= 1ull << j;
-                    }
-                    const unsigned long long tagm = (LONG && plong) ? (keep & RL) : 0ull;
-                    const uint32_t cu = (uint32_t)__popcll(keep & ~tagm), ct = (uint32_t)__popcll(tagm);
-                    const uint32_t incl = wave_incl_scan(cu | (ct << 16));
-                    const uint32_t tot = (uint32_t)uni32(__builtin_amdgcn_readlane((int)incl, 63));
-                    const int total_u = (int)(tot & 0xffffu), total_t = LONG ? (int)(tot >> 16) : 0;
-                    if (!(total_u | total_t)) continue;
-                    WaveOut::Span su{}, st{};
-                    if (total_u) su = out.reserve(a.out.ps, total_u);
-                    if (LONG && total_t) st = tout.reserve(a.out.ts, total_t);
-                    const bool wu = out.have != 0, wt = LONG && tout.have != 0;
-                    if ((int64_t)(total_u + total_t) * kEmitDensity <= (int64_t)nb * __popcll(vmask)) {
-                        if (!LONG && kOutStage && wu && total_u <= kOutStage) {
-                            uint32_t iu = (incl & 0xffffu) - cu;
-                            unsigned long long kk = keep & ~tagm;
-                            while (kk) {
-                                const int j = __builtin_ctzll(kk);
-                                kk &= kk - 1;
-                                s_out[w][iu++] = make_uint2((uint32_t)__float_as_int(ra_[j].z) & ~kQFlags, pent);
-                            }
-                            __builtin_amdgcn_wave_barrier();
-                            for (int p = lane; p < total_u; p += 64) {
-                                const uint2 v = s_out[w][p];
-                                const unsigned long long pos = su.at((unsigned long long)p);
-                                a.out.q[pos] = v.x;
-                                a.out.e[pos] = v.y;
-                            }
-                            __builtin_amdgcn_wave_barrier();
-                        } else if (wu) {
-                            unsigned long long iu = (incl & 0xffffu) - cu, kk = keep & ~tagm;
-                            while (kk) {
-                                const int j = __builtin_ctzll(kk);
-                                kk &= kk - 1;
-                                const uint32_t q = (uint32_t)__float_as_int(ra_[j].z) & ~kQFlags;
-                                const unsigned long long pos = su.at(iu++);
-                                a.out.q[pos] = q;
-                                a.out.e[pos] = pent;
-                            }
-                        }
-                        if (LONG && wt) {
-                            unsigned long long it = (incl >> 16) - ct, kk = tagm;
-                            while (kk) {
-                                const int j = __builtin_ctzll(kk);
-                                kk &= kk - 1;
-                                const uint32_t q = (uint32_t)__float_as_int(ra_[j].z) & ~kQFlags;
-                                a.out.tk[st.at(it++)] = tag_key(q, pent, a.out.eb, a.out.hbm);
-                            }
-                        }
-                    } else {
-                        const unsigned long long lm = LONG ? __ballot(plong) : 0ull;
-                        unsigned long long ou = 0, ot = 0;
-                        for (int j = 0; j < nb; j++) {
-                            const unsigned long long kj = __ballot((keep >> j) & 1ull);
-                            if (!kj) continue;
-                            const unsigned long long kt = (LONG && ((RL >> j) & 1ull)) ? (kj & lm) : 0ull, ku = kj & ~kt;
-                            const uint32_t q = (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(ra_[j].z)) & ~kQFlags;
-                            if ((ku >> lane) & 1ull) {
-                                const unsigned long long pos = su.at(ou + mbcnt64(ku));
-                                if (wu) {
-                                    a.out.q[pos] = q;
-                                    a.out.e[pos] = pent;
-                                }
-                            }
-                            if (LONG && ((kt >> lane) & 1ull)) {
-                                const unsigned long long pos = st.at(ot + mbcnt64(kt));
-                                if (wt) a.out.tk[pos] = tag_key(q, pent, a.out.eb, a.out.hbm);
-                            }
-                            ou += (unsigned long long)__popcll(ku);
-                            ot += (unsigned long long)__popcll(kt);
-                        }
-                    }
-                }
-                __syncthreads();  // the next batch overwrites the staged records
-            }
-        }
-        __syncthreads();  // s_unit / s_hull are rewritten for the next unit
-    }
-    out.finish(a.out.ps, &a.out.counter[0]);
-    if (LONG) tout.finish(a.out.ts, &a.out.counter[1]);
-    if (lane == 0) {
-        atomicAdd(&a.out.counter[2], n_tests);
-        atomicAdd(&a.out.counter[3], n_bcast);
-    }
-}
-
 // Closing the output holes: chunk c holds fills[c] pairs at c * kOutChunk
 // (0 = never reserved); with n pairs in all, the holes below n are filled
 // with the pairs at or above n, in order.  k_fix_counts: per chunk its holes
@@ -2435,7 +2153,6 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         DSS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
         n_cu_ = ncu > 0 ? ncu : 256;
     }
-    const int tiles = join_tiles_ == kBlkTiles ? kBlkTiles : 1;  // 64-posting tiles per unit (k_join_blk: one per wave)
     int64_t ucap = std::max<int64_t>(units_cap_hint_, 1024);  // per region
     Unit *units = nullptr;
     const unsigned ugrid = (unsigned)std::min<int64_t>((nqc + 63) / 64 / (kBlock / 64) + 1, (int64_t)n_cu_ * 16);
@@ -2443,7 +2160,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         units = (Unit *)units_buf_.ensure(sizeof(Unit) * (kRegions * ucap + 1));
         DSS_HIP(hipMemsetAsync(ctl + kCtlUnits, 0, kR * sizeof(unsigned long long), s));
         hipLaunchKernelGGL(k_units, dim3(ugrid), dim3(kBlock), 0, s, ix, skey, dnkeys, Regions{ctl + kCtlUnits, ucap},
-                           units, (uint32_t)(64 * tiles));
+                           units, 64u);
         hipLaunchKernelGGL(k_unit_ranges, dim3((unsigned)n_cu_ * 8), dim3(kBlock), 0, s, ix,
                            Regions{ctl + kCtlUnits, ucap}, units, (const uint32_t *)sval, (const QRec *)recs,
                            (const unsigned long long *)(ctl + kCtlDq), (long long)idx->tbase, idx->qshift);
@@ -2492,10 +2209,8 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         ja.out = OutArgs{oq, oe, OutStream{out_rcap_, fills, ctl + kCtlOut}, tk, OutStream{tag_rcap_, tfills, ctl + kCtlTOut},
                          eb, hbm, cnt};
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
-        auto kern = tiles > 1 ? (q_owner ? (any_long ? k_join_blk<true, true> : k_join_blk<true, false>)
-                                         : (any_long ? k_join_blk<false, true> : k_join_blk<false, false>))
-                              : (q_owner ? (any_long ? k_join<true, true> : k_join<true, false>)
-                                         : (any_long ? k_join<false, true> : k_join<false, false>));
+        auto kern = q_owner ? (any_long ? k_join<true, true> : k_join<true, false>)
+                            : (any_long ? k_join<false, true> : k_join<false, false>);
         hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs, (const uint32_t *)sval,
                            (const Unit *)units, ctl + kCtlQueue);
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));

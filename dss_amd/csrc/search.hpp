@@ -116,16 +116,12 @@ class SearchEngine {
     // batches of at most this many queries (and 16x as many cells) take the
     // one-launch small path (k_small_join); 0: never
     void set_small_max_q(int64_t v) { small_max_q_ = v; }
-    // 64-posting tiles per join unit: 1 = k_join (a wave per tile), 4 =
-    // k_join_blk (a workgroup per 4 tiles of one cell, records staged once)
-    void set_join_tiles(int64_t v) { join_tiles_ = (int)v; }
 
    private:
     void search_small(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
                       const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
                       const int32_t *q_owner, int64_t nqc, hipStream_t s, dssg_pairs *out);
     int64_t small_max_q_ = 4096, small_cap_ = 0;
-    int join_tiles_ = 1;
     DevBuf<unsigned long long> small_cnt_;
     DevBuf<unsigned char> tmp_, tmp2_;
     // query side

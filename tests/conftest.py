@@ -31,22 +31,15 @@ def golden_search():
     return dict(np.load(os.path.join(ROOT, "tests", "golden", "search.npz"), allow_pickle=False))
 
 
-@pytest.fixture(params=["units", "block", "small"])
+@pytest.fixture(params=["units", "small"])
 def join_path(request):
-    """Run a search test through every join of the shared context: "units"
-    (the tiled band join, a wave per 64-posting tile: k_join), "block" (a
-    workgroup per 4 tiles of a cell: k_join_blk) -- both with small_search =
-    0 -- and "small" (the one-launch small-batch join, k_small_join, forced
-    for every batch)."""
+    """Run a search test through both joins of the shared context: "units"
+    (the tiled band join, k_join; small_search = 0) and "small" (the
+    one-launch small-batch join, k_small_join, forced for every batch)."""
     from dss_amd import _lib
     ctx = _lib.context(0)
-    ctx.set_tuning("small_search", 1 << 24 if request.param == "small" else 0)
-    ctx.set_tuning("join_tiles", 4 if request.param == "block" else 1)
+    ctx.set_tuning("small_search", 0 if request.param == "units" else 1 << 24)
     try:
         yield request.param
     finally:
         ctx.set_tuning("small_search", 4096)
-        ctx.set_tuning("join_tiles", JOIN_TILES_DEFAULT)
-
-
-JOIN_TILES_DEFAULT = 1  # the library's default (search.hpp join_tiles_)

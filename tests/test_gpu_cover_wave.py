@@ -15,13 +15,17 @@ pytestmark = pytest.mark.gpu
 def _both_paths(fp):
     from dss_amd import _lib, geo
     ctx = _lib.context(0)
-    wave = geo.cover_batch(fp.kind, fp.voff, fp.lat, fp.lng, fp.radius_m)
-    ctx.set_tuning("cover_wave", 0)
+    ctx.set_tuning("cover_wave", 1 << 40)  # every batch through the wave path
     try:
+        wave = geo.cover_batch(fp.kind, fp.voff, fp.lat, fp.lng, fp.radius_m)
+        ctx.set_tuning("cover_wave", 0)
         gen = geo.cover_batch(fp.kind, fp.voff, fp.lat, fp.lng, fp.radius_m)
     finally:
-        ctx.set_tuning("cover_wave", 1)
+        ctx.set_tuning("cover_wave", COVER_WAVE_DEFAULT)
     return wave, gen
+
+
+COVER_WAVE_DEFAULT = 16384  # CoverEngine::wave_max_
 
 
 def _same(a, b):

@@ -22,9 +22,15 @@ cut -c1-400 $O/gloo2.json
 timeout -k 10 300 python -u bench.py --mode sharded --exchange native --scale 0.1 --steps 5 --warmup 1 > $O/native1.json 2> $O/native1.err || { echo NATIVE1_FAILED; tail -30 $O/native1.err; exit 1; }
 cut -c1-400 $O/native1.json
 echo done
+if [ -n "$AB" ]; then
+for c in 1 2; do
+timeout -k 10 300 python -u bench.py --config $c --steps 20 --warmup 3 --cpu-sample 0 --latency 0 --survey-model 0 $ABARGS > $O/ab_c${c}.json 2> $O/ab_c${c}.err || { echo AB_FAILED c$c; tail -20 $O/ab_c${c}.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/ab_c${c}.json'));print('AB c$c', round(d['value']/1e6,1), 'Mq/s', d['phase_ms'], round(d['roofline']['frac'],3), round(d['cover_roofline']['frac'],3))"
+done
+fi
 if [ -n "$PROF" ]; then
-KT_ONLY=1 STEPS=4 BENCH_ARGS="--config 2" NI=10000000 bash tools/profile.sh ${TAG}_c2 > $O/prof_c2.log 2>&1 || { echo PROF_C2_FAILED; tail -20 $O/prof_c2.log; exit 1; }
-head -25 gpurun_out/prof/${TAG}_c2/summary.csv | cut -c1-120
+STEPS=4 BENCH_ARGS="--config 2" NI=10000000 bash tools/profile.sh ${TAG}_c2 > $O/prof_c2.log 2>&1 || { echo PROF_C2_FAILED; tail -20 $O/prof_c2.log; exit 1; }
+head -25 gpurun_out/prof/${TAG}_c2/summary.csv | cut -c1-160
 KT_ONLY=1 STEPS=4 BENCH_ARGS="--config 1" NI=1000000 bash tools/profile.sh ${TAG}_c1 > $O/prof_c1.log 2>&1 || { echo PROF_C1_FAILED; tail -20 $O/prof_c1.log; exit 1; }
 head -25 gpurun_out/prof/${TAG}_c1/summary.csv | cut -c1-120
 fi
