@@ -1218,6 +1218,11 @@ struct dssg_batcher {
     int busy = 0;
     int64_t n_requests = 0, n_batches = 0;
     std::vector<Worker *> workers;
+    // DSSG_BATCHER_PROFILE=1: mean host time per batch of the cover, join and
+    // copy-back phases, printed to stderr when the batcher is freed
+    bool prof = false;
+    double prof_us[3] = {0, 0, 0};
+    int64_t prof_n = 0;
     // answers a caller could not take (DSSG_ERR_CAPACITY): kept for its retry
     std::mutex cache_mu;
     std::deque<std::pair<uint64_t, std::pair<double, std::vector<uint32_t>>>> cache;
@@ -1273,23 +1278,49 @@ struct dssg_batcher {
             unsigned char *d = w.d_in.ensure(in_bytes + 8);
             DSS_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s));
             dssg_cells cov;
+            const auto t0 = std::chrono::steady_clock::now();
             w.ctx->cover.run(n, (const int32_t *)(d + o_kind), (const int64_t *)(d + o_voff), (const double *)(d + o_lat),
                              (const double *)(d + o_lng), (const float *)(d + o_rad), s, &cov);
-            dssg_pairs res{};
-            if (cov.total_cells > 0)
-                w.ctx->search.search(idx, n, cov.offs, cov.cells, (const float *)(d + o_alo), (const float *)(d + o_ahi),
-                                     (const int64_t *)(d + o_tlo), (const int64_t *)(d + o_thi), nullptr, s, &res);
-            npairs = res.n;
-            const size_t r_area = 0, r_stat = 8 * n, r_q = al8(r_stat + 4 * n), r_e = r_q + 4 * npairs,
-                         out_bytes = r_e + 4 * npairs;
-            pinned(w.h_out, w.out_cap, out_bytes + 8);
+            // status and area ride along with the pairs' copy (pinned, no extra sync)
+            const size_t r_area = 0, r_stat = 8 * n, r_q = al8(r_stat + 4 * n);
+            pinned(w.h_out, w.out_cap, r_q + 8);
             DSS_HIP(hipMemcpyAsync(w.h_out + r_area, cov.area_km2, 8 * n, hipMemcpyDeviceToHost, s));
             DSS_HIP(hipMemcpyAsync(w.h_out + r_stat, cov.status, 4 * n, hipMemcpyDeviceToHost, s));
+            const auto t1 = std::chrono::steady_clock::now();
+            dssg_pairs res{};
+            const float *dlo = (const float *)(d + o_alo), *dhi = (const float *)(d + o_ahi);
+            const int64_t *dtl = (const int64_t *)(d + o_tlo), *dth = (const int64_t *)(d + o_thi);
+            if (cov.total_cells > 0) {
+                if (n <= w.ctx->search.small_max_q() && cov.total_cells <= 16 * w.ctx->search.small_max_q() &&
+                    idx->n_p > 0)  // the cell count is known here: the small join without a fetch
+                    w.ctx->search.search_small(idx, n, cov.offs, cov.cells, dlo, dhi, dtl, dth, nullptr,
+                                               cov.total_cells, s, &res);
+                else
+                    w.ctx->search.search(idx, n, cov.offs, cov.cells, dlo, dhi, dtl, dth, nullptr, s, &res);
+            }
+            npairs = res.n;
+            const auto t2 = std::chrono::steady_clock::now();
+            const size_t r_e = r_q + 4 * npairs, out_bytes = r_e + 4 * npairs;
+            if (out_bytes + 8 > w.out_cap) {  // regrow: the status/area copies must land first
+                DSS_HIP(hipStreamSynchronize(s));
+                std::vector<unsigned char> keep(w.h_out, w.h_out + r_q);
+                pinned(w.h_out, w.out_cap, out_bytes + 8);
+                std::memcpy(w.h_out, keep.data(), r_q);
+            }
             if (npairs > 0) {
                 DSS_HIP(hipMemcpyAsync(w.h_out + r_q, res.q, 4 * npairs, hipMemcpyDeviceToHost, s));
                 DSS_HIP(hipMemcpyAsync(w.h_out + r_e, res.e, 4 * npairs, hipMemcpyDeviceToHost, s));
             }
             DSS_HIP(hipStreamSynchronize(s));
+            const auto t3 = std::chrono::steady_clock::now();
+            if (prof) {
+                auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+                std::lock_guard<std::mutex> lk(mu);
+                prof_us[0] += us(t0, t1);
+                prof_us[1] += us(t1, t2);
+                prof_us[2] += us(t2, t3);
+                prof_n++;
+            }
             // each request's ids (unsorted here; the caller sorts its own)
             const uint32_t *pq = (const uint32_t *)(w.h_out + r_q), *pe = (const uint32_t *)(w.h_out + r_e);
             w.cnt.assign((size_t)n, 0);
@@ -1383,6 +1414,7 @@ int dssg_batcher_create(int device, const dssg_index *idx, int32_t max_batch, in
     b->idx = idx;
     b->max_batch = max_batch;
     b->max_wait_us = max_wait_us;
+    b->prof = std::getenv("DSSG_BATCHER_PROFILE") != nullptr;
     for (int k = 0; k < nw; k++) {
         auto *w = new dssg_batcher::Worker();
         const int rc = dssg_create(device, &w->ctx);
@@ -1407,6 +1439,10 @@ void dssg_batcher_free(dssg_batcher *b)
         b->stop = true;
     }
     b->cv.notify_all();
+    if (b->prof && b->prof_n)
+        fprintf(stderr, "[dssg_batcher] %lld batches, %lld requests; mean us per batch: cover %.1f join %.1f copy %.1f\n",
+                (long long)b->prof_n, (long long)b->n_requests, b->prof_us[0] / b->prof_n, b->prof_us[1] / b->prof_n,
+                b->prof_us[2] / b->prof_n);
     for (auto *w : b->workers) {
         if (w->th.joinable()) w->th.join();
         if (w->ctx) {

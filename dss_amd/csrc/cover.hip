@@ -1699,6 +1699,42 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     uint8_t *slow = w_slow_.ensure(n + 1);
     hipLaunchKernelGGL(k_cover_wave, dim3(grid_for(n, kWaveFp)), dim3(64 * kWaveFp), 0, s, n, kind, voff, lat, lng,
                        radius_m, status, area, cnt, rec, slow);
+    // counts and slow flags to the host (the batch is small): offsets and
+    // total there, one sync; only a batch with slow footprints takes the
+    // device compaction and the general pipeline below
+    h_cnt_.resize((size_t)n);
+    h_slow_.resize((size_t)n);
+    DSS_HIP(hipMemcpyAsync(h_cnt_.data(), cnt, sizeof(int64_t) * (size_t)n, hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipMemcpyAsync(h_slow_.data(), slow, (size_t)n, hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
+    bool any_slow = false;
+    for (int64_t i = 0; i < n && !any_slow; i++) any_slow = h_slow_[i] != 0;
+    if (!any_slow) {
+        last_slow_ = 0;
+        // pinned staging of the offsets; its previous upload (maybe on
+        // another stream) has finished once h_ev_ has
+        if (h_ev_) DSS_HIP(hipEventSynchronize(h_ev_));
+        else DSS_HIP(hipEventCreateWithFlags(&h_ev_, hipEventDisableTiming));
+        if (h_offs_cap_ < n + 1) {
+            if (h_offs_) DSS_HIP(hipHostFree(h_offs_));
+            h_offs_cap_ = std::max<int64_t>(2 * (n + 1), 4096);
+            DSS_HIP(hipHostMalloc((void **)&h_offs_, sizeof(int64_t) * (size_t)h_offs_cap_, hipHostMallocDefault));
+        }
+        h_offs_[0] = 0;
+        for (int64_t i = 0; i < n; i++) h_offs_[i + 1] = h_offs_[i] + h_cnt_[i];
+        const int64_t total = h_offs_[n];
+        DSS_HIP(hipMemcpyAsync(offs, h_offs_, sizeof(int64_t) * (size_t)(n + 1), hipMemcpyHostToDevice, s));
+        DSS_HIP(hipEventRecord(h_ev_, s));
+        uint64_t *cells = w_cells_.ensure(total + 1);
+        hipLaunchKernelGGL(k_emit_wave, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, n, slow, rec, offs, cells);
+        out->n = n;
+        out->offs = offs;
+        out->cells = cells;
+        out->status = status;
+        out->area_km2 = area;
+        out->total_cells = total;
+        return;
+    }
     // the footprints the wave path left: one sub-batch through the general pipeline
     uint32_t *list = s_list_.ensure(n + 1);
     int64_t ns = 0;

@@ -1,5 +1,7 @@
 // Host-side driver of the covering kernels (cover.hip).
 #pragma once
+#include <vector>
+
 #include "common.hpp"
 
 namespace dss {
@@ -20,6 +22,14 @@ struct Frontier {
 
 class CoverEngine {
    public:
+    CoverEngine() = default;
+    CoverEngine(const CoverEngine &) = delete;
+    CoverEngine &operator=(const CoverEngine &) = delete;
+    ~CoverEngine()
+    {
+        if (h_offs_) (void)hipHostFree(h_offs_);
+        if (h_ev_) (void)hipEventDestroy(h_ev_);
+    }
     // Device pointers in, context-owned device buffers out (see dssg_cells).
     // The wave path (one wavefront per footprint) covers every footprint it
     // can decide; the rest go through the general pipeline (run_general) as
@@ -47,6 +57,10 @@ class CoverEngine {
     DevBuf<uint32_t> s_list_;
     DevBuf<float> s_rad_;
     DevBuf<uint64_t> w_cells_;
+    std::vector<int64_t> h_cnt_;
+    int64_t *h_offs_ = nullptr, h_offs_cap_ = 0;  // pinned
+    hipEvent_t h_ev_ = nullptr;                   // the last upload from h_offs_
+    std::vector<uint8_t> h_slow_;
     DevBuf<int64_t> cnt_, xoff_, eoff_, soff_, offs_, ncnt_, npos_, fc64_;
     DevBuf<int32_t> status_, nvx_;
     DevBuf<double> area_, xyz_;

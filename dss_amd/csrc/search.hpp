@@ -117,10 +117,14 @@ class SearchEngine {
     // one-launch small path (k_small_join); 0: never
     void set_small_max_q(int64_t v) { small_max_q_ = v; }
 
-   private:
+    // The one-launch small-batch join (k_small_join) with the batch's cell
+    // count nqc known to the caller (no fetch of q_offs[nq]).
     void search_small(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
                       const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
                       const int32_t *q_owner, int64_t nqc, hipStream_t s, dssg_pairs *out);
+    int64_t small_max_q() const { return small_max_q_; }
+
+   private:
     int64_t small_max_q_ = 4096, small_cap_ = 0;
     DevBuf<unsigned long long> small_cnt_;
     DevBuf<unsigned char> tmp_, tmp2_;
