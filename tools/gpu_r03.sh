@@ -28,6 +28,13 @@ timeout -k 10 300 python -u bench.py --config $c --steps 20 --warmup 3 --cpu-sam
 python3 -c "import json;d=json.load(open('$O/ab_c${c}.json'));print('AB c$c', round(d['value']/1e6,1), 'Mq/s', d['phase_ms'], round(d['roofline']['frac'],3), round(d['cover_roofline']['frac'],3))"
 done
 fi
+if [ -n "$LAT" ]; then
+for w in 2 4; do
+DSSG_BATCHER_WORKERS=$w DSSG_BATCHER_PROFILE=1 timeout -k 10 300 python -u bench.py --config 1 --steps 3 --warmup 1 --cpu-sample 0 --survey-model 0 > $O/lat_w$w.json 2> $O/lat_w$w.err || { echo LAT_FAILED w$w; tail -20 $O/lat_w$w.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/lat_w$w.json'));r=d['request_latency'];print('LAT w$w', json.dumps({k:{kk:round(vv,3) for kk,vv in v.items() if isinstance(vv,float)} for k,v in r.items() if isinstance(v,dict)}))"
+grep "dssg_batcher" $O/lat_w$w.err | tail -2
+done
+fi
 if [ -n "$PROF" ]; then
 STEPS=4 BENCH_ARGS="--config 2" NI=10000000 bash tools/profile.sh ${TAG}_c2 > $O/prof_c2.log 2>&1 || { echo PROF_C2_FAILED; tail -20 $O/prof_c2.log; exit 1; }
 head -25 gpurun_out/prof/${TAG}_c2/summary.csv | cut -c1-160
