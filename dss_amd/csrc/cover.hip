@@ -25,6 +25,9 @@
 // Roofline: FP64 VALU (edge clip / crossing tests); see DESIGN.md.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.hpp"
 #include "compact.cuh"
 #include "cover.hpp"
@@ -1866,6 +1869,9 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     DSS_HIP(hipMemcpyAsync(&h2[1], coff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
     const int64_t ne = h2[0], NC = h2[1];
+    if (std::getenv("DSS_COVER_STATS"))
+        fprintf(stderr, "[cover] n %lld vertices %lld candidates %lld clipped edges %lld\n", (long long)n, (long long)nx,
+                (long long)NC, (long long)ne);
     // direct candidates (most footprints): test now, compact after the counts
     uint32_t *cand_f = cand_f_.ensure(NC + 1);
     const int64_t G = (NC + 63) / 64;  // mask words; kept_rank(NC) reads word G

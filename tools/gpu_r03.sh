@@ -23,10 +23,15 @@ timeout -k 10 300 python -u bench.py --mode sharded --exchange native --scale 0.
 cut -c1-400 $O/native1.json
 echo done
 if [ -n "$AB" ]; then
+# variants: name=bench args (ABV="name1:args1;name2:args2")
+IFS=';' read -ra VS <<< "${ABV:-base:}"
+for v in "${VS[@]}"; do
+name=${v%%:*}; vargs=${v#*:}
 for c in 1 2; do
-timeout -k 10 300 python -u bench.py --config $c --steps 20 --warmup 3 --cpu-sample 0 --latency 0 --survey-model 0 $ABARGS > $O/ab_c${c}.json 2> $O/ab_c${c}.err || { echo AB_FAILED c$c; tail -20 $O/ab_c${c}.err; exit 1; }
-python3 -c "import json;d=json.load(open('$O/ab_c${c}.json'));print('AB c$c', round(d['value']/1e6,1), 'Mq/s', d['phase_ms'], round(d['roofline']['frac'],3), round(d['cover_roofline']['frac'],3))"
-done
+DSS_COVER_STATS=1 timeout -k 10 300 python -u bench.py --config $c --steps 20 --warmup 3 --cpu-sample 0 --latency 0 --survey-model 0 $vargs > $O/ab_${name}_c${c}.json 2> $O/ab_${name}_c${c}.err || { echo AB_FAILED $name c$c; tail -20 $O/ab_${name}_c${c}.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/ab_${name}_c${c}.json'));print('AB $name c$c', round(d['value']/1e6,1), 'Mq/s', {k:round(x,3) for k,x in d['phase_ms'].items()}, round(d['roofline']['frac'],3), round(d['cover_roofline']['frac'],3))"
+done; done
+grep -h "\[cover\]" $O/ab_*_c*.err | sort | uniq -c | sort -rn | head -6
 fi
 if [ -n "$LAT" ]; then
 for w in 2 4; do
