@@ -47,8 +47,7 @@ enum : uint8_t { FL_SMALL = 1, FL_PLANAR = 2, FL_FAST = 4 };
 // Direct candidate path: single-face small loops whose start block is at
 // level >= kFastMinLevel (<= 4 * 4^(13 - L) level-13 candidates).
 constexpr int kFastMinLevel = 10;
-constexpr int kCandBlock = 256;
-constexpr int kCandStageV = 1024;  // (u,v) vertices a k_cand_test_c block stages in LDS (16 KiB)
+constexpr int kCandStageV = 1024;  // (u,v) vertices a k_cand_fp block stages in LDS (16 KiB)
 // node meta: level (bits 0-4), orientation (5-6), done (7), face (8-10)
 __device__ __forceinline__ uint32_t pack_meta(int level, int orient, int done, int face)
 {
@@ -349,7 +348,7 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
                                           const float *radius_m, const int64_t *xoff, V3 *xyz, int32_t *status,
                                           double *area_out, uint8_t *mode, uint8_t *origin_in, uint8_t *fmask,
                                           uint8_t *flags, int32_t *nvx, double2 *uv, uint64_t *st_id, uint32_t *st_i,
-                                          uint32_t *st_j, uint32_t *finfo, int64_t *ncand, uint4 *fbox,
+                                          uint32_t *st_j, uint32_t *finfo, uint4 *fbox,
                                           const double *fwd, const double *rev, const uint8_t *fan_fail,
                                           const uint8_t *not_inner, const uint8_t *omode)
 {
@@ -489,13 +488,17 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
     mode[f] = md;
     origin_in[f] = l.origin_inside ? 1 : 0;
     fmask[f] = mask;
-    // bbox-limited start is valid for polylines (no interior) and for loops
-    // whose edges all lie inside one face and whose interior is the small side.
-    uint8_t fl = (md == MODE_POLYLINE || (md == MODE_LOOP && inner && small && __builtin_popcount(mask) == 1)) ? FL_SMALL : 0;
-    // Planar containment (see contains_node): a single-face small loop whose
-    // (u,v) bound does not come near OriginPoint's projection.
-    int64_t nc = 0;
-    if (md == MODE_LOOP && (fl & FL_SMALL)) {
+    // bbox-limited start (per touched face, the bound of the edges clipped to
+    // it) is valid for polylines (no interior) and for loops whose interior is
+    // the small side: a small loop's part of a face is bounded by its clipped
+    // edges and the face-boundary pieces between their clip points, which lie
+    // in those points' bound (a face corner inside the part included, since
+    // the part's boundary then reaches both face edges through it).
+    uint8_t fl = (md == MODE_POLYLINE || (md == MODE_LOOP && small)) ? FL_SMALL : 0;
+    // Planar containment (see contains_node) and direct candidates: a small
+    // loop inside one face whose (u,v) bound does not come near OriginPoint's
+    // projection.
+    if (md == MODE_LOOP && small && inner && __builtin_popcount(mask) == 1) {
         const int face0 = xyz_face(p[0]);
         double2 *uvp = uv + xoff[f];
         double ulo = 1e300, uhi = -1e300, vlo = 1e300, vhi = -1e300;
@@ -536,7 +539,6 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
                 info |= (uint32_t)meta_orient(mt[q]) << (8 + 2 * q);
             }
             finfo[f] = info;
-            nc = (int64_t)k << (2 * (kCoverLevel - L));
             // level-13 (i, j) range of the padded bound: candidates outside it
             // are > 1e-7 (uv) from every vertex, so neither touch an edge nor
             // lie inside this single-face loop
@@ -547,7 +549,6 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
                                  (uint32_t)(st_to_ij(uv_to_st(fmin(b.vhi, 1.0))) >> sh13));
         }
     }
-    ncand[f] = nc;
     flags[f] = fl;
     nvx[f] = nv;
 }
@@ -559,7 +560,7 @@ template <bool FAST>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAST ? DSS_SETUP_WPE : 1))) void k_setup(uint32_t *slow_list, unsigned int *slow_n, int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
                         const float *radius_m, const int64_t *xoff, V3 *xyz, int32_t *status, double *area_out,
                         uint8_t *mode, uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx, double2 *uv,
-                        uint64_t *st_id, uint32_t *st_i, uint32_t *st_j, uint32_t *finfo, int64_t *ncand,
+                        uint64_t *st_id, uint32_t *st_i, uint32_t *st_j, uint32_t *finfo,
                         uint4 *fbox, const double *fwd, const double *rev, const uint8_t *fan_fail,
                         const uint8_t *not_inner, const uint8_t *omode, const uint32_t *perm)
 {
@@ -570,12 +571,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAST ? DSS_S
     } else {  // a small grid strides over the footprints the triage left undecided
         for (int64_t i = f; i < (int64_t)*slow_n; i += (int64_t)gridDim.x * blockDim.x)
             setup_one<false>(slow_list[i], nullptr, nullptr, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out,
-                             mode, origin_in, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, ncand, fbox, nullptr,
+                             mode, origin_in, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, nullptr,
                              nullptr, nullptr, nullptr, nullptr);
         return;
     }
     setup_one<true>(f, slow_list, slow_n, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out, mode, origin_in,
-                    fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, ncand, fbox, fwd, rev, fan_fail, not_inner, omode);
+                    fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, fwd, rev, fan_fail, not_inner, omode);
 }
 
 __device__ __forceinline__ int num_edges(uint8_t md, int nv) { return md == MODE_LOOP ? nv : (md == MODE_POLYLINE ? nv - 1 : 0); }
@@ -905,44 +906,48 @@ __global__ void k_emit_big(const uint32_t *big, const uint32_t *nf, const uint64
 }
 
 // ---------------------------------------------------------------------------
-// Direct candidate path (FL_FAST footprints).  The level-13 descendants of a
-// footprint's <= 4 start cells, taken start cell by start cell in id order,
-// are consecutive ids, so enumerating them by index lists the footprint's
-// candidates sorted; each is tested exactly as k_expand_count tests a level-13
-// node, and an order-preserving scan compacts the survivors.
-// Candidate -> footprint, one block per 256 footprints: their candidate
-// offsets go to LDS, then the block's whole candidate range is written
-// coalesced, each candidate finding its footprint by binary search in LDS.
-__global__ __launch_bounds__(256) void k_cand_owner(int64_t n, const int64_t *coff, uint32_t *cand_f)
+// Direct candidate path (FL_FAST footprints: single-face small loops whose
+// padded bound lies in <= 4 start cells at level >= kFastMinLevel).  The
+// candidates are the level-13 cells of the footprint's padded (i, j) bound
+// (fbox; every one lies in a start cell), each tested exactly as
+// k_expand_count tests a level-13 node.  A candidate's key is its index among
+// the start cells' level-13 descendants in id order (start cell s, Hilbert
+// position inside it), so a footprint's verdicts are two 256-bit masks
+// (kept, undecided) whose bit order is the cell-id order of the output.
+constexpr int kFpBlock = 256;  // threads of a k_cand_fp block
+constexpr int kFpPer = 64;     // footprints per k_cand_fp block (one wave loads them)
+
+// Key of level-13 cell (i13, j13) of footprint f, or -1 outside its start
+// cells (cannot happen for a cell of the bound).
+__device__ __forceinline__ int rect_key(uint32_t i13, uint32_t j13, const uint32_t *sti, const uint32_t *stj,
+                                        uint32_t info)
 {
-    __shared__ int64_t sc[257];
-    const int64_t f0 = (int64_t)blockIdx.x * 256;
-    const int nf = (int)(n - f0 < 256 ? n - f0 : 256);
-    for (int i = threadIdx.x; i <= nf; i += 256) sc[i] = coff[f0 + i];
-    __syncthreads();
-    const int64_t c1 = sc[nf];
-    for (int64_t c = sc[0] + threadIdx.x; c < c1; c += 256) {
-        int lo = 0, hi = nf;  // sc[lo] <= c < sc[hi]
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (sc[mid] <= c) lo = mid;
-            else hi = mid;
-        }
-        cand_f[c] = (uint32_t)(f0 + lo);
+    const int L = (int)(info & 31u), k = (int)((info >> 5) & 7u), shL = kMaxLevel - L;
+    const uint32_t i30 = i13 << (kMaxLevel - kCoverLevel), j30 = j13 << (kMaxLevel - kCoverLevel);
+    int s = -1;
+    for (int q = 0; q < k; q++)  // (unsigned wrap: a start cell above the cell gives a huge difference)
+        if (((i30 - sti[q]) >> shL) == 0u && ((j30 - stj[q]) >> shL) == 0u) s = q;
+    if (s < 0) return -1;
+    int o = (int)((info >> (8 + 2 * s)) & 3u);
+    uint32_t pos = 0;
+    for (int l = L + 1; l <= kCoverLevel; l++) {
+        const int ib = (int)((i30 >> (kMaxLevel - l)) & 1u), jb = (int)((j30 >> (kMaxLevel - l)) & 1u);
+        const int p = ij_to_pos(o, (ib << 1) | jb);
+        pos = (pos << 2) | (uint32_t)p;
+        o ^= pos_to_orientation(p);
     }
+    return (s << (2 * (kCoverLevel - L))) | (int)pos;
 }
 
-// Level-13 (i, j) and id of candidate c of footprint f.
-__device__ __forceinline__ void cand_cell(int64_t c, uint32_t f, const int64_t *coff, const uint64_t *st_id,
-                                          const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, int &face,
-                                          uint32_t &i, uint32_t &j, uint64_t &id)
+// Level-30 (i, j) corner, face and id of candidate `key` of footprint f.
+__device__ __forceinline__ void key_cell(int key, uint32_t f, const uint64_t *st_id, const uint32_t *st_i,
+                                         const uint32_t *st_j, uint32_t info, int &face, uint32_t &i, uint32_t &j,
+                                         uint64_t &id)
 {
-    const int64_t d = c - coff[f];
-    const uint32_t info = finfo[f];
     const int L = (int)(info & 31u);
     const int sh = 2 * (kCoverLevel - L);
-    const int s = (int)(d >> sh);
-    const uint32_t r = (uint32_t)(d & ((1ll << sh) - 1));
+    const int s = key >> sh;
+    const uint32_t r = (uint32_t)key & ((1u << sh) - 1u);
     int o = (int)((info >> (8 + 2 * s)) & 3u);
     i = st_i[4 * f + s];
     j = st_j[4 * f + s];
@@ -960,131 +965,22 @@ __device__ __forceinline__ void cand_cell(int64_t c, uint32_t f, const int64_t *
     id = sid - lsb_for_level(L) + lsb13 + (uint64_t)r * (lsb13 << 1);  // cellid.go ChildBeginAtLevel + r steps
 }
 
-// Candidate c's verdict: 0 / 1, or 2 = undecided (centre containment needs
-// the exact S2 test, done by k_cand_exact so that this one stays
-// register-light).
-__device__ __forceinline__ int cand_decide(int64_t c, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
-                                           const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo,
-                                           const uint4 *fbox, const int64_t *xoff, const double2 *uv, const int32_t *nvx,
-                                           const uint8_t *origin_in, const uint8_t *flags)
+// loop.go IntersectsCell for a level-13 cell at level-30 corner (i, j): the
+// padded edge test (stop at the first hit) and, for planar footprints,
+// contains_node's ray cast from the centre on the same (u,v) edge images --
+// used only when no edge hits.  uc < a.x + (vc - a.y)(b.x - a.x)/(b.y - a.y),
+// multiplied through by (b.y - a.y): an edge that misses the padded cell
+// crosses v = vc at least half a cell (1.2e-4) from uc, so the rounding
+// (~1e-16 relative) cannot flip the comparison.  0 / 1, or 2 = undecided
+// (centre containment needs the exact S2 test: k_cand_exact).
+__device__ __forceinline__ int cand_edges_uv(uint32_t i, uint32_t j, const double2 *up, int nv, bool planar,
+                                             bool origin_in)
 {
-    constexpr int kVU = 4;
-    const uint32_t f = cand_f[c];
-    // the first vertex batch is loaded before the candidate's cell is known
-    // (speculatively: a candidate outside the bound discards it), so its
-    // round trip overlaps the start-cell loads of cand_cell
-    const int nv = nvx[f];
-    const double2 *up = uv + xoff[f];
-    double2 a = up[0];
-    double2 bb0[kVU];
-#pragma unroll
-    for (int u = 0; u < kVU; u++) bb0[u] = up[u + 1 < nv ? u + 1 : 0];
-    int face;
-    uint32_t i, j;
-    uint64_t id;
-    cand_cell(c, f, coff, st_id, st_i, st_j, finfo, face, i, j, id);
-    const uint4 bx = fbox[f];
-    const uint32_t i13 = i >> (kMaxLevel - kCoverLevel), j13 = j >> (kMaxLevel - kCoverLevel);
-    if (i13 < bx.x || i13 > bx.y || j13 < bx.z || j13 > bx.w) return 0;
-    const uint32_t size = 1u << (kMaxLevel - kCoverLevel);
-    const double ulo = st_to_uv((double)i / (double)kMaxSize), uhi = st_to_uv((double)(i + size) / (double)kMaxSize);
-    const double vlo = st_to_uv((double)j / (double)kMaxSize), vhi = st_to_uv((double)(j + size) / (double)kMaxSize);
-    // loop.go IntersectsCell: padded edge test, else centre containment.
-    // One pass over the edges does both: the padded test (stop at the first
-    // hit) and, for planar footprints, contains_node's ray cast from the
-    // centre on the same (u,v) edge images -- only used when no edge hits.
-    // uc < a.x + (vc - a.y)(b.x - a.x)/(b.y - a.y), multiplied through by
-    // (b.y - a.y): an edge that misses the padded cell crosses v = vc >= half
-    // a cell (1.2e-4) from uc, so the rounding (~1e-16 relative) cannot flip
-    // the comparison.
-    const double pm = kFinePad;
-    const bool planar = (flags[f] & FL_PLANAR) != 0;
-    const double half = 0.5 / (double)kMaxSize, sz = (double)size;
-    const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
-    bool in = false, par = false;
-    // vertices are loaded kVU at a time (independent loads in flight
-    // together), then the edges are tested in order; indices past the
-    // closing edge read vertex 0 (valid, unused)
-    for (int e0 = 0; e0 < nv && !in; e0 += kVU) {
-        double2 bb[kVU];
-#pragma unroll
-        for (int u = 0; u < kVU; u++) {
-            const int e = e0 + u + 1;
-            bb[u] = e0 == 0 ? bb0[u] : up[e < nv ? e : 0];
-        }
-#pragma unroll
-        for (int u = 0; u < kVU; u++) {
-            if (e0 + u >= nv) break;
-            const double2 b = bb[u];
-            if (edge_intersects_rect(a.x, a.y, b.x, b.y, ulo - pm, uhi + pm, vlo - pm, vhi + pm)) {
-                in = true;
-                break;
-            }
-            if ((a.y > vc) != (b.y > vc)) {
-                const double d = b.y - a.y;
-                const double lhs = (uc - a.x) * d, rhs = (vc - a.y) * (b.x - a.x);
-                if (d > 0 ? lhs < rhs : lhs > rhs) par = !par;
-            }
-            a = b;
-        }
-    }
-    return in ? 1 : planar ? (((origin_in[f] != 0) != par) ? 1 : 0) : 2;
-}
-
-// The edge / centre test of candidate c of footprint f at level-13 (i, j)
-// inside the footprint's bound (cand_decide past its bound check).
-__device__ __forceinline__ int cand_edges(uint32_t f, uint32_t i, uint32_t j, const int64_t *xoff, const double2 *uv,
-                                          const int32_t *nvx, const uint8_t *origin_in, const uint8_t *flags)
-{
-    constexpr int kVU = 4;
-    const int nv = nvx[f];
-    const double2 *up = uv + xoff[f];
     double2 a = up[0];
     const uint32_t size = 1u << (kMaxLevel - kCoverLevel);
     const double ulo = st_to_uv((double)i / (double)kMaxSize), uhi = st_to_uv((double)(i + size) / (double)kMaxSize);
     const double vlo = st_to_uv((double)j / (double)kMaxSize), vhi = st_to_uv((double)(j + size) / (double)kMaxSize);
     const double pm = kFinePad;
-    const bool planar = (flags[f] & FL_PLANAR) != 0;
-    const double half = 0.5 / (double)kMaxSize, sz = (double)size;
-    const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
-    bool in = false, par = false;
-    for (int e0 = 0; e0 < nv && !in; e0 += kVU) {
-        double2 bb[kVU];
-#pragma unroll
-        for (int u = 0; u < kVU; u++) {
-            const int e = e0 + u + 1;
-            bb[u] = up[e < nv ? e : 0];
-        }
-#pragma unroll
-        for (int u = 0; u < kVU; u++) {
-            if (e0 + u >= nv) break;
-            const double2 b = bb[u];
-            if (edge_intersects_rect(a.x, a.y, b.x, b.y, ulo - pm, uhi + pm, vlo - pm, vhi + pm)) {
-                in = true;
-                break;
-            }
-            if ((a.y > vc) != (b.y > vc)) {
-                const double d = b.y - a.y;
-                const double lhs = (uc - a.x) * d, rhs = (vc - a.y) * (b.x - a.x);
-                if (d > 0 ? lhs < rhs : lhs > rhs) par = !par;
-            }
-            a = b;
-        }
-    }
-    return in ? 1 : planar ? (((origin_in[f] != 0) != par) ? 1 : 0) : 2;
-}
-
-// cand_edges over vertices already at `up` (the block's LDS stage).
-__device__ __forceinline__ int cand_edges_at(uint32_t f, uint32_t i, uint32_t j, const double2 *up, const int32_t *nvx,
-                                             const uint8_t *origin_in, const uint8_t *flags)
-{
-    const int nv = nvx[f];
-    double2 a = up[0];
-    const uint32_t size = 1u << (kMaxLevel - kCoverLevel);
-    const double ulo = st_to_uv((double)i / (double)kMaxSize), uhi = st_to_uv((double)(i + size) / (double)kMaxSize);
-    const double vlo = st_to_uv((double)j / (double)kMaxSize), vhi = st_to_uv((double)(j + size) / (double)kMaxSize);
-    const double pm = kFinePad;
-    const bool planar = (flags[f] & FL_PLANAR) != 0;
     const double half = 0.5 / (double)kMaxSize, sz = (double)size;
     const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
     bool in = false, par = false;
@@ -1101,166 +997,188 @@ __device__ __forceinline__ int cand_edges_at(uint32_t f, uint32_t i, uint32_t j,
         }
         a = b;
     }
-    return in ? 1 : planar ? (((origin_in[f] != 0) != par) ? 1 : 0) : 2;
+    return in ? 1 : planar ? ((origin_in != par) ? 1 : 0) : 2;
 }
 
-// Verdicts leave as two ballot masks per wave of 64 candidates (kept, and
-// undecided): 16 B per 64 candidates instead of a per-candidate word, and
-// the compaction below ranks by popcount, with no candidate-sized scan.
-// The block first tests its 256 candidates against their footprints' level-13
-// bounds, compacts the ones inside to its first threads (LDS), and only those
-// run the edge loop: the out-of-bound lanes no longer idle through it.
-__global__ __launch_bounds__(kCandBlock) void k_cand_test_c(int64_t NC, const uint32_t *cand_f, const int64_t *coff,
-                                                            const uint64_t *st_id, const uint32_t *st_i,
-                                                            const uint32_t *st_j, const uint32_t *finfo,
-                                                            const uint4 *fbox, const int64_t *xoff, const double2 *uv,
-                                                            const int32_t *nvx, const uint8_t *origin_in,
-                                                            const uint8_t *flags, unsigned long long *kmask,
-                                                            unsigned long long *umask, uint32_t *ulist,
-                                                            unsigned int *ulist_n)
+// One block per kFpPer consecutive footprints: wave 0 loads their bounds,
+// start cells and flags into LDS (one round trip for the block, none per
+// candidate), the block stages their (u,v) vertices, then its threads stride
+// over the block's bound cells (footprint by LDS search, cell by position in
+// its bound) and set key bits in the footprints' LDS masks.  Wave 0 writes the
+// kept masks, and lists the footprints with undecided bits for k_cand_exact.
+__global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *flags, const uint4 *fbox,
+                                                      const uint32_t *finfo, const uint32_t *st_i,
+                                                      const uint32_t *st_j, const int64_t *xoff, const int32_t *nvx,
+                                                      const double2 *uv, const uint8_t *origin_in,
+                                                      unsigned long long *fkm, unsigned long long *fum, uint32_t *ulist,
+                                                      unsigned int *ulist_n)
 {
-    __shared__ uint32_t s_lt[kCandBlock], s_ci[kCandBlock], s_cj[kCandBlock], s_f[kCandBlock];
-    __shared__ unsigned int s_n;
-    __shared__ unsigned long long s_k[kCandBlock / 64], s_u[kCandBlock / 64];
-    __shared__ double2 s_uv[kCandStageV];  // the block's footprints' (u,v) vertices, when they fit
+    __shared__ uint4 s_bx[kFpPer];
+    __shared__ uint32_t s_info[kFpPer], s_sti[kFpPer][4], s_stj[kFpPer][4];
+    __shared__ int s_cb[kFpPer + 1], s_vb[kFpPer], s_nv[kFpPer], s_fl[kFpPer];
+    __shared__ int64_t s_xo[kFpPer];
+    __shared__ unsigned long long s_km[kFpPer][4], s_um[kFpPer][4];
+    __shared__ double2 s_uv[kCandStageV];
     const int t = threadIdx.x, lane = t & 63;
-    const int64_t c0 = (int64_t)blockIdx.x * kCandBlock, c = c0 + t;
-    if (t == 0) s_n = 0;
-    if (t < kCandBlock / 64) s_k[t] = s_u[t] = 0;
-    // candidates are grouped by footprint: the block's footprints are
-    // [cand_f[c0], cand_f[last]], their vertices one contiguous range
-    const int64_t clast = min(c0 + kCandBlock, NC) - 1;
-    const uint32_t f_first = cand_f[c0], f_last = cand_f[clast];
-    const int64_t vb = xoff[f_first], ve = xoff[f_last] + nvx[f_last];
-    const bool staged = ve - vb <= kCandStageV;
-    if (staged)
-        for (int64_t v = vb + t; v < ve; v += kCandBlock) s_uv[v - vb] = uv[v];
-    __syncthreads();
-    bool inb = false;
-    uint32_t i = 0, j = 0, f = 0;
-    if (c < NC) {
-        f = cand_f[c];
-        int face;
-        uint64_t id;
-        cand_cell(c, f, coff, st_id, st_i, st_j, finfo, face, i, j, id);
-        const uint4 bx = fbox[f];
-        const uint32_t i13 = i >> (kMaxLevel - kCoverLevel), j13 = j >> (kMaxLevel - kCoverLevel);
-        inb = !(i13 < bx.x || i13 > bx.y || j13 < bx.z || j13 > bx.w);
-    }
-    const unsigned long long m = __ballot(inb);
-    unsigned int base = 0;
-    if (lane == 0 && m) base = atomicAdd(&s_n, (unsigned int)__popcll(m));
-    base = (unsigned int)__shfl((int)base, 0);
-    if (inb) {
-        const unsigned int p = base + (unsigned int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        s_lt[p] = (uint32_t)t;
-        s_ci[p] = i;
-        s_cj[p] = j;
-        s_f[p] = f;
-    }
-    __syncthreads();
-    if ((unsigned int)t < s_n) {
-        const uint32_t lt = s_lt[t];
-        const int v = staged ? cand_edges_at(s_f[t], s_ci[t], s_cj[t], s_uv + (xoff[s_f[t]] - vb), nvx, origin_in, flags)
-                             : cand_edges(s_f[t], s_ci[t], s_cj[t], xoff, uv, nvx, origin_in, flags);
-        if (v == 1) atomicOr(&s_k[lt >> 6], 1ull << (lt & 63));
-        else if (v == 2) atomicOr(&s_u[lt >> 6], 1ull << (lt & 63));
+    const int64_t F0 = (int64_t)blockIdx.x * kFpPer;
+    if (t < kFpPer) {
+        const int64_t f = F0 + t;
+        const bool fast = f < n && (flags[f] & FL_FAST);
+        uint32_t cnt = 0, nvv = 0;
+        if (fast) {
+            const uint4 bx = fbox[f];
+            s_bx[t] = bx;
+            s_info[t] = finfo[f];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                s_sti[t][q] = st_i[4 * f + q];
+                s_stj[t][q] = st_j[4 * f + q];
+            }
+            s_xo[t] = xoff[f];
+            nvv = (uint32_t)nvx[f];
+            s_fl[t] = ((flags[f] & FL_PLANAR) ? 1 : 0) | (origin_in[f] ? 2 : 0);
+            cnt = (bx.y - bx.x + 1) * (bx.w - bx.z + 1);
+        }
+        s_nv[t] = (int)nvv;
+#pragma unroll
+        for (int q = 0; q < 4; q++) s_km[t][q] = s_um[t][q] = 0ull;
+        // candidate and vertex prefixes over the block's footprints (wave scans)
+        uint32_t ci = cnt, vi = nvv;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t a = (uint32_t)__shfl_up((int)ci, o), b = (uint32_t)__shfl_up((int)vi, o);
+            if (lane >= o) {
+                ci += a;
+                vi += b;
+            }
+        }
+        s_cb[t + 1] = (int)ci;
+        if (t == 0) s_cb[0] = 0;
+        s_vb[t] = vi <= (uint32_t)kCandStageV ? (int)(vi - nvv) : -1;  // LDS offset, or -1: read from global
     }
     __syncthreads();
-    if (t < kCandBlock / 64 && c0 + 64 * t < NC) {
-        kmask[(c0 >> 6) + t] = s_k[t];
-        umask[(c0 >> 6) + t] = s_u[t];
-        if (s_u[t]) ulist[atomicAdd(ulist_n, 1u)] = (uint32_t)((c0 >> 6) + t);  // words k_cand_exact must finish
+    for (int fi = t >> 6; fi < kFpPer; fi += kFpBlock / 64) {  // a wave per footprint's vertices
+        const int vb = s_vb[fi];
+        if (vb < 0 || s_cb[fi + 1] == s_cb[fi]) continue;
+        for (int v = lane; v < s_nv[fi]; v += 64) s_uv[vb + v] = uv[s_xo[fi] + v];
+    }
+    __syncthreads();
+    const int total = s_cb[kFpPer];
+    for (int k = t; k < total; k += kFpBlock) {
+        int lo = 0, hi = kFpPer;  // s_cb[lo] <= k < s_cb[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_cb[mid] <= k) lo = mid;
+            else hi = mid;
+        }
+        const uint4 bx = s_bx[lo];
+        const uint32_t w = bx.y - bx.x + 1, d = (uint32_t)(k - s_cb[lo]);
+        const uint32_t dj = d / w, i13 = bx.x + (d - dj * w), j13 = bx.z + dj;
+        const uint32_t info = s_info[lo];
+        const int key = rect_key(i13, j13, s_sti[lo], s_stj[lo], info);
+        if (key < 0) continue;
+        const int vb = s_vb[lo], fl = s_fl[lo];
+        const double2 *up = vb >= 0 ? s_uv + vb : uv + s_xo[lo];
+        const int v = cand_edges_uv(i13 << (kMaxLevel - kCoverLevel), j13 << (kMaxLevel - kCoverLevel), up, s_nv[lo],
+                                    (fl & 1) != 0, (fl & 2) != 0);
+        if (v == 1) atomicOr(&s_km[lo][key >> 6], 1ull << (key & 63));
+        else if (v == 2) atomicOr(&s_um[lo][key >> 6], 1ull << (key & 63));
+    }
+    __syncthreads();
+    if (t < kFpPer) {
+        const int64_t f = F0 + t;
+        const bool has = f < n && s_cb[t + 1] > s_cb[t];
+        if (has) {
+            ulonglong2 *km = reinterpret_cast<ulonglong2 *>(fkm + 4 * f);
+            km[0] = make_ulonglong2(s_km[t][0], s_km[t][1]);
+            km[1] = make_ulonglong2(s_km[t][2], s_km[t][3]);
+        }
+        const bool und = has && (s_um[t][0] | s_um[t][1] | s_um[t][2] | s_um[t][3]) != 0ull;
+        const unsigned long long um = __ballot(und);
+        if (um) {
+            unsigned int base = 0;
+            if (lane == 0) base = atomicAdd(ulist_n, (unsigned int)__popcll(um));
+            base = (unsigned int)__shfl((int)base, 0);
+            if (und) {
+                ulist[base + cmpct::lanes_below(um)] = (uint32_t)f;
+                ulonglong2 *u = reinterpret_cast<ulonglong2 *>(fum + 4 * f);
+                u[0] = make_ulonglong2(s_um[t][0], s_um[t][1]);
+                u[1] = make_ulonglong2(s_um[t][2], s_um[t][3]);
+            }
+        }
     }
 }
 
 // Undecided candidates: exact S2 containment of the cell centre.  One wave
-// per listed mask word (k_cand_test_c lists the words with undecided bits;
-// a fixed grid strides over the list, so a batch with none costs one small
-// launch); the wave folds its results into the word.
-__device__ __forceinline__ void cand_exact_word(uint32_t g, int64_t NC, const uint32_t *cand_f, const int64_t *coff,
-                                                const uint64_t *st_id, const uint32_t *st_i, const uint32_t *st_j,
-                                                const uint32_t *finfo, const int64_t *xoff, const V3 *xyz,
-                                                const int32_t *nvx, const uint8_t *origin_in, unsigned long long *kmask,
-                                                const unsigned long long *umask)
-{
-    const int64_t c = ((int64_t)g << 6) + (threadIdx.x & 63);
-    const unsigned long long um = umask[g];
-    bool in = false;
-    if (c < NC && ((um >> (threadIdx.x & 63)) & 1ull)) {
-        const uint32_t f = cand_f[c];
-        int face;
-        uint32_t i, j;
-        uint64_t id;
-        cand_cell(c, f, coff, st_id, st_i, st_j, finfo, face, i, j, id);
-        LoopView l{xyz + xoff[f], nvx[f], origin_in[f] != 0};
-        in = loop_contains(l, node_center(face, i, j, kCoverLevel));
-    }
-    const unsigned long long m = __ballot(in);
-    if ((threadIdx.x & 63) == 0) kmask[g] |= m;
-}
-
-__global__ __launch_bounds__(256) void k_cand_exact(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
-                             const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo, const int64_t *xoff,
-                             const V3 *xyz, const int32_t *nvx, const uint8_t *origin_in, unsigned long long *kmask,
-                             const unsigned long long *umask, const uint32_t *ulist, const unsigned int *ulist_n)
+// per listed footprint (a fixed grid strides over the list, so a batch with
+// none costs one small launch), lane = key within a mask word; the wave folds
+// its results into the footprint's kept mask.
+__global__ __launch_bounds__(256) void k_cand_exact(const uint32_t *ulist, const unsigned int *ulist_n,
+                                                    const uint64_t *st_id, const uint32_t *st_i, const uint32_t *st_j,
+                                                    const uint32_t *finfo, const int64_t *xoff, const V3 *xyz,
+                                                    const int32_t *nvx, const uint8_t *origin_in,
+                                                    unsigned long long *fkm, const unsigned long long *fum)
 {
     const unsigned int nl = *ulist_n;
+    const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
-    for (int64_t wi = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); wi < (int64_t)nl; wi += nw)
-        cand_exact_word(ulist[wi], NC, cand_f, coff, st_id, st_i, st_j, finfo, xoff, xyz, nvx, origin_in, kmask, umask);
+    for (int64_t wi = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); wi < (int64_t)nl; wi += nw) {
+        const uint32_t f = ulist[wi];
+        const uint32_t info = finfo[f];
+        for (int q = 0; q < 4; q++) {
+            const unsigned long long um = fum[4 * (int64_t)f + q];
+            if (!um) continue;
+            bool in = false;
+            if ((um >> lane) & 1ull) {
+                int face;
+                uint32_t i, j;
+                uint64_t id;
+                key_cell(64 * q + lane, f, st_id, st_i, st_j, info, face, i, j, id);
+                LoopView l{xyz + xoff[f], nvx[f], origin_in[f] != 0};
+                in = loop_contains(l, node_center(face, i, j, kCoverLevel));
+            }
+            const unsigned long long m = __ballot(in);
+            if (lane == 0 && m) fkm[4 * (int64_t)f + q] |= m;
+        }
+    }
 }
 
-__global__ void k_mask_counts(int64_t G, const unsigned long long *kmask, int64_t *gcnt)
-{
-    const int64_t g = tid64();
-    if (g < G) gcnt[g] = __popcll(kmask[g]);
-}
-
-// Kept candidates before candidate c (c <= NC): group prefix + popcount.
-__device__ __forceinline__ int64_t kept_rank(int64_t c, const unsigned long long *kmask, const int64_t *gpos)
-{
-    const int64_t g = c >> 6;
-    const int r = (int)(c & 63);
-    return gpos[g] + (r ? __popcll(kmask[g] & ((1ull << r) - 1)) : 0);
-}
-
-// Per-footprint cell counts: direct-path count from the candidate scan plus
-// the descent count the item atomics left in dcnt.
-__global__ void k_counts(int64_t n, const int64_t *coff, const unsigned long long *kmask, const int64_t *gpos,
+// Per-footprint cell counts: kept direct candidates plus the descent count
+// the item atomics left in dcnt.
+__global__ void k_counts(int64_t n, const uint8_t *flags, const unsigned long long *fkm,
                          const unsigned long long *dcnt, int64_t *total, int64_t *dc64)
 {
-    int64_t f = tid64();
+    const int64_t f = tid64();
     if (f >= n) return;
-    total[f] = (kept_rank(coff[f + 1], kmask, gpos) - kept_rank(coff[f], kmask, gpos)) + (int64_t)dcnt[f];
+    int64_t c = 0;
+    if (flags[f] & FL_FAST) {
+        const ulonglong2 *km = reinterpret_cast<const ulonglong2 *>(fkm + 4 * f);
+        const ulonglong2 a = km[0], b = km[1];
+        c = __popcll(a.x) + __popcll(a.y) + __popcll(b.x) + __popcll(b.y);
+    }
+    total[f] = c + (int64_t)dcnt[f];
     dc64[f] = (int64_t)dcnt[f];
 }
 
-// Per footprint: where its kept candidates start in the output, less their
-// rank among all kept candidates (so an emitted cell lands at ebase[f] +
-// kept_rank(c), one load instead of three).
-__global__ void k_emit_base(int64_t n, const int64_t *coff, const unsigned long long *kmask, const int64_t *gpos,
-                            const int64_t *offs, int64_t *ebase)
+// The kept direct candidates of a footprint at its CSR offset, in id order
+// (one thread per footprint; keys ascend with the cell id).
+__global__ void k_cand_emit(int64_t n, const uint8_t *flags, const unsigned long long *fkm, const uint64_t *st_id,
+                            const uint32_t *finfo, const int64_t *offs, uint64_t *cells)
 {
     const int64_t f = tid64();
-    if (f < n) ebase[f] = offs[f] - kept_rank(coff[f], kmask, gpos);
-}
-
-__global__ void k_cand_emit(int64_t NC, const uint32_t *cand_f, const int64_t *coff, const uint64_t *st_id,
-                            const uint32_t *st_i, const uint32_t *st_j, const uint32_t *finfo,
-                            const unsigned long long *kmask, const int64_t *gpos, const int64_t *ebase, uint64_t *cells)
-{
-    const int64_t c = tid64();
-    if (c >= NC) return;
-    const unsigned long long km = kmask[c >> 6];
-    if (!((km >> (c & 63)) & 1ull)) return;
-    const uint32_t f = cand_f[c];
-    int face;
-    uint32_t i, j;
-    uint64_t id;
-    cand_cell(c, f, coff, st_id, st_i, st_j, finfo, face, i, j, id);
-    cells[ebase[f] + kept_rank(c, kmask, gpos)] = id;
+    if (f >= n || !(flags[f] & FL_FAST)) return;
+    int64_t w = offs[f];
+    const int L = (int)(finfo[f] & 31u);
+    const int sh = 2 * (kCoverLevel - L);
+    const uint64_t lsbL = lsb_for_level(L), lsb13 = lsb_for_level(kCoverLevel);
+    for (int q = 0; q < 4; q++) {
+        unsigned long long mk = fkm[4 * f + q];
+        while (mk) {
+            const int c = 64 * q + __builtin_ctzll(mk);
+            mk &= mk - 1;
+            const uint64_t r = (uint64_t)(c & ((1 << sh) - 1));
+            cells[w++] = st_id[4 * f + (c >> sh)] - lsbL + lsb13 + r * (lsb13 << 1);
+        }
+    }
 }
 
 __global__ void k_u64_to_i64(int64_t n, const unsigned long long *a, int64_t *b)
@@ -1822,7 +1740,6 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     double2 *uv = uv_.ensure(nx + 1);
     uint64_t *st_id = st_id_.ensure(4 * n + 4);
     uint32_t *st_i = st_i_.ensure(4 * n + 4), *st_j = st_j_.ensure(4 * n + 4), *finfo = finfo_.ensure(n + 1);
-    int64_t *ncand = ncand_.ensure(n + 1), *coff = coff_.ensure(n + 1);
     uint4 *fbox = fbox_.ensure(n + 1);
     uint32_t *slow = slow_.ensure(n + 1);
     unsigned int *slow_n = slow_n_.ensure(1);
@@ -1856,41 +1773,28 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
                        towner, toff, omode, nv, xoff, xyz, fwd, rev, fan_fail);
     hipLaunchKernelGGL(k_setup<true>, dim3(grid_for(n, 64)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng,
                        radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo,
-                       ncand, fbox, fwd, rev, fan_fail, not_inner, omode, perm);
+                       fbox, fwd, rev, fan_fail, not_inner, omode, perm);
     hipLaunchKernelGGL(k_setup<false>, dim3(min(grid_for(n, 64), 512u)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat,
                        lng, radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j,
-                       finfo, ncand, fbox, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                       finfo, fbox, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
     int64_t *eoff = eoff_.ensure(n + 1);
     hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv);
     exclusive_scan_i64(nv, eoff, n, tmp_, s);
-    exclusive_scan_i64(ncand, coff, n, tmp_, s);
-    int64_t h2[2] = {0, 0};
-    DSS_HIP(hipMemcpyAsync(&h2[0], eoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    DSS_HIP(hipMemcpyAsync(&h2[1], coff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    int64_t ne = 0;
+    DSS_HIP(hipMemcpyAsync(&ne, eoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
-    const int64_t ne = h2[0], NC = h2[1];
     if (std::getenv("DSS_COVER_STATS"))
-        fprintf(stderr, "[cover] n %lld vertices %lld candidates %lld clipped edges %lld\n", (long long)n, (long long)nx,
-                (long long)NC, (long long)ne);
-    // direct candidates (most footprints): test now, compact after the counts
-    uint32_t *cand_f = cand_f_.ensure(NC + 1);
-    const int64_t G = (NC + 63) / 64;  // mask words; kept_rank(NC) reads word G
-    unsigned long long *kmask = kmask_.ensure(2 * (G + 1)), *umask = kmask + (G + 1);
-    int64_t *gcnt = gcnt_.ensure(G + 1), *gpos = gpos_.ensure(G + 2);
-    DSS_HIP(hipMemsetAsync(kmask + G, 0, sizeof(unsigned long long), s));
-    if (NC > 0) {
-        hipLaunchKernelGGL(k_cand_owner, dim3(grid_for(n, 256)), dim3(256), 0, s, n, coff, cand_f);
-        uint32_t *ulist = ulist_.ensure(G + 1);
-        unsigned int *ulist_n = ulist_n_.ensure(1);
-        DSS_HIP(hipMemsetAsync(ulist_n, 0, sizeof(unsigned int), s));
-        hipLaunchKernelGGL(k_cand_test_c, dim3(grid_for(NC, kCandBlock)), dim3(kCandBlock), 0, s, NC, cand_f, coff, st_id,
-                           st_i, st_j, finfo, fbox, xoff, uv, nvx, orig, flags, kmask, umask, ulist, ulist_n);
-        hipLaunchKernelGGL(k_cand_exact, dim3((unsigned)std::min<int64_t>(grid_for(G, B / 64), 1024)), dim3(B), 0, s, NC,
-                           cand_f, coff, st_id, st_i, st_j, finfo, xoff, xyz, nvx, orig, kmask, umask, ulist, ulist_n);
-        hipLaunchKernelGGL(k_mask_counts, dim3(grid_for(G, B)), dim3(B), 0, s, G, kmask, gcnt);
-    }
-    exclusive_scan_i64(gcnt, gpos, G, tmp_, s);
-    DSS_HIP(hipMemsetAsync(gpos + G + 1, 0, sizeof(int64_t), s));
+        fprintf(stderr, "[cover] n %lld vertices %lld clipped edges %lld\n", (long long)n, (long long)nx, (long long)ne);
+    // direct candidates (most footprints): the cells of each one's bound,
+    // tested now, compacted after the counts
+    unsigned long long *fkm = kmask_.ensure(8 * (n + 1)), *fum = fkm + 4 * (n + 1);
+    uint32_t *ulist = ulist_.ensure(n + 1);
+    unsigned int *ulist_n = ulist_n_.ensure(1);
+    DSS_HIP(hipMemsetAsync(ulist_n, 0, sizeof(unsigned int), s));
+    hipLaunchKernelGGL(k_cand_fp, dim3(grid_for(n, kFpPer)), dim3(kFpBlock), 0, s, n, flags, fbox, finfo, st_i, st_j,
+                       xoff, nvx, uv, orig, fkm, fum, ulist, ulist_n);
+    hipLaunchKernelGGL(k_cand_exact, dim3((unsigned)std::min<int64_t>(grid_for(n, B / 64), 1024)), dim3(B), 0, s, ulist,
+                       ulist_n, st_id, st_i, st_j, finfo, xoff, xyz, nvx, orig, fkm, fum);
     // hierarchical descent for the rest (big, multi-face, polyline footprints)
     double4 *clip_f = clipf_.ensure(ne + 1), *clip_c = clipc_.ensure(ne + 1);
     uint8_t *cflags = cflags_.ensure(ne + 1);
@@ -1917,15 +1821,14 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
         hipLaunchKernelGGL(k_expand_count, dim3(grid_for(nn, 64)), dim3(64), 0, s, nn, F->f.p, F->i.p, F->j.p, F->meta.p,
                            act, c, xoff, xyz, mode, fmask, orig, nvx, eoff, clip_f, clip_c, cflags, flags);
         exclusive_scan_i64(c, pos, nn, tmp_, s);
-        int64_t nn2 = 0;
-        DSS_HIP(hipMemcpyAsync(&nn2, pos + nn, sizeof(int64_t), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipMemsetAsync(any_open, 0, sizeof(int), s));
-        DSS_HIP(hipStreamSynchronize(s));
         Frontier *G = &fr_[cur ^ 1];
-        G->ensure(nn2 + 1);
+        G->ensure(4 * nn + 1);  // <= 4 children per node: no host round trip before the write
         hipLaunchKernelGGL(k_expand_write, dim3(grid_for(nn, B)), dim3(B), 0, s, nn, F->f.p, F->id.p, F->i.p, F->j.p,
                            F->meta.p, act, pos, G->f.p, G->id.p, G->i.p, G->j.p, G->meta.p, any_open);
+        int64_t nn2 = 0;
         int open = 0;
+        DSS_HIP(hipMemcpyAsync(&nn2, pos + nn, sizeof(int64_t), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipMemcpyAsync(&open, any_open, sizeof(int), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipStreamSynchronize(s));
         cur ^= 1;
@@ -1941,7 +1844,7 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
         hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nn, kItemBlock)), dim3(kItemBlock), 0, s, nn, F->f.p, F->meta.p,
                            icnt, dcnt);
     int64_t *tot64 = fc64_.ensure(n + 1), *dc64 = dc64_.ensure(n + 1), *dpre = dpre_.ensure(n + 1);
-    hipLaunchKernelGGL(k_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, coff, kmask, gpos, dcnt, tot64, dc64);
+    hipLaunchKernelGGL(k_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, flags, fkm, dcnt, tot64, dc64);
     exclusive_scan_i64(tot64, offs, n, tmp_, s);
     int64_t total = 0;
     if (nn > 0) {
@@ -1951,12 +1854,7 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     DSS_HIP(hipMemcpyAsync(&total, offs + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
     uint64_t *cells = cells_.ensure(total + 1);
-    if (NC > 0) {
-        int64_t *ebase = fc64_.ensure(n + 1);  // tot64 is consumed by the scan above
-        hipLaunchKernelGGL(k_emit_base, dim3(grid_for(n, B)), dim3(B), 0, s, n, coff, kmask, gpos, offs, ebase);
-        hipLaunchKernelGGL(k_cand_emit, dim3(grid_for(NC, B)), dim3(B), 0, s, NC, cand_f, coff, st_id, st_i, st_j, finfo,
-                           kmask, gpos, ebase, cells);
-    }
+    hipLaunchKernelGGL(k_cand_emit, dim3(grid_for(n, B)), dim3(B), 0, s, n, flags, fkm, st_id, finfo, offs, cells);
     if (nn > 0) {
         uint32_t *big = big_.ensure(nn + 1);
         int *nbig = flag_.ensure(1);

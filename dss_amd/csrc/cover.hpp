@@ -83,10 +83,10 @@ class CoverEngine {
     // direct candidate path
     DevBuf<double2> uv_;
     DevBuf<uint64_t> st_id_;
-    DevBuf<uint32_t> st_i_, st_j_, finfo_, cand_f_;
-    DevBuf<int64_t> ncand_, coff_, gcnt_, gpos_, dc64_, dpre_;
+    DevBuf<uint32_t> st_i_, st_j_, finfo_;
+    DevBuf<int64_t> dc64_, dpre_;
     DevBuf<unsigned long long> kmask_;
-    DevBuf<uint32_t> ulist_;          // mask words with undecided candidates
+    DevBuf<uint32_t> ulist_;          // footprints with undecided candidates
     DevBuf<unsigned int> ulist_n_;
     DevBuf<uint4> fbox_;
     bool tables_ = false;

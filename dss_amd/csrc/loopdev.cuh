@@ -308,7 +308,19 @@ DSS_HD bool loop_contains(const LoopView &l, V3 p, bool &fail)
     e.init(origin_point(), p);
     e.restart_at(l.vertex(0));
     bool inside = l.origin_inside;
-    for (int i = 1; i <= l.n; i++) inside = inside != edge_or_vertex_chain_crossing(e, l.vertex(i), fail);
+    // vertices loaded 4 at a time (independent loads in flight together; the
+    // chain itself is evaluated in order, as loop.go does)
+    for (int i0 = 1; i0 <= l.n; i0 += 4) {
+        V3 q[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int i = i0 + u <= l.n ? i0 + u : l.n;
+            q[u] = l.v[i == l.n ? 0 : i];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (i0 + u <= l.n) inside = inside != edge_or_vertex_chain_crossing(e, q[u], fail);
+    }
     return inside;
 }
 DSS_HD void loop_init_origin(LoopView &l, bool &fail)
