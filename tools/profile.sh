@@ -24,4 +24,7 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_AN
 fi
 cd "$R"
 python3 tools/pmc_summary.py "$OUT" --skip-first ${SKIP:-2} --json "$OUT/pmc_traffic.json" --queries ${NQ:-1000000} --intents ${NI:-10000000} --source "profiles/$TAG" > "$OUT/summary.csv"
+if [ -n "$FULL_PMC" ] || [ -n "$FP64" ]; then
+python3 tools/fp64_summary.py "$OUT" "$OUT/fp64_cover.json" ${NQ:-1000000} ${NI:-10000000} ${SKIP:-2} "profiles/$TAG" > "$OUT/fp64.txt"
+fi
 cat "$OUT/summary.csv" | head -30
