@@ -506,6 +506,14 @@ __global__ void k_slot_counts(int64_t ns, const uint32_t *sfirst, const uint32_t
     if ((threadIdx.x & 63) == 0 && c) atomicMax(maxc, c);
 }
 
+// Slots holding a long-footprint posting: their join units take the long
+// join variant (the others' postings all have compact prefixes).
+__global__ void k_slot_lfp(int64_t NP, const uint32_t *key, const uint8_t *b_meta, uint8_t *s_lfp)
+{
+    const int64_t j = tid64();
+    if (j < NP && (b_meta[j] & kMetaLongFp)) s_lfp[key[j] >> 1] = 1;
+}
+
 __global__ void k_owner_keys(int64_t n, const int32_t *owner, uint32_t *key, uint32_t *val)
 {
     const int64_t e = tid64();
@@ -852,7 +860,7 @@ static_assert(sizeof(Unit) == 32, "Unit layout");
 // past it) and emits one unit per 64-posting tile of the cell's regular
 // and long parts; slots come from one atomic per wave (region counters).
 __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *skey, const int64_t *dnkeys, Regions ur,
-                                                  Unit *units, uint32_t tp)
+                                                  Unit *units, Regions url, Unit *units_l, uint32_t tp)
 {
     const int lane = threadIdx.x & 63;
     const uint32_t nkeys = (uint32_t)*dnkeys;
@@ -870,6 +878,7 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
         const bool wstart = valid && (key & 1u) && (p == 0 || prev != key);
         const unsigned long long cm = __ballot(cstart), wm = __ballot(wstart);
         uint32_t nu = 0, rw = 0, re = 0, slot = key >> 1, ntr = 0;
+        bool lfp = false;  // the cell holds long-footprint postings: its units go to the long queue
         uint64_t s0 = 0, sr = 0, s1 = 0;
         if (cstart) {
             const unsigned long long above = lane == 63 ? 0ull : (cm >> (lane + 1)) << (lane + 1);
@@ -886,12 +895,20 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
             sr = s0 + a.s_nreg[slot];
             ntr = (uint32_t)((sr - s0 + tp - 1) / tp);
             nu = ntr + (uint32_t)((s1 - sr + tp - 1) / tp);
+            lfp = a.s_lfp[slot] != 0;
         }
-        uint32_t x = wave_incl_scan(nu);
-        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-        unsigned long long bu = 0;
-        if (lane == 0 && tot) bu = atomicAdd(ur.counter(reg), (unsigned long long)tot);
-        bu = __shfl(bu, 0) + (x - nu);
+        const uint32_t ns_ = lfp ? 0u : nu, nl_ = lfp ? nu : 0u;
+        const uint32_t xs = wave_incl_scan(ns_), xl = wave_incl_scan(nl_);
+        const uint32_t tots = (uint32_t)__builtin_amdgcn_readlane((int)xs, 63);
+        const uint32_t totl = (uint32_t)__builtin_amdgcn_readlane((int)xl, 63);
+        unsigned long long bs = 0, bl = 0;
+        if (lane == 0 && tots) bs = atomicAdd(ur.counter(reg), (unsigned long long)tots);
+        if (lane == 0 && totl) bl = atomicAdd(url.counter(reg), (unsigned long long)totl);
+        bs = __shfl(bs, 0) + (xs - ns_);
+        bl = __shfl(bl, 0) + (xl - nl_);
+        const unsigned long long bu = lfp ? bl : bs;
+        const Regions &dr = lfp ? url : ur;
+        Unit *du = lfp ? units_l : units;
         for (uint32_t t = 0; t < nu; t++) {
             Unit d;
             const bool lng = t >= ntr;
@@ -905,7 +922,7 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
             d.w0 = lng ? re : rw;
             d.w1 = re;
             const unsigned long long wpos = bu + t;
-            if ((int64_t)wpos < ur.cap) units[reg * ur.cap + (int64_t)wpos] = d;
+            if ((int64_t)wpos < dr.cap) du[reg * dr.cap + (int64_t)wpos] = d;
         }
     }
 }
@@ -2371,6 +2388,9 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
         exclusive_scan_i64(cnt, off, ns, tmp2_, s);
         uint64_t *sp = idx->s_post.ensure_exact(ns + 1);
         hipLaunchKernelGGL(k_u64_store, dim3(grid_for(ns + 1, kBlock)), dim3(kBlock), 0, s, ns + 1, off, sp);
+        uint8_t *lfp = idx->s_lfp.ensure_exact(ns + 1);
+        DSS_HIP(hipMemsetAsync(lfp, 0, ns + 1, s));
+        if (NP) hipLaunchKernelGGL(k_slot_lfp, dim3(grid_for(NP, kBlock)), dim3(kBlock), 0, s, NP, key2, b_meta, lfp);
     }
     stage_check(s, "index build: slot table");
     // (7) entity-level attributes: ends_at, owner, owner -> entities, counters
@@ -2457,12 +2477,14 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     if (nq <= small_max_q_ && nqc <= 16 * small_max_q_)
         return search_small(idx, nq, q_offs, q_cells, q_alt_lo, q_alt_hi, q_tlo, q_thi, q_owner, nqc, s, out);
     // one control block (a single memset to start, one copy back per join):
-    // dqmax slots, unit region counters, misc counters ([0] pairs [1] tagged
+    // dqmax slots, unit region counters (short / long queues), misc counters ([0] pairs [1] tagged
     // [2] lane tests [3] broadcasts [5] long queries [9] scratch), unit queue
     // heads, output region counters -- kRegStride words between counters
     constexpr int kR = kRegions * kRegStride;
-    constexpr int kCtlDq = 0, kCtlUnits = kR, kCtlMisc = 2 * kR, kCtlQueue = 2 * kR + 16, kCtlOut = 3 * kR + 16,
-                  kCtlTOut = 4 * kR + 16, kCtlWords = 5 * kR + 16;
+    // (the unit counters come before the misc words: each join attempt
+    // zeroes everything from misc word 6 on)
+    constexpr int kCtlDq = 0, kCtlUnits = kR, kCtlUnitsL = 2 * kR, kCtlMisc = 3 * kR, kCtlQueue = 3 * kR + 16,
+                  kCtlQueueL = 4 * kR + 16, kCtlOut = 5 * kR + 16, kCtlTOut = 6 * kR + 16, kCtlWords = 7 * kR + 16;
     unsigned long long *ctl = counter_.ensure(kCtlWords);
     unsigned long long *cnt = ctl + kCtlMisc;
     DSS_HIP(hipMemsetAsync(ctl, 0, kCtlWords * sizeof(unsigned long long), s));
@@ -2503,16 +2525,26 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     }
     const int kp = join_kp_ == 2 ? 2 : 1;  // 64-posting tiles per join unit (postings per lane)
     int64_t ucap = std::max<int64_t>(units_cap_hint_, 1024);  // per region
-    Unit *units = nullptr;
+    // units of cells with long-footprint postings (idx->s_lfp) go to a second
+    // set of queues joined by the long variant; the rest by the short one
+    const bool any_long = idx->n_long_fp > 0;
+    int64_t ucap_l = any_long ? std::max<int64_t>(units_cap_hint_l_, 1024) : 0;
+    Unit *units = nullptr, *units_l = nullptr;
     const unsigned ugrid = (unsigned)std::min<int64_t>((nqc + 63) / 64 / (kBlock / 64) + 1, (int64_t)n_cu_ * 16);
     auto build_units = [&]() {
-        units = (Unit *)units_buf_.ensure(sizeof(Unit) * (kRegions * ucap + 1));
+        units = (Unit *)units_buf_.ensure(sizeof(Unit) * (kRegions * (ucap + ucap_l) + 1));
+        units_l = units + kRegions * ucap;
         DSS_HIP(hipMemsetAsync(ctl + kCtlUnits, 0, kR * sizeof(unsigned long long), s));
+        DSS_HIP(hipMemsetAsync(ctl + kCtlUnitsL, 0, kR * sizeof(unsigned long long), s));
         hipLaunchKernelGGL(k_units, dim3(ugrid), dim3(kBlock), 0, s, ix, skey, dnkeys, Regions{ctl + kCtlUnits, ucap},
-                           units, (uint32_t)(64 * kp));
+                           units, Regions{ctl + kCtlUnitsL, ucap_l}, units_l, (uint32_t)(64 * kp));
         hipLaunchKernelGGL(k_unit_ranges, dim3((unsigned)n_cu_ * 8), dim3(kBlock), 0, s, ix,
                            Regions{ctl + kCtlUnits, ucap}, units, (const uint32_t *)sval, (const QRec *)recs,
                            (const unsigned long long *)(ctl + kCtlDq), (long long)idx->tbase, idx->qshift);
+        if (any_long)
+            hipLaunchKernelGGL(k_unit_ranges, dim3((unsigned)n_cu_ * 2), dim3(kBlock), 0, s, ix,
+                               Regions{ctl + kCtlUnitsL, ucap_l}, units_l, (const uint32_t *)sval, (const QRec *)recs,
+                               (const unsigned long long *)(ctl + kCtlDq), (long long)idx->tbase, idx->qshift);
     };
     build_units();
     // (6) join; grow the output (and the units) and rerun if too small
@@ -2522,7 +2554,6 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     ja.lazy_sig_recs = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(lazy_sig_recs_, 0xffffffffll));
     const unsigned nblocks = (unsigned)n_cu_ * (join_kp_ == 2 ? kJoinKpBlocksPerCU : kJoinBlocksPerCU);
     if (out_rcap_ == 0) out_rcap_ = ((int64_t)nq * 16 / kRegions / kOutChunk + 2) * kOutChunk;
-    const bool any_long = idx->n_long_fp > 0;  // the batch's long flag is only known on the device
     if (any_long && tag_rcap_ == 0) tag_rcap_ = ((int64_t)nq * 4 / kRegions / kOutChunk + 2) * kOutChunk;
     const int qb = bits_for(nq), eb = bits_for(idx->n_e);
     const int hbm = std::min(24, 64 - qb - eb);  // qb <= 29, eb <= 32: 3 <= hbm <= 24
@@ -2558,30 +2589,39 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         ja.out = OutArgs{oq, oe, OutStream{out_rcap_, fills, ctl + kCtlOut}, tk, OutStream{tag_rcap_, tfills, ctl + kCtlTOut},
                          eb, hbm, cnt};
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
-        auto kern = kp == 2 ? (q_owner ? (any_long ? k_join_kp<true, true, 2> : k_join_kp<true, false, 2>)
-                                       : (any_long ? k_join_kp<false, true, 2> : k_join_kp<false, false, 2>))
-                            : (q_owner ? (any_long ? k_join<true, true> : k_join<true, false>)
-                                       : (any_long ? k_join<false, true> : k_join<false, false>));
-        hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs, (const uint32_t *)sval,
-                           (const Unit *)units, ctl + kCtlQueue);
+        auto kshort = kp == 2 ? (q_owner ? k_join_kp<true, false, 2> : k_join_kp<false, false, 2>)
+                              : (q_owner ? k_join<true, false> : k_join<false, false>);
+        hipLaunchKernelGGL(kshort, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
+                           (const uint32_t *)sval, (const Unit *)units, ctl + kCtlQueue);
+        if (any_long) {  // the same output streams, continued
+            auto klong = kp == 2 ? (q_owner ? k_join_kp<true, true, 2> : k_join_kp<false, true, 2>)
+                                 : (q_owner ? k_join<true, true> : k_join<false, true>);
+            JoinArgs jl = ja;
+            jl.ur = Regions{ctl + kCtlUnitsL, ucap_l};
+            hipLaunchKernelGGL(klong, dim3(nblocks), dim3(64 * kWaves), 0, s, jl, (const QRec *)recs,
+                               (const uint32_t *)sval, (const Unit *)units_l, ctl + kCtlQueueL);
+        }
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
         unsigned long long h[kCtlWords];
         DSS_HIP(hipMemcpyAsync(h, ctl, sizeof(h), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipStreamSynchronize(s));
-        int64_t nu = 0, umax = 0, omax = 0, tmax = 0;
+        int64_t nu = 0, umax = 0, umax_l = 0, omax = 0, tmax = 0;
         for (int r = 0; r < kRegions; r++) {
-            const int64_t u = (int64_t)h[kCtlUnits + r * kRegStride];
-            nu += u;
+            const int64_t u = (int64_t)h[kCtlUnits + r * kRegStride], ul = (int64_t)h[kCtlUnitsL + r * kRegStride];
+            nu += u + ul;
             umax = std::max(umax, u);
+            umax_l = std::max(umax_l, ul);
             omax = std::max(omax, (int64_t)h[kCtlOut + r * kRegStride]);
             tmax = std::max(tmax, (int64_t)h[kCtlTOut + r * kRegStride]);
         }
-        if (umax > ucap) {  // the units did not fit: regrow, rebuild them, rerun the join
-            ucap = umax + umax / 4 + 1024;
+        if (umax > ucap || umax_l > ucap_l) {  // the units did not fit: regrow, rebuild them, rerun the join
+            if (umax > ucap) ucap = umax + umax / 4 + 1024;
+            if (umax_l > ucap_l) ucap_l = umax_l + umax_l / 4 + 1024;
             build_units();
             continue;
         }
         units_cap_hint_ = std::max<int64_t>(units_cap_hint_, umax + umax / 8);
+        units_cap_hint_l_ = std::max<int64_t>(units_cap_hint_l_, umax_l + umax_l / 8);
         bool rerun = false;
         if (omax > out_rcap_) {  // an output region filled up: regrow (per region) and rerun
             out_rcap_ = ((omax + omax / 8) / kOutChunk + 2) * kOutChunk;

@@ -29,6 +29,7 @@ struct dssg_index {
     dss::DevBuf<uint64_t> irr_cells;  // n_irr, sorted
     dss::DevBuf<uint64_t> s_post;     // n_slots + 1: first posting of each slot
     dss::DevBuf<uint32_t> s_nreg;     // n_slots: regular-duration postings of the slot
+    dss::DevBuf<uint8_t> s_lfp;       // n_slots: 1 = the slot holds a long-footprint posting (join variant)
     // ---- time --------------------------------------------------------------------
     int64_t dcap = 0;      // max duration of a regular posting's entity (us)
     int64_t dcap_thr = 0;  // class threshold: duration <= dcap_thr is regular
@@ -148,7 +149,7 @@ class SearchEngine {
     int n_cu_ = 0;
     int64_t out_rcap_ = 0;  // output slots per region
     int64_t tag_rcap_ = 0;  // tagged-key slots per region
-    int64_t units_cap_hint_ = 0;
+    int64_t units_cap_hint_ = 0, units_cap_hint_l_ = 0;
     bool timing_ = false;
     int64_t tag_bucket_avg_ = 1024;
     int64_t lazy_sig_recs_ = 0;
