@@ -589,33 +589,31 @@ __global__ void k_edge_counts(int64_t n, const uint8_t *mode, const uint8_t *fma
     cnt[f] = (flags[f] & FL_FAST) ? 0 : (int64_t)__builtin_popcount(fmask[f]) * num_edges(mode[f], nvx[f]);
 }
 
-// Clip every edge to every touched face (ascending face order).
-__global__ __launch_bounds__(64) void k_clip(int64_t n, const int64_t *xoff, const V3 *xyz, const uint8_t *mode, const uint8_t *fmask,
-                       const uint8_t *flags, const int32_t *nvx, const int64_t *eoff, double4 *clip_f, double4 *clip_c,
-                       uint8_t *cflags)
+// Clip every edge to every touched face (ascending face order), one thread
+// per (footprint, touched face, edge) item: the few multi-face / big /
+// polyline footprints of a batch carry up to 6 x 20 clips each, which one
+// thread per footprint walked serially (0.17 ms on configs[2]).
+__global__ void k_clip_items(int64_t ne_all, const uint32_t *eown, const int64_t *xoff, const V3 *xyz,
+                             const uint8_t *mode, const uint8_t *fmask, const int32_t *nvx, const int64_t *eoff,
+                             double4 *clip_f, double4 *clip_c, uint8_t *cflags)
 {
-    int64_t f = tid64();
-    if (f >= n) return;
-    uint8_t md = mode[f];
-    if (md == MODE_NONE || (flags[f] & FL_FAST)) return;
-    int nv = nvx[f], ne = num_edges(md, nv);
+    const int64_t k = tid64();
+    if (k >= ne_all) return;
+    const uint32_t f = eown[k];
+    const int nv = nvx[f], ne = num_edges(mode[f], nv);
+    const int64_t local = k - eoff[f];
+    const int fi = (int)(local / ne), e = (int)(local - (int64_t)fi * ne);
+    uint32_t fm = fmask[f];
+    for (int q = 0; q < fi; q++) fm &= fm - 1;  // the fi-th touched face, ascending
+    const int fc = __builtin_ctz(fm);
     const V3 *p = xyz + xoff[f];
-    int64_t base = eoff[f];
-    int fi = 0;
-    for (int fc = 0; fc < 6; fc++) {
-        if (!(fmask[f] >> fc & 1)) continue;
-        for (int e = 0; e < ne; e++) {
-            V3 a = p[e], b = p[(e + 1) % nv];
-            double uf[4], uc[4];
-            bool okf = clip_to_padded_face(a, b, fc, kFinePad, uf);
-            bool okc = clip_to_padded_face(a, b, fc, kCoarsePad, uc);
-            int64_t k = base + (int64_t)fi * ne + e;
-            clip_f[k] = make_double4(uf[0], uf[1], uf[2], uf[3]);
-            clip_c[k] = make_double4(uc[0], uc[1], uc[2], uc[3]);
-            cflags[k] = (uint8_t)((okf ? 1 : 0) | (okc ? 2 : 0));
-        }
-        fi++;
-    }
+    const V3 a = p[e], b = p[(e + 1) % nv];
+    double uf[4], uc[4];
+    const bool okf = clip_to_padded_face(a, b, fc, kFinePad, uf);
+    const bool okc = clip_to_padded_face(a, b, fc, kCoarsePad, uc);
+    clip_f[k] = make_double4(uf[0], uf[1], uf[2], uf[3]);
+    clip_c[k] = make_double4(uc[0], uc[1], uc[2], uc[3]);
+    cflags[k] = (uint8_t)((okf ? 1 : 0) | (okc ? 2 : 0));
 }
 
 // Face-cell id for face fc (level 0).
@@ -1798,8 +1796,12 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     // hierarchical descent for the rest (big, multi-face, polyline footprints)
     double4 *clip_f = clipf_.ensure(ne + 1), *clip_c = clipc_.ensure(ne + 1);
     uint8_t *cflags = cflags_.ensure(ne + 1);
-    hipLaunchKernelGGL(k_clip, dim3(grid_for(n, 64)), dim3(64), 0, s, n, xoff, xyz, mode, fmask, flags, nvx, eoff, clip_f,
-                       clip_c, cflags);
+    if (ne > 0) {
+        uint32_t *eown = eown_.ensure(ne + 1);
+        hipLaunchKernelGGL(k_vowner, dim3(grid_for(n, B)), dim3(B), 0, s, n, eoff, eown);
+        hipLaunchKernelGGL(k_clip_items, dim3(grid_for(ne, B)), dim3(B), 0, s, ne, eown, xoff, xyz, mode, fmask, nvx, eoff,
+                           clip_f, clip_c, cflags);
+    }
     int64_t *soff = soff_.ensure(n + 1);
     hipLaunchKernelGGL(k_start<0>, dim3(grid_for(n, 64)), dim3(64), 0, s, n, xoff, xyz, mode, fmask, flags, orig, nvx,
                        eoff, clip_c, cflags, nv, soff, nullptr, nullptr, nullptr, nullptr, nullptr);
