@@ -243,11 +243,6 @@ int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value)
         ctx->search.set_small_max_q(value);
         return DSSG_OK;
     }
-    if (std::string(key) == "join_kp") {  // postings per lane of the tiled join (1 or 2)
-        if (value != 1 && value != 2) return DSSG_ERR_INVALID;
-        ctx->search.set_join_kp(value);
-        return DSSG_OK;
-    }
     if (std::string(key) == "cover_wave") {  // max batch of the wave-path covering (0: general pipeline only)
         ctx->cover.set_wave_max(value);
         return DSSG_OK;

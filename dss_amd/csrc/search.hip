@@ -92,10 +92,7 @@ constexpr int kWaves = 4;                       // waves per join workgroup
 #define DSS_EMIT_DENSITY 4
 #endif
 constexpr int kEmitDensity = DSS_EMIT_DENSITY;
-#ifndef DSS_OUT_STAGE
-#define DSS_OUT_STAGE 256
-#endif
-constexpr int kOutStage = DSS_OUT_STAGE;  // pairs per wave staged in LDS before the stores (0: direct stores)  // record-major emission above 1 / kEmitDensity pass density
+constexpr int kOutStage = 1024;  // pairs per wave staged in LDS (16-bit codes) before the stores
 // ---- level-13 decode + prefix signatures -----------------------------------
 __device__ __forceinline__ int s2pos_to_ij(int o, int pos) { return (int)((0x874B78B4u >> (8 * o + 2 * pos)) & 3u); }
 __device__ __forceinline__ int s2pos_to_orientation(int pos) { return (int)((0xC1u >> (2 * pos)) & 3u); }
@@ -985,7 +982,7 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m)
 // -- so every region fills the bottom of the buffer: the holes below the
 // total are only the waves' last, partly filled chunks and the few chunks of
 // the regions' imbalance, which k_fix_* close.
-constexpr int kOutChunk = 1024, kOutChunkLog = 10, kRegionsLog = 3;
+constexpr int kOutChunkLog = 10, kOutChunk = 1 << kOutChunkLog, kRegionsLog = 3;  // (4096-pair chunks: no faster)
 static_assert((1 << kOutChunkLog) == kOutChunk && (1 << kRegionsLog) == kRegions, "output layout");
 struct OutStream {
     int64_t rcap;                  // slots per region (a multiple of kOutChunk)
@@ -1126,7 +1123,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
     __shared__ longlong2 s_rt[kWaves][64];      // record (tlo, thi)
     __shared__ float4 s_ra[kWaves][64];         // record (alo, ahi, qv, own)
     __shared__ ulonglong2 s_rs[kWaves][2][64];  // record near-prefix signature
-    __shared__ uint2 s_out[kWaves][kOutStage];   // a sparse batch's pairs, staged for coalesced stores
+    __shared__ uint16_t s_os[kWaves][kOutStage];  // a batch's pairs as (record slot << 6 | lane), staged
+    __shared__ uint32_t s_pe[kWaves][64];         // each lane's posting entity (for the staged stores)
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const IndexView &ix = a.ix;
@@ -1217,6 +1215,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
         if (un >= 0) prefetch(un);
         if (d.n1 <= d.n0 && d.w1 <= d.w0) continue;
         const uint32_t pent = pe & ~kFirstBit;
+        s_pe[w][lane] = pent;  // (read after the wave barrier of the emission below)
         const unsigned long long vmask = __ballot(pv);
         if (!vmask) continue;  // (un, the next unit, is already in flight)
         // tile time bounds (a regular tile is sorted by m = min(t0, t1)):
@@ -1355,24 +1354,28 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 const bool wu = out.have != 0, wt = LONG && tout.have != 0;  // else counted only (rerun)
                 if ((int64_t)(total_u + total_t) * kEmitDensity <= (int64_t)nrel * __popcll(vmask)) {
                     // (one loop per stream: no divergent double bodies)
-                    if (!LONG && kOutStage && wu && total_u <= kOutStage) {  // (long variants: direct, no VGPR headroom)
-                        // each lane's pairs into the wave's LDS stage (one 8-B
-                        // LDS store per pair), then the batch leaves as runs of
-                        // consecutive slots: full-width coalesced global stores
-                        // instead of one scattered 4-B store per pair and array
+                    if (!LONG && wu && total_u <= kOutStage) {  // (long variants: direct, no VGPR headroom)
+                        // each lane's pairs into the wave's LDS stage as 16-bit
+                        // (record slot, lane) codes, then the batch leaves as
+                        // runs of consecutive slots: full-width coalesced global
+                        // stores instead of one scattered 4-B store per pair and
+                        // array (configs[2] k_join 3.89 -> 3.70 ms against an
+                        // 8-B (q, e) stage of a quarter the pairs)
                         uint32_t iu = (incl & 0xffffu) - cu;
                         unsigned long long kk = keep & ~tagm;
                         while (kk) {
                             const int j = __builtin_ctzll(kk);
                             kk &= kk - 1;
-                            s_out[w][iu++] = make_uint2((uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags, pent);
+                            s_os[w][iu++] = (uint16_t)((uint32_t)j << 6 | (uint32_t)lane);
                         }
                         __builtin_amdgcn_wave_barrier();
                         for (int p = lane; p < total_u; p += 64) {
-                            const uint2 v = s_out[w][p];
+                            const uint32_t v = s_os[w][p];
+                            const uint32_t q = (uint32_t)__float_as_int(s_ra[w][v >> 6].z) & ~kQFlags;
+                            const uint32_t e = s_pe[w][v & 63u];
                             const unsigned long long pos = su.at((unsigned long long)p);
-                            a.out.q[pos] = v.x;
-                            a.out.e[pos] = v.y;
+                            a.out.q[pos] = q;
+                            a.out.e[pos] = e;
                         }
                         __builtin_amdgcn_wave_barrier();
                     } else if (wu) {
@@ -1419,354 +1422,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                         ot += (unsigned long long)__popcll(kt);
                     }
                 }
-            }
-        }
-    }
-    out.finish(a.out.ps, &a.out.counter[0]);
-    if (LONG) tout.finish(a.out.ts, &a.out.counter[1]);
-    if (lane == 0) {
-        atomicAdd(&a.out.counter[2], n_tests);
-        atomicAdd(&a.out.counter[3], n_bcast);
-    }
-}
-
-// k_join with KP consecutive 64-posting tiles per unit, lane k-th posting =
-// p0 + lane + 64 k (KP postings per lane, in registers).  A hot cell's
-// records are staged once per KP tiles instead of once per tile: the band a
-// unit stages spans KP tiles' starts plus the widest window and the longest
-// duration, which in dense cells (tile span << band) is little more than one
-// tile's band.  Everything per (posting, record) is k_join's.
-constexpr int kJoinKpBlocksPerCU = 5;  // k_join_kp<2>'s register budget: 5 waves per SIMD
-template <bool OWNER, bool LONG, int KP>
-__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LONG ? 1 : kJoinKpBlocksPerCU))) void k_join_kp(JoinArgs a, const QRec *__restrict__ recs,
-                                                      const uint32_t *__restrict__ sval,
-                                                      const Unit *__restrict__ units,
-                                                      unsigned long long *__restrict__ work)
-{
-    __shared__ longlong2 s_rt[kWaves][64];      // record (tlo, thi)
-    __shared__ float4 s_ra[kWaves][64];         // record (alo, ahi, qv, own)
-    __shared__ ulonglong2 s_rs[kWaves][2][64];  // record near-prefix signature
-    __shared__ uint2 s_out[kWaves][kOutStage];   // a sparse batch's pairs, staged for coalesced stores
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const IndexView &ix = a.ix;
-    WaveOut out, tout;  // pairs, tagged keys
-    unsigned long long n_tests = 0, n_bcast = 0;
-    // units: kRegions queues (the unit regions), a wave starts on its own
-    // region's and moves on when it is drained; grabs of g units per atomic
-    int qreg = (int)(blockIdx.x % kRegions), visited = 0;
-    int64_t qn = min((int64_t)a.ur.cnt[qreg * kRegStride], a.ur.cap);
-    const int64_t wpr = max((int64_t)1, (int64_t)gridDim.x * kWaves / kRegions);  // waves per region
-    int64_t ucur = 0, uend = 0;
-    auto next_unit = [&]() -> int64_t {
-        while (ucur >= uend) {
-            const int64_t g = min((int64_t)32, max((int64_t)1, qn / (wpr * 8)));
-            unsigned long long ub = 0;
-            if (lane == 0) ub = atomicAdd(&work[qreg * kRegStride], (unsigned long long)g);
-            // lane 0's grab into scalar registers: the unit loop's exits stay
-            // wave-uniform, so its loop-carried state (output chunk, counters)
-            // stays scalar too
-            ub = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ub >> 32), 0) << 32) |
-                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ub, 0);
-            if ((int64_t)ub < qn) {
-                ucur = (int64_t)ub;
-                uend = min((int64_t)ub + g, qn);
-                break;
-            }
-            if (++visited >= kRegions) return -1;
-            qreg = (qreg + 1) % kRegions;
-            qn = min((int64_t)a.ur.cnt[qreg * kRegStride], a.ur.cap);
-        }
-        return (int64_t)qreg * a.ur.cap + ucur++;
-    };
-    // software pipeline: the next unit's descriptor and postings are loaded
-    // while this one's records are joined
-    Unit dn{};
-    longlong2 nt[KP];
-    float2 na[KP];
-    uint32_t ne[KP], nmeta[KP];
-    int32_t nown[KP];
-    ulonglong2 ns01[KP], ns23[KP];
-    bool nsig = false;
-    auto prefetch = [&](int64_t u) {
-        dn = units[u];
-        const uint32_t nrec = (dn.n1 > dn.n0 ? dn.n1 - dn.n0 : 0u) + (dn.w1 > dn.w0 ? dn.w1 - dn.w0 : 0u);
-        nsig = nrec > a.lazy_sig_recs;
-        const uint32_t npn = dn.np & ~kUnitLong;
-#pragma unroll
-        for (int k = 0; k < KP; k++) {
-            nt[k] = make_longlong2(LLONG_MAX, LLONG_MIN);
-            na[k] = make_float2(INFINITY, -INFINITY);
-            ne[k] = nmeta[k] = 0;
-            nown[k] = 0;
-            ns01[k] = ns23[k] = make_ulonglong2(0, 0);
-            if (nrec && (uint32_t)(lane + 64 * k) < npn) {
-                const uint64_t p = dn.p0 + (uint64_t)(lane + 64 * k);
-                ne[k] = ix.b_e[p];
-                nmeta[k] = ix.b_meta[p];
-                nt[k] = ix.b_t[p];
-                na[k] = ix.b_alt[p];
-                if (nsig) {
-                    ns01[k] = ix.b_sig[2 * p];
-                    ns23[k] = ix.b_sig[2 * p + 1];
-                }
-                if (OWNER) nown[k] = ix.b_owner[p];
-            }
-        }
-    };
-    int64_t un = next_unit();
-    if (un >= 0) prefetch(un);
-    while (un >= 0) {
-        Unit d = dn;  // (a uniform load; made explicit for the compiler)
-        d.np = (uint32_t)uni32((int)d.np);
-        d.slot = (uint32_t)uni32((int)d.slot);
-        d.n0 = (uint32_t)uni32((int)d.n0);
-        d.n1 = (uint32_t)uni32((int)d.n1);
-        d.w0 = (uint32_t)uni32((int)d.w0);
-        d.w1 = (uint32_t)uni32((int)d.w1);
-        const uint32_t np = d.np & ~kUnitLong;
-        // ---- this lane's postings
-        longlong2 pt[KP];
-        float2 pa[KP];
-        uint32_t pent[KP];
-        int32_t pown[KP];
-        ulonglong2 ps01[KP], ps23[KP];
-        bool pv[KP], pfirst[KP], pcompact[KP], plong[KP], lsig[KP];
-        unsigned long long vm[KP], vmask = 0;
-        long long tend = LLONG_MIN;
-#pragma unroll
-        for (int k = 0; k < KP; k++) {
-            pt[k] = nt[k];
-            pa[k] = na[k];
-            pent[k] = ne[k] & ~kFirstBit;
-            pown[k] = nown[k];
-            ps01[k] = ns01[k];
-            ps23[k] = ns23[k];
-            lsig[k] = false;
-            const bool in = (uint32_t)(lane + 64 * k) < np;
-            pv[k] = in && !is_dead(ix, pent[k]);  // tombstones match nothing
-            pfirst[k] = (ne[k] & kFirstBit) != 0;                 // entity's smallest cell
-            pcompact[k] = (nmeta[k] & kMetaCompact) != 0;         // compact prefix
-            plong[k] = LONG && (nmeta[k] & kMetaLongFp) != 0;     // long footprint
-            vm[k] = __ballot(pv[k]);
-            vmask |= vm[k];
-            if (in) tend = max(tend, pt[k].x > pt[k].y ? pt[k].x : pt[k].y);
-        }
-        const bool usig = nsig;  // the signatures are loaded (else: per lane, on first need)
-        un = next_unit();
-        if (un >= 0) prefetch(un);
-        if (d.n1 <= d.n0 && d.w1 <= d.w0) continue;
-        if (!vmask) continue;  // (un, the next unit, is already in flight)
-        // unit time bounds (a regular unit is sorted by m = min(t0, t1)):
-        // records whose window misses every posting are skipped (a long
-        // unit: no bound)
-        long long t0min = LLONG_MIN, t1max = LLONG_MAX;
-        if (!(d.np & kUnitLong)) {
-            t0min = readlane64(tmin2(pt[0].x, pt[0].y), 0);  // <= every t0 of the unit
-            t1max = wave_max_i64(tend);
-        }
-        const uint32_t ra0 = d.n0, ra1 = d.n1, rb0 = d.w0, rb1 = d.w1;
-        unsigned long long nvalid = 0;
-#pragma unroll
-        for (int k = 0; k < KP; k++) nvalid += (unsigned long long)__popcll(vm[k]);
-        for (int part = 0; part < 2; part++) {
-            const uint32_t x0 = part ? rb0 : ra0, x1 = part ? rb1 : ra1;
-            for (uint32_t base = x0; base < x1; base += 64) {
-                // stage the batch's records whose window meets the tile's time
-                // hull, compacted to slots [0, nrel)
-                const uint32_t r = base + (uint32_t)lane;
-                bool rel = false;
-                int4 h0 = make_int4(0, 0, 0, 0), h1 = h0;
-                ulonglong2 g0 = make_ulonglong2(0, 0), g1 = g0;
-                if (r < x1) {
-                    const int4 *r4 = reinterpret_cast<const int4 *>(recs + sval[r]);
-                    h0 = r4[0];
-                    h1 = r4[1];
-                    const long long tlo = ((long long)h0.y << 32) | (uint32_t)h0.x;
-                    const long long thi = ((long long)h0.w << 32) | (uint32_t)h0.z;
-                    rel = t1max >= tlo && t0min <= thi;
-                    if (rel) {
-                        g0 = reinterpret_cast<const ulonglong2 *>(r4)[2];
-                        g1 = reinterpret_cast<const ulonglong2 *>(r4)[3];
-                    }
-                }
-                const unsigned long long relm = __ballot(rel);
-                const int nrel = uni32(__popcll(relm));
-                if (!nrel) continue;
-                const uint32_t slot = mbcnt64(relm);
-                __builtin_amdgcn_wave_barrier();
-                if (rel) {
-                    s_rt[w][slot] = make_longlong2(((long long)h0.y << 32) | (uint32_t)h0.x,
-                                                   ((long long)h0.w << 32) | (uint32_t)h0.z);
-                    s_ra[w][slot] = make_float4(__int_as_float(h1.x), __int_as_float(h1.y), __int_as_float(h1.z),
-                                                __int_as_float(h1.w));
-                    s_rs[w][0][slot] = g0;
-                    s_rs[w][1][slot] = g1;
-                }
-                __builtin_amdgcn_wave_barrier();
-                // record flags by slot, as wave-uniform masks
-                const uint32_t qslot = (lane < nrel) ? (uint32_t)__float_as_int(s_ra[w][lane].z) : 0u;
-                const unsigned long long R0 = __ballot((qslot & kRank0) != 0);
-                const unsigned long long RC = __ballot((qslot & kCompactQ) != 0);
-                const unsigned long long RL = LONG ? __ballot((qslot & kLongQ) != 0) : 0ull;
-                n_bcast += (unsigned long long)nrel;
-                n_tests += (unsigned long long)nrel * nvalid;
-                // (1) each lane's postings against every staged record: a bit
-                // per passing record.  COALESCE'd predicates of
-                // operations.go:394-402 (NULL -> sentinels).
-                uint32_t mlo[KP], mhi[KP];
-#pragma unroll
-                for (int k = 0; k < KP; k++) mlo[k] = mhi[k] = 0;
-                const int nlo = nrel < 32 ? nrel : 32;
-#pragma unroll 2
-                for (int j = 0; j < nlo; j++) {
-                    const longlong2 rt = s_rt[w][j];
-                    const float4 ra = s_ra[w][j];
-#pragma unroll
-                    for (int k = 0; k < KP; k++) {
-                        bool pass = (pt[k].y >= rt.x) & (pt[k].x <= rt.y) & (pa[k].y >= ra.x) & (pa[k].x <= ra.y);
-                        if (OWNER) {
-                            const int32_t own = __float_as_int(ra.w);
-                            pass &= (own < 0) | (pown[k] == own);
-                        }
-                        mlo[k] |= (uint32_t)pass << j;
-                    }
-                }
-#pragma unroll 2
-                for (int j = 32; j < nrel; j++) {
-                    const longlong2 rt = s_rt[w][j];
-                    const float4 ra = s_ra[w][j];
-#pragma unroll
-                    for (int k = 0; k < KP; k++) {
-                        bool pass = (pt[k].y >= rt.x) & (pt[k].x <= rt.y) & (pa[k].y >= ra.x) & (pa[k].x <= ra.y);
-                        if (OWNER) {
-                            const int32_t own = __float_as_int(ra.w);
-                            pass &= (own < 0) | (pown[k] == own);
-                        }
-                        mhi[k] |= (uint32_t)pass << (j - 32);
-                    }
-                }
-                for (int k = 0; k < KP; k++) {
-                const unsigned long long m = pv[k] ? (((unsigned long long)mhi[k] << 32) | mlo[k]) : 0ull;
-                if (!__ballot(m != 0ull)) continue;
-                // (2) smallest shared cell only (SQL DISTINCT, Q13): a rank-0 record
-                // (the query's first cell) or a posting at its entity's first cell
-                // has no smaller cell on one side; otherwise the near-prefix
-                // signatures decide -- overlap: drop; none and either prefix
-                // compact: keep (exact); both footprints long: keep, tagged (the
-                // tagged set is deduplicated after the join); else exact merge.
-                unsigned long long keep = pfirst[k] ? m : (m & R0);
-                unsigned long long need = m & ~keep;
-                if (!usig) {  // lazy signatures: the lanes that need them now
-                    const bool want = need != 0ull && !lsig[k];
-                    if (__ballot(want)) {
-                        if (want) {
-                            const uint64_t p = d.p0 + (uint64_t)(lane + 64 * k);
-                            ps01[k] = ix.b_sig[2 * p];
-                            ps23[k] = ix.b_sig[2 * p + 1];
-                            lsig[k] = true;
-                        }
-                    }
-                }
-                // lane-major (each lane walks its own checks): full batches
-                while (need) {
-                    const int j = __builtin_ctzll(need);
-                    need &= need - 1;
-                    const ulonglong2 c0 = s_rs[w][0][j], c1 = s_rs[w][1][j];
-                    if (((c0.x & ps01[k].x) | (c0.y & ps01[k].y) | (c1.x & ps23[k].x) | (c1.y & ps23[k].y)) != 0ull) continue;
-                    // (without long postings every posting's prefix is compact:
-                    // all of its entity's cells lie in an 8 x 8 window)
-                    bool kp = !LONG || pcompact[k] || ((RC >> j) & 1ull) || (plong[k] && ((RL >> j) & 1ull));
-                    if (LONG && !kp) {  // neither prefix compact, not both long (rare; needs long postings)
-                        const uint32_t q = (uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags;
-                        kp = no_smaller_shared<2>(ix, pent[k], cell_of_slot(ix, d.slot), a.qv.cells + a.qv.offs[q],
-                                                 a.qv.offs[q + 1] - a.qv.offs[q]);
-                    }
-                    if (kp) keep |= 1ull << j;
-                }
-                // (3) emission, the batch's pairs contiguous per stream (pairs;
-                // long x long keys): lane-major (each lane's pairs after the
-                // lanes before it; iterations = the largest lane count) at low
-                // pass density, else record-major (one coalesced row per record:
-                // dense batches would scatter too many lane stores).  Both
-                // streams' counts ride one scan (16-bit halves: <= 64 x 64).
-                const unsigned long long tagm = (LONG && plong[k]) ? (keep & RL) : 0ull;
-                const uint32_t cu = (uint32_t)__popcll(keep & ~tagm), ct = (uint32_t)__popcll(tagm);
-                const uint32_t incl = wave_incl_scan(cu | (ct << 16));
-                const uint32_t tot = (uint32_t)uni32(__builtin_amdgcn_readlane((int)incl, 63));
-                const int total_u = (int)(tot & 0xffffu), total_t = LONG ? (int)(tot >> 16) : 0;
-                if (!(total_u | total_t)) continue;
-                WaveOut::Span su{}, st{};
-                if (total_u) su = out.reserve(a.out.ps, total_u);
-                if (LONG && total_t) st = tout.reserve(a.out.ts, total_t);
-                const bool wu = out.have != 0, wt = LONG && tout.have != 0;  // else counted only (rerun)
-                if ((int64_t)(total_u + total_t) * kEmitDensity <= (int64_t)nrel * __popcll(vm[k])) {
-                    // (one loop per stream: no divergent double bodies)
-                    if (!LONG && kOutStage && wu && total_u <= kOutStage) {  // (long variants: direct, no VGPR headroom)
-                        // each lane's pairs into the wave's LDS stage (one 8-B
-                        // LDS store per pair), then the batch leaves as runs of
-                        // consecutive slots: full-width coalesced global stores
-                        // instead of one scattered 4-B store per pair and array
-                        uint32_t iu = (incl & 0xffffu) - cu;
-                        unsigned long long kk = keep & ~tagm;
-                        while (kk) {
-                            const int j = __builtin_ctzll(kk);
-                            kk &= kk - 1;
-                            s_out[w][iu++] = make_uint2((uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags, pent[k]);
-                        }
-                        __builtin_amdgcn_wave_barrier();
-                        for (int p = lane; p < total_u; p += 64) {
-                            const uint2 v = s_out[w][p];
-                            const unsigned long long pos = su.at((unsigned long long)p);
-                            a.out.q[pos] = v.x;
-                            a.out.e[pos] = v.y;
-                        }
-                        __builtin_amdgcn_wave_barrier();
-                    } else if (wu) {
-                        unsigned long long iu = (incl & 0xffffu) - cu, kk = keep & ~tagm;
-                        while (kk) {
-                            const int j = __builtin_ctzll(kk);
-                            kk &= kk - 1;
-                            const uint32_t q = (uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags;
-                            const unsigned long long pos = su.at(iu++);
-                            a.out.q[pos] = q;
-                            a.out.e[pos] = pent[k];
-                        }
-                    }
-                    if (LONG && wt) {
-                        unsigned long long it = (incl >> 16) - ct, kk = tagm;
-                        while (kk) {
-                            const int j = __builtin_ctzll(kk);
-                            kk &= kk - 1;
-                            const uint32_t q = (uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags;
-                            a.out.tk[st.at(it++)] = tag_key(q, pent[k], a.out.eb, a.out.hbm);
-                        }
-                    }
-                } else {
-                    const unsigned long long lm = LONG ? __ballot(plong[k]) : 0ull;
-                    unsigned long long ou = 0, ot = 0;
-                    for (int j = 0; j < nrel; j++) {
-                        const unsigned long long kj = __ballot((keep >> j) & 1ull);
-                        if (!kj) continue;
-                        const unsigned long long kt = (LONG && ((RL >> j) & 1ull)) ? (kj & lm) : 0ull, ku = kj & ~kt;
-                        const uint32_t q =
-                            (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s_ra[w][j].z)) & ~kQFlags;
-                        if ((ku >> lane) & 1ull) {
-                            const unsigned long long pos = su.at(ou + mbcnt64(ku));
-                            if (wu) {
-                                a.out.q[pos] = q;
-                                a.out.e[pos] = pent[k];
-                            }
-                        }
-                        if (LONG && ((kt >> lane) & 1ull)) {
-                            const unsigned long long pos = st.at(ot + mbcnt64(kt));
-                            if (wt) a.out.tk[pos] = tag_key(q, pent[k], a.out.eb, a.out.hbm);
-                        }
-                        ou += (unsigned long long)__popcll(ku);
-                        ot += (unsigned long long)__popcll(kt);
-                    }
-                }
-                }  // k
             }
         }
     }
@@ -2523,7 +2178,6 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         DSS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
         n_cu_ = ncu > 0 ? ncu : 256;
     }
-    const int kp = join_kp_ == 2 ? 2 : 1;  // 64-posting tiles per join unit (postings per lane)
     int64_t ucap = std::max<int64_t>(units_cap_hint_, 1024);  // per region
     // units of cells with long-footprint postings (idx->s_lfp) go to a second
     // set of queues joined by the long variant; the rest by the short one
@@ -2537,7 +2191,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         DSS_HIP(hipMemsetAsync(ctl + kCtlUnits, 0, kR * sizeof(unsigned long long), s));
         DSS_HIP(hipMemsetAsync(ctl + kCtlUnitsL, 0, kR * sizeof(unsigned long long), s));
         hipLaunchKernelGGL(k_units, dim3(ugrid), dim3(kBlock), 0, s, ix, skey, dnkeys, Regions{ctl + kCtlUnits, ucap},
-                           units, Regions{ctl + kCtlUnitsL, ucap_l}, units_l, (uint32_t)(64 * kp));
+                           units, Regions{ctl + kCtlUnitsL, ucap_l}, units_l, 64u);
         hipLaunchKernelGGL(k_unit_ranges, dim3((unsigned)n_cu_ * 8), dim3(kBlock), 0, s, ix,
                            Regions{ctl + kCtlUnits, ucap}, units, (const uint32_t *)sval, (const QRec *)recs,
                            (const unsigned long long *)(ctl + kCtlDq), (long long)idx->tbase, idx->qshift);
@@ -2552,7 +2206,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     ja.ix = ix;
     ja.qv = qv;
     ja.lazy_sig_recs = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(lazy_sig_recs_, 0xffffffffll));
-    const unsigned nblocks = (unsigned)n_cu_ * (join_kp_ == 2 ? kJoinKpBlocksPerCU : kJoinBlocksPerCU);
+    const unsigned nblocks = (unsigned)n_cu_ * kJoinBlocksPerCU;
     if (out_rcap_ == 0) out_rcap_ = ((int64_t)nq * 16 / kRegions / kOutChunk + 2) * kOutChunk;
     if (any_long && tag_rcap_ == 0) tag_rcap_ = ((int64_t)nq * 4 / kRegions / kOutChunk + 2) * kOutChunk;
     const int qb = bits_for(nq), eb = bits_for(idx->n_e);
@@ -2589,13 +2243,11 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         ja.out = OutArgs{oq, oe, OutStream{out_rcap_, fills, ctl + kCtlOut}, tk, OutStream{tag_rcap_, tfills, ctl + kCtlTOut},
                          eb, hbm, cnt};
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
-        auto kshort = kp == 2 ? (q_owner ? k_join_kp<true, false, 2> : k_join_kp<false, false, 2>)
-                              : (q_owner ? k_join<true, false> : k_join<false, false>);
+        auto kshort = q_owner ? k_join<true, false> : k_join<false, false>;
         hipLaunchKernelGGL(kshort, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
                            (const uint32_t *)sval, (const Unit *)units, ctl + kCtlQueue);
         if (any_long) {  // the same output streams, continued
-            auto klong = kp == 2 ? (q_owner ? k_join_kp<true, true, 2> : k_join_kp<false, true, 2>)
-                                 : (q_owner ? k_join<true, true> : k_join<false, true>);
+            auto klong = q_owner ? k_join<true, true> : k_join<false, true>;
             JoinArgs jl = ja;
             jl.ur = Regions{ctl + kCtlUnitsL, ucap_l};
             hipLaunchKernelGGL(klong, dim3(nblocks), dim3(64 * kWaves), 0, s, jl, (const QRec *)recs,

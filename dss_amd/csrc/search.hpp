@@ -124,14 +124,9 @@ class SearchEngine {
                       const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
                       const int32_t *q_owner, int64_t nqc, hipStream_t s, dssg_pairs *out);
     int64_t small_max_q() const { return small_max_q_; }
-    // postings per lane of the tiled join: 1 = k_join (a unit = one
-    // 64-posting tile), 2 = k_join_kp<2> (a unit = two consecutive tiles of a
-    // cell, its records staged once for both)
-    void set_join_kp(int64_t v) { join_kp_ = v == 2 ? 2 : 1; }
 
    private:
     int64_t small_max_q_ = 4096, small_cap_ = 0;
-    int join_kp_ = 1;
     DevBuf<unsigned long long> small_cnt_;
     DevBuf<unsigned char> tmp_, tmp2_;
     // query side

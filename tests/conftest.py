@@ -31,22 +31,16 @@ def golden_search():
     return dict(np.load(os.path.join(ROOT, "tests", "golden", "search.npz"), allow_pickle=False))
 
 
-@pytest.fixture(params=["units", "kp2", "small"])
+@pytest.fixture(params=["units", "small"])
 def join_path(request):
-    """Run a search test through every join of the shared context: "units"
-    (the tiled band join, one 64-posting tile per unit: k_join), "kp2" (two
-    tiles per unit, two postings per lane: k_join_kp<2>) -- both with
-    small_search = 0 -- and "small" (the one-launch small-batch join,
-    k_small_join, forced for every batch)."""
+    """Run a search test through both joins of the shared context: "units"
+    (the tiled band join, one 64-posting tile per unit: k_join; small_search
+    = 0) and "small" (the one-launch small-batch join, k_small_join, forced
+    for every batch)."""
     from dss_amd import _lib
     ctx = _lib.context(0)
     ctx.set_tuning("small_search", 1 << 24 if request.param == "small" else 0)
-    ctx.set_tuning("join_kp", 2 if request.param == "kp2" else 1)
     try:
         yield request.param
     finally:
         ctx.set_tuning("small_search", 4096)
-        ctx.set_tuning("join_kp", JOIN_KP_DEFAULT)
-
-
-JOIN_KP_DEFAULT = 1  # SearchEngine::join_kp_
