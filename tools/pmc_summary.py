@@ -20,7 +20,9 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.search(r"(k_\w+)", name)
+    """Kernel name with its template arguments (k_join<false, true>): the
+    variants of one kernel are summarized apart."""
+    m = re.search(r"(k_\w+(?:<[^>(]*>)?)", name)
     return m.group(1) if m else name[:40]
 
 
@@ -77,6 +79,19 @@ def main():
         print(",".join(row))
         out[k] = {"dispatches": len(ds), "avg_ms": (sum(ds) / len(ds)) if ds else None,
                   "fetch_kib": f, "write_kib": w, "hbm_bytes_per_launch": hbm}
+    # a kernel launched as several template variants per search (k_join's
+    # short and long variants): the base name carries the per-search sum of
+    # the variants' per-launch averages
+    groups = {}
+    for k, v in out.items():
+        if "<" in k and v["hbm_bytes_per_launch"] is not None:
+            groups.setdefault(k.split("<")[0], []).append(v)
+    for base, vs in groups.items():
+        if len(vs) > 1 and base not in out:
+            out[base] = {"dispatches": sum(v["dispatches"] for v in vs), "avg_ms": sum(v["avg_ms"] or 0 for v in vs),
+                         "fetch_kib": sum(v["fetch_kib"] for v in vs), "write_kib": sum(v["write_kib"] for v in vs),
+                         "hbm_bytes_per_launch": sum(v["hbm_bytes_per_launch"] for v in vs),
+                         "note": "per search: the sum over the template variants, each launched once per search"}
     if a.json:
         with open(a.json, "w") as fh:
             json.dump({"source": a.source, "queries": a.queries, "intents": a.intents, "skip_first": a.skip_first,
