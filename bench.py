@@ -378,8 +378,9 @@ def main():
     torch.cuda.synchronize()
     build_s = time.time() - tb
     n_post = int(ctx.L.dssg_index_num_postings(index))
+    free_b, total_b = torch.cuda.mem_get_info(local)
     log(f"[rank {rank}] mode {mode}, setup {time.time() - t_setup:.1f}s, intent cover {cover_i_s:.2f}s, index build "
-        f"{build_s:.2f}s, postings {n_post}")
+        f"{build_s:.2f}s, postings {n_post}, HBM free {free_b / 2**30:.1f} of {total_b / 2**30:.1f} GiB")
     sort_ph = None
     if rank == 0 and mode != "sharded":
         sort_ph = (sort_phase(ctx, torch, dev, i_offs_t, i_cells_t) if not large else

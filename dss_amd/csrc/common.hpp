@@ -46,8 +46,7 @@ struct DevBuf {
         // 25 % growth slack, at most 256 MiB of it
         const size_t slack = std::min(n / 4, ((size_t)256 << 20) / sizeof(T));
         size_t c = n < 16 ? 16 : n + slack;
-        DSS_HIP(hipMalloc(&p, c * sizeof(T)));
-        cap = c;
+        alloc(c);
         return p;
     }
     // no growth slack: for the long-lived index arrays (tens of GB at the
@@ -57,9 +56,19 @@ struct DevBuf {
         if (n <= cap && p) return p;
         release();
         const size_t c = n < 16 ? 16 : n;
-        DSS_HIP(hipMalloc(&p, c * sizeof(T)));
-        cap = c;
+        alloc(c);
         return p;
+    }
+    void alloc(size_t c)
+    {
+        const hipError_t e = hipMalloc(&p, c * sizeof(T));
+        if (e != hipSuccess) {
+            p = nullptr;
+            cap = 0;
+            (void)hipGetLastError();
+            throw Error(DSSG_ERR_DEVICE, "hipMalloc of " + std::to_string(c * sizeof(T)) + " bytes: " + hipGetErrorString(e));
+        }
+        cap = c;
     }
 };
 
