@@ -790,29 +790,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
     return x;
 }
 
-// 64-bit wave maximum by DPP (no LDS round trips): lanes a step does not
-// feed see the identity (LLONG_MIN).
-template <int ctl, int rmask>
-__device__ __forceinline__ long long dpp_i64(long long x)
-{
-    const int lo = (int)(uint32_t)(unsigned long long)x, hi = (int)(uint32_t)((unsigned long long)x >> 32);
-    const uint32_t l = (uint32_t)__builtin_amdgcn_update_dpp(0, lo, ctl, rmask, 0xf, false);
-    const uint32_t h = (uint32_t)__builtin_amdgcn_update_dpp((int)0x80000000, hi, ctl, rmask, 0xf, false);
-    return (long long)(((unsigned long long)h << 32) | l);
-}
-__device__ __forceinline__ long long wave_max_i64(long long x)
-{
-    x = max(x, dpp_i64<0x111, 0xf>(x));  // row_shr:1
-    x = max(x, dpp_i64<0x112, 0xf>(x));  // row_shr:2
-    x = max(x, dpp_i64<0x114, 0xf>(x));  // row_shr:4
-    x = max(x, dpp_i64<0x118, 0xf>(x));  // row_shr:8
-    x = max(x, dpp_i64<0x142, 0xa>(x));  // row_bcast:15
-    x = max(x, dpp_i64<0x143, 0xc>(x));  // row_bcast:31
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(unsigned long long)x, 63);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((unsigned long long)x >> 32), 63);
-    return (long long)(((unsigned long long)hi << 32) | lo);
-}
-
 // Wave maximum (lane 63 of a DPP max-scan; no LDS round trips).
 __device__ __forceinline__ uint32_t wave_max(uint32_t x)
 {
@@ -823,6 +800,18 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x)
     x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));  // row_bcast:15
     x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));  // row_bcast:31
     return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// An upper bound (within 2^24 us) of the wave maximum of a 64-bit time, by a
+// 32-bit DPP max of the times' top bits: the tile hull only needs to contain
+// every posting's window (a looser hull stages a few more records; the
+// per-lane tests stay exact).  ~8 VALU against ~32 for a 64-bit DPP max.
+__device__ __forceinline__ long long wave_max_bound(long long x)
+{
+    const long long h = x >> 24;  // arithmetic: order preserving
+    const int32_t c = h > (long long)INT32_MAX ? INT32_MAX : h < (long long)INT32_MIN ? INT32_MIN : (int32_t)h;
+    const int32_t m = (int32_t)(wave_max((uint32_t)c ^ 0x80000000u) ^ 0x80000000u);
+    return m == INT32_MAX ? LLONG_MAX : ((long long)m << 24) + ((1ll << 24) - 1);
 }
 
 __device__ __forceinline__ uint32_t lb_u32(const uint32_t *x, uint32_t lo, uint32_t hi, uint32_t v)
@@ -1225,7 +1214,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
         if (!(d.np & kUnitLong)) {
             const long long m = tmin2(pt.x, pt.y);
             t0min = readlane64(m, 0);  // <= every t0 of the tile
-            t1max = wave_max_i64((uint32_t)lane < np ? (pt.x > pt.y ? pt.x : pt.y) : LLONG_MIN);
+            t1max = wave_max_bound((uint32_t)lane < np ? (pt.x > pt.y ? pt.x : pt.y) : LLONG_MIN);
         }
         const uint32_t ra0 = d.n0, ra1 = d.n1, rb0 = d.w0, rb1 = d.w1;
         const bool pfirst = (pe & kFirstBit) != 0;                  // entity's smallest cell
