@@ -1013,7 +1013,7 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
 {
     __shared__ uint4 s_bx[kFpPer];
     __shared__ uint32_t s_info[kFpPer], s_sti[kFpPer][4], s_stj[kFpPer][4];
-    __shared__ int s_cb[kFpPer + 1], s_vb[kFpPer], s_nv[kFpPer], s_fl[kFpPer];
+    __shared__ int s_cb[kFpPer + 1], s_vb[kFpPer], s_nv[kFpPer], s_fl[kFpPer], s_vp[kFpPer + 1];
     __shared__ int64_t s_xo[kFpPer];
     __shared__ unsigned long long s_km[kFpPer][4], s_um[kFpPer][4];
     __shared__ double2 s_uv[kCandStageV];
@@ -1052,12 +1052,23 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
         s_cb[t + 1] = (int)ci;
         if (t == 0) s_cb[0] = 0;
         s_vb[t] = vi <= (uint32_t)kCandStageV ? (int)(vi - nvv) : -1;  // LDS offset, or -1: read from global
+        s_vp[t] = (int)(vi - nvv);
+        if (t == kFpPer - 1) s_vp[kFpPer] = (int)vi;
     }
     __syncthreads();
-    for (int fi = t >> 6; fi < kFpPer; fi += kFpBlock / 64) {  // a wave per footprint's vertices
-        const int vb = s_vb[fi];
-        if (vb < 0 || s_cb[fi + 1] == s_cb[fi]) continue;
-        for (int v = lane; v < s_nv[fi]; v += 64) s_uv[vb + v] = uv[s_xo[fi] + v];
+    // the block's staged vertices, all threads over them (vertex -> footprint
+    // by LDS search: the last footprint whose prefix is <= k holds it), so a
+    // block of small footprints (configs[3]'s 4-gons) does not walk them one
+    // footprint per wave
+    const int nvs = min(s_vp[kFpPer], kCandStageV);
+    for (int k = t; k < nvs; k += kFpBlock) {
+        int lo = 0, hi = kFpPer;  // s_vp[lo] <= k < s_vp[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_vp[mid] <= k) lo = mid;
+            else hi = mid;
+        }
+        s_uv[k] = uv[s_xo[lo] + (k - s_vp[lo])];
     }
     __syncthreads();
     const int total = s_cb[kFpPer];
