@@ -99,6 +99,15 @@ class EntityIndex:
     def num_postings(self) -> int:
         return int(self.ctx.L.dssg_index_num_postings(self.h))
 
+    def info(self) -> dict:
+        """dssg_index_info: postings, distinct cells, long-duration and
+        long-footprint postings, the largest cell's postings, dcap (us)."""
+        import ctypes as C
+        v = [C.c_int64() for _ in range(6)]
+        self.ctx.check(self.ctx.L.dssg_index_info(self.h, *[C.byref(x) for x in v]))
+        return dict(zip(["postings", "cells", "long_duration_postings", "long_footprint_postings", "max_cell_postings",
+                         "dcap_us"], [x.value for x in v]))
+
     def free(self):
         if getattr(self, "h", None):
             self.ctx.L.dssg_index_free(self.h)

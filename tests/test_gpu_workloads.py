@@ -14,7 +14,10 @@ def _keys(q, e):
     return np.sort((np.asarray(q, np.uint64) << np.uint64(32)) | np.asarray(e, np.uint64))
 
 
-@pytest.mark.parametrize("cfg,scale", [(2, 0.002), (3, 0.004), (4, 0.0004)])
+# (2, 0.1): 1M California intents and 100k queries -- hotspot cells with
+# hundreds of postings and records, and a few long footprints, so both join
+# queues (short and long variants) run in one search
+@pytest.mark.parametrize("cfg,scale", [(2, 0.002), (3, 0.004), (4, 0.0004), (2, 0.1), (3, 0.1), (4, 0.01)])
 def test_config_parity(oracle, cfg, scale, join_path):
     from dss_amd import geo, workload as W
     from dss_amd.store import EntityIndex
@@ -35,6 +38,8 @@ def test_config_parity(oracle, cfg, scale, join_path):
     oq, oe = oracle.search(io, ic, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1, None, qo, qc, qa.alt_lo, qa.alt_hi, tlo, thi)
     assert len(oq) > 0
     assert np.array_equal(_keys(gq, ge), _keys(oq, oe))
+    if (cfg, scale) == (2, 0.1):
+        assert idx.info()["long_footprint_postings"] > 0  # the long queue is exercised
 
 
 @pytest.fixture(scope="module")
