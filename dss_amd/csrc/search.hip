@@ -918,18 +918,27 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
 // start-sorted tile that is [m_first - dqmax, m_last + dcap]; the records'
 // quantised starts (their order) bracket it by binary search.  One thread
 // per unit.
-__device__ __forceinline__ uint32_t lb_rec_q(const uint32_t *sval, const QRec *recs, uint32_t lo, uint32_t hi, uint32_t v,
-                                             long long tbase, int qshift)
+__device__ __forceinline__ uint32_t lb_q(const uint32_t *sq, uint32_t lo, uint32_t hi, uint32_t v)
 {
-    while (lo < hi) {  // first record in [lo, hi) with order_q(tlo) >= v
+    while (lo < hi) {  // first record in [lo, hi) with quantised start >= v
         const uint32_t m = (lo + hi) >> 1;
-        if (order_q(recs[sval[m]].tlo, tbase, qshift) < v) lo = m + 1;
+        if (sq[m] < v) lo = m + 1;
         else hi = m;
     }
     return lo;
 }
 
-__global__ void k_unit_ranges(IndexView a, Regions ur, Unit *units, const uint32_t *sval, const QRec *recs,
+// Each sorted key's record's quantised start, contiguous: the unit-range
+// searches then probe one 4-B array instead of two dependent gathers
+// (sval, then the 64-B record) per step.
+__global__ void k_rec_q(const int64_t *dnkeys, const uint32_t *sval, const QRec *recs, long long tbase, int qshift,
+                        uint32_t *sq)
+{
+    const int64_t i = tid64();
+    if (i < *dnkeys) sq[i] = order_q(recs[sval[i]].tlo, tbase, qshift);
+}
+
+__global__ void k_unit_ranges(IndexView a, Regions ur, Unit *units, const uint32_t *sq,
                               const unsigned long long *dqslots, long long tbase, int qshift)
 {
     int64_t pre[kRegions + 1];
@@ -944,8 +953,8 @@ __global__ void k_unit_ranges(IndexView a, Regions ur, Unit *units, const uint32
         const long long m0 = tmin2(f.x, f.y), m1 = tmin2(l.x, l.y);
         const long long lo = m0 < LLONG_MIN + dq ? LLONG_MIN : m0 - dq;
         const long long hi = m1 > LLONG_MAX - a.dcap ? LLONG_MAX : m1 + a.dcap;
-        const uint32_t n0 = lb_rec_q(sval, recs, d.n0, d.n1, order_q(lo, tbase, qshift), tbase, qshift);
-        d.n1 = lb_rec_q(sval, recs, n0, d.n1, order_q(hi, tbase, qshift) + 1u, tbase, qshift);
+        const uint32_t n0 = lb_q(sq, d.n0, d.n1, order_q(lo, tbase, qshift));
+        d.n1 = lb_q(sq, n0, d.n1, order_q(hi, tbase, qshift) + 1u);
         d.n0 = n0;
     }
 }
@@ -2159,6 +2168,9 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     // order), over the device key count qo[nq] (<= nqc)
     const int64_t *dnkeys = qo + nq;
     radix_sort_pairs_dn(key, skey, val, sval, nqc, dnkeys, bits_for(idx->n_slots()) + 1, tmp_, s);
+    uint32_t *sq = key;  // (the unsorted keys are consumed)
+    hipLaunchKernelGGL(k_rec_q, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, dnkeys, (const uint32_t *)sval,
+                       (const QRec *)recs, (long long)idx->tbase, idx->qshift, sq);
     // (5) join units = 64-posting tiles of every cell the batch meets, each
     // with the records it can meet
     if (n_cu_ == 0) {
@@ -2182,11 +2194,11 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         hipLaunchKernelGGL(k_units, dim3(ugrid), dim3(kBlock), 0, s, ix, skey, dnkeys, Regions{ctl + kCtlUnits, ucap},
                            units, Regions{ctl + kCtlUnitsL, ucap_l}, units_l, 64u);
         hipLaunchKernelGGL(k_unit_ranges, dim3((unsigned)n_cu_ * 8), dim3(kBlock), 0, s, ix,
-                           Regions{ctl + kCtlUnits, ucap}, units, (const uint32_t *)sval, (const QRec *)recs,
+                           Regions{ctl + kCtlUnits, ucap}, units, (const uint32_t *)sq,
                            (const unsigned long long *)(ctl + kCtlDq), (long long)idx->tbase, idx->qshift);
         if (any_long)
             hipLaunchKernelGGL(k_unit_ranges, dim3((unsigned)n_cu_ * 2), dim3(kBlock), 0, s, ix,
-                               Regions{ctl + kCtlUnitsL, ucap_l}, units_l, (const uint32_t *)sval, (const QRec *)recs,
+                               Regions{ctl + kCtlUnitsL, ucap_l}, units_l, (const uint32_t *)sq,
                                (const unsigned long long *)(ctl + kCtlDq), (long long)idx->tbase, idx->qshift);
     };
     build_units();
