@@ -392,12 +392,26 @@ def main():
         # the timed steps use the library's own RCCL exchange when native
         sharded = shard.ShardedSearch(ctx, index, ranges, stage_host=stage_host)
         if exchange == "native":
-            uid = torch.zeros(_lib.COMM_ID_BYTES, dtype=torch.uint8, device=dev)
-            if rank == 0:
-                uid.copy_(torch.frombuffer(bytearray(shard.NativeComm.unique_id(ctx)), dtype=torch.uint8))
-            dist.broadcast(uid, 0)  # bootstrap only: the id travels once
-            native = shard.NativeShardedSearch(ctx, shard.NativeComm(ctx, world, rank, bytes(uid.cpu().numpy())),
-                                               index, ranges)
+            # the library's own communicator; if any rank cannot open it (no
+            # RCCL to dlopen, init error) every rank falls back to the torch
+            # exchange, agreed by one all-reduce, and the line says so
+            ok = torch.ones(1, device=dev)
+            err = None
+            try:
+                uid = torch.zeros(_lib.COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+                if rank == 0:
+                    uid.copy_(torch.frombuffer(bytearray(shard.NativeComm.unique_id(ctx)), dtype=torch.uint8))
+                dist.broadcast(uid, 0)  # bootstrap only: the id travels once
+                native = shard.NativeShardedSearch(ctx, shard.NativeComm(ctx, world, rank, bytes(uid.cpu().numpy())),
+                                                   index, ranges)
+            except Exception as e:  # noqa: BLE001 -- reported in the result line
+                err = f"{type(e).__name__}: {e}"
+                ok.zero_()
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if ok.item() < 1:
+                log(f"[rank {rank}] native exchange unavailable ({err}); using the torch exchange")
+                native = None
+                exchange = f"torch (native exchange init failed on some rank: {err})"
 
     def shard_search(cells, timed_phases=False):
         if native is not None and not timed_phases:
