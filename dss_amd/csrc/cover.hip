@@ -581,12 +581,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAST ? DSS_S
 
 __device__ __forceinline__ int num_edges(uint8_t md, int nv) { return md == MODE_LOOP ? nv : (md == MODE_POLYLINE ? nv - 1 : 0); }
 
+// Per footprint its clipped-edge items (descent footprints only), and the
+// list of descent footprints (any order; one atomic per wave).
 __global__ void k_edge_counts(int64_t n, const uint8_t *mode, const uint8_t *fmask, const uint8_t *flags, const int32_t *nvx,
-                              int64_t *cnt)
+                              int64_t *cnt, uint32_t *dlist, unsigned int *dlist_n)
 {
-    int64_t f = tid64();
-    if (f >= n) return;
-    cnt[f] = (flags[f] & FL_FAST) ? 0 : (int64_t)__builtin_popcount(fmask[f]) * num_edges(mode[f], nvx[f]);
+    const int64_t f = tid64();
+    bool desc = false;
+    if (f < n) {
+        desc = !(flags[f] & FL_FAST) && mode[f] != MODE_NONE;
+        cnt[f] = desc ? (int64_t)__builtin_popcount(fmask[f]) * num_edges(mode[f], nvx[f]) : 0;
+    }
+    const unsigned long long m = __ballot(desc);
+    if (!m) return;
+    const int lane = threadIdx.x & 63, leader = __builtin_ctzll(m);
+    unsigned int b = 0;
+    if (lane == leader) b = atomicAdd(dlist_n, (unsigned int)__popcll(m));
+    b = (unsigned int)__shfl((int)b, leader);
+    if (desc) dlist[b + cmpct::lanes_below(m)] = (uint32_t)f;
 }
 
 // Clip every edge to every touched face (ascending face order), one thread
@@ -657,13 +669,14 @@ __device__ bool contains_node(const LoopView &l, bool planar, const double4 *cli
 // Count (pass 0) or write (pass 1) start nodes; big loops also get whole-face
 // nodes for faces without edges whose centre the loop contains.
 template <int PASS>
-__global__ __launch_bounds__(64) void k_start(int64_t n, const int64_t *xoff, const V3 *xyz, const uint8_t *mode, const uint8_t *fmask,
+__global__ __launch_bounds__(64) void k_start(int64_t nd, const uint32_t *dlist, const int64_t *xoff, const V3 *xyz, const uint8_t *mode, const uint8_t *fmask,
                         const uint8_t *flags, const uint8_t *origin_in, const int32_t *nvx, const int64_t *eoff,
                         const double4 *clip_c, const uint8_t *cflags, int64_t *cnt, const int64_t *soff,
                         uint32_t *nf, uint64_t *nid, uint32_t *ni, uint32_t *nj, uint32_t *nmeta)
 {
-    int64_t f = tid64();
-    if (f >= n) return;
+    const int64_t k = tid64();
+    if (k >= nd) return;
+    const int64_t f = dlist[k];  // a descent footprint (k_edge_counts)
     uint8_t md = mode[f];
     int64_t c = 0;
     if (md != MODE_NONE && !(flags[f] & FL_FAST)) {
@@ -1787,11 +1800,17 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
                        lng, radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j,
                        finfo, fbox, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
     int64_t *eoff = eoff_.ensure(n + 1);
-    hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv);
+    uint32_t *dlist = dlist_.ensure(n + 1);
+    unsigned int *dlist_n = dlist_n_.ensure(1);
+    DSS_HIP(hipMemsetAsync(dlist_n, 0, sizeof(unsigned int), s));
+    hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv, dlist, dlist_n);
     exclusive_scan_i64(nv, eoff, n, tmp_, s);
     int64_t ne = 0;
+    unsigned int nd_u = 0;
     DSS_HIP(hipMemcpyAsync(&ne, eoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipMemcpyAsync(&nd_u, dlist_n, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
+    const int64_t nd = nd_u;  // descent footprints (big, multi-face, polyline): the only ones k_start visits
     if (std::getenv("DSS_COVER_STATS"))
         fprintf(stderr, "[cover] n %lld vertices %lld clipped edges %lld\n", (long long)n, (long long)nx, (long long)ne);
     // direct candidates (most footprints): the cells of each one's bound,
@@ -1814,18 +1833,21 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
                            clip_f, clip_c, cflags);
     }
     int64_t *soff = soff_.ensure(n + 1);
-    hipLaunchKernelGGL(k_start<0>, dim3(grid_for(n, 64)), dim3(64), 0, s, n, xoff, xyz, mode, fmask, flags, orig, nvx,
-                       eoff, clip_c, cflags, nv, soff, nullptr, nullptr, nullptr, nullptr, nullptr);
-    exclusive_scan_i64(nv, soff, n, tmp_, s);
     int64_t nn = 0;
-    DSS_HIP(hipMemcpyAsync(&nn, soff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    DSS_HIP(hipStreamSynchronize(s));
+    if (nd > 0) {  // (none: no start nodes, no second sync)
+        DSS_HIP(hipMemsetAsync(nv, 0, sizeof(int64_t) * n, s));
+        hipLaunchKernelGGL(k_start<0>, dim3(grid_for(nd, 64)), dim3(64), 0, s, nd, dlist, xoff, xyz, mode, fmask, flags,
+                           orig, nvx, eoff, clip_c, cflags, nv, soff, nullptr, nullptr, nullptr, nullptr, nullptr);
+        exclusive_scan_i64(nv, soff, n, tmp_, s);
+        DSS_HIP(hipMemcpyAsync(&nn, soff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipStreamSynchronize(s));
+    }
     int cur = 0;
     Frontier *F = &fr_[cur];
     F->ensure(nn + 1);
     if (nn > 0)
-        hipLaunchKernelGGL(k_start<1>, dim3(grid_for(n, 64)), dim3(64), 0, s, n, xoff, xyz, mode, fmask, flags, orig, nvx,
-                           eoff, clip_c, cflags, nullptr, soff, F->f.p, F->id.p, F->i.p, F->j.p, F->meta.p);
+        hipLaunchKernelGGL(k_start<1>, dim3(grid_for(nd, 64)), dim3(64), 0, s, nd, dlist, xoff, xyz, mode, fmask, flags,
+                           orig, nvx, eoff, clip_c, cflags, nullptr, soff, F->f.p, F->id.p, F->i.p, F->j.p, F->meta.p);
     int *any_open = flag_.ensure(1);
     for (int iter = 0; iter < 32 && nn > 0; iter++) {
         uint8_t *act = act_.ensure(nn + 1);
