@@ -495,7 +495,7 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
     // in those points' bound (a face corner inside the part included, since
     // the part's boundary then reaches both face edges through it).
     uint8_t fl = (md == MODE_POLYLINE || (md == MODE_LOOP && small)) ? FL_SMALL : 0;
-    // Planar containment (see contains_node) and direct candidates: a small
+    // Planar containment (see planar_contains) and direct candidates: a small
     // loop inside one face whose (u,v) bound does not come near OriginPoint's
     // projection.
     if (md == MODE_LOOP && small && inner && __builtin_popcount(mask) == 1) {
@@ -648,10 +648,9 @@ __device__ V3 node_center(int face, uint32_t i0, uint32_t j0, int level)
 // path independent, so it equals the parity S2 counts along OriginPoint->p
 // (loop.go bruteForceContainsPoint), flipped by originInside; FL_PLANAR
 // excludes loops whose bound surrounds OriginPoint's own projection.
-__device__ bool contains_node(const LoopView &l, bool planar, const double4 *clip, int ne, int face, uint32_t i0, uint32_t j0,
-                              int level)
+__device__ __forceinline__ bool planar_contains(bool origin_inside, const double4 *clip, int ne, uint32_t i0, uint32_t j0,
+                                                int level)
 {
-    if (!planar) return loop_contains(l, node_center(face, i0, j0, level));
     double size = (double)(1u << (kMaxLevel - level));
     const double half = 0.5 / (double)kMaxSize;
     double uc = st_to_uv(half * (2.0 * (double)i0 + size)), vc = st_to_uv(half * (2.0 * (double)j0 + size));
@@ -663,7 +662,7 @@ __device__ bool contains_node(const LoopView &l, bool planar, const double4 *cli
             if (uc < x) par = !par;
         }
     }
-    return l.origin_inside != par;
+    return origin_inside != par;
 }
 
 // Count (pass 0) or write (pass 1) start nodes; big loops also get whole-face
@@ -750,72 +749,118 @@ __device__ bool polyline_intersects_cell(const V3 *p, int nv, int face, double u
 }
 
 // Classify each frontier node: 0 drop, 1 keep (done), 2 subdivide (4 children).
+// The exact S2 paths (centre containment of a non-planar loop, a polyline's
+// level-13 cell test) are deferred to k_expand_exact through a list, so this
+// kernel does not carry their registers (248 VGPRs, 2 waves per SIMD, when
+// they were inlined) for the planar majority.
 __global__ __launch_bounds__(64) void k_expand_count(int64_t nn, const uint32_t *nf, const uint32_t *ni, const uint32_t *nj,
                                const uint32_t *nmeta, uint8_t *act, int64_t *cnt, const int64_t *xoff, const V3 *xyz,
                                const uint8_t *mode, const uint8_t *fmask, const uint8_t *origin_in, const int32_t *nvx,
                                const int64_t *eoff, const double4 *clip_f, const double4 *clip_c, const uint8_t *cflags,
-                               const uint8_t *flags)
+                               const uint8_t *flags, uint32_t *xlist, unsigned int *xlist_n)
 {
-    int64_t k = tid64();
-    if (k >= nn) return;
-    uint32_t m = nmeta[k];
-    uint8_t a;
-    if (meta_done(m)) {
-        a = 1;
-    } else {
-        uint32_t f = nf[k];
-        int level = meta_level(m), face = meta_face(m);
-        uint8_t md = mode[f];
-        int nv = nvx[f], ne = num_edges(md, nv);
-        uint8_t mask = fmask[f];
-        int fi = __builtin_popcount((unsigned)mask & ((1u << face) - 1u));
-        int64_t base = eoff[f] + (int64_t)fi * ne;
-        uint32_t size = 1u << (kMaxLevel - level);
-        double ulo = st_to_uv((double)ni[k] / (double)kMaxSize), uhi = st_to_uv((double)(ni[k] + size) / (double)kMaxSize);
-        double vlo = st_to_uv((double)nj[k] / (double)kMaxSize), vhi = st_to_uv((double)(nj[k] + size) / (double)kMaxSize);
-        const V3 *p = xyz + xoff[f];
-        if (level < kCoverLevel) {
-            const double pm = kCoarsePad;
-            bool hit = false;
-            for (int e = 0; e < ne && !hit; e++) {
-                if (!(cflags[base + e] & 2)) continue;
-                double4 c = clip_c[base + e];
-                hit = edge_intersects_rect(c.x, c.y, c.z, c.w, ulo - pm, uhi + pm, vlo - pm, vhi + pm);
-            }
-            if (!hit && md == MODE_POLYLINE) {
-                for (int i = 0; i < nv && !hit; i++) {
-                    double u, v;
-                    hit = face_xyz_to_uv(face, p[i], u, v) && (ulo - pm) <= u && u <= (uhi + pm) && (vlo - pm) <= v && v <= (vhi + pm);
-                }
-            }
-            if (hit) a = 2;
-            else if (md == MODE_LOOP) {
-                LoopView l{p, nv, origin_in[f] != 0};
-                a = contains_node(l, (flags[f] & FL_PLANAR) != 0, clip_f + base, ne, face, ni[k], nj[k], level) ? 1 : 0;
-            } else a = 0;
+    const int64_t k = tid64();
+    bool defer = false;
+    if (k < nn) {
+        const uint32_t m = nmeta[k];
+        uint8_t a = 0;
+        if (meta_done(m)) {
+            a = 1;
         } else {
-            bool in;
-            if (md == MODE_LOOP) {
+            const uint32_t f = nf[k];
+            const int level = meta_level(m), face = meta_face(m);
+            const uint8_t md = mode[f];
+            const int nv = nvx[f], ne = num_edges(md, nv);
+            const uint8_t mask = fmask[f];
+            const int fi = __builtin_popcount((unsigned)mask & ((1u << face) - 1u));
+            const int64_t base = eoff[f] + (int64_t)fi * ne;
+            const uint32_t size = 1u << (kMaxLevel - level);
+            const double ulo = st_to_uv((double)ni[k] / (double)kMaxSize),
+                         uhi = st_to_uv((double)(ni[k] + size) / (double)kMaxSize);
+            const double vlo = st_to_uv((double)nj[k] / (double)kMaxSize),
+                         vhi = st_to_uv((double)(nj[k] + size) / (double)kMaxSize);
+            const bool planar = (flags[f] & FL_PLANAR) != 0;
+            if (level < kCoverLevel) {
+                const double pm = kCoarsePad;
+                bool hit = false;
+                for (int e = 0; e < ne && !hit; e++) {
+                    if (!(cflags[base + e] & 2)) continue;
+                    const double4 c = clip_c[base + e];
+                    hit = edge_intersects_rect(c.x, c.y, c.z, c.w, ulo - pm, uhi + pm, vlo - pm, vhi + pm);
+                }
+                if (!hit && md == MODE_POLYLINE) {
+                    const V3 *p = xyz + xoff[f];
+                    for (int i = 0; i < nv && !hit; i++) {
+                        double u, v;
+                        hit = face_xyz_to_uv(face, p[i], u, v) && (ulo - pm) <= u && u <= (uhi + pm) && (vlo - pm) <= v &&
+                              v <= (vhi + pm);
+                    }
+                }
+                if (hit) a = 2;
+                else if (md == MODE_LOOP) {
+                    if (planar) a = planar_contains(origin_in[f] != 0, clip_f + base, ne, ni[k], nj[k], level) ? 1 : 0;
+                    else defer = true;
+                } else a = 0;
+            } else if (md == MODE_LOOP) {
                 // loop.go IntersectsCell: padded edge test, else centre containment
                 const double pm = kFinePad;
-                in = false;
+                bool in = false;
                 for (int e = 0; e < ne && !in; e++) {
                     if (!(cflags[base + e] & 1)) continue;
-                    double4 c = clip_f[base + e];
+                    const double4 c = clip_f[base + e];
                     in = edge_intersects_rect(c.x, c.y, c.z, c.w, ulo - pm, uhi + pm, vlo - pm, vhi + pm);
                 }
-                if (!in) {
-                    LoopView l{p, nv, origin_in[f] != 0};
-                    in = contains_node(l, (flags[f] & FL_PLANAR) != 0, clip_f + base, ne, face, ni[k], nj[k], level);
-                }
+                if (in) a = 1;
+                else if (planar) a = planar_contains(origin_in[f] != 0, clip_f + base, ne, ni[k], nj[k], level) ? 1 : 0;
+                else defer = true;
             } else {
-                in = polyline_intersects_cell(p, nv, face, ulo, uhi, vlo, vhi);
+                defer = true;  // polyline.go IntersectsCell
             }
-            a = in ? 1 : 0;
+        }
+        if (!defer) {
+            act[k] = a;
+            cnt[k] = a == 2 ? 4 : a;
         }
     }
-    act[k] = a;
-    cnt[k] = a == 2 ? 4 : a;
+    const unsigned long long dm = __ballot(defer);
+    if (!dm) return;
+    const int lane = threadIdx.x & 63, leader = __builtin_ctzll(dm);
+    unsigned int b = 0;
+    if (lane == leader) b = atomicAdd(xlist_n, (unsigned int)__popcll(dm));
+    b = (unsigned int)__shfl((int)b, leader);
+    if (defer) xlist[b + cmpct::lanes_below(dm)] = (uint32_t)k;
+}
+
+// The deferred nodes of k_expand_count: exact centre containment of a
+// non-planar loop (drop / keep) or a polyline's level-13 cell test.  A fixed
+// grid strides over the device-side list (no host sync).
+__global__ __launch_bounds__(64) void k_expand_exact(const uint32_t *xlist, const unsigned int *xlist_n, const uint32_t *nf,
+                                                     const uint32_t *ni, const uint32_t *nj, const uint32_t *nmeta,
+                                                     uint8_t *act, int64_t *cnt, const int64_t *xoff, const V3 *xyz,
+                                                     const uint8_t *mode, const uint8_t *origin_in, const int32_t *nvx)
+{
+    const int64_t nl = *xlist_n;
+    for (int64_t t = tid64(); t < nl; t += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t k = xlist[t];
+        const uint32_t m = nmeta[k], f = nf[k];
+        const int level = meta_level(m), face = meta_face(m);
+        const V3 *p = xyz + xoff[f];
+        const int nv = nvx[f];
+        bool in;
+        if (mode[f] == MODE_LOOP) {
+            LoopView l{p, nv, origin_in[f] != 0};
+            in = loop_contains(l, node_center(face, ni[k], nj[k], level));
+        } else {
+            const uint32_t size = 1u << (kMaxLevel - level);
+            const double ulo = st_to_uv((double)ni[k] / (double)kMaxSize),
+                         uhi = st_to_uv((double)(ni[k] + size) / (double)kMaxSize);
+            const double vlo = st_to_uv((double)nj[k] / (double)kMaxSize),
+                         vhi = st_to_uv((double)(nj[k] + size) / (double)kMaxSize);
+            in = polyline_intersects_cell(p, nv, face, ulo, uhi, vlo, vhi);
+        }
+        act[k] = in ? 1 : 0;
+        cnt[k] = in ? 1 : 0;
+    }
 }
 
 __global__ void k_expand_write(int64_t nn, const uint32_t *nf, const uint64_t *nid, const uint32_t *ni, const uint32_t *nj,
@@ -978,7 +1023,7 @@ __device__ __forceinline__ void key_cell(int key, uint32_t f, const uint64_t *st
 
 // loop.go IntersectsCell for a level-13 cell at level-30 corner (i, j): the
 // padded edge test (stop at the first hit) and, for planar footprints,
-// contains_node's ray cast from the centre on the same (u,v) edge images --
+// planar_contains's ray cast from the centre on the same (u,v) edge images --
 // used only when no edge hits.  uc < a.x + (vc - a.y)(b.x - a.x)/(b.y - a.y),
 // multiplied through by (b.y - a.y): an edge that misses the padded cell
 // crosses v = vc at least half a cell (1.2e-4) from uc, so the rounding
@@ -1849,12 +1894,17 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
         hipLaunchKernelGGL(k_start<1>, dim3(grid_for(nd, 64)), dim3(64), 0, s, nd, dlist, xoff, xyz, mode, fmask, flags,
                            orig, nvx, eoff, clip_c, cflags, nullptr, soff, F->f.p, F->id.p, F->i.p, F->j.p, F->meta.p);
     int *any_open = flag_.ensure(1);
+    unsigned int *xlist_n = xlist_n_.ensure(1);
     for (int iter = 0; iter < 32 && nn > 0; iter++) {
         uint8_t *act = act_.ensure(nn + 1);
         int64_t *c = ncnt_.ensure(nn + 1);
         int64_t *pos = npos_.ensure(nn + 1);
+        DSS_HIP(hipMemsetAsync(xlist_n, 0, sizeof(unsigned int), s));
+        uint32_t *xlist = xlist_.ensure(nn + 1);
         hipLaunchKernelGGL(k_expand_count, dim3(grid_for(nn, 64)), dim3(64), 0, s, nn, F->f.p, F->i.p, F->j.p, F->meta.p,
-                           act, c, xoff, xyz, mode, fmask, orig, nvx, eoff, clip_f, clip_c, cflags, flags);
+                           act, c, xoff, xyz, mode, fmask, orig, nvx, eoff, clip_f, clip_c, cflags, flags, xlist, xlist_n);
+        hipLaunchKernelGGL(k_expand_exact, dim3((unsigned)std::min<int64_t>(grid_for(nn, 64), 1024)), dim3(64), 0, s, xlist,
+                           xlist_n, F->f.p, F->i.p, F->j.p, F->meta.p, act, c, xoff, xyz, mode, orig, nvx);
         exclusive_scan_i64(c, pos, nn, tmp_, s);
         DSS_HIP(hipMemsetAsync(any_open, 0, sizeof(int), s));
         Frontier *G = &fr_[cur ^ 1];

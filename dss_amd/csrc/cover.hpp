@@ -65,8 +65,8 @@ class CoverEngine {
     DevBuf<int32_t> status_, nvx_;
     DevBuf<double> area_, xyz_;
     DevBuf<uint8_t> mode_, orig_, fmask_, flags_, cflags_, act_;
-    DevBuf<uint32_t> slow_, vown_, eown_, dlist_;
-    DevBuf<unsigned int> dlist_n_;
+    DevBuf<uint32_t> slow_, vown_, eown_, dlist_, xlist_;
+    DevBuf<unsigned int> dlist_n_, xlist_n_;
     DevBuf<uint8_t> fanf_, ninner_;
     DevBuf<uint32_t> perm_, towner_;
     DevBuf<uint8_t> omode_;
