@@ -5,23 +5,27 @@
 // 20-gon, polygon range checks), golang/geo RegionCoverer{13,13}: the result
 // is the sorted set of level-13 cells c with region.IntersectsCell(c).
 //
-// Pipeline (one batch of N footprints, all device resident):
-//   k_nverts   vertex slots per footprint (polygon V, circle 20) -> scan
-//   k_setup    one thread per footprint: lat/lng -> S2 xyz with Go's Cephes
-//              trig, RegularLoop, loop origin containment, Loop.Area,
-//              reversal, status/mode, touched-face mask
-//   k_clip     ClipToPaddedFace of every edge on every touched face, with the
-//              exact reference padding (fine, level-13 decisions) and a
-//              1e-9 padding (coarse, pruning only)
+// Two paths (CoverEngine::run): batches of <= 16k footprints (the per-request
+// path) take k_cover_wave, one wavefront per footprint; larger batches take
+// the general pipeline (all device resident):
+//   k_nverts, k_circle_frames, k_verts, k_fan, k_orient, k_fan_area
+//              vertex slots, S2 points with Go's Cephes trig, RegularLoop,
+//              (u,v) images, Loop.Area's fan terms (one thread per vertex /
+//              needed triangle)
+//   k_setup    one thread per footprint: origin containment, area sum,
+//              reversal, status/mode, touched-face mask, start cells
+//   k_cand_fp / k_cand_exact
+//              direct candidates of the single-face small loops (most
+//              footprints): the cells of their padded bound, tested exactly
+//   k_clip_items  ClipToPaddedFace of every edge of the descent footprints on
+//              every touched face, fine (level-13) and coarse (pruning) pads
 //   k_start    <= 4 start cells per face around the clipped-edge bound
-//   k_expand_* level-synchronous descent over ALL footprints' frontier nodes
-//              at once.  Coarse levels prune with the enlarged padding; a node
-//              no edge touches is uniform: its centre's containment decides
-//              the whole subtree (emitted as a range).  Level 13 applies the
-//              reference test exactly.  Children are written in Hilbert (=id)
-//              order behind an exclusive scan, so each footprint's output is
-//              sorted by construction -- no sort pass.
-//   k_emit     expand ranges into level-13 ids (CSR per footprint).
+//   k_expand_* level-synchronous descent over the descent footprints'
+//              frontier nodes at once (exact S2 node tests deferred to
+//              k_expand_exact); children written in Hilbert (= id) order
+//              behind an exclusive scan, so each footprint's output is sorted
+//              by construction -- no sort pass
+//   k_cand_emit / k_emit   level-13 ids into the CSR per footprint.
 // Roofline: FP64 VALU (edge clip / crossing tests); see DESIGN.md.
 #include <hip/hip_runtime.h>
 
