@@ -219,26 +219,46 @@ def timed(torch, dist, dev, world, fn):
     return elapsed
 
 
+class StepFailure(RuntimeError):
+    """A pipeline failed inside the timed region: no result line may be
+    printed for the run (a rate over steps that did not finish is not a
+    measurement), and the process exits non-zero."""
+
+
 def replica_steps(torch, D, ctx, workers, d_q, index, qargs, steps):
     """`steps` replica steps (cover + join against the whole index) over the
     main context and the worker pipelines; the steps are handed out one at a
     time, so no pipeline idles while another still has a queue (the tail is
-    at most one step)."""
+    at most one step).  A pipeline that raises stops every other one from
+    taking further steps; the first error is re-raised as StepFailure after
+    all threads have joined, and so is a count of finished steps short of
+    `steps` -- the caller never divides `steps` by a time in which fewer
+    finished."""
     import threading
     tickets = [0]
+    finished = [0]
+    errors = []
     lock = threading.Lock()
 
     def take():
         with lock:
+            if errors:
+                return False
             t = tickets[0]
             tickets[0] += 1
         return t < steps
 
     def run(wctx, wstream):
-        with torch.cuda.stream(wstream):
-            while take():
-                D.search(wctx, index, D.cover(wctx, d_q), *qargs)
-            wstream.synchronize()
+        try:
+            with torch.cuda.stream(wstream):
+                while take():
+                    D.search(wctx, index, D.cover(wctx, d_q), *qargs)
+                    with lock:
+                        finished[0] += 1
+                wstream.synchronize()
+        except BaseException as e:  # noqa: BLE001 -- re-raised below, on the calling thread
+            with lock:
+                errors.append(e)
 
     threads = [threading.Thread(target=run, args=w) for w in workers]
     for th in threads:
@@ -246,6 +266,64 @@ def replica_steps(torch, D, ctx, workers, d_q, index, qargs, steps):
     run(ctx, torch.cuda.current_stream())
     for th in threads:
         th.join()
+    if errors:
+        raise StepFailure(f"{len(errors)} pipeline(s) failed in the timed steps ({finished[0]} of {steps} steps "
+                          f"finished): {type(errors[0]).__name__}: {errors[0]}") from errors[0]
+    if finished[0] != steps:
+        raise StepFailure(f"{finished[0]} of {steps} steps finished")
+
+
+HBM_RESERVE = 4 << 30  # kept free beside the pipelines' steady-state buffers
+
+
+def add_pipelines(args, torch, D, _lib, local, dev, tunes, d_q, join):
+    """Up to --pipelines - 1 worker pipelines beside the main context.  Each
+    new context is warmed with two full steps (cover + join when `join` =
+    (index, qargs) is given; the second step settles buffers the first one
+    sized, such as the pair buffer after a long x long overflow) and kept only
+    if the HBM left after it still holds another context of the same size
+    plus HBM_RESERVE -- so the timed steps never allocate.  A context whose
+    warm-up runs out of memory is dropped.  Returns (workers, note)."""
+    workers = []
+    foot = 0
+    want = max(0, args.pipelines - 1)
+    note = None
+    for _ in range(want):
+        free0, _t = torch.cuda.mem_get_info(local)
+        if workers and free0 < foot + HBM_RESERVE:
+            note = f"{len(workers) + 1} of {args.pipelines} pipelines: {free0 / 2**30:.1f} GiB free, one more " \
+                   f"pipeline holds {foot / 2**30:.1f} GiB"
+            break
+        wctx = _lib.Context(local)
+        ws = torch.cuda.Stream(device=dev)
+        try:
+            for k, v in tunes:
+                wctx.set_tuning(k, v)
+            with torch.cuda.stream(ws):
+                for _rep in range(2):
+                    c = D.cover(wctx, d_q)
+                    if join is not None:
+                        D.search(wctx, join[0], c, *join[1])
+                ws.synchronize()
+        except _lib.DssgError as e:
+            wctx.close()
+            torch.cuda.synchronize()
+            note = f"{len(workers) + 1} of {args.pipelines} pipelines: warming pipeline {len(workers) + 2} failed " \
+                   f"({e})"
+            break
+        free1, _t = torch.cuda.mem_get_info(local)
+        foot = max(foot, free0 - free1)
+        workers.append((wctx, ws))
+        if free1 < HBM_RESERVE:  # this one fits only without the reserve: drop it
+            wctx.close()
+            workers.pop()
+            torch.cuda.synchronize()
+            note = f"{len(workers) + 1} of {args.pipelines} pipelines: the last one left " \
+                   f"{free1 / 2**30:.1f} GiB free"
+            break
+    if note:
+        log(f"[bench] {note}")
+    return workers, note
 
 
 def cover_ahead_steps(torch, D, ctx, covers, d_q, steps, search_fn):
@@ -266,6 +344,7 @@ def cover_ahead_steps(torch, D, ctx, covers, d_q, steps, search_fn):
     free = [threading.Semaphore(1) for _ in range(P)]
     done = [None] * P
     err = []
+    stop = threading.Event()
 
     def cover_loop(p):
         wctx, ws = covers[p]
@@ -273,13 +352,16 @@ def cover_ahead_steps(torch, D, ctx, covers, d_q, steps, search_fn):
             with torch.cuda.stream(ws):
                 for _ in range(p, steps, P):
                     free[p].acquire()
+                    if stop.is_set():
+                        return
                     if done[p] is not None:
                         ws.wait_event(done[p])
                     c = D.cover(wctx, d_q)
                     ev = torch.cuda.Event()
                     ev.record(ws)
                     ready[p].put((c, ev))
-        except BaseException as e:  # handed to the search thread
+                ws.synchronize()
+        except BaseException as e:  # noqa: BLE001 -- handed to the search thread
             err.append(e)
             ready[p].put(None)
 
@@ -287,17 +369,26 @@ def cover_ahead_steps(torch, D, ctx, covers, d_q, steps, search_fn):
     for th in threads:
         th.start()
     main = torch.cuda.current_stream()
-    for k in range(steps):
-        item = ready[k % P].get()
-        if item is None:
-            raise err[0]
-        c, ev = item
-        main.wait_event(ev)
-        search_fn(c)
-        ev_done = torch.cuda.Event()
-        ev_done.record(main)
-        done[k % P] = ev_done
-        free[k % P].release()
+    finished = 0
+    try:
+        for k in range(steps):
+            item = ready[k % P].get()
+            if item is None:
+                raise StepFailure(f"a cover pipeline failed in the timed steps ({finished} of {steps} steps "
+                                  f"finished): {type(err[0]).__name__}: {err[0]}") from err[0]
+            c, ev = item
+            main.wait_event(ev)
+            search_fn(c)
+            finished += 1
+            ev_done = torch.cuda.Event()
+            ev_done.record(main)
+            done[k % P] = ev_done
+            free[k % P].release()
+    finally:
+        if finished != steps:  # release the cover threads so they end
+            stop.set()
+            for f in free:
+                f.release()
     for th in threads:
         th.join()
 
@@ -428,19 +519,10 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    # extra pipelines: each its own context (engine scratch), stream and host thread
-    workers = []
-    for _ in range(max(0, args.pipelines - 1)):
-        wctx = _lib.Context(local)
-        for k, v in tunes:
-            wctx.set_tuning(k, v)
-        workers.append((wctx, torch.cuda.Stream(device=dev)))
-    for wctx, ws in workers:  # warm the extra contexts (buffers at steady-state size)
-        with torch.cuda.stream(ws):
-            c = D.cover(wctx, d_q)
-            if sharded is None:
-                D.search(wctx, index, c, *qargs)
-            ws.synchronize()
+    # extra pipelines: each its own context (engine scratch), stream and host
+    # thread, warmed to its steady-state buffers and kept only if HBM holds it
+    workers, pipe_note = add_pipelines(args, torch, D, _lib, local, dev, tunes, d_q,
+                                       None if sharded is not None else (index, qargs))
 
     # ------------------------------------------------------------ timed steps
     stage("timed steps")
@@ -461,7 +543,7 @@ def main():
         rt = timed(torch, dist, dev, world,
                    lambda: replica_steps(torch, D, ctx, workers, d_q, full_index, qargs, args.steps))
         replica = {"value": world * nq * args.steps / rt, "ms_per_step": 1000.0 * rt / max(1, args.steps),
-                   "pipelines_per_gpu": args.pipelines,
+                   "pipelines_per_gpu": 1 + len(workers),
                    "note": "whole index on every GPU, each rank's batch joined locally (no exchange)"}
         native_pairs = None
         if native is not None:  # the timed path's own output, checked below beside the torch path's
@@ -563,7 +645,7 @@ def main():
                                    + (" (SearchISAs semantics)" if rid else ""),
                        "queries_per_gpu_step": nq, "intents": ni, "postings": n_post, "index": index_info(ctx, index),
                        "parallelism": f"query-sharded x{world}, index replicated", "scale": args.scale,
-                       "pipelines_per_gpu": args.pipelines},
+                       "pipelines_per_gpu": 1 + len(workers), "pipelines_note": pipe_note},
             "coverings_per_s": world * nq / (cover_avg * 1e-3),
             "phase_ms": {"cover": cover_avg, "join": join_avg, "join_kernel": kern_avg_ms},
             "pairs_per_step": r_tot,

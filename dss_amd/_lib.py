@@ -137,6 +137,7 @@ def load():
         L.dssg_store_stats.argtypes = [vp, P(i64), P(i64), P(i64), P(i64)]
         L.dssg_store_search.argtypes = [vp, vp, i64, P(i64), P(u64), P(f), P(f), P(i64), P(i64), P(i32), P(u32),
                                         P(u32), i64, P(i64)]
+        L.dssg_store_max_subscription_count.argtypes = [vp, vp, i64, P(i64), P(u64), P(i32), i64, P(i64)]
         L.dssg_index_set_notification_index.argtypes = [vp, vp, P(i64)]
         L.dssg_index_get_notification_index.argtypes = [vp, vp, P(i64)]
         L.dssg_notify_subscriptions.argtypes = [vp, vp, i64, P(i64), P(u64), i64, P(u32), P(u32), P(i64), i64, P(i64)]

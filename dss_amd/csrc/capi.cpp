@@ -742,7 +742,7 @@ int dssg_max_subscription_count(dssg_ctx *ctx, const dssg_index *idx, int64_t nq
         const int64_t *dqo = upload(ctx->d_qoffs, q_offs, nq + 1, s);
         const uint64_t *dqc = upload(ctx->d_cells, q_cells, nqc, s);
         const int32_t *dow = upload(ctx->d_owner, owner, nq, s);
-        ctx->subs.max_count(idx, nq, dqo, dqc, nqc, dow, now_us, s, out_count);
+        ctx->subs.max_count(&idx, 1, nq, dqo, dqc, nqc, dow, now_us, s, out_count);
     });
 }
 
@@ -796,6 +796,25 @@ int dssg_store_stats(const dssg_store *st, int64_t *live, int64_t *base, int64_t
     if (delta) *delta = st->st.delta_size();
     if (compactions) *compactions = st->st.compactions();
     return DSSG_OK;
+}
+
+int dssg_store_max_subscription_count(dssg_ctx *ctx, dssg_store *st, int64_t nq, const int64_t *q_offs,
+                                      const uint64_t *q_cells, const int32_t *owner, int64_t now_us,
+                                      int64_t *out_count)
+{
+    if (!ctx || !st || nq < 0 || !q_offs || (nq > 0 && (!owner || !out_count)) || now_us == INT64_MIN)
+        return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        if (!st->st.with_owner()) throw dss::Error(DSSG_ERR_INVALID, "store created without owners");
+        hipStream_t s = ctx->stream;
+        const int64_t nqc = q_offs[nq] - q_offs[0];
+        if (nqc < 0 || q_offs[0] != 0) throw dss::Error(DSSG_ERR_INVALID, "q_offs must start at 0 and ascend");
+        const int64_t *dqo = upload(ctx->d_qoffs, q_offs, nq + 1, s);
+        const uint64_t *dqc = upload(ctx->d_cells, q_cells, nqc, s);
+        const int32_t *dow = upload(ctx->d_owner, owner, nq, s);
+        const dssg_index *sides[2] = {st->st.base(), st->st.delta()};
+        ctx->subs.max_count(sides, 2, nq, dqo, dqc, nqc, dow, now_us, s, out_count);
+    });
 }
 
 int dssg_store_search(dssg_ctx *ctx, dssg_store *st, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
@@ -1223,9 +1242,22 @@ struct dssg_batcher {
     bool prof = false;
     double prof_us[3] = {0, 0, 0};
     int64_t prof_n = 0;
-    // answers a caller could not take (DSSG_ERR_CAPACITY): kept for its retry
+    // answers a caller could not take (DSSG_ERR_CAPACITY): kept for its
+    // retry, matched on the request's full inputs (the hash only picks
+    // candidates) and dropped after kCacheTtl or when 1024 newer ones wait
+    struct Cached {
+        uint64_t key = 0;
+        int32_t kind = 0;
+        float radius = 0, alo = 0, ahi = 0;
+        int64_t start = 0, end = 0, now = 0;
+        std::vector<double> lat, lng;
+        double area = 0;
+        std::vector<uint32_t> ids;
+        std::chrono::steady_clock::time_point at;
+    };
+    static constexpr std::chrono::milliseconds kCacheTtl{2000};
     std::mutex cache_mu;
-    std::deque<std::pair<uint64_t, std::pair<double, std::vector<uint32_t>>>> cache;
+    std::deque<Cached> cache;
 
     static size_t al8(size_t x) { return (x + 7) & ~(size_t)7; }
 
@@ -1469,10 +1501,18 @@ int dssg_batcher_search_operations(dssg_batcher *b, int32_t kind, int64_t nv, co
     bool cached = false;
     {  // the retry of a request whose answer did not fit: no second cover + join
         std::lock_guard<std::mutex> lk(b->cache_mu);
+        const auto now_t = std::chrono::steady_clock::now();
+        while (!b->cache.empty() && now_t - b->cache.front().at > dssg_batcher::kCacheTtl) b->cache.pop_front();
+        auto same = [&](const dssg_batcher::Cached &c) {
+            return c.key == key && c.kind == kind && (int64_t)c.lat.size() == nv && c.radius == radius_m &&
+                   c.alo == alt_lo && c.ahi == alt_hi && c.start == start && c.end == end && c.now == now_us &&
+                   (nv == 0 || (std::memcmp(c.lat.data(), lat, sizeof(double) * (size_t)nv) == 0 &&
+                                std::memcmp(c.lng.data(), lng, sizeof(double) * (size_t)nv) == 0));
+        };
         for (auto it = b->cache.begin(); it != b->cache.end(); ++it)
-            if (it->first == key && (int64_t)it->second.second.size() <= cap) {
-                r.area = it->second.first;
-                r.ids = std::move(it->second.second);
+            if (same(*it) && (int64_t)it->ids.size() <= cap) {
+                r.area = it->area;
+                r.ids = std::move(it->ids);
                 b->cache.erase(it);
                 cached = true;
                 break;
@@ -1504,8 +1544,24 @@ int dssg_batcher_search_operations(dssg_batcher *b, int32_t kind, int64_t nv, co
     }
     *needed = (int64_t)r.ids.size();
     if ((int64_t)r.ids.size() > cap) {
+        dssg_batcher::Cached c;
+        c.key = key;
+        c.kind = kind;
+        c.radius = radius_m;
+        c.alo = alt_lo;
+        c.ahi = alt_hi;
+        c.start = start;
+        c.end = end;
+        c.now = now_us;
+        if (nv > 0) {
+            c.lat.assign(lat, lat + nv);
+            c.lng.assign(lng, lng + nv);
+        }
+        c.area = r.area;
+        c.ids = std::move(r.ids);
+        c.at = std::chrono::steady_clock::now();
         std::lock_guard<std::mutex> lk(b->cache_mu);
-        b->cache.emplace_back(key, std::make_pair(r.area, std::move(r.ids)));
+        b->cache.push_back(std::move(c));
         while (b->cache.size() > 1024) b->cache.pop_front();
         return DSSG_ERR_CAPACITY;
     }

@@ -27,6 +27,8 @@ class CoverEngine {
     CoverEngine &operator=(const CoverEngine &) = delete;
     ~CoverEngine()
     {
+        // the last upload out of the pinned offsets must have landed first
+        if (h_ev_) (void)hipEventSynchronize(h_ev_);
         if (h_offs_) (void)hipHostFree(h_offs_);
         if (h_ev_) (void)hipEventDestroy(h_ev_);
     }

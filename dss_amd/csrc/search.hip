@@ -1827,12 +1827,22 @@ T fetch(const T *p, hipStream_t s)
 
 }  // namespace
 
+// the join's timing events, created on first use by either join path
+void SearchEngine::timing_events()
+{
+    if (timing_ && !ev0_) {
+        DSS_HIP(hipEventCreate(&ev0_));
+        DSS_HIP(hipEventCreate(&ev1_));
+    }
+}
+
 // ============================================================ small batches
 void SearchEngine::search_small(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
                                 const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo,
                                 const int64_t *q_thi, const int32_t *q_owner, int64_t nqc, hipStream_t s,
                                 dssg_pairs *out)
 {
+    timing_events();  // (the batcher calls this directly, not through search())
     const IndexView ix = view_of(idx);
     const QueryView qv{nq, q_offs, q_cells, q_alt_lo, q_alt_hi, q_tlo, q_thi, q_owner};
     unsigned long long *count = small_cnt_.ensure(1);
@@ -2107,10 +2117,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
 {
     if (q_owner && !idx->has_owner) throw Error(DSSG_ERR_INVALID, "search by owner on an index built without owners");
     if (nq >= (int64_t)kLongQ) throw Error(DSSG_ERR_INVALID, "search: more than 2^29 queries per batch");
-    if (timing_ && !ev0_) {
-        DSS_HIP(hipEventCreate(&ev0_));
-        DSS_HIP(hipEventCreate(&ev1_));
-    }
+    timing_events();
     const IndexView ix = view_of(idx);
     const QueryView qv{nq, q_offs, q_cells, q_alt_lo, q_alt_hi, q_tlo, q_thi, q_owner};
     auto empty = [&]() {
@@ -2230,6 +2237,11 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
                                dim3(kFixBlock), 0, s, nch, (const uint32_t *)list, (const unsigned int *)nlist, fills, n,
                                hole, hoff, toff, mover);
     };
+    // the overflow pair buffers of an earlier batch (whose output this batch
+    // replaces) go before the primary ones regrow to take their place: one
+    // context never holds both at their full size
+    oq2_.release();
+    oe2_.release();
     for (int attempt = 0; attempt < 6; attempt++) {
         const int64_t cap = kRegions * out_rcap_, nch = cap / kOutChunk;
         uint32_t *oq = oq_.ensure(cap + 1), *oe = oe_.ensure(cap + 1);

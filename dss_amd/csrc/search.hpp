@@ -152,6 +152,7 @@ class SearchEngine {
     int64_t units_ = 0, keys_ = 0, runs_ = 0, iters_ = 0, tests_ = 0;
     int64_t flushes_ = 0, merges_ = 0, merge_lanes_ = 0, tagged_ = 0, long_queries_ = 0, long_postings_ = 0;
     hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+    void timing_events();
 };
 
 }  // namespace dss

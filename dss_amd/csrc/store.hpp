@@ -33,6 +33,10 @@ class Store {
     int64_t delta_size() const { return delta_ ? delta_->n_e : 0; }
     int64_t compactions() const { return compactions_; }
     bool with_owner() const { return with_owner_; }
+    // the indexes a search covers (either may be null): every live row is in
+    // exactly one of them (base rows rewritten since are tombstoned there)
+    const dssg_index *base() const { return base_; }
+    const dssg_index *delta() const { return delta_; }
 
    private:
     struct Row {

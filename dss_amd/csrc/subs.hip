@@ -39,9 +39,10 @@ __global__ void k_cell_q(int64_t nq, const int64_t *offs, uint32_t *cq)
 }
 
 // One thread per query cell: the owner's unexpired entities posted in the
-// cell, repeats counted; the query keeps the max over its cells.
-__global__ void k_max_count(IndexView a, int64_t nqc, const uint64_t *cells, const uint32_t *cq, const int32_t *owner,
-                            long long now, unsigned long long *out)
+// cell, repeats counted, added to the cell's count (one index of several:
+// a store's base and delta hold disjoint live entities).
+__global__ void k_cell_count(IndexView a, int64_t nqc, const uint64_t *cells, const uint32_t *cq, const int32_t *owner,
+                             long long now, unsigned long long *cell_cnt)
 {
     const int64_t k = tid64();
     if (k >= nqc) return;
@@ -49,14 +50,21 @@ __global__ void k_max_count(IndexView a, int64_t nqc, const uint64_t *cells, con
     uint64_t s = 0, e = 0;
     if (!find_slot(a, cells[k], slot)) return;
     slot_range(a, slot, s, e);
-    const uint32_t q = cq[k];
-    const int32_t own = owner[q];
+    const int32_t own = owner[cq[k]];
     unsigned long long cnt = 0;
     for (uint64_t p = s; p < e; p++) {
         const uint32_t ent = a.b_e[p] & ~kFirstBit;
         if (a.e_owner[ent] == own && a.e_t1[ent] >= now && !is_dead(a, ent)) cnt += a.b_mult ? a.b_mult[p] : 1u;
     }
-    if (cnt) atomicMax(&out[q], cnt);
+    cell_cnt[k] += cnt;  // (one thread per cell; the sides run one after another)
+}
+
+// The query keeps the max over its cells.
+__global__ void k_cell_max(int64_t nqc, const uint32_t *cq, const unsigned long long *cell_cnt, unsigned long long *out)
+{
+    const int64_t k = tid64();
+    if (k >= nqc) return;
+    if (cell_cnt[k]) atomicMax(&out[cq[k]], cell_cnt[k]);
 }
 
 __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t *x, uint32_t n, uint32_t v)
@@ -148,17 +156,25 @@ int bits_for_n(int64_t n)
 
 }  // namespace
 
-void SubsEngine::max_count(const dssg_index *idx, int64_t nq, const int64_t *offs, const uint64_t *cells, int64_t nqc,
-                           const int32_t *owner, int64_t now, hipStream_t s, int64_t *out)
+void SubsEngine::max_count(const dssg_index *const *sides, int nsides, int64_t nq, const int64_t *offs,
+                           const uint64_t *cells, int64_t nqc, const int32_t *owner, int64_t now, hipStream_t s,
+                           int64_t *out)
 {
-    if (!idx->has_owner) throw Error(DSSG_ERR_INVALID, "max subscription count on an index built without owners");
+    for (int k = 0; k < nsides; k++)
+        if (sides[k] && !sides[k]->has_owner)
+            throw Error(DSSG_ERR_INVALID, "max subscription count on an index built without owners");
     unsigned long long *d = cnt_.ensure(nq + 1);
     DSS_HIP(hipMemsetAsync(d, 0, sizeof(unsigned long long) * (nq + 1), s));
     if (nqc > 0) {
         uint32_t *cq = cq_.ensure(nqc + 1);
+        unsigned long long *cc = k0_.ensure(nqc + 1);
+        DSS_HIP(hipMemsetAsync(cc, 0, sizeof(unsigned long long) * nqc, s));
         hipLaunchKernelGGL(k_cell_q, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, offs, cq);
-        hipLaunchKernelGGL(k_max_count, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, view_of(idx), nqc, cells, cq, owner,
-                           (long long)now, d);
+        for (int k = 0; k < nsides; k++)
+            if (sides[k] && sides[k]->n_p > 0)
+                hipLaunchKernelGGL(k_cell_count, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, view_of(sides[k]), nqc,
+                                   cells, cq, owner, (long long)now, cc);
+        hipLaunchKernelGGL(k_cell_max, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, nqc, cq, cc, d);
     }
     if (nq > 0) DSS_HIP(hipMemcpyAsync(out, d, sizeof(int64_t) * nq, hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));

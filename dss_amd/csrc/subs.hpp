@@ -8,9 +8,11 @@ namespace dss {
 class SubsEngine {
    public:
     // out[q] (host) = max over the query's cells of the owner's unexpired
-    // entities posted in the cell (repeats counted), 0 if none.
-    void max_count(const dssg_index *idx, int64_t nq, const int64_t *offs, const uint64_t *cells, int64_t nqc,
-                   const int32_t *owner, int64_t now, hipStream_t s, int64_t *out);
+    // entities posted in the cell (repeats counted), 0 if none; the entities
+    // of all `sides` (indexes over disjoint live entities: a store's base and
+    // delta; null sides skipped) count together.
+    void max_count(const dssg_index *const *sides, int nsides, int64_t nq, const int64_t *offs, const uint64_t *cells,
+                   int64_t nqc, const int32_t *owner, int64_t now, hipStream_t s, int64_t *out);
     // Every entity of owner[q] with ends_at >= now; device outputs, count returned.
     int64_t owner_subs(const dssg_index *idx, int64_t nq, const int32_t *owner, int64_t now, hipStream_t s,
                        uint32_t **out_q, uint32_t **out_e);

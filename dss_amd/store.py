@@ -365,6 +365,19 @@ class Store:
         self.ctx.check(self.ctx.L.dssg_store_stats(self.h, *[C.byref(x) for x in v]))
         return dict(zip(["live", "base", "delta", "compactions"], [x.value for x in v]))
 
+    def max_subscription_count_batch(self, q_offs, q_cells, owner, now_us) -> np.ndarray:
+        """RID MaxSubscriptionCountInCellsByOwner (subscriptions.go:83-116)
+        over the store's live rows (dssg_store_max_subscription_count)."""
+        q_offs = np.ascontiguousarray(q_offs, dtype=np.int64)
+        q_cells = np.ascontiguousarray(q_cells, dtype=np.uint64)
+        ow = np.ascontiguousarray(owner, dtype=np.int32)
+        nq = len(q_offs) - 1
+        out = np.zeros(max(nq, 1), dtype=np.int64)
+        self.ctx.check(self.ctx.L.dssg_store_max_subscription_count(
+            self.ctx.h, self.h, nq, _p(q_offs, C.c_int64), _p(q_cells, C.c_uint64), _p(ow, C.c_int32), int(now_us),
+            _p(out, C.c_int64)))
+        return out[:nq]
+
     def search_batch(self, q_offs, q_cells, alt_lo, alt_hi, tlo, thi, owner=None):
         """(query, id) pairs, sorted; the generic predicate of dssg_search."""
         q_offs = np.ascontiguousarray(q_offs, dtype=np.int64)

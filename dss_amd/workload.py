@@ -216,9 +216,10 @@ def rid_attrs(rng, n, query: bool) -> Attrs:
 # BASELINE.json configs: (queries, entities, kind) at scale 1
 CONFIG_SIZES = {0: (10_000, 100_000), 1: (1_000_000, 1_000_000), 2: (1_000_000, 10_000_000),
                 3: (1_000_000, 5_000_000), 4: (1_000_000, 50_000_000)}
-CONFIG_NAMES = {0: "Go CPU ref: SF-Bay metro, circles+polygons",
-                1: "1xMI355X: SF-Bay metro, circles+polygons",
-                2: "8xMI355X: California, 70% around 4 hotspots",
+# (workload descriptions only: the GPU count of a line is its n_gpus)
+CONFIG_NAMES = {0: "Go CPU ref workload: SF-Bay metro, circles+polygons",
+                1: "metro: SF-Bay, circles+polygons",
+                2: "north-star airspace: California, 70% around 4 hotspots",
                 3: "RID ISAs: NYC city blocks, 30 s windows",
                 4: "continent stress: CONUS corridors, 80% around 20 hotspots"}
 

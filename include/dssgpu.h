@@ -244,6 +244,15 @@ int dssg_store_stats(const dssg_store *st, int64_t *live, int64_t *base, int64_t
 int dssg_store_search(dssg_ctx *ctx, dssg_store *st, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
                       const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
                       const int32_t *q_owner, uint32_t *out_q, uint32_t *out_id, int64_t cap, int64_t *needed);
+/* RID MaxSubscriptionCountInCellsByOwner (pkg/rid/cockroach/
+ * subscriptions.go:83-116) over a store's live rows (base + delta, the GPU
+ * mirror the Go binding keeps): out_count[q] = max over q's cells of the
+ * owner[q] rows with ends_at >= now posted in the cell, repeats of the cell
+ * in a row counted (`unnest(cells)`), 0 if none (IFNULL(MAX(..), 0)).  The
+ * store must be created with owners. */
+int dssg_store_max_subscription_count(dssg_ctx *ctx, dssg_store *st, int64_t nq, const int64_t *q_offs,
+                                      const uint64_t *q_cells, const int32_t *owner, int64_t now_us,
+                                      int64_t *out_count);
 
 /* ---- subscription-store queries -----------------------------------------
  * Notification fan-out: RID UpdateNotificationIdxsInCells

@@ -240,6 +240,63 @@ int main(void)
         CHECK(rc == DSSG_OK && needed == 1 && oid[0] == idB, "after delete A n=%lld", (long long)needed);
         dssg_store_free(ms);
     }
+    /* ---- RID subscription mirror, as go/pkg/gpu/rid.go calls it -------------
+     * UpdateNotificationIdxsInCells (subscriptions.go:204-219): the mirror
+     * finds the subscriptions sharing a cell with the ISA and unexpired
+     * (cells && $1 AND ends_at >= now); CRDB only runs the UPDATE ... WHERE
+     * id = ANY($ids) ... RETURNING (the counters here stand in for that
+     * column).  The reference's fan-out KAT (isa_test.go:266-324: 42 -> 43
+     * on the ISA insert -> 44 on its delete) and the max-count KAT
+     * (subscriptions_test.go:275-287: 2 of "myself"'s subscriptions share
+     * cell 12494535935418957824) over the subscriptions pool of
+     * subscriptions_test.go:19-64. */
+    {
+        const uint64_t pool = 12494535935418957824ull, overflow = 17106221850767130624ull;
+        const uint64_t cells[4] = {overflow, pool, pool, pool};
+        const int64_t soffs[4] = {0, 2, 3, 4};
+        const uint32_t sid[3] = {0, 1, 2};
+        const int32_t sowner[3] = {0, 0, 1}; /* "myself", "myself", "me" */
+        const int64_t now = 1600000000000000ll, day = 86400000000ll;
+        const int64_t st0[3] = {now, now, now}, st1[3] = {now + day, now + day, now + day};
+        const float slo[3] = {-INFINITY, -INFINITY, -INFINITY}, shi[3] = {INFINITY, INFINITY, INFINITY};
+        int64_t counter[3] = {42, 42, 42}; /* notification_index in CRDB */
+        dssg_store *subs = NULL;
+        rc = dssg_store_create(ctx, 1, &subs);
+        CHECK(rc == DSSG_OK && subs, "subscription mirror create rc=%d", rc);
+        rc = dssg_store_upsert(ctx, subs, 3, sid, soffs, cells, slo, shi, st0, st1, sowner);
+        CHECK(rc == DSSG_OK, "subscription mirror upsert rc=%d", rc);
+        const int64_t qoffs[2] = {0, 1};
+        const float qlo = -INFINITY, qhi = INFINITY;
+        for (int round = 0; round < 2; round++) { /* the ISA insert, then its delete */
+            int64_t qtlo = now, qthi = DSSG_TIME_NULL_END_Q;
+            uint32_t oq[8], oid[8];
+            rc = dssg_store_search(ctx, subs, 1, qoffs, &pool, &qlo, &qhi, &qtlo, &qthi, NULL, oq, oid, 8, &needed);
+            CHECK(rc == DSSG_OK && needed == 3, "fan-out search n=%lld", (long long)needed);
+            for (int64_t k = 0; k < needed; k++)
+                if (oid[k] < 3 && st1[oid[k]] >= now) counter[oid[k]]++; /* UPDATE ... WHERE id = ANY($ids) */
+            CHECK(counter[0] == 43 + round && counter[1] == 43 + round && counter[2] == 43 + round,
+                  "notification index after round %d: %lld %lld %lld", round, (long long)counter[0],
+                  (long long)counter[1], (long long)counter[2]);
+        }
+        /* expired subscriptions are not notified (ends_at >= now) */
+        {
+            int64_t qtlo = now + 2 * day, qthi = DSSG_TIME_NULL_END_Q;
+            uint32_t oq[8], oid[8];
+            rc = dssg_store_search(ctx, subs, 1, qoffs, &pool, &qlo, &qhi, &qtlo, &qthi, NULL, oq, oid, 8, &needed);
+            CHECK(rc == DSSG_OK && needed == 0, "expired fan-out n=%lld", (long long)needed);
+        }
+        int64_t count = -1;
+        const int32_t myself = 0, me = 1;
+        rc = dssg_store_max_subscription_count(ctx, subs, 1, qoffs, &pool, &myself, now, &count);
+        CHECK(rc == DSSG_OK && count == 2, "max count KAT rc=%d count=%lld", rc, (long long)count);
+        rc = dssg_store_max_subscription_count(ctx, subs, 1, qoffs, &overflow, &me, now, &count);
+        CHECK(rc == DSSG_OK && count == 0, "max count (none) count=%lld", (long long)count);
+        int32_t found = 0;
+        rc = dssg_store_delete(ctx, subs, 1, &sid[1], &found);
+        rc = dssg_store_max_subscription_count(ctx, subs, 1, qoffs, &pool, &myself, now, &count);
+        CHECK(rc == DSSG_OK && found == 1 && count == 1, "max count after delete count=%lld", (long long)count);
+        dssg_store_free(subs);
+    }
     free(ecells);
     dssg_destroy(ctx);
     if (failures) {

@@ -90,3 +90,57 @@ def test_random_against_oracle(oracle):
     sq, se = idx.owner_subscriptions_batch(qown[:20], now_q)
     wq, we = oracle.owner_subscriptions(owner, t1, qown[:20], now_q)
     assert np.array_equal(sq, wq) and np.array_equal(se, we)
+
+
+def test_store_max_count_kat_and_writes(oracle):
+    """The GPU mirror's form (dssg_store_max_subscription_count, what the Go
+    binding serves MaxSubscriptionCountInCellsByOwner from): the reference
+    KAT (subscriptions_test.go:275-287) on a store, then random upserts,
+    rewrites and deletes (rows split over the base, the delta and base
+    tombstones) against the oracle over the live rows."""
+    from dss_amd import geo, workload as W
+    from dss_amd.store import Store
+    st = Store(with_owner=True)
+    st.upsert([0, 1, 2], POOL_CELLS, [-np.inf] * 3, [np.inf] * 3, [NOW] * 3, [NOW + DAY] * 3, owner=POOL_OWNER)
+    cnt = lambda cells, ow, now: int(st.max_subscription_count_batch([0, len(cells)], cells, [ow], now)[0])  # noqa
+    assert cnt([POOL_CELL], 0, NOW) == 2
+    assert cnt([POOL_CELL], 1, NOW) == 1
+    assert cnt([OVERFLOW_CELL], 1, NOW) == 0
+    assert cnt([POOL_CELL], 0, NOW + 2 * DAY) == 0
+    st.delete([1])
+    assert cnt([POOL_CELL], 0, NOW) == 1
+    st.upsert([1], [[POOL_CELL, POOL_CELL]], [0.0], [1.0], [NOW], [NOW + DAY], owner=[0])  # repeats count
+    assert cnt([POOL_CELL], 0, NOW) == 3
+    st.free()
+
+    _, q, qa, it, ia, now = W.config(0, scale=0.02)   # 200 queries, 2000 subscriptions
+    rng = np.random.default_rng(5)
+    ci = geo.cover_batch(it.kind, it.voff, it.lat, it.lng, it.radius_m)
+    cq = geo.cover_batch(q.kind, q.voff, q.lat, q.lng, q.radius_m)
+    lists = [ci.cells[ci.offs[k]:ci.offs[k + 1]] for k in range(it.n)]
+    owner = rng.integers(0, 5, it.n).astype(np.int32)
+    t1 = ia.t1.copy()
+    st = Store(with_owner=True)
+    n0 = it.n // 2
+    st.upsert(np.arange(n0), lists[:n0], ia.alt_lo[:n0], ia.alt_hi[:n0], ia.t0[:n0], t1[:n0], owner=owner[:n0])
+    st.compact()  # the first half becomes the base
+    rest = np.arange(n0, it.n)
+    st.upsert(rest, [lists[k] for k in rest], ia.alt_lo[rest], ia.alt_hi[rest], ia.t0[rest], t1[rest],
+              owner=owner[rest])
+    rew = rng.choice(n0, 50, replace=False)  # base rows rewritten (tombstoned in the base, live in the delta)
+    owner[rew] = rng.integers(0, 5, len(rew))
+    st.upsert(rew, [lists[k] for k in rew], ia.alt_lo[rew], ia.alt_hi[rew], ia.t0[rew], t1[rew], owner=owner[rew])
+    dead = rng.choice(it.n, 200, replace=False)
+    st.delete(dead)
+    live = np.ones(it.n, bool)
+    live[dead] = False
+    assert st.stats()["delta"] > 0
+    qown = rng.integers(0, 6, q.n).astype(np.int32)
+    now_q = int(np.median(ia.t0))
+    got = st.max_subscription_count_batch(cq.offs, cq.cells, qown, now_q)
+    keep = np.nonzero(live)[0]
+    offs = np.concatenate([[0], np.cumsum([len(lists[k]) for k in keep])]).astype(np.int64)
+    cells = np.concatenate([lists[k] for k in keep]).astype(np.uint64)
+    want = oracle.max_subscription_count(offs, cells, owner[keep], t1[keep], cq.offs, cq.cells, qown, now_q)
+    assert got.max() > 0 and np.array_equal(got, want)
+    st.free()
