@@ -250,6 +250,37 @@ func (m *Mirror) Search(qs []Query) ([][]string, error) {
 	}
 }
 
+// MaxCount is RID MaxSubscriptionCountInCellsByOwner
+// (pkg/rid/cockroach/subscriptions.go:83-116) over the mirror's live rows
+// (dssg_store_max_subscription_count): the most rows of owner with ends_at
+// >= now posted in any one of cells, repeats of a cell in a row's array
+// counted (`unnest(cells)`), 0 when none (IFNULL(MAX(..), 0)).  An owner with
+// no row in the mirror has 0 everywhere and is answered here.
+func (m *Mirror) MaxCount(cells s2.CellUnion, owner string, now int64) (int, error) {
+	if !m.withOwner {
+		return 0, fmt.Errorf("MaxCount on a mirror without owners")
+	}
+	m.mu.RLock()
+	defer m.mu.RUnlock()
+	id, ok := m.owners[owner]
+	if !ok || len(cells) == 0 {
+		return 0, nil
+	}
+	c, err := getCtx()
+	if err != nil {
+		return 0, err
+	}
+	defer putCtx(c)
+	offs := []C.int64_t{0, C.int64_t(len(cells))}
+	own := C.int32_t(id)
+	var count C.int64_t
+	if rc := C.dssg_store_max_subscription_count(c.c, m.st, 1, &offs[0], cellsPtr(cells), &own, C.int64_t(now),
+		&count); rc != C.DSSG_OK {
+		return 0, c.err("dssg_store_max_subscription_count", rc)
+	}
+	return int(count), nil
+}
+
 // Len is the number of live rows.
 func (m *Mirror) Len() int {
 	m.mu.RLock()

@@ -15,11 +15,14 @@ import (
 
 // RIDTransactor decorates the reference's CockroachDB repos.Transactor
 // (pkg/rid/cockroach/store.go): writes and point reads go to CRDB, while
-// SearchISAs, SearchSubscriptions and SearchSubscriptionsByOwner run on GPU
-// mirrors of the identification_service_areas / subscriptions tables'
-// cells, time and owner columns.  Writes made inside InTxnRetrier reach the
-// mirrors once the transaction has committed; inside it, searches go to CRDB
-// so a transaction sees its own writes.
+// SearchISAs, SearchSubscriptions, SearchSubscriptionsByOwner and
+// MaxSubscriptionCountInCellsByOwner run on GPU mirrors of the
+// identification_service_areas / subscriptions tables' cells, time and
+// owner columns, and UpdateNotificationIdxsInCells finds its subscriptions
+// on the mirror (CRDB runs only the UPDATE ... RETURNING of their counters,
+// through the hook of go/patches/0002).  Writes made inside InTxnRetrier
+// reach the mirrors once the transaction has committed; inside it, the
+// fan-out overlays the transaction's own subscription writes.
 type RIDTransactor struct {
 	repos.Transactor
 	// Now is the store clock (cockroach.DefaultClock in the reference).
@@ -131,7 +134,7 @@ func (t *RIDTransactor) InTxnRetrier(ctx context.Context, f func(repo repos.Repo
 	var w *ridWrites
 	err := t.Transactor.InTxnRetrier(ctx, func(repo repos.Repository) error {
 		w = newRIDWrites() // a retried attempt starts over
-		return f(&ridRepo{Repository: repo, w: w})
+		return f(&ridRepo{Repository: repo, w: w, t: t})
 	})
 	if err != nil || w == nil {
 		return err
@@ -202,10 +205,65 @@ func (t *RIDTransactor) DeleteSubscription(ctx context.Context, sub *ridmodels.S
 	return res, err
 }
 
-// UpdateNotificationIdxsInCells stays on CRDB (it is an UPDATE ... RETURNING
-// of the rows' counters); the returned rows refresh the cache.
+// idUpdater is the reference subscription store with the hook of
+// go/patches/0002-scd-rid-gpu-store-hooks.patch.
+type idUpdater interface {
+	UpdateNotificationIdxsByIDs(ctx context.Context, ids []dssmodels.ID) ([]*ridmodels.Subscription, error)
+}
+
+// notifyIDs is UpdateNotificationIdxsInCells' `cells && $1 AND ends_at >=
+// now` (subscriptions.go:204-219) on the subscriptions mirror, with the
+// subscription writes w of the calling transaction (nil outside one)
+// overlaid.  ok = false: the mirror cannot answer (invalid).
+func (t *RIDTransactor) notifyIDs(cells s2.CellUnion, w *ridWrites) (ids []dssmodels.ID, ok bool, err error) {
+	if t.Invalid() {
+		return nil, false, nil
+	}
+	if len(cells) == 0 {
+		return nil, true, nil // cells && '{}' holds for no row
+	}
+	q := Query{Cells: cells, AltLo: negInf, AltHi: posInf, TLo: t.Now().UnixNano() / 1000, THi: timeNullEndQ}
+	t.mu.RLock()
+	keys, err := t.subs.Search([]Query{q})
+	t.mu.RUnlock()
+	if err != nil {
+		return nil, false, err
+	}
+	for _, k := range keys[0] {
+		id := dssmodels.ID(k)
+		if w != nil {
+			if _, written := w.subs[id]; written {
+				continue // this transaction's version decides
+			}
+		}
+		ids = append(ids, id)
+	}
+	if w != nil {
+		for id, sub := range w.subs {
+			if sub != nil && ridSubRow(sub).Matches(q) {
+				ids = append(ids, id)
+			}
+		}
+	}
+	return ids, true, nil
+}
+
+// UpdateNotificationIdxsInCells: the subscriptions are found on the mirror
+// (notifyIDs); CRDB runs only the UPDATE ... WHERE id = ANY($ids) ...
+// RETURNING of their counters (UpdateNotificationIdxsByIDs, patch 0002).
+// The returned rows refresh the cache.
 func (t *RIDTransactor) UpdateNotificationIdxsInCells(ctx context.Context, cells s2.CellUnion) ([]*ridmodels.Subscription, error) {
-	res, err := t.Transactor.UpdateNotificationIdxsInCells(ctx, cells)
+	var res []*ridmodels.Subscription
+	var err error
+	ids, ok, err := t.notifyIDs(cells, nil)
+	if err != nil {
+		return nil, err
+	}
+	if u, hooked := t.Transactor.(idUpdater); hooked && ok {
+		res, err = u.UpdateNotificationIdxsByIDs(ctx, ids)
+	} else {
+		res, err = t.Transactor.UpdateNotificationIdxsInCells(ctx, cells)
+	}
 	if err == nil && len(res) > 0 {
 		w := newRIDWrites()
 		for _, s := range res {
@@ -214,6 +272,21 @@ func (t *RIDTransactor) UpdateNotificationIdxsInCells(ctx context.Context, cells
 		t.applyCommitted(w)
 	}
 	return res, err
+}
+
+// MaxSubscriptionCountInCellsByOwner replaces the reference's
+// (pkg/rid/cockroach/subscriptions.go:83-116; its TODO at :87-89 asks for
+// this count to be kept in memory): the subscriptions mirror answers it
+// (Mirror.MaxCount, dssg_store_max_subscription_count).  The caller
+// (application/subscription.go:69) runs it outside a transaction, as the
+// reference does.
+func (t *RIDTransactor) MaxSubscriptionCountInCellsByOwner(ctx context.Context, cells s2.CellUnion, owner dssmodels.Owner) (int, error) {
+	if t.Invalid() {
+		return t.Transactor.MaxSubscriptionCountInCellsByOwner(ctx, cells, owner)
+	}
+	t.mu.RLock()
+	defer t.mu.RUnlock()
+	return t.subs.MaxCount(cells, owner.String(), t.Now().UnixNano()/1000)
 }
 
 // SearchISAs replaces (*ISAStore).SearchISAs
@@ -292,6 +365,7 @@ func (t *RIDTransactor) SearchSubscriptionsByOwner(ctx context.Context, cells s2
 type ridRepo struct {
 	repos.Repository
 	w *ridWrites
+	t *RIDTransactor
 }
 
 func (r *ridRepo) InsertISA(ctx context.Context, isa *ridmodels.IdentificationServiceArea) (*ridmodels.IdentificationServiceArea, error) {
@@ -342,8 +416,21 @@ func (r *ridRepo) DeleteSubscription(ctx context.Context, sub *ridmodels.Subscri
 	return res, err
 }
 
+// UpdateNotificationIdxsInCells inside the transaction (application/isa.go:69
+// and its insert / delete siblings): the subscription ids from the mirror
+// with this transaction's own subscription writes overlaid, the UPDATE ...
+// RETURNING on the transaction.
 func (r *ridRepo) UpdateNotificationIdxsInCells(ctx context.Context, cells s2.CellUnion) ([]*ridmodels.Subscription, error) {
-	res, err := r.Repository.UpdateNotificationIdxsInCells(ctx, cells)
+	var res []*ridmodels.Subscription
+	ids, ok, err := r.t.notifyIDs(cells, r.w)
+	if err != nil {
+		return nil, err
+	}
+	if u, hooked := r.Repository.(idUpdater); hooked && ok {
+		res, err = u.UpdateNotificationIdxsByIDs(ctx, ids)
+	} else {
+		res, err = r.Repository.UpdateNotificationIdxsInCells(ctx, cells)
+	}
 	if err == nil {
 		for _, s := range res {
 			r.w.subs[s.ID] = s

@@ -11,6 +11,7 @@ import (
 	dssmodels "github.com/interuss/dss/pkg/models"
 	scdmodels "github.com/interuss/dss/pkg/scd/models"
 	scdstore "github.com/interuss/dss/pkg/scd/store"
+	scdc "github.com/interuss/dss/pkg/scd/store/cockroach"
 )
 
 // SCDTransactor decorates the reference's CockroachDB transactor
@@ -19,17 +20,27 @@ import (
 // searches run on GPU mirrors of the scd_operations / scd_subscriptions
 // columns:
 //   - SearchOperations and SearchSubscriptions;
-//   - UpsertOperation's conflict search and OVN set difference
-//     (operations.go:304-372), through the store hook of
-//     go/patches/0002 (UpsertOperationWithConflictSearch), so the
-//     transaction's SQL does only the row writes and the notification;
+//   - through the store hooks of go/patches/0002 (Store.SetHooks), the write
+//     path's two searches: UpsertOperation's conflict search
+//     (operations.go:337-348; the OVN check itself stays the reference's) and
+//     the notification fan-out's subscription ids
+//     (fetchSubscriptionsForNotification, subscriptions.go:128-173; CRDB runs
+//     only the UPDATE ... RETURNING of their counters);
 //   - inside a transaction, the searches see its own uncommitted writes
 //     (read-your-writes): the mirror's answer minus the rows the transaction
 //     has written, plus those of its written rows that match.
-// A transaction's writes reach the mirrors when it commits.  The mirrors see
-// only this process's writes (single writer per CRDB cluster, INTEGRATION.md);
-// if applying a committed transaction to them fails, they are marked invalid
-// and every search goes to CRDB from then on.
+// A transaction's writes reach the mirrors when it commits.
+//
+// Serialisation of the conflict check.  In the reference the conflict search
+// is a SQL read inside a SERIALIZABLE transaction, so CRDB aborts one of two
+// concurrent upserts whose volumes overlap.  A mirror read registers nothing
+// with CRDB, so a transaction that runs a conflict search on the mirror takes
+// the transactor's write lock first and holds it until its commit has been
+// applied to the mirrors (or it rolls back): the next conflict search waits
+// for it and sees its operation.  The mirrors see only this process's writes
+// (single writer per CRDB cluster, INTEGRATION.md); if applying a committed
+// transaction to them fails, they are marked invalid and every search goes
+// to CRDB from then on.
 type SCDTransactor struct {
 	Inner scdstore.Transactor
 	// Now is the store clock (the reference's cockroach.DefaultClock).
@@ -37,6 +48,7 @@ type SCDTransactor struct {
 
 	ops, subs *Mirror
 	mu        sync.RWMutex
+	writeMu   sync.Mutex // held by a transaction from its first mirror conflict search to its commit's apply
 	opRows    map[scdmodels.ID]*scdmodels.Operation
 	subRows   map[scdmodels.ID]*scdmodels.Subscription
 	invalid   int32 // atomic: 1 after a failed apply of a committed transaction
@@ -123,10 +135,17 @@ func (t *SCDTransactor) Transact() (scdstore.Transaction, error) {
 
 // scdTx records a transaction's writes (nil value: deleted) until commit.
 type scdTx struct {
-	inner scdstore.Transaction
-	t     *SCDTransactor
-	ops   map[scdmodels.ID]*scdmodels.Operation
-	subs  map[scdmodels.ID]*scdmodels.Subscription
+	inner  scdstore.Transaction
+	t      *SCDTransactor
+	ops    map[scdmodels.ID]*scdmodels.Operation
+	subs   map[scdmodels.ID]*scdmodels.Subscription
+	locked bool // holds t.writeMu (a mirror conflict search ran)
+}
+
+// hookable is the reference store with the hooks of
+// go/patches/0002-scd-rid-gpu-store-hooks.patch.
+type hookable interface {
+	SetHooks(h *scdc.Hooks)
 }
 
 func (x *scdTx) Store() (scdstore.Store, error) {
@@ -134,10 +153,34 @@ func (x *scdTx) Store() (scdstore.Store, error) {
 	if err != nil {
 		return nil, err
 	}
-	return &scdStore{Store: s, tx: x}, nil
+	st := &scdStore{Store: s, tx: x}
+	if h, ok := s.(hookable); ok && !x.t.Invalid() {
+		h.SetHooks(&scdc.Hooks{ConflictSearch: st.conflicts, NotificationSearch: st.notificationIDs})
+	}
+	return st, nil
 }
 
+// lockWrites takes the transactor's write lock once per transaction, before
+// its first conflict search on the mirror (see SCDTransactor).
+func (x *scdTx) lockWrites() {
+	if !x.locked {
+		x.t.writeMu.Lock()
+		x.locked = true
+	}
+}
+
+func (x *scdTx) unlockWrites() {
+	if x.locked {
+		x.locked = false
+		x.t.writeMu.Unlock()
+	}
+}
+
+// Commit commits on CRDB, applies the writes to the mirrors and only then
+// releases the write lock, whatever the outcome (PerformOperationWithRetries
+// starts a new transaction after a failed commit without a rollback).
 func (x *scdTx) Commit() error {
+	defer x.unlockWrites()
 	if err := x.inner.Commit(); err != nil {
 		return err
 	}
@@ -172,6 +215,7 @@ func (x *scdTx) flush() error {
 }
 
 func (x *scdTx) Rollback() error {
+	defer x.unlockWrites()
 	x.ops, x.subs = map[scdmodels.ID]*scdmodels.Operation{}, map[scdmodels.ID]*scdmodels.Subscription{}
 	return x.inner.Rollback()
 }
@@ -198,24 +242,11 @@ func (s *scdStore) refreshSub(ctx context.Context, id scdmodels.ID, owner dssmod
 	}
 }
 
-// conflictSearchStore is the reference store with the hook of
-// go/patches/0002-scd-rid-gpu-store-hooks.patch.
-type conflictSearchStore interface {
-	UpsertOperationWithConflictSearch(ctx context.Context, operation *scdmodels.Operation, key []scdmodels.OVN,
-		search func(ctx context.Context, op *scdmodels.Operation) ([]*scdmodels.Operation, error)) (*scdmodels.Operation, []*scdmodels.Subscription, error)
-}
-
+// UpsertOperation is the reference's own (its conflict search and the
+// notification ids come from the hooks installed by scdTx.Store); the
+// written row is recorded for the mirrors.
 func (s *scdStore) UpsertOperation(ctx context.Context, op *scdmodels.Operation, key []scdmodels.OVN) (*scdmodels.Operation, []*scdmodels.Subscription, error) {
-	var (
-		res  *scdmodels.Operation
-		subs []*scdmodels.Subscription
-		err  error
-	)
-	if cs, ok := s.Store.(conflictSearchStore); ok && !s.tx.t.Invalid() {
-		res, subs, err = cs.UpsertOperationWithConflictSearch(ctx, op, key, s.conflicts)
-	} else {
-		res, subs, err = s.Store.UpsertOperation(ctx, op, key)
-	}
+	res, subs, err := s.Store.UpsertOperation(ctx, op, key)
 	if err == nil && res != nil {
 		s.tx.ops[res.ID] = res
 		s.refreshSub(ctx, res.SubscriptionID, res.Owner)
@@ -225,10 +256,52 @@ func (s *scdStore) UpsertOperation(ctx context.Context, op *scdmodels.Operation,
 
 // conflicts is UpsertOperation's search (operations.go:337-348: the
 // operation's own cells, altitudes and times, ends_at >= now) on the GPU
-// mirror, with this transaction's writes overlaid.
+// mirror, with this transaction's writes overlaid, after searchOperations'
+// argument check (operations.go:405-414: the footprint is the operation's
+// cells, so only an empty covering can fail).  The transaction takes the
+// write lock first and keeps it until its commit has reached the mirrors.
 func (s *scdStore) conflicts(ctx context.Context, op *scdmodels.Operation) ([]*scdmodels.Operation, error) {
+	if len(op.Cells) == 0 {
+		return nil, dsserr.BadRequest("missing cell IDs for query")
+	}
+	s.tx.lockWrites()
 	q := opQuery(op.Cells, op.AltitudeLower, op.AltitudeUpper, op.StartTime, op.EndTime, s.tx.t.Now())
 	return s.searchOps(q)
+}
+
+// notificationIDs is fetchSubscriptionsForNotification's SELECT DISTINCT
+// (subscriptions.go:131-152) on the subscriptions mirror: the subscriptions
+// sharing a cell with cells and unexpired (the UPDATE that follows in SQL
+// keeps only ends_at >= now), with this transaction's own subscription
+// writes overlaid.
+func (s *scdStore) notificationIDs(ctx context.Context, cells []int64) ([]scdmodels.ID, error) {
+	if len(cells) == 0 {
+		return nil, nil // cell_id = ANY('{}'): no rows
+	}
+	cu := make(s2.CellUnion, len(cells))
+	for i, c := range cells {
+		cu[i] = s2.CellID(uint64(c))
+	}
+	t := s.tx.t
+	q := Query{Cells: cu, AltLo: negInf, AltHi: posInf, TLo: t.Now().UnixNano() / 1000, THi: timeNullEndQ}
+	t.mu.RLock()
+	keys, err := t.subs.Search([]Query{q})
+	t.mu.RUnlock()
+	if err != nil {
+		return nil, err
+	}
+	out := make([]scdmodels.ID, 0, len(keys[0]))
+	for _, k := range keys[0] {
+		if _, written := s.tx.subs[scdmodels.ID(k)]; !written {
+			out = append(out, scdmodels.ID(k))
+		}
+	}
+	for id, sub := range s.tx.subs {
+		if sub != nil && subRow(sub).Matches(q) {
+			out = append(out, id)
+		}
+	}
+	return out, nil
 }
 
 func (s *scdStore) DeleteOperation(ctx context.Context, id scdmodels.ID, owner dssmodels.Owner) (*scdmodels.Operation, []*scdmodels.Subscription, error) {

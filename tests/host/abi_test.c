@@ -184,7 +184,7 @@ int main(void)
         dssg_store_free(store);
     }
     /* ---- UpsertOperation replayed as go/pkg/gpu runs it --------------------
-     * (operations.go:304-372 through UpsertOperationWithConflictSearch): the
+     * (operations.go:304-372 through the ConflictSearch hook of patch 0002): the
      * conflict search on the store with the transaction's pending writes
      * overlaid on the host (Row.Matches), the OVN set difference, the write at
      * commit, the re-search. */
