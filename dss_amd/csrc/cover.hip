@@ -354,9 +354,10 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
                                           uint8_t *flags, int32_t *nvx, double2 *uv, uint64_t *st_id, uint32_t *st_i,
                                           uint32_t *st_j, uint32_t *finfo, uint4 *fbox,
                                           const double *fwd, const double *rev, const uint8_t *fan_fail,
-                                          const uint8_t *not_inner, const uint8_t *omode)
+                                          const uint8_t *not_inner, const uint8_t *omode, uint8_t *rev_out)
 {
     bool fail = false;
+    if constexpr (FAST) rev_out[f] = 0;  // (set before any bail: the exact instance reverses in place itself)
     auto bail = [&]() {
         if constexpr (FAST) {
             if (fail) slow_list[atomicAdd(slow_n, 1u)] = (uint32_t)f;
@@ -438,15 +439,19 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
             if (FAST && om == 0 && area > DSS_MAX_AREA_KM2) fail = true;  // mispredicted: no reversed terms
             if (bail()) return;
             if (area > DSS_MAX_AREA_KM2) {  // Q4: reverse in place and rebuild
-                for (int i = 0, j = nv - 1; i < j; i++, j--) {
-                    V3 t = p[i];
-                    p[i] = p[j];
-                    p[j] = t;
-                    if constexpr (FAST) {  // k_fan's (u,v) images follow the vertices
-                        double2 *uvp = uv + xoff[f];
-                        double2 w = uvp[i];
-                        uvp[i] = uvp[j];
-                        uvp[j] = w;
+                if constexpr (FAST) {
+                    // the reversed loop through a reversed view (LoopView.rev):
+                    // later kernels read it through rev_out, and k_reverse_list
+                    // moves only the descent footprints' vertices -- this
+                    // thread's serial walk of them cost 0.16 of k_setup's
+                    // 0.55 ms on configs[2]
+                    l.rev = true;
+                    rev_out[f] = 1;
+                } else {
+                    for (int i = 0, j = nv - 1; i < j; i++, j--) {
+                        V3 t = p[i];
+                        p[i] = p[j];
+                        p[j] = t;
                     }
                 }
                 origin_of<FAST>(l, fail);
@@ -566,7 +571,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAST ? DSS_S
                         uint8_t *mode, uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx, double2 *uv,
                         uint64_t *st_id, uint32_t *st_i, uint32_t *st_j, uint32_t *finfo,
                         uint4 *fbox, const double *fwd, const double *rev, const uint8_t *fan_fail,
-                        const uint8_t *not_inner, const uint8_t *omode, const uint32_t *perm)
+                        const uint8_t *not_inner, const uint8_t *omode, const uint32_t *perm, uint8_t *rev_out)
 {
     int64_t f = tid64();
     if constexpr (FAST) {
@@ -576,11 +581,41 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAST ? DSS_S
         for (int64_t i = f; i < (int64_t)*slow_n; i += (int64_t)gridDim.x * blockDim.x)
             setup_one<false>(slow_list[i], nullptr, nullptr, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out,
                              mode, origin_in, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, nullptr,
-                             nullptr, nullptr, nullptr, nullptr);
+                             nullptr, nullptr, nullptr, nullptr, nullptr);
         return;
     }
     setup_one<true>(f, slow_list, slow_n, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out, mode, origin_in,
-                    fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, fwd, rev, fan_fail, not_inner, omode);
+                    fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, fwd, rev, fan_fail, not_inner, omode,
+                    rev_out);
+}
+
+// Q4's in-place reversal, moved out of k_setup<true> (its serial walk of a
+// lane's own footprint cost 0.16 of its 0.55 ms on configs[2]): the direct
+// candidate kernels read a reversed loop through the rev flag (LoopView.rev,
+// mirrored (u,v) staging), so only the descent footprints -- a few per batch,
+// read by many kernels -- are reversed in memory here, one wave per listed
+// footprint, lanes over its vertex pairs.
+__global__ void k_reverse_list(const uint32_t *dlist, const unsigned int *dlist_n, const int64_t *xoff,
+                               const int32_t *nvx, const uint8_t *rev_flag, V3 *xyz, double2 *uv)
+{
+    const unsigned int nl = *dlist_n;
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
+    for (int64_t wi = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); wi < (int64_t)nl; wi += nw) {
+        const uint32_t f = dlist[wi];
+        if (!rev_flag[f]) continue;
+        const int64_t x0 = xoff[f];
+        const int n = nvx[f];
+        for (int i = lane; i < n / 2; i += 64) {
+            const int64_t x = x0 + i, y = x0 + (n - 1 - i);
+            const V3 a = xyz[x], b = xyz[y];
+            xyz[x] = b;
+            xyz[y] = a;
+            const double2 c = uv[x], d = uv[y];
+            uv[x] = d;
+            uv[y] = c;
+        }
+    }
 }
 
 __device__ __forceinline__ int num_edges(uint8_t md, int nv) { return md == MODE_LOOP ? nv : (md == MODE_POLYLINE ? nv - 1 : 0); }
@@ -1034,9 +1069,11 @@ __device__ __forceinline__ void key_cell(int key, uint32_t f, const uint64_t *st
 // (~1e-16 relative) cannot flip the comparison.  0 / 1, or 2 = undecided
 // (centre containment needs the exact S2 test: k_cand_exact).
 __device__ __forceinline__ int cand_edges_uv(uint32_t i, uint32_t j, const double2 *up, int nv, bool planar,
-                                             bool origin_in)
+                                             bool origin_in, bool rev)
 {
-    double2 a = up[0];
+    // (rev: a loop k_setup reversed without moving it, read mirrored)
+    auto at = [&](int e) { return up[rev ? nv - 1 - e : e]; };
+    double2 a = at(0);
     const uint32_t size = 1u << (kMaxLevel - kCoverLevel);
     const double ulo = st_to_uv((double)i / (double)kMaxSize), uhi = st_to_uv((double)(i + size) / (double)kMaxSize);
     const double vlo = st_to_uv((double)j / (double)kMaxSize), vhi = st_to_uv((double)(j + size) / (double)kMaxSize);
@@ -1045,7 +1082,7 @@ __device__ __forceinline__ int cand_edges_uv(uint32_t i, uint32_t j, const doubl
     const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
     bool in = false, par = false;
     for (int e = 0; e < nv; e++) {
-        const double2 b = up[e + 1 < nv ? e + 1 : 0];
+        const double2 b = at(e + 1 < nv ? e + 1 : 0);
         if (edge_intersects_rect(a.x, a.y, b.x, b.y, ulo - pm, uhi + pm, vlo - pm, vhi + pm)) {
             in = true;
             break;
@@ -1070,8 +1107,8 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
                                                       const uint32_t *finfo, const uint32_t *st_i,
                                                       const uint32_t *st_j, const int64_t *xoff, const int32_t *nvx,
                                                       const double2 *uv, const uint8_t *origin_in,
-                                                      unsigned long long *fkm, unsigned long long *fum, uint32_t *ulist,
-                                                      unsigned int *ulist_n)
+                                                      const uint8_t *rev_flag, unsigned long long *fkm,
+                                                      unsigned long long *fum, uint32_t *ulist, unsigned int *ulist_n)
 {
     __shared__ uint4 s_bx[kFpPer];
     __shared__ uint32_t s_info[kFpPer], s_sti[kFpPer][4], s_stj[kFpPer][4];
@@ -1096,7 +1133,7 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
             }
             s_xo[t] = xoff[f];
             nvv = (uint32_t)nvx[f];
-            s_fl[t] = ((flags[f] & FL_PLANAR) ? 1 : 0) | (origin_in[f] ? 2 : 0);
+            s_fl[t] = ((flags[f] & FL_PLANAR) ? 1 : 0) | (origin_in[f] ? 2 : 0) | (rev_flag[f] ? 4 : 0);
             cnt = (bx.y - bx.x + 1) * (bx.w - bx.z + 1);
         }
         s_nv[t] = (int)nvv;
@@ -1130,7 +1167,8 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
             if (s_vp[mid] <= k) lo = mid;
             else hi = mid;
         }
-        s_uv[k] = uv[s_xo[lo] + (k - s_vp[lo])];
+        const int i = k - s_vp[lo];
+        s_uv[k] = uv[s_xo[lo] + ((s_fl[lo] & 4) ? s_nv[lo] - 1 - i : i)];  // a reversed loop staged in its order
     }
     __syncthreads();
     const int total = s_cb[kFpPer];
@@ -1148,9 +1186,11 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
         const int key = rect_key(i13, j13, s_sti[lo], s_stj[lo], info);
         if (key < 0) continue;
         const int vb = s_vb[lo], fl = s_fl[lo];
+        // (staged vertices are in loop order already; unstaged ones are read
+        // through the reversal)
         const double2 *up = vb >= 0 ? s_uv + vb : uv + s_xo[lo];
         const int v = cand_edges_uv(i13 << (kMaxLevel - kCoverLevel), j13 << (kMaxLevel - kCoverLevel), up, s_nv[lo],
-                                    (fl & 1) != 0, (fl & 2) != 0);
+                                    (fl & 1) != 0, (fl & 2) != 0, vb < 0 && (fl & 4) != 0);
         if (v == 1) atomicOr(&s_km[lo][key >> 6], 1ull << (key & 63));
         else if (v == 2) atomicOr(&s_um[lo][key >> 6], 1ull << (key & 63));
     }
@@ -1187,7 +1227,8 @@ __global__ __launch_bounds__(256) void k_cand_exact(const uint32_t *ulist, const
                                                     const uint64_t *st_id, const uint32_t *st_i, const uint32_t *st_j,
                                                     const uint32_t *finfo, const int64_t *xoff, const V3 *xyz,
                                                     const int32_t *nvx, const uint8_t *origin_in,
-                                                    unsigned long long *fkm, const unsigned long long *fum)
+                                                    const uint8_t *rev_flag, unsigned long long *fkm,
+                                                    const unsigned long long *fum)
 {
     const unsigned int nl = *ulist_n;
     const int lane = threadIdx.x & 63;
@@ -1204,7 +1245,7 @@ __global__ __launch_bounds__(256) void k_cand_exact(const uint32_t *ulist, const
                 uint32_t i, j;
                 uint64_t id;
                 key_cell(64 * q + lane, f, st_id, st_i, st_j, info, face, i, j, id);
-                LoopView l{xyz + xoff[f], nvx[f], origin_in[f] != 0};
+                LoopView l{xyz + xoff[f], nvx[f], origin_in[f] != 0, rev_flag[f] != 0};
                 in = loop_contains(l, node_center(face, i, j, kCoverLevel));
             }
             const unsigned long long m = __ballot(in);
@@ -1842,12 +1883,13 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     hipLaunchKernelGGL(k_vowner, dim3(grid_for(n, B)), dim3(B), 0, s, n, toff, towner);
     hipLaunchKernelGGL(k_fan_area, dim3(std::min<int64_t>(grid_for(2 * nx + 1, B), 2048)), dim3(B), 0, s, toff + n,
                        towner, toff, omode, nv, xoff, xyz, fwd, rev, fan_fail);
+    uint8_t *rev_flag = revf_.ensure(n + 1);
     hipLaunchKernelGGL(k_setup<true>, dim3(grid_for(n, 64)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng,
                        radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo,
-                       fbox, fwd, rev, fan_fail, not_inner, omode, perm);
+                       fbox, fwd, rev, fan_fail, not_inner, omode, perm, rev_flag);
     hipLaunchKernelGGL(k_setup<false>, dim3(min(grid_for(n, 64), 512u)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat,
                        lng, radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j,
-                       finfo, fbox, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                       finfo, fbox, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
     int64_t *eoff = eoff_.ensure(n + 1);
     uint32_t *dlist = dlist_.ensure(n + 1);
     unsigned int *dlist_n = dlist_n_.ensure(1);
@@ -1860,6 +1902,9 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     DSS_HIP(hipMemcpyAsync(&nd_u, dlist_n, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
     const int64_t nd = nd_u;  // descent footprints (big, multi-face, polyline): the only ones k_start visits
+    if (nd > 0)
+        hipLaunchKernelGGL(k_reverse_list, dim3((unsigned)std::min<int64_t>((nd + 3) / 4, 1024)), dim3(256), 0, s, dlist,
+                           dlist_n, xoff, nvx, rev_flag, xyz, uv);
     if (std::getenv("DSS_COVER_STATS"))
         fprintf(stderr, "[cover] n %lld vertices %lld clipped edges %lld\n", (long long)n, (long long)nx, (long long)ne);
     // direct candidates (most footprints): the cells of each one's bound,
@@ -1869,9 +1914,9 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     unsigned int *ulist_n = ulist_n_.ensure(1);
     DSS_HIP(hipMemsetAsync(ulist_n, 0, sizeof(unsigned int), s));
     hipLaunchKernelGGL(k_cand_fp, dim3(grid_for(n, kFpPer)), dim3(kFpBlock), 0, s, n, flags, fbox, finfo, st_i, st_j,
-                       xoff, nvx, uv, orig, fkm, fum, ulist, ulist_n);
+                       xoff, nvx, uv, orig, rev_flag, fkm, fum, ulist, ulist_n);
     hipLaunchKernelGGL(k_cand_exact, dim3((unsigned)std::min<int64_t>(grid_for(n, B / 64), 1024)), dim3(B), 0, s, ulist,
-                       ulist_n, st_id, st_i, st_j, finfo, xoff, xyz, nvx, orig, fkm, fum);
+                       ulist_n, st_id, st_i, st_j, finfo, xoff, xyz, nvx, orig, rev_flag, fkm, fum);
     // hierarchical descent for the rest (big, multi-face, polyline footprints)
     double4 *clip_f = clipf_.ensure(ne + 1), *clip_c = clipc_.ensure(ne + 1);
     uint8_t *cflags = cflags_.ensure(ne + 1);

@@ -71,7 +71,7 @@ class CoverEngine {
     DevBuf<unsigned int> dlist_n_, xlist_n_;
     DevBuf<uint8_t> fanf_, ninner_;
     DevBuf<uint32_t> perm_, towner_;
-    DevBuf<uint8_t> omode_;
+    DevBuf<uint8_t> omode_, revf_;
     DevBuf<int64_t> tcnt_, toff_;
     DevBuf<double> fwd_, rev_;
     DevBuf<unsigned char> frames_;

@@ -17,7 +17,13 @@ struct LoopView {
     const V3 *v;
     int n;
     bool origin_inside;
-    DSS_HD V3 vertex(int i) const { return v[i % n]; }
+    bool rev = false;  // the loop is v[n-1], ..., v[0]: Q4's reversal without moving the vertices
+    DSS_HD V3 vertex(int i) const
+    {
+        const int k = i % n;
+        return v[rev ? n - 1 - k : k];
+    }
+    DSS_HD V3 at(int i) const { return v[rev ? n - 1 - i : i]; }  // 0 <= i < n
 };
 
 // loop.go bruteForceContainsPoint
@@ -306,7 +312,7 @@ DSS_HD bool loop_contains(const LoopView &l, V3 p, bool &fail)
 {
     EdgeCrosser e;
     e.init(origin_point(), p);
-    e.restart_at(l.vertex(0));
+    e.restart_at(l.at(0));
     bool inside = l.origin_inside;
     // vertices loaded 4 at a time (independent loads in flight together; the
     // chain itself is evaluated in order, as loop.go does)
@@ -315,7 +321,7 @@ DSS_HD bool loop_contains(const LoopView &l, V3 p, bool &fail)
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int i = i0 + u <= l.n ? i0 + u : l.n;
-            q[u] = l.v[i == l.n ? 0 : i];
+            q[u] = l.at(i == l.n ? 0 : i);
         }
 #pragma unroll
         for (int u = 0; u < 4; u++)
@@ -325,9 +331,10 @@ DSS_HD bool loop_contains(const LoopView &l, V3 p, bool &fail)
 }
 DSS_HD void loop_init_origin(LoopView &l, bool &fail)
 {
-    bool v1_inside = !eq(l.v[0], l.v[1]) && !eq(l.v[2], l.v[1]) && angle_contains_vertex(l.v[0], l.v[1], l.v[2], fail);
+    const V3 v0 = l.at(0), v1 = l.at(1), v2 = l.at(2);
+    bool v1_inside = !eq(v0, v1) && !eq(v2, v1) && angle_contains_vertex(v0, v1, v2, fail);
     l.origin_inside = false;
-    if (v1_inside != loop_contains(l, l.v[1], fail)) l.origin_inside = true;
+    if (v1_inside != loop_contains(l, v1, fail)) l.origin_inside = true;
 }
 DSS_HD double signed_area(V3 a, V3 b, V3 c, bool &fail) { return (double)robust_sign(a, b, c, fail) * point_area(a, b, c); }
 DSS_HD double loop_signed_area_sum(const LoopView &l, bool &fail)

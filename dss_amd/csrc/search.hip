@@ -51,9 +51,14 @@ constexpr uint32_t kLongQ = 0x20000000u;     // record: the query footprint is l
 constexpr uint32_t kQFlags = kRank0 | kCompactQ | kLongQ;
 constexpr uint32_t kNoDecode = 0xffffffffu;
 constexpr uint32_t kNoSlot = 0xffffffffu;
-// Query windows wider than this (us, ~72 min) form their own per-cell runs:
-// a narrow batch's posting range stays [min tlo - dcap, max tlo + 72 min].
-constexpr unsigned long long kWideWindow = 1ull << 32;
+// Query windows wider than a per-batch threshold T form their own per-cell
+// runs (met by every tile of the cell); the narrow ones are met only by the
+// tiles whose start range reaches [tlo - dcap, tlo + dqmax], dqmax the widest
+// narrow window.  T = 2^b minimises narrow(b) (2^b + dcap) + wide(b) H over the
+// batch's window histogram (k_qwin), H the index's time span (choose_wide_log).
+// (A fixed T = 2^32 us let a few NULL-start queries near `now` set dqmax to
+// 72 min on configs[2], whose windows are otherwise <= 30 min.)
+constexpr int kWinBuckets = 65;  // ceil(log2(window)) in 0..64
 constexpr int kOrderBits = 16;                          // query order key: quantised tlo (2 radix passes)
 constexpr uint32_t kWideKey = (1u << kOrderBits) - 1u;  // ... wide queries last
 
@@ -547,9 +552,49 @@ static_assert(sizeof(QRec) == 64, "QRec layout");
 
 
 
-__host__ __device__ __forceinline__ bool is_wide(long long tlo, long long thi)
+// ceil(log2(thi - tlo)) of a non-empty window (0 for a point), -1 if empty.
+__device__ __forceinline__ int win_bucket(long long tlo, long long thi)
 {
-    return thi >= tlo && (unsigned long long)thi - (unsigned long long)tlo > kWideWindow;
+    if (thi < tlo) return -1;
+    const unsigned long long w = (unsigned long long)thi - (unsigned long long)tlo;
+    return w <= 1ull ? (int)w : 64 - __clzll(w - 1ull);
+}
+
+// Histogram of the batch's window buckets (one LDS histogram per block).
+__global__ __launch_bounds__(kBlock) void k_qwin(int64_t nq, const int64_t *tlo, const int64_t *thi,
+                                                 unsigned long long *hist)
+{
+    __shared__ unsigned int h[kWinBuckets];
+    for (int i = threadIdx.x; i < kWinBuckets; i += kBlock) h[i] = 0;
+    __syncthreads();
+    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < nq; q += (int64_t)gridDim.x * kBlock) {
+        const int b = win_bucket(tlo[q], thi[q]);
+        if (b >= 0) atomicAdd(&h[b], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kWinBuckets; i += kBlock)
+        if (h[i]) atomicAdd(&hist[i], (unsigned long long)h[i]);
+}
+
+// The wide threshold's log2 from the histogram: windows with bucket <= b are
+// narrow.  A narrow record is loaded by the tiles of its cell whose starts lie
+// within (dqmax + dcap) of its start, a wide one by every tile (the index's
+// time span H); the cost of b is narrow(b) * (2^b + dcap) + wide(b) * H.
+__device__ __forceinline__ int choose_wide_log(const unsigned long long *hist, double dcap, double span)
+{
+    double tot = 0;
+    for (int i = 0; i < kWinBuckets; i++) tot += (double)hist[i];
+    double nar = 0, best = 1e300;
+    int bb = 64;
+    for (int b = 0; b < kWinBuckets; b++) {
+        nar += (double)hist[b];
+        const double c = nar * (ldexp(1.0, b) + dcap) + (tot - nar) * span;
+        if (c < best) {
+            best = c;
+            bb = b;
+        }
+    }
+    return bb;
 }
 
 // Per query cell: its query, level-13 decode and slot (kNoSlot when the
@@ -652,17 +697,23 @@ __device__ __forceinline__ uint32_t order_q(long long t, long long tbase, int qs
 }
 
 // Query order key: quantised tlo (narrow windows), kWideKey (wide ones); the
-// widest narrow window of the batch -> *dqmax.
+// widest narrow window of the batch -> *dqmax.  Every block derives the same
+// threshold from the batch's window histogram (k_qwin).
 __global__ __launch_bounds__(kBlock) void k_qorder(int64_t nq, const int64_t *tlo, const int64_t *thi, long long tbase,
-                                                   int qshift, uint32_t *key, uint32_t *val, unsigned long long *dqmax)
+                                                   int qshift, double dcap, const unsigned long long *whist,
+                                                   uint32_t *key, uint32_t *val, unsigned long long *dqmax)
 {
     __shared__ unsigned long long wmax[kBlock / 64];
+    __shared__ int s_wb;
+    if (threadIdx.x == 0) s_wb = choose_wide_log(whist, dcap, ldexp(1.0, kOrderBits + qshift));
+    __syncthreads();
+    const int wb = s_wb;
     const int64_t q = tid64();
     unsigned long long dq = 0;
     if (q < nq) {
         const long long a = tlo[q], b = thi[q];
         uint32_t k = kWideKey;
-        if (!is_wide(a, b)) {
+        if (win_bucket(a, b) <= wb) {  // narrow (or empty: matches nothing)
             k = order_q(a, tbase, qshift);
             if (b >= a) dq = (unsigned long long)b - (unsigned long long)a;
         }
@@ -2144,7 +2195,8 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     // (the unit counters come before the misc words: each join attempt
     // zeroes everything from misc word 6 on)
     constexpr int kCtlDq = 0, kCtlUnits = kR, kCtlUnitsL = 2 * kR, kCtlMisc = 3 * kR, kCtlQueue = 3 * kR + 16,
-                  kCtlQueueL = 4 * kR + 16, kCtlOut = 5 * kR + 16, kCtlTOut = 6 * kR + 16, kCtlWords = 7 * kR + 16;
+                  kCtlQueueL = 4 * kR + 16, kCtlOut = 5 * kR + 16, kCtlTOut = 6 * kR + 16, kCtlWin = 7 * kR + 16,
+                  kCtlWords = 7 * kR + 16 + kWinBuckets;
     unsigned long long *ctl = counter_.ensure(kCtlWords);
     unsigned long long *cnt = ctl + kCtlMisc;
     DSS_HIP(hipMemsetAsync(ctl, 0, kCtlWords * sizeof(unsigned long long), s));
@@ -2158,8 +2210,11 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     // (2) query order: narrow windows by start time, wide ones last
     uint32_t *ok0 = okey_.ensure(nq + 1), *ok1 = okey2_.ensure(nq + 1), *ov0 = oval_.ensure(nq + 1),
              *perm = perm_.ensure(nq + 1);
+    hipLaunchKernelGGL(k_qwin, dim3((unsigned)std::min<int64_t>(grid_for(nq, kBlock), 1024)), dim3(kBlock), 0, s, nq,
+                       q_tlo, q_thi, ctl + kCtlWin);
     hipLaunchKernelGGL(k_qorder, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_tlo, q_thi, (long long)idx->tbase,
-                       idx->qshift, ok0, ov0, ctl + kCtlDq);
+                       idx->qshift, (double)idx->dcap, (const unsigned long long *)(ctl + kCtlWin), ok0, ov0,
+                       ctl + kCtlDq);
     radix_sort_pairs(ok0, ok1, ov0, perm, nq, kOrderBits, tmp_, s);
     // (3) keys (slot << 1 | wide, query cell) in that order; records per cell
     int64_t *qc = qcnt_.ensure(nq + 1), *qo = qoff_.ensure(nq + 2);

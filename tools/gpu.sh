@@ -89,6 +89,26 @@ for step in "$@"; do
         [ -n "$KS" ] && cp "$KS" "$D/kernel_stats.csv"
         rm -rf "$P"
         head -${TOP:-20} "$D/pmc_summary.csv" | cut -c1-160 ;;
+    kt)  # kt:CFG:V1,V2[:ARGS] -- kernel-trace summaries of library variants (one pipeline)
+        cfg=${rest%%:*}
+        r2=${rest#*:}
+        vs=${r2%%:*}
+        args=""
+        [ "$r2" != "$vs" ] && args=${r2#*:}
+        for v in ${vs//,/ }; do
+            if [ "$v" = base ]; then unset DSS_AMD_LIB; else export DSS_AMD_LIB=$GRAFT_REPO_ROOT/dss_amd/variants/$v.so; fi
+            T=${TAG}_kt_$v
+            KT_ONLY=1 STEPS=${PSTEPS:-4} BENCH_ARGS="--config $cfg $args" bash tools/profile.sh "$T" > "$O/kt_$v.log" 2>&1 \
+                || { echo KT_FAILED $v; tail -30 "$O/kt_$v.log"; exit 1; }
+            mkdir -p "$O/kt_$v"
+            cp gpurun_out/prof/$T/summary.csv "$O/kt_$v/pmc_summary.csv"
+            KS=$(find gpurun_out/prof/$T -name 'kt_kernel_stats.csv' | head -1)
+            [ -n "$KS" ] && cp "$KS" "$O/kt_$v/kernel_stats.csv"
+            rm -rf gpurun_out/prof/$T
+            echo "-- $v"
+            head -${TOP:-16} "$O/kt_$v/pmc_summary.csv" | cut -c1-110
+        done
+        unset DSS_AMD_LIB ;;
     gloo2)
         timeout -k 10 ${BENCH_TIMEOUT:-400} python -u bench.py --gpus 2 --same-device --dist-backend gloo \
             ${rest:---scale 0.05 --steps 3 --warmup 1} > "$O/$name.json" 2> "$O/$name.err" \
