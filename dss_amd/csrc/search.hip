@@ -60,7 +60,8 @@ constexpr uint32_t kNoSlot = 0xffffffffu;
 // 72 min on configs[2], whose windows are otherwise <= 30 min.)
 constexpr int kWinBuckets = 65;  // ceil(log2(window)) in 0..64
 constexpr int kOrderBits = 16;                          // query order key: quantised tlo (2 radix passes)
-constexpr uint32_t kWideKey = (1u << kOrderBits) - 1u;  // ... wide queries last
+constexpr uint32_t kWideKey = (1u << kOrderBits) - 1u;  // quantised-start clamp
+constexpr uint32_t kWideBit = 1u << kOrderBits;  // order key: a wide query (carried above the sorted bits)
 
 // Work lists written from kRegions counters (spread 256 B apart; one
 // same-address counter saturates at ~88 atomics/us, MI355X_MICROARCH.md
@@ -696,7 +697,7 @@ __device__ __forceinline__ uint32_t order_q(long long t, long long tbase, int qs
     return d >= (unsigned long long)(kWideKey - 1) ? kWideKey - 1 : (uint32_t)d;
 }
 
-// Query order key: quantised tlo (narrow windows), kWideKey (wide ones); the
+// Query order key: quantised tlo, | kWideBit for the wide windows; the
 // widest narrow window of the batch -> *dqmax.  Every block derives the same
 // threshold from the batch's window histogram (k_qwin).
 __global__ __launch_bounds__(kBlock) void k_qorder(int64_t nq, const int64_t *tlo, const int64_t *thi, long long tbase,
@@ -712,10 +713,14 @@ __global__ __launch_bounds__(kBlock) void k_qorder(int64_t nq, const int64_t *tl
     unsigned long long dq = 0;
     if (q < nq) {
         const long long a = tlo[q], b = thi[q];
-        uint32_t k = kWideKey;
+        // wide queries are ordered by start too (kWideBit rides above the
+        // sorted bits): a regular tile's wide records are then a prefix of
+        // the cell's wide run, cut at the tile's latest possible end
+        uint32_t k = order_q(a, tbase, qshift);
         if (win_bucket(a, b) <= wb) {  // narrow (or empty: matches nothing)
-            k = order_q(a, tbase, qshift);
             if (b >= a) dq = (unsigned long long)b - (unsigned long long)a;
+        } else {
+            k |= kWideBit;
         }
         key[q] = k;
         val[q] = (uint32_t)q;
@@ -752,7 +757,7 @@ __global__ void k_qemit(int64_t nqc, const uint32_t *cq, const uint32_t *cslot, 
     const uint32_t s = cslot[k];
     if (s == kNoSlot) return;
     const uint32_t q = cq[k], r = rank[q];
-    const uint32_t wide = okey[r] == kWideKey ? 1u : 0u;
+    const uint32_t wide = (okey[r] & kWideBit) ? 1u : 0u;
     const int64_t w = off[r] + (int64_t)(vpre[k] - qvb[q]);
     key[w] = s << 1 | wide;
     val[w] = (uint32_t)k;
@@ -999,14 +1004,20 @@ __global__ void k_unit_ranges(IndexView a, Regions ur, Unit *units, const uint32
     const long long dq = (long long)min(dqm, 1ull << 62);
     for (int64_t u = tid64(); u < n; u += nthreads64()) {
         Unit &d = units[ur.slot_of(pre, u)];
-        if ((d.np & kUnitLong) || d.n1 <= d.n0) continue;
+        if ((d.np & kUnitLong) || (d.n1 <= d.n0 && d.w1 <= d.w0)) continue;
         const longlong2 f = a.b_t[d.p0], l = a.b_t[d.p0 + d.np - 1];
         const long long m0 = tmin2(f.x, f.y), m1 = tmin2(l.x, l.y);
         const long long lo = m0 < LLONG_MIN + dq ? LLONG_MIN : m0 - dq;
         const long long hi = m1 > LLONG_MAX - a.dcap ? LLONG_MAX : m1 + a.dcap;
-        const uint32_t n0 = lb_q(sq, d.n0, d.n1, order_q(lo, tbase, qshift));
-        d.n1 = lb_q(sq, n0, d.n1, order_q(hi, tbase, qshift) + 1u);
-        d.n0 = n0;
+        const uint32_t qhi = order_q(hi, tbase, qshift) + 1u;
+        if (d.n1 > d.n0) {
+            const uint32_t n0 = lb_q(sq, d.n0, d.n1, order_q(lo, tbase, qshift));
+            d.n1 = lb_q(sq, n0, d.n1, qhi);
+            d.n0 = n0;
+        }
+        // wide records (start-ordered within the cell's wide run) starting
+        // after every posting of the tile has ended meet none of them
+        if (d.w1 > d.w0) d.w1 = lb_q(sq, d.w0, d.w1, qhi);
     }
 }
 
