@@ -393,6 +393,44 @@ def cover_ahead_steps(torch, D, ctx, covers, d_q, steps, search_fn):
         th.join()
 
 
+def sharded_pipeline_steps(torch, D, pipes, d_q, qargs, nq, steps):
+    """`steps` native sharded steps over P pipelines, each its own context,
+    stream, host thread and communicator (dssg_sharded_search_device): step k
+    runs on pipeline k % P, so every communicator sees its calls in the same
+    order on every rank while the pipelines overlap one another's cover, join
+    and exchanges.  A failing pipeline raises StepFailure (the others are
+    left to finish their own steps: a collective cannot be abandoned on one
+    rank alone)."""
+    import threading
+    P = len(pipes)
+    errors = []
+    done = [0] * P
+
+    def run(p):
+        pctx, ps, nat = pipes[p]
+        try:
+            with torch.cuda.stream(ps):
+                for _ in range(p, steps, P):
+                    c = D.cover(pctx, d_q)
+                    nat.step(c.offs, c.cells, nq, *qargs)
+                    done[p] += 1
+                ps.synchronize()
+        except BaseException as e:  # noqa: BLE001 -- re-raised on the calling thread
+            errors.append(e)
+
+    threads = [threading.Thread(target=run, args=(p,)) for p in range(1, P)]
+    for th in threads:
+        th.start()
+    run(0)
+    for th in threads:
+        th.join()
+    if errors:
+        raise StepFailure(f"{len(errors)} sharded pipeline(s) failed ({sum(done)} of {steps} steps finished): "
+                          f"{type(errors[0]).__name__}: {errors[0]}") from errors[0]
+    if sum(done) != steps:
+        raise StepFailure(f"{sum(done)} of {steps} sharded steps finished")
+
+
 def main():
     argv = sys.argv[1:]
     args = parse_args(argv)
@@ -523,10 +561,48 @@ def main():
     # thread, warmed to its steady-state buffers and kept only if HBM holds it
     workers, pipe_note = add_pipelines(args, torch, D, _lib, local, dev, tunes, d_q,
                                        None if sharded is not None else (index, qargs))
+    pipes = []  # native sharded pipelines: (context, stream, NativeShardedSearch), one communicator each
+    if native is not None:
+        # every rank runs the same number of pipelines (one communicator per
+        # pipeline, created in the same order everywhere)
+        npipe = torch.tensor([1 + len(workers)], device=dev)
+        dist.all_reduce(npipe, op=dist.ReduceOp.MIN)
+        while 1 + len(workers) > int(npipe.item()):
+            workers.pop()[0].close()
+        pipes.append((ctx, torch.cuda.current_stream(), native))
+        for wctx, ws in workers:
+            uid = torch.zeros(_lib.COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+            if rank == 0:
+                uid.copy_(torch.frombuffer(bytearray(shard.NativeComm.unique_id(ctx)), dtype=torch.uint8))
+            dist.broadcast(uid, 0)
+            nat = shard.NativeShardedSearch(wctx, shard.NativeComm(wctx, world, rank, bytes(uid.cpu().numpy())),
+                                            index, ranges)
+            with torch.cuda.stream(ws):  # warm it (a collective step: same order on every rank)
+                c = D.cover(wctx, d_q)
+                nat.step(c.offs, c.cells, nq, *qargs)
+                ws.synchronize()
+            pipes.append((wctx, ws, nat))
 
     # ------------------------------------------------------------ timed steps
     stage("timed steps")
-    if sharded is not None:
+    general = None
+    if pipes:
+        elapsed = timed(torch, dist, dev, world,
+                        lambda: sharded_pipeline_steps(torch, D, pipes, d_q, qargs, nq, args.steps))
+        if world == 1:
+            # one rank: the library routes by the identity; the general path
+            # (route, own segment copied, unpack, join, own pairs to the
+            # output) timed beside it
+            for pctx, _, _ in pipes:
+                pctx.set_tuning("route_identity", 0)
+            sharded_pipeline_steps(torch, D, pipes, d_q, qargs, nq, len(pipes))
+            gt = timed(torch, dist, dev, world,
+                       lambda: sharded_pipeline_steps(torch, D, pipes, d_q, qargs, nq, args.steps))
+            for pctx, _, _ in pipes:
+                pctx.set_tuning("route_identity", 1)
+            general = {"value": world * nq * args.steps / gt, "ms_per_step": 1000.0 * gt / max(1, args.steps),
+                       "note": "one rank with the routing forced through the general path (route_identity=0)"}
+    elif sharded is not None:
         elapsed = timed(torch, dist, dev, world,
                         lambda: cover_ahead_steps(torch, D, ctx, workers, d_q, args.steps, shard_search))
     else:
@@ -545,6 +621,8 @@ def main():
         replica = {"value": world * nq * args.steps / rt, "ms_per_step": 1000.0 * rt / max(1, args.steps),
                    "pipelines_per_gpu": 1 + len(workers),
                    "note": "whole index on every GPU, each rank's batch joined locally (no exchange)"}
+        if general is not None:
+            replica["sharded_general_path"] = general
         native_pairs = None
         if native is not None:  # the timed path's own output, checked below beside the torch path's
             c = D.cover(ctx, d_q)
@@ -552,11 +630,13 @@ def main():
             nq_ = D.copy_back(ctx, p.q, int(p.n), np.uint32).astype(np.uint64)
             ne_ = D.copy_back(ctx, p.e, int(p.n), np.uint32).astype(np.uint64)
             native_pairs = (nq_ << np.uint64(32)) | ne_
+        for _, _, nat in pipes:
+            nat.comm.close()
         for wctx, _ in workers:
             wctx.close()
         sharded_report(args, ctx, D, dist, torch, sharded, step, None if args.no_verify else full_index,
                        i_cells_h, ranges, rank, world, nq, ni, n_post, build_s, value, ms_per_step, *qargs,
-                       exchange=exchange, replica=replica, native_pairs=native_pairs)
+                       exchange=exchange, replica=replica, native_pairs=native_pairs, pipelines=max(1, len(pipes)))
         if args.no_verify:
             ctx.L.dssg_index_free(full_index)
         ctx.L.dssg_index_free(index)
@@ -698,7 +778,7 @@ def pair_checksum(keys: np.ndarray) -> int:
 
 def sharded_report(args, ctx, D, dist, torch, sh, step, full, i_cells_h, ranges, rank, world, nq, ni, n_post, build_s,
                    value, ms_per_step, q_alo, q_ahi, q_tlo, q_thi, exchange="torch", replica=None,
-                   native_pairs=None):
+                   native_pairs=None, pipelines=1):
     """Phase breakdown (synchronised passes, max over ranks), the shard join's
     roofline, and parity: every rank's delivered pair set == a whole-index
     search of its own queries (count + order-independent checksum)."""
@@ -724,11 +804,11 @@ def sharded_report(args, ctx, D, dist, torch, sh, step, full, i_cells_h, ranges,
     ph = tph.tolist()
     phase = dict(zip(["cover"] + names + ["join_kernel"], ph))
     # shard join roofline (DESIGN.md s5 byte model over what this shard joined)
-    rc = sh.last_recv_cells.cpu().numpy().view(np.uint64)
+    nrc = sh.last_recv_ncells
     p_touched = sh.last_touched
-    jb = 24 * sh.last_rows + 8 * len(rc) + 28 * p_touched + 8 * sh.last_shard_pairs
+    jb = 24 * sh.last_rows + 8 * nrc + 28 * p_touched + 8 * sh.last_shard_pairs
     kern = ph[-1]
-    local = torch.tensor([jb / (float(np.mean(kern_ms)) * 1e-3) / 1e9, float(sh.last_rows), float(len(rc)),
+    local = torch.tensor([jb / (float(np.mean(kern_ms)) * 1e-3) / 1e9, float(sh.last_rows), float(nrc),
                           float(sh.last_shard_pairs), float(out.numel())], dtype=torch.float64, device=dev)
     mins = local.clone()
     dist.all_reduce(mins, op=dist.ReduceOp.MIN)
@@ -773,7 +853,9 @@ def sharded_report(args, ctx, D, dist, torch, sh, step, full, i_cells_h, ranges,
                    "queries_per_gpu_step": nq, "intents": ni, "postings_rank0": n_post,
                    "parallelism": f"cell-range shards x{world}; queries routed to shards and pairs routed home by "
                                   f"all-to-all ({'the library RCCL communicator' if exchange == 'native' else args.dist_backend})",
-                   "exchange": exchange, "scale": args.scale},
+                   "exchange": exchange, "scale": args.scale, "pipelines_per_gpu": pipelines,
+                   "pipelines_note": "one communicator per pipeline; step k on pipeline k % P" if pipelines > 1 else
+                   "one pipeline (exchange + shard join in step order; covers ahead on the others)"},
         "replica": replica,
         "coverings_per_s": world * nq / (phase["cover"] * 1e-3),
         "phase_ms_max_over_ranks": phase,

@@ -143,11 +143,12 @@ def load():
         L.dssg_notify_subscriptions.argtypes = [vp, vp, i64, P(i64), P(u64), i64, P(u32), P(u32), P(i64), i64, P(i64)]
         L.dssg_owner_subscriptions.argtypes = [vp, vp, i64, P(i32), i64, P(u32), P(u32), i64, P(i64)]
         L.dssg_max_subscription_count.argtypes = [vp, vp, i64, P(i64), P(u64), P(i32), i64, P(i64)]
-        L.dssg_route_plan_device.argtypes = [vp, i64, vp, vp, i32, vp, vp, P(i64), P(i64)]
-        L.dssg_route_fill_device.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
-        L.dssg_unpack_queries_device.argtypes = [vp, i64, vp, vp, i32, P(i64), vp, P(Batch)]
-        L.dssg_route_pairs_plan_device.argtypes = [vp, P(Batch), P(Pairs), i32, vp, P(i64)]
-        L.dssg_route_pairs_fill_device.argtypes = [vp, P(Batch), P(Pairs), vp, vp]
+        L.dssg_route_plan_device.argtypes = [vp, i64, vp, vp, i32, vp, vp, P(i64), P(i64), P(i64)]
+        L.dssg_route_fill_device.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.dssg_unpack_queries_device.argtypes = [vp, vp, i32, P(i64), P(i64), vp, P(Batch)]
+        L.dssg_route_pairs_plan_device.argtypes = [vp, P(Batch), P(Pairs), i32, i32, vp, P(i64)]
+        L.dssg_route_pairs_fill_device.argtypes = [vp, P(Batch), P(Pairs), vp, vp, vp, vp]
+        L.dssg_unpack_pairs_device.argtypes = [vp, i64, vp, vp, vp, vp]
         L.dssg_phase_times.argtypes = [vp, P(d), P(d), P(d)]
         L.dssg_set_timing.argtypes = [vp, C.c_int]
         L.dssg_set_timing.restype = None

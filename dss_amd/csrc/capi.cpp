@@ -37,6 +37,7 @@ struct dssg_ctx {
     dss::IngressEngine ingress;
     std::string last_error;
     bool timing = false;
+    bool route_identity = true;  // sharded step on one rank: the batch is its own (see dssg_sharded_search_device)
     double cover_ms = 0, join_ms = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // host-API staging
@@ -241,6 +242,10 @@ int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value)
     }
     if (std::string(key) == "small_search") {  // max queries of the one-launch small-batch join (0: never)
         ctx->search.set_small_max_q(value);
+        return DSSG_OK;
+    }
+    if (std::string(key) == "route_identity") {  // 0: a one-rank sharded step still routes (the general path)
+        ctx->route_identity = value != 0;
         return DSSG_OK;
     }
     if (std::string(key) == "cover_wave") {  // max batch of the wave-path covering (0: general pipeline only)
@@ -591,59 +596,68 @@ int dssg_search_subscriptions(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, 
 
 int dssg_route_plan_device(dssg_ctx *ctx, int64_t nq, const int64_t *d_q_offs, const uint64_t *d_q_cells,
                            int32_t nparts, const uint64_t *d_part_hi, void *stream, int64_t *row_counts,
-                           int64_t *cell_counts)
+                           int64_t *cell_counts, int64_t *seg_bytes)
 {
-    if (!ctx || nq < 0 || !d_part_hi || !row_counts || !cell_counts || nparts < 1 || nparts > DSSG_MAX_PARTS ||
-        (nq > 0 && (!d_q_offs || !d_q_cells)))
+    if (!ctx || nq < 0 || !d_part_hi || !row_counts || !cell_counts || !seg_bytes || nparts < 1 ||
+        nparts > DSSG_MAX_PARTS || (nq > 0 && (!d_q_offs || !d_q_cells)))
         return DSSG_ERR_INVALID;
     return guarded(ctx, [&] {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-        ctx->route.plan(nq, d_q_offs, d_q_cells, nparts, d_part_hi, s, row_counts, cell_counts);
+        ctx->route.plan(nq, d_q_offs, d_q_cells, nparts, d_part_hi, s, row_counts, cell_counts, seg_bytes);
     });
 }
 
 int dssg_route_fill_device(dssg_ctx *ctx, int64_t nq, const int64_t *d_q_offs, const uint64_t *d_q_cells,
                            const float *d_q_alt_lo, const float *d_q_alt_hi, const int64_t *d_q_tlo,
-                           const int64_t *d_q_thi, void *stream, void *d_rows_out, uint64_t *d_cells_out)
+                           const int64_t *d_q_thi, void *stream, void *d_send)
 {
     if (!ctx || nq < 0 || (nq > 0 && (!d_q_offs || !d_q_cells || !d_q_alt_lo || !d_q_alt_hi || !d_q_tlo || !d_q_thi ||
-                                      !d_rows_out || !d_cells_out)))
+                                      !d_send)))
         return DSSG_ERR_INVALID;
     return guarded(ctx, [&] {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-        ctx->route.fill(nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo, d_q_thi, s, d_rows_out, d_cells_out);
+        ctx->route.fill(nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo, d_q_thi, s, d_send);
     });
 }
 
-int dssg_unpack_queries_device(dssg_ctx *ctx, int64_t nrows, const void *d_rows, const uint64_t *d_cells,
-                               int32_t nparts, const int64_t *src_rows, void *stream, dssg_batch *out)
+int dssg_unpack_queries_device(dssg_ctx *ctx, const void *d_recv, int32_t nparts, const int64_t *src_rows,
+                               const int64_t *src_cells, void *stream, dssg_batch *out)
 {
-    if (!ctx || !out || nrows < 0 || !src_rows || nparts < 1 || nparts > DSSG_MAX_PARTS || (nrows > 0 && !d_rows))
-        return DSSG_ERR_INVALID;
+    if (!ctx || !out || !src_rows || !src_cells || nparts < 1 || nparts > DSSG_MAX_PARTS) return DSSG_ERR_INVALID;
     return guarded(ctx, [&] {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-        ctx->route.unpack(nrows, d_rows, d_cells, nparts, src_rows, s, out);
+        ctx->route.unpack(d_recv, nparts, src_rows, src_cells, s, out);
     });
 }
 
 int dssg_route_pairs_plan_device(dssg_ctx *ctx, const dssg_batch *batch, const dssg_pairs *pairs, int32_t nparts,
-                                 void *stream, int64_t *counts)
+                                 int32_t self_part, void *stream, int64_t *counts)
 {
-    if (!ctx || !batch || !pairs || !counts || nparts < 1 || nparts > DSSG_MAX_PARTS || pairs->n < 0)
+    if (!ctx || !batch || !pairs || !counts || nparts < 1 || nparts > DSSG_MAX_PARTS || pairs->n < 0 ||
+        self_part < -1 || self_part >= nparts)
         return DSSG_ERR_INVALID;
     return guarded(ctx, [&] {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-        ctx->route.pairs_plan(batch, pairs, nparts, s, counts);
+        ctx->route.pairs_plan(batch, pairs, nparts, self_part, s, counts);
     });
 }
 
 int dssg_route_pairs_fill_device(dssg_ctx *ctx, const dssg_batch *batch, const dssg_pairs *pairs, void *stream,
-                                 uint64_t *d_out)
+                                 uint64_t *d_send, uint32_t *d_self_q, uint32_t *d_self_e)
 {
-    if (!ctx || !batch || !pairs || pairs->n < 0 || (pairs->n > 0 && !d_out)) return DSSG_ERR_INVALID;
+    if (!ctx || !batch || !pairs || pairs->n < 0) return DSSG_ERR_INVALID;
     return guarded(ctx, [&] {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-        ctx->route.pairs_fill(batch, pairs, s, d_out);
+        ctx->route.pairs_fill(batch, pairs, s, d_send, d_self_q, d_self_e);
+    });
+}
+
+int dssg_unpack_pairs_device(dssg_ctx *ctx, int64_t n, const uint64_t *d_in, uint32_t *d_q, uint32_t *d_e, void *stream)
+{
+    if (!ctx || n < 0 || (n > 0 && (!d_in || !d_q || !d_e))) return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        dss::RouteEngine::split_pairs(n, d_in, d_q, d_e, s);
     });
 }
 
@@ -1024,38 +1038,50 @@ struct dssg_comm {
     ncclComm_t comm = nullptr;
     int nranks = 0, rank = 0, device = 0;
     dss::DevBuf<int64_t> d_counts;                 // allgathered count vectors
-    dss::DevBuf<unsigned char> send_rows, recv_rows, recv_cells_b;
-    dss::DevBuf<uint64_t> send_cells, send_pairs, recv_pairs;
+    int64_t *h_counts = nullptr;                   // pinned: their host copy
+    dss::DevBuf<unsigned char> send_q, recv_q;     // fused query segments
+    dss::DevBuf<uint64_t> send_pairs, recv_pairs;  // packed pairs of the other ranks' queries
     dss::DevBuf<uint32_t> out_q, out_e;
+    ~dssg_comm()
+    {
+        if (h_counts) (void)hipHostFree(h_counts);
+    }
 };
 
 namespace {
 
-// Every rank's k-vector of int64 counts -> counts[s * k + j] = rank s's j-th (host).
-void allgather_counts(dssg_comm *c, const int64_t *mine, int k, std::vector<int64_t> &all, hipStream_t s)
+// Every rank's k-vector of int64 counts -> all[s * k + j] = rank s's j-th
+// (host, pinned: no staging copy).
+const int64_t *allgather_counts(dssg_comm *c, const int64_t *mine, int k, hipStream_t s)
 {
-    int64_t *d = c->d_counts.ensure((size_t)k * (c->nranks + 1));
-    DSS_HIP(hipMemcpyAsync(d + (size_t)k * c->nranks, mine, sizeof(int64_t) * k, hipMemcpyHostToDevice, s));
+    const size_t words = (size_t)k * (c->nranks + 1);
+    int64_t *d = c->d_counts.ensure(words);
+    if (!c->h_counts) DSS_HIP(hipHostMalloc((void **)&c->h_counts, sizeof(int64_t) * 2 * DSSG_MAX_PARTS *
+                                                                       (DSSG_MAX_PARTS + 1), hipHostMallocDefault));
+    int64_t *h = c->h_counts;
+    std::memcpy(h + (size_t)k * c->nranks, mine, sizeof(int64_t) * k);
+    DSS_HIP(hipMemcpyAsync(d + (size_t)k * c->nranks, h + (size_t)k * c->nranks, sizeof(int64_t) * k,
+                           hipMemcpyHostToDevice, s));
     nccl_check(rccl().allGather(d + (size_t)k * c->nranks, d, (size_t)k * sizeof(int64_t), ncclChar, c->comm, s),
                "ncclAllGather");
-    all.resize((size_t)k * c->nranks);
-    DSS_HIP(hipMemcpyAsync(all.data(), d, sizeof(int64_t) * all.size(), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipMemcpyAsync(h, d, sizeof(int64_t) * (size_t)k * c->nranks, hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
+    return h;
 }
 
-// Grouped point-to-point all-to-all of byte blocks (part-major buffers).
-void alltoallv(dssg_comm *c, const void *send, const int64_t *sbytes, void *recv, const int64_t *rbytes, hipStream_t s)
+// Grouped point-to-point all-to-all of byte blocks at explicit offsets; the
+// caller's own block (p == rank) is not sent (it is copied, or used in place).
+void alltoallv(dssg_comm *c, const void *send, const int64_t *soff, const int64_t *sbytes, void *recv,
+               const int64_t *roff, const int64_t *rbytes, hipStream_t s)
 {
     Rccl &r = rccl();
     nccl_check(r.groupStart(), "ncclGroupStart");
-    int64_t so = 0, ro = 0;
     for (int p = 0; p < c->nranks; p++) {
+        if (p == c->rank) continue;
         if (sbytes[p] > 0)
-            nccl_check(r.send((const char *)send + so, (size_t)sbytes[p], ncclChar, p, c->comm, s), "ncclSend");
+            nccl_check(r.send((const char *)send + soff[p], (size_t)sbytes[p], ncclChar, p, c->comm, s), "ncclSend");
         if (rbytes[p] > 0)
-            nccl_check(r.recv((char *)recv + ro, (size_t)rbytes[p], ncclChar, p, c->comm, s), "ncclRecv");
-        so += sbytes[p];
-        ro += rbytes[p];
+            nccl_check(r.recv((char *)recv + roff[p], (size_t)rbytes[p], ncclChar, p, c->comm, s), "ncclRecv");
     }
     nccl_check(r.groupEnd(), "ncclGroupEnd");
 }
@@ -1110,7 +1136,17 @@ int dssg_comm_alltoallv_device(dssg_ctx *ctx, dssg_comm *comm, const void *d_sen
     if (!ctx || !comm || !send_bytes || !recv_bytes) return DSSG_ERR_INVALID;
     return guarded(ctx, [&] {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-        alltoallv(comm, d_send, send_bytes, d_recv, recv_bytes, s);
+        int64_t so[DSSG_MAX_PARTS], ro[DSSG_MAX_PARTS], a = 0, b = 0;
+        for (int p = 0; p < comm->nranks; p++) {
+            so[p] = a;
+            ro[p] = b;
+            a += send_bytes[p];
+            b += recv_bytes[p];
+        }
+        const int me = comm->rank;
+        if (send_bytes[me] != recv_bytes[me]) throw dss::Error(DSSG_ERR_INVALID, "alltoallv: own block sizes differ");
+        if (send_bytes[me] > 0) dss::device_copy((char *)d_recv + ro[me], (const char *)d_send + so[me], send_bytes[me], s);
+        alltoallv(comm, d_send, so, send_bytes, d_recv, ro, recv_bytes, s);
     });
 }
 
@@ -1125,71 +1161,73 @@ int dssg_sharded_search_device(dssg_ctx *ctx, dssg_comm *comm, const dssg_index 
     return guarded(ctx, [&] {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
         const int W = comm->nranks, me = comm->rank;
-        // (1) route this rank's queries to the shards owning their cells
-        int64_t rows_n[DSSG_MAX_PARTS], cells_n[DSSG_MAX_PARTS];
-        ctx->route.plan(nq, d_q_offs, d_q_cells, W, d_part_hi, s, rows_n, cells_n);
-        int64_t nrow = 0, ncell = 0;
-        for (int p = 0; p < W; p++) {
-            nrow += rows_n[p];
-            ncell += cells_n[p];
+        if (W == 1 && ctx->route_identity) {
+            // one part owns every cell: routing is the identity, the batch
+            // is joined as given (no copies, no collectives)
+            ctx->search.search(shard, nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo, d_q_thi, nullptr, s, out);
+            out->n_tagged = 0;
+            return;
         }
-        unsigned char *srows = comm->send_rows.ensure((size_t)nrow * DSSG_ROUTE_ROW_BYTES + 1);
-        uint64_t *scells = comm->send_cells.ensure((size_t)ncell + 1);
-        ctx->route.fill(nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo, d_q_thi, s, srows, scells);
-        // (2) exchange the query rows and their cell lists
-        std::vector<int64_t> cnt;
+        // (1) route this rank's queries to the parts owning their cells: one
+        // fused segment [rows | cells] per part
+        int64_t rows_n[DSSG_MAX_PARTS], cells_n[DSSG_MAX_PARTS], seg[DSSG_MAX_PARTS];
+        ctx->route.plan(nq, d_q_offs, d_q_cells, W, d_part_hi, s, rows_n, cells_n, seg);
+        int64_t so[DSSG_MAX_PARTS], stot = 0;
+        for (int p = 0; p < W; p++) {
+            so[p] = stot;
+            stot += seg[p];
+        }
+        unsigned char *sq = comm->send_q.ensure((size_t)stot + 32);
+        ctx->route.fill(nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo, d_q_thi, s, sq);
+        // (2) one count exchange, one all-to-all of the segments (own segment copied)
         int64_t mine[2 * DSSG_MAX_PARTS];
         for (int p = 0; p < W; p++) {
             mine[p] = rows_n[p];
             mine[W + p] = cells_n[p];
         }
-        allgather_counts(comm, mine, 2 * W, cnt, s);
-        int64_t sb[DSSG_MAX_PARTS], rb[DSSG_MAX_PARTS], src_rows[DSSG_MAX_PARTS], rrow = 0, rcell = 0;
+        const int64_t *cnt = allgather_counts(comm, mine, 2 * W, s);
+        int64_t src_rows[DSSG_MAX_PARTS], src_cells[DSSG_MAX_PARTS], rb[DSSG_MAX_PARTS], ro[DSSG_MAX_PARTS], rtot = 0;
         for (int p = 0; p < W; p++) {
             src_rows[p] = cnt[(size_t)p * 2 * W + me];
-            rrow += src_rows[p];
-            rcell += cnt[(size_t)p * 2 * W + W + me];
+            src_cells[p] = cnt[(size_t)p * 2 * W + W + me];
+            rb[p] = dss::route_segment_bytes(src_rows[p], src_cells[p]);
+            ro[p] = rtot;
+            rtot += rb[p];
         }
-        unsigned char *rrows = comm->recv_rows.ensure((size_t)rrow * DSSG_ROUTE_ROW_BYTES + 1);
-        uint64_t *rcells = (uint64_t *)comm->recv_cells_b.ensure(sizeof(uint64_t) * ((size_t)rcell + 1));
-        for (int p = 0; p < W; p++) {
-            sb[p] = rows_n[p] * DSSG_ROUTE_ROW_BYTES;
-            rb[p] = src_rows[p] * DSSG_ROUTE_ROW_BYTES;
-        }
-        alltoallv(comm, srows, sb, rrows, rb, s);
-        for (int p = 0; p < W; p++) {
-            sb[p] = cells_n[p] * (int64_t)sizeof(uint64_t);
-            rb[p] = cnt[(size_t)p * 2 * W + W + me] * (int64_t)sizeof(uint64_t);
-        }
-        alltoallv(comm, scells, sb, rcells, rb, s);
+        unsigned char *rq = comm->recv_q.ensure((size_t)rtot + 32);
+        if (seg[me] > 0) dss::device_copy(rq + ro[me], sq + so[me], (size_t)seg[me], s);
+        alltoallv(comm, sq, so, seg, rq, ro, rb, s);
         // (3) the received queries against this rank's shard
         dssg_batch batch{};
-        ctx->route.unpack(rrow, rrows, rcells, W, src_rows, s, &batch);
+        ctx->route.unpack(rq, W, src_rows, src_cells, s, &batch);
         dssg_pairs pairs{};
         ctx->search.search(shard, batch.n, batch.offs, batch.cells, batch.alt_lo, batch.alt_hi, batch.tlo, batch.thi,
                            nullptr, s, &pairs);
-        // (4) pairs back to their queries' home ranks
+        // (4) pairs home: this rank's own straight into its output, the
+        // others' packed (home-local query << 32 | entity) and all-to-all'd
         int64_t pn[DSSG_MAX_PARTS];
-        ctx->route.pairs_plan(&batch, &pairs, W, s, pn);
-        int64_t npair = 0;
-        for (int p = 0; p < W; p++) npair += pn[p];
-        uint64_t *spairs = comm->send_pairs.ensure((size_t)npair + 1);
-        ctx->route.pairs_fill(&batch, &pairs, s, spairs);
-        allgather_counts(comm, pn, W, cnt, s);
-        int64_t rpair = 0;
+        ctx->route.pairs_plan(&batch, &pairs, W, me, s, pn);
+        const int64_t *pc = allgather_counts(comm, pn, W, s);
+        int64_t psb[DSSG_MAX_PARTS], pso[DSSG_MAX_PARTS], prb[DSSG_MAX_PARTS], pro[DSSG_MAX_PARTS], ps = 0, pr = 0;
         for (int p = 0; p < W; p++) {
-            sb[p] = pn[p] * (int64_t)sizeof(uint64_t);
-            rb[p] = cnt[(size_t)p * W + me] * (int64_t)sizeof(uint64_t);
-            rpair += cnt[(size_t)p * W + me];
+            psb[p] = p == me ? 0 : pn[p] * (int64_t)sizeof(uint64_t);
+            pso[p] = ps;
+            ps += psb[p];
+            prb[p] = p == me ? 0 : pc[(size_t)p * W + me] * (int64_t)sizeof(uint64_t);
+            pro[p] = pr;
+            pr += prb[p];
         }
-        uint64_t *rpairs = comm->recv_pairs.ensure((size_t)rpair + 1);
-        alltoallv(comm, spairs, sb, rpairs, rb, s);
-        uint32_t *q = comm->out_q.ensure((size_t)rpair + 1), *e = comm->out_e.ensure((size_t)rpair + 1);
-        dss::RouteEngine::split_pairs(rpair, rpairs, q, e, s);
+        const int64_t nself = pn[me], nrecv = pr / (int64_t)sizeof(uint64_t);
+        uint64_t *spairs = comm->send_pairs.ensure((size_t)ps / sizeof(uint64_t) + 1);
+        uint32_t *q = comm->out_q.ensure((size_t)(nself + nrecv) + 1), *e = comm->out_e.ensure((size_t)(nself + nrecv) + 1);
+        ctx->route.pairs_fill(&batch, &pairs, s, spairs, q, e);
+        uint64_t *rpairs = comm->recv_pairs.ensure((size_t)nrecv + 1);
+        alltoallv(comm, spairs, pso, psb, rpairs, pro, prb, s);
+        dss::RouteEngine::split_pairs(nrecv, rpairs, q + nself, e + nself, s);
         DSS_HIP(hipStreamSynchronize(s));
         out->q = q;
         out->e = e;
-        out->n = rpair;
+        out->n = nself + nrecv;
         out->n_tagged = 0;
     });
 }

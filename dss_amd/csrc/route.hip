@@ -5,14 +5,18 @@
 // and lets the SQL layer fan a query out to the ranges its cells hit.  Here
 // the fan-out is explicit, one process per GPU:
 //
-//   home rank:  covered query batch --k_route<0>/k_route<1>--> part-major
-//               send buffers (one 32-byte row + the query's whole cell list
-//               per (query, shard that owns >= 1 of its cells));
+//   home rank:  covered query batch --k_route<0>/k_route<1>--> one send
+//               buffer of part-major segments, each [rows | cells] (one
+//               32-byte row per (query, shard that owns >= 1 of its cells),
+//               then those queries' whole cell lists, padded to 32 bytes):
+//               one all-to-all carries both;
 //   exchange:   all-to-all (RCCL over xGMI; dss_amd/shard.py);
-//   shard:      k_unpack_rows -> a plain query batch for dssg_search_device
-//               against the shard's cell-range index;
-//   shard:      k_route_pairs<0>/<1> -> the pair set, part-major by the
-//               query's home rank, packed (home-local query << 32 | entity);
+//   shard:      k_unpack_rows + k_gather_cells -> a plain query batch for
+//               dssg_search_device against the shard's cell-range index;
+//   shard:      k_route_pairs<0>/<1> -> the pair set by the query's home
+//               rank: the shard's own queries' pairs straight into its
+//               output arrays, the others part-major, packed
+//               (home-local query << 32 | entity);
 //   exchange:   all-to-all back; each home rank holds its queries' pairs.
 //
 // A shard receives a query's WHOLE cell list, and the shard index keeps every
@@ -129,17 +133,30 @@ __global__ __launch_bounds__(kBlock) void k_route(int64_t nq, const int64_t *off
     }
 }
 
-// Received rows (source-part-major) -> a plain query batch: SoA attributes,
-// per-row cell counts (scanned into offsets by the host driver), home part
-// and home-local query id.
-__global__ void k_unpack_rows(int64_t n, const QRow *rows, int np, const int64_t *src_base, int64_t *ncells, float *alo,
+// Received segments (source-part-major) -> a plain query batch: SoA
+// attributes, per-row cell counts (scanned into offsets by the host driver),
+// home part and home-local query id.  t: per source, its first batch row (a),
+// its segment's byte offset (b) and its first batch cell (c).
+struct PartTable {
+    int64_t a[DSSG_MAX_PARTS + 1], b[DSSG_MAX_PARTS + 1], c[DSSG_MAX_PARTS + 1];
+};
+__device__ __forceinline__ int src_of(const int64_t *base, int np, int64_t i)  // last s with base[s] <= i
+{
+    int lo = 0, hi = np;
+    while (hi - lo > 1) {
+        const int m = (lo + hi) >> 1;
+        if (base[m] <= i) lo = m;
+        else hi = m;
+    }
+    return lo;
+}
+__global__ void k_unpack_rows(int64_t n, const unsigned char *recv, int np, PartTable t, int64_t *ncells, float *alo,
                               float *ahi, int64_t *tlo, int64_t *thi, uint32_t *home, uint32_t *qid)
 {
     const int64_t i = tid64();
     if (i >= n) return;
-    const QRow r = rows[i];
-    int src = 0;
-    while (src + 1 < np && src_base[src + 1] <= i) src++;
+    const int src = src_of(t.a, np, i);
+    const QRow r = reinterpret_cast<const QRow *>(recv + t.b[src])[i - t.a[src]];
     ncells[i] = r.ncells;
     alo[i] = r.alo;
     ahi[i] = r.ahi;
@@ -147,6 +164,16 @@ __global__ void k_unpack_rows(int64_t n, const QRow *rows, int np, const int64_t
     thi[i] = r.thi;
     home[i] = (uint32_t)src;
     qid[i] = r.qid;
+}
+// Each source's cell lists (after its rows) into one contiguous array, in
+// source order -- the batch's CSR order.  t.b here: the byte offset of the
+// source's cells.
+__global__ void k_gather_cells(int64_t nc, const unsigned char *recv, int np, PartTable t, uint64_t *out)
+{
+    for (int64_t k = tid64(); k < nc; k += (int64_t)gridDim.x * blockDim.x) {
+        const int src = src_of(t.c, np, k);
+        out[k] = reinterpret_cast<const uint64_t *>(recv + t.b[src])[k - t.c[src]];
+    }
 }
 
 // Pairs (batch row, entity) -> part-major by the row's home part, packed
@@ -162,7 +189,8 @@ __global__ __launch_bounds__(kBlock) void k_route_pairs(int64_t n, const uint32_
                                                         const uint32_t *__restrict__ pe, const uint32_t *__restrict__ home,
                                                         const uint32_t *__restrict__ qid, int np,
                                                         unsigned long long *tot, const int64_t *base_d,
-                                                        unsigned long long *cursor, uint64_t *out)
+                                                        unsigned long long *cursor, uint64_t *out, int self_part,
+                                                        uint32_t *__restrict__ self_q, uint32_t *__restrict__ self_e)
 {
     __shared__ uint32_t s_cnt[DSSG_MAX_PARTS];
     __shared__ unsigned long long s_base[DSSG_MAX_PARTS];
@@ -193,14 +221,25 @@ __global__ __launch_bounds__(kBlock) void k_route_pairs(int64_t n, const uint32_
     for (int j = 0; j < kPairItems; j++) {
         if (dst[j] < 0) continue;
         const int64_t i = t0 + (int64_t)j * kBlock + threadIdx.x;
-        out[base_d[dst[j]] + (int64_t)(s_base[dst[j]] + rank[j])] = ((uint64_t)qid[pq[i]] << 32) | pe[i];
+        const int64_t w = (int64_t)(s_base[dst[j]] + rank[j]);
+        if (dst[j] == self_part) {  // this rank's own queries: final (q, e) at once, no exchange
+            self_q[w] = qid[pq[i]];
+            self_e[w] = pe[i];
+        } else {
+            out[base_d[dst[j]] + w] = ((uint64_t)qid[pq[i]] << 32) | pe[i];
+        }
     }
 }
 
 }  // namespace
 
+int64_t route_segment_bytes(int64_t rows, int64_t cells)
+{
+    return rows * (int64_t)sizeof(QRow) + ((cells * 8 + 31) / 32) * 32;
+}
+
 void RouteEngine::plan(int64_t nq, const int64_t *offs, const uint64_t *cells, int np, const uint64_t *part_hi,
-                       hipStream_t s, int64_t *row_counts, int64_t *cell_counts)
+                       hipStream_t s, int64_t *row_counts, int64_t *cell_counts, int64_t *seg_bytes)
 {
     if (np < 1 || np > kMaxParts) throw Error(DSSG_ERR_INVALID, "route: nparts must be in [1, 64]");
     if (nq >= (1ll << 24)) throw Error(DSSG_ERR_INVALID, "route: more than 2^24 queries per batch");
@@ -211,23 +250,26 @@ void RouteEngine::plan(int64_t nq, const int64_t *offs, const uint64_t *cells, i
         hipLaunchKernelGGL(k_route<0>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, offs, cells, nullptr, nullptr,
                            nullptr, nullptr, np, part_hi, mask, acc, acc + kMaxParts, nullptr, nullptr, nullptr, nullptr,
                            nullptr);
-    unsigned long long h[2 * kMaxParts];
-    DSS_HIP(hipMemcpyAsync(h, acc, sizeof(h), hipMemcpyDeviceToHost, s));
+    unsigned long long *h = host_words();
+    DSS_HIP(hipMemcpyAsync(h, acc, sizeof(unsigned long long) * 2 * kMaxParts, hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
-    int64_t rb[kMaxParts], cb[kMaxParts], R = 0, Cn = 0;
+    // fused layout: part d's segment = its rows, then its cell lists, padded
+    // to 32 bytes; the fill kernel's bases are the segment's row and cell
+    // positions in QRow / uint64 units of the one send buffer
+    int64_t *hb = reinterpret_cast<int64_t *>(host_words() + 2 * kMaxParts);
+    int64_t off = 0, Cn = 0;
     for (int d = 0; d < np; d++) {
-        rb[d] = R;
-        cb[d] = Cn;
         row_counts[d] = (int64_t)h[d];
         cell_counts[d] = (int64_t)h[kMaxParts + d];
-        R += row_counts[d];
+        seg_bytes[d] = route_segment_bytes(row_counts[d], cell_counts[d]);
+        hb[d] = off / (int64_t)sizeof(QRow);
+        hb[kMaxParts + d] = (off + row_counts[d] * (int64_t)sizeof(QRow)) / 8;
+        off += seg_bytes[d];
         Cn += cell_counts[d];
     }
     if (Cn >= (int64_t)kCellMask) throw Error(DSSG_ERR_INVALID, "route: more than 2^40 routed cells");
     int64_t *bases = base_.ensure(2 * kMaxParts);
-    DSS_HIP(hipMemcpyAsync(bases, rb, sizeof(int64_t) * np, hipMemcpyHostToDevice, s));
-    DSS_HIP(hipMemcpyAsync(bases + kMaxParts, cb, sizeof(int64_t) * np, hipMemcpyHostToDevice, s));
-    DSS_HIP(hipStreamSynchronize(s));  // rb/cb are stack arrays
+    DSS_HIP(hipMemcpyAsync(bases, hb, sizeof(int64_t) * 2 * kMaxParts, hipMemcpyHostToDevice, s));
     plan_nq_ = nq;
     plan_np_ = np;
     plan_offs_ = offs;
@@ -236,7 +278,7 @@ void RouteEngine::plan(int64_t nq, const int64_t *offs, const uint64_t *cells, i
 }
 
 void RouteEngine::fill(int64_t nq, const int64_t *offs, const uint64_t *cells, const float *alo, const float *ahi,
-                       const int64_t *tlo, const int64_t *thi, hipStream_t s, void *rows, uint64_t *out_cells)
+                       const int64_t *tlo, const int64_t *thi, hipStream_t s, void *send)
 {
     if (plan_np_ == 0 || nq != plan_nq_ || offs != plan_offs_ || cells != plan_cells_)
         throw Error(DSSG_ERR_INVALID, "route fill: no matching dssg_route_plan_device on this context");
@@ -244,31 +286,40 @@ void RouteEngine::fill(int64_t nq, const int64_t *offs, const uint64_t *cells, c
     if (nq > 0)
         hipLaunchKernelGGL(k_route<1>, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, offs, cells, alo, ahi, tlo, thi,
                            plan_np_, plan_part_hi_, mask_.p, nullptr, nullptr, base_.p, base_.p + kMaxParts,
-                           acc + 2 * kMaxParts, (QRow *)rows, out_cells);
+                           acc + 2 * kMaxParts, (QRow *)send, (uint64_t *)send);
     plan_np_ = 0;  // one fill per plan (the cursors are spent)
 }
 
-void RouteEngine::unpack(int64_t nrows, const void *rows, const uint64_t *cells, int np, const int64_t *src_rows,
-                         hipStream_t s, dssg_batch *out)
+void RouteEngine::unpack(const void *recv, int np, const int64_t *src_rows, const int64_t *src_cells, hipStream_t s,
+                         dssg_batch *out)
 {
     if (np < 1 || np > kMaxParts) throw Error(DSSG_ERR_INVALID, "unpack: nparts must be in [1, 64]");
-    int64_t sb[kMaxParts], acc = 0;
+    PartTable rt{}, ct{};
+    int64_t nrows = 0, ncells = 0, off = 0;
     for (int d = 0; d < np; d++) {
-        sb[d] = acc;
-        acc += src_rows[d];
+        if (src_rows[d] < 0 || src_cells[d] < 0) throw Error(DSSG_ERR_INVALID, "unpack: negative counts");
+        rt.a[d] = nrows;
+        rt.b[d] = off;
+        ct.c[d] = ncells;
+        ct.b[d] = off + src_rows[d] * (int64_t)sizeof(QRow);
+        nrows += src_rows[d];
+        ncells += src_cells[d];
+        off += route_segment_bytes(src_rows[d], src_cells[d]);
     }
-    if (acc != nrows) throw Error(DSSG_ERR_INVALID, "unpack: per-source row counts do not sum to nrows");
-    int64_t *d_sb = sbase_.ensure(kMaxParts);
-    DSS_HIP(hipMemcpyAsync(d_sb, sb, sizeof(int64_t) * np, hipMemcpyHostToDevice, s));
-    DSS_HIP(hipStreamSynchronize(s));  // sb is a stack array
+    if ((nrows > 0 || ncells > 0) && !recv) throw Error(DSSG_ERR_INVALID, "unpack: NULL receive buffer");
     int64_t *nc = ncell_.ensure(nrows + 1);
     float *alo = alo_.ensure(nrows + 1), *ahi = ahi_.ensure(nrows + 1);
     int64_t *tlo = tlo_.ensure(nrows + 1), *thi = thi_.ensure(nrows + 1);
     uint32_t *home = home_.ensure(nrows + 1), *qid = qid_.ensure(nrows + 1);
     int64_t *offs = offs_.ensure(nrows + 2);
+    uint64_t *cells = cells_.ensure(ncells + 1);
+    const unsigned char *r = (const unsigned char *)recv;
     if (nrows > 0)
-        hipLaunchKernelGGL(k_unpack_rows, dim3(grid_for(nrows, kBlock)), dim3(kBlock), 0, s, nrows, (const QRow *)rows, np,
-                           d_sb, nc, alo, ahi, tlo, thi, home, qid);
+        hipLaunchKernelGGL(k_unpack_rows, dim3(grid_for(nrows, kBlock)), dim3(kBlock), 0, s, nrows, r, np, rt, nc, alo,
+                           ahi, tlo, thi, home, qid);
+    if (ncells > 0)
+        hipLaunchKernelGGL(k_gather_cells, dim3((unsigned)std::min<int64_t>(grid_for(ncells, kBlock), 8192)),
+                           dim3(kBlock), 0, s, ncells, r, np, ct, cells);
     exclusive_scan_i64(nc, offs, nrows, tmp_, s);
     out->n = nrows;
     out->offs = offs;
@@ -281,40 +332,64 @@ void RouteEngine::unpack(int64_t nrows, const void *rows, const uint64_t *cells,
     out->qid = qid;
 }
 
-void RouteEngine::pairs_plan(const dssg_batch *b, const dssg_pairs *p, int np, hipStream_t s, int64_t *counts)
+void RouteEngine::pairs_plan(const dssg_batch *b, const dssg_pairs *p, int np, int self_part, hipStream_t s,
+                             int64_t *counts)
 {
     if (np < 1 || np > kMaxParts) throw Error(DSSG_ERR_INVALID, "route_pairs: nparts must be in [1, 64]");
+    if (self_part < -1 || self_part >= np) throw Error(DSSG_ERR_INVALID, "route_pairs: self part out of range");
     unsigned long long *acc = pacc_.ensure(2 * kMaxParts);
     DSS_HIP(hipMemsetAsync(acc, 0, 2 * kMaxParts * sizeof(unsigned long long), s));
     const int64_t n = p->n;
     if (n > 0)
         hipLaunchKernelGGL(k_route_pairs<0>, dim3(grid_for(n, kPairTile)), dim3(kBlock), 0, s, n, p->q, p->e, b->home,
-                           b->qid, np, acc, nullptr, nullptr, nullptr);
-    unsigned long long h[kMaxParts];
-    DSS_HIP(hipMemcpyAsync(h, acc, sizeof(h), hipMemcpyDeviceToHost, s));
+                           b->qid, np, acc, nullptr, nullptr, nullptr, -1, nullptr, nullptr);
+    unsigned long long *h = host_words() + 4 * kMaxParts;
+    DSS_HIP(hipMemcpyAsync(h, acc, sizeof(unsigned long long) * kMaxParts, hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
-    int64_t pb[kMaxParts], tot = 0;
+    // send-buffer bases: part-major, the self part (written to its own
+    // output arrays instead) taking no space
+    int64_t *pb = reinterpret_cast<int64_t *>(host_words() + 5 * kMaxParts), tot = 0;
     for (int d = 0; d < np; d++) {
         pb[d] = tot;
         counts[d] = (int64_t)h[d];
-        tot += counts[d];
+        if (d != self_part) tot += counts[d];
     }
     int64_t *d_pb = pbase_.ensure(kMaxParts);
     DSS_HIP(hipMemcpyAsync(d_pb, pb, sizeof(int64_t) * np, hipMemcpyHostToDevice, s));
-    DSS_HIP(hipStreamSynchronize(s));
     pplan_n_ = n;
     pplan_np_ = np;
+    pplan_self_ = self_part;
+    pplan_self_n_ = self_part >= 0 ? counts[self_part] : 0;
     pplan_q_ = p->q;
 }
 
-void RouteEngine::pairs_fill(const dssg_batch *b, const dssg_pairs *p, hipStream_t s, uint64_t *out)
+void RouteEngine::pairs_fill(const dssg_batch *b, const dssg_pairs *p, hipStream_t s, uint64_t *out, uint32_t *self_q,
+                             uint32_t *self_e)
 {
     if (pplan_np_ == 0 || p->n != pplan_n_ || p->q != pplan_q_)
         throw Error(DSSG_ERR_INVALID, "route_pairs fill: no matching dssg_route_pairs_plan_device on this context");
+    if (pplan_self_n_ > 0 && (!self_q || !self_e)) throw Error(DSSG_ERR_INVALID, "route_pairs fill: NULL self output");
+    if (p->n > pplan_self_n_ && !out) throw Error(DSSG_ERR_INVALID, "route_pairs fill: NULL send buffer");
     if (p->n > 0)
         hipLaunchKernelGGL(k_route_pairs<1>, dim3(grid_for(p->n, kPairTile)), dim3(kBlock), 0, s, p->n, p->q, p->e,
-                           b->home, b->qid, pplan_np_, nullptr, pbase_.p, pacc_.p + kMaxParts, out);
+                           b->home, b->qid, pplan_np_, nullptr, pbase_.p, pacc_.p + kMaxParts, out, pplan_self_,
+                           self_q, self_e);
     pplan_np_ = 0;
+}
+
+// Pinned host words for the count round trips (no pageable staging copy):
+// [0, 2P) plan counts, [2P, 4P) plan bases, [4P, 5P) pair counts, [5P, 6P)
+// pair bases -- separate regions, so no host write races a pending copy.
+unsigned long long *RouteEngine::host_words()
+{
+    if (!h_counts_) DSS_HIP(hipHostMalloc((void **)&h_counts_, sizeof(unsigned long long) * 6 * kMaxParts,
+                                          hipHostMallocDefault));
+    return h_counts_;
+}
+
+RouteEngine::~RouteEngine()
+{
+    if (h_counts_) (void)hipHostFree(h_counts_);
 }
 
 namespace {

@@ -14,30 +14,46 @@ struct QRow {
 static_assert(sizeof(QRow) == 32, "QRow layout");
 static_assert(sizeof(QRow) == DSSG_ROUTE_ROW_BYTES, "QRow size vs dssgpu.h");
 
+// Bytes of one part's segment in the fused send buffer: its rows, then its
+// cell lists, padded to 32 bytes.
+int64_t route_segment_bytes(int64_t rows, int64_t cells);
+
 class RouteEngine {
    public:
     static constexpr int kMaxParts = DSSG_MAX_PARTS;
-    // pass 0: per-query destination masks, per-part row / cell counts (host)
+    RouteEngine() = default;
+    RouteEngine(const RouteEngine &) = delete;
+    RouteEngine &operator=(const RouteEngine &) = delete;
+    ~RouteEngine();
+    // pass 0: per-query destination masks, per-part row / cell counts and
+    // fused segment sizes (host)
     void plan(int64_t nq, const int64_t *offs, const uint64_t *cells, int np, const uint64_t *part_hi, hipStream_t s,
-              int64_t *row_counts, int64_t *cell_counts);
-    // pass 1: rows + cell lists into caller-owned part-major buffers
+              int64_t *row_counts, int64_t *cell_counts, int64_t *seg_bytes);
+    // pass 1: rows + cell lists into the caller-owned fused send buffer
     void fill(int64_t nq, const int64_t *offs, const uint64_t *cells, const float *alo, const float *ahi,
-              const int64_t *tlo, const int64_t *thi, hipStream_t s, void *rows, uint64_t *out_cells);
-    void unpack(int64_t nrows, const void *rows, const uint64_t *cells, int np, const int64_t *src_rows, hipStream_t s,
+              const int64_t *tlo, const int64_t *thi, hipStream_t s, void *send);
+    // received fused segments (src_rows / src_cells per source part) -> batch
+    void unpack(const void *recv, int np, const int64_t *src_rows, const int64_t *src_cells, hipStream_t s,
                 dssg_batch *out);
-    void pairs_plan(const dssg_batch *b, const dssg_pairs *p, int np, hipStream_t s, int64_t *counts);
-    void pairs_fill(const dssg_batch *b, const dssg_pairs *p, hipStream_t s, uint64_t *out);
+    // pair counts per home part; the send-buffer bases skip self_part (-1: none)
+    void pairs_plan(const dssg_batch *b, const dssg_pairs *p, int np, int self_part, hipStream_t s, int64_t *counts);
+    // other parts' pairs packed into `out`, the self part's to (self_q, self_e)
+    void pairs_fill(const dssg_batch *b, const dssg_pairs *p, hipStream_t s, uint64_t *out, uint32_t *self_q,
+                    uint32_t *self_e);
     // routed pairs (home-local qid << 32 | entity) -> (q, e) arrays
     static void split_pairs(int64_t n, const uint64_t *in, uint32_t *q, uint32_t *e, hipStream_t s);
 
    private:
+    unsigned long long *host_words();
     DevBuf<unsigned char> tmp_;
     DevBuf<unsigned long long> mask_, acc_, pacc_;
-    DevBuf<int64_t> base_, sbase_, pbase_, ncell_, tlo_, thi_, offs_;
+    DevBuf<int64_t> base_, pbase_, ncell_, tlo_, thi_, offs_;
+    DevBuf<uint64_t> cells_;
     DevBuf<float> alo_, ahi_;
     DevBuf<uint32_t> home_, qid_;
-    int64_t plan_nq_ = 0, pplan_n_ = 0;
-    int plan_np_ = 0, pplan_np_ = 0;
+    unsigned long long *h_counts_ = nullptr;  // pinned
+    int64_t plan_nq_ = 0, pplan_n_ = 0, pplan_self_n_ = 0;
+    int plan_np_ = 0, pplan_np_ = 0, pplan_self_ = -1;
     const int64_t *plan_offs_ = nullptr;
     const uint64_t *plan_cells_ = nullptr, *plan_part_hi_ = nullptr;
     const uint32_t *pplan_q_ = nullptr;

@@ -200,41 +200,48 @@ class ShardedSearch:
         return t0
 
     def step(self, offs_ptr, cells_ptr, nq, alo, ahi, tlo, thi, timed: bool = False):
+        """The routing protocol of dssgpu.h (the one dssg_sharded_search_device
+        runs), with torch.distributed doing the two all-to-alls: fused
+        [rows | cells] query segments out, pairs home.  Returns this rank's
+        pairs packed (query << 32 | entity) as one int64 tensor."""
         import time
         import torch
         from . import _lib
         D, ctx, L = self._D, self.ctx, self.ctx.L
-        W = self.world
+        W, me = self.world, self.rank
         st = D._stream_ptr()
         t = time.perf_counter()
         if timed:
             torch.cuda.synchronize()
             t = time.perf_counter()
-        # (1) route this rank's queries to the shards owning their cells
+        # (1) route this rank's queries to the shards owning their cells: one
+        # fused segment per shard
         rc = (C.c_int64 * _lib.MAX_PARTS)()
         cc = (C.c_int64 * _lib.MAX_PARTS)()
+        sb = (C.c_int64 * _lib.MAX_PARTS)()
         ctx.check(L.dssg_route_plan_device(ctx.h, nq, C.c_void_p(offs_ptr), C.c_void_p(cells_ptr), W,
-                                           D._ptr(self.part_hi), st, rc, cc))
-        rows_n, cells_n = [rc[d] for d in range(W)], [cc[d] for d in range(W)]
-        words = _lib.ROUTE_ROW_BYTES // 8
-        send_rows = torch.empty(sum(rows_n) * words + 1, dtype=torch.int64, device=self.dev)
-        send_cells = torch.empty(sum(cells_n) + 1, dtype=torch.int64, device=self.dev)
+                                           D._ptr(self.part_hi), st, rc, cc, sb))
+        seg_words = [sb[d] // 8 for d in range(W)]
+        send = torch.empty(sum(seg_words) + 4, dtype=torch.int64, device=self.dev)
         ctx.check(L.dssg_route_fill_device(ctx.h, nq, C.c_void_p(offs_ptr), C.c_void_p(cells_ptr), D._ptr(alo),
-                                           D._ptr(ahi), D._ptr(tlo), D._ptr(thi), st, D._ptr(send_rows),
-                                           D._ptr(send_cells)))
+                                           D._ptr(ahi), D._ptr(tlo), D._ptr(thi), st, D._ptr(send)))
+        # counts travel with a small all-gather (rows, cells per destination)
+        mine = torch.tensor([rc[d] for d in range(W)] + [cc[d] for d in range(W)], dtype=torch.int64,
+                            device="cpu" if self.stage_host else self.dev)
+        allc = [torch.zeros_like(mine) for _ in range(W)]
+        _dist().all_gather(allc, mine, group=self.group)
+        allc = [x.cpu() for x in allc]
+        src_rows = [int(allc[p][me]) for p in range(W)]
+        src_cells = [int(allc[p][W + me]) for p in range(W)]
         t = self._mark("route", t, timed)
-        # (2) exchange (all-to-all over xGMI)
-        recv_rows, src_words = all_to_all(send_rows[:-1], [r * words for r in rows_n], self.group, self.stage_host)
-        recv_cells, _ = all_to_all(send_cells[:-1], cells_n, self.group, self.stage_host)
+        # (2) one exchange of the fused segments (all-to-all over xGMI)
+        recv, _ = all_to_all(send[:sum(seg_words)], seg_words, self.group, self.stage_host)
         t = self._mark("exchange_queries", t, timed)
         # (3) unpack + join against this rank's shard
-        src_rows = (C.c_int64 * _lib.MAX_PARTS)(*[w // words for w in src_words])
-        nrows = sum(src_words) // words
         batch = _lib.Batch()
-        recv_rows = recv_rows if recv_rows.numel() else torch.empty(1, dtype=torch.int64, device=self.dev)
-        recv_cells = recv_cells if recv_cells.numel() else torch.empty(1, dtype=torch.int64, device=self.dev)
-        ctx.check(L.dssg_unpack_queries_device(ctx.h, nrows, D._ptr(recv_rows), C.c_void_p(recv_cells.data_ptr()), W,
-                                               src_rows, st, C.byref(batch)))
+        recv = recv if recv.numel() else torch.empty(4, dtype=torch.int64, device=self.dev)
+        ctx.check(L.dssg_unpack_queries_device(ctx.h, D._ptr(recv), W, (C.c_int64 * _lib.MAX_PARTS)(*src_rows),
+                                               (C.c_int64 * _lib.MAX_PARTS)(*src_cells), st, C.byref(batch)))
         pairs = _lib.Pairs()
         ctx.check(L.dssg_search_device(ctx.h, self.index, batch.n, C.c_void_p(batch.offs), C.c_void_p(batch.cells),
                                        C.c_void_p(batch.alt_lo), C.c_void_p(batch.alt_hi), C.c_void_p(batch.tlo),
@@ -246,17 +253,25 @@ class ShardedSearch:
                                                    C.c_void_p(batch.cells), st, C.byref(tch)))
             self.last_touched = int(tch.value)
             t = time.perf_counter()
-        # (4) pairs back to their queries' home ranks
+        # (4) pairs home: this rank's own straight to its output, the others'
+        # packed and all-to-all'd back
         pc = (C.c_int64 * _lib.MAX_PARTS)()
-        ctx.check(L.dssg_route_pairs_plan_device(ctx.h, C.byref(batch), C.byref(pairs), W, st, pc))
+        ctx.check(L.dssg_route_pairs_plan_device(ctx.h, C.byref(batch), C.byref(pairs), W, me, st, pc))
         pn = [pc[d] for d in range(W)]
-        send_pairs = torch.empty(sum(pn) + 1, dtype=torch.int64, device=self.dev)
-        ctx.check(L.dssg_route_pairs_fill_device(ctx.h, C.byref(batch), C.byref(pairs), st, D._ptr(send_pairs)))
+        send_pairs = torch.empty(sum(pn) - pn[me] + 1, dtype=torch.int64, device=self.dev)
+        self_q = torch.empty(pn[me] + 1, dtype=torch.int32, device=self.dev)
+        self_e = torch.empty(pn[me] + 1, dtype=torch.int32, device=self.dev)
+        ctx.check(L.dssg_route_pairs_fill_device(ctx.h, C.byref(batch), C.byref(pairs), st, D._ptr(send_pairs),
+                                                 D._ptr(self_q), D._ptr(self_e)))
         t = self._mark("route_pairs", t, timed)
-        out, _ = all_to_all(send_pairs[:-1], pn, self.group, self.stage_host)
+        got, _ = all_to_all(send_pairs[:-1], [0 if d == me else pn[d] for d in range(W)], self.group,
+                            self.stage_host)
+        own = (self_q[:pn[me]].to(torch.int64) << 32) | (self_e[:pn[me]].to(torch.int64) & 0xFFFFFFFF)
+        out = torch.cat([own, got])
         self._mark("exchange_pairs", t, timed)
-        self.last_rows = nrows
-        self.last_recv_cells = recv_cells[: int(batch.n and recv_cells.numel())] if nrows else recv_cells[:0]
+        self.last_rows = int(batch.n)
+        self.last_recv_cells = recv[:0]
+        self.last_recv_ncells = sum(src_cells)
         self.last_shard_pairs = int(pairs.n)
         return out
 

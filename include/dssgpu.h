@@ -293,20 +293,27 @@ int dssg_max_subscription_count(dssg_ctx *ctx, const dssg_index *idx, int64_t nq
  * fans `cell_id = ANY($cells)` (operations.go:384-390) out to the ranges.
  * Here, one process per GPU:
  *  1. dssg_route_plan_device + dssg_route_fill_device: the home rank's
- *     covered batch -> part-major send buffers (caller-owned device memory):
- *     per (query, part owning >= 1 of its cells) one DSSG_ROUTE_ROW_BYTES row
- *     {i64 tlo, i64 thi, f32 alo, f32 ahi, u32 qid, u32 ncells} and the
- *     query's whole cell list (a part's cell lists in the order of its rows).
- *     Part d owns cells c with part_hi[d-1] < c <= part_hi[d] (uint64 order,
- *     part_hi[nparts-1] = UINT64_MAX; d_part_hi is a device array).  The plan
- *     returns the per-part row and cell counts (host arrays of nparts).
- *  2. the caller all-to-alls rows and cells (RCCL over xGMI);
- *  3. dssg_unpack_queries_device: received rows (source-part-major, src_rows[s]
- *     rows from part s) -> a query batch for dssg_search_device against the
+ *     covered batch -> ONE send buffer (caller-owned device memory) of
+ *     part-major segments.  Part d's segment holds, per query with >= 1 cell
+ *     in part d, one DSSG_ROUTE_ROW_BYTES row {i64 tlo, i64 thi, f32 alo,
+ *     f32 ahi, u32 qid, u32 ncells}, then those queries' whole cell lists (in
+ *     the order of the rows), padded to 32 bytes: seg_bytes[d] =
+ *     32 * row_counts[d] + 32 * ceil(cell_counts[d] / 4).  Part d owns cells
+ *     c with part_hi[d-1] < c <= part_hi[d] (uint64 order, part_hi[nparts-1]
+ *     = UINT64_MAX; d_part_hi is a device array).  The plan returns the
+ *     per-part row and cell counts and segment sizes (host arrays of nparts).
+ *  2. the caller all-to-alls the segments (one exchange: RCCL over xGMI);
+ *  3. dssg_unpack_queries_device: the received segments (source-part-major,
+ *     src_rows[s] rows and src_cells[s] cells from part s, each segment laid
+ *     out as above) -> a query batch for dssg_search_device against the
  *     part's dssg_index_build_range index (context-owned until the next unpack);
  *  4. dssg_route_pairs_plan_device + dssg_route_pairs_fill_device: that
- *     search's pairs -> part-major by home part, packed
- *     (home-local qid << 32 | entity); the caller all-to-alls them back.
+ *     search's pairs by home part: the pairs of self_part's own queries go
+ *     straight to (d_self_q, d_self_e) as (home-local qid, entity) -- no
+ *     exchange, no unpacking -- the others part-major into d_send, packed
+ *     (home-local qid << 32 | entity), the self part taking no space there;
+ *     the caller all-to-alls them back and dssg_unpack_pairs_device splits
+ *     the received ones into (qid, entity) arrays.
  * A part sees a query's whole cell list and every entity's whole cell list, so
  * each (query, entity) pair is emitted by exactly one part (the one owning
  * their smallest shared cell; long x long pairs, met on every shard they
@@ -325,16 +332,18 @@ typedef struct {
 } dssg_batch;
 int dssg_route_plan_device(dssg_ctx *ctx, int64_t nq, const int64_t *d_q_offs, const uint64_t *d_q_cells,
                            int32_t nparts, const uint64_t *d_part_hi, void *stream, int64_t *row_counts,
-                           int64_t *cell_counts);
+                           int64_t *cell_counts, int64_t *seg_bytes);
 int dssg_route_fill_device(dssg_ctx *ctx, int64_t nq, const int64_t *d_q_offs, const uint64_t *d_q_cells,
                            const float *d_q_alt_lo, const float *d_q_alt_hi, const int64_t *d_q_tlo,
-                           const int64_t *d_q_thi, void *stream, void *d_rows_out, uint64_t *d_cells_out);
-int dssg_unpack_queries_device(dssg_ctx *ctx, int64_t nrows, const void *d_rows, const uint64_t *d_cells,
-                               int32_t nparts, const int64_t *src_rows, void *stream, dssg_batch *out);
+                           const int64_t *d_q_thi, void *stream, void *d_send);
+int dssg_unpack_queries_device(dssg_ctx *ctx, const void *d_recv, int32_t nparts, const int64_t *src_rows,
+                               const int64_t *src_cells, void *stream, dssg_batch *out);
 int dssg_route_pairs_plan_device(dssg_ctx *ctx, const dssg_batch *batch, const dssg_pairs *pairs, int32_t nparts,
-                                 void *stream, int64_t *counts);
+                                 int32_t self_part, void *stream, int64_t *counts);
 int dssg_route_pairs_fill_device(dssg_ctx *ctx, const dssg_batch *batch, const dssg_pairs *pairs, void *stream,
-                                 uint64_t *d_out);
+                                 uint64_t *d_send, uint32_t *d_self_q, uint32_t *d_self_e);
+int dssg_unpack_pairs_device(dssg_ctx *ctx, int64_t n, const uint64_t *d_in, uint32_t *d_q, uint32_t *d_e,
+                             void *stream);
 
 /* ---- native exchange over RCCL (xGMI) -----------------------------------
  * The sharded step without any framework: one process per GPU, one
@@ -343,18 +352,26 @@ int dssg_route_pairs_fill_device(dssg_ctx *ctx, const dssg_batch *batch, const d
  * each calls dssg_comm_init.  RCCL is opened on first use (dlopen, local
  * symbols); without it these calls return DSSG_ERR_DEVICE.
  * dssg_sharded_search_device runs steps 1-4 of the routing protocol above:
- * route the rank's covered batch, all-to-all the query rows and cell lists
- * (grouped ncclSend/ncclRecv; counts by ncclAllGather), join them against
- * this rank's dssg_index_build_range shard, route the pairs home and
- * all-to-all them back.  Output: this rank's pairs (query index in its own
- * batch, entity), each exactly once, in device memory owned by the
- * communicator until its next call.  Collective: every rank calls it. */
+ * route the rank's covered batch, all-to-all the fused query segments (one
+ * count allgather, one grouped ncclSend/ncclRecv exchange; the rank's own
+ * segment is copied locally), join them against this rank's
+ * dssg_index_build_range shard, write its own queries' pairs to the output
+ * and all-to-all the others' home (one more count allgather + exchange).
+ * With one rank the routing is the identity and the batch is joined as
+ * given (dssg_set_tuning "route_identity" = 0 forces the general path).
+ * Output: this rank's pairs (query index in its own batch, entity), each
+ * exactly once, in device memory owned by the communicator or the context
+ * until the next call on either.  Collective: every rank calls it; several
+ * communicators (one per pipeline thread, each with its own context and
+ * stream) may run concurrently, each issuing its calls in the same order on
+ * every rank. */
 #define DSSG_COMM_ID_BYTES 128
 typedef struct dssg_comm dssg_comm;
 int dssg_comm_unique_id(uint8_t *id);
 int dssg_comm_init(dssg_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t *id, dssg_comm **out);
 void dssg_comm_free(dssg_comm *comm);
-/* Byte blocks, part-major: send_bytes[d] to rank d, recv_bytes[s] from rank s. */
+/* Byte blocks, part-major: send_bytes[d] to rank d, recv_bytes[s] from rank s
+ * (the own block, send_bytes[rank] == recv_bytes[rank], is copied locally). */
 int dssg_comm_alltoallv_device(dssg_ctx *ctx, dssg_comm *comm, const void *d_send, const int64_t *send_bytes,
                                void *d_recv, const int64_t *recv_bytes, void *stream);
 int dssg_sharded_search_device(dssg_ctx *ctx, dssg_comm *comm, const dssg_index *shard, const uint64_t *d_part_hi,

@@ -54,37 +54,37 @@ def test_routed_shards_equal_full_search(cfg, scale, nparts):
     nq = len(cq.offs) - 1
     rc = (C.c_int64 * _lib.MAX_PARTS)()
     cc = (C.c_int64 * _lib.MAX_PARTS)()
-    ctx.check(L.dssg_route_plan_device(ctx.h, nq, D._ptr(offs), D._ptr(cells), nparts, D._ptr(part_hi), st, rc, cc))
-    rows_n, cells_n = [rc[d] for d in range(nparts)], [cc[d] for d in range(nparts)]
+    sb = (C.c_int64 * _lib.MAX_PARTS)()
+    ctx.check(L.dssg_route_plan_device(ctx.h, nq, D._ptr(offs), D._ptr(cells), nparts, D._ptr(part_hi), st, rc, cc,
+                                       sb))
+    rows_n, cells_n, seg = [rc[d] for d in range(nparts)], [cc[d] for d in range(nparts)], [sb[d] for d in range(nparts)]
     # every query goes to exactly the parts owning one of its cells
     want_rows = [0] * nparts
     for q in range(nq):
         for d in {shard.owner_of(ranges, int(c)) for c in cq.cells[cq.offs[q]:cq.offs[q + 1]]}:
             want_rows[d] += 1
     assert rows_n == want_rows
-    send_rows = torch.empty(sum(rows_n) * 4 + 1, dtype=torch.int64, device=dev)
-    send_cells = torch.empty(sum(cells_n) + 1, dtype=torch.int64, device=dev)
+    assert seg == [32 * r + 32 * ((c + 3) // 4) for r, c in zip(rows_n, cells_n)]  # the fused layout of dssgpu.h
+    send = torch.empty(sum(seg) // 8 + 4, dtype=torch.int64, device=dev)
     ctx.check(L.dssg_route_fill_device(ctx.h, nq, D._ptr(offs), D._ptr(cells), D._ptr(alo), D._ptr(ahi), D._ptr(dtlo),
-                                       D._ptr(dthi), st, D._ptr(send_rows), D._ptr(send_cells)))
+                                       D._ptr(dthi), st, D._ptr(send)))
     got, per_part = [], []
-    r0 = c0 = 0
+    w0 = 0
     for d in range(nparts):
         idx = EntityIndex(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1, cell_range=ranges[d])
-        rows_d = send_rows[4 * r0: 4 * (r0 + rows_n[d])].clone()
-        cells_d = send_cells[c0: c0 + cells_n[d]].clone()
-        r0 += rows_n[d]
-        c0 += cells_n[d]
-        if rows_d.numel() == 0:
+        seg_d = send[w0: w0 + seg[d] // 8].clone()  # part d's segment, as the exchange delivers it
+        w0 += seg[d] // 8
+        if rows_n[d] == 0:
             per_part.append(0)
             continue
-        src = (C.c_int64 * _lib.MAX_PARTS)(rows_n[d])
         batch = _lib.Batch()
-        ctx.check(L.dssg_unpack_queries_device(ctx.h, rows_n[d], D._ptr(rows_d), D._ptr(cells_d), 1, src, st,
-                                               C.byref(batch)))
+        ctx.check(L.dssg_unpack_queries_device(ctx.h, D._ptr(seg_d), 1, (C.c_int64 * _lib.MAX_PARTS)(rows_n[d]),
+                                               (C.c_int64 * _lib.MAX_PARTS)(cells_n[d]), st, C.byref(batch)))
         # the received rows carry the home batch's cell lists and attributes
         ro = D.copy_back(ctx, batch.offs, rows_n[d] + 1, np.int64)
         rq = D.copy_back(ctx, batch.qid, rows_n[d], np.uint32)
-        rcl = cells_d.cpu().numpy().view(np.uint64)
+        rcl = D.copy_back(ctx, batch.cells, int(ro[-1]), np.uint64)
+        assert int(ro[-1]) == cells_n[d]
         for k in range(0, rows_n[d], max(1, rows_n[d] // 50)):
             q = int(rq[k])
             assert np.array_equal(rcl[ro[k]:ro[k + 1]], cq.cells[cq.offs[q]:cq.offs[q + 1]])
@@ -92,13 +92,28 @@ def test_routed_shards_equal_full_search(cfg, scale, nparts):
         ctx.check(L.dssg_search_device(ctx.h, idx.h, batch.n, C.c_void_p(batch.offs), C.c_void_p(batch.cells),
                                        C.c_void_p(batch.alt_lo), C.c_void_p(batch.alt_hi), C.c_void_p(batch.tlo),
                                        C.c_void_p(batch.thi), C.c_void_p(0), st, C.byref(pairs)))
+        # pairs home, both ways: home part 0 as this rank's own (straight to
+        # the output arrays) and as another rank's (packed for the exchange)
         pc = (C.c_int64 * _lib.MAX_PARTS)()
-        ctx.check(L.dssg_route_pairs_plan_device(ctx.h, C.byref(batch), C.byref(pairs), 1, st, pc))
-        assert pc[0] == pairs.n
+        ctx.check(L.dssg_route_pairs_plan_device(ctx.h, C.byref(batch), C.byref(pairs), 2, 0, st, pc))
+        assert pc[0] == pairs.n and pc[1] == 0
+        sq = torch.empty(pairs.n + 1, dtype=torch.int32, device=dev)
+        se = torch.empty(pairs.n + 1, dtype=torch.int32, device=dev)
+        ctx.check(L.dssg_route_pairs_fill_device(ctx.h, C.byref(batch), C.byref(pairs), st, C.c_void_p(0), D._ptr(sq),
+                                                 D._ptr(se)))
+        own = _keys(sq[: pairs.n].cpu().numpy().view(np.uint32), se[: pairs.n].cpu().numpy().view(np.uint32))
+        ctx.check(L.dssg_route_pairs_plan_device(ctx.h, C.byref(batch), C.byref(pairs), 2, 1, st, pc))
         outp = torch.empty(pairs.n + 1, dtype=torch.int64, device=dev)
-        ctx.check(L.dssg_route_pairs_fill_device(ctx.h, C.byref(batch), C.byref(pairs), st, D._ptr(outp)))
+        ctx.check(L.dssg_route_pairs_fill_device(ctx.h, C.byref(batch), C.byref(pairs), st, D._ptr(outp),
+                                                 C.c_void_p(0), C.c_void_p(0)))
+        uq = torch.empty(pairs.n + 1, dtype=torch.int32, device=dev)
+        ue = torch.empty(pairs.n + 1, dtype=torch.int32, device=dev)
+        ctx.check(L.dssg_unpack_pairs_device(ctx.h, pairs.n, D._ptr(outp), D._ptr(uq), D._ptr(ue), st))
         torch.cuda.synchronize()
-        pk = outp[: pairs.n].cpu().numpy().view(np.uint64)
+        pk = np.sort(outp[: pairs.n].cpu().numpy().view(np.uint64))
+        assert np.array_equal(pk, own)
+        assert np.array_equal(_keys(uq[: pairs.n].cpu().numpy().view(np.uint32),
+                                    ue[: pairs.n].cpu().numpy().view(np.uint32)), own)
         got.append(pk)
         per_part.append(len(pk))
         idx.free()
@@ -201,10 +216,18 @@ def test_native_rccl_one_rank_equals_full_search():
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")  # noqa: E731
     offs, cells = t(cq.offs), t(cq.cells.view(np.int64))
     ns = shard.NativeShardedSearch(ctx, comm, idx.h, ranges)
-    for _ in range(2):  # a second step reuses the communicator's buffers
-        p = ns.step(offs.data_ptr(), cells.data_ptr(), len(cq.offs) - 1, t(qa.alt_lo), t(qa.alt_hi), t(tlo), t(thi))
-        gq = D.copy_back(ctx, p.q, int(p.n), np.uint32)
-        ge = D.copy_back(ctx, p.e, int(p.n), np.uint32)
-        assert np.array_equal(_keys(gq, ge), _keys(fq, fe))
+    try:
+        # identity routing (one part), then the general path forced: route,
+        # own segment copied, unpack, join, own pairs straight to the output
+        for identity in (1, 0):
+            ctx.set_tuning("route_identity", identity)
+            for _ in range(2):  # a second step reuses the communicator's buffers
+                p = ns.step(offs.data_ptr(), cells.data_ptr(), len(cq.offs) - 1, t(qa.alt_lo), t(qa.alt_hi), t(tlo),
+                            t(thi))
+                gq = D.copy_back(ctx, p.q, int(p.n), np.uint32)
+                ge = D.copy_back(ctx, p.e, int(p.n), np.uint32)
+                assert np.array_equal(_keys(gq, ge), _keys(fq, fe))
+    finally:
+        ctx.set_tuning("route_identity", 1)
     comm.close()
     idx.free()

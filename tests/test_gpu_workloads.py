@@ -17,7 +17,8 @@ def _keys(q, e):
 # (2, 0.1): 1M California intents and 100k queries -- hotspot cells with
 # hundreds of postings and records, and a few long footprints, so both join
 # queues (short and long variants) run in one search
-@pytest.mark.parametrize("cfg,scale", [(2, 0.002), (3, 0.004), (4, 0.0004), (2, 0.1), (3, 0.1), (4, 0.01)])
+@pytest.mark.parametrize("cfg,scale", [(1, 0.02), (2, 0.002), (3, 0.004), (4, 0.0004), (2, 0.1), (3, 0.1),
+                                       (4, 0.01)])
 def test_config_parity(oracle, cfg, scale, join_path):
     from dss_amd import geo, workload as W
     from dss_amd.store import EntityIndex

@@ -1,11 +1,16 @@
-"""Cell-range sharding protocol (dss_amd/shard.py) on CPU with gloo, world 2.
+"""Cell-range sharding protocol on CPU with gloo, world 2.
 
-What runs here is the host side of SURVEY.md s8(e): splitters, the
-all-gather of a covered query batch, the pair gather, and the invariant the
-whole design rests on -- with whole cell lists, the smallest-shared-cell rule
-puts every (query, entity) pair on exactly one shard.  The shard-local join
-is the device kernel in production (tests/test_gpu_shard.py checks it on a
-GPU); here the oracle plays it, as the checker.
+What runs here is the protocol the product ships (include/dssgpu.h, routing
+section; dssg_sharded_search_device): each rank routes its covered queries
+into fused [rows | cells] segments, one all-to-all delivers them, the shard
+unpacks and joins them, its own queries' pairs stay home and the others' go
+back in a second all-to-all.  The device kernels are restated in numpy by
+oracle/route_oracle.py and the shard join is the oracle's search filtered to
+the pairs whose smallest shared cell lies in the rank's range -- the checker
+standing in for route.hip and k_join (tests/test_gpu_shard.py runs the real
+kernels against it).  Plus the invariant the design rests on: with whole cell
+lists, the smallest-shared-cell rule puts every (query, entity) pair on
+exactly one shard.
 """
 import os
 import socket
@@ -57,37 +62,56 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from oracle import oracle as O
+        from oracle import oracle as O, route_oracle as R
         O.build()
-        _, qs, qa, it, ia, now = W.config(0, scale=0.004)
+        _, qs, qa, it, ia, now = W.config(0, scale=0.03)
         ioffs, icells, _, _ = O.cover_batch(it.kind, it.voff, it.lat, it.lng, it.radius_m, nthreads=2)
         ranges = shard.cell_splitters(icells, world)
+        part_hi = shard.part_his(ranges)
+        tlo_all, thi_all = W.query_bounds(qa, now)
         # this rank covers its contiguous slice of the query batch
         n = qs.n
         lo, hi = rank * n // world, (rank + 1) * n // world
         sub = qs.subset(np.arange(lo, hi))
         qo, qcells, _, _ = O.cover_batch(sub.kind, sub.voff, sub.lat, sub.lng, sub.radius_m, nthreads=2)
-        tlo, thi = W.query_bounds(qa, now)
-        t = lambda a: torch.as_tensor(np.ascontiguousarray(a))  # noqa: E731
-        offs, cells, attrs, base = shard.allgather_csr(t(qo), t(qcells.view(np.int64)), t(qa.alt_lo[lo:hi]),
-                                                       t(qa.alt_hi[lo:hi]), t(tlo[lo:hi]), t(thi[lo:hi]))
-        assert base == [r * n // world for r in range(world)]
-        fo, fc, _, _ = O.cover_batch(qs.kind, qs.voff, qs.lat, qs.lng, qs.radius_m, nthreads=2)
-        assert np.array_equal(offs.numpy(), fo) and np.array_equal(cells.numpy().view(np.uint64), fc)
-        assert np.array_equal(attrs[2].numpy(), tlo) and np.array_equal(attrs[1].numpy(), qa.alt_hi)
-        # shard-local join (oracle as the stand-in for the device kernel):
-        # the pairs whose smallest shared cell lies in this rank's range
-        rq, re = O.search(ioffs, icells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1, None, fo, fc, qa.alt_lo, qa.alt_hi,
-                          tlo, thi)
-        keep = []
-        for k in range(len(rq)):
-            c = _smallest_shared(fc[fo[rq[k]]:fo[rq[k] + 1]], icells[ioffs[re[k]]:ioffs[re[k] + 1]])
-            keep.append(shard.owner_of(ranges, c) == rank)
-        keep = np.array(keep, dtype=bool)
-        gq, ge = shard.gather_pairs(t(rq[keep].astype(np.int64)), t(re[keep].astype(np.int64)))
-        got = np.sort((gq.numpy() << 32) | ge.numpy())
-        want = np.sort((rq.astype(np.int64) << 32) | re.astype(np.int64))
-        q.put((rank, bool(np.array_equal(got, want)), int(len(got)), int(keep.sum())))
+        alo, ahi, tlo, thi = qa.alt_lo[lo:hi], qa.alt_hi[lo:hi], tlo_all[lo:hi], thi_all[lo:hi]
+        # (1) route: fused segments + counts
+        send, rows_n, cells_n, seg = R.route(qo, qcells, alo, ahi, tlo, thi, part_hi)
+        assert seg == [32 * r + 32 * ((c + 3) // 4) for r, c in zip(rows_n, cells_n)]
+        mine = torch.tensor(rows_n + cells_n, dtype=torch.int64)
+        allc = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allc, mine)
+        src_rows = [int(allc[p][rank]) for p in range(world)]
+        src_cells = [int(allc[p][world + rank]) for p in range(world)]
+        # (2) one all-to-all of the segments
+        rseg = [R.segment_bytes(r, c) for r, c in zip(src_rows, src_cells)]
+        recv = torch.empty(sum(rseg), dtype=torch.uint8)
+        dist.all_to_all_single(recv, torch.from_numpy(send), rseg, seg)
+        # (3) unpack + shard join (oracle as the stand-in for k_join): the
+        # pairs whose smallest shared cell lies in this rank's range
+        b = R.unpack(recv.numpy(), src_rows, src_cells)
+        assert len(b["qid"]) == sum(src_rows) and b["offs"][-1] == sum(src_cells)
+        rq, re = O.search(ioffs, icells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1, None, b["offs"], b["cells"], b["alo"],
+                          b["ahi"], b["tlo"], b["thi"])
+        keep = np.array([shard.owner_of(ranges, _smallest_shared(b["cells"][b["offs"][rq[k]]:b["offs"][rq[k] + 1]],
+                                                                icells[ioffs[re[k]]:ioffs[re[k] + 1]])) == rank
+                         for k in range(len(rq))], dtype=bool)
+        rq, re = rq[keep], re[keep]
+        # (4) pairs home: own ones kept, the others all-to-all'd back
+        oq, oe, packed, pcounts = R.route_pairs(b, rq, re, world, rank)
+        sc = [0 if d == rank else int(pcounts[d]) for d in range(world)]
+        pcs = torch.tensor([int(x) for x in pcounts], dtype=torch.int64)
+        allp = [torch.zeros_like(pcs) for _ in range(world)]
+        dist.all_gather(allp, pcs)
+        rc = [0 if p == rank else int(allp[p][rank]) for p in range(world)]
+        got_p = torch.empty(sum(rc), dtype=torch.int64)
+        dist.all_to_all_single(got_p, torch.from_numpy(packed.view(np.int64)), rc, sc)
+        gq, ge = R.unpack_pairs(got_p.numpy().view(np.uint64))
+        got = np.sort((np.concatenate([oq, gq]).astype(np.uint64) << np.uint64(32)) |
+                      np.concatenate([oe, ge]).astype(np.uint64))
+        fq, fe = O.search(ioffs, icells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1, None, qo, qcells, alo, ahi, tlo, thi)
+        want = np.sort((fq.astype(np.uint64) << np.uint64(32)) | fe.astype(np.uint64))
+        q.put((rank, bool(np.array_equal(got, want)), int(len(want)), int(len(rq)), int(len(oq)), sum(rows_n)))
     finally:
         dist.destroy_process_group()
 
@@ -104,6 +128,10 @@ def test_sharded_protocol_gloo_world2():
         p.join(timeout=300)
     res = sorted(q.get(timeout=5) for _ in range(world))
     assert all(p.exitcode == 0 for p in procs)
-    assert all(ok for _, ok, _, _ in res)
-    assert sum(k for _, _, _, k in res) == res[0][2]  # disjoint: every pair on exactly one rank
-    assert res[0][2] > 0
+    assert all(ok for _, ok, _, _, _, _ in res), res
+    # every pair computed on exactly one shard: the shards' pairs add up to
+    # the pairs delivered home
+    assert sum(r[3] for r in res) == sum(r[2] for r in res) > 0
+    # both paths carried pairs: some stayed home, some crossed
+    assert 0 < sum(r[4] for r in res) < sum(r[2] for r in res)
+    assert all(r[5] > 0 for r in res)
