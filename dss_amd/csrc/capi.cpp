@@ -40,6 +40,11 @@ struct dssg_ctx {
     bool route_identity = true;  // sharded step on one rank: the batch is its own (see dssg_sharded_search_device)
     double cover_ms = 0, join_ms = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // the most recent device covering's output (its buffers belong to the
+    // cover engine until the next covering): a search over exactly that CSR
+    // takes its cell count from here instead of reading q_offs[nq] back
+    const int64_t *cov_offs = nullptr;
+    int64_t cov_n = -1, cov_total = -1;
     // host-API staging
     dss::DevBuf<int32_t> d_kind, d_owner;
     dss::DevBuf<int64_t> d_voff, d_qoffs, d_tlo, d_thi;
@@ -310,7 +315,11 @@ int dssg_cover_batch_device(dssg_ctx *ctx, int64_t n, const int32_t *d_kind, con
             if (!ctx->ev0) { DSS_HIP(hipEventCreate(&ctx->ev0)); DSS_HIP(hipEventCreate(&ctx->ev1)); }
             DSS_HIP(hipEventRecord(ctx->ev0, s));
         }
+        ctx->cov_offs = nullptr;
         ctx->cover.run(n, d_kind, d_voff, d_lat, d_lng, d_radius_m, s, out);
+        ctx->cov_offs = out->offs;
+        ctx->cov_n = n;
+        ctx->cov_total = out->total_cells;
         if (ctx->timing) {
             DSS_HIP(hipEventRecord(ctx->ev1, s));
             DSS_HIP(hipEventSynchronize(ctx->ev1));
@@ -505,7 +514,9 @@ int dssg_search_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const i
             if (!ctx->ev0) { DSS_HIP(hipEventCreate(&ctx->ev0)); DSS_HIP(hipEventCreate(&ctx->ev1)); }
             DSS_HIP(hipEventRecord(ctx->ev0, s));
         }
-        ctx->search.search(idx, nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo, d_q_thi, d_q_owner, s, out);
+        const int64_t nqc = d_q_offs == ctx->cov_offs && nq == ctx->cov_n ? ctx->cov_total : -1;
+        ctx->search.search(idx, nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo, d_q_thi, d_q_owner, s, out,
+                           nqc);
         if (ctx->timing) {
             DSS_HIP(hipEventRecord(ctx->ev1, s));
             DSS_HIP(hipEventSynchronize(ctx->ev1));
@@ -1366,7 +1377,8 @@ struct dssg_batcher {
                     w.ctx->search.search_small(idx, n, cov.offs, cov.cells, dlo, dhi, dtl, dth, nullptr,
                                                cov.total_cells, s, &res);
                 else
-                    w.ctx->search.search(idx, n, cov.offs, cov.cells, dlo, dhi, dtl, dth, nullptr, s, &res);
+                    w.ctx->search.search(idx, n, cov.offs, cov.cells, dlo, dhi, dtl, dth, nullptr, s, &res,
+                                         cov.total_cells);
             }
             npairs = res.n;
             const auto t2 = std::chrono::steady_clock::now();

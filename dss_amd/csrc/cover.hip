@@ -51,7 +51,7 @@ enum : uint8_t { FL_SMALL = 1, FL_PLANAR = 2, FL_FAST = 4 };
 // Direct candidate path: single-face small loops whose start block is at
 // level >= kFastMinLevel (<= 4 * 4^(13 - L) level-13 candidates).
 constexpr int kFastMinLevel = 10;
-constexpr int kCandStageV = 1024;  // (u,v) vertices a k_cand_fp block stages in LDS (16 KiB)
+constexpr int kCandStageV = 2048;  // (u,v) vertices a k_cand_fp block stages in LDS (float2: 16 KiB)
 // node meta: level (bits 0-4), orientation (5-6), done (7), face (8-10)
 __device__ __forceinline__ uint32_t pack_meta(int level, int orient, int done, int face)
 {
@@ -185,9 +185,13 @@ __global__ void k_vowner(int64_t n, const int64_t *xoff, uint32_t *vown)
 }
 
 // One thread per vertex slot: S2 point of a polygon vertex
-// (PointFromLatLng(LatLngFromDegrees)) or of a RegularLoop vertex.
+// (PointFromLatLng(LatLngFromDegrees)) or of a RegularLoop vertex.  A polygon
+// vertex out of range (Q17: GeoPolygon.CalculateCovering's check precedes the
+// count check) marks its footprint bad[f] (zeroed before), so k_setup reads
+// one flag instead of re-walking the footprint's coordinates.
 __global__ void k_verts(int64_t nx, const uint32_t *vown, const int32_t *kind, const int64_t *voff,
-                        const double *lat, const double *lng, const int64_t *xoff, const CircleFrame *fr, V3 *xyz)
+                        const double *lat, const double *lng, const int64_t *xoff, const CircleFrame *fr, V3 *xyz,
+                        uint8_t *bad)
 {
     const int64_t x = tid64();
     if (x >= nx) return;
@@ -199,7 +203,9 @@ __global__ void k_verts(int64_t nx, const uint32_t *vown, const int32_t *kind, c
         xyz[x] = normalize(v3(F.c0.x * px + F.c1.x * py + F.c.x * pz, F.c0.y * px + F.c1.y * py + F.c.y * pz,
                               F.c0.z * px + F.c1.z * py + F.c.z * pz));
     } else {
-        xyz[x] = point_from_degrees(lat[voff[f] + i], lng[voff[f] + i]);
+        const double la = lat[voff[f] + i], ln = lng[voff[f] + i];
+        if (kind[f] == DSSG_KIND_POLYGON && (la > 90.0 || la < -90.0 || ln > 180.0 || ln < -180.0)) bad[f] = 1;
+        xyz[x] = point_from_degrees(la, ln);
     }
 }
 
@@ -354,7 +360,8 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
                                           uint8_t *flags, int32_t *nvx, double2 *uv, uint64_t *st_id, uint32_t *st_i,
                                           uint32_t *st_j, uint32_t *finfo, uint4 *fbox,
                                           const double *fwd, const double *rev, const uint8_t *fan_fail,
-                                          const uint8_t *not_inner, const uint8_t *omode, uint8_t *rev_out)
+                                          const uint8_t *not_inner, const uint8_t *omode, uint8_t *rev_out,
+                                          const uint8_t *bad_in)
 {
     bool fail = false;
     if constexpr (FAST) rev_out[f] = 0;  // (set before any bail: the exact instance reverses in place itself)
@@ -402,10 +409,12 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
     } else {
         nv = (int)(voff[f + 1] - v0);
         if (k == DSSG_KIND_POLYGON) {  // Q17: range check precedes the count check
-            // 4 vertices' loads in flight together; the verdict is the same
-            // whichever out-of-range vertex is seen first
+            // (FAST: flagged per vertex by k_verts) 4 vertices' loads in
+            // flight together; the verdict is the same whichever
+            // out-of-range vertex is seen first
             bool bad = false;
-            for (int i0 = 0; i0 < nv && !bad; i0 += 4) {
+            if constexpr (FAST) bad = bad_in[f] != 0;
+            for (int i0 = 0; !FAST && i0 < nv && !bad; i0 += 4) {
                 double la[4], ln[4];
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
@@ -571,7 +580,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAST ? DSS_S
                         uint8_t *mode, uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx, double2 *uv,
                         uint64_t *st_id, uint32_t *st_i, uint32_t *st_j, uint32_t *finfo,
                         uint4 *fbox, const double *fwd, const double *rev, const uint8_t *fan_fail,
-                        const uint8_t *not_inner, const uint8_t *omode, const uint32_t *perm, uint8_t *rev_out)
+                        const uint8_t *not_inner, const uint8_t *omode, const uint32_t *perm, uint8_t *rev_out,
+                        const uint8_t *bad_in)
 {
     int64_t f = tid64();
     if constexpr (FAST) {
@@ -581,12 +591,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAST ? DSS_S
         for (int64_t i = f; i < (int64_t)*slow_n; i += (int64_t)gridDim.x * blockDim.x)
             setup_one<false>(slow_list[i], nullptr, nullptr, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out,
                              mode, origin_in, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, nullptr,
-                             nullptr, nullptr, nullptr, nullptr, nullptr);
+                             nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
         return;
     }
     setup_one<true>(f, slow_list, slow_n, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out, mode, origin_in,
                     fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, fwd, rev, fan_fail, not_inner, omode,
-                    rev_out);
+                    rev_out, bad_in);
 }
 
 // Q4's in-place reversal, moved out of k_setup<true> (its serial walk of a
@@ -1097,6 +1107,64 @@ __device__ __forceinline__ int cand_edges_uv(uint32_t i, uint32_t j, const doubl
     return in ? 1 : planar ? ((origin_in != par) ? 1 : 0) : 2;
 }
 
+// cand_edges_uv over LDS-staged loops of <= 64 vertices, two passes: a float
+// prefilter over every edge (the vertices' (u,v) also staged as float2)
+// marks the edges that can touch the cell's padded rect (both end points
+// beyond one side of it, by more than 1e-6, cannot: float rounding of a
+// vertex or a bound is < 1e-7 for |u|, |v| < 2) and the edges that can
+// straddle the centre's row (both end points above, or below, vc by more
+// than 1e-6 cannot); then only the marked edges run the exact tests, in the
+// same double arithmetic -- the result is cand_edges_uv's.  NaN end points
+// fail every float comparison, so their edges stay marked.
+__device__ __forceinline__ int cand_edges_uv_f(uint32_t i, uint32_t j, const double2 *upg, bool rev,
+                                               const float2 *upf, int nv, bool planar, bool origin_in)
+{
+    // (the exact tests read the loop from global memory; rev: a loop k_setup
+    // reversed without moving it, read mirrored -- the float stage is in
+    // loop order already)
+    auto at = [&](int e) { return upg[rev ? nv - 1 - e : e]; };
+    const uint32_t size = 1u << (kMaxLevel - kCoverLevel);
+    const double ulo = st_to_uv((double)i / (double)kMaxSize), uhi = st_to_uv((double)(i + size) / (double)kMaxSize);
+    const double vlo = st_to_uv((double)j / (double)kMaxSize), vhi = st_to_uv((double)(j + size) / (double)kMaxSize);
+    const double pm = kFinePad;
+    const double half = 0.5 / (double)kMaxSize, sz = (double)size;
+    const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
+    constexpr float kSlack = 1e-6f;
+    const float rlu = (float)(ulo - pm) - kSlack, rhu = (float)(uhi + pm) + kSlack;
+    const float rlv = (float)(vlo - pm) - kSlack, rhv = (float)(vhi + pm) + kSlack;
+    const float vcl = (float)vc - kSlack, vch = (float)vc + kSlack;
+    unsigned long long near = 0, strad = 0;
+    float2 a = upf[0];
+    for (int e = 0; e < nv; e++) {
+        const float2 b = upf[e + 1 < nv ? e + 1 : 0];
+        const bool far = ((a.x < rlu) & (b.x < rlu)) | ((a.x > rhu) & (b.x > rhu)) | ((a.y < rlv) & (b.y < rlv)) |
+                         ((a.y > rhv) & (b.y > rhv));
+        const bool level = ((a.y > vch) & (b.y > vch)) | ((a.y < vcl) & (b.y < vcl));
+        near |= (unsigned long long)!far << e;
+        strad |= (unsigned long long)!level << e;
+        a = b;
+    }
+    while (near) {
+        const int e = __builtin_ctzll(near);
+        near &= near - 1;
+        const double2 x = at(e), y = at(e + 1 < nv ? e + 1 : 0);
+        if (edge_intersects_rect(x.x, x.y, y.x, y.y, ulo - pm, uhi + pm, vlo - pm, vhi + pm)) return 1;
+    }
+    if (!planar) return 2;
+    bool par = false;
+    while (strad) {
+        const int e = __builtin_ctzll(strad);
+        strad &= strad - 1;
+        const double2 x = at(e), y = at(e + 1 < nv ? e + 1 : 0);
+        if ((x.y > vc) != (y.y > vc)) {
+            const double d = y.y - x.y;
+            const double lhs = (uc - x.x) * d, rhs = (vc - x.y) * (y.x - x.x);
+            if (d > 0 ? lhs < rhs : lhs > rhs) par = !par;
+        }
+    }
+    return (origin_in != par) ? 1 : 0;
+}
+
 // One block per kFpPer consecutive footprints: wave 0 loads their bounds,
 // start cells and flags into LDS (one round trip for the block, none per
 // candidate), the block stages their (u,v) vertices, then its threads stride
@@ -1115,7 +1183,7 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
     __shared__ int s_cb[kFpPer + 1], s_vb[kFpPer], s_nv[kFpPer], s_fl[kFpPer], s_vp[kFpPer + 1];
     __shared__ int64_t s_xo[kFpPer];
     __shared__ unsigned long long s_km[kFpPer][4], s_um[kFpPer][4];
-    __shared__ double2 s_uv[kCandStageV];
+    __shared__ float2 s_uvf[kCandStageV];  // the block's (u,v) vertices in float (cand_edges_uv_f's prefilter)
     const int t = threadIdx.x, lane = t & 63;
     const int64_t F0 = (int64_t)blockIdx.x * kFpPer;
     if (t < kFpPer) {
@@ -1168,7 +1236,8 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
             else hi = mid;
         }
         const int i = k - s_vp[lo];
-        s_uv[k] = uv[s_xo[lo] + ((s_fl[lo] & 4) ? s_nv[lo] - 1 - i : i)];  // a reversed loop staged in its order
+        const double2 w = uv[s_xo[lo] + ((s_fl[lo] & 4) ? s_nv[lo] - 1 - i : i)];  // a reversed loop staged in its order
+        s_uvf[k] = make_float2((float)w.x, (float)w.y);
     }
     __syncthreads();
     const int total = s_cb[kFpPer];
@@ -1188,9 +1257,13 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
         const int vb = s_vb[lo], fl = s_fl[lo];
         // (staged vertices are in loop order already; unstaged ones are read
         // through the reversal)
-        const double2 *up = vb >= 0 ? s_uv + vb : uv + s_xo[lo];
-        const int v = cand_edges_uv(i13 << (kMaxLevel - kCoverLevel), j13 << (kMaxLevel - kCoverLevel), up, s_nv[lo],
-                                    (fl & 1) != 0, (fl & 2) != 0, vb < 0 && (fl & 4) != 0);
+        const double2 *up = uv + s_xo[lo];
+        const int nvf = s_nv[lo];
+        const int v = vb >= 0 && nvf <= 64
+                          ? cand_edges_uv_f(i13 << (kMaxLevel - kCoverLevel), j13 << (kMaxLevel - kCoverLevel), up,
+                                            (fl & 4) != 0, s_uvf + vb, nvf, (fl & 1) != 0, (fl & 2) != 0)
+                          : cand_edges_uv(i13 << (kMaxLevel - kCoverLevel), j13 << (kMaxLevel - kCoverLevel), up, nvf,
+                                          (fl & 1) != 0, (fl & 2) != 0, (fl & 4) != 0);
         if (v == 1) atomicOr(&s_km[lo][key >> 6], 1ull << (key & 63));
         else if (v == 2) atomicOr(&s_um[lo][key >> 6], 1ull << (key & 63));
     }
@@ -1867,12 +1940,15 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     DSS_HIP(hipMemsetAsync(slow_n, 0, sizeof(unsigned int), s));
     DSS_HIP(hipMemsetAsync(fan_fail, 0, n, s));
     DSS_HIP(hipMemsetAsync(not_inner, 0, n, s));
+    uint8_t *bad = badv_.ensure(n + 1);
+    DSS_HIP(hipMemsetAsync(bad, 0, n, s));
     partition_polygons_first(kind, perm, fcnt_.ensure(n + 2), n, tmp_, tmp2_, s);
     // per-vertex pre-pass: frames, owners, S2 points, fan terms
     hipLaunchKernelGGL(k_circle_frames, dim3(grid_for(n, B)), dim3(B), 0, s, n, kind, voff, lat, lng, radius_m, frames);
     hipLaunchKernelGGL(k_vowner, dim3(grid_for(n, B)), dim3(B), 0, s, n, xoff, vown);
     if (nx > 0) {
-        hipLaunchKernelGGL(k_verts, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, kind, voff, lat, lng, xoff, frames, xyz);
+        hipLaunchKernelGGL(k_verts, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, kind, voff, lat, lng, xoff, frames, xyz,
+                           bad);
         hipLaunchKernelGGL(k_fan, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, nv, xoff, xyz, uv, not_inner);
     }
     // fan triangle terms of Loop.Area: orientation first, then one thread per
@@ -1886,10 +1962,10 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     uint8_t *rev_flag = revf_.ensure(n + 1);
     hipLaunchKernelGGL(k_setup<true>, dim3(grid_for(n, 64)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng,
                        radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo,
-                       fbox, fwd, rev, fan_fail, not_inner, omode, perm, rev_flag);
+                       fbox, fwd, rev, fan_fail, not_inner, omode, perm, rev_flag, bad);
     hipLaunchKernelGGL(k_setup<false>, dim3(min(grid_for(n, 64), 512u)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat,
                        lng, radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j,
-                       finfo, fbox, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                       finfo, fbox, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
     int64_t *eoff = eoff_.ensure(n + 1);
     uint32_t *dlist = dlist_.ensure(n + 1);
     unsigned int *dlist_n = dlist_n_.ensure(1);

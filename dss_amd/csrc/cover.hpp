@@ -69,7 +69,7 @@ class CoverEngine {
     DevBuf<uint8_t> mode_, orig_, fmask_, flags_, cflags_, act_;
     DevBuf<uint32_t> slow_, vown_, eown_, dlist_, xlist_;
     DevBuf<unsigned int> dlist_n_, xlist_n_;
-    DevBuf<uint8_t> fanf_, ninner_;
+    DevBuf<uint8_t> fanf_, ninner_, badv_;
     DevBuf<uint32_t> perm_, towner_;
     DevBuf<uint8_t> omode_, revf_;
     DevBuf<int64_t> tcnt_, toff_;

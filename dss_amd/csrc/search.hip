@@ -89,16 +89,19 @@ struct Regions {
     }
 };
 
-#ifndef DSS_JOIN_BPC
-#define DSS_JOIN_BPC 6
-#endif
-constexpr int kJoinBlocksPerCU = DSS_JOIN_BPC;  // persistent workgroups per CU
-constexpr int kWaves = 4;                       // waves per join workgroup
+// k_join occupancy and its LDS pair stage, two shapes: sparse-output joins
+// (configs[2]: ~6 pairs per staged record) run 7 workgroups per CU with a
+// 640-pair stage per wave (k_join 3.45 -> 3.24 ms against 6 x 1024);
+// dense-output joins (configs[3], RID 30-s windows: ~29 pairs per record,
+// pass density 0.45) keep 6 x 1024 (0.55 against 0.61 ms).  The search
+// picks the shape from the previous batch's pass density (dense_out_).
+constexpr int kWaves = 4;  // waves per join workgroup
+constexpr int kJoinBpcSparse = 7, kJoinBpcDense = 6;
+constexpr int kStageSparse = 640, kStageDense = 1024;
 #ifndef DSS_EMIT_DENSITY
 #define DSS_EMIT_DENSITY 4
 #endif
 constexpr int kEmitDensity = DSS_EMIT_DENSITY;
-constexpr int kOutStage = 1024;  // pairs per wave staged in LDS (16-bit codes) before the stores
 // ---- level-13 decode + prefix signatures -----------------------------------
 __device__ __forceinline__ int s2pos_to_ij(int o, int pos) { return (int)((0x874B78B4u >> (8 * o + 2 * pos)) & 3u); }
 __device__ __forceinline__ int s2pos_to_orientation(int pos) { return (int)((0xC1u >> (2 * pos)) & 3u); }
@@ -1174,8 +1177,8 @@ struct JoinArgs {
 // the fused altitude/time/owner predicate is one wave mask; the
 // smallest-shared-cell rule (SQL DISTINCT, Q13) compares the record's
 // near-prefix signature (broadcast) with each lane's posting signature.
-template <bool OWNER, bool LONG>
-__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LONG ? 1 : kJoinBlocksPerCU))) void k_join(JoinArgs a, const QRec *__restrict__ recs,
+template <bool OWNER, bool LONG, bool DENSE>
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LONG ? 1 : DENSE ? kJoinBpcDense : kJoinBpcSparse))) void k_join(JoinArgs a, const QRec *__restrict__ recs,
                                                       const uint32_t *__restrict__ sval,
                                                       const Unit *__restrict__ units,
                                                       unsigned long long *__restrict__ work)
@@ -1183,6 +1186,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
     __shared__ longlong2 s_rt[kWaves][64];      // record (tlo, thi)
     __shared__ float4 s_ra[kWaves][64];         // record (alo, ahi, qv, own)
     __shared__ ulonglong2 s_rs[kWaves][2][64];  // record near-prefix signature
+    constexpr int kOutStage = LONG ? 1 : DENSE ? kStageDense : kStageSparse;
     __shared__ uint16_t s_os[kWaves][kOutStage];  // a batch's pairs as (record slot << 6 | lane), staged
     __shared__ uint32_t s_pe[kWaves][64];         // each lane's posting entity (for the staged stores)
     const int lane = threadIdx.x & 63;
@@ -2175,7 +2179,7 @@ int64_t SearchEngine::touched(const dssg_index *idx, int64_t nq, const int64_t *
 
 void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
                           const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
-                          const int32_t *q_owner, hipStream_t s, dssg_pairs *out)
+                          const int32_t *q_owner, hipStream_t s, dssg_pairs *out, int64_t nqc_known)
 {
     if (q_owner && !idx->has_owner) throw Error(DSSG_ERR_INVALID, "search by owner on an index built without owners");
     if (nq >= (int64_t)kLongQ) throw Error(DSSG_ERR_INVALID, "search: more than 2^29 queries per batch");
@@ -2191,9 +2195,10 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         join_ms_ = 0;
     };
     if (nq <= 0 || idx->n_p == 0) return empty();
-    // the one host sync before the join: the batch's cell count sizes the
-    // per-cell buffers and bounds every later device count
-    const int64_t nqc = fetch(q_offs + nq, s);
+    // the batch's cell count sizes the per-cell buffers and bounds every
+    // later device count: from the caller (a covering it just ran), else the
+    // one host sync before the join
+    const int64_t nqc = nqc_known >= 0 ? nqc_known : fetch(q_offs + nq, s);
     if (nqc >= (int64_t)0xffffffffll) throw Error(DSSG_ERR_CAPACITY, "search: more than 2^32 - 1 query cells per batch");
     if (nqc == 0) return empty();
     if (nq <= small_max_q_ && nqc <= 16 * small_max_q_)
@@ -2280,7 +2285,8 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     ja.ix = ix;
     ja.qv = qv;
     ja.lazy_sig_recs = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(lazy_sig_recs_, 0xffffffffll));
-    const unsigned nblocks = (unsigned)n_cu_ * kJoinBlocksPerCU;
+    const bool dense = dense_out_;
+    const unsigned nblocks = (unsigned)n_cu_ * (dense ? kJoinBpcDense : kJoinBpcSparse);
     if (out_rcap_ == 0) out_rcap_ = ((int64_t)nq * 16 / kRegions / kOutChunk + 2) * kOutChunk;
     if (any_long && tag_rcap_ == 0) tag_rcap_ = ((int64_t)nq * 4 / kRegions / kOutChunk + 2) * kOutChunk;
     const int qb = bits_for(nq), eb = bits_for(idx->n_e);
@@ -2322,11 +2328,12 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         ja.out = OutArgs{oq, oe, OutStream{out_rcap_, fills, ctl + kCtlOut}, tk, OutStream{tag_rcap_, tfills, ctl + kCtlTOut},
                          eb, hbm, cnt};
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
-        auto kshort = q_owner ? k_join<true, false> : k_join<false, false>;
+        auto kshort = dense ? (q_owner ? k_join<true, false, true> : k_join<false, false, true>)
+                            : (q_owner ? k_join<true, false, false> : k_join<false, false, false>);
         hipLaunchKernelGGL(kshort, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
                            (const uint32_t *)sval, (const Unit *)units, ctl + kCtlQueue);
         if (any_long) {  // the same output streams, continued
-            auto klong = q_owner ? k_join<true, true> : k_join<false, true>;
+            auto klong = q_owner ? k_join<true, true, false> : k_join<false, true, false>;
             JoinArgs jl = ja;
             jl.ur = Regions{ctl + kCtlUnitsL, ucap_l};
             hipLaunchKernelGGL(klong, dim3(nblocks), dim3(64 * kWaves), 0, s, jl, (const QRec *)recs,
@@ -2373,6 +2380,9 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         runs_ = 0;
         units_ = nu;
         tests_ = (int64_t)h[kCtlMisc + 2];
+        // the next batch's join shape: dense output (pairs above a quarter of
+        // the lane tests) takes the wider stage
+        if (tests_ > 0) dense_out_ = 4 * n > tests_;
         iters_ = (int64_t)h[kCtlMisc + 3];
         long_queries_ = (int64_t)h[kCtlMisc + 5];
         long_postings_ = idx->n_long_fp;

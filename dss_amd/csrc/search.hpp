@@ -75,9 +75,11 @@ class SearchEngine {
     // ones) are long x long pairs, deduplicated after the join (on a
     // cell-range shard: kept only by the shard of their smallest shared cell,
     // so each comes back once across shards).
+    // nqc >= 0: the batch's cell count q_offs[nq], known to the caller (no
+    // read back before the join).
     void search(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
                 const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
-                const int32_t *q_owner, hipStream_t s, dssg_pairs *out);
+                const int32_t *q_owner, hipStream_t s, dssg_pairs *out, int64_t nqc = -1);
     // Roofline accounting: postings scanned and distinct candidate entities
     // (predicate disabled), i.e. sum_q M_q and sum_q D_q of SURVEY s8(d).
     void stats(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells, hipStream_t s,
@@ -148,6 +150,7 @@ class SearchEngine {
     bool timing_ = false;
     int64_t tag_bucket_avg_ = 1024;
     int64_t lazy_sig_recs_ = 0;
+    bool dense_out_ = false;  // the previous batch's pass density was high: k_join's 6 x 1024-pair stage shape
     double join_ms_ = 0;
     int64_t units_ = 0, keys_ = 0, runs_ = 0, iters_ = 0, tests_ = 0;
     int64_t flushes_ = 0, merges_ = 0, merge_lanes_ = 0, tagged_ = 0, long_queries_ = 0, long_postings_ = 0;
