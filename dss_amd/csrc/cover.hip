@@ -1981,8 +1981,12 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     if (nd > 0)
         hipLaunchKernelGGL(k_reverse_list, dim3((unsigned)std::min<int64_t>((nd + 3) / 4, 1024)), dim3(256), 0, s, dlist,
                            dlist_n, xoff, nvx, rev_flag, xyz, uv);
-    if (std::getenv("DSS_COVER_STATS"))
-        fprintf(stderr, "[cover] n %lld vertices %lld clipped edges %lld\n", (long long)n, (long long)nx, (long long)ne);
+    if (std::getenv("DSS_COVER_STATS")) {
+        unsigned int ns = 0;
+        DSS_HIP(hipMemcpy(&ns, slow_n, sizeof(ns), hipMemcpyDeviceToHost));
+        fprintf(stderr, "[cover] n %lld vertices %lld clipped edges %lld descent %lld exact-setup %u\n", (long long)n,
+                (long long)nx, (long long)ne, (long long)nd, ns);
+    }
     // direct candidates (most footprints): the cells of each one's bound,
     // tested now, compacted after the counts
     unsigned long long *fkm = kmask_.ensure(8 * (n + 1)), *fum = fkm + 4 * (n + 1);

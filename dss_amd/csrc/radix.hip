@@ -387,6 +387,9 @@ template void radix_sort_pairs<uint32_t, unsigned long>(const uint32_t *, uint32
 template void radix_sort_pairs<unsigned long long, uint32_t>(const unsigned long long *, unsigned long long *,
                                                              const uint32_t *, uint32_t *, int64_t, int,
                                                              DevBuf<unsigned char> &, hipStream_t);
+template void radix_sort_pairs_dn<uint32_t, unsigned long>(const uint32_t *, uint32_t *, const unsigned long *,
+                                                           unsigned long *, int64_t, const int64_t *, int,
+                                                           DevBuf<unsigned char> &, hipStream_t);
 template void radix_sort_pairs_dn<uint32_t, uint32_t>(const uint32_t *, uint32_t *, const uint32_t *, uint32_t *, int64_t,
                                                       const int64_t *, int, DevBuf<unsigned char> &, hipStream_t);
 template void radix_sort_keys<unsigned long long>(const unsigned long long *, unsigned long long *, int64_t, int,

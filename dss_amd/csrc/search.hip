@@ -749,11 +749,14 @@ __global__ void k_qcount(int64_t nq, const uint32_t *perm, const uint32_t *qvali
 }
 
 // Per query cell with postings: its key (slot << 1 | wide) and value (the
-// query cell) at off[rank of its query] + its rank among the query's cells
-// with postings -- the queries in order, each query's cells in cell order.
+// query cell | its query's quantised start << 32: after the sort by cell the
+// unit-range searches probe one 8-B value per step, and no pass gathers the
+// 64-B records for their starts) at off[rank of its query] + its rank among
+// the query's cells with postings -- the queries in order, each query's
+// cells in cell order.
 __global__ void k_qemit(int64_t nqc, const uint32_t *cq, const uint32_t *cslot, const uint32_t *vpre,
                         const uint32_t *qvb, const uint32_t *rank, const uint32_t *okey, const int64_t *off,
-                        uint32_t *key, uint32_t *val)
+                        uint32_t *key, uint64_t *val)
 {
     const int64_t k = tid64();
     if (k >= nqc) return;
@@ -763,7 +766,7 @@ __global__ void k_qemit(int64_t nqc, const uint32_t *cq, const uint32_t *cslot, 
     const uint32_t wide = (okey[r] & kWideBit) ? 1u : 0u;
     const int64_t w = off[r] + (int64_t)(vpre[k] - qvb[q]);
     key[w] = s << 1 | wide;
-    val[w] = (uint32_t)k;
+    val[w] = (uint64_t)(uint32_t)k | (uint64_t)(okey[r] & (kWideBit - 1u)) << 32;
 }
 
 // One record per query cell: time window, altitudes, owner, flags and the
@@ -977,27 +980,17 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
 // start-sorted tile that is [m_first - dqmax, m_last + dcap]; the records'
 // quantised starts (their order) bracket it by binary search.  One thread
 // per unit.
-__device__ __forceinline__ uint32_t lb_q(const uint32_t *sq, uint32_t lo, uint32_t hi, uint32_t v)
+__device__ __forceinline__ uint32_t lb_q(const uint64_t *sv, uint32_t lo, uint32_t hi, uint32_t v)
 {
-    while (lo < hi) {  // first record in [lo, hi) with quantised start >= v
+    while (lo < hi) {  // first record in [lo, hi) with quantised start (sv's high word) >= v
         const uint32_t m = (lo + hi) >> 1;
-        if (sq[m] < v) lo = m + 1;
+        if ((uint32_t)(sv[m] >> 32) < v) lo = m + 1;
         else hi = m;
     }
     return lo;
 }
 
-// Each sorted key's record's quantised start, contiguous: the unit-range
-// searches then probe one 4-B array instead of two dependent gathers
-// (sval, then the 64-B record) per step.
-__global__ void k_rec_q(const int64_t *dnkeys, const uint32_t *sval, const QRec *recs, long long tbase, int qshift,
-                        uint32_t *sq)
-{
-    const int64_t i = tid64();
-    if (i < *dnkeys) sq[i] = order_q(recs[sval[i]].tlo, tbase, qshift);
-}
-
-__global__ void k_unit_ranges(IndexView a, Regions ur, Unit *units, const uint32_t *sq,
+__global__ void k_unit_ranges(IndexView a, Regions ur, Unit *units, const uint64_t *sq,
                               const unsigned long long *dqslots, long long tbase, int qshift)
 {
     int64_t pre[kRegions + 1];
@@ -1179,7 +1172,7 @@ struct JoinArgs {
 // near-prefix signature (broadcast) with each lane's posting signature.
 template <bool OWNER, bool LONG, bool DENSE>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LONG ? 1 : DENSE ? kJoinBpcDense : kJoinBpcSparse))) void k_join(JoinArgs a, const QRec *__restrict__ recs,
-                                                      const uint32_t *__restrict__ sval,
+                                                      const uint64_t *__restrict__ sval,
                                                       const Unit *__restrict__ units,
                                                       unsigned long long *__restrict__ work)
 {
@@ -1305,7 +1298,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 int4 h0 = make_int4(0, 0, 0, 0), h1 = h0;
                 ulonglong2 g0 = make_ulonglong2(0, 0), g1 = g0;
                 if (r < x1) {
-                    const int4 *r4 = reinterpret_cast<const int4 *>(recs + sval[r]);
+                    const int4 *r4 = reinterpret_cast<const int4 *>(recs + (uint32_t)sval[r]);
                     h0 = r4[0];
                     h1 = r4[1];
                     const long long tlo = ((long long)h0.y << 32) | (uint32_t)h0.x;
@@ -2236,8 +2229,8 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     int64_t *qc = qcnt_.ensure(nq + 1), *qo = qoff_.ensure(nq + 2);
     hipLaunchKernelGGL(k_qcount, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, perm, qvalid, qc, qrank);
     exclusive_scan_i64(qc, qo, nq, tmp2_, s);
-    uint32_t *key = kkey_.ensure(nqc + 1), *skey = kkey2_.ensure(nqc + 1), *val = kval_.ensure(nqc + 1),
-             *sval = kval2_.ensure(nqc + 1);
+    uint32_t *key = kkey_.ensure(nqc + 1), *skey = kkey2_.ensure(nqc + 1);
+    uint64_t *val = kv64_.ensure(nqc + 1), *sval = kv64b_.ensure(nqc + 1);
     hipLaunchKernelGGL(k_qemit, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, nqc, cq, cslot, vpre, qvb, qrank, ok1,
                        qo, key, val);
     QRec *recs = (QRec *)rec_.ensure(sizeof(QRec) * (nqc + 1));
@@ -2246,9 +2239,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     // order), over the device key count qo[nq] (<= nqc)
     const int64_t *dnkeys = qo + nq;
     radix_sort_pairs_dn(key, skey, val, sval, nqc, dnkeys, bits_for(idx->n_slots()) + 1, tmp_, s);
-    uint32_t *sq = key;  // (the unsorted keys are consumed)
-    hipLaunchKernelGGL(k_rec_q, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, dnkeys, (const uint32_t *)sval,
-                       (const QRec *)recs, (long long)idx->tbase, idx->qshift, sq);
+    const uint64_t *sq = sval;  // (quantised starts in the high words)
     // (5) join units = 64-posting tiles of every cell the batch meets, each
     // with the records it can meet
     if (n_cu_ == 0) {
@@ -2272,11 +2263,11 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         hipLaunchKernelGGL(k_units, dim3(ugrid), dim3(kBlock), 0, s, ix, skey, dnkeys, Regions{ctl + kCtlUnits, ucap},
                            units, Regions{ctl + kCtlUnitsL, ucap_l}, units_l, 64u);
         hipLaunchKernelGGL(k_unit_ranges, dim3((unsigned)n_cu_ * 8), dim3(kBlock), 0, s, ix,
-                           Regions{ctl + kCtlUnits, ucap}, units, (const uint32_t *)sq,
+                           Regions{ctl + kCtlUnits, ucap}, units, sq,
                            (const unsigned long long *)(ctl + kCtlDq), (long long)idx->tbase, idx->qshift);
         if (any_long)
             hipLaunchKernelGGL(k_unit_ranges, dim3((unsigned)n_cu_ * 2), dim3(kBlock), 0, s, ix,
-                               Regions{ctl + kCtlUnitsL, ucap_l}, units_l, (const uint32_t *)sq,
+                               Regions{ctl + kCtlUnitsL, ucap_l}, units_l, sq,
                                (const unsigned long long *)(ctl + kCtlDq), (long long)idx->tbase, idx->qshift);
     };
     build_units();
@@ -2331,13 +2322,13 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         auto kshort = dense ? (q_owner ? k_join<true, false, true> : k_join<false, false, true>)
                             : (q_owner ? k_join<true, false, false> : k_join<false, false, false>);
         hipLaunchKernelGGL(kshort, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
-                           (const uint32_t *)sval, (const Unit *)units, ctl + kCtlQueue);
+                           (const uint64_t *)sval, (const Unit *)units, ctl + kCtlQueue);
         if (any_long) {  // the same output streams, continued
             auto klong = q_owner ? k_join<true, true, false> : k_join<false, true, false>;
             JoinArgs jl = ja;
             jl.ur = Regions{ctl + kCtlUnitsL, ucap_l};
             hipLaunchKernelGGL(klong, dim3(nblocks), dim3(64 * kWaves), 0, s, jl, (const QRec *)recs,
-                               (const uint32_t *)sval, (const Unit *)units_l, ctl + kCtlQueueL);
+                               (const uint64_t *)sval, (const Unit *)units_l, ctl + kCtlQueueL);
         }
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
         unsigned long long h[kCtlWords];

@@ -132,8 +132,9 @@ class SearchEngine {
     DevBuf<unsigned long long> small_cnt_;
     DevBuf<unsigned char> tmp_, tmp2_;
     // query side
-    DevBuf<uint32_t> cq_, dec_, okey_, okey2_, oval_, perm_, kkey_, kkey2_, kval_, kval2_, rbeg_, bt_;
+    DevBuf<uint32_t> cq_, dec_, okey_, okey2_, oval_, perm_, kkey_, kkey2_, rbeg_, bt_;
     DevBuf<int64_t> qcnt_, qoff_, rcnt_, roff_, ucnt_, uoff_, cnt64_;
+    DevBuf<uint64_t> kv64_, kv64b_;  // query-cell keys' values: cell | quantised start << 32
     DevBuf<uint8_t> qlong_;
     DevBuf<unsigned char> rec_, units_buf_, batch_buf_;
     DevBuf<unsigned long long> counter_, regcnt_;
