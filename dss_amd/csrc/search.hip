@@ -910,6 +910,9 @@ static_assert(sizeof(Unit) == 32, "Unit layout");
 __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *skey, const int64_t *dnkeys, Regions ur,
                                                   Unit *units, Regions url, Unit *units_l, uint32_t tp)
 {
+    __shared__ uint32_t s_xa[kBlock / 64][64];
+    __shared__ uint64_t s_s0[kBlock / 64][64], s_sr[kBlock / 64][64], s_s1[kBlock / 64][64], s_bu[kBlock / 64][64];
+    __shared__ uint4 s_par[kBlock / 64][64];  // ntr | lfp << 31, slot, first wide record, record end
     const int lane = threadIdx.x & 63;
     const uint32_t nkeys = (uint32_t)*dnkeys;
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
@@ -954,22 +957,47 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
         if (lane == 0 && totl) bl = atomicAdd(url.counter(reg), (unsigned long long)totl);
         bs = __shfl(bs, 0) + (xs - ns_);
         bl = __shfl(bl, 0) + (xl - nl_);
-        const unsigned long long bu = lfp ? bl : bs;
-        const Regions &dr = lfp ? url : ur;
-        Unit *du = lfp ? units_l : units;
-        for (uint32_t t = 0; t < nu; t++) {
+        // the wave's units written by all its lanes (a hot cell owns ~150
+        // tiles: one lane per cell would loop that long while the rest idle):
+        // each lane's cell parameters go to LDS, then lane u of every round
+        // finds the cell of unit u by a search over the units' prefix
+        const uint32_t xa = wave_incl_scan(nu);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)xa, 63);
+        const int wv = threadIdx.x >> 6;
+        __builtin_amdgcn_wave_barrier();
+        s_xa[wv][lane] = xa;
+        s_s0[wv][lane] = s0;
+        s_sr[wv][lane] = sr;
+        s_s1[wv][lane] = s1;
+        s_bu[wv][lane] = lfp ? bl : bs;
+        s_par[wv][lane] = make_uint4(ntr | (lfp ? 0x80000000u : 0u), slot, rw, re);
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t u = (uint32_t)lane; u < tot; u += 64) {
+            int lo = 0, hi = 63;  // the first lane L with s_xa[L] > u
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_xa[wv][mid] > u) hi = mid;
+                else lo = mid + 1;
+            }
+            const uint32_t t = u - (lo ? s_xa[wv][lo - 1] : 0u);  // the unit's tile within its cell
+            const uint4 pr = s_par[wv][lo];
+            const uint32_t lntr = pr.x & 0x7fffffffu;
+            const bool llfp = (pr.x >> 31) != 0;
+            const uint64_t l0 = s_s0[wv][lo], lr = s_sr[wv][lo], l1 = s_s1[wv][lo];
             Unit d;
-            const bool lng = t >= ntr;
-            const uint64_t b = lng ? sr + (uint64_t)tp * (t - ntr) : s0 + (uint64_t)tp * t;
-            const uint64_t e = lng ? s1 : sr;
+            const bool lng = t >= lntr;
+            const uint64_t b = lng ? lr + (uint64_t)tp * (t - lntr) : l0 + (uint64_t)tp * t;
+            const uint64_t e = lng ? l1 : lr;
             d.p0 = b;
             d.np = (uint32_t)min((uint64_t)tp, e - b) | (lng ? kUnitLong : 0u);
-            d.slot = slot;
-            d.n0 = p;
-            d.n1 = lng ? re : rw;  // a long tile meets every record
-            d.w0 = lng ? re : rw;
-            d.w1 = re;
-            const unsigned long long wpos = bu + t;
+            d.slot = pr.y;
+            d.n0 = w0 + (uint32_t)lo;
+            d.n1 = lng ? pr.w : pr.z;  // a long tile meets every record
+            d.w0 = lng ? pr.w : pr.z;
+            d.w1 = pr.w;
+            const unsigned long long wpos = s_bu[wv][lo] + t;
+            const Regions &dr = llfp ? url : ur;
+            Unit *du = llfp ? units_l : units;
             if ((int64_t)wpos < dr.cap) du[reg * dr.cap + (int64_t)wpos] = d;
         }
     }
