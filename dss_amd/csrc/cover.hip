@@ -367,7 +367,13 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
     if constexpr (FAST) rev_out[f] = 0;  // (set before any bail: the exact instance reverses in place itself)
     auto bail = [&]() {
         if constexpr (FAST) {
-            if (fail) slow_list[atomicAdd(slow_n, 1u)] = (uint32_t)f;
+            if (fail) {
+                // redone by the exact instance, launched only when the list
+                // is not empty; until then k_edge_counts sees nothing here
+                slow_list[atomicAdd(slow_n, 1u)] = (uint32_t)f;
+                mode[f] = MODE_NONE;
+                flags[f] = 0;
+            }
         }
         return FAST && fail;
     };
@@ -716,11 +722,21 @@ __device__ __forceinline__ bool planar_contains(bool origin_inside, const double
 
 // Count (pass 0) or write (pass 1) start nodes; big loops also get whole-face
 // nodes for faces without edges whose centre the loop contains.
+// A small descent footprint's start cell whose level-13 cells inside the
+// footprint's per-face bound become start nodes at once (k_start13).
+struct StartDesc {
+    uint64_t id;   // the start cell
+    int64_t w;     // its first output node
+    uint32_t f, i, j, meta;
+    uint4 box;     // the bound's level-13 (i0, i1, j0, j1)
+};
+
 template <int PASS>
 __global__ __launch_bounds__(64) void k_start(int64_t nd, const uint32_t *dlist, const int64_t *xoff, const V3 *xyz, const uint8_t *mode, const uint8_t *fmask,
                         const uint8_t *flags, const uint8_t *origin_in, const int32_t *nvx, const int64_t *eoff,
                         const double4 *clip_c, const uint8_t *cflags, int64_t *cnt, const int64_t *soff,
-                        uint32_t *nf, uint64_t *nid, uint32_t *ni, uint32_t *nj, uint32_t *nmeta)
+                        uint32_t *nf, uint64_t *nid, uint32_t *ni, uint32_t *nj, uint32_t *nmeta, StartDesc *sdesc,
+                        unsigned int *sdesc_n)
 {
     const int64_t k = tid64();
     if (k >= nd) return;
@@ -755,11 +771,54 @@ __global__ __launch_bounds__(64) void k_start(int64_t nd, const uint32_t *dlist,
                     uint64_t id[4];
                     uint32_t ii[4], jj[4], mt[4];
                     int k = start_cells(b, fc, id, ii, jj, mt);
-                    if (PASS)
-                        for (int q = 0; q < k; q++, w++) {
-                            nf[w] = (uint32_t)f; nid[w] = id[q]; ni[w] = ii[q]; nj[w] = jj[q]; nmeta[w] = mt[q];
+                    const int L = k > 0 ? meta_level(mt[0]) : 0;
+                    if (k > 0 && L >= kFastMinLevel && L < kCoverLevel) {
+                        // a small bound (<= 4 x 4^(13 - L) level-13 cells):
+                        // its level-13 cells are the start nodes, in id order
+                        // (start cells by id, Hilbert order inside each), so
+                        // the descent decides them in one level instead of
+                        // walking down from L -- every cell that can
+                        // intersect the face part lies in the bound
+                        const int sh13 = kMaxLevel - kCoverLevel;
+                        const uint32_t i0 = (uint32_t)st_to_ij(uv_to_st(fmax(b.ulo, -1.0))) >> sh13,
+                                       i1 = (uint32_t)st_to_ij(uv_to_st(fmin(b.uhi, 1.0))) >> sh13;
+                        const uint32_t j0 = (uint32_t)st_to_ij(uv_to_st(fmax(b.vlo, -1.0))) >> sh13,
+                                       j1 = (uint32_t)st_to_ij(uv_to_st(fmin(b.vhi, 1.0))) >> sh13;
+                        // (the start cells cover the bound's cells: the
+                        // count is the rectangle's; the write pass walks
+                        // each start cell's Hilbert order, skipping every
+                        // subtree outside the rectangle)
+                        // (the start cells cover the bound's cells: each
+                        // start cell's share is its intersection with the
+                        // rectangle; k_start13 writes them, a wave per start
+                        // cell, in Hilbert order)
+                        const uint32_t span = 1u << (kCoverLevel - L);
+                        for (int q = 0; q < k; q++) {
+                            const uint32_t a0 = ii[q] >> sh13, b0 = jj[q] >> sh13;
+                            const uint32_t x0 = max(a0, i0), x1 = min(a0 + span - 1, i1);
+                            const uint32_t y0 = max(b0, j0), y1 = min(b0 + span - 1, j1);
+                            const int64_t cq = x1 >= x0 && y1 >= y0 ? (int64_t)(x1 - x0 + 1) * (y1 - y0 + 1) : 0;
+                            if (PASS && cq > 0) {
+                                StartDesc sd;
+                                sd.id = id[q];
+                                sd.w = w;
+                                sd.f = (uint32_t)f;
+                                sd.i = ii[q];
+                                sd.j = jj[q];
+                                sd.meta = mt[q];
+                                sd.box = make_uint4(i0, i1, j0, j1);
+                                sdesc[atomicAdd(sdesc_n, 1u)] = sd;
+                                w += cq;
+                            }
+                            c += cq;
                         }
-                    c += k;
+                    } else {
+                        if (PASS)
+                            for (int q = 0; q < k; q++, w++) {
+                                nf[w] = (uint32_t)f; nid[w] = id[q]; ni[w] = ii[q]; nj[w] = jj[q]; nmeta[w] = mt[q];
+                            }
+                        c += k;
+                    }
                 }
             } else {
                 if (PASS) {
@@ -773,6 +832,51 @@ __global__ __launch_bounds__(64) void k_start(int64_t nd, const uint32_t *dlist,
         }
     }
     if (!PASS) cnt[f] = c;
+}
+
+// The level-13 start nodes of k_start's listed start cells: a wave per start
+// cell, lanes over its 4^(13 - L) descendants in Hilbert (= id) order, the
+// ones inside the bound written contiguously from the cell's first node.
+__global__ __launch_bounds__(256) void k_start13(const StartDesc *sdesc, const unsigned int *sdesc_n, uint32_t *nf,
+                                                 uint64_t *nid, uint32_t *ni, uint32_t *nj, uint32_t *nmeta)
+{
+    const unsigned int n = *sdesc_n;
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
+    const int sh13 = kMaxLevel - kCoverLevel;
+    const uint64_t lsb13 = lsb_for_level(kCoverLevel);
+    for (int64_t d = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); d < (int64_t)n; d += nw) {
+        const StartDesc sd = sdesc[d];
+        const int L = meta_level(sd.meta), fc = meta_face(sd.meta);
+        const uint32_t nd13 = 1u << (2 * (kCoverLevel - L));
+        const uint64_t lsbL = lsb_for_level(L);
+        int64_t w = sd.w;
+        for (uint32_t r0 = 0; r0 < nd13; r0 += 64) {
+            const uint32_t r = r0 + (uint32_t)lane;
+            int o = meta_orient(sd.meta);
+            uint32_t ci = sd.i, cj = sd.j;
+            for (int l = L + 1; l <= kCoverLevel; l++) {
+                const int digit = (int)((r >> (2 * (kCoverLevel - l))) & 3u);
+                const int ij = pos_to_ij(o, digit);
+                const uint32_t half = 1u << (kMaxLevel - l);
+                if (ij >> 1) ci += half;
+                if (ij & 1) cj += half;
+                o ^= pos_to_orientation(digit);
+            }
+            const uint32_t c13 = ci >> sh13, d13 = cj >> sh13;
+            const bool in = r < nd13 && c13 >= sd.box.x && c13 <= sd.box.y && d13 >= sd.box.z && d13 <= sd.box.w;
+            const unsigned long long m = __ballot(in);
+            if (in) {
+                const int64_t p = w + (int64_t)cmpct::lanes_below(m);
+                nf[p] = sd.f;
+                nid[p] = sd.id - lsbL + lsb13 + (uint64_t)r * (lsb13 << 1);
+                ni[p] = ci;
+                nj[p] = cj;
+                nmeta[p] = pack_meta(kCoverLevel, o, 0, fc);
+            }
+            w += (int64_t)__popcll(m);
+        }
+    }
 }
 
 // golang/geo polyline.go Polyline.IntersectsCell for a level-13 node.
@@ -829,7 +933,9 @@ __global__ __launch_bounds__(64) void k_expand_count(int64_t nn, const uint32_t 
             const double vlo = st_to_uv((double)nj[k] / (double)kMaxSize),
                          vhi = st_to_uv((double)(nj[k] + size) / (double)kMaxSize);
             const bool planar = (flags[f] & FL_PLANAR) != 0;
-            if (level < kCoverLevel) {
+            // coarse test: a clipped edge (or a polyline vertex) within the
+            // coarse padding of the node; a node it misses meets nothing
+            auto coarse_hit = [&]() {
                 const double pm = kCoarsePad;
                 bool hit = false;
                 for (int e = 0; e < ne && !hit; e++) {
@@ -845,6 +951,10 @@ __global__ __launch_bounds__(64) void k_expand_count(int64_t nn, const uint32_t 
                               v <= (vhi + pm);
                     }
                 }
+                return hit;
+            };
+            if (level < kCoverLevel) {
+                const bool hit = coarse_hit();
                 if (hit) a = 2;
                 else if (md == MODE_LOOP) {
                     if (planar) a = planar_contains(origin_in[f] != 0, clip_f + base, ne, ni[k], nj[k], level) ? 1 : 0;
@@ -862,8 +972,10 @@ __global__ __launch_bounds__(64) void k_expand_count(int64_t nn, const uint32_t 
                 if (in) a = 1;
                 else if (planar) a = planar_contains(origin_in[f] != 0, clip_f + base, ne, ni[k], nj[k], level) ? 1 : 0;
                 else defer = true;
-            } else {
+            } else if (coarse_hit()) {
                 defer = true;  // polyline.go IntersectsCell
+            } else {
+                a = 0;  // (a level-13 start node of a small polyline's bound that no edge comes near)
             }
         }
         if (!defer) {
@@ -1963,30 +2075,38 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     hipLaunchKernelGGL(k_setup<true>, dim3(grid_for(n, 64)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng,
                        radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo,
                        fbox, fwd, rev, fan_fail, not_inner, omode, perm, rev_flag, bad);
-    hipLaunchKernelGGL(k_setup<false>, dim3(min(grid_for(n, 64), 512u)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat,
-                       lng, radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j,
-                       finfo, fbox, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
     int64_t *eoff = eoff_.ensure(n + 1);
     uint32_t *dlist = dlist_.ensure(n + 1);
     unsigned int *dlist_n = dlist_n_.ensure(1);
-    DSS_HIP(hipMemsetAsync(dlist_n, 0, sizeof(unsigned int), s));
-    hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv, dlist, dlist_n);
-    exclusive_scan_i64(nv, eoff, n, tmp_, s);
     int64_t ne = 0;
-    unsigned int nd_u = 0;
-    DSS_HIP(hipMemcpyAsync(&ne, eoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    DSS_HIP(hipMemcpyAsync(&nd_u, dlist_n, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
-    DSS_HIP(hipStreamSynchronize(s));
+    unsigned int nd_u = 0, ns_u = 0;
+    // per footprint its clipped-edge items and the descent list, then one
+    // sync for their totals; the exact setup of the footprints the triage
+    // left (a kernel whose 492 B of scratch per lane cost ~0.09 ms per launch
+    // even over an empty list) runs only when there are any, and the counts
+    // are taken again after it
+    for (int pass = 0; pass < 2; pass++) {
+        DSS_HIP(hipMemsetAsync(dlist_n, 0, sizeof(unsigned int), s));
+        hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv, dlist,
+                           dlist_n);
+        exclusive_scan_i64(nv, eoff, n, tmp_, s);
+        DSS_HIP(hipMemcpyAsync(&ne, eoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipMemcpyAsync(&nd_u, dlist_n, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+        if (pass == 0) DSS_HIP(hipMemcpyAsync(&ns_u, slow_n, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipStreamSynchronize(s));
+        if (pass == 1 || ns_u == 0) break;
+        hipLaunchKernelGGL(k_setup<false>, dim3(std::min<unsigned>((ns_u + 63) / 64, 512u)), dim3(64), 0, s, slow, slow_n, n, kind,
+                           voff, lat, lng, radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id,
+                           st_i, st_j, finfo, fbox, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           nullptr);
+    }
     const int64_t nd = nd_u;  // descent footprints (big, multi-face, polyline): the only ones k_start visits
     if (nd > 0)
         hipLaunchKernelGGL(k_reverse_list, dim3((unsigned)std::min<int64_t>((nd + 3) / 4, 1024)), dim3(256), 0, s, dlist,
                            dlist_n, xoff, nvx, rev_flag, xyz, uv);
-    if (std::getenv("DSS_COVER_STATS")) {
-        unsigned int ns = 0;
-        DSS_HIP(hipMemcpy(&ns, slow_n, sizeof(ns), hipMemcpyDeviceToHost));
+    if (std::getenv("DSS_COVER_STATS"))
         fprintf(stderr, "[cover] n %lld vertices %lld clipped edges %lld descent %lld exact-setup %u\n", (long long)n,
-                (long long)nx, (long long)ne, (long long)nd, ns);
-    }
+                (long long)nx, (long long)ne, (long long)nd, ns_u);
     // direct candidates (most footprints): the cells of each one's bound,
     // tested now, compacted after the counts
     unsigned long long *fkm = kmask_.ensure(8 * (n + 1)), *fum = fkm + 4 * (n + 1);
@@ -2011,7 +2131,8 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     if (nd > 0) {  // (none: no start nodes, no second sync)
         DSS_HIP(hipMemsetAsync(nv, 0, sizeof(int64_t) * n, s));
         hipLaunchKernelGGL(k_start<0>, dim3(grid_for(nd, 64)), dim3(64), 0, s, nd, dlist, xoff, xyz, mode, fmask, flags,
-                           orig, nvx, eoff, clip_c, cflags, nv, soff, nullptr, nullptr, nullptr, nullptr, nullptr);
+                           orig, nvx, eoff, clip_c, cflags, nv, soff, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           nullptr);
         exclusive_scan_i64(nv, soff, n, tmp_, s);
         DSS_HIP(hipMemcpyAsync(&nn, soff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipStreamSynchronize(s));
@@ -2019,9 +2140,16 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     int cur = 0;
     Frontier *F = &fr_[cur];
     F->ensure(nn + 1);
-    if (nn > 0)
+    if (nn > 0) {
+        StartDesc *sdesc = (StartDesc *)sdesc_.ensure(sizeof(StartDesc) * (size_t)(24 * nd + 1));
+        unsigned int *sdesc_n = sdesc_n_.ensure(1);
+        DSS_HIP(hipMemsetAsync(sdesc_n, 0, sizeof(unsigned int), s));
         hipLaunchKernelGGL(k_start<1>, dim3(grid_for(nd, 64)), dim3(64), 0, s, nd, dlist, xoff, xyz, mode, fmask, flags,
-                           orig, nvx, eoff, clip_c, cflags, nullptr, soff, F->f.p, F->id.p, F->i.p, F->j.p, F->meta.p);
+                           orig, nvx, eoff, clip_c, cflags, nullptr, soff, F->f.p, F->id.p, F->i.p, F->j.p, F->meta.p,
+                           sdesc, sdesc_n);
+        hipLaunchKernelGGL(k_start13, dim3((unsigned)std::min<int64_t>((24 * nd + 3) / 4, 1024)), dim3(256), 0, s, sdesc,
+                           sdesc_n, F->f.p, F->id.p, F->i.p, F->j.p, F->meta.p);
+    }
     int *any_open = flag_.ensure(1);
     unsigned int *xlist_n = xlist_n_.ensure(1);
     for (int iter = 0; iter < 32 && nn > 0; iter++) {

@@ -70,6 +70,8 @@ class CoverEngine {
     DevBuf<uint32_t> slow_, vown_, eown_, dlist_, xlist_;
     DevBuf<unsigned int> dlist_n_, xlist_n_;
     DevBuf<uint8_t> fanf_, ninner_, badv_;
+    DevBuf<unsigned char> sdesc_;      // k_start13's start cells
+    DevBuf<unsigned int> sdesc_n_;
     DevBuf<uint32_t> perm_, towner_;
     DevBuf<uint8_t> omode_, revf_;
     DevBuf<int64_t> tcnt_, toff_;
