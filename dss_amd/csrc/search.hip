@@ -98,6 +98,10 @@ struct Regions {
 constexpr int kWaves = 4;  // waves per join workgroup
 constexpr int kJoinBpcSparse = 7, kJoinBpcDense = 6;
 constexpr int kStageSparse = 640, kStageDense = 1024;
+#ifndef DSS_JOIN_LONG_WPE
+#define DSS_JOIN_LONG_WPE 1
+#endif
+constexpr int kJoinLongWpe = DSS_JOIN_LONG_WPE;  // the long variant's register budget (waves per SIMD)
 #ifndef DSS_EMIT_DENSITY
 #define DSS_EMIT_DENSITY 4
 #endif
@@ -1199,7 +1203,7 @@ struct JoinArgs {
 // smallest-shared-cell rule (SQL DISTINCT, Q13) compares the record's
 // near-prefix signature (broadcast) with each lane's posting signature.
 template <bool OWNER, bool LONG, bool DENSE>
-__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LONG ? 1 : DENSE ? kJoinBpcDense : kJoinBpcSparse))) void k_join(JoinArgs a, const QRec *__restrict__ recs,
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LONG ? kJoinLongWpe : DENSE ? kJoinBpcDense : kJoinBpcSparse))) void k_join(JoinArgs a, const QRec *__restrict__ recs,
                                                       const uint64_t *__restrict__ sval,
                                                       const Unit *__restrict__ units,
                                                       unsigned long long *__restrict__ work)
