@@ -894,7 +894,7 @@ __device__ __forceinline__ uint32_t lb_u32(const uint32_t *x, uint32_t lo, uint3
 // postings in start order, or of its long-duration ones) x that cell's
 // query records to test (positions in the sorted keys): narrow ones [n0, n1)
 // -- for a regular tile the sub-range whose quantised start can meet the
-// tile (k_unit_ranges) -- and wide ones [w0, w1); a long tile meets every
+// tile (unit_ranges) -- and wide ones [w0, w1); a long tile meets every
 // record of the cell.  32 bytes.
 constexpr uint32_t kUnitLong = 0x80000000u;  // np: long-duration tile
 struct alignas(16) Unit {
@@ -906,13 +906,51 @@ struct alignas(16) Unit {
 };
 static_assert(sizeof(Unit) == 32, "Unit layout");
 
+// Narrow record sub-range of every regular tile: a narrow record (window <=
+// dqmax) meets a posting only if tlo in [m - dqmax, max(t0, t1)], and over a
+// start-sorted tile that is [m_first - dqmax, m_last + dcap]; the records'
+// quantised starts (their order) bracket it by binary search, done by
+// k_units as it writes each unit (round 4: one pass over the units fewer).
+__device__ __forceinline__ uint32_t lb_q(const uint64_t *sv, uint32_t lo, uint32_t hi, uint32_t v)
+{
+    while (lo < hi) {  // first record in [lo, hi) with quantised start (sv's high word) >= v
+        const uint32_t m = (lo + hi) >> 1;
+        if ((uint32_t)(sv[m] >> 32) < v) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ void unit_ranges(const IndexView &a, Unit &d, const uint64_t *sq, long long dq, long long tbase,
+                                            int qshift)
+{
+    if ((d.np & kUnitLong) || (d.n1 <= d.n0 && d.w1 <= d.w0)) return;
+    {
+        const longlong2 f = a.b_t[d.p0], l = a.b_t[d.p0 + d.np - 1];
+        const long long m0 = tmin2(f.x, f.y), m1 = tmin2(l.x, l.y);
+        const long long lo = m0 < LLONG_MIN + dq ? LLONG_MIN : m0 - dq;
+        const long long hi = m1 > LLONG_MAX - a.dcap ? LLONG_MAX : m1 + a.dcap;
+        const uint32_t qhi = order_q(hi, tbase, qshift) + 1u;
+        if (d.n1 > d.n0) {
+            const uint32_t n0 = lb_q(sq, d.n0, d.n1, order_q(lo, tbase, qshift));
+            d.n1 = lb_q(sq, n0, d.n1, qhi);
+            d.n0 = n0;
+        }
+        // wide records (start-ordered within the cell's wide run) starting
+        // after every posting of the tile has ended meet none of them
+        if (d.w1 > d.w0) d.w1 = lb_q(sq, d.w0, d.w1, qhi);
+    }
+}
+
 // Join units, one wave per window of 64 sorted keys (grid-stride over the
 // device key count): every lane that starts a cell (a run of equal slot)
 // finds the cell's record ranges (within the window, or by binary search
 // past it) and emits one unit per 64-posting tile of the cell's regular
 // and long parts; slots come from one atomic per wave (region counters).
 __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *skey, const int64_t *dnkeys, Regions ur,
-                                                  Unit *units, Regions url, Unit *units_l, uint32_t tp)
+                                                  Unit *units, Regions url, Unit *units_l, uint32_t tp,
+                                                  const uint64_t *sq, const unsigned long long *dqslots, long long tbase,
+                                                  int qshift)
 {
     __shared__ uint32_t s_xa[kBlock / 64][64];
     __shared__ uint64_t s_s0[kBlock / 64][64], s_sr[kBlock / 64][64], s_s1[kBlock / 64][64], s_bu[kBlock / 64][64];
@@ -923,6 +961,9 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
     const int64_t nwaves = (int64_t)gridDim.x * (kBlock / 64);
     const int64_t nwin = ((int64_t)nkeys + 63) / 64;
     const int reg = (int)(blockIdx.x % kRegions);
+    unsigned long long dqm = 0;
+    for (int r = 0; r < kRegions; r++) dqm = max(dqm, dqslots[r * kRegStride]);
+    const long long dq = (long long)min(dqm, 1ull << 62);
     for (int64_t win = wave; win < nwin; win += nwaves) {
         const uint32_t w0 = (uint32_t)(win * 64), wend = min(w0 + 64u, nkeys);
         const uint32_t p = w0 + (uint32_t)lane;
@@ -999,6 +1040,7 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
             d.n1 = lng ? pr.w : pr.z;  // a long tile meets every record
             d.w0 = lng ? pr.w : pr.z;
             d.w1 = pr.w;
+            unit_ranges(a, d, sq, dq, tbase, qshift);  // a regular tile's record sub-ranges
             const unsigned long long wpos = s_bu[wv][lo] + t;
             const Regions &dr = llfp ? url : ur;
             Unit *du = llfp ? units_l : units;
@@ -1007,47 +1049,6 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
     }
 }
 
-// Narrow record sub-range of every regular tile: a narrow record (window <=
-// dqmax) meets a posting only if tlo in [m - dqmax, max(t0, t1)], and over a
-// start-sorted tile that is [m_first - dqmax, m_last + dcap]; the records'
-// quantised starts (their order) bracket it by binary search.  One thread
-// per unit.
-__device__ __forceinline__ uint32_t lb_q(const uint64_t *sv, uint32_t lo, uint32_t hi, uint32_t v)
-{
-    while (lo < hi) {  // first record in [lo, hi) with quantised start (sv's high word) >= v
-        const uint32_t m = (lo + hi) >> 1;
-        if ((uint32_t)(sv[m] >> 32) < v) lo = m + 1;
-        else hi = m;
-    }
-    return lo;
-}
-
-__global__ void k_unit_ranges(IndexView a, Regions ur, Unit *units, const uint64_t *sq,
-                              const unsigned long long *dqslots, long long tbase, int qshift)
-{
-    int64_t pre[kRegions + 1];
-    const int64_t n = ur.total(pre);
-    unsigned long long dqm = 0;
-    for (int r = 0; r < kRegions; r++) dqm = max(dqm, dqslots[r * kRegStride]);
-    const long long dq = (long long)min(dqm, 1ull << 62);
-    for (int64_t u = tid64(); u < n; u += nthreads64()) {
-        Unit &d = units[ur.slot_of(pre, u)];
-        if ((d.np & kUnitLong) || (d.n1 <= d.n0 && d.w1 <= d.w0)) continue;
-        const longlong2 f = a.b_t[d.p0], l = a.b_t[d.p0 + d.np - 1];
-        const long long m0 = tmin2(f.x, f.y), m1 = tmin2(l.x, l.y);
-        const long long lo = m0 < LLONG_MIN + dq ? LLONG_MIN : m0 - dq;
-        const long long hi = m1 > LLONG_MAX - a.dcap ? LLONG_MAX : m1 + a.dcap;
-        const uint32_t qhi = order_q(hi, tbase, qshift) + 1u;
-        if (d.n1 > d.n0) {
-            const uint32_t n0 = lb_q(sq, d.n0, d.n1, order_q(lo, tbase, qshift));
-            d.n1 = lb_q(sq, n0, d.n1, qhi);
-            d.n0 = n0;
-        }
-        // wide records (start-ordered within the cell's wide run) starting
-        // after every posting of the tile has ended meet none of them
-        if (d.w1 > d.w0) d.w1 = lb_q(sq, d.w0, d.w1, qhi);
-    }
-}
 
 __device__ __forceinline__ long long readlane64(long long v, int lane)
 {
@@ -1458,13 +1459,24 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                             s_os[w][iu++] = (uint16_t)((uint32_t)j << 6 | (uint32_t)lane);
                         }
                         __builtin_amdgcn_wave_barrier();
-                        for (int p = lane; p < total_u; p += 64) {
-                            const uint32_t v = s_os[w][p];
-                            const uint32_t q = (uint32_t)__float_as_int(s_ra[w][v >> 6].z) & ~kQFlags;
-                            const uint32_t e = s_pe[w][v & 63u];
-                            const unsigned long long pos = su.at((unsigned long long)p);
-                            a.out.q[pos] = q;
-                            a.out.e[pos] = e;
+                        // (the batch usually fits what is left of the wave's
+                        // chunk: one contiguous run, no chunk-strided mapping)
+                        if (su.n0 >= total_u) {
+                            const unsigned long long a0 = uni64(su.a0);
+                            for (int p = lane; p < total_u; p += 64) {
+                                const uint32_t v = s_os[w][p];
+                                a.out.q[a0 + p] = (uint32_t)__float_as_int(s_ra[w][v >> 6].z) & ~kQFlags;
+                                a.out.e[a0 + p] = s_pe[w][v & 63u];
+                            }
+                        } else {
+                            for (int p = lane; p < total_u; p += 64) {
+                                const uint32_t v = s_os[w][p];
+                                const uint32_t q = (uint32_t)__float_as_int(s_ra[w][v >> 6].z) & ~kQFlags;
+                                const uint32_t e = s_pe[w][v & 63u];
+                                const unsigned long long pos = su.at((unsigned long long)p);
+                                a.out.q[pos] = q;
+                                a.out.e[pos] = e;
+                            }
                         }
                         __builtin_amdgcn_wave_barrier();
                     } else if (wu) {
@@ -2293,14 +2305,8 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         DSS_HIP(hipMemsetAsync(ctl + kCtlUnits, 0, kR * sizeof(unsigned long long), s));
         DSS_HIP(hipMemsetAsync(ctl + kCtlUnitsL, 0, kR * sizeof(unsigned long long), s));
         hipLaunchKernelGGL(k_units, dim3(ugrid), dim3(kBlock), 0, s, ix, skey, dnkeys, Regions{ctl + kCtlUnits, ucap},
-                           units, Regions{ctl + kCtlUnitsL, ucap_l}, units_l, 64u);
-        hipLaunchKernelGGL(k_unit_ranges, dim3((unsigned)n_cu_ * 8), dim3(kBlock), 0, s, ix,
-                           Regions{ctl + kCtlUnits, ucap}, units, sq,
+                           units, Regions{ctl + kCtlUnitsL, ucap_l}, units_l, 64u, sq,
                            (const unsigned long long *)(ctl + kCtlDq), (long long)idx->tbase, idx->qshift);
-        if (any_long)
-            hipLaunchKernelGGL(k_unit_ranges, dim3((unsigned)n_cu_ * 2), dim3(kBlock), 0, s, ix,
-                               Regions{ctl + kCtlUnitsL, ucap_l}, units_l, sq,
-                               (const unsigned long long *)(ctl + kCtlDq), (long long)idx->tbase, idx->qshift);
     };
     build_units();
     // (6) join; grow the output (and the units) and rerun if too small
