@@ -1,0 +1,85 @@
+"""GPU parity of the general covering pipeline (batches above the wave path's
+16384 footprints) on the geometry its special paths handle -- GPU == CPU
+oracle bit for bit (status, cells, area):
+
+* small loops straddling cube-face edges and corners (multi-face: the
+  descent, started at the bound's level-13 cells by k_start / k_start13);
+* zero-area loops (Q3: open polylines; the descent's coarse test before the
+  exact list), across face edges and inside faces;
+* small loops with vertices on level-13 cell corners and edges 1e-15..1e-12
+  off cell boundary lines (k_cand_fp's float prefilter next to the exact
+  double tests);
+* footprints that the triage hands to the exact setup (k_setup<false>,
+  launched only when the list is not empty): fan loops around a pole.
+
+Semantics: pkg/geo/s2.go:99-122 (Covering), pkg/models/geo.go:224-268.
+"""
+import numpy as np
+import pytest
+
+from test_gpu_covering import _check_batch, _corner_uv, _face_uv_to_latlng
+
+pytestmark = pytest.mark.gpu
+
+
+def _base_footprints(rng):
+    polys = []
+    d = 4e-5
+    for face in range(6):
+        # straddling each face edge and corner: a few level-13 cells on each side
+        for (u, v) in ((1.0, 0.3), (-1.0, -0.2), (0.4, 1.0), (-0.7, -1.0), (1.0, 1.0), (-1.0, 1.0), (1.0, -1.0)):
+            for s in (1.0, 2.0, 5.0):
+                e = s * d
+                polys.append([_face_uv_to_latlng(face, *p) for p in
+                              ((u - e, v - e), (u + e, v - e), (u + e, v + e), (u - e, v + e))])
+                polys.append([_face_uv_to_latlng(face, *p) for p in
+                              ((u + e, v + e), (u + e, v - e), (u - e, v - e), (u - e, v + e))])  # clockwise: Q4
+                # zero area (A, B, A): an open polyline across the edge
+                a, b = (u - e, v - 0.5 * e), (u + e, v + 0.5 * e)
+                polys.append([_face_uv_to_latlng(face, *p) for p in (a, b, a)])
+        # inside the face: cell corners, boundary-hugging edges, polylines
+        for _ in range(4):
+            u, v = _corner_uv(rng)
+            a = rng.uniform(0, 2 * np.pi)
+            polys.append([_face_uv_to_latlng(face, *p) for p in
+                          ((u, v), (u + d * np.cos(a), v + d * np.sin(a)), (u + d * np.cos(a + 2), v + d * np.sin(a + 2)))])
+            for off in (0.0, 1e-15, -1e-13, 1e-12):
+                uu = u + off
+                polys.append([_face_uv_to_latlng(face, *p) for p in
+                              ((uu, v - 2 * d), (uu, v + 2 * d), (uu + (d if off >= 0 else -d), v))])
+            p0, p1 = (u, v), (u + 3 * d, v + 1.5 * d)
+            polys.append([_face_uv_to_latlng(face, *p) for p in (p0, p1, p0)])
+    # around the poles (fan terms far from the fan origin: the exact setup)
+    for lat0 in (89.9995, -89.9995):
+        for k in (3, 5, 8):
+            polys.append([(lat0, -180.0 + 360.0 * i / k) for i in range(k)])
+    return polys
+
+
+@pytest.mark.parametrize("seed", [7, 8])
+def test_general_pipeline_special_paths(oracle, seed):
+    from dss_amd import geo
+    rng = np.random.default_rng(seed)
+    base = _base_footprints(rng)
+    # replicate with small seeded jitter past the wave path's batch limit
+    reps = 20000 // len(base) + 1
+    polys = []
+    for r in range(reps):
+        for p in base:
+            if r == 0:
+                polys.append(p)
+                continue
+            j = rng.normal(0, 2e-6, size=(len(p), 2))
+            polys.append([(float(np.clip(la + dj[0], -90, 90)), float(((ln + dj[1] + 180) % 360) - 180))
+                          for (la, ln), dj in zip(p, j)])
+    assert len(polys) > 16384
+    kind = np.zeros(len(polys), np.int32)
+    voff = np.zeros(len(polys) + 1, np.int64)
+    voff[1:] = np.cumsum([len(p) for p in polys])
+    lat = np.array([q[0] for p in polys for q in p], dtype=np.float64)
+    lng = np.array([q[1] for p in polys for q in p], dtype=np.float64)
+    rad = np.zeros(len(polys), np.float32)
+    offs, cells, status, area = oracle.cover_batch(kind, voff, lat, lng, rad)
+    res = geo.cover_batch(kind, voff, lat, lng, rad)
+    _check_batch(dict(status=status, offs=offs, cells=cells, area_km2=area), res)
+    assert (status == 0).sum() > len(polys) // 2
