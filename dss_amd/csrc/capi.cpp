@@ -245,6 +245,11 @@ int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value)
         ctx->search.set_lazy_sig_recs(value);
         return DSSG_OK;
     }
+    if (std::string(key) == "join_shape") {  // 0 auto (default), 1 sparse 7 x 640, 2 dense 6 x 1024
+        if (value < 0 || value > 2) return DSSG_ERR_INVALID;
+        ctx->search.set_join_shape((int)value);
+        return DSSG_OK;
+    }
     if (std::string(key) == "small_search") {  // max queries of the one-launch small-batch join (0: never)
         ctx->search.set_small_max_q(value);
         return DSSG_OK;

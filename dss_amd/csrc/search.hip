@@ -2314,7 +2314,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     ja.ix = ix;
     ja.qv = qv;
     ja.lazy_sig_recs = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(lazy_sig_recs_, 0xffffffffll));
-    const bool dense = dense_out_;
+    const bool dense = join_shape_ == 0 ? dense_out_ : join_shape_ == 2;
     const unsigned nblocks = (unsigned)n_cu_ * (dense ? kJoinBpcDense : kJoinBpcSparse);
     if (out_rcap_ == 0) out_rcap_ = ((int64_t)nq * 16 / kRegions / kOutChunk + 2) * kOutChunk;
     if (any_long && tag_rcap_ == 0) tag_rcap_ = ((int64_t)nq * 4 / kRegions / kOutChunk + 2) * kOutChunk;

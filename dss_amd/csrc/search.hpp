@@ -92,6 +92,9 @@ class SearchEngine {
     // join units with at most this many records load the posting signatures
     // only for the lanes that need them (0: always prefetched)
     void set_lazy_sig_recs(int64_t v) { lazy_sig_recs_ = v; }
+    // k_join's occupancy / pair-stage shape: 0 picks by the previous batch's
+    // pass density, 1 forces 7 x 640, 2 forces 6 x 1024
+    void set_join_shape(int v) { join_shape_ = v; }
     double last_join_kernel_ms() const { return join_ms_; }
     int64_t last_units() const { return units_; }
     int64_t last_keys() const { return keys_; }
@@ -149,9 +152,10 @@ class SearchEngine {
     int64_t tag_rcap_ = 0;  // tagged-key slots per region
     int64_t units_cap_hint_ = 0, units_cap_hint_l_ = 0;
     bool timing_ = false;
-    int64_t tag_bucket_avg_ = 1024;
+    int64_t tag_bucket_avg_ = 2048;
     int64_t lazy_sig_recs_ = 0;
     bool dense_out_ = false;  // the previous batch's pass density was high: k_join's 6 x 1024-pair stage shape
+    int join_shape_ = 0;      // 0: by dense_out_; 1: the sparse shape; 2: the dense shape (tests)
     double join_ms_ = 0;
     int64_t units_ = 0, keys_ = 0, runs_ = 0, iters_ = 0, tests_ = 0;
     int64_t flushes_ = 0, merges_ = 0, merge_lanes_ = 0, tagged_ = 0, long_queries_ = 0, long_postings_ = 0;

@@ -406,10 +406,13 @@ int dssg_phase_times(dssg_ctx *ctx, double *cover_ms, double *join_ms, double *j
 void dssg_set_timing(dssg_ctx *ctx, int enabled);
 /* Tuning knobs of this context's engines (defaults suit every BASELINE
  * config):  "tag_bucket_avg" = average long x long pairs per deduplication
- * bucket (default 1024; <= 0 selects the full-sort path); "lazy_sig_recs" =
+ * bucket (default 2048; <= 0 selects the full-sort path); "lazy_sig_recs" =
  * join units with at most this many query records load the postings'
  * near-prefix signatures only for the lanes that need them (default 0:
- * always prefetched).  Unknown key: DSSG_ERR_INVALID. */
+ * always prefetched); "join_shape" = the join's occupancy / pair-stage shape
+ * (0: picked per batch from the previous batch's pass density, the default;
+ * 1: 7 workgroups per CU with 640-pair stages; 2: 6 with 1024).  Unknown key
+ * or value: DSSG_ERR_INVALID. */
 int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value);
 /* Work counters of the most recent search: query-cell keys (cells of the
  * batch whose cell holds postings), join units (<= 64 records x a posting
