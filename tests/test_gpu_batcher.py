@@ -1,6 +1,7 @@
 """The per-request path (dssg_batcher): concurrent single searchOperations
 requests, each an uncovered footprint, coalesced into shared batches; every
-caller's answer equals a direct batch search of its own request, covering
+caller's answer and covering status equal the oracle's (CPU covering + join
+of the same request) and a direct batch search of its own request; covering
 errors come back as statuses."""
 import threading
 
@@ -10,7 +11,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_batcher_matches_direct_search():
+def test_batcher_matches_oracle_and_direct_search(oracle):
     from dss_amd import geo, workload as W
     from dss_amd.store import Batcher, EntityIndex
     _, q, qa, it, ia, now = W.config(0, scale=0.02)
@@ -19,6 +20,13 @@ def test_batcher_matches_direct_search():
     cq = geo.cover_batch(q.kind, q.voff, q.lat, q.lng, q.radius_m)
     wq, we = idx.search_operations_batch(cq.offs, cq.cells, qa.alt_lo, qa.alt_hi, qa.t0, qa.t1, now)
     want = [we[wq == i] for i in range(q.n)]
+    # the oracle's answer per request (pkg/scd/store/cockroach/operations.go:376-402)
+    io, ic, _, _ = oracle.cover_batch(it.kind, it.voff, it.lat, it.lng, it.radius_m)
+    qo, qc, qst, _ = oracle.cover_batch(q.kind, q.voff, q.lat, q.lng, q.radius_m)
+    oq, oe = oracle.search(io, ic, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1, None, qo, qc, qa.alt_lo, qa.alt_hi,
+                           np.maximum(qa.t0, now), qa.t1)
+    want_o = [oe[oq == i] for i in range(q.n)]
+    assert sum(len(w) for w in want_o) > 0
     b = Batcher(idx, max_batch=64, max_wait_us=500)
     got = [None] * q.n
     errors = []
@@ -42,7 +50,8 @@ def test_batcher_matches_direct_search():
     assert not errors, errors[0]
     for i in range(q.n):
         st, ids = got[i]
-        assert st == int(cq.status[i])
+        assert st == int(cq.status[i]) == int(qst[i])
+        assert np.array_equal(np.sort(ids), np.sort(want_o[i])), i
         assert np.array_equal(np.sort(ids), np.sort(want[i])), i
     nreq, nbatch = b.stats()
     assert nreq == q.n and nbatch < q.n  # requests really were coalesced
