@@ -7,12 +7,17 @@
 // balanced across passes: 18 bits -> 3 x 6, level-13 cell ids -> 4 x 7-8;
 // 9-bit digits measured slower: 0.26 vs 0.20 ms on 11.6M 18-bit keys),
 // three launches:
-//   k_rs_hist    one 4096-key tile per block: per-wave LDS digit counts,
+//   k_rs_hist    one 2048-key tile per block (8 keys per thread: the
+//                scatter's 24 KiB of LDS staging for (u32, u64) pairs lets
+//                more blocks share a CU than 16 keys' 48 KiB; configs[2]'s
+//                per-search key-sort scatter 0.059 -> 0.041 ms per pass,
+//                187.2M against 183.9M q/s, profiles/r04s_radix_tiles), per-wave
+//                LDS digit counts,
 //                written digit-major hist[d][tile] (so one row scan gives
 //                every tile its global start per digit);
 //   k_rs_scan    one block per digit: exclusive scan of its row in place,
 //                row total -> dtot[d];
-//   k_rs_scatter the same tile again: each wave ranks its 1024 keys by
+//   k_rs_scatter the same tile again: each wave ranks its 512 keys by
 //                ballot match (rb ballots per 64 keys -> the lanes holding the
 //                same digit; rank = popcount of those below the lane) against
 //                a per-wave LDS digit counter, so the order stays stable
@@ -35,15 +40,15 @@ constexpr int kRBlock = 256;
 #define DSS_RADIX_BITS 8
 #endif
 #ifndef DSS_RADIX_ITEMS
-#define DSS_RADIX_ITEMS 16
+#define DSS_RADIX_ITEMS 8
 #endif
 constexpr int kMaxDigitBits = DSS_RADIX_BITS;    // digit bits per pass (8: 256 digits, one per thread)
 constexpr int kMaxDigits = 1 << kMaxDigitBits;
 constexpr int kDPT = kMaxDigits / kRBlock;       // digits per thread in the per-digit phases
 constexpr int kRWaves = kRBlock / 64;
 constexpr int kItems = DSS_RADIX_ITEMS;
-constexpr int kTile = kRBlock * kItems;  // 4096 keys per block
-constexpr int kWaveTile = 64 * kItems;   // 1024 keys per wave, contiguous
+constexpr int kTile = kRBlock * kItems;  // 2048 keys per block
+constexpr int kWaveTile = 64 * kItems;   // 512 keys per wave, contiguous
 
 template <typename K>
 __device__ __forceinline__ uint32_t digit_of(K k, int shift, uint32_t mask)
@@ -297,7 +302,7 @@ void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, const int64_t
 {
     if (n <= 0) return;
     // positions are uint32: the digit offsets of the last tile stay < 2^32
-    if (n >= ((int64_t)1 << 32) - kTile) throw Error(DSSG_ERR_CAPACITY, "radix sort: more than 2^32 - 4096 keys");
+    if (n >= ((int64_t)1 << 32) - kTile) throw Error(DSSG_ERR_CAPACITY, "radix sort: more than 2^32 - 2048 keys");
     const int kbits = (int)(8 * sizeof(K));
     if (bits > kbits) bits = kbits;
     if (bits <= 0) {
