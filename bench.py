@@ -47,8 +47,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-_STAGE = ["start"]
+_STAGE = ["start", time.time()]
 _JSON_FD = [None]
+# Stages with collectives in them: one that runs past its limit is taken to be
+# hung (a peer that never issued its side of a collective); the process exits
+# non-zero instead of holding its GPU until an outside timeout (the launcher
+# then stops the other ranks).
+STAGE_LIMIT_S = {"warmup": 900, "timed steps": 900, "replica rate beside the sharded one": 900,
+                 "sharded phases": 900}
 
 
 def keep_stdout_for_json():
@@ -72,6 +78,7 @@ def emit(result):
 def stage(name):
     """Name the current stage (the heartbeat reports it)."""
     _STAGE[0] = name
+    _STAGE[1] = time.time()
     log(f"[bench] {name}")
 
 
@@ -84,6 +91,10 @@ def heartbeat(every=30.0):
         while True:
             time.sleep(every)
             log(f"[bench] alive {time.time() - t0:.0f}s, stage: {_STAGE[0]}")
+            limit = STAGE_LIMIT_S.get(_STAGE[0])
+            if limit and time.time() - _STAGE[1] > limit:
+                log(f"[bench] stage '{_STAGE[0]}' exceeded {limit}s: exiting (a collective is presumed hung)")
+                os._exit(3)
     threading.Thread(target=run, daemon=True).start()
 
 
@@ -106,6 +117,9 @@ def parse_args(argv=None):
                     help="queries in the CPU-baseline sample (-1: auto -- the whole step's batch for configs[0]..[3], a "
                          "bounded sample of ~10-30 s of CPU work for configs[4]; 0: skip).  The sample's "
                          "cells and pairs are compared with the GPU step's (parity on the sampled queries)")
+    ap.add_argument("--parity-sample", type=int, default=20000,
+                    help="ranks other than 0 (N > 1): queries of their own batch whose cells and pairs are compared "
+                         "with the oracle after the timed steps (0: skip)")
     ap.add_argument("--no-verify", action="store_true", help="skip the full-size GPU-vs-oracle parity check")
     ap.add_argument("--survey-model", type=int, default=1, help="also count SURVEY s8(d)'s per-query byte model")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -199,6 +213,15 @@ def launch_probe(path):
         json.dump(rec, f)
     if rank == 0:
         print(json.dumps({"launch_probe": rec}), flush=True)
+
+
+def allreduce_vals(dist, torch, vals, op):
+    """All-reduce a few float64 control values over the process group (on the
+    GPU when the group is RCCL, else on the host); returns a list."""
+    dev = f"cuda:{torch.cuda.current_device()}" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=op)
+    return t.cpu().tolist()
 
 
 def timed(torch, dist, dev, world, fn):
@@ -393,44 +416,6 @@ def cover_ahead_steps(torch, D, ctx, covers, d_q, steps, search_fn):
         th.join()
 
 
-def sharded_pipeline_steps(torch, D, pipes, d_q, qargs, nq, steps):
-    """`steps` native sharded steps over P pipelines, each its own context,
-    stream, host thread and communicator (dssg_sharded_search_device): step k
-    runs on pipeline k % P, so every communicator sees its calls in the same
-    order on every rank while the pipelines overlap one another's cover, join
-    and exchanges.  A failing pipeline raises StepFailure (the others are
-    left to finish their own steps: a collective cannot be abandoned on one
-    rank alone)."""
-    import threading
-    P = len(pipes)
-    errors = []
-    done = [0] * P
-
-    def run(p):
-        pctx, ps, nat = pipes[p]
-        try:
-            with torch.cuda.stream(ps):
-                for _ in range(p, steps, P):
-                    c = D.cover(pctx, d_q)
-                    nat.step(c.offs, c.cells, nq, *qargs)
-                    done[p] += 1
-                ps.synchronize()
-        except BaseException as e:  # noqa: BLE001 -- re-raised on the calling thread
-            errors.append(e)
-
-    threads = [threading.Thread(target=run, args=(p,)) for p in range(1, P)]
-    for th in threads:
-        th.start()
-    run(0)
-    for th in threads:
-        th.join()
-    if errors:
-        raise StepFailure(f"{len(errors)} sharded pipeline(s) failed ({sum(done)} of {steps} steps finished): "
-                          f"{type(errors[0]).__name__}: {errors[0]}") from errors[0]
-    if sum(done) != steps:
-        raise StepFailure(f"{sum(done)} of {steps} sharded steps finished")
-
-
 def main():
     argv = sys.argv[1:]
     args = parse_args(argv)
@@ -453,14 +438,19 @@ def main():
     mode = args.mode or ("sharded" if world > 1 else "replica")
     exchange = args.exchange or ("native" if args.dist_backend == "nccl" else "torch")
     torch.cuda.set_device(local)
-    stage_host = args.dist_backend != "nccl"
+    # The process group is the control plane (rendezvous, barriers, the
+    # timing max, parity flags).  With the library's own RCCL exchange it is
+    # gloo, so each process holds one RCCL (the library's); the torch
+    # exchange (fallback / rehearsals) runs over the PG or an RCCL subgroup.
+    native_wanted = mode == "sharded" and exchange == "native"
+    pg_backend = "gloo" if native_wanted else args.dist_backend
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")   # single-process sharded runs (no launcher)
     os.environ.setdefault("MASTER_PORT", "29533")
     if world > 1 or mode == "sharded":
-        if args.dist_backend == "nccl":
+        if pg_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
         else:
-            dist.init_process_group(args.dist_backend, rank=rank, world_size=world)
+            dist.init_process_group(pg_backend, rank=rank, world_size=world)
 
     from dss_amd import _lib, device as D, workload as W
 
@@ -517,22 +507,23 @@ def main():
                                f"beside it; the build's sorts are inside index_build_s"})
     sharded = native = None
     if mode == "sharded":
-        # the instrumented torch-exchange path always exists (phase breakdown);
-        # the timed steps use the library's own RCCL exchange when native
-        sharded = shard.ShardedSearch(ctx, index, ranges, stage_host=stage_host)
-        if exchange == "native":
-            # the library's own communicator; if any rank cannot open it (no
-            # RCCL to dlopen, init error) every rank falls back to the torch
-            # exchange, agreed by one all-reduce, and the line says so
-            ok = torch.ones(1, device=dev)
+        if native_wanted:
+            # the library's own communicators (queries; pairs home on a second
+            # stream); if any rank cannot open them (no RCCL to dlopen, init
+            # error) every rank falls back to the torch exchange, agreed by
+            # one all-reduce, and the line says so
+            ok = torch.ones(1)
             err = None
             try:
-                uid = torch.zeros(_lib.COMM_ID_BYTES, dtype=torch.uint8, device=dev)
-                if rank == 0:
-                    uid.copy_(torch.frombuffer(bytearray(shard.NativeComm.unique_id(ctx)), dtype=torch.uint8))
-                dist.broadcast(uid, 0)  # bootstrap only: the id travels once
-                native = shard.NativeShardedSearch(ctx, shard.NativeComm(ctx, world, rank, bytes(uid.cpu().numpy())),
-                                                   index, ranges)
+                comms = []
+                for _ in range(2):
+                    uid = torch.zeros(_lib.COMM_ID_BYTES, dtype=torch.uint8)
+                    if rank == 0:
+                        uid.copy_(torch.frombuffer(bytearray(shard.NativeComm.unique_id(ctx)), dtype=torch.uint8))
+                    dist.broadcast(uid, 0)  # bootstrap only: the id travels once
+                    comms.append(shard.NativeComm(ctx, world, rank, bytes(uid.numpy())))
+                native = shard.NativeShardedSearch(ctx, comms[0], index, ranges, xcomm=comms[1],
+                                                   xstream=torch.cuda.Stream(device=dev))
             except Exception as e:  # noqa: BLE001 -- reported in the result line
                 err = f"{type(e).__name__}: {e}"
                 ok.zero_()
@@ -541,77 +532,62 @@ def main():
                 log(f"[rank {rank}] native exchange unavailable ({err}); using the torch exchange")
                 native = None
                 exchange = f"torch (native exchange init failed on some rank: {err})"
+        if native is None:
+            # the torch-collective exchange: over RCCL when the data path may
+            # use it (a subgroup beside the gloo control group), else staged
+            # through host memory (gloo rehearsals)
+            group = None
+            if pg_backend != "nccl" and args.dist_backend == "nccl":
+                group = dist.new_group(backend="nccl")
+            sharded = shard.ShardedSearch(ctx, index, ranges, group=group,
+                                          stage_host=group is None and pg_backend != "nccl")
 
     def shard_search(cells, timed_phases=False):
-        if native is not None and not timed_phases:
+        if native is not None:
             return native.step(cells.offs, cells.cells, nq, *qargs)
         return sharded.step(cells.offs, cells.cells, nq, *qargs, timed=timed_phases)
 
     def step(timed=False):
         cells = D.cover(ctx, d_q)
-        if sharded is not None:
+        if mode == "sharded":
             return cells, shard_search(cells, timed)
         return cells, D.search(ctx, index, cells, *qargs)
 
+    stage("warmup")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
     # extra pipelines: each its own context (engine scratch), stream and host
     # thread, warmed to its steady-state buffers and kept only if HBM holds it
+    # (sharded: they cover ahead; every collective is issued by this thread)
     workers, pipe_note = add_pipelines(args, torch, D, _lib, local, dev, tunes, d_q,
-                                       None if sharded is not None else (index, qargs))
-    pipes = []  # native sharded pipelines: (context, stream, NativeShardedSearch), one communicator each
-    if native is not None:
-        # every rank runs the same number of pipelines (one communicator per
-        # pipeline, created in the same order everywhere)
-        npipe = torch.tensor([1 + len(workers)], device=dev)
-        dist.all_reduce(npipe, op=dist.ReduceOp.MIN)
-        while 1 + len(workers) > int(npipe.item()):
-            workers.pop()[0].close()
-        pipes.append((ctx, torch.cuda.current_stream(), native))
-        for wctx, ws in workers:
-            uid = torch.zeros(_lib.COMM_ID_BYTES, dtype=torch.uint8, device=dev)
-            if rank == 0:
-                uid.copy_(torch.frombuffer(bytearray(shard.NativeComm.unique_id(ctx)), dtype=torch.uint8))
-            dist.broadcast(uid, 0)
-            nat = shard.NativeShardedSearch(wctx, shard.NativeComm(wctx, world, rank, bytes(uid.cpu().numpy())),
-                                            index, ranges)
-            with torch.cuda.stream(ws):  # warm it (a collective step: same order on every rank)
-                c = D.cover(wctx, d_q)
-                nat.step(c.offs, c.cells, nq, *qargs)
-                ws.synchronize()
-            pipes.append((wctx, ws, nat))
+                                       None if mode == "sharded" else (index, qargs))
 
     # ------------------------------------------------------------ timed steps
     stage("timed steps")
     general = None
-    if pipes:
-        elapsed = timed(torch, dist, dev, world,
-                        lambda: sharded_pipeline_steps(torch, D, pipes, d_q, qargs, nq, args.steps))
-        if world == 1:
-            # one rank: the library routes by the identity; the general path
-            # (route, own segment copied, unpack, join, own pairs to the
-            # output) timed beside it
-            for pctx, _, _ in pipes:
-                pctx.set_tuning("route_identity", 0)
-            sharded_pipeline_steps(torch, D, pipes, d_q, qargs, nq, len(pipes))
-            gt = timed(torch, dist, dev, world,
-                       lambda: sharded_pipeline_steps(torch, D, pipes, d_q, qargs, nq, args.steps))
-            for pctx, _, _ in pipes:
-                pctx.set_tuning("route_identity", 1)
-            general = {"value": world * nq * args.steps / gt, "ms_per_step": 1000.0 * gt / max(1, args.steps),
-                       "note": "one rank with the routing forced through the general path (route_identity=0)"}
-    elif sharded is not None:
+    if mode == "sharded":
         elapsed = timed(torch, dist, dev, world,
                         lambda: cover_ahead_steps(torch, D, ctx, workers, d_q, args.steps, shard_search))
+        if world == 1 and native is not None:
+            # one rank: the library routes by the identity; the general path
+            # (route, own segment copied, unpack, join, own pairs to the
+            # output, pairs on the exchange stream) timed beside it
+            ctx.set_tuning("route_identity", 0)
+            cover_ahead_steps(torch, D, ctx, workers, d_q, 2, shard_search)
+            gt = timed(torch, dist, dev, world,
+                       lambda: cover_ahead_steps(torch, D, ctx, workers, d_q, args.steps, shard_search))
+            ctx.set_tuning("route_identity", 1)
+            general = {"value": world * nq * args.steps / gt, "ms_per_step": 1000.0 * gt / max(1, args.steps),
+                       "note": "one rank with the routing forced through the general path (route_identity=0)"}
     else:
         elapsed = timed(torch, dist, dev, world,
                         lambda: replica_steps(torch, D, ctx, workers, d_q, index, qargs, args.steps))
     ms_per_step = 1000.0 * elapsed / max(1, args.steps)
     value = world * nq * args.steps / elapsed
 
-    if sharded is not None:
+    if mode == "sharded":
         # the replica layout beside it: every rank joins its own batch against
         # the whole index, same pipelines, no exchange
         stage("replica rate beside the sharded one")
@@ -623,22 +599,13 @@ def main():
                    "note": "whole index on every GPU, each rank's batch joined locally (no exchange)"}
         if general is not None:
             replica["sharded_general_path"] = general
-        native_pairs = None
-        if native is not None:  # the timed path's own output, checked below beside the torch path's
-            c = D.cover(ctx, d_q)
-            p = native.step(c.offs, c.cells, nq, *qargs)
-            nq_ = D.copy_back(ctx, p.q, int(p.n), np.uint32).astype(np.uint64)
-            ne_ = D.copy_back(ctx, p.e, int(p.n), np.uint32).astype(np.uint64)
-            native_pairs = (nq_ << np.uint64(32)) | ne_
-        for _, _, nat in pipes:
-            nat.comm.close()
         for wctx, _ in workers:
             wctx.close()
-        sharded_report(args, ctx, D, dist, torch, sharded, step, None if args.no_verify else full_index,
-                       i_cells_h, ranges, rank, world, nq, ni, n_post, build_s, value, ms_per_step, *qargs,
-                       exchange=exchange, replica=replica, native_pairs=native_pairs, pipelines=max(1, len(pipes)))
-        if args.no_verify:
-            ctx.L.dssg_index_free(full_index)
+        sharded_report(args, ctx, D, dist, torch, sharded, native, step, full_index, i_offs_t, i_cells_t, ranges, rank,
+                       world, nq, ni, n_post, build_s, value, ms_per_step, qargs, queries, qa, intents, ia, now,
+                       exchange=exchange, replica=replica, pipelines=1 + len(workers), pipe_note=pipe_note)
+        if native is not None:
+            native.close()
         ctx.L.dssg_index_free(index)
         dist.destroy_process_group()
         return
@@ -692,14 +659,17 @@ def main():
                                                  C.c_void_p(cells.cells), D._stream_ptr(), C.byref(m_tot),
                                                  C.byref(d_tot)))
     survey_bytes = 8 * c_tot + 12 * m_tot.value + 24 * d_tot.value + 8 * r_tot
+    stage("device copy bandwidth")
+    copy_bw = copy_bandwidth(ctx, torch, dev)
 
+    # every rank: its step's covering and pairs against the oracle (rank 0:
+    # the timed CPU baseline on its --cpu-sample; the others: --parity-sample
+    # queries), the flags reduced over ranks
+    stage("oracle parity" + (" + cpu baseline" if rank == 0 else ""))
+    cpu, parity = oracle_leg(args, ctx, D, dist, torch, dev, rank, world, queries, qa, intents, ia, now, i_offs_t,
+                             i_cells_t, cells, pairs)
     result = None
     if rank == 0:
-        cpu = parity = None
-        if args.cpu_sample != 0 and world == 1:
-            stage("cpu baseline")
-            cpu, parity = cpu_baseline(args, ctx, intents, ia, queries, qa, now,
-                                       lambda sc: intent_csr(torch, i_offs_t, i_cells_t, sc), cells, pairs)
         # last: the per-request calls reuse the context's cover / search
         # buffers that `cells` and `pairs` point into
         latency = None
@@ -742,6 +712,8 @@ def main():
             "roofline": {"kernel": "k_join (overlap join + fused altitude/time filter)", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
+                         "hbm_copy_measured_GBs": copy_bw,
+                         "frac_of_measured_copy": achieved / copy_bw if copy_bw else None,
                          "traffic": traffic["bytes_per_launch"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
                          "algorithmic_bytes": join_bytes, "launch_ms": kern_avg_ms,
@@ -776,63 +748,79 @@ def pair_checksum(keys: np.ndarray) -> int:
     return int(tot)
 
 
-def sharded_report(args, ctx, D, dist, torch, sh, step, full, i_cells_h, ranges, rank, world, nq, ni, n_post, build_s,
-                   value, ms_per_step, q_alo, q_ahi, q_tlo, q_thi, exchange="torch", replica=None,
-                   native_pairs=None, pipelines=1):
-    """Phase breakdown (synchronised passes, max over ranks), the shard join's
-    roofline, and parity: every rank's delivered pair set == a whole-index
-    search of its own queries (count + order-independent checksum)."""
+def sharded_report(args, ctx, D, dist, torch, sh, native, step, full, i_offs_t, i_cells_t, ranges, rank, world, nq,
+                   ni, n_post, build_s, value, ms_per_step, qargs, queries, qa, intents, ia, now, exchange="torch",
+                   replica=None, pipelines=1, pipe_note=None):
+    """Phase breakdown (synchronised passes, max over ranks), the exchanged
+    bytes, the shard join's roofline, and parity: every rank's delivered pair
+    set (a) == a whole-index search of its own queries (count +
+    order-independent checksum) and (b) against the oracle, cells and pairs
+    compared exactly (rank 0: the timed CPU baseline on its --cpu-sample; the
+    others: --parity-sample queries)."""
     import ctypes as C
 
     from dss_amd import workload as W
     dev = f"cuda:{torch.cuda.current_device()}"
+    names = ["route", "exchange_queries", "join", "route_pairs", "exchange_pairs"]
+    stage("sharded phases")
     ctx.L.dssg_set_timing(ctx.h, 1)
-    sh.times = {}
+    if sh is not None:
+        sh.times = {}
     reps = 5
-    cover_ms, kern_ms = [], []
+    cover_ms, kern_ms, ph_sum, moved = [], [], dict.fromkeys(names, 0.0), {}
+    shard_rows = shard_cells = shard_pairs = touched = 0
     for _ in range(reps):
         cells, out = step(timed=True)
         ca, cb, cc = C.c_double(), C.c_double(), C.c_double()
         ctx.L.dssg_phase_times(ctx.h, C.byref(ca), C.byref(cb), C.byref(cc))
         cover_ms.append(ca.value)
         kern_ms.append(cc.value)
+        if native is not None:
+            ms, cnt = native.stats()
+            for k in names:
+                ph_sum[k] += ms[k]
+            moved = {k: cnt[k] for k in ("query_bytes_sent", "query_bytes_recv", "pair_bytes_sent", "pair_bytes_recv")}
+            shard_rows, shard_cells, shard_pairs, touched = cnt["rows"], cnt["cells"], cnt["shard_pairs"], cnt["touched"]
     ctx.L.dssg_set_timing(ctx.h, 0)
-    names = ["route", "exchange_queries", "join", "route_pairs", "exchange_pairs"]
-    ph = [float(np.mean(cover_ms))] + [1000.0 * sh.times.get(k, 0.0) / reps for k in names] + [float(np.mean(kern_ms))]
-    tph = torch.tensor(ph, dtype=torch.float64, device=dev)
-    dist.all_reduce(tph, op=dist.ReduceOp.MAX)
-    ph = tph.tolist()
-    phase = dict(zip(["cover"] + names + ["join_kernel"], ph))
+    if native is None:
+        ph_sum = {k: 1000.0 * sh.times.get(k, 0.0) for k in names}
+        moved = dict(sh.last_bytes)
+        shard_rows, shard_cells, shard_pairs, touched = sh.last_rows, sh.last_recv_ncells, sh.last_shard_pairs, \
+            sh.last_touched
+    torch.cuda.synchronize()
+    ph = [float(np.mean(cover_ms))] + [ph_sum[k] / reps for k in names] + [float(np.mean(kern_ms))]
+    phase = dict(zip(["cover"] + names + ["join_kernel"], allreduce_vals(dist, torch, ph, dist.ReduceOp.MAX)))
     # shard join roofline (DESIGN.md s5 byte model over what this shard joined)
-    nrc = sh.last_recv_ncells
-    p_touched = sh.last_touched
-    jb = 24 * sh.last_rows + 8 * nrc + 28 * p_touched + 8 * sh.last_shard_pairs
-    kern = ph[-1]
-    local = torch.tensor([jb / (float(np.mean(kern_ms)) * 1e-3) / 1e9, float(sh.last_rows), float(nrc),
-                          float(sh.last_shard_pairs), float(out.numel())], dtype=torch.float64, device=dev)
-    mins = local.clone()
-    dist.all_reduce(mins, op=dist.ReduceOp.MIN)
-    sums = local.clone()
-    dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-    # parity: whole-index search of this rank's own queries
-    parity = None
+    jb = 24 * shard_rows + 8 * shard_cells + 28 * touched + 8 * shard_pairs
+    kern = float(np.mean(kern_ms))
+    n_out = int(out.numel()) if torch.is_tensor(out) else int(out.n)
+    local = [jb / (kern * 1e-3) / 1e9, shard_rows, shard_cells, shard_pairs, n_out, sum(moved.values()),
+             moved.get("pair_bytes_recv", 0)]
+    mins = allreduce_vals(dist, torch, local, dist.ReduceOp.MIN)
+    sums = allreduce_vals(dist, torch, local, dist.ReduceOp.SUM)
+    # parity (a): whole-index search of this rank's own queries (the same
+    # covering `cells` the last sharded step routed)
+    parity = {}
+    gq, ge = sample_pairs_host(ctx, D, torch, dev, out, nq)
     if full is not None:
-        pairs = D.search(ctx, full, cells, q_alo, q_ahi, q_tlo, q_thi)  # cells: the last step's covering
-        torch.cuda.synchronize()
-        fq = D.copy_back(ctx, pairs.q, pairs.n, np.uint32).astype(np.uint64)
-        fe = D.copy_back(ctx, pairs.e, pairs.n, np.uint32).astype(np.uint64)
-        ctx.L.dssg_index_free(full)
-        want = (fq << np.uint64(32)) | fe
-        got = out.cpu().numpy().view(np.uint64)
+        pairs = D.search(ctx, full, cells, *qargs)
+        fq, fe = sample_pairs_host(ctx, D, torch, dev, pairs, nq)
+        want = (fq.astype(np.uint64) << np.uint64(32)) | fe.astype(np.uint64)
+        got = (gq.astype(np.uint64) << np.uint64(32)) | ge.astype(np.uint64)
         ok = len(want) == len(got) and pair_checksum(want) == pair_checksum(got)
-        nok = native_pairs is None or (len(want) == len(native_pairs) and
-                                       pair_checksum(want) == pair_checksum(native_pairs))
-        t = torch.tensor([1.0 if ok else 0.0, 1.0 if nok else 0.0, float(len(got))], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        parity = {"check": "per rank: count + sum(splitmix64(q << 32 | e)) of the delivered pairs == a whole-index "
-                           "search of the rank's own queries", "all_ranks_equal": bool(t[0].item() == 1.0)}
-        if native_pairs is not None:
-            parity["native_exchange_equal"] = bool(t[1].item() == 1.0)
+        t = allreduce_vals(dist, torch, [1.0 if ok else 0.0], dist.ReduceOp.MIN)
+        parity["whole_index_check"] = "per rank: count + sum(splitmix64(q << 32 | e)) of the delivered pairs == a " \
+                                      "whole-index GPU search of the rank's own queries"
+        parity["all_ranks_equal"] = bool(t[0] == 1.0)
+        del want, got, fq, fe
+        ctx.L.dssg_index_free(full)
+    # parity (b) + the CPU baseline: the oracle on every rank
+    stage("oracle parity" + (" + cpu baseline" if rank == 0 else ""))
+    cpu, opar = oracle_leg(args, ctx, D, dist, torch, dev, rank, world, queries, qa, intents, ia, now, i_offs_t,
+                           i_cells_t, cells, None, host_pairs=(gq, ge))
+    if opar:
+        parity.update(opar)
+    traffic = pmc_traffic("k_join", nq, ni, world=world, mode="sharded")
     if rank != 0:
         return
     result = {
@@ -852,24 +840,126 @@ def sharded_report(args, ctx, D, dist, torch, sh, step, full, i_cells_h, ranges,
                                f"sharded by S2 cell range over {world} GPU(s), {W.CONFIG_NAMES[args.config]}, S2 level 13",
                    "queries_per_gpu_step": nq, "intents": ni, "postings_rank0": n_post,
                    "parallelism": f"cell-range shards x{world}; queries routed to shards and pairs routed home by "
-                                  f"all-to-all ({'the library RCCL communicator' if exchange == 'native' else args.dist_backend})",
+                                  f"all-to-all ({'the library RCCL communicators' if exchange == 'native' else exchange})",
                    "exchange": exchange, "scale": args.scale, "pipelines_per_gpu": pipelines,
-                   "pipelines_note": "one communicator per pipeline; step k on pipeline k % P" if pipelines > 1 else
-                   "one pipeline (exchange + shard join in step order; covers ahead on the others)"},
+                   "pipelines_note": pipe_note or ("the other pipelines cover ahead; one host thread issues every "
+                                                   "collective (route, query all-to-all, join on the step stream; "
+                                                   "pairs home on the exchange stream, overlapping the next step)")},
         "replica": replica,
         "coverings_per_s": world * nq / (phase["cover"] * 1e-3),
         "phase_ms_max_over_ranks": phase,
-        "routed": {"rows_total": sums[1].item(), "rows_min_rank": mins[1].item(), "cells_total": sums[2].item(),
-                   "pairs_total": sums[4].item()},
+        "exchanged": {"bytes_per_step_rank0": moved, "bytes_per_step_all_ranks": sums[5],
+                      "pair_bytes_per_returned_pair": sums[6] / max(1.0, sums[4]),
+                      "pair_format": "8 B (home-local query << 32 | entity) per pair that crosses ranks; a rank's "
+                                     "own queries' pairs move no bytes"},
+        "routed": {"rows_total": sums[1], "rows_min_rank": mins[1], "cells_total": sums[2],
+                   "pairs_total": sums[4]},
         "index_build_s": build_s,
         "roofline": {"kernel": "k_join on the shard (overlap join + fused altitude/time filter)", "bound": "hbm",
-                     "achieved": local[0].item(), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": local[0].item() / HBM_PEAK_GBS, "traffic": None, "rank": 0,
-                     "algorithmic_bytes": jb, "launch_ms": float(np.mean(kern_ms))},
-        "cpu_baseline": None,
+                     "achieved": local[0], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": local[0] / HBM_PEAK_GBS,
+                     "traffic": traffic["bytes_per_launch"] if traffic else None,
+                     "traffic_source": traffic["source"] if traffic else None, "rank": 0,
+                     "algorithmic_bytes": jb, "launch_ms": kern,
+                     "counts": {"rows": shard_rows, "C": shard_cells, "P_touched": touched, "R": shard_pairs}},
+        "cpu_baseline": cpu,
         "parity": parity,
     }
     emit(result)
+
+
+def sample_pairs_host(ctx, D, torch, dev, pairs, n):
+    """(q, e) host arrays of the pairs whose query index is < n, filtered on
+    the GPU; `pairs` is a _lib.Pairs (device q / e arrays) or an int64
+    tensor packed (q << 32 | e)."""
+    import ctypes as C
+    if torch.is_tensor(pairs):
+        sel = pairs[(pairs >> 32) < n]
+        h = sel.cpu().numpy()
+        return (h >> 32).astype(np.uint32), (h & 0xFFFFFFFF).astype(np.uint32)
+    m = int(pairs.n)
+    if m == 0:
+        return np.zeros(0, np.uint32), np.zeros(0, np.uint32)
+    q = torch.empty(m, dtype=torch.int32, device=dev)
+    e = torch.empty(m, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    ctx.check(ctx.L.dssg_copy_device(ctx.h, C.c_void_p(q.data_ptr()), C.c_void_p(pairs.q), 4 * m, D._stream_ptr()))
+    ctx.check(ctx.L.dssg_copy_device(ctx.h, C.c_void_p(e.data_ptr()), C.c_void_p(pairs.e), 4 * m, D._stream_ptr()))
+    # (the copies run on the library stream when torch's is the default one:
+    # a device-wide sync orders them before torch reads the tensors)
+    torch.cuda.synchronize()
+    keep = q < n  # query ids < 2^24: no sign issue in int32
+    return q[keep].cpu().numpy().view(np.uint32), e[keep].cpu().numpy().view(np.uint32)
+
+
+def oracle_leg(args, ctx, D, dist, torch, dev, rank, world, queries, qa, intents, ia, now, i_offs_t, i_cells_t, cells,
+               pairs, host_pairs=None):
+    """The oracle on every rank, after the timed steps: rank 0 runs the CPU
+    baseline (timed; --cpu-sample queries, -1 = the config's auto sample),
+    every other rank --parity-sample queries of its own batch; each compares
+    the oracle's cells and pairs of its sample with its GPU step exactly
+    (`cells` = the step's covering, `pairs` or `host_pairs` its pairs).  The
+    flags are reduced over ranks.  Returns (rank 0's cpu_baseline or None,
+    parity dict or None)."""
+    n = args.cpu_sample if rank == 0 else args.parity_sample
+    if n < 0:
+        auto = AUTO_CPU_SAMPLE.get(args.config)
+        n = queries.n if auto is None else auto
+    n = min(n, queries.n)
+    if world > 1:  # one build of the checker (a no-op when prebuilt), then every rank loads it
+        from oracle import oracle as O
+        if rank == 0:
+            O.build()
+        dist.barrier()
+    cpu = parity = None
+    if n > 0 and not (args.no_verify and rank != 0):
+        g_offs = D.copy_back(ctx, cells.offs, n + 1, np.int64)
+        g_c = D.copy_back(ctx, cells.cells, int(g_offs[-1]), np.uint64)
+        gq, ge = host_pairs if host_pairs is not None else sample_pairs_host(ctx, D, torch, dev, pairs, n)
+        keep = gq < n
+        gq, ge = gq[keep], ge[keep]
+        cpu, parity = cpu_baseline(args, rank, n, intents, ia, queries, qa, now,
+                                   lambda sc, sub: intent_csr(torch, i_offs_t, i_cells_t, sc, subset=sub),
+                                   g_offs, g_c, gq, ge)
+    if world > 1:
+        ok = parity is not None and parity["cells_equal"] and parity["pairs_equal"]
+        f = [1.0 if ok else 0.0, n, parity["gpu_pairs"] if parity else 0]
+        fmin = allreduce_vals(dist, torch, f, dist.ReduceOp.MIN)
+        fsum = allreduce_vals(dist, torch, f, dist.ReduceOp.SUM)
+        parity = dict(parity or {}, rank0_check="oracle cells + pairs of rank 0's sample (exact)",
+                      oracle_all_ranks_equal=bool(fmin[0] == 1.0), oracle_ranks=world,
+                      oracle_queries_all_ranks=int(fsum[1]), oracle_pairs_all_ranks=int(fsum[2]),
+                      oracle_note=f"every rank compared the oracle's cells and pairs of its first queries "
+                                  f"(rank 0: {n}, the others: --parity-sample {args.parity_sample}) with what its "
+                                  f"GPU step delivered, exactly")
+    return cpu, parity
+
+
+def copy_bandwidth(ctx, torch, dev, nbytes=4 << 30):
+    """Measured device copy (the library's 16-B-vector copy kernel,
+    dssg_copy_device) in GB/s of read + write, beside the 8 TB/s spec
+    (SURVEY.md s8(d)); HIP events on the copy's own stream."""
+    import ctypes as C
+    try:
+        a = torch.empty(nbytes // 8, dtype=torch.int64, device=dev)
+        b = torch.empty_like(a)
+    except RuntimeError:
+        return None
+    a.fill_(1)
+    torch.cuda.synchronize()
+    st = torch.cuda.Stream(device=dev)  # events and the copy on one explicit stream
+    times = []
+    for _ in range(6):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        ctx.check(ctx.L.dssg_copy_device(ctx.h, C.c_void_p(b.data_ptr()), C.c_void_p(a.data_ptr()), nbytes,
+                                         C.c_void_p(st.cuda_stream)))
+        e1.record(st)
+        e1.synchronize()
+        times.append(e0.elapsed_time(e1))
+    del a, b
+    torch.cuda.empty_cache()
+    return 2 * nbytes / (float(np.median(times[1:])) * 1e-3) / 1e9
 
 
 LARGE_POSTINGS = 600_000_000  # above: no host copy of the intents' cells, no standalone sort-phase run
@@ -910,12 +1000,12 @@ def cover_chunked(ctx, D, torch, fp, dev, chunk=4_000_000):
     return offs, cells[:total]
 
 
-def intent_csr(torch, offs_t, cells_t, sample_cells):
+def intent_csr(torch, offs_t, cells_t, sample_cells, subset=False):
     """Host CSR of the intents the CPU baseline's index needs: all of them,
     or -- for airspaces past LARGE_POSTINGS -- only those sharing a cell with
     the sample's queries (the only ones that can pair with them), found on the
     GPU.  Returns (offs, cells, entity ids)."""
-    if cells_t.numel() <= LARGE_POSTINGS:
+    if cells_t.numel() <= LARGE_POSTINGS and not subset:
         offs = offs_t.cpu().numpy()
         return offs, cells_t.cpu().numpy().view(np.uint64), np.arange(len(offs) - 1, dtype=np.int64)
     dev = cells_t.device
@@ -967,10 +1057,16 @@ def sort_phase(ctx, torch, dev, i_offs_t, i_cells_t):
         times.append(ms.value)
     t = float(np.median(times[1:]))
     alg = 24 * P
+    passes = 4
+    phys = 32 * P  # per pass: k_rs_hist reads the 8-B keys, k_rs_scatter reads and writes key + value (12 + 12 B)
     return {"kernel": "radix sort of (cell, entity) postings (k_rs_hist/k_rs_scan/k_rs_scatter)", "bound": "hbm",
             "postings": P, "ms": t, "achieved": alg / t / 1e6, "peak": 8000.0, "unit": "GB/s",
             "frac": alg / t / 1e6 / 8000.0, "algorithmic_bytes": alg,
-            "note": "level-13 ids vary in bits 35..63 only: 4 digit passes of <= 8 bits"}
+            "passes": passes, "physical_bytes_per_pass": phys,
+            "per_pass_physical_GBs": phys / (t / passes) / 1e6,
+            "per_pass_physical_frac": phys / (t / passes) / 1e6 / 8000.0,
+            "note": "level-13 ids vary in bits 35..63 only: 4 digit passes of <= 8 bits; the 24-B model counts one "
+                    "read + one write of each posting, each pass moves 32 B of it"}
 
 
 def touched_postings(ctx, D, index, cells):
@@ -991,7 +1087,7 @@ def index_info(ctx, index):
                      "dcap_us"], [x.value for x in v]))
 
 
-def pmc_traffic(kernel, nq, ni):
+def pmc_traffic(kernel, nq, ni, world=1, mode="replica"):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
     summary (tools/pmc_summary.py --json; FETCH_SIZE x2 + WRITE_SIZE, the
     gfx950 correction of MI355X_MICROARCH.md s HBM), if one exists for this
@@ -1002,8 +1098,16 @@ def pmc_traffic(kernel, nq, ni):
             d = json.load(f)
     except (OSError, ValueError):
         return None
+    if d.get("queries") != nq or d.get("intents") != ni:
+        return None
+    if mode == "sharded" and world > 1:
+        # a shard's k_join (rank 0's cell range, the queries routed to it),
+        # profiled per world size in a same-device rehearsal
+        d = d.get("sharded", {}).get(str(world))
+        if not d:
+            return None
     k = d.get("kernels", {}).get(kernel)
-    if not k or d.get("queries") != nq or d.get("intents") != ni:
+    if not k:
         return None
     return {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": d.get("source", path)}
 
@@ -1180,42 +1284,49 @@ def cpu_threads(args):
 AUTO_CPU_SAMPLE = {0: None, 1: None, 2: None, 3: None, 4: 20000}
 
 
-def cpu_baseline(args, ctx, intents, ia, queries, qa, now, intent_csr_fn, g_cells, g_pairs):
+def cpu_baseline(args, rank, n, intents, ia, queries, qa, now, intent_csr_fn, g_offs, g_c, gq, ge):
     """The CPU restatement (oracle/, kind "port": pthreads over the process's
-    CPU share) timed on the same step: cover the sample's query footprints and
-    search them against the intents' posting list (built untimed; for the
-    largest airspaces only the intents sharing a cell with the sample, which
-    are the only ones that can pair with it).  The sample is the first n
-    queries of the batch; their oracle cell sets and pair set are compared
-    with the GPU step's (every cell and every pair of the sampled queries; the
-    whole batch for configs[0]..[3])."""
-    from dss_amd import device as D
+    CPU share) on the first n queries of the rank's batch: cover them, search
+    them against the intents' posting list (built untimed; for the largest
+    airspaces, and on ranks other than 0, only the intents sharing a cell
+    with the sample, which are the only ones that can pair with it), and
+    compare every cell and every pair with the GPU step's (g_offs / g_c: the
+    GPU covering of those queries, gq / ge: the GPU pairs with q < n).  Rank
+    0 also reports the timing as the baseline: queries/s on `cores` threads,
+    the one-thread rate and a per-request sample."""
     from oracle import oracle as O
     O.build()
-    n = args.cpu_sample
-    if n < 0:
-        auto = AUTO_CPU_SAMPLE.get(args.config)
-        n = queries.n if auto is None else auto
-    n = min(n, queries.n)
     sub = queries if n == queries.n else queries.subset(np.arange(n))
     th = cpu_threads(args)
     t0 = time.perf_counter()
     qo, qc, _, _ = O.cover_batch(sub.kind, sub.voff, sub.lat, sub.lng, sub.radius_m, nthreads=th)
     t1 = time.perf_counter()
-    stage(f"cpu baseline: {n} queries covered in {t1 - t0:.1f}s; intents for the oracle index")
-    i_offs, i_cells, ents = intent_csr_fn(qc)
-    stage(f"cpu baseline: oracle index over {len(ents)} intents, {len(i_cells)} postings")
+    stage(f"oracle: {n} queries covered in {t1 - t0:.1f}s; intents for the oracle index")
+    i_offs, i_cells, ents = intent_csr_fn(qc, rank != 0)
+    stage(f"oracle: index over {len(ents)} intents, {len(i_cells)} postings")
     sel = lambda a: a[ents] if len(ents) != len(a) else a  # noqa: E731
     idx = O.Index(i_offs, i_cells, sel(ia.alt_lo), sel(ia.alt_hi), sel(ia.t0), sel(ia.t1))
     tlo = np.maximum(qa.t0[:n], now)
     t2 = time.perf_counter()
-    stage("cpu baseline: oracle search")
+    stage("oracle: search")
     rq, re = idx.search(qo, qc, qa.alt_lo[:n], qa.alt_hi[:n], tlo, qa.t1[:n], nthreads=th)
     t3 = time.perf_counter()
-    stage(f"cpu baseline: search {t3 - t2:.1f}s; parity")
+    stage(f"oracle: search {t3 - t2:.1f}s; parity")
     re = ents[re]
+    gk = np.sort((gq.astype(np.uint64) << np.uint64(32)) | ge.astype(np.uint64))
+    ok = (rq.astype(np.uint64) << np.uint64(32)) | re.astype(np.uint64)
+    ok.sort()
+    parity = None
+    if not args.no_verify:
+        parity = {"queries": n, "of_batch": queries.n, "cells_equal": bool(np.array_equal(g_offs, qo) and
+                                                                            np.array_equal(g_c, qc)),
+                  "pairs_equal": bool(np.array_equal(gk, ok)), "gpu_pairs": int(len(gk)), "oracle_pairs": int(len(ok)),
+                  "cells": int(len(qc)), "unique": bool(len(gk) == 0 or np.all(gk[1:] != gk[:-1]))}
+    if rank != 0 or args.cpu_sample == 0:
+        return None, parity
     # the reference's per-request shape on the CPU: one covering + one search
-    # per request, one thread (ctypes call overhead included, ~10 us)
+    # per request, one thread (ctypes call overhead included, ~10 us); the
+    # same loop gives the one-thread rate
     req_ms = []
     for k in range(min(400, n)):
         v0, v1 = int(sub.voff[k]), int(sub.voff[k + 1])
@@ -1226,28 +1337,21 @@ def cpu_baseline(args, ctx, intents, ia, queries, qa, now, intent_csr_fn, g_cell
         req_ms.append(1000.0 * (time.perf_counter() - tr))
     info = cpu_info()
     secs = (t1 - t0) + (t3 - t2)
+    one_thread = 1000.0 / float(np.mean(req_ms)) if req_ms else None
     cpu = {"value": n / secs, "unit": "queries/s", "cores": th, "kind": "port",
            "sample": f"{n} of the step's {queries.n} queries (cover + search) vs the {intents.n}-intent index"
                      + ("" if len(ents) == intents.n else f" (the {len(ents)} intents sharing a cell with the sample)"),
            "coverings_per_s": n / (t1 - t0), "seconds": secs, "cpu_model": info["model"],
            "single_request": {"requests": len(req_ms), "p50_ms": float(np.percentile(req_ms, 50)),
                               "p99_ms": float(np.percentile(req_ms, 99)), "threads": 1},
+           "one_thread_queries_per_s": one_thread,
+           "all_affinity_estimate": {"cpus": info["affinity"],
+                                     "queries_per_s_upper_bound": (n / secs) / th * info["affinity"],
+                                     "how": "the measured rate per thread x every CPU in the process's affinity mask "
+                                            "(linear scaling: an upper bound); not run, since the GPU box's pool "
+                                            "gives a process a CPU share of OMP_NUM_THREADS"},
            "nproc": info["nproc"], "affinity_cpus": info["affinity"],
            "threads_note": "threads = the process's CPU share on the GPU box (OMP_NUM_THREADS / affinity)"}
-    parity = None
-    if not args.no_verify:
-        g_offs = D.copy_back(ctx, g_cells.offs, n + 1, np.int64)
-        g_c = D.copy_back(ctx, g_cells.cells, int(g_offs[-1]), np.uint64)
-        gq = D.copy_back(ctx, g_pairs.q, int(g_pairs.n), np.uint32)
-        ge = D.copy_back(ctx, g_pairs.e, int(g_pairs.n), np.uint32)
-        keep = gq < n
-        gk = np.sort((gq[keep].astype(np.uint64) << np.uint64(32)) | ge[keep].astype(np.uint64))
-        ok = (rq.astype(np.uint64) << np.uint64(32)) | re.astype(np.uint64)
-        ok.sort()
-        parity = {"queries": n, "of_batch": queries.n, "cells_equal": bool(np.array_equal(g_offs, qo) and
-                                                                            np.array_equal(g_c, qc)),
-                  "pairs_equal": bool(np.array_equal(gk, ok)), "gpu_pairs": int(len(gk)), "oracle_pairs": int(len(ok)),
-                  "cells": int(len(qc)), "unique": bool(len(gk) == 0 or np.all(gk[1:] != gk[:-1]))}
     return cpu, parity
 
 

@@ -174,6 +174,9 @@ def load():
                                                       P(C.c_int32), P(C.c_double)]
         L.dssg_batcher_stats.argtypes = [vp, P(C.c_int64), P(C.c_int64)]
         L.dssg_sharded_search_device.argtypes = [vp, vp, vp, vp, C.c_int64, vp, vp, vp, vp, vp, vp, vp, P(Pairs)]
+        L.dssg_sharded_search_async_device.argtypes = [vp, vp, vp, vp, vp, C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp,
+                                                       P(Pairs)]
+        L.dssg_sharded_stats.argtypes = [vp, P(d), P(i64)]
         L.dssg_radix_sort_device.argtypes = [vp, C.c_int, i64, C.c_int, vp, vp, vp, vp, vp, P(d)]
         L.dssg_selftest_scan.argtypes = [vp, i64, C.c_int, P(i64), P(i64)]
         L.dssg_selftest_math.argtypes = [vp, C.c_int, i64, P(d), P(d), P(d)]

@@ -38,6 +38,8 @@ struct dssg_ctx {
     std::string last_error;
     bool timing = false;
     bool route_identity = true;  // sharded step on one rank: the batch is its own (see dssg_sharded_search_device)
+    dss::ShardStats shard_stats;  // the most recent sharded step on this context
+    hipEvent_t shard_ev[8] = {};
     double cover_ms = 0, join_ms = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // the most recent device covering's output (its buffers belong to the
@@ -223,6 +225,8 @@ void dssg_destroy(dssg_ctx *ctx)
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    for (hipEvent_t e : ctx->shard_ev)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -354,6 +358,7 @@ int dssg_cover_batch(dssg_ctx *ctx, int64_t n, const int32_t *kind, const int64_
         if (!radius_m) zeros.assign((size_t)(n > 0 ? n : 1), 0.0f);
         const float *dr = upload(ctx->d_rad, radius_m ? radius_m : zeros.data(), n, s);
         dssg_cells res;
+        ctx->cov_offs = nullptr;  // the engine's buffers are rewritten: no device search may take its cached total
         ctx->cover.run(n, dk, dv, dla, dln, dr, s, &res);
         DSS_HIP(hipMemcpyAsync(out_offs, res.offs, sizeof(int64_t) * (size_t)(n + 1), hipMemcpyDeviceToHost, s));
         if (n > 0) DSS_HIP(hipMemcpyAsync(status, res.status, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, s));
@@ -387,6 +392,7 @@ int dssg_union_volumes_device(dssg_ctx *ctx, int64_t nvol, const int64_t *d_vol_
         if (nx > 0 && (!d_kind || !d_voff || !d_lat || !d_lng || !d_radius_m || !d_has_fp || !d_alt_lo || !d_alt_hi ||
                        !d_t0 || !d_t1))
             throw dss::Error(DSSG_ERR_INVALID, "extent arrays are NULL");
+        ctx->cov_offs = nullptr;  // the union covers through this context's cover engine
         ctx->ingress.union_volumes(ctx->cover, nvol, d_vol_offs, nx, d_kind, d_voff, d_lat, d_lng, d_radius_m, d_has_fp,
                                    d_alt_lo, d_alt_hi, d_t0, d_t1, s, out);
     });
@@ -1056,10 +1062,15 @@ struct dssg_comm {
     dss::DevBuf<int64_t> d_counts;                 // allgathered count vectors
     int64_t *h_counts = nullptr;                   // pinned: their host copy
     dss::DevBuf<unsigned char> send_q, recv_q;     // fused query segments
-    dss::DevBuf<uint64_t> send_pairs, recv_pairs;  // packed pairs of the other ranks' queries
-    dss::DevBuf<uint32_t> out_q, out_e;
+    // pairs home, two buffer sets used alternately: with an exchange stream
+    // step k's pairs are still in flight while step k+1 fills the other set
+    dss::DevBuf<uint64_t> send_pairs[2], recv_pairs[2];  // packed pairs of the other ranks' queries
+    dss::DevBuf<uint32_t> out_q[2], out_e[2];
+    int flip = 0;
+    hipEvent_t ev_fill = nullptr;  // pairs packed on the step's stream -> the exchange stream may send them
     ~dssg_comm()
     {
+        if (ev_fill) (void)hipEventDestroy(ev_fill);
         if (h_counts) (void)hipHostFree(h_counts);
     }
 };
@@ -1166,6 +1177,143 @@ int dssg_comm_alltoallv_device(dssg_ctx *ctx, dssg_comm *comm, const void *d_sen
     });
 }
 
+namespace {
+
+// Phase events of an instrumented sharded step (timing on): on the step's
+// stream route | query exchange | join | pairs packed, on the exchange stream
+// the pairs' count exchange + all-to-all + split.
+enum { kShRoute0, kShRoute1, kShXq1, kShJoin1, kShPack1, kShXp0, kShXp1, kShEvents };
+
+void sharded_step(dssg_ctx *ctx, dssg_comm *cq, dssg_comm *cx, const dssg_index *shard, const uint64_t *d_part_hi,
+                  int64_t nq, const int64_t *d_q_offs, const uint64_t *d_q_cells, const float *d_q_alt_lo,
+                  const float *d_q_alt_hi, const int64_t *d_q_tlo, const int64_t *d_q_thi, hipStream_t s,
+                  hipStream_t x, dssg_pairs *out)
+{
+    const int W = cq->nranks, me = cq->rank;
+    if (cx->nranks != W || cx->rank != me) throw dss::Error(DSSG_ERR_INVALID, "sharded step: communicators differ");
+    dss::ShardStats &st = ctx->shard_stats;
+    st = dss::ShardStats{};
+    hipEvent_t *ev = ctx->shard_ev;
+    const bool timing = ctx->timing;
+    if (timing && !ev[0])
+        for (int k = 0; k < kShEvents; k++) DSS_HIP(hipEventCreate(&ev[k]));
+    auto mark = [&](int k, hipStream_t on) {
+        if (timing) DSS_HIP(hipEventRecord(ev[k], on));
+    };
+    mark(kShRoute0, s);
+    if (W == 1 && ctx->route_identity) {
+        // one part owns every cell: routing is the identity, the batch
+        // is joined as given (no copies, no collectives)
+        const int64_t nqc = d_q_offs == ctx->cov_offs && nq == ctx->cov_n ? ctx->cov_total : -1;
+        ctx->search.search(shard, nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo, d_q_thi, nullptr, s, out, nqc);
+        out->n_tagged = 0;
+        st.join_ms = -1;
+        return;
+    }
+    // (1) route this rank's queries to the parts owning their cells: one
+    // fused segment [rows | cells] per part
+    int64_t rows_n[DSSG_MAX_PARTS], cells_n[DSSG_MAX_PARTS], seg[DSSG_MAX_PARTS];
+    ctx->route.plan(nq, d_q_offs, d_q_cells, W, d_part_hi, s, rows_n, cells_n, seg);
+    int64_t so[DSSG_MAX_PARTS], stot = 0;
+    for (int p = 0; p < W; p++) {
+        so[p] = stot;
+        stot += seg[p];
+    }
+    unsigned char *sq = cq->send_q.ensure((size_t)stot + 32);
+    ctx->route.fill(nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo, d_q_thi, s, sq);
+    mark(kShRoute1, s);
+    // (2) one count exchange, one all-to-all of the segments (own segment copied)
+    int64_t mine[2 * DSSG_MAX_PARTS];
+    for (int p = 0; p < W; p++) {
+        mine[p] = rows_n[p];
+        mine[W + p] = cells_n[p];
+    }
+    const int64_t *cnt = allgather_counts(cq, mine, 2 * W, s);
+    int64_t src_rows[DSSG_MAX_PARTS], src_cells[DSSG_MAX_PARTS], rb[DSSG_MAX_PARTS], ro[DSSG_MAX_PARTS], rtot = 0;
+    int64_t ncells_recv = 0;
+    for (int p = 0; p < W; p++) {
+        src_rows[p] = cnt[(size_t)p * 2 * W + me];
+        src_cells[p] = cnt[(size_t)p * 2 * W + W + me];
+        ncells_recv += src_cells[p];
+        rb[p] = dss::route_segment_bytes(src_rows[p], src_cells[p]);
+        ro[p] = rtot;
+        rtot += rb[p];
+    }
+    unsigned char *rq = cq->recv_q.ensure((size_t)rtot + 32);
+    if (seg[me] > 0) dss::device_copy(rq + ro[me], sq + so[me], (size_t)seg[me], s);
+    alltoallv(cq, sq, so, seg, rq, ro, rb, s);
+    st.q_bytes_sent = stot - seg[me];
+    st.q_bytes_recv = rtot - rb[me];
+    // (3) the received queries against this rank's shard
+    dssg_batch batch{};
+    ctx->route.unpack(rq, W, src_rows, src_cells, s, &batch);
+    mark(kShXq1, s);
+    dssg_pairs pairs{};
+    ctx->search.search(shard, batch.n, batch.offs, batch.cells, batch.alt_lo, batch.alt_hi, batch.tlo, batch.thi,
+                       nullptr, s, &pairs);
+    mark(kShJoin1, s);
+    st.rows = batch.n;
+    st.cells = ncells_recv;
+    st.shard_pairs = pairs.n;
+    // (4) pairs home: this rank's own straight into its output, the others'
+    // packed (home-local query << 32 | entity) and all-to-all'd -- on the
+    // exchange stream x, into the buffer set not used by the previous step
+    // (whose pairs may still be in flight there)
+    int64_t pn[DSSG_MAX_PARTS];
+    ctx->route.pairs_plan(&batch, &pairs, W, me, s, pn);
+    mark(kShXp0, x);
+    const int64_t *pc = allgather_counts(cx, pn, W, x);  // waits for x: the previous step's pairs have landed
+    int64_t psb[DSSG_MAX_PARTS], pso[DSSG_MAX_PARTS], prb[DSSG_MAX_PARTS], pro[DSSG_MAX_PARTS], ps = 0, pr = 0;
+    for (int p = 0; p < W; p++) {
+        psb[p] = p == me ? 0 : pn[p] * (int64_t)sizeof(uint64_t);
+        pso[p] = ps;
+        ps += psb[p];
+        prb[p] = p == me ? 0 : pc[(size_t)p * W + me] * (int64_t)sizeof(uint64_t);
+        pro[p] = pr;
+        pr += prb[p];
+    }
+    const int64_t nself = pn[me], nrecv = pr / (int64_t)sizeof(uint64_t);
+    const int b = cx->flip;
+    cx->flip ^= 1;
+    uint64_t *spairs = cx->send_pairs[b].ensure((size_t)ps / sizeof(uint64_t) + 1);
+    uint32_t *q = cx->out_q[b].ensure((size_t)(nself + nrecv) + 1), *e = cx->out_e[b].ensure((size_t)(nself + nrecv) + 1);
+    uint64_t *rpairs = cx->recv_pairs[b].ensure((size_t)nrecv + 1);
+    ctx->route.pairs_fill(&batch, &pairs, s, spairs, q, e);
+    mark(kShPack1, s);
+    if (x != s) {
+        if (!cx->ev_fill) DSS_HIP(hipEventCreateWithFlags(&cx->ev_fill, hipEventDisableTiming));
+        DSS_HIP(hipEventRecord(cx->ev_fill, s));
+        DSS_HIP(hipStreamWaitEvent(x, cx->ev_fill, 0));
+    }
+    alltoallv(cx, spairs, pso, psb, rpairs, pro, prb, x);
+    dss::RouteEngine::split_pairs(nrecv, rpairs, q + nself, e + nself, x);
+    mark(kShXp1, x);
+    st.p_bytes_sent = ps;
+    st.p_bytes_recv = pr;
+    out->q = q;
+    out->e = e;
+    out->n = nself + nrecv;
+    out->n_tagged = 0;
+    if (timing) {
+        DSS_HIP(hipStreamSynchronize(x));
+        DSS_HIP(hipStreamSynchronize(s));
+        auto el = [&](int a, int z) {
+            float ms = 0;
+            DSS_HIP(hipEventElapsedTime(&ms, ev[a], ev[z]));
+            return (double)ms;
+        };
+        st.route_ms = el(kShRoute0, kShRoute1);
+        st.xq_ms = el(kShRoute1, kShXq1);
+        st.join_ms = el(kShXq1, kShJoin1);
+        st.pack_ms = el(kShJoin1, kShPack1);
+        st.xp_ms = el(kShXp0, kShXp1);
+        // roofline accounting: postings of the distinct cells this shard was asked for
+        st.touched = ctx->search.touched(shard, batch.n, batch.offs, batch.cells, s);
+    }
+}
+
+}  // namespace
+
 int dssg_sharded_search_device(dssg_ctx *ctx, dssg_comm *comm, const dssg_index *shard, const uint64_t *d_part_hi,
                                int64_t nq, const int64_t *d_q_offs, const uint64_t *d_q_cells,
                                const float *d_q_alt_lo, const float *d_q_alt_hi, const int64_t *d_q_tlo,
@@ -1176,76 +1324,51 @@ int dssg_sharded_search_device(dssg_ctx *ctx, dssg_comm *comm, const dssg_index 
         return DSSG_ERR_INVALID;
     return guarded(ctx, [&] {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-        const int W = comm->nranks, me = comm->rank;
-        if (W == 1 && ctx->route_identity) {
-            // one part owns every cell: routing is the identity, the batch
-            // is joined as given (no copies, no collectives)
-            ctx->search.search(shard, nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo, d_q_thi, nullptr, s, out);
-            out->n_tagged = 0;
-            return;
-        }
-        // (1) route this rank's queries to the parts owning their cells: one
-        // fused segment [rows | cells] per part
-        int64_t rows_n[DSSG_MAX_PARTS], cells_n[DSSG_MAX_PARTS], seg[DSSG_MAX_PARTS];
-        ctx->route.plan(nq, d_q_offs, d_q_cells, W, d_part_hi, s, rows_n, cells_n, seg);
-        int64_t so[DSSG_MAX_PARTS], stot = 0;
-        for (int p = 0; p < W; p++) {
-            so[p] = stot;
-            stot += seg[p];
-        }
-        unsigned char *sq = comm->send_q.ensure((size_t)stot + 32);
-        ctx->route.fill(nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo, d_q_thi, s, sq);
-        // (2) one count exchange, one all-to-all of the segments (own segment copied)
-        int64_t mine[2 * DSSG_MAX_PARTS];
-        for (int p = 0; p < W; p++) {
-            mine[p] = rows_n[p];
-            mine[W + p] = cells_n[p];
-        }
-        const int64_t *cnt = allgather_counts(comm, mine, 2 * W, s);
-        int64_t src_rows[DSSG_MAX_PARTS], src_cells[DSSG_MAX_PARTS], rb[DSSG_MAX_PARTS], ro[DSSG_MAX_PARTS], rtot = 0;
-        for (int p = 0; p < W; p++) {
-            src_rows[p] = cnt[(size_t)p * 2 * W + me];
-            src_cells[p] = cnt[(size_t)p * 2 * W + W + me];
-            rb[p] = dss::route_segment_bytes(src_rows[p], src_cells[p]);
-            ro[p] = rtot;
-            rtot += rb[p];
-        }
-        unsigned char *rq = comm->recv_q.ensure((size_t)rtot + 32);
-        if (seg[me] > 0) dss::device_copy(rq + ro[me], sq + so[me], (size_t)seg[me], s);
-        alltoallv(comm, sq, so, seg, rq, ro, rb, s);
-        // (3) the received queries against this rank's shard
-        dssg_batch batch{};
-        ctx->route.unpack(rq, W, src_rows, src_cells, s, &batch);
-        dssg_pairs pairs{};
-        ctx->search.search(shard, batch.n, batch.offs, batch.cells, batch.alt_lo, batch.alt_hi, batch.tlo, batch.thi,
-                           nullptr, s, &pairs);
-        // (4) pairs home: this rank's own straight into its output, the
-        // others' packed (home-local query << 32 | entity) and all-to-all'd
-        int64_t pn[DSSG_MAX_PARTS];
-        ctx->route.pairs_plan(&batch, &pairs, W, me, s, pn);
-        const int64_t *pc = allgather_counts(comm, pn, W, s);
-        int64_t psb[DSSG_MAX_PARTS], pso[DSSG_MAX_PARTS], prb[DSSG_MAX_PARTS], pro[DSSG_MAX_PARTS], ps = 0, pr = 0;
-        for (int p = 0; p < W; p++) {
-            psb[p] = p == me ? 0 : pn[p] * (int64_t)sizeof(uint64_t);
-            pso[p] = ps;
-            ps += psb[p];
-            prb[p] = p == me ? 0 : pc[(size_t)p * W + me] * (int64_t)sizeof(uint64_t);
-            pro[p] = pr;
-            pr += prb[p];
-        }
-        const int64_t nself = pn[me], nrecv = pr / (int64_t)sizeof(uint64_t);
-        uint64_t *spairs = comm->send_pairs.ensure((size_t)ps / sizeof(uint64_t) + 1);
-        uint32_t *q = comm->out_q.ensure((size_t)(nself + nrecv) + 1), *e = comm->out_e.ensure((size_t)(nself + nrecv) + 1);
-        ctx->route.pairs_fill(&batch, &pairs, s, spairs, q, e);
-        uint64_t *rpairs = comm->recv_pairs.ensure((size_t)nrecv + 1);
-        alltoallv(comm, spairs, pso, psb, rpairs, pro, prb, s);
-        dss::RouteEngine::split_pairs(nrecv, rpairs, q + nself, e + nself, s);
+        sharded_step(ctx, comm, comm, shard, d_part_hi, nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo,
+                     d_q_thi, s, s, out);
         DSS_HIP(hipStreamSynchronize(s));
-        out->q = q;
-        out->e = e;
-        out->n = nself + nrecv;
-        out->n_tagged = 0;
     });
+}
+
+int dssg_sharded_search_async_device(dssg_ctx *ctx, dssg_comm *comm, dssg_comm *xcomm, const dssg_index *shard,
+                                     const uint64_t *d_part_hi, int64_t nq, const int64_t *d_q_offs,
+                                     const uint64_t *d_q_cells, const float *d_q_alt_lo, const float *d_q_alt_hi,
+                                     const int64_t *d_q_tlo, const int64_t *d_q_thi, void *stream, void *xstream,
+                                     dssg_pairs *out)
+{
+    if (!ctx || !comm || !xcomm || comm == xcomm || !xstream || !shard || !d_part_hi || !out || nq < 0 ||
+        (nq > 0 && (!d_q_offs || !d_q_cells || !d_q_alt_lo || !d_q_alt_hi || !d_q_tlo || !d_q_thi)))
+        return DSSG_ERR_INVALID;
+    return guarded(ctx, [&] {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        if ((hipStream_t)xstream == s) throw dss::Error(DSSG_ERR_INVALID, "the exchange stream must differ");
+        sharded_step(ctx, comm, xcomm, shard, d_part_hi, nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo,
+                     d_q_thi, s, (hipStream_t)xstream, out);
+    });
+}
+
+int dssg_sharded_stats(dssg_ctx *ctx, double *ms, int64_t *counts)
+{
+    if (!ctx) return DSSG_ERR_INVALID;
+    const dss::ShardStats &st = ctx->shard_stats;
+    if (ms) {
+        ms[0] = st.route_ms;
+        ms[1] = st.xq_ms;
+        ms[2] = st.join_ms;
+        ms[3] = st.pack_ms;
+        ms[4] = st.xp_ms;
+    }
+    if (counts) {
+        counts[0] = st.q_bytes_sent;
+        counts[1] = st.q_bytes_recv;
+        counts[2] = st.p_bytes_sent;
+        counts[3] = st.p_bytes_recv;
+        counts[4] = st.rows;
+        counts[5] = st.shard_pairs;
+        counts[6] = st.cells;
+        counts[7] = st.touched;
+    }
+    return DSSG_OK;
 }
 
 /* ======================================================================
@@ -1365,6 +1488,7 @@ struct dssg_batcher {
             DSS_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s));
             dssg_cells cov;
             const auto t0 = std::chrono::steady_clock::now();
+            w.ctx->cov_offs = nullptr;
             w.ctx->cover.run(n, (const int32_t *)(d + o_kind), (const int64_t *)(d + o_voff), (const double *)(d + o_lat),
                              (const double *)(d + o_lng), (const float *)(d + o_rad), s, &cov);
             // status and area ride along with the pairs' copy (pinned, no extra sync)

@@ -257,6 +257,7 @@ void RouteEngine::plan(int64_t nq, const int64_t *offs, const uint64_t *cells, i
     // to 32 bytes; the fill kernel's bases are the segment's row and cell
     // positions in QRow / uint64 units of the one send buffer
     int64_t *hb = reinterpret_cast<int64_t *>(host_words() + 2 * kMaxParts);
+    wait_h2d(h2d_plan_);
     int64_t off = 0, Cn = 0;
     for (int d = 0; d < np; d++) {
         row_counts[d] = (int64_t)h[d];
@@ -270,6 +271,7 @@ void RouteEngine::plan(int64_t nq, const int64_t *offs, const uint64_t *cells, i
     if (Cn >= (int64_t)kCellMask) throw Error(DSSG_ERR_INVALID, "route: more than 2^40 routed cells");
     int64_t *bases = base_.ensure(2 * kMaxParts);
     DSS_HIP(hipMemcpyAsync(bases, hb, sizeof(int64_t) * 2 * kMaxParts, hipMemcpyHostToDevice, s));
+    mark_h2d(h2d_plan_, s);
     plan_nq_ = nq;
     plan_np_ = np;
     plan_offs_ = offs;
@@ -349,6 +351,7 @@ void RouteEngine::pairs_plan(const dssg_batch *b, const dssg_pairs *p, int np, i
     // send-buffer bases: part-major, the self part (written to its own
     // output arrays instead) taking no space
     int64_t *pb = reinterpret_cast<int64_t *>(host_words() + 5 * kMaxParts), tot = 0;
+    wait_h2d(h2d_pairs_);
     for (int d = 0; d < np; d++) {
         pb[d] = tot;
         counts[d] = (int64_t)h[d];
@@ -356,6 +359,7 @@ void RouteEngine::pairs_plan(const dssg_batch *b, const dssg_pairs *p, int np, i
     }
     int64_t *d_pb = pbase_.ensure(kMaxParts);
     DSS_HIP(hipMemcpyAsync(d_pb, pb, sizeof(int64_t) * np, hipMemcpyHostToDevice, s));
+    mark_h2d(h2d_pairs_, s);
     pplan_n_ = n;
     pplan_np_ = np;
     pplan_self_ = self_part;
@@ -387,8 +391,27 @@ unsigned long long *RouteEngine::host_words()
     return h_counts_;
 }
 
+void RouteEngine::wait_h2d(hipEvent_t &ev)
+{
+    if (ev) DSS_HIP(hipEventSynchronize(ev));
+}
+
+void RouteEngine::mark_h2d(hipEvent_t &ev, hipStream_t s)
+{
+    if (!ev) DSS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    DSS_HIP(hipEventRecord(ev, s));
+}
+
 RouteEngine::~RouteEngine()
 {
+    if (h2d_plan_) {
+        (void)hipEventSynchronize(h2d_plan_);
+        (void)hipEventDestroy(h2d_plan_);
+    }
+    if (h2d_pairs_) {
+        (void)hipEventSynchronize(h2d_pairs_);
+        (void)hipEventDestroy(h2d_pairs_);
+    }
     if (h_counts_) (void)hipHostFree(h_counts_);
 }
 

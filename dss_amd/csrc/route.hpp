@@ -18,6 +18,15 @@ static_assert(sizeof(QRow) == DSSG_ROUTE_ROW_BYTES, "QRow size vs dssgpu.h");
 // cell lists, padded to 32 bytes.
 int64_t route_segment_bytes(int64_t rows, int64_t cells);
 
+// What the most recent sharded step on a context moved and how long its
+// phases took (HIP events; timing on, else 0).  join_ms < 0: the one-rank
+// identity route (no exchange).
+struct ShardStats {
+    double route_ms = 0, xq_ms = 0, join_ms = 0, pack_ms = 0, xp_ms = 0;
+    int64_t q_bytes_sent = 0, q_bytes_recv = 0, p_bytes_sent = 0, p_bytes_recv = 0, rows = 0, shard_pairs = 0;
+    int64_t cells = 0, touched = 0;  // routed query cells joined here; postings of their distinct cells (timing on)
+};
+
 class RouteEngine {
    public:
     static constexpr int kMaxParts = DSSG_MAX_PARTS;
@@ -51,7 +60,12 @@ class RouteEngine {
     DevBuf<uint64_t> cells_;
     DevBuf<float> alo_, ahi_;
     DevBuf<uint32_t> home_, qid_;
+    // an H2D copy of host-written bases may still be pending (on any stream)
+    // when the next plan rewrites them: the host waits for it first
+    void wait_h2d(hipEvent_t &ev);
+    void mark_h2d(hipEvent_t &ev, hipStream_t s);
     unsigned long long *h_counts_ = nullptr;  // pinned
+    hipEvent_t h2d_plan_ = nullptr, h2d_pairs_ = nullptr;
     int64_t plan_nq_ = 0, pplan_n_ = 0, pplan_self_n_ = 0;
     int plan_np_ = 0, pplan_np_ = 0, pplan_self_ = -1;
     const int64_t *plan_offs_ = nullptr;

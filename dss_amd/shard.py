@@ -269,6 +269,9 @@ class ShardedSearch:
         own = (self_q[:pn[me]].to(torch.int64) << 32) | (self_e[:pn[me]].to(torch.int64) & 0xFFFFFFFF)
         out = torch.cat([own, got])
         self._mark("exchange_pairs", t, timed)
+        self.last_bytes = {"query_bytes_sent": 8 * (sum(seg_words) - seg_words[me]),
+                           "query_bytes_recv": 8 * (int(recv.numel()) - seg_words[me]) if sum(src_rows) else 0,
+                           "pair_bytes_sent": 8 * (sum(pn) - pn[me]), "pair_bytes_recv": 8 * int(got.numel())}
         self.last_rows = int(batch.n)
         self.last_recv_cells = recv[:0]
         self.last_recv_ncells = sum(src_cells)
@@ -315,13 +318,24 @@ class NativeShardedSearch:
     """`ShardedSearch` with the whole step in the library
     (dssg_sharded_search_device: route, RCCL all-to-alls, shard join, pairs
     home).  step() returns this rank's (query, entity) pairs as device
-    pointers (a _lib.Pairs, valid until the next step)."""
+    pointers (a _lib.Pairs, valid until the next step).
 
-    def __init__(self, ctx, comm: NativeComm, index, ranges: Sequence[Tuple[int, int]]):
+    With `xcomm` (a second NativeComm) and `xstream` (a torch stream) the
+    step is dssg_sharded_search_async_device: the pairs' trip home runs on
+    xstream over xcomm, overlapping the next step's routing and join; the
+    returned pairs are complete once xstream's queued work has run and stay
+    valid until the second next step.  Every collective of a rank must be
+    issued by one host thread (dssgpu.h)."""
+
+    def __init__(self, ctx, comm: NativeComm, index, ranges: Sequence[Tuple[int, int]], xcomm: NativeComm = None,
+                 xstream=None):
         import torch
         if len(ranges) != comm.nranks:
             raise ValueError("one cell range per rank")
+        if (xcomm is None) != (xstream is None):
+            raise ValueError("xcomm and xstream go together")
         self.ctx, self.comm, self.index = ctx, comm, index
+        self.xcomm, self.xstream = xcomm, xstream
         self.part_hi = torch.as_tensor(part_his(ranges).view(np.int64),
                                        device=torch.device("cuda", torch.cuda.current_device()))
 
@@ -329,8 +343,28 @@ class NativeShardedSearch:
         from . import _lib, device as D
         ctx = self.ctx
         out = _lib.Pairs()
-        ctx.check(ctx.L.dssg_sharded_search_device(ctx.h, self.comm.h, self.index, D._ptr(self.part_hi), nq,
-                                                   C.c_void_p(offs_ptr), C.c_void_p(cells_ptr), D._ptr(alo),
-                                                   D._ptr(ahi), D._ptr(tlo), D._ptr(thi), D._stream_ptr(),
-                                                   C.byref(out)))
+        args = (D._ptr(self.part_hi), nq, C.c_void_p(offs_ptr), C.c_void_p(cells_ptr), D._ptr(alo), D._ptr(ahi),
+                D._ptr(tlo), D._ptr(thi), D._stream_ptr())
+        if self.xcomm is None:
+            ctx.check(ctx.L.dssg_sharded_search_device(ctx.h, self.comm.h, self.index, *args, C.byref(out)))
+        else:
+            ctx.check(ctx.L.dssg_sharded_search_async_device(ctx.h, self.comm.h, self.xcomm.h, self.index, *args,
+                                                             C.c_void_p(self.xstream.cuda_stream), C.byref(out)))
         return out
+
+    def stats(self):
+        """dssg_sharded_stats of the most recent step on this context: phase
+        ms (route, exchange_queries, join, route_pairs, exchange_pairs; timing
+        on) and the bytes / rows / pairs it moved."""
+        ms = (C.c_double * 5)()
+        cnt = (C.c_int64 * 8)()
+        self.ctx.check(self.ctx.L.dssg_sharded_stats(self.ctx.h, ms, cnt))
+        names = ["route", "exchange_queries", "join", "route_pairs", "exchange_pairs"]
+        keys = ["query_bytes_sent", "query_bytes_recv", "pair_bytes_sent", "pair_bytes_recv", "rows", "shard_pairs",
+                "cells", "touched"]
+        return dict(zip(names, list(ms))), dict(zip(keys, [int(v) for v in cnt]))
+
+    def close(self):
+        self.comm.close()
+        if self.xcomm is not None:
+            self.xcomm.close()

@@ -86,11 +86,20 @@ const (
 	timeNullStored = math.MinInt64 // DSSG_TIME_NULL_END: a stored ends_at NULL never matches
 )
 
+// usOf is a time as CockroachDB stores and compares a TIMESTAMPTZ: rounded
+// to the microsecond (tree.MakeDTimestampTZ rounds with time.Round, half
+// up), as int64 microseconds since the Unix epoch.  Every time that reaches
+// the mirrors -- query bounds, now, stored rows -- goes through it, so a
+// bound within 500 ns of a stored value compares as it does in SQL.
+func usOf(t time.Time) int64 {
+	return t.Round(time.Microsecond).UnixNano() / 1000
+}
+
 func usOrNull(t *time.Time, null int64) int64 {
 	if t == nil {
 		return null
 	}
-	return t.UnixNano() / 1000
+	return usOf(*t)
 }
 
 func altOr(a *float32, null float32) float32 {

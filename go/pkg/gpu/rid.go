@@ -30,6 +30,16 @@ type RIDTransactor struct {
 
 	isas, subs *Mirror
 	mu         sync.RWMutex
+	// writeMu serialises the writers (as SCDTransactor.writeMu does): every
+	// write and every notification fan-out read of the subscriptions mirror
+	// runs under it, from before the write / read to the mirrors' apply, so
+	// a subscription committed to CRDB is on the mirror before any later
+	// fan-out reads it.  Autocommit methods hold it for their one statement;
+	// a transaction run by InTxnRetrier from its first write or fan-out until
+	// its commit is applied.  (A transaction must not call the transactor's
+	// autocommit methods after its own first write: the reference's
+	// application never does -- InsertISA's transaction calls only those.)
+	writeMu    sync.Mutex
 	isaRows    map[dssmodels.ID]*ridmodels.IdentificationServiceArea
 	subRows    map[dssmodels.ID]*ridmodels.Subscription
 	invalid    int32 // atomic: 1 after a failed apply of committed writes (searches then run on CRDB)
@@ -132,9 +142,11 @@ func (t *RIDTransactor) apply(w *ridWrites) error {
 // mirrored once the inner retrier reports the transaction committed.
 func (t *RIDTransactor) InTxnRetrier(ctx context.Context, f func(repo repos.Repository) error) error {
 	var w *ridWrites
+	lk := &txLock{mu: &t.writeMu}
+	defer lk.unlock() // after the apply below
 	err := t.Transactor.InTxnRetrier(ctx, func(repo repos.Repository) error {
 		w = newRIDWrites() // a retried attempt starts over
-		return f(&ridRepo{Repository: repo, w: w, t: t})
+		return f(&ridRepo{Repository: repo, w: w, t: t, lk: lk})
 	})
 	if err != nil || w == nil {
 		return err
@@ -143,9 +155,32 @@ func (t *RIDTransactor) InTxnRetrier(ctx context.Context, f func(repo repos.Repo
 	return nil
 }
 
+// txLock is a transaction's hold on the write lock: taken once, at its first
+// write or fan-out read, released after its commit's apply.
+type txLock struct {
+	mu     *sync.Mutex
+	locked bool
+}
+
+func (l *txLock) lock() {
+	if !l.locked {
+		l.mu.Lock()
+		l.locked = true
+	}
+}
+
+func (l *txLock) unlock() {
+	if l.locked {
+		l.locked = false
+		l.mu.Unlock()
+	}
+}
+
 // ---- the transactor's own (autocommit) repository methods ---------------
 
 func (t *RIDTransactor) InsertISA(ctx context.Context, isa *ridmodels.IdentificationServiceArea) (*ridmodels.IdentificationServiceArea, error) {
+	t.writeMu.Lock()
+	defer t.writeMu.Unlock()
 	res, err := t.Transactor.InsertISA(ctx, isa)
 	if err == nil && res != nil {
 		w := newRIDWrites()
@@ -156,6 +191,8 @@ func (t *RIDTransactor) InsertISA(ctx context.Context, isa *ridmodels.Identifica
 }
 
 func (t *RIDTransactor) UpdateISA(ctx context.Context, isa *ridmodels.IdentificationServiceArea) (*ridmodels.IdentificationServiceArea, error) {
+	t.writeMu.Lock()
+	defer t.writeMu.Unlock()
 	res, err := t.Transactor.UpdateISA(ctx, isa)
 	if err == nil && res != nil {
 		w := newRIDWrites()
@@ -166,6 +203,8 @@ func (t *RIDTransactor) UpdateISA(ctx context.Context, isa *ridmodels.Identifica
 }
 
 func (t *RIDTransactor) DeleteISA(ctx context.Context, isa *ridmodels.IdentificationServiceArea) (*ridmodels.IdentificationServiceArea, error) {
+	t.writeMu.Lock()
+	defer t.writeMu.Unlock()
 	res, err := t.Transactor.DeleteISA(ctx, isa)
 	if err == nil {
 		w := newRIDWrites()
@@ -176,6 +215,8 @@ func (t *RIDTransactor) DeleteISA(ctx context.Context, isa *ridmodels.Identifica
 }
 
 func (t *RIDTransactor) InsertSubscription(ctx context.Context, sub *ridmodels.Subscription) (*ridmodels.Subscription, error) {
+	t.writeMu.Lock()
+	defer t.writeMu.Unlock()
 	res, err := t.Transactor.InsertSubscription(ctx, sub)
 	if err == nil && res != nil {
 		w := newRIDWrites()
@@ -186,6 +227,8 @@ func (t *RIDTransactor) InsertSubscription(ctx context.Context, sub *ridmodels.S
 }
 
 func (t *RIDTransactor) UpdateSubscription(ctx context.Context, sub *ridmodels.Subscription) (*ridmodels.Subscription, error) {
+	t.writeMu.Lock()
+	defer t.writeMu.Unlock()
 	res, err := t.Transactor.UpdateSubscription(ctx, sub)
 	if err == nil && res != nil {
 		w := newRIDWrites()
@@ -196,6 +239,8 @@ func (t *RIDTransactor) UpdateSubscription(ctx context.Context, sub *ridmodels.S
 }
 
 func (t *RIDTransactor) DeleteSubscription(ctx context.Context, sub *ridmodels.Subscription) (*ridmodels.Subscription, error) {
+	t.writeMu.Lock()
+	defer t.writeMu.Unlock()
 	res, err := t.Transactor.DeleteSubscription(ctx, sub)
 	if err == nil {
 		w := newRIDWrites()
@@ -222,7 +267,7 @@ func (t *RIDTransactor) notifyIDs(cells s2.CellUnion, w *ridWrites) (ids []dssmo
 	if len(cells) == 0 {
 		return nil, true, nil // cells && '{}' holds for no row
 	}
-	q := Query{Cells: cells, AltLo: negInf, AltHi: posInf, TLo: t.Now().UnixNano() / 1000, THi: timeNullEndQ}
+	q := Query{Cells: cells, AltLo: negInf, AltHi: posInf, TLo: usOf(t.Now()), THi: timeNullEndQ}
 	t.mu.RLock()
 	keys, err := t.subs.Search([]Query{q})
 	t.mu.RUnlock()
@@ -253,6 +298,8 @@ func (t *RIDTransactor) notifyIDs(cells s2.CellUnion, w *ridWrites) (ids []dssmo
 // RETURNING of their counters (UpdateNotificationIdxsByIDs, patch 0002).
 // The returned rows refresh the cache.
 func (t *RIDTransactor) UpdateNotificationIdxsInCells(ctx context.Context, cells s2.CellUnion) ([]*ridmodels.Subscription, error) {
+	t.writeMu.Lock()
+	defer t.writeMu.Unlock()
 	var res []*ridmodels.Subscription
 	var err error
 	ids, ok, err := t.notifyIDs(cells, nil)
@@ -286,7 +333,7 @@ func (t *RIDTransactor) MaxSubscriptionCountInCellsByOwner(ctx context.Context, 
 	}
 	t.mu.RLock()
 	defer t.mu.RUnlock()
-	return t.subs.MaxCount(cells, owner.String(), t.Now().UnixNano()/1000)
+	return t.subs.MaxCount(cells, owner.String(), usOf(t.Now()))
 }
 
 // SearchISAs replaces (*ISAStore).SearchISAs
@@ -302,7 +349,7 @@ func (t *RIDTransactor) SearchISAs(ctx context.Context, cells s2.CellUnion, earl
 	if t.Invalid() {
 		return t.Transactor.SearchISAs(ctx, cells, earliest, latest)
 	}
-	q := Query{Cells: cells, AltLo: negInf, AltHi: posInf, TLo: earliest.UnixNano() / 1000,
+	q := Query{Cells: cells, AltLo: negInf, AltHi: posInf, TLo: usOf(*earliest),
 		THi: usOrNull(latest, timeNullEndQ)}
 	t.mu.RLock() // across the search and the lookup: no apply lands in between
 	defer t.mu.RUnlock()
@@ -324,7 +371,7 @@ func (t *RIDTransactor) searchSubs(cells s2.CellUnion, owner string) ([]*ridmode
 	if len(cells) == 0 {
 		return nil, dsserr.BadRequest("no location provided")
 	}
-	q := Query{Cells: cells, AltLo: negInf, AltHi: posInf, TLo: t.Now().UnixNano() / 1000, THi: timeNullEndQ,
+	q := Query{Cells: cells, AltLo: negInf, AltHi: posInf, TLo: usOf(t.Now()), THi: timeNullEndQ,
 		Owner: owner}
 	t.mu.RLock() // across the search and the lookup: no apply lands in between
 	defer t.mu.RUnlock()
@@ -364,11 +411,13 @@ func (t *RIDTransactor) SearchSubscriptionsByOwner(ctx context.Context, cells s2
 // transaction, with writes recorded for the mirrors.
 type ridRepo struct {
 	repos.Repository
-	w *ridWrites
-	t *RIDTransactor
+	w  *ridWrites
+	t  *RIDTransactor
+	lk *txLock
 }
 
 func (r *ridRepo) InsertISA(ctx context.Context, isa *ridmodels.IdentificationServiceArea) (*ridmodels.IdentificationServiceArea, error) {
+	r.lk.lock()
 	res, err := r.Repository.InsertISA(ctx, isa)
 	if err == nil && res != nil {
 		r.w.isas[res.ID] = res
@@ -377,6 +426,7 @@ func (r *ridRepo) InsertISA(ctx context.Context, isa *ridmodels.IdentificationSe
 }
 
 func (r *ridRepo) UpdateISA(ctx context.Context, isa *ridmodels.IdentificationServiceArea) (*ridmodels.IdentificationServiceArea, error) {
+	r.lk.lock()
 	res, err := r.Repository.UpdateISA(ctx, isa)
 	if err == nil && res != nil {
 		r.w.isas[res.ID] = res
@@ -385,6 +435,7 @@ func (r *ridRepo) UpdateISA(ctx context.Context, isa *ridmodels.IdentificationSe
 }
 
 func (r *ridRepo) DeleteISA(ctx context.Context, isa *ridmodels.IdentificationServiceArea) (*ridmodels.IdentificationServiceArea, error) {
+	r.lk.lock()
 	res, err := r.Repository.DeleteISA(ctx, isa)
 	if err == nil {
 		r.w.isas[isa.ID] = nil
@@ -393,6 +444,7 @@ func (r *ridRepo) DeleteISA(ctx context.Context, isa *ridmodels.IdentificationSe
 }
 
 func (r *ridRepo) InsertSubscription(ctx context.Context, sub *ridmodels.Subscription) (*ridmodels.Subscription, error) {
+	r.lk.lock()
 	res, err := r.Repository.InsertSubscription(ctx, sub)
 	if err == nil && res != nil {
 		r.w.subs[res.ID] = res
@@ -401,6 +453,7 @@ func (r *ridRepo) InsertSubscription(ctx context.Context, sub *ridmodels.Subscri
 }
 
 func (r *ridRepo) UpdateSubscription(ctx context.Context, sub *ridmodels.Subscription) (*ridmodels.Subscription, error) {
+	r.lk.lock()
 	res, err := r.Repository.UpdateSubscription(ctx, sub)
 	if err == nil && res != nil {
 		r.w.subs[res.ID] = res
@@ -409,6 +462,7 @@ func (r *ridRepo) UpdateSubscription(ctx context.Context, sub *ridmodels.Subscri
 }
 
 func (r *ridRepo) DeleteSubscription(ctx context.Context, sub *ridmodels.Subscription) (*ridmodels.Subscription, error) {
+	r.lk.lock()
 	res, err := r.Repository.DeleteSubscription(ctx, sub)
 	if err == nil {
 		r.w.subs[sub.ID] = nil
@@ -421,6 +475,7 @@ func (r *ridRepo) DeleteSubscription(ctx context.Context, sub *ridmodels.Subscri
 // with this transaction's own subscription writes overlaid, the UPDATE ...
 // RETURNING on the transaction.
 func (r *ridRepo) UpdateNotificationIdxsInCells(ctx context.Context, cells s2.CellUnion) ([]*ridmodels.Subscription, error) {
+	r.lk.lock()
 	var res []*ridmodels.Subscription
 	ids, ok, err := r.t.notifyIDs(cells, r.w)
 	if err != nil {

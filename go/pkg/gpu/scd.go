@@ -31,16 +31,23 @@ import (
 //     has written, plus those of its written rows that match.
 // A transaction's writes reach the mirrors when it commits.
 //
-// Serialisation of the conflict check.  In the reference the conflict search
-// is a SQL read inside a SERIALIZABLE transaction, so CRDB aborts one of two
-// concurrent upserts whose volumes overlap.  A mirror read registers nothing
-// with CRDB, so a transaction that runs a conflict search on the mirror takes
-// the transactor's write lock first and holds it until its commit has been
-// applied to the mirrors (or it rolls back): the next conflict search waits
-// for it and sees its operation.  The mirrors see only this process's writes
-// (single writer per CRDB cluster, INTEGRATION.md); if applying a committed
-// transaction to them fails, they are marked invalid and every search goes
-// to CRDB from then on.
+// Serialisation of the write path.  In the reference the conflict search and
+// the notification fan-out are SQL reads inside SERIALIZABLE transactions, so
+// CRDB aborts one of two concurrent transactions whose reads and writes
+// overlap: of an operation upsert and a subscription upsert that cover the
+// same cells, either the operation's fan-out sees the subscription or the
+// subscription's own operation search (subscriptions.go:416) sees the
+// operation.  A mirror read registers nothing with CRDB, so every writing
+// transaction takes the transactor's write lock before its first write or
+// write-path mirror search (conflict search, notification fan-out) and holds
+// it until its commit has been applied to the mirrors (or it rolls back):
+// writers run one at a time, each seeing every earlier writer's rows.  No
+// writer waits for the lock while holding CRDB write intents (it takes the
+// lock before its first write), so the lock cannot deadlock against CRDB's
+// own locks.  Read-only searches do not take it.  The mirrors see only this
+// process's writes (single writer per CRDB cluster, INTEGRATION.md); if
+// applying a committed transaction to them fails, they are marked invalid
+// and every search goes to CRDB from then on.
 type SCDTransactor struct {
 	Inner scdstore.Transactor
 	// Now is the store clock (the reference's cockroach.DefaultClock).
@@ -48,7 +55,7 @@ type SCDTransactor struct {
 
 	ops, subs *Mirror
 	mu        sync.RWMutex
-	writeMu   sync.Mutex // held by a transaction from its first mirror conflict search to its commit's apply
+	writeMu   sync.Mutex // held by a writing transaction from its first write / write-path search to its commit's apply
 	opRows    map[scdmodels.ID]*scdmodels.Operation
 	subRows   map[scdmodels.ID]*scdmodels.Subscription
 	invalid   int32 // atomic: 1 after a failed apply of a committed transaction
@@ -139,7 +146,7 @@ type scdTx struct {
 	t      *SCDTransactor
 	ops    map[scdmodels.ID]*scdmodels.Operation
 	subs   map[scdmodels.ID]*scdmodels.Subscription
-	locked bool // holds t.writeMu (a mirror conflict search ran)
+	locked bool // holds t.writeMu (it wrote, or ran a write-path search)
 }
 
 // hookable is the reference store with the hooks of
@@ -161,7 +168,7 @@ func (x *scdTx) Store() (scdstore.Store, error) {
 }
 
 // lockWrites takes the transactor's write lock once per transaction, before
-// its first conflict search on the mirror (see SCDTransactor).
+// its first write or write-path mirror search (see SCDTransactor).
 func (x *scdTx) lockWrites() {
 	if !x.locked {
 		x.t.writeMu.Lock()
@@ -246,6 +253,7 @@ func (s *scdStore) refreshSub(ctx context.Context, id scdmodels.ID, owner dssmod
 // notification ids come from the hooks installed by scdTx.Store); the
 // written row is recorded for the mirrors.
 func (s *scdStore) UpsertOperation(ctx context.Context, op *scdmodels.Operation, key []scdmodels.OVN) (*scdmodels.Operation, []*scdmodels.Subscription, error) {
+	s.tx.lockWrites()
 	res, subs, err := s.Store.UpsertOperation(ctx, op, key)
 	if err == nil && res != nil {
 		s.tx.ops[res.ID] = res
@@ -273,8 +281,11 @@ func (s *scdStore) conflicts(ctx context.Context, op *scdmodels.Operation) ([]*s
 // (subscriptions.go:131-152) on the subscriptions mirror: the subscriptions
 // sharing a cell with cells and unexpired (the UPDATE that follows in SQL
 // keeps only ends_at >= now), with this transaction's own subscription
-// writes overlaid.
+// writes overlaid.  The transaction holds the write lock (its operation
+// write came first), so no subscription can commit between this read and
+// the transaction's own commit unseen.
 func (s *scdStore) notificationIDs(ctx context.Context, cells []int64) ([]scdmodels.ID, error) {
+	s.tx.lockWrites()
 	if len(cells) == 0 {
 		return nil, nil // cell_id = ANY('{}'): no rows
 	}
@@ -283,7 +294,7 @@ func (s *scdStore) notificationIDs(ctx context.Context, cells []int64) ([]scdmod
 		cu[i] = s2.CellID(uint64(c))
 	}
 	t := s.tx.t
-	q := Query{Cells: cu, AltLo: negInf, AltHi: posInf, TLo: t.Now().UnixNano() / 1000, THi: timeNullEndQ}
+	q := Query{Cells: cu, AltLo: negInf, AltHi: posInf, TLo: usOf(t.Now()), THi: timeNullEndQ}
 	t.mu.RLock()
 	keys, err := t.subs.Search([]Query{q})
 	t.mu.RUnlock()
@@ -305,6 +316,7 @@ func (s *scdStore) notificationIDs(ctx context.Context, cells []int64) ([]scdmod
 }
 
 func (s *scdStore) DeleteOperation(ctx context.Context, id scdmodels.ID, owner dssmodels.Owner) (*scdmodels.Operation, []*scdmodels.Subscription, error) {
+	s.tx.lockWrites()
 	res, subs, err := s.Store.DeleteOperation(ctx, id, owner)
 	if err == nil {
 		s.tx.ops[id] = nil
@@ -315,7 +327,11 @@ func (s *scdStore) DeleteOperation(ctx context.Context, id scdmodels.ID, owner d
 	return res, subs, err
 }
 
+// UpsertSubscription writes under the write lock: its own operation search
+// (SQL, subscriptions.go:416) then sees every operation committed before it,
+// and every later operation's fan-out sees this subscription.
 func (s *scdStore) UpsertSubscription(ctx context.Context, sub *scdmodels.Subscription) (*scdmodels.Subscription, []*scdmodels.Operation, error) {
+	s.tx.lockWrites()
 	res, ops, err := s.Store.UpsertSubscription(ctx, sub)
 	if err == nil && res != nil {
 		s.tx.subs[res.ID] = res
@@ -324,6 +340,7 @@ func (s *scdStore) UpsertSubscription(ctx context.Context, sub *scdmodels.Subscr
 }
 
 func (s *scdStore) DeleteSubscription(ctx context.Context, id scdmodels.ID, owner dssmodels.Owner, version scdmodels.Version) (*scdmodels.Subscription, error) {
+	s.tx.lockWrites()
 	res, err := s.Store.DeleteSubscription(ctx, id, owner, version)
 	if err == nil {
 		s.tx.subs[id] = nil
@@ -335,9 +352,9 @@ func (s *scdStore) DeleteSubscription(ctx context.Context, id scdmodels.ID, owne
 // mirror query: tlo = max(start, now) (COALESCE(ends_at >= start) AND
 // ends_at >= now), NULL end -> open.
 func opQuery(cells s2.CellUnion, lo, hi *float32, start, end *time.Time, now time.Time) Query {
-	tlo := now.UnixNano() / 1000
+	tlo := usOf(now)
 	if start != nil {
-		if st := start.UnixNano() / 1000; st > tlo {
+		if st := usOf(*start); st > tlo {
 			tlo = st
 		}
 	}

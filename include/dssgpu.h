@@ -21,7 +21,12 @@
  *   - cells are uint64 S2 CellIDs (level 13 on every covering output); the
  *     store's INT64 columns are the same bits reinterpreted (quirk Q12);
  *   - times are int64 microseconds since the Unix epoch (CRDB TIMESTAMPTZ
- *     resolution, quirk Q19); altitudes float32 metres (REAL columns, Q20);
+ *     resolution, quirk Q19); the caller converts a finer time the way CRDB
+ *     does, rounding to the nearest microsecond, half up (Go:
+ *     t.Round(time.Microsecond), as go/pkg/gpu's usOf), for query bounds,
+ *     `now` and stored rows alike -- truncation would disagree with SQL for
+ *     a sub-microsecond remainder >= 500 ns; altitudes float32 metres (REAL
+ *     columns, Q20);
  *   - NULLs: stored/query NULL altitude -> -INFINITY (lower) / +INFINITY
  *     (upper); stored NULL starts_at -> DSSG_TIME_NULL_START; stored NULL
  *     ends_at -> DSSG_TIME_NULL_END (such a row never matches, Q9); query
@@ -361,10 +366,30 @@ int dssg_unpack_pairs_device(dssg_ctx *ctx, int64_t n, const uint64_t *d_in, uin
  * given (dssg_set_tuning "route_identity" = 0 forces the general path).
  * Output: this rank's pairs (query index in its own batch, entity), each
  * exactly once, in device memory owned by the communicator or the context
- * until the next call on either.  Collective: every rank calls it; several
- * communicators (one per pipeline thread, each with its own context and
- * stream) may run concurrently, each issuing its calls in the same order on
- * every rank. */
+ * until the next call on either.  Collective: every rank calls it, in the
+ * same order.  Collectives of different communicators issued by different
+ * host threads are NOT supported: RCCL kernels wait for their peers, so two
+ * ranks that interleave two communicators' calls differently can deadlock
+ * when those kernels share a hardware queue.  One host thread issues every
+ * collective of a rank (other threads may cover ahead: no collectives).
+ *
+ * dssg_sharded_search_async_device: the same step with the pairs' trip home
+ * on a second communicator and stream (xcomm, xstream; both distinct from
+ * comm, stream): the query exchange and the join run on `stream`, the pair
+ * counts, the pair all-to-all and the split on `xstream`, so step k's pairs
+ * travel while step k+1 routes and joins.  The output is complete once the
+ * work queued on xstream has run; it lives in one of two buffer sets of
+ * xcomm, used alternately, so it stays valid until the second next call on
+ * xcomm.  Both communicators must span the same ranks in the same order.
+ *
+ * dssg_sharded_stats: the most recent sharded step on this context --
+ * ms[5] = route, query exchange (+ unpack), join, pair packing, pair
+ * exchange (+ split), by HIP events when timing is on (dssg_set_timing;
+ * the call then waits for both streams), else 0; counts[8] = query bytes
+ * sent to / received from other ranks, pair bytes sent / received, routed
+ * rows joined here, pairs this shard produced, routed query cells joined
+ * here, postings of their distinct cells (timing on, else 0).  Either
+ * pointer may be NULL. */
 #define DSSG_COMM_ID_BYTES 128
 typedef struct dssg_comm dssg_comm;
 int dssg_comm_unique_id(uint8_t *id);
@@ -378,6 +403,12 @@ int dssg_sharded_search_device(dssg_ctx *ctx, dssg_comm *comm, const dssg_index 
                                int64_t nq, const int64_t *d_q_offs, const uint64_t *d_q_cells,
                                const float *d_q_alt_lo, const float *d_q_alt_hi, const int64_t *d_q_tlo,
                                const int64_t *d_q_thi, void *stream, dssg_pairs *out);
+int dssg_sharded_search_async_device(dssg_ctx *ctx, dssg_comm *comm, dssg_comm *xcomm, const dssg_index *shard,
+                                     const uint64_t *d_part_hi, int64_t nq, const int64_t *d_q_offs,
+                                     const uint64_t *d_q_cells, const float *d_q_alt_lo, const float *d_q_alt_hi,
+                                     const int64_t *d_q_tlo, const int64_t *d_q_thi, void *stream, void *xstream,
+                                     dssg_pairs *out);
+int dssg_sharded_stats(dssg_ctx *ctx, double *ms, int64_t *counts);
 
 /* ---- per-request path: micro-batcher -------------------------------------
  * The reference covers and searches once per RPC (pkg/scd/operations_handler

@@ -27,6 +27,16 @@ static int failures = 0;
         }                                         \
     } while (0)
 
+/* Nanoseconds since the epoch -> the microseconds CockroachDB keeps (round
+ * half up, as go/pkg/gpu's usOf does with time.Round(time.Microsecond)). */
+static int64_t us_round(int64_t ns)
+{
+    const int64_t q = ns / 1000, r = ns % 1000;
+    if (r >= 500) return q + 1;
+    if (r < -500) return q - 1;
+    return q;
+}
+
 static uint64_t token_id(const char *tok)
 {
     return (uint64_t)strtoull(tok, NULL, 16) << (64 - 4 * strlen(tok));
@@ -140,6 +150,22 @@ int main(void)
         /* now past every ends_at -> none */
         rc = dssg_search_operations(ctx, idx, 1, qoffs, circle, &qlo, &qhi, &qs, &qe, 2001, oq, oe, 16, &needed);
         CHECK(rc == DSSG_OK && needed == 0, "expired n=%lld", (long long)needed);
+        /* the caller's time rule (dssgpu.h "Times"): CockroachDB stores and
+         * compares TIMESTAMPTZ rounded to the microsecond, half up (Go's
+         * time.Round), so `now` = 2000 us + 500 ns is 2001 us and no row whose
+         * ends_at is 2000 us matches, while 2000 us + 499 ns is 2000 us and both
+         * match (truncating the nanoseconds would return them for +500 too). */
+        {
+            const int64_t now_ns[2] = {2000 * 1000 + 500, 2000 * 1000 + 499};
+            const int64_t want[2] = {0, 2};
+            for (int k = 0; k < 2; k++) {
+                const int64_t now_us = us_round(now_ns[k]);
+                rc = dssg_search_operations(ctx, idx, 1, qoffs, circle, &qlo, &qhi, &qs, &qe, now_us, oq, oe, 16,
+                                            &needed);
+                CHECK(rc == DSSG_OK && needed == want[k], "now %lld ns (%lld us): n=%lld want %lld",
+                      (long long)now_ns[k], (long long)now_us, (long long)needed, (long long)want[k]);
+            }
+        }
         /* RID SearchISAs: earliest 1999, latest NULL -> e0, e1 */
         int64_t earliest = 1999, latest = DSSG_TIME_NULL_END_Q;
         rc = dssg_search_isas(ctx, idx, 1, qoffs, circle, &earliest, &latest, oq, oe, 16, &needed);

@@ -41,3 +41,28 @@ def undefined_names(path):
 
 def test_bench_has_no_undefined_names():
     assert undefined_names(os.path.join(ROOT, "bench.py")) == []
+
+
+def _result_dict(fn_name):
+    tree = ast.parse(open(os.path.join(ROOT, "bench.py")).read())
+    fn = next(n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == fn_name)
+    for n in ast.walk(fn):
+        if isinstance(n, ast.Assign) and any(isinstance(t, ast.Name) and t.id == "result" for t in n.targets) \
+                and isinstance(n.value, ast.Dict):
+            return {k.value: v for k, v in zip(n.value.keys, n.value.values) if isinstance(k, ast.Constant)}
+    raise AssertionError(f"no result dict in {fn_name}")
+
+
+def test_every_line_carries_baseline_parity_and_traffic():
+    """Both result lines (replica: main, sharded N > 1: sharded_report) carry
+    a computed cpu_baseline, parity and roofline.traffic -- never a literal
+    None (the N > 1 lines had cpu_baseline None)."""
+    for fn in ("main", "sharded_report"):
+        res = _result_dict(fn)
+        for key in ("cpu_baseline", "parity", "roofline", "value", "metric", "config"):
+            assert key in res, (fn, key)
+        for key in ("cpu_baseline", "parity"):
+            assert not (isinstance(res[key], ast.Constant) and res[key].value is None), (fn, key)
+        roof = {k.value: v for k, v in zip(res["roofline"].keys, res["roofline"].values)}
+        assert "traffic" in roof and not (isinstance(roof["traffic"], ast.Constant) and roof["traffic"].value is None)
+    assert "exchanged" in _result_dict("sharded_report")

@@ -231,3 +231,59 @@ def test_native_rccl_one_rank_equals_full_search():
         ctx.set_tuning("route_identity", 1)
     comm.close()
     idx.free()
+
+
+def test_native_async_exchange_stream_one_rank():
+    """dssg_sharded_search_async_device: the pairs' trip home on a second
+    communicator and stream.  On one rank with the general routing forced:
+    every step equals the whole-index search once the exchange stream has
+    run, a step's output stays valid through the next step (two buffer
+    sets), and the stats report the routed rows and no bytes to other ranks."""
+    import torch
+    from dss_amd import _lib, device as D, shard
+    from dss_amd.store import EntityIndex
+    ci, cq, qa, ia, tlo, thi = _covered(0.05)
+    full = EntityIndex(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1)
+    want = _keys(*full.search_batch(cq.offs, cq.cells, qa.alt_lo, qa.alt_hi, tlo, thi))
+    ctx = _lib.context()
+    comms = [shard.NativeComm(ctx, 1, 0, shard.NativeComm.unique_id(ctx)) for _ in range(2)]
+    ranges = shard.cell_splitters(ci.cells, 1)
+    idx = EntityIndex(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1, cell_range=ranges[0])
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")  # noqa: E731
+    offs, cells = t(cq.offs), t(cq.cells.view(np.int64))
+    qargs = (t(qa.alt_lo), t(qa.alt_hi), t(tlo), t(thi))
+    xs = torch.cuda.Stream()
+    ns = shard.NativeShardedSearch(ctx, comms[0], idx.h, ranges, xcomm=comms[1], xstream=xs)
+    with pytest.raises(ValueError):
+        shard.NativeShardedSearch(ctx, comms[0], idx.h, ranges, xcomm=comms[1])
+    try:
+        for identity in (1, 0):
+            ctx.set_tuning("route_identity", identity)
+            prev = None
+            for k in range(3):
+                p = ns.step(offs.data_ptr(), cells.data_ptr(), len(cq.offs) - 1, *qargs)
+                torch.cuda.synchronize()
+                got = _keys(D.copy_back(ctx, p.q, int(p.n), np.uint32), D.copy_back(ctx, p.e, int(p.n), np.uint32))
+                assert np.array_equal(got, want), (identity, k)
+                if prev is not None:  # the previous step's output, read after this step
+                    pq_, pn_ = prev
+                    again = _keys(D.copy_back(ctx, pq_.q, pn_, np.uint32), D.copy_back(ctx, pq_.e, pn_, np.uint32))
+                    assert np.array_equal(again, want), (identity, k)
+                prev = (p, int(p.n))
+            ms, cnt = ns.stats()
+            if identity == 0:
+                assert cnt["rows"] > 0
+                assert cnt["query_bytes_sent"] == 0 and cnt["pair_bytes_sent"] == 0
+                assert cnt["shard_pairs"] == len(want)
+        # timing on: phases measured, touched postings counted
+        ctx.set_tuning("route_identity", 0)
+        ctx.L.dssg_set_timing(ctx.h, 1)
+        p = ns.step(offs.data_ptr(), cells.data_ptr(), len(cq.offs) - 1, *qargs)
+        ctx.L.dssg_set_timing(ctx.h, 0)
+        ms, cnt = ns.stats()
+        assert ms["join"] > 0 and ms["exchange_pairs"] >= 0 and cnt["touched"] > 0
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_tuning("route_identity", 1)
+    ns.close()
+    idx.free()
