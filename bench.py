@@ -1083,8 +1083,10 @@ def index_info(ctx, index):
     import ctypes as C
     v = [C.c_int64() for _ in range(6)]
     ctx.check(ctx.L.dssg_index_info(index, *[C.byref(x) for x in v]))
-    return dict(zip(["postings", "cells", "long_duration_postings", "long_footprint_postings", "max_cell_postings",
-                     "dcap_us"], [x.value for x in v]))
+    d = dict(zip(["postings", "groups", "long_duration_postings", "long_footprint_postings", "max_group_postings",
+                  "dcap_us"], [x.value for x in v]))
+    d["grain_level"] = int(ctx.L.dssg_index_grain(index))  # 12: (entity, quad) postings; 13: (entity, cell)
+    return d
 
 
 def pmc_traffic(kernel, nq, ni, world=1, mode="replica"):

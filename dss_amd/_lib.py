@@ -119,6 +119,8 @@ def load():
         L.dssg_index_num_postings.restype = i64
         L.dssg_index_num_cells.argtypes = [vp]
         L.dssg_index_num_cells.restype = i64
+        L.dssg_index_grain.argtypes = [vp]
+        L.dssg_index_grain.restype = C.c_int32
         L.dssg_search_device.argtypes = [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, P(Pairs)]
         L.dssg_search.argtypes = [vp, vp, i64, P(i64), P(u64), P(f), P(f), P(i64), P(i64), P(i32), P(u32), P(u32),
                                   i64, P(i64)]

@@ -254,6 +254,11 @@ int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value)
         ctx->search.set_join_shape((int)value);
         return DSSG_OK;
     }
+    if (std::string(key) == "index_grain") {  // 0 auto (default), 1 level-13 cells, 2 quads (level-12 cells)
+        if (value < 0 || value > 2) return DSSG_ERR_INVALID;
+        ctx->search.set_grain((int)value);
+        return DSSG_OK;
+    }
     if (std::string(key) == "small_search") {  // max queries of the one-launch small-batch join (0: never)
         ctx->search.set_small_max_q(value);
         return DSSG_OK;
@@ -511,6 +516,7 @@ void dssg_index_free(dssg_index *idx)
 }
 int64_t dssg_index_num_postings(const dssg_index *idx) { return idx ? idx->n_p : 0; }
 int64_t dssg_index_num_cells(const dssg_index *idx) { return idx ? idx->n_cells : 0; }
+int32_t dssg_index_grain(const dssg_index *idx) { return idx ? (idx->gshift == 37 ? 12 : 13) : 0; }
 
 int dssg_search_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *d_q_offs,
                        const uint64_t *d_q_cells, const float *d_q_alt_lo, const float *d_q_alt_hi,

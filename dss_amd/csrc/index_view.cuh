@@ -9,10 +9,24 @@
 namespace dss {
 namespace {
 
-constexpr uint32_t kFirstBit = 0x80000000u;  // b_e: the cell is the entity's smallest cell
-constexpr uint8_t kMetaCompact = 0x80;      // b_meta: every smaller cell of the entity is within +-7 cells
+// Postings are per (entity, group): an index is built at one of two grains
+// (dssg_index.gshift, chosen per build from the footprints' shape):
+//   * quads (gshift 37): a group is a level-12 cell, the 2 x 2 level-13 cells
+//     below it (ids contiguous in S2 order: a quad's cells are one run of a
+//     sorted cell list); a posting carries the 4-bit mask of the entity's
+//     cells in the quad (b_meta low bits, bit = the child position
+//     (c >> 35) & 3);
+//   * cells (gshift 35): a group is one level-13 cell, mask 1.
+// An id that is not a valid level-13 cell (the reference tests use invalid
+// face-7 ids as opaque keys, Q12) is a group of its own with mask 1, so it
+// meets only an equal id.  "Quad" below means a group of either grain.
+constexpr uint32_t kFirstBit = 0x80000000u;  // b_e: the quad is the entity's first (holds its smallest cell)
+constexpr uint8_t kMetaCompact = 0x80;      // b_meta: every cell of the entity before the quad lies in its window
 constexpr uint8_t kMetaLongFp = 0x40;       // b_meta: the entity's footprint is long (long_cells)
+constexpr uint8_t kMetaMask = 0x0F;         // b_meta: the entity's cells in the quad (child bits)
 constexpr uint64_t kLsb13 = 1ull << 34;
+constexpr int kQuadShift = 37;              // group key of a level-13 id at the quad grain: c >> 37
+constexpr int kCellShift = 35;              // ... at the cell grain: c >> 35
 
 __device__ __forceinline__ int64_t tid64() { return (int64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 __device__ __forceinline__ int64_t nthreads64() { return (int64_t)gridDim.x * blockDim.x; }
@@ -42,13 +56,14 @@ struct IndexView {
     const longlong2 *b_t;
     const ulonglong2 *b_sig;
     const int32_t *b_owner;  // nullptr: built without owners
-    const uint32_t *b_mult;  // nullptr: every multiplicity is 1
+    const uint32_t *b_mult;  // nullptr: every multiplicity is 1; else 8 bits per child of the quad
     const int64_t *e_offs;
     const uint64_t *e_cells;
     const int64_t *e_t1;     // entity end time (us)
     const int32_t *e_owner;  // entity owner (nullptr: built without owners)
     const uint32_t *dead;    // tombstone bitmap (nullptr: none)
     long long dcap;
+    int gshift;              // group key = cell >> gshift (kQuadShift or kCellShift)
 };
 
 IndexView view_of(const dssg_index *idx)
@@ -74,14 +89,27 @@ IndexView view_of(const dssg_index *idx)
     v.e_owner = idx->has_owner ? idx->e_owner.p : nullptr;
     v.dead = idx->has_dead ? idx->dead.p : nullptr;
     v.dcap = idx->dcap;
+    v.gshift = idx->gshift;
     return v;
 }
 
-// Slot of cell c, or false if c is in neither table.
+// Child bit of a cell in its group (1 at the cell grain, and for an
+// irregular id: its own group).
+__host__ __device__ __forceinline__ uint32_t child_bit(uint64_t c, int gshift)
+{
+    return (gshift == kQuadShift && is_regular(c)) ? 1u << (uint32_t)((c >> 35) & 3u) : 1u;
+}
+// Two cells of one sorted list in the same group (irregular ids never share).
+__host__ __device__ __forceinline__ bool same_quad(uint64_t a, uint64_t b, int gshift)
+{
+    return is_regular(a) && is_regular(b) && (a >> gshift) == (b >> gshift);
+}
+
+// Slot of the quad holding cell c, or false if it is in neither table.
 __device__ __forceinline__ bool find_slot(const IndexView &a, uint64_t c, uint32_t &slot)
 {
     if (is_regular(c)) {
-        uint64_t k = c >> 35;
+        uint64_t k = c >> a.gshift;
         if (k < a.kmin || (int64_t)(k - a.kmin) >= a.n_dense) return false;
         slot = (uint32_t)(k - a.kmin);
         return true;
@@ -98,10 +126,19 @@ __device__ __forceinline__ bool find_slot(const IndexView &a, uint64_t c, uint32
     }
     return false;
 }
-__device__ __forceinline__ uint64_t cell_of_slot(const IndexView &a, uint32_t slot)
+// The smallest cell a slot's quad can hold (its child 0; an irregular id
+// itself): "cells below the quad" are the cells < this one.
+__device__ __forceinline__ uint64_t quad_first_cell(const IndexView &a, uint32_t slot)
 {
-    if ((int64_t)slot < a.n_dense) return ((a.kmin + slot) << 35) | kLsb13;
+    if ((int64_t)slot < a.n_dense) return ((a.kmin + slot) << a.gshift) | kLsb13;
     return a.irr_cells[slot - (uint32_t)a.n_dense];
+}
+// A posting's multiplicity for one child of its quad (the times (cell,
+// entity) occurs in the stored array: 8 bits per child, b_mult).
+__device__ __forceinline__ uint32_t child_mult(const IndexView &a, uint64_t p, uint32_t bit)
+{
+    if (!a.b_mult) return 1u;
+    return (a.b_mult[p] >> (8u * (uint32_t)__builtin_ctz(bit))) & 0xffu;
 }
 // Postings of a slot: [s, e), the regular ones [s, s + nreg).
 __device__ __forceinline__ void slot_range(const IndexView &a, uint32_t slot, uint64_t &s, uint64_t &e)

@@ -8,10 +8,14 @@
 //     and the `cells && $n` queries (identification_service_area.go:170-180,
 //     subscriptions.go:222-273).
 //
-// Index: one posting per unique (cell, entity), sorted by
-// (cell, duration class, m = min(t0, t1)); a cell's postings are found with
-// one dense lookup (slot = cell >> 35 for level-13 ids; a sorted side table
-// for any other id -- the reference tests use invalid face-7 ids, Q12).
+// Index: one posting per (entity, quad) -- a quad is the
+// level-12 parent of 2 x 2 level-13 cells, the posting carries the mask of the
+// entity's cells in it -- sorted by (quad, duration class, m = min(t0, t1));
+// a quad's postings are found with one dense lookup (slot = cell >> 37 for
+// level-13 ids; a sorted side table for any other id, each its own quad --
+// the reference tests use invalid face-7 ids, Q12).  A query and an entity
+// meet in a quad where their masks intersect, and the pair is emitted in the
+// quad holding their smallest shared cell (SQL DISTINCT).
 // Filter attributes (altitudes, times, a 256-bit "near prefix" signature) are
 // inlined per posting, SoA.  No posting is copied: 2.2e9 postings (configs[4],
 // 50M corridors) fit one GPU.
@@ -45,10 +49,13 @@ namespace dss {
 namespace {
 
 constexpr unsigned kBlock = 256;
-constexpr uint32_t kRank0 = 0x80000000u;     // record: the cell is the query's first cell
-constexpr uint32_t kCompactQ = 0x40000000u;  // record: the query's prefix at this cell is compact
+constexpr uint32_t kRank0 = 0x80000000u;     // record: the quad is the query's first (holds its smallest cell)
+constexpr uint32_t kCompactQ = 0x40000000u;  // record: the query's cells before the quad lie in its window
 constexpr uint32_t kLongQ = 0x20000000u;     // record: the query footprint is long (long_cells)
-constexpr uint32_t kQFlags = kRank0 | kCompactQ | kLongQ;
+constexpr int kQMaskShift = 25;              // record: the query's cells in the quad (child bits 25..28)
+constexpr uint32_t kQMask = 0xFu << kQMaskShift;
+constexpr uint32_t kQFlags = kRank0 | kCompactQ | kLongQ | kQMask;
+constexpr int64_t kMaxBatchQ = (int64_t)1 << kQMaskShift;  // queries per batch (ids below the flag bits)
 constexpr uint32_t kNoDecode = 0xffffffffu;
 constexpr uint32_t kNoSlot = 0xffffffffu;
 // Query windows wider than a per-batch threshold T form their own per-cell
@@ -129,14 +136,14 @@ __device__ __forceinline__ uint32_t decode13(uint64_t c)
     return (uint32_t)face << 26 | (uint32_t)i << 13 | (uint32_t)j;
 }
 
-// Near-prefix signature at cell c of a sorted cell list: one bit per
-// (i mod 16, j mod 16) for every cell < c that lies on c's face within +-7
-// cells of c (mod 16 is injective on that window, so equal bits are equal
-// cells); `compact` iff every cell < c is such a near cell.  For two lists
-// that meet at c:
-//   * near bits overlap            -> they share a cell < c (exact);
-//   * no overlap, one side compact -> they share no cell < c (exact: a shared
-//     cell < c lies in the compact side's window, so in both near sets);
+// Near-prefix signature of a sorted cell list at a quad: one bit per
+// (i mod 16, j mod 16) for every cell below the quad that lies on its face in
+// the quad's 16 x 16 window (mod 16 is injective on it, so equal bits are
+// equal cells); `compact` iff every cell below the quad is such a near cell.
+// For two lists that meet in the quad:
+//   * near bits overlap            -> they share a cell below it (exact);
+//   * no overlap, one side compact -> they share no cell below it (exact: a
+//     shared cell would lie in the compact side's window, so in both sets);
 //   * otherwise both footprints are "long" (cells outside an 8 x 8 window,
 //     long_cells): their pairs are tagged and deduplicated after the join.
 struct Sig256 {
@@ -152,14 +159,21 @@ __device__ __forceinline__ void sig_set(Sig256 &sig, int i, int j)
     sig.w[2] |= wi == 2 ? bit : 0;
     sig.w[3] |= wi == 3 ? bit : 0;
 }
-// Signature of the decoded prefix dec[0..n) (the cells before c) at cell c
-// (decoded dc).  The loads go 8 at a time (independent, in flight together).
-__device__ __forceinline__ void prefix_sig_dec(const uint32_t *dec, int64_t n, uint32_t dc, Sig256 &sig, bool &compact)
+// Signature of the decoded prefix dec[0..n) (the cells below the quad) at the
+// quad of the decoded cell dc: the window is the 16 x
+// 16 cells [i0 - 7, i0 + 8] x [j0 - 7, j0 + 8] around the quad's even anchor
+// (i0, j0), so mod 16 stays injective; `compact` iff every cell of the prefix
+// (the cells in earlier quads) lies in it.  Two lists meeting in the quad
+// share a cell below it iff (when either is compact) their signatures
+// overlap.  A footprint inside an 8 x 8 window is compact at each of its
+// quads.
+__device__ __forceinline__ void prefix_sig_quad(const uint32_t *dec, int64_t n, uint32_t dc, Sig256 &sig,
+                                                bool &compact)
 {
     sig.w[0] = sig.w[1] = sig.w[2] = sig.w[3] = 0;
     const bool v = dc != kNoDecode;
     compact = v;
-    const int f = (int)(dc >> 26), ic = (int)((dc >> 13) & 8191u), jc = (int)(dc & 8191u);
+    const int f = (int)(dc >> 26), i0 = (int)((dc >> 13) & 8190u), j0 = (int)(dc & 8190u);
     constexpr int kU = 8;
     for (int64_t k0 = 0; k0 < n; k0 += kU) {
         uint32_t dd[kU];
@@ -170,8 +184,8 @@ __device__ __forceinline__ void prefix_sig_dec(const uint32_t *dec, int64_t n, u
             if (k0 + u >= n) break;
             const uint32_t d = dd[u];
             const int ci = (int)((d >> 13) & 8191u), cj = (int)(d & 8191u);
-            const int di = ci - ic, dj = cj - jc;
-            if (v && d != kNoDecode && (int)(d >> 26) == f && di >= -7 && di <= 7 && dj >= -7 && dj <= 7)
+            const int di = ci - i0, dj = cj - j0;
+            if (v && d != kNoDecode && (int)(d >> 26) == f && di >= -7 && di <= 8 && dj >= -7 && dj <= 8)
                 sig_set(sig, ci, cj);
             else
                 compact = false;
@@ -181,7 +195,7 @@ __device__ __forceinline__ void prefix_sig_dec(const uint32_t *dec, int64_t n, u
 
 // A footprint is "long" unless all its cells are valid level-13 cells of one
 // face inside an 8 x 8 window: then every prefix of it is compact at every
-// one of its cells.
+// one of its quads.
 __device__ __forceinline__ bool long_cells_dec(const uint32_t *dec, int64_t n)
 {
     int f0 = -1, imin = 0, imax = 0, jmin = 0, jmax = 0;
@@ -339,9 +353,10 @@ __global__ void k_dcap(int64_t n, const int64_t *t0, const int64_t *t1, unsigned
     if ((threadIdx.x & 63) == 0 && d) atomicMax(dmax, d);
 }
 
-// Range of (cell >> 35) over the regular in-range cells of included rows.
+// Range of the group keys (cell >> gshift) over the regular in-range cells of
+// included rows.
 __global__ void k_dense_range(int64_t P, const uint64_t *cells, const uint32_t *pent, const int64_t *t1, uint64_t lo,
-                              uint64_t hi, unsigned long long *mm, unsigned long long *n_irr)
+                              uint64_t hi, int gshift, unsigned long long *mm, unsigned long long *n_irr)
 {
     const int64_t i = tid64();
     unsigned long long kmn = ~0ull, kmx = 0;
@@ -349,7 +364,7 @@ __global__ void k_dense_range(int64_t P, const uint64_t *cells, const uint32_t *
     if (i < P) {
         const uint64_t c = cells[i];
         if (c >= lo && c <= hi && row_included(t1[pent[i]])) {
-            if (is_regular(c)) kmn = kmx = c >> 35;
+            if (is_regular(c)) kmn = kmx = c >> gshift;
             else irr = true;
         }
     }
@@ -364,12 +379,37 @@ __global__ void k_dense_range(int64_t P, const uint64_t *cells, const uint32_t *
     wave_count(irr, n_irr);
 }
 
+// Cells and quad heads (the first of an entity's cells in a quad) among the
+// in-range cells of included rows: the grain choice of the build.
+__global__ void k_grain_counts(int64_t P, const uint64_t *cells, const uint32_t *pent, const int64_t *t1, uint64_t lo,
+                               uint64_t hi, unsigned long long *cnt)
+{
+    const int64_t i = tid64();
+    bool in = false, head = false;
+    if (i < P) {
+        const uint64_t c = cells[i];
+        in = c >= lo && c <= hi && row_included(t1[pent[i]]);
+        head = in && (i == 0 || pent[i - 1] != pent[i] || !same_quad(cells[i - 1], c, kQuadShift));
+    }
+    wave_count(in, &cnt[0]);
+    wave_count(head, &cnt[1]);
+}
+
 struct BuildCtx {
     const uint64_t *cells;  // e_cells
     const uint32_t *pent;   // entity of each e_cells position
     const int64_t *t0, *t1;
     uint64_t lo, hi;
+    int gshift;
+    // e_cells position i heads a posting: the first of its entity's cells in
+    // its quad (a quad-aligned range holds all of them or none)
     __device__ bool posting(int64_t i) const
+    {
+        const uint64_t c = cells[i];
+        if (!(c >= lo && c <= hi && row_included(t1[pent[i]]))) return false;
+        return i == 0 || pent[i - 1] != pent[i] || !same_quad(cells[i - 1], c, gshift);
+    }
+    __device__ bool in_range(int64_t i) const
     {
         const uint64_t c = cells[i];
         return c >= lo && c <= hi && row_included(t1[pent[i]]);
@@ -393,7 +433,7 @@ struct EmitPostingKey {  // (order_key(m), position)
 };
 struct PredIrr {
     BuildCtx b;
-    __device__ bool operator()(int64_t i) const { return b.posting(i) && !is_regular(b.cells[i]); }
+    __device__ bool operator()(int64_t i) const { return b.in_range(i) && !is_regular(b.cells[i]); }
 };
 struct EmitIrr {
     const uint64_t *cells;
@@ -451,31 +491,44 @@ __global__ void k_slot_keys(int64_t NP, IndexView a, const uint32_t *pos, const 
     key[j] = slot_of(a, cells[i]) << 1 | (lng ? 1u : 0u);
 }
 
-// Posting attributes in final order.
+// Posting attributes in final order: the quad's cell mask (the entity's run
+// of cells in the quad, <= 4), per-child multiplicities, the near-prefix
+// signature of its cells below the quad.
 __global__ void k_gather(int64_t NP, const uint32_t *pos, const uint32_t *pent, const int64_t *e_offs,
-                         const uint32_t *dec, const uint8_t *elong, const float *alo, const float *ahi,
-                         const int64_t *t0, const int64_t *t1, const int32_t *owner, const uint32_t *mult,
-                         uint32_t *b_e, uint8_t *b_meta, float2 *b_alt, longlong2 *b_t, ulonglong2 *b_sig,
-                         int32_t *b_owner, uint32_t *b_mult, unsigned long long *nlongfp)
+                         const uint64_t *e_cells, const uint32_t *dec, const uint8_t *elong, const float *alo,
+                         const float *ahi, const int64_t *t0, const int64_t *t1, const int32_t *owner,
+                         const uint32_t *mult, int gshift, uint32_t *b_e, uint8_t *b_meta, float2 *b_alt,
+                         longlong2 *b_t, ulonglong2 *b_sig, int32_t *b_owner, uint32_t *b_mult,
+                         unsigned long long *nlongfp)
 {
     const int64_t j = tid64();
     bool lf = false;
     if (j < NP) {
         const uint32_t i = pos[j];
         const uint32_t e = pent[i];
-        const int64_t o = e_offs[e];
+        const int64_t o = e_offs[e], oe = e_offs[e + 1];
+        const uint64_t c = e_cells[i];
+        uint32_t mask = child_bit(c, gshift), mm = 0;
+        if (mult) mm = min(mult[i], 255u) << (8u * (uint32_t)__builtin_ctz(mask));
+        for (int64_t r = (int64_t)i + 1; r < oe && r < (int64_t)i + 4; r++) {
+            const uint64_t cr = e_cells[r];
+            if (!same_quad(c, cr, gshift)) break;
+            const uint32_t b = child_bit(cr, gshift);
+            mask |= b;
+            if (mult) mm |= min(mult[r], 255u) << (8u * (uint32_t)__builtin_ctz(b));
+        }
         Sig256 sig;
         bool compact = false;
-        prefix_sig_dec(dec + o, (int64_t)i - o, dec[i], sig, compact);
+        prefix_sig_quad(dec + o, (int64_t)i - o, dec[i], sig, compact);
         lf = elong[e] != 0;
         b_e[j] = e | ((int64_t)i == o ? kFirstBit : 0u);
-        b_meta[j] = (uint8_t)((compact ? kMetaCompact : 0) | (lf ? kMetaLongFp : 0));
+        b_meta[j] = (uint8_t)((compact ? kMetaCompact : 0) | (lf ? kMetaLongFp : 0) | mask);
         b_alt[j] = make_float2(alo[e], ahi[e]);
         b_t[j] = make_longlong2(t0[e], t1[e]);
         b_sig[2 * j] = make_ulonglong2(sig.w[0], sig.w[1]);
         b_sig[2 * j + 1] = make_ulonglong2(sig.w[2], sig.w[3]);
         if (owner) b_owner[j] = owner[e];
-        if (mult) b_mult[j] = mult[i];
+        if (mult) b_mult[j] = mm;
     }
     wave_count(lf, nlongfp);
 }
@@ -552,7 +605,7 @@ struct QueryView {
 struct alignas(16) QRec {
     long long tlo, thi;
     float alo, ahi;
-    uint32_t qv;   // query | kRank0 | kCompactQ | kLongQ
+    uint32_t qv;   // query | kRank0 | kCompactQ | kLongQ | the query's cells in the quad << kQMaskShift
     int32_t own;   // owner filter (-1: any)
     unsigned long long sig[4];  // near-prefix signature of the query's cells before this one
 };
@@ -610,10 +663,11 @@ __device__ __forceinline__ int choose_wide_log(const unsigned long long *hist, d
 // (long_cells) from per-query LDS min/max/face-mask reductions.  One block
 // per 256 queries: their cell offsets go to LDS, the block's cells are then
 // visited coalesced, each finding its query by binary search in LDS.
-// Per query cell: its query, decode and slot (kNoSlot if the cell holds no
-// postings), and its rank among its query's cells with postings (vpre[k] -
-// qvb[q]); per query: the long flag and the count of cells with postings.
-// One block per 256 queries, their cells in kBlock-wide steps.
+// Per query cell: its query, decode and slot (kNoSlot unless the cell is the
+// first of its query's cells in its quad -- the quad's record -- and the
+// quad holds postings), and its rank among its query's records with postings
+// (vpre[k] - qvb[q]); per query: the long flag and the count of records with
+// postings.  One block per 256 queries, their cells in kBlock-wide steps.
 __global__ __launch_bounds__(kBlock) void k_cell_query(IndexView a, int64_t nq, const int64_t *offs,
                                                        const uint64_t *cells, uint32_t *cq, uint32_t *dec,
                                                        uint32_t *cslot, uint8_t *qlong, uint32_t *vpre,
@@ -650,8 +704,11 @@ __global__ __launch_bounds__(kBlock) void k_cell_query(IndexView a, int64_t nq, 
             const uint64_t c = cells[k];
             const uint32_t d = decode13(c);
             dec[k] = d;
+            // one record per (query, quad): the quad's first cell in the
+            // query's sorted list carries it
+            const bool head = k == so[lo] || !same_quad(cells[k - 1], c, a.gshift);
             uint32_t sl = kNoSlot;
-            if (find_slot(a, c, sl) && a.s_post[sl + 1] == a.s_post[sl]) sl = kNoSlot;
+            if (head && find_slot(a, c, sl) && a.s_post[sl + 1] == a.s_post[sl]) sl = kNoSlot;
             cslot[k] = sl;
             valid = sl != kNoSlot;
             if (valid) atomicAdd(&s_cnt[lo], 1u);
@@ -778,7 +835,7 @@ __global__ void k_qemit(int64_t nqc, const uint32_t *cq, const uint32_t *cslot, 
 // decodes loaded 8 at a time).  A wave's 64 records leave through LDS as four
 // coalesced 1 KiB stores.
 __global__ __launch_bounds__(kBlock) void k_qrecs(QueryView qv, int64_t nqc, const uint32_t *cq, const uint32_t *dec,
-                                                  const uint8_t *qlong, QRec *recs)
+                                                  const uint32_t *cslot, const uint8_t *qlong, int gshift, QRec *recs)
 {
     const int64_t k = tid64();
     if (k - (threadIdx.x & 63) >= nqc) return;  // whole wave past the end
@@ -788,17 +845,25 @@ __global__ __launch_bounds__(kBlock) void k_qrecs(QueryView qv, int64_t nqc, con
     r.qv = 0;
     r.own = -1;
     r.sig[0] = r.sig[1] = r.sig[2] = r.sig[3] = 0;
-    if (k < nqc) {
+    if (k < nqc && cslot[k] != kNoSlot) {  // (a record only where a quad's postings will read it)
         const uint32_t q = cq[k];
-        const int64_t c0 = qv.offs[q];
+        const int64_t c0 = qv.offs[q], c1 = qv.offs[q + 1];
+        const uint64_t c = qv.cells[k];
+        uint32_t mask = child_bit(c, gshift);
+        for (int64_t x = k + 1; x < c1 && x < k + 4; x++) {
+            const uint64_t cx = qv.cells[x];
+            if (!same_quad(c, cx, gshift)) break;
+            mask |= child_bit(cx, gshift);
+        }
         Sig256 sig;
         bool compact = false;
-        prefix_sig_dec(dec + c0, k - c0, dec[k], sig, compact);
+        prefix_sig_quad(dec + c0, k - c0, dec[k], sig, compact);
         r.tlo = qv.tlo[q];
         r.thi = qv.thi[q];
         r.alo = qv.alo[q];
         r.ahi = qv.ahi[q];
-        r.qv = q | (k == c0 ? kRank0 : 0u) | (compact ? kCompactQ : 0u) | (qlong[q] ? kLongQ : 0u);
+        r.qv = q | (k == c0 ? kRank0 : 0u) | (compact ? kCompactQ : 0u) | (qlong[q] ? kLongQ : 0u) |
+               (mask << kQMaskShift);
         r.own = qv.owner ? qv.owner[q] : -1;
         r.sig[0] = sig.w[0];
         r.sig[1] = sig.w[1];
@@ -1361,6 +1426,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 const unsigned long long R0 = __ballot((qslot & kRank0) != 0);
                 const unsigned long long RC = __ballot((qslot & kCompactQ) != 0);
                 const unsigned long long RL = LONG ? __ballot((qslot & kLongQ) != 0) : 0ull;
+                // the records whose cells in the quad meet this posting's:
+                // one ballot per child, ORed over the posting's children
+                const unsigned long long Q0 = __ballot((qslot >> kQMaskShift) & 1u);
+                const unsigned long long Q1 = __ballot((qslot >> (kQMaskShift + 1)) & 1u);
+                const unsigned long long Q2 = __ballot((qslot >> (kQMaskShift + 2)) & 1u);
+                const unsigned long long Q3 = __ballot((qslot >> (kQMaskShift + 3)) & 1u);
+                const unsigned long long meets = ((pmeta & 1u) ? Q0 : 0ull) | ((pmeta & 2u) ? Q1 : 0ull) |
+                                                 ((pmeta & 4u) ? Q2 : 0ull) | ((pmeta & 8u) ? Q3 : 0ull);
                 n_bcast += (unsigned long long)nrel;
                 n_tests += (unsigned long long)nrel * (unsigned long long)__popcll(vmask);
                 // (1) this lane's posting against every staged record: a bit per
@@ -1390,11 +1463,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                     }
                     mhi |= (uint32_t)pass << (j - 32);
                 }
-                const unsigned long long m = pv ? (((unsigned long long)mhi << 32) | mlo) : 0ull;
-                // (2) smallest shared cell only (SQL DISTINCT, Q13): a rank-0 record
-                // (the query's first cell) or a posting at its entity's first cell
-                // has no smaller cell on one side; otherwise the near-prefix
-                // signatures decide -- overlap: drop; none and either prefix
+                const unsigned long long m = pv ? (((unsigned long long)mhi << 32) | mlo) & meets : 0ull;
+                // (2) the quad of the smallest shared cell only (SQL DISTINCT,
+                // Q13): a rank-0 record (the query's first quad) or a posting in
+                // its entity's first quad has no cell below the quad on one
+                // side; otherwise the near-prefix signatures of the cells below
+                // the quad decide -- overlap: drop; none and either prefix
                 // compact: keep (exact); both footprints long: keep, tagged (the
                 // tagged set is deduplicated after the join); else exact merge.
                 unsigned long long keep = pfirst ? m : (m & R0);
@@ -1421,7 +1495,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                     bool k = !LONG || pcompact || ((RC >> j) & 1ull) || (plong && ((RL >> j) & 1ull));
                     if (LONG && !k) {  // neither prefix compact, not both long (rare; needs long postings)
                         const uint32_t q = (uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags;
-                        k = no_smaller_shared<2>(ix, pent, cell_of_slot(ix, d.slot), a.qv.cells + a.qv.offs[q],
+                        k = no_smaller_shared<2>(ix, pent, quad_first_cell(ix, d.slot), a.qv.cells + a.qv.offs[q],
                                                  a.qv.offs[q + 1] - a.qv.offs[q]);
                     }
                     if (k) keep |= 1ull << j;
@@ -1808,18 +1882,30 @@ __global__ __launch_bounds__(kBlock) void k_stats(IndexView a, QueryView qv, uns
         const int64_t c0 = qv.offs[q], c1 = qv.offs[q + 1];
         for (int64_t ci = c0; ci < c1; ci++) {
             const uint64_t c = qv.cells[ci];
-            uint32_t slot;
+            const uint32_t bit = child_bit(c, a.gshift);
+            // the quad's first cell in the query also counts its pairs (the
+            // query's cells in the quad: qmask)
+            const bool head = ci == c0 || !same_quad(qv.cells[ci - 1], c, a.gshift);
+            uint32_t qmask = bit;
+            for (int64_t x = ci + 1; head && x < c1 && x < ci + 4 && same_quad(c, qv.cells[x], a.gshift); x++)
+                qmask |= child_bit(qv.cells[x], a.gshift);
+            uint32_t slot = 0;
             uint64_t s = 0, e = 0;
             if (find_slot(a, c, slot)) slot_range(a, slot, s, e);
+            const uint64_t cq0 = s < e ? quad_first_cell(a, slot) : c;
             for (uint64_t base = s; base < e; base += 64) {
                 const uint64_t p = base + lane;
-                bool pass = false;
+                bool inc = false, pass = false;
                 if (p < e) {
-                    const uint32_t pe = a.b_e[p];
-                    pass = ci == c0 || (pe & kFirstBit) ||
-                           no_smaller_shared<8>(a, pe & ~kFirstBit, c, qv.cells + c0, ci - c0);
+                    const uint32_t pm = a.b_meta[p];
+                    inc = (pm & bit) != 0;  // a posting of this very cell (cell-level M)
+                    if (head && (pm & qmask)) {
+                        const uint32_t pe = a.b_e[p];
+                        pass = ci == c0 || (pe & kFirstBit) ||
+                               no_smaller_shared<8>(a, pe & ~kFirstBit, cq0, qv.cells + c0, ci - c0);
+                    }
                 }
-                my_m += e - base < 64 ? e - base : 64;
+                my_m += (unsigned long long)__popcll(__ballot(inc));
                 my_d += (unsigned long long)__popcll(__ballot(pass));
             }
         }
@@ -1831,12 +1917,13 @@ __global__ __launch_bounds__(kBlock) void k_stats(IndexView a, QueryView qv, uns
 }
 
 // Small batches (the per-RPC path, pkg/scd/operations_handler.go:118-168:
-// one covering and one search per request): one wave per query cell, lanes
-// over the cell's postings in the band [tlo - dcap, thi] plus its long
-// postings, the fused altitude/time/owner filter, and the smallest-shared-cell
-// rule (SQL DISTINCT, Q13) decided exactly by a merge of the two sorted cell
-// lists below the cell -- no query ordering, units or dedupe pass: one
-// launch, its pairs through one wave-aggregated atomic per 64 postings.
+// one covering and one search per request): one wave per query cell that
+// opens a quad of the query, lanes over the quad's postings in the band
+// [tlo - dcap, thi] plus its long postings, the cell-mask and fused
+// altitude/time/owner filter, and the smallest-shared-cell rule (SQL
+// DISTINCT, Q13) decided exactly by a merge of the two sorted cell lists
+// below the quad -- no query ordering, units or dedupe pass: one launch, its
+// pairs through one wave-aggregated atomic per 64 postings.
 constexpr int kSmallBlock = 256;
 __global__ __launch_bounds__(kSmallBlock) void k_small_join(IndexView ix, QueryView qv, int64_t nqc, int64_t cap,
                                                              uint32_t *__restrict__ oq, uint32_t *__restrict__ oe,
@@ -1852,10 +1939,18 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_join(IndexView ix, QueryV
         else hi = mid;
     }
     const uint32_t q = (uint32_t)lo;
-    const int64_t c0 = qv.offs[q];
+    const int64_t c0 = qv.offs[q], c1 = qv.offs[q + 1];
     const uint64_t c = qv.cells[k];
+    if (k > c0 && same_quad(qv.cells[k - 1], c, ix.gshift)) return;  // the quad's first cell in the query carries it
+    uint32_t qmask = child_bit(c, ix.gshift);
+    for (int64_t x = k + 1; x < c1 && x < k + 4; x++) {
+        const uint64_t cx = qv.cells[x];
+        if (!same_quad(c, cx, ix.gshift)) break;
+        qmask |= child_bit(cx, ix.gshift);
+    }
     uint32_t slot;
     if (!find_slot(ix, c, slot)) return;
+    const uint64_t cq0 = quad_first_cell(ix, slot);
     const uint64_t s0 = ix.s_post[slot], s1 = ix.s_post[slot + 1], sr = s0 + ix.s_nreg[slot];
     const long long tlo = qv.tlo[q], thi = qv.thi[q];
     const float alo = qv.alo[q], ahi = qv.ahi[q];
@@ -1875,10 +1970,11 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_join(IndexView ix, QueryV
             const uint32_t pe = ix.b_e[p];
             ent = pe & ~kFirstBit;
             // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels)
-            bool pass = (pt.y >= tlo) & (pt.x <= thi) & (pa.y >= alo) & (pa.x <= ahi);
+            bool pass = (pt.y >= tlo) & (pt.x <= thi) & (pa.y >= alo) & (pa.x <= ahi) &
+                        ((ix.b_meta[p] & qmask) != 0);
             if (own >= 0) pass &= ix.b_owner[p] == own;
             if (pass && !is_dead(ix, ent))
-                keep = k == c0 || (pe & kFirstBit) || no_smaller_shared<2>(ix, ent, c, qv.cells + c0, k - c0);
+                keep = k == c0 || (pe & kFirstBit) || no_smaller_shared<2>(ix, ent, cq0, qv.cells + c0, k - c0);
         }
         const unsigned long long m = __ballot(keep);
         if (!m) continue;
@@ -1895,19 +1991,23 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_join(IndexView ix, QueryV
     }
 }
 
-// Postings of the distinct cells a batch touches: mark, then sum.
-__global__ void k_touch_mark(IndexView a, int64_t nqc, const uint64_t *cells, uint8_t *mark)
+// Cell-level postings of the distinct cells a batch touches (each (cell,
+// entity) once, as a per-cell index would hold them): the touched cells'
+// child bits per quad, then per posting of a touched quad the touched cells
+// among its own.
+__global__ void k_touch_mark(IndexView a, int64_t nqc, const uint64_t *cells, uint32_t *mark)
 {
     const int64_t k = tid64();
     if (k >= nqc) return;
     uint32_t s;
-    if (find_slot(a, cells[k], s)) mark[s] = 1;
+    if (find_slot(a, cells[k], s)) atomicOr(&mark[s], child_bit(cells[k], a.gshift));
 }
-__global__ void k_touch_sum(IndexView a, int64_t ns, const uint8_t *mark, unsigned long long *sum)
+__global__ void k_touch_sum(IndexView a, int64_t ns, const uint32_t *mark, unsigned long long *sum)
 {
     const int64_t s = tid64();
     unsigned long long c = 0;
-    if (s < ns && mark[s]) c = a.s_post[s + 1] - a.s_post[s];
+    if (s < ns && mark[s])
+        for (uint64_t p = a.s_post[s]; p < a.s_post[s + 1]; p++) c += (unsigned long long)__popc(a.b_meta[p] & mark[s]);
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(sum, c);
 }
@@ -1983,6 +2083,10 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
                          const float *alt_lo, const float *alt_hi, const int64_t *t0, const int64_t *t1,
                          const int32_t *owner, uint64_t cell_lo, uint64_t cell_hi, hipStream_t s)
 {
+    // a cell-range shard holds whole quads: ranges cut at quad boundaries
+    constexpr uint64_t kQuadSpan = (1ull << kQuadShift) - 1;  // the low bits of every id under one quad
+    if ((cell_lo != 0 && (cell_lo & kQuadSpan) != 0) || (cell_hi != ~0ull && (cell_hi & kQuadSpan) != kQuadSpan))
+        throw Error(DSSG_ERR_INVALID, "index: a cell range must start and end at quad (level-12 cell) boundaries");
     idx->cell_lo = cell_lo;
     idx->cell_hi = cell_hi;
     idx->n_e = n;
@@ -1992,7 +2096,8 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     if (P >= (int64_t)0xffffffffll) throw Error(DSSG_ERR_INVALID, "index: more than 2^32 - 1 cells in one build");
     DevBuf<unsigned long long> stat_b;
     unsigned long long *stat = stat_b.ensure(80);  // [0..64] hist, 65..66 m range, 67 dcap, 68..69 dense range,
-                                                   // 70 n_irr, 71 nlongfp, 72..73 runs/long, 74 max cell
+                                                   // 70 n_irr, 71 nlongfp, 72..73 runs/long, 74 max cell,
+                                                   // 75..76 grain counts
     DSS_HIP(hipMemsetAsync(stat, 0, 80 * sizeof(unsigned long long), s));
     {
         const unsigned long long init[2] = {~0ull, 0ull};
@@ -2068,11 +2173,25 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
         idx->tbase = mlo;
         idx->qshift = sh;
     }
-    // (3) slots: dense range and the irregular side table
-    const BuildCtx bc{e_cells, pent, t0, t1, cell_lo, cell_hi};
+    // (3) the grain: quads when an entity's cells fill them (>= 1.5 cells
+    // per (entity, quad): metro footprints, corridors), else level-13 cells
+    // (city blocks of 1-4 cells, whose quads would add candidates without
+    // saving postings)
+    int gshift = grain_ == 1 ? kCellShift : kQuadShift;
+    if (grain_ == 0 && Pu) {
+        hipLaunchKernelGGL(k_grain_counts, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, e_cells, pent, t1, cell_lo,
+                           cell_hi, stat + 75);
+        unsigned long long g[2];
+        DSS_HIP(hipMemcpyAsync(g, stat + 75, sizeof(g), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipStreamSynchronize(s));
+        gshift = 2 * g[0] >= 3 * g[1] ? kQuadShift : kCellShift;
+    }
+    idx->gshift = gshift;
+    // (4) slots: dense range and the irregular side table
+    const BuildCtx bc{e_cells, pent, t0, t1, cell_lo, cell_hi, gshift};
     if (Pu)
         hipLaunchKernelGGL(k_dense_range, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, e_cells, pent, t1, cell_lo,
-                           cell_hi, stat + 68, stat + 70);
+                           cell_hi, gshift, stat + 68, stat + 70);
     DSS_HIP(hipMemcpyAsync(h + 67, stat + 67, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
     idx->dcap = (int64_t)h[67];
@@ -2093,8 +2212,8 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     }
     const int64_t ns = idx->n_slots();
     if (ns >= (int64_t)0x7fffffff) throw Error(DSSG_ERR_INVALID, "index: more than 2^31 - 1 cell slots");
-    // (4) postings: in-range positions of included rows, sorted by m, then
-    // stably by (slot, long) -> (slot, class, m)
+    // (5) postings: the first in-range position of each (entity, group) of
+    // included rows, sorted by m, then stably by (slot, long) -> (slot, class, m)
     int64_t NP = 0;
     DevBuf<uint32_t> pos_b;
     uint32_t *pos = nullptr;
@@ -2120,7 +2239,7 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     key_b.release();
     pos_b.release();
     tmp_.release();  // the sort's alternate buffers
-    // (5) posting attributes in final order
+    // (6) posting attributes in final order
     uint32_t *b_e = idx->b_e.ensure_exact(NP + 1);
     uint8_t *b_meta = idx->b_meta.ensure_exact(NP + 1);
     float2 *b_alt = idx->b_alt.ensure_exact(NP + 1);
@@ -2129,13 +2248,13 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     int32_t *b_owner = idx->b_owner.ensure_exact(owner ? NP + 1 : 1);
     uint32_t *b_mult = idx->b_mult.ensure_exact(mult ? NP + 1 : 1);
     if (NP)
-        hipLaunchKernelGGL(k_gather, dim3(grid_for(NP, kBlock)), dim3(kBlock), 0, s, NP, pos2, pent, e_offs, dec, elong,
-                           alt_lo, alt_hi, t0, t1, owner, mult, b_e, b_meta, b_alt, b_t, b_sig, b_owner, b_mult,
-                           stat + 71);
+        hipLaunchKernelGGL(k_gather, dim3(grid_for(NP, kBlock)), dim3(kBlock), 0, s, NP, pos2, pent, e_offs, e_cells,
+                           dec, elong, alt_lo, alt_hi, t0, t1, owner, mult, gshift, b_e, b_meta, b_alt, b_t, b_sig,
+                           b_owner, b_mult, stat + 71);
     stage_check(s, "index build: gather");
     pos2_b.release();
     dec_b.release();
-    // (6) slot table: s_post (first posting per slot, scan of counts), s_nreg
+    // (7) slot table: s_post (first posting per slot, scan of counts), s_nreg
     {
         DevBuf<uint32_t> f_b, e_b, r_b;
         uint32_t *sf = f_b.ensure(ns + 1), *se = e_b.ensure(ns + 1), *sr = r_b.ensure(ns + 1);
@@ -2159,7 +2278,7 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
         if (NP) hipLaunchKernelGGL(k_slot_lfp, dim3(grid_for(NP, kBlock)), dim3(kBlock), 0, s, NP, key2, b_meta, lfp);
     }
     stage_check(s, "index build: slot table");
-    // (7) entity-level attributes: ends_at, owner, owner -> entities, counters
+    // (8) entity-level attributes: ends_at, owner, owner -> entities, counters
     int64_t *et1 = idx->e_t1.ensure_exact(n + 1);
     device_copy(et1, t1, sizeof(int64_t) * n, s);
     int64_t *notify = idx->e_notify.ensure_exact(n + 1);
@@ -2203,9 +2322,9 @@ int64_t SearchEngine::touched(const dssg_index *idx, int64_t nq, const int64_t *
 {
     if (nq <= 0) return 0;
     const int64_t nqc = fetch(q_offs + nq, s), ns = idx->n_slots();
-    DevBuf<uint8_t> mark_b;
-    uint8_t *mark = mark_b.ensure(ns + 1);
-    DSS_HIP(hipMemsetAsync(mark, 0, ns + 1, s));
+    DevBuf<uint32_t> mark_b;
+    uint32_t *mark = mark_b.ensure(ns + 1);
+    DSS_HIP(hipMemsetAsync(mark, 0, sizeof(uint32_t) * (ns + 1), s));
     unsigned long long *sum = counter_.ensure(8) + 4;
     DSS_HIP(hipMemsetAsync(sum, 0, sizeof(unsigned long long), s));
     const IndexView a = view_of(idx);
@@ -2219,7 +2338,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
                           const int32_t *q_owner, hipStream_t s, dssg_pairs *out, int64_t nqc_known)
 {
     if (q_owner && !idx->has_owner) throw Error(DSSG_ERR_INVALID, "search by owner on an index built without owners");
-    if (nq >= (int64_t)kLongQ) throw Error(DSSG_ERR_INVALID, "search: more than 2^29 queries per batch");
+    if (nq >= kMaxBatchQ) throw Error(DSSG_ERR_INVALID, "search: more than 2^25 queries per batch");
     timing_events();
     const IndexView ix = view_of(idx);
     const QueryView qv{nq, q_offs, q_cells, q_alt_lo, q_alt_hi, q_tlo, q_thi, q_owner};
@@ -2278,7 +2397,8 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     hipLaunchKernelGGL(k_qemit, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, nqc, cq, cslot, vpre, qvb, qrank, ok1,
                        qo, key, val);
     QRec *recs = (QRec *)rec_.ensure(sizeof(QRec) * (nqc + 1));
-    hipLaunchKernelGGL(k_qrecs, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, qv, nqc, cq, dec, qlong, recs);
+    hipLaunchKernelGGL(k_qrecs, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, qv, nqc, cq, dec, cslot, qlong,
+                       idx->gshift, recs);
     // (4) group the keys by cell (stable: each cell's records stay in query
     // order), over the device key count qo[nq] (<= nqc)
     const int64_t *dnkeys = qo + nq;

@@ -32,6 +32,7 @@ struct dssg_index {
     dss::DevBuf<uint8_t> s_lfp;       // n_slots: 1 = the slot holds a long-footprint posting (join variant)
     // ---- time --------------------------------------------------------------------
     int64_t dcap = 0;      // max duration of a regular posting's entity (us)
+    int gshift = 37;       // posting groups: cell >> gshift (37: quads = level-12 cells, 35: level-13 cells)
     int64_t dcap_thr = 0;  // class threshold: duration <= dcap_thr is regular
     int64_t tbase = 0;     // query-order quantisation: (tlo - tbase) >> qshift
     int qshift = 0;
@@ -95,6 +96,10 @@ class SearchEngine {
     // k_join's occupancy / pair-stage shape: 0 picks by the previous batch's
     // pass density, 1 forces 7 x 640, 2 forces 6 x 1024
     void set_join_shape(int v) { join_shape_ = v; }
+    // posting grain of the next builds: 0 picks per build (quads when an
+    // entity's cells fill them: >= 1.5 cells per (entity, quad)), 1 level-13
+    // cells, 2 quads (level-12 cells)
+    void set_grain(int v) { grain_ = v; }
     double last_join_kernel_ms() const { return join_ms_; }
     int64_t last_units() const { return units_; }
     int64_t last_keys() const { return keys_; }
@@ -156,6 +161,7 @@ class SearchEngine {
     int64_t lazy_sig_recs_ = 0;
     bool dense_out_ = false;  // the previous batch's pass density was high: k_join's 6 x 1024-pair stage shape
     int join_shape_ = 0;      // 0: by dense_out_; 1: the sparse shape; 2: the dense shape (tests)
+    int grain_ = 0;           // 0: auto; 1: cells; 2: quads
     double join_ms_ = 0;
     int64_t units_ = 0, keys_ = 0, runs_ = 0, iters_ = 0, tests_ = 0;
     int64_t flushes_ = 0, merges_ = 0, merge_lanes_ = 0, tagged_ = 0, long_queries_ = 0, long_postings_ = 0;

@@ -51,10 +51,12 @@ __global__ void k_cell_count(IndexView a, int64_t nqc, const uint64_t *cells, co
     if (!find_slot(a, cells[k], slot)) return;
     slot_range(a, slot, s, e);
     const int32_t own = owner[cq[k]];
+    const uint32_t bit = child_bit(cells[k], a.gshift);
     unsigned long long cnt = 0;
-    for (uint64_t p = s; p < e; p++) {
+    for (uint64_t p = s; p < e; p++) {  // the quad's postings that hold this cell
+        if (!(a.b_meta[p] & bit)) continue;
         const uint32_t ent = a.b_e[p] & ~kFirstBit;
-        if (a.e_owner[ent] == own && a.e_t1[ent] >= now && !is_dead(a, ent)) cnt += a.b_mult ? a.b_mult[p] : 1u;
+        if (a.e_owner[ent] == own && a.e_t1[ent] >= now && !is_dead(a, ent)) cnt += child_mult(a, p, bit);
     }
     cell_cnt[k] += cnt;  // (one thread per cell; the sides run one after another)
 }

@@ -38,11 +38,21 @@ import numpy as np
 U64_MAX = 2**64 - 1
 
 
+QUAD_SPAN = 1 << 37  # ids under one level-12 cell (a quad of the index): [k * 2^37, (k + 1) * 2^37)
+
+
+def quad_end(c: int) -> int:
+    """The last id of the quad (level-12 cell) span holding id c."""
+    return int(c) | (QUAD_SPAN - 1)
+
+
 def cell_splitters(cells: np.ndarray, parts: int) -> List[Tuple[int, int]]:
     """Inclusive uint64 ranges [lo, hi], in order, partitioning the whole id
-    space into `parts`; each cut falls right after the distinct cell where
-    the running posting count reaches r/parts of the total (a hot cell is
-    never split).  Parts beyond the number of distinct cells hold no cell."""
+    space into `parts`; each cut falls at the end of the quad (level-12 cell:
+    the index keeps one posting per (entity, quad), so a shard holds whole
+    quads, dssg_index_build_range) holding the distinct cell where the running
+    posting count reaches r/parts of the total (a hot cell is never split).
+    Parts beyond the number of distinct quads hold no cell."""
     if parts < 1:
         raise ValueError("parts must be >= 1")
     cells = np.asarray(cells, dtype=np.uint64)
@@ -58,7 +68,8 @@ def cell_splitters(cells: np.ndarray, parts: int) -> List[Tuple[int, int]]:
         his = [0] * (parts - 1)
     ranges, lo, prev = [], 0, -1
     for hi in his:
-        hi = min(max(hi, prev + 1), U64_MAX - (parts - len(ranges)))  # strictly increasing, room left
+        room = (parts - len(ranges) - 1) * QUAD_SPAN  # a quad span for each part still to come
+        hi = min(quad_end(max(hi, prev + 1)), U64_MAX - room)  # strictly increasing, quad-aligned
         ranges.append((lo, hi))
         lo, prev = hi + 1, hi
     ranges.append((lo, U64_MAX))

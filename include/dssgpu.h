@@ -161,6 +161,11 @@ int dssg_union_volumes_device(dssg_ctx *ctx, int64_t nvol, const int64_t *d_vol_
  * columns with INVERTED INDEX (pkg/rid/cockroach/store.go:122-151).
  * Entity e: cells[cell_offs[e] .. cell_offs[e+1]), altitude [alt_lo, alt_hi],
  * time [t0, t1] (us), owner id (int32, for SearchSubscriptionsByOwner).
+ * Postings are kept per (entity, group of cells), each with the mask of the
+ * entity's cells in the group, at one of two grains picked per build: quads
+ * (level-12 cells, 2 x 2 level-13 cells: when an entity's cells fill them,
+ * >= 1.5 per (entity, quad)) or level-13 cells; dssg_set_tuning
+ * "index_grain" forces one.  Results do not depend on the grain.
  */
 int dssg_index_build(dssg_ctx *ctx, int64_t n, const int64_t *cell_offs, const uint64_t *cells, const float *alt_lo,
                      const float *alt_hi, const int64_t *t0, const int64_t *t1, const int32_t *owner,
@@ -173,7 +178,8 @@ int dssg_index_build_device(dssg_ctx *ctx, int64_t n, const int64_t *d_cell_offs
  * postings only for cells in [cell_lo, cell_hi] (uint64 order), entity cell
  * lists whole, so a (query, entity) pair is emitted by exactly one shard --
  * the one holding their smallest shared cell.  Searches take the full query
- * batch. */
+ * batch.  A range holds whole quads: cell_lo is 0 or a multiple of 2^37 and
+ * cell_hi is UINT64_MAX or ends in 37 one bits (else DSSG_ERR_INVALID). */
 int dssg_index_build_range(dssg_ctx *ctx, int64_t n, const int64_t *cell_offs, const uint64_t *cells,
                            const float *alt_lo, const float *alt_hi, const int64_t *t0, const int64_t *t1,
                            const int32_t *owner, uint64_t cell_lo, uint64_t cell_hi, dssg_index **out);
@@ -183,7 +189,8 @@ int dssg_index_build_range_device(dssg_ctx *ctx, int64_t n, const int64_t *d_cel
                                   dssg_index **out);
 void dssg_index_free(dssg_index *idx);
 int64_t dssg_index_num_postings(const dssg_index *idx);
-int64_t dssg_index_num_cells(const dssg_index *idx);
+int64_t dssg_index_num_cells(const dssg_index *idx);  /* distinct groups (quads or cells) with postings */
+int32_t dssg_index_grain(const dssg_index *idx);      /* S2 level of the posting groups: 12 or 13 */
 
 /* ---- search -------------------------------------------------------------
  * Generic 4D overlap join, the predicate every store search reduces to:
@@ -442,7 +449,9 @@ void dssg_set_timing(dssg_ctx *ctx, int enabled);
  * near-prefix signatures only for the lanes that need them (default 0:
  * always prefetched); "join_shape" = the join's occupancy / pair-stage shape
  * (0: picked per batch from the previous batch's pass density, the default;
- * 1: 7 workgroups per CU with 640-pair stages; 2: 6 with 1024).  Unknown key
+ * 1: 7 workgroups per CU with 640-pair stages; 2: 6 with 1024);
+ * "index_grain" = the posting grain of the indexes this context builds (0:
+ * picked per build, the default; 1: level-13 cells; 2: quads).  Unknown key
  * or value: DSSG_ERR_INVALID. */
 int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value);
 /* Work counters of the most recent search: query-cell keys (cells of the

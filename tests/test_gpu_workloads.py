@@ -43,6 +43,48 @@ def test_config_parity(oracle, cfg, scale, join_path):
         assert idx.info()["long_footprint_postings"] > 0  # the long queue is exercised
 
 
+# The posting grain forced both ways (the build picks one per index: quads
+# for metro / California / corridor footprints, cells for city blocks):
+# identical pair sets, on every join path's default shape.
+@pytest.mark.parametrize("grain", [1, 2])
+@pytest.mark.parametrize("cfg,scale", [(1, 0.02), (2, 0.1), (3, 0.1), (4, 0.01)])
+def test_config_parity_both_grains(oracle, cfg, scale, grain):
+    from dss_amd import _lib, geo, workload as W
+    from dss_amd.store import EntityIndex
+    _, q, qa, it, ia, now = W.config(cfg, scale=scale)
+    ci = geo.cover_batch(it.kind, it.voff, it.lat, it.lng, it.radius_m)
+    cq = geo.cover_batch(q.kind, q.voff, q.lat, q.lng, q.radius_m)
+    tlo, thi = W.query_bounds(qa, now)
+    ctx = _lib.context(0)
+    ctx.set_tuning("index_grain", grain)
+    try:
+        idx = EntityIndex(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1)
+    finally:
+        ctx.set_tuning("index_grain", 0)
+    assert ctx.L.dssg_index_grain(idx.h) == (13 if grain == 1 else 12)
+    if cfg == 3:
+        gq, ge = idx.search_isas_batch(cq.offs, cq.cells, tlo, thi)
+    else:
+        gq, ge = idx.search_operations_batch(cq.offs, cq.cells, qa.alt_lo, qa.alt_hi, qa.t0, qa.t1, now)
+    oq, oe = oracle.search(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1, None, cq.offs, cq.cells, qa.alt_lo,
+                           qa.alt_hi, tlo, thi)
+    assert len(oq) > 0
+    assert np.array_equal(_keys(gq, ge), _keys(oq, oe))
+
+
+def test_grain_picked_by_footprint_shape():
+    """Auto grain: quads for metro footprints (~6 cells, ~2 per quad), cells
+    for RID city blocks (~1.4 cells, ~1.2 per quad)."""
+    from dss_amd import _lib, geo, workload as W
+    from dss_amd.store import EntityIndex
+    ctx = _lib.context(0)
+    for cfg, want in ((1, 12), (3, 13)):
+        _, q, qa, it, ia, now = W.config(cfg, scale=0.01)
+        ci = geo.cover_batch(it.kind, it.voff, it.lat, it.lng, it.radius_m)
+        idx = EntityIndex(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1)
+        assert ctx.L.dssg_index_grain(idx.h) == want, cfg
+
+
 @pytest.fixture(scope="module")
 def corridors_case(oracle):
     """configs[4] corridors at a scale with ~45k long x long occurrences."""
