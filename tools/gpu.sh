@@ -89,6 +89,20 @@ for step in "$@"; do
         [ -n "$KS" ] && cp "$KS" "$D/kernel_stats.csv"
         rm -rf "$P"
         head -${TOP:-20} "$D/pmc_summary.csv" | cut -c1-160 ;;
+    probe)  # probe:N -- rocprofv3 passes over one rank's shard join at world size N (tools/shard_probe.py)
+        T=${TAG}_probe$rest
+        PROBE=$rest STEPS=${PSTEPS:-4} NQ=1000000 NI=10000000 bash tools/profile.sh "$T" > "$O/probe$rest.log" 2>&1 \
+            || { echo PROBE_FAILED; tail -30 "$O/probe$rest.log"; exit 1; }
+        P=gpurun_out/prof/$T
+        D=$O/probe$rest
+        mkdir -p "$D"
+        cp "$P/summary.csv" "$D/pmc_summary.csv"
+        cp "$P/pmc_traffic.json" "$D/" 2>/dev/null
+        grep '^{' "$P/kt.log" > "$D/probe.json" || true
+        KS=$(find "$P" -name 'kt_kernel_stats.csv' | head -1)
+        [ -n "$KS" ] && cp "$KS" "$D/kernel_stats.csv"
+        rm -rf "$P"
+        cat "$D/probe.json"; head -${TOP:-8} "$D/pmc_summary.csv" | cut -c1-160 ;;
     kt)  # kt:CFG:V1,V2[:ARGS] -- kernel-trace summaries of library variants (one pipeline)
         cfg=${rest%%:*}
         r2=${rest#*:}

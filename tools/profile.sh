@@ -10,6 +10,8 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/prof/$TAG
 mkdir -p "$OUT"
 B="$R/bench.py --steps $STEPS --warmup 1 --cpu-sample 0 --survey-model 0 --pipelines 1 --latency 0 --no-verify $BENCH_ARGS"
+# PROBE=N: one rank's shard join at world size N (tools/shard_probe.py, one process)
+[ -n "$PROBE" ] && B="$R/tools/shard_probe.py $PROBE --steps $STEPS --warmup 1 $PROBE_ARGS"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT" -o kt --output-format csv -- python3 $B > "$OUT/kt.log" 2>&1
 [ -n "$KT_ONLY" ] || timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT" -o pmc_fetch --output-format csv -- python3 $B > "$OUT/pmc_fetch.log" 2>&1
