@@ -809,80 +809,59 @@ __global__ void k_qcount(int64_t nq, const uint32_t *perm, const uint32_t *qvali
     rank[q] = (uint32_t)r;
 }
 
-// Per query cell with postings: its key (slot << 1 | wide) and value (the
-// query cell | its query's quantised start << 32: after the sort by cell the
-// unit-range searches probe one 8-B value per step, and no pass gathers the
-// 64-B records for their starts) at off[rank of its query] + its rank among
-// the query's cells with postings -- the queries in order, each query's
-// cells in cell order.
-__global__ void k_qemit(int64_t nqc, const uint32_t *cq, const uint32_t *cslot, const uint32_t *vpre,
-                        const uint32_t *qvb, const uint32_t *rank, const uint32_t *okey, const int64_t *off,
-                        uint32_t *key, uint64_t *val)
+// One record per (query, group) with postings -- the group's first cell in
+// the query's sorted list carries it -- written at its key's position w =
+// off[rank of its query] + its rank among the query's records (the keys in
+// query order, each query's groups in cell order): the key (slot << 1 |
+// wide), its value (w | the query's quantised start << 32: after the sort by
+// slot the unit-range searches probe one 8-B value per step and the join
+// finds the record at the low word) and the 64-B record -- time window,
+// altitudes, owner, flags, the query's cells in the group, and the
+// near-prefix signature of its cells below the group (the prefix's decodes
+// loaded 8 at a time).  (Round 5 fused the key emission into this pass and
+// writes records only where a key points: half the cells of a quad-grain
+// batch carry none.)
+__global__ __launch_bounds__(kBlock) void k_qrecs(QueryView qv, int64_t nqc, const uint32_t *cq, const uint32_t *dec,
+                                                  const uint32_t *cslot, const uint8_t *qlong, const uint32_t *vpre,
+                                                  const uint32_t *qvb, const uint32_t *rank, const uint32_t *okey,
+                                                  const int64_t *off, int gshift, uint32_t *key, uint64_t *val,
+                                                  QRec *recs)
 {
     const int64_t k = tid64();
     if (k >= nqc) return;
-    const uint32_t s = cslot[k];
-    if (s == kNoSlot) return;
-    const uint32_t q = cq[k], r = rank[q];
-    const uint32_t wide = (okey[r] & kWideBit) ? 1u : 0u;
+    const uint32_t sl = cslot[k];
+    if (sl == kNoSlot) return;
+    const uint32_t q = cq[k], r = rank[q], ok = okey[r];
     const int64_t w = off[r] + (int64_t)(vpre[k] - qvb[q]);
-    key[w] = s << 1 | wide;
-    val[w] = (uint64_t)(uint32_t)k | (uint64_t)(okey[r] & (kWideBit - 1u)) << 32;
-}
-
-// One record per query cell: time window, altitudes, owner, flags and the
-// near-prefix signature of the query's cells before this one (the prefix's
-// decodes loaded 8 at a time).  A wave's 64 records leave through LDS as four
-// coalesced 1 KiB stores.
-__global__ __launch_bounds__(kBlock) void k_qrecs(QueryView qv, int64_t nqc, const uint32_t *cq, const uint32_t *dec,
-                                                  const uint32_t *cslot, const uint8_t *qlong, int gshift, QRec *recs)
-{
-    const int64_t k = tid64();
-    if (k - (threadIdx.x & 63) >= nqc) return;  // whole wave past the end
-    QRec r;
-    r.tlo = r.thi = 0;
-    r.alo = r.ahi = 0.f;
-    r.qv = 0;
-    r.own = -1;
-    r.sig[0] = r.sig[1] = r.sig[2] = r.sig[3] = 0;
-    if (k < nqc && cslot[k] != kNoSlot) {  // (a record only where a quad's postings will read it)
-        const uint32_t q = cq[k];
-        const int64_t c0 = qv.offs[q], c1 = qv.offs[q + 1];
-        const uint64_t c = qv.cells[k];
-        uint32_t mask = child_bit(c, gshift);
-        for (int64_t x = k + 1; x < c1 && x < k + 4; x++) {
-            const uint64_t cx = qv.cells[x];
-            if (!same_quad(c, cx, gshift)) break;
-            mask |= child_bit(cx, gshift);
-        }
-        Sig256 sig;
-        bool compact = false;
-        prefix_sig_quad(dec + c0, k - c0, dec[k], sig, compact);
-        r.tlo = qv.tlo[q];
-        r.thi = qv.thi[q];
-        r.alo = qv.alo[q];
-        r.ahi = qv.ahi[q];
-        r.qv = q | (k == c0 ? kRank0 : 0u) | (compact ? kCompactQ : 0u) | (qlong[q] ? kLongQ : 0u) |
-               (mask << kQMaskShift);
-        r.own = qv.owner ? qv.owner[q] : -1;
-        r.sig[0] = sig.w[0];
-        r.sig[1] = sig.w[1];
-        r.sig[2] = sig.w[2];
-        r.sig[3] = sig.w[3];
+    key[w] = sl << 1 | ((ok & kWideBit) ? 1u : 0u);
+    val[w] = (uint64_t)w | (uint64_t)(ok & (kWideBit - 1u)) << 32;
+    const int64_t c0 = qv.offs[q], c1 = qv.offs[q + 1];
+    const uint64_t c = qv.cells[k];
+    uint32_t mask = child_bit(c, gshift);
+    for (int64_t x = k + 1; x < c1 && x < k + 4; x++) {
+        const uint64_t cx = qv.cells[x];
+        if (!same_quad(c, cx, gshift)) break;
+        mask |= child_bit(cx, gshift);
     }
-    __shared__ int4 stage[kBlock / 64][64 * 4];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int4 *rr = reinterpret_cast<const int4 *>(&r);
+    Sig256 sig;
+    bool compact = false;
+    prefix_sig_quad(dec + c0, k - c0, dec[k], sig, compact);
+    QRec rec;
+    rec.tlo = qv.tlo[q];
+    rec.thi = qv.thi[q];
+    rec.alo = qv.alo[q];
+    rec.ahi = qv.ahi[q];
+    rec.qv = q | (k == c0 ? kRank0 : 0u) | (compact ? kCompactQ : 0u) | (qlong[q] ? kLongQ : 0u) |
+             (mask << kQMaskShift);
+    rec.own = qv.owner ? qv.owner[q] : -1;
+    rec.sig[0] = sig.w[0];
+    rec.sig[1] = sig.w[1];
+    rec.sig[2] = sig.w[2];
+    rec.sig[3] = sig.w[3];
+    const int4 *src = reinterpret_cast<const int4 *>(&rec);
+    int4 *dst = reinterpret_cast<int4 *>(recs + w);
 #pragma unroll
-    for (int u = 0; u < 4; u++) stage[wv][4 * lane + u] = rr[u];
-    __builtin_amdgcn_wave_barrier();  // one wave writes and reads its own slice, in order
-    const int64_t kw = k - lane;
-    int4 *dst = reinterpret_cast<int4 *>(recs + kw);
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-        const int c = 64 * u + lane;
-        if (kw + (c >> 2) < nqc) dst[c] = stage[wv][c];
-    }
+    for (int u = 0; u < 4; u++) dst[u] = src[u];
 }
 
 // Lower / upper bound over a slot's regular postings (sorted by m).
@@ -2394,11 +2373,9 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     exclusive_scan_i64(qc, qo, nq, tmp2_, s);
     uint32_t *key = kkey_.ensure(nqc + 1), *skey = kkey2_.ensure(nqc + 1);
     uint64_t *val = kv64_.ensure(nqc + 1), *sval = kv64b_.ensure(nqc + 1);
-    hipLaunchKernelGGL(k_qemit, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, nqc, cq, cslot, vpre, qvb, qrank, ok1,
-                       qo, key, val);
     QRec *recs = (QRec *)rec_.ensure(sizeof(QRec) * (nqc + 1));
-    hipLaunchKernelGGL(k_qrecs, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, qv, nqc, cq, dec, cslot, qlong,
-                       idx->gshift, recs);
+    hipLaunchKernelGGL(k_qrecs, dim3(grid_for(nqc, kBlock)), dim3(kBlock), 0, s, qv, nqc, cq, dec, cslot, qlong, vpre,
+                       qvb, qrank, ok1, qo, idx->gshift, key, val, recs);
     // (4) group the keys by cell (stable: each cell's records stay in query
     // order), over the device key count qo[nq] (<= nqc)
     const int64_t *dnkeys = qo + nq;
