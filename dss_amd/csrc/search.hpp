@@ -29,7 +29,12 @@ struct dssg_index {
     dss::DevBuf<uint64_t> irr_cells;  // n_irr, sorted
     dss::DevBuf<uint64_t> s_post;     // n_slots + 1: first posting of each slot
     dss::DevBuf<uint32_t> s_nreg;     // n_slots: regular-duration postings of the slot
-    dss::DevBuf<uint8_t> s_lfp;       // n_slots: 1 = the slot holds a long-footprint posting (join variant)
+    // long-footprint tiles: per slot 0, or 1 + the bit offset in lfp_bits of
+    // its join tiles (64-posting tiles of the regular part, then of the
+    // long-duration part: k_units' tiling), a set bit = the tile holds a
+    // long-footprint posting and goes to the long join variant
+    dss::DevBuf<uint64_t> s_lfpb;
+    dss::DevBuf<unsigned long long> lfp_bits;
     // ---- time --------------------------------------------------------------------
     int64_t dcap = 0;      // max duration of a regular posting's entity (us)
     int gshift = 37;       // posting groups: cell >> gshift (37: quads = level-12 cells, 35: level-13 cells)
