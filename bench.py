@@ -53,8 +53,8 @@ _JSON_FD = [None]
 # hung (a peer that never issued its side of a collective); the process exits
 # non-zero instead of holding its GPU until an outside timeout (the launcher
 # then stops the other ranks).
-STAGE_LIMIT_S = {"warmup": 900, "timed steps": 900, "replica rate beside the sharded one": 900,
-                 "sharded phases": 900}
+STAGE_LIMIT_S = {"native exchange init": 300, "warmup": 900, "timed steps": 900,
+                 "replica rate beside the sharded one": 900, "sharded phases": 900}
 
 
 def keep_stdout_for_json():
@@ -512,20 +512,32 @@ def main():
             # stream); if any rank cannot open them (no RCCL to dlopen, init
             # error) every rank falls back to the torch exchange, agreed by
             # one all-reduce, and the line says so
+            stage("native exchange init")
             ok = torch.ones(1)
             err = None
-            try:
-                comms = []
-                for _ in range(2):
-                    uid = torch.zeros(_lib.COMM_ID_BYTES, dtype=torch.uint8)
-                    if rank == 0:
-                        uid.copy_(torch.frombuffer(bytearray(shard.NativeComm.unique_id(ctx)), dtype=torch.uint8))
-                    dist.broadcast(uid, 0)  # bootstrap only: the id travels once
-                    comms.append(shard.NativeComm(ctx, world, rank, bytes(uid.numpy())))
-                native = shard.NativeShardedSearch(ctx, comms[0], index, ranges, xcomm=comms[1],
-                                                   xstream=torch.cuda.Stream(device=dev))
-            except Exception as e:  # noqa: BLE001 -- reported in the result line
-                err = f"{type(e).__name__}: {e}"
+            # the ids travel once over the control group, with rank 0's
+            # success flag: every rank takes part in every broadcast, and no
+            # rank starts a communicator init another rank will not join
+            uids = torch.zeros(2, _lib.COMM_ID_BYTES + 1, dtype=torch.uint8)
+            if rank == 0:
+                try:
+                    for k in range(2):
+                        uids[k, :-1].copy_(torch.frombuffer(bytearray(shard.NativeComm.unique_id(ctx)),
+                                                            dtype=torch.uint8))
+                        uids[k, -1] = 1
+                except Exception as e:  # noqa: BLE001 -- reported in the result line
+                    err = f"{type(e).__name__}: {e}"
+            dist.broadcast(uids, 0)
+            if int(uids[:, -1].min()) == 1:
+                try:
+                    comms = [shard.NativeComm(ctx, world, rank, bytes(uids[k, :-1].numpy())) for k in range(2)]
+                    native = shard.NativeShardedSearch(ctx, comms[0], index, ranges, xcomm=comms[1],
+                                                       xstream=torch.cuda.Stream(device=dev))
+                except Exception as e:  # noqa: BLE001 -- reported in the result line
+                    err = f"{type(e).__name__}: {e}"
+                    ok.zero_()
+            else:
+                err = err or "rank 0 could not make an RCCL id"
                 ok.zero_()
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
             if ok.item() < 1:

@@ -49,8 +49,7 @@ struct IndexView {
     const uint64_t *irr_cells;
     const uint64_t *s_post;
     const uint32_t *s_nreg;
-    const uint64_t *s_lfpb;                  // per slot: 0, or 1 + the bit offset of its tile flags
-    const unsigned long long *lfp_bits;      // tile flags: the tile holds a long-footprint posting
+    const uint8_t *s_lfp;
     const uint32_t *b_e;
     const uint8_t *b_meta;
     const float2 *b_alt;
@@ -76,8 +75,7 @@ IndexView view_of(const dssg_index *idx)
     v.irr_cells = idx->irr_cells.p;
     v.s_post = idx->s_post.p;
     v.s_nreg = idx->s_nreg.p;
-    v.s_lfpb = idx->s_lfpb.p;
-    v.lfp_bits = idx->lfp_bits.p;
+    v.s_lfp = idx->s_lfp.p;
     v.b_e = idx->b_e.p;
     v.b_meta = idx->b_meta.p;
     v.b_alt = idx->b_alt.p;

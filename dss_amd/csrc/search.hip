@@ -571,59 +571,10 @@ __global__ void k_slot_counts(int64_t ns, const uint32_t *sfirst, const uint32_t
 
 // Slots holding a long-footprint posting: their join units take the long
 // join variant (the others' postings all have compact prefixes).
-// Join tiles (k_units' tiling: kTile postings from the slot's start for
-// the regular part, then from its end of the regular part for the
-// long-duration part) per slot: slots holding a long-footprint posting count
-// theirs (lfp_n), the others 0.
-constexpr uint32_t kTile = 64;
-__global__ void k_slot_lfp(int64_t NP, const uint32_t *key, const uint8_t *b_meta, uint8_t *mark)
+__global__ void k_slot_lfp(int64_t NP, const uint32_t *key, const uint8_t *b_meta, uint8_t *s_lfp)
 {
     const int64_t j = tid64();
-    if (j < NP && (b_meta[j] & kMetaLongFp)) mark[key[j] >> 1] = 1;
-}
-__global__ void k_lfp_tiles(int64_t ns, const uint8_t *mark, const uint64_t *s_post, const uint32_t *s_nreg,
-                            int64_t *lfp_n)
-{
-    const int64_t s = tid64();
-    if (s >= ns) return;
-    int64_t t = 0;
-    if (mark[s]) {
-        const uint64_t n = s_post[s + 1] - s_post[s], nr = s_nreg[s];
-        t = (int64_t)((nr + kTile - 1) / kTile + (n - nr + kTile - 1) / kTile);
-    }
-    lfp_n[s] = t;
-}
-// The tile flags: bit (base of the slot + its tile) for every long-footprint
-// posting (one atomicOr per such posting: they are few), and s_lfpb.
-__global__ void k_lfp_flags(int64_t NP, const uint32_t *key, const uint8_t *b_meta, const uint64_t *s_post,
-                            const uint32_t *s_nreg, const int64_t *lfp_off, unsigned long long *bits)
-{
-    const int64_t j = tid64();
-    if (j >= NP || !(b_meta[j] & kMetaLongFp)) return;
-    const uint32_t s = key[j] >> 1;
-    const uint64_t s0 = s_post[s], sr = s0 + s_nreg[s];
-    const uint64_t t = (uint64_t)j < sr ? ((uint64_t)j - s0) / kTile : (sr - s0 + kTile - 1) / kTile + ((uint64_t)j - sr) / kTile;
-    const uint64_t b = (uint64_t)lfp_off[s] + t;
-    atomicOr(&bits[b >> 6], 1ull << (b & 63));
-}
-__global__ void k_lfp_base(int64_t ns, const int64_t *lfp_n, const int64_t *lfp_off, uint64_t *s_lfpb)
-{
-    const int64_t s = tid64();
-    if (s < ns) s_lfpb[s] = lfp_n[s] ? (uint64_t)lfp_off[s] + 1 : 0;
-}
-// Set bits of the flag bitmap in [b, b + n).
-__device__ __forceinline__ uint32_t bits_in(const unsigned long long *bits, uint64_t b, uint64_t n)
-{
-    uint32_t c = 0;
-    while (n) {
-        const uint32_t o = (uint32_t)(b & 63);
-        const uint64_t take = min(n, (uint64_t)(64 - o));
-        const unsigned long long w = bits[b >> 6] >> o;
-        c += (uint32_t)__popcll(take == 64 ? w : (w & ((1ull << take) - 1)));
-        b += take;
-        n -= take;
-    }
-    return c;
+    if (j < NP && (b_meta[j] & kMetaLongFp)) s_lfp[key[j] >> 1] = 1;
 }
 
 __global__ void k_owner_keys(int64_t n, const int32_t *owner, uint32_t *key, uint32_t *val)
@@ -1046,9 +997,8 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
                                                   int qshift)
 {
     __shared__ uint32_t s_xa[kBlock / 64][64];
-    __shared__ uint64_t s_s0[kBlock / 64][64], s_sr[kBlock / 64][64], s_s1[kBlock / 64][64], s_bs[kBlock / 64][64],
-        s_bl[kBlock / 64][64], s_lb[kBlock / 64][64];
-    __shared__ uint4 s_par[kBlock / 64][64];  // ntr, slot, first wide record, record end
+    __shared__ uint64_t s_s0[kBlock / 64][64], s_sr[kBlock / 64][64], s_s1[kBlock / 64][64], s_bu[kBlock / 64][64];
+    __shared__ uint4 s_par[kBlock / 64][64];  // ntr | lfp << 31, slot, first wide record, record end
     const int lane = threadIdx.x & 63;
     const uint32_t nkeys = (uint32_t)*dnkeys;
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
@@ -1067,8 +1017,8 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
         const bool cstart = valid && (p == 0 || (prev >> 1) != (key >> 1));
         const bool wstart = valid && (key & 1u) && (p == 0 || prev != key);
         const unsigned long long cm = __ballot(cstart), wm = __ballot(wstart);
-        uint32_t nu = 0, rw = 0, re = 0, slot = key >> 1, ntr = 0, nl = 0;
-        uint64_t lb = 0;  // the cell's tile flags (0: no long-footprint posting: every tile to the short queue)
+        uint32_t nu = 0, rw = 0, re = 0, slot = key >> 1, ntr = 0;
+        bool lfp = false;  // the cell holds long-footprint postings: its units go to the long queue
         uint64_t s0 = 0, sr = 0, s1 = 0;
         if (cstart) {
             const unsigned long long above = lane == 63 ? 0ull : (cm >> (lane + 1)) << (lane + 1);
@@ -1085,10 +1035,9 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
             sr = s0 + a.s_nreg[slot];
             ntr = (uint32_t)((sr - s0 + tp - 1) / tp);
             nu = ntr + (uint32_t)((s1 - sr + tp - 1) / tp);
-            lb = a.s_lfpb[slot];
-            if (lb) nl = bits_in(a.lfp_bits, lb - 1, nu);  // its tiles holding a long-footprint posting
+            lfp = a.s_lfp[slot] != 0;
         }
-        const uint32_t ns_ = nu - nl, nl_ = nl;
+        const uint32_t ns_ = lfp ? 0u : nu, nl_ = lfp ? nu : 0u;
         const uint32_t xs = wave_incl_scan(ns_), xl = wave_incl_scan(nl_);
         const uint32_t tots = (uint32_t)__builtin_amdgcn_readlane((int)xs, 63);
         const uint32_t totl = (uint32_t)__builtin_amdgcn_readlane((int)xl, 63);
@@ -1109,10 +1058,8 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
         s_s0[wv][lane] = s0;
         s_sr[wv][lane] = sr;
         s_s1[wv][lane] = s1;
-        s_bs[wv][lane] = bs;
-        s_bl[wv][lane] = bl;
-        s_lb[wv][lane] = lb;
-        s_par[wv][lane] = make_uint4(ntr, slot, rw, re);
+        s_bu[wv][lane] = lfp ? bl : bs;
+        s_par[wv][lane] = make_uint4(ntr | (lfp ? 0x80000000u : 0u), slot, rw, re);
         __builtin_amdgcn_wave_barrier();
         for (uint32_t u = (uint32_t)lane; u < tot; u += 64) {
             int lo = 0, hi = 63;  // the first lane L with s_xa[L] > u
@@ -1123,13 +1070,8 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
             }
             const uint32_t t = u - (lo ? s_xa[wv][lo - 1] : 0u);  // the unit's tile within its cell
             const uint4 pr = s_par[wv][lo];
-            const uint32_t lntr = pr.x;
-            // the long queue takes the tiles flagged as holding a
-            // long-footprint posting; a tile's place in its queue is its rank
-            // among the cell's tiles of the same kind
-            const uint64_t llb = s_lb[wv][lo];
-            const bool llfp = llb && ((a.lfp_bits[(llb - 1 + t) >> 6] >> ((llb - 1 + t) & 63)) & 1ull);
-            const uint32_t nlb = llb ? bits_in(a.lfp_bits, llb - 1, t) : 0u;  // flagged tiles before this one
+            const uint32_t lntr = pr.x & 0x7fffffffu;
+            const bool llfp = (pr.x >> 31) != 0;
             const uint64_t l0 = s_s0[wv][lo], lr = s_sr[wv][lo], l1 = s_s1[wv][lo];
             Unit d;
             const bool lng = t >= lntr;
@@ -1143,7 +1085,7 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
             d.w0 = lng ? pr.w : pr.z;
             d.w1 = pr.w;
             unit_ranges(a, d, sq, dq, tbase, qshift);  // a regular tile's record sub-ranges
-            const unsigned long long wpos = llfp ? s_bl[wv][lo] + nlb : s_bs[wv][lo] + (t - nlb);
+            const unsigned long long wpos = s_bu[wv][lo] + t;
             const Regions &dr = llfp ? url : ur;
             Unit *du = llfp ? units_l : units;
             if ((int64_t)wpos < dr.cap) du[reg * dr.cap + (int64_t)wpos] = d;
@@ -2315,23 +2257,9 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
         exclusive_scan_i64(cnt, off, ns, tmp2_, s);
         uint64_t *sp = idx->s_post.ensure_exact(ns + 1);
         hipLaunchKernelGGL(k_u64_store, dim3(grid_for(ns + 1, kBlock)), dim3(kBlock), 0, s, ns + 1, off, sp);
-        // long-footprint tiles (k_units sends them, and only them, to the
-        // long join variant)
-        DevBuf<uint8_t> mark_b;
-        uint8_t *mark = mark_b.ensure(ns + 1);
-        DSS_HIP(hipMemsetAsync(mark, 0, ns + 1, s));
-        if (NP) hipLaunchKernelGGL(k_slot_lfp, dim3(grid_for(NP, kBlock)), dim3(kBlock), 0, s, NP, key2, b_meta, mark);
-        int64_t *lfp_n = c_b.ensure(ns + 1), *lfp_off = o_b.ensure(ns + 2);  // (the slot counts are spent)
-        if (ns) hipLaunchKernelGGL(k_lfp_tiles, dim3(grid_for(ns, kBlock)), dim3(kBlock), 0, s, ns, mark, sp, nreg, lfp_n);
-        exclusive_scan_i64(lfp_n, lfp_off, ns, tmp2_, s);
-        const int64_t ntiles = fetch(lfp_off + ns, s);
-        unsigned long long *bits = idx->lfp_bits.ensure_exact((size_t)(ntiles + 63) / 64 + 1);
-        DSS_HIP(hipMemsetAsync(bits, 0, sizeof(unsigned long long) * ((size_t)(ntiles + 63) / 64 + 1), s));
-        if (NP && ntiles)
-            hipLaunchKernelGGL(k_lfp_flags, dim3(grid_for(NP, kBlock)), dim3(kBlock), 0, s, NP, key2, b_meta, sp, nreg,
-                               lfp_off, bits);
-        uint64_t *lfpb = idx->s_lfpb.ensure_exact(ns + 1);
-        if (ns) hipLaunchKernelGGL(k_lfp_base, dim3(grid_for(ns, kBlock)), dim3(kBlock), 0, s, ns, lfp_n, lfp_off, lfpb);
+        uint8_t *lfp = idx->s_lfp.ensure_exact(ns + 1);
+        DSS_HIP(hipMemsetAsync(lfp, 0, ns + 1, s));
+        if (NP) hipLaunchKernelGGL(k_slot_lfp, dim3(grid_for(NP, kBlock)), dim3(kBlock), 0, s, NP, key2, b_meta, lfp);
     }
     stage_check(s, "index build: slot table");
     // (8) entity-level attributes: ends_at, owner, owner -> entities, counters
@@ -2467,7 +2395,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         n_cu_ = ncu > 0 ? ncu : 256;
     }
     int64_t ucap = std::max<int64_t>(units_cap_hint_, 1024);  // per region
-    // tiles holding a long-footprint posting (idx->lfp_bits) go to a second
+    // units of cells with long-footprint postings (idx->s_lfp) go to a second
     // set of queues joined by the long variant; the rest by the short one
     const bool any_long = idx->n_long_fp > 0;
     int64_t ucap_l = any_long ? std::max<int64_t>(units_cap_hint_l_, 1024) : 0;
@@ -2479,7 +2407,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         DSS_HIP(hipMemsetAsync(ctl + kCtlUnits, 0, kR * sizeof(unsigned long long), s));
         DSS_HIP(hipMemsetAsync(ctl + kCtlUnitsL, 0, kR * sizeof(unsigned long long), s));
         hipLaunchKernelGGL(k_units, dim3(ugrid), dim3(kBlock), 0, s, ix, skey, dnkeys, Regions{ctl + kCtlUnits, ucap},
-                           units, Regions{ctl + kCtlUnitsL, ucap_l}, units_l, kTile, sq,
+                           units, Regions{ctl + kCtlUnitsL, ucap_l}, units_l, 64u, sq,
                            (const unsigned long long *)(ctl + kCtlDq), (long long)idx->tbase, idx->qshift);
     };
     build_units();
@@ -2539,7 +2467,21 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             auto klong = q_owner ? k_join<true, true, false> : k_join<false, true, false>;
             JoinArgs jl = ja;
             jl.ur = Regions{ctl + kCtlUnitsL, ucap_l};
-            hipLaunchKernelGGL(klong, dim3(nblocks), dim3(64 * kWaves), 0, s, jl, (const QRec *)recs,
+            // sized by the previous batch's long units (>= ~8 per wave), at
+            // most what fits at the variant's occupancy: its waves loop over
+            // the queue until it is drained, and every idle wave still visits
+            // the 8 region counters -- a full-chip launch over a few
+            // thousand units cost configs[2] ~0.2 ms
+            if (occ_long_ == 0) {
+                int occ = 0;
+                DSS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void *>(klong),
+                                                                     64 * kWaves, 0));
+                occ_long_ = std::max(1, occ);
+            }
+            const int64_t want = (long_units_prev_ + 8 * kWaves - 1) / (8 * kWaves);
+            const unsigned lblocks = (unsigned)std::max<int64_t>(
+                std::min<int64_t>((int64_t)n_cu_ * occ_long_, std::max<int64_t>(want, n_cu_)), 1);
+            hipLaunchKernelGGL(klong, dim3(lblocks), dim3(64 * kWaves), 0, s, jl, (const QRec *)recs,
                                (const uint64_t *)sval, (const Unit *)units_l, ctl + kCtlQueueL);
         }
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
@@ -2561,6 +2503,9 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             build_units();
             continue;
         }
+        int64_t nul = 0;
+        for (int r = 0; r < kRegions; r++) nul += (int64_t)h[kCtlUnitsL + r * kRegStride];
+        long_units_prev_ = nul;
         units_cap_hint_ = std::max<int64_t>(units_cap_hint_, umax + umax / 8);
         units_cap_hint_l_ = std::max<int64_t>(units_cap_hint_l_, umax_l + umax_l / 8);
         bool rerun = false;

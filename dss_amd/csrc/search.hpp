@@ -29,12 +29,7 @@ struct dssg_index {
     dss::DevBuf<uint64_t> irr_cells;  // n_irr, sorted
     dss::DevBuf<uint64_t> s_post;     // n_slots + 1: first posting of each slot
     dss::DevBuf<uint32_t> s_nreg;     // n_slots: regular-duration postings of the slot
-    // long-footprint tiles: per slot 0, or 1 + the bit offset in lfp_bits of
-    // its join tiles (64-posting tiles of the regular part, then of the
-    // long-duration part: k_units' tiling), a set bit = the tile holds a
-    // long-footprint posting and goes to the long join variant
-    dss::DevBuf<uint64_t> s_lfpb;
-    dss::DevBuf<unsigned long long> lfp_bits;
+    dss::DevBuf<uint8_t> s_lfp;       // n_slots: 1 = the slot holds a long-footprint posting (join variant)
     // ---- time --------------------------------------------------------------------
     int64_t dcap = 0;      // max duration of a regular posting's entity (us)
     int gshift = 37;       // posting groups: cell >> gshift (37: quads = level-12 cells, 35: level-13 cells)
@@ -161,6 +156,8 @@ class SearchEngine {
     int64_t out_rcap_ = 0;  // output slots per region
     int64_t tag_rcap_ = 0;  // tagged-key slots per region
     int64_t units_cap_hint_ = 0, units_cap_hint_l_ = 0;
+    int64_t long_units_prev_ = INT64_MAX / 2;  // the previous batch's long-variant units (sizes its launch)
+    int occ_long_ = 0;                         // long-variant workgroups per CU
     bool timing_ = false;
     int64_t tag_bucket_avg_ = 2048;
     int64_t lazy_sig_recs_ = 0;
