@@ -391,22 +391,26 @@ def cover_ahead_steps(torch, D, ctx, covers, d_q, steps, search_fn):
     threads = [threading.Thread(target=cover_loop, args=(p,), daemon=True) for p in range(P)]
     for th in threads:
         th.start()
-    main = torch.cuda.current_stream()
+    # an explicit stream (never the default one, whose handle 0 sends the
+    # library to the context's own non-blocking stream, which the waits
+    # below would not order): the step's kernels run after its covering
+    main = torch.cuda.Stream()
     finished = 0
     try:
-        for k in range(steps):
-            item = ready[k % P].get()
-            if item is None:
-                raise StepFailure(f"a cover pipeline failed in the timed steps ({finished} of {steps} steps "
-                                  f"finished): {type(err[0]).__name__}: {err[0]}") from err[0]
-            c, ev = item
-            main.wait_event(ev)
-            search_fn(c)
-            finished += 1
-            ev_done = torch.cuda.Event()
-            ev_done.record(main)
-            done[k % P] = ev_done
-            free[k % P].release()
+        with torch.cuda.stream(main):
+            for k in range(steps):
+                item = ready[k % P].get()
+                if item is None:
+                    raise StepFailure(f"a cover pipeline failed in the timed steps ({finished} of {steps} steps "
+                                      f"finished): {type(err[0]).__name__}: {err[0]}") from err[0]
+                c, ev = item
+                main.wait_event(ev)
+                search_fn(c)
+                finished += 1
+                ev_done = torch.cuda.Event()
+                ev_done.record(main)
+                done[k % P] = ev_done
+                free[k % P].release()
     finally:
         if finished != steps:  # release the cover threads so they end
             stop.set()

@@ -33,7 +33,7 @@ class _Event:
 
 def fake_torch():
     cuda = types.SimpleNamespace(stream=lambda s: contextlib.nullcontext(), current_stream=lambda: _Stream(),
-                                 Event=_Event)
+                                 Stream=_Stream, Event=_Event)
     return types.SimpleNamespace(cuda=cuda)
 
 
