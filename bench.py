@@ -15,16 +15,20 @@ HBM.  The index (intent coverings + posting lists) is built before timing.
 Ranks: one process per GPU.  Under torchrun (WORLD_SIZE set) each process is
 one rank; `--gpus N` without a launcher starts the N rank processes itself
 (self_launch) before anything touches a GPU.  --mode:
-  sharded (default on N > 1; BASELINE's layout): the intent
-    index is split into N uint64 cell ranges at posting quantiles, one shard
-    per GPU.  Each rank covers its own 1M queries, routes every query (row +
-    whole cell list) to the shards owning its cells (all-to-all over
+  replica (the default at every N): each rank holds the whole index (a few
+    GB of its 288 GB of HBM) and covers + joins its own 1M-query batch; the
+    query batches are the units sharded across ranks, with no collective on
+    the data path.  "scaling": "weak" (1M queries per GPU).
+  sharded (--mode sharded; BASELINE's cell-range layout): the
+    intent index is split into N uint64 cell ranges at posting quantiles, one
+    shard per GPU.  Each rank covers its own 1M queries, routes every query
+    (row + whole cell list) to the shards owning its cells (all-to-all over
     RCCL/xGMI, the library's own communicator), joins what it receives
     against its shard, and routes the pairs back to their queries' home ranks
-    (second all-to-all).  "scaling": "weak" (1M queries per GPU).  The
-    replica rate (same pipelines, no exchange) is reported beside it.
-  replica (default on one GPU): the rank holds the whole index and covers +
-    joins its own batch; no collective on the data path.
+    (second all-to-all).  The replica rate is reported beside it.  Not the
+    default: at N = 8 about 7/8 of a step's ~256M pairs cross ranks, ~1.8 GB
+    per rank per step against a ~4 ms step, while the whole index fits every
+    GPU many times over.
 Timing: barrier + synchronize on both sides of exactly --steps steps, max
 over ranks.
 """
@@ -126,9 +130,9 @@ def parse_args(argv=None):
                     help="CPU-baseline threads (0: the process's CPU share -- the affinity mask, capped by "
                          "OMP_NUM_THREADS, which the GPU box sets to its per-GPU share of 16)")
     ap.add_argument("--mode", choices=["sharded", "replica"], default=None,
-                    help="multi-GPU layout: sharded (index split by S2 cell range, queries and pairs exchanged by "
-                         "all-to-all; the default on N > 1 GPUs, BASELINE's layout, with the replica rate reported "
-                         "beside it) or replica (index on every GPU, queries split; the default on one GPU)")
+                    help="multi-GPU layout: replica (index on every GPU, query batches split across ranks, no "
+                         "data-path collective; the default) or sharded (index split by S2 cell range, queries and "
+                         "pairs exchanged by all-to-all, BASELINE's layout, with the replica rate reported beside it)")
     ap.add_argument("--exchange", choices=["native", "torch"], default=None,
                     help="sharded mode's all-to-alls: native (the library's own RCCL communicator, "
                          "dssg_sharded_search_device) or torch (torch.distributed; the instrumented path).  Default: "
@@ -439,7 +443,7 @@ def main():
     if world != args.gpus:
         log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}; the line reports n_gpus = WORLD_SIZE")
     local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", 0))
-    mode = args.mode or ("sharded" if world > 1 else "replica")
+    mode = args.mode or "replica"
     exchange = args.exchange or ("native" if args.dist_backend == "nccl" else "torch")
     torch.cuda.set_device(local)
     # The process group is the control plane (rendezvous, barriers, the
