@@ -1247,7 +1247,7 @@ struct JoinArgs {
 // the fused altitude/time/owner predicate is one wave mask; the
 // smallest-shared-cell rule (SQL DISTINCT, Q13) compares the record's
 // near-prefix signature (broadcast) with each lane's posting signature.
-template <bool OWNER, bool LONG, bool DENSE>
+template <bool OWNER, bool LONG, bool DENSE, bool QUADS>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LONG ? kJoinLongWpe : DENSE ? kJoinBpcDense : kJoinBpcSparse))) void k_join(JoinArgs a, const QRec *__restrict__ recs,
                                                       const uint64_t *__restrict__ sval,
                                                       const Unit *__restrict__ units,
@@ -1262,7 +1262,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const IndexView &ix = a.ix;
-    const bool quads = ix.gshift == kQuadShift;  // (kernel argument: uniform)
     WaveOut out, tout;  // pairs, tagged keys
     unsigned long long n_tests = 0, n_bcast = 0;
     // units: kRegions queues (the unit regions), a wave starts on its own
@@ -1410,7 +1409,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 // one ballot per child, ORed over the posting's children (at
                 // the cell grain every mask is 1: all records meet)
                 unsigned long long meets = ~0ull;
-                if (quads) {
+                if constexpr (QUADS) {  // (a template parameter: a runtime flag here cost the quad join ~3 %)
                     const unsigned long long Q0 = __ballot((qslot >> kQMaskShift) & 1u);
                     const unsigned long long Q1 = __ballot((qslot >> (kQMaskShift + 1)) & 1u);
                     const unsigned long long Q2 = __ballot((qslot >> (kQMaskShift + 2)) & 1u);
@@ -2459,12 +2458,16 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         ja.out = OutArgs{oq, oe, OutStream{out_rcap_, fills, ctl + kCtlOut}, tk, OutStream{tag_rcap_, tfills, ctl + kCtlTOut},
                          eb, hbm, cnt};
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
-        auto kshort = dense ? (q_owner ? k_join<true, false, true> : k_join<false, false, true>)
-                            : (q_owner ? k_join<true, false, false> : k_join<false, false, false>);
+        const bool quads = idx->gshift == kQuadShift;
+        auto kshort = quads ? (dense ? (q_owner ? k_join<true, false, true, true> : k_join<false, false, true, true>)
+                                     : (q_owner ? k_join<true, false, false, true> : k_join<false, false, false, true>))
+                            : (dense ? (q_owner ? k_join<true, false, true, false> : k_join<false, false, true, false>)
+                                     : (q_owner ? k_join<true, false, false, false> : k_join<false, false, false, false>));
         hipLaunchKernelGGL(kshort, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
                            (const uint64_t *)sval, (const Unit *)units, ctl + kCtlQueue);
         if (any_long) {  // the same output streams, continued
-            auto klong = q_owner ? k_join<true, true, false> : k_join<false, true, false>;
+            auto klong = quads ? (q_owner ? k_join<true, true, false, true> : k_join<false, true, false, true>)
+                               : (q_owner ? k_join<true, true, false, false> : k_join<false, true, false, false>);
             JoinArgs jl = ja;
             jl.ur = Regions{ctl + kCtlUnitsL, ucap_l};
             // sized by the previous batch's long units (>= ~8 per wave), at
