@@ -361,7 +361,7 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
                                           uint32_t *st_j, uint32_t *finfo, uint4 *fbox,
                                           const double *fwd, const double *rev, const uint8_t *fan_fail,
                                           const uint8_t *not_inner, const uint8_t *omode, uint8_t *rev_out,
-                                          const uint8_t *bad_in)
+                                          const uint8_t *bad_in, const CircleFrame *frames)
 {
     bool fail = false;
     if constexpr (FAST) rev_out[f] = 0;  // (set before any bail: the exact instance reverses in place itself)
@@ -407,7 +407,19 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
             }
             nv = 20;
             l.n = 20;
-            origin_of<FAST>(l, fail);
+            // RegularLoop is simple and lies in its cap (centre, radius):
+            // OriginPoint clearly outside the cap is outside the loop, which
+            // is what initOriginAndBound's crossing walk finds there (the
+            // circles' walks were ~0.05 of k_setup's 0.37 ms on configs[2])
+            bool far = false;
+            if constexpr (FAST) {
+                const CircleFrame &F = frames[f];
+                const V3 o = origin_point();
+                far = radius > 1e-7 && radius < 0.5 &&
+                      F.c.x * o.x + F.c.y * o.y + F.c.z * o.z < F.z - 1e-6 * F.rr - 1e-12;  // angle > radius + 1e-6
+            }
+            if (far) l.origin_inside = false;
+            else origin_of<FAST>(l, fail);
             if (bail()) return;
             md = MODE_LOOP;
             small = radius < 0.5;
@@ -587,7 +599,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAST ? DSS_S
                         uint64_t *st_id, uint32_t *st_i, uint32_t *st_j, uint32_t *finfo,
                         uint4 *fbox, const double *fwd, const double *rev, const uint8_t *fan_fail,
                         const uint8_t *not_inner, const uint8_t *omode, const uint32_t *perm, uint8_t *rev_out,
-                        const uint8_t *bad_in)
+                        const uint8_t *bad_in, const CircleFrame *frames)
 {
     int64_t f = tid64();
     if constexpr (FAST) {
@@ -597,12 +609,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAST ? DSS_S
         for (int64_t i = f; i < (int64_t)*slow_n; i += (int64_t)gridDim.x * blockDim.x)
             setup_one<false>(slow_list[i], nullptr, nullptr, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out,
                              mode, origin_in, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, nullptr,
-                             nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                             nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
         return;
     }
     setup_one<true>(f, slow_list, slow_n, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out, mode, origin_in,
                     fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, fwd, rev, fan_fail, not_inner, omode,
-                    rev_out, bad_in);
+                    rev_out, bad_in, frames);
 }
 
 // Q4's in-place reversal, moved out of k_setup<true> (its serial walk of a
@@ -2061,6 +2073,8 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     if (nx > 0) {
         hipLaunchKernelGGL(k_verts, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, kind, voff, lat, lng, xoff, frames, xyz,
                            bad);
+        // (k_fan fused into k_verts -- neighbours by shuffle, recomputed across
+        // wave edges -- measured slower: 0.355 against 0.317 ms, r05v)
         hipLaunchKernelGGL(k_fan, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, nv, xoff, xyz, uv, not_inner);
     }
     // fan triangle terms of Loop.Area: orientation first, then one thread per
@@ -2074,7 +2088,7 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     uint8_t *rev_flag = revf_.ensure(n + 1);
     hipLaunchKernelGGL(k_setup<true>, dim3(grid_for(n, 64)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng,
                        radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo,
-                       fbox, fwd, rev, fan_fail, not_inner, omode, perm, rev_flag, bad);
+                       fbox, fwd, rev, fan_fail, not_inner, omode, perm, rev_flag, bad, frames);
     int64_t *eoff = eoff_.ensure(n + 1);
     uint32_t *dlist = dlist_.ensure(n + 1);
     unsigned int *dlist_n = dlist_n_.ensure(1);
@@ -2098,7 +2112,7 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
         hipLaunchKernelGGL(k_setup<false>, dim3(std::min<unsigned>((ns_u + 63) / 64, 512u)), dim3(64), 0, s, slow, slow_n, n, kind,
                            voff, lat, lng, radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id,
                            st_i, st_j, finfo, fbox, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                           nullptr);
+                           nullptr, nullptr);
     }
     const int64_t nd = nd_u;  // descent footprints (big, multi-face, polyline): the only ones k_start visits
     if (nd > 0)
