@@ -4,7 +4,7 @@
 // pred(i), rank = number of earlier i with pred -- without materialising a
 // flag array (the predicate is evaluated twice, once per pass); split_if
 // also places the failing elements (rank i - passing before i):
-//   k_cmp_count  one 4096-element tile per block: count -> cnt[tile]
+//   k_cmp_count  one 1024-element tile per block: count -> cnt[tile]
 //   exclusive_scan_i64 over the tile counts (scan.hip)
 //   k_cmp_emit   the tile again: per 256-element row a ballot per wave, the
 //                row/wave prefix from LDS, rank = tile base + prefix + mbcnt.
@@ -24,7 +24,7 @@
 namespace dss {
 namespace cmpct {
 
-constexpr int kBlock = 256, kWaves = kBlock / 64, kRows = 16, kTile = kBlock * kRows;
+constexpr int kBlock = 256, kWaves = kBlock / 64, kRows = 4, kTile = kBlock * kRows;  // (1024-element tiles: a 1M-element split fills the chip; 4096 left it at one block per CU)
 
 __device__ __forceinline__ uint32_t lanes_below(unsigned long long m)
 {
@@ -78,15 +78,16 @@ __global__ __launch_bounds__(kBlock) void k_cmp_emit(int64_t n, Pred pred, Emit 
         if (lane == 0) rc[r * kWaves + w] = (uint32_t)__popcll(bal[r]);
     }
     __syncthreads();
-    if (threadIdx.x < 64) {  // exclusive scan of the 64 (row, wave) counts, row-major = element order
-        const uint32_t v = rc[threadIdx.x];
+    static_assert(kRows * kWaves <= 64, "one wave scans the (row, wave) counts");
+    if (threadIdx.x < 64) {  // exclusive scan of the (row, wave) counts, row-major = element order
+        const uint32_t v = threadIdx.x < kRows * kWaves ? rc[threadIdx.x] : 0u;
         uint32_t x = v;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = __shfl_up(x, o, 64);
             if (lane >= o) x += y;
         }
-        rc[threadIdx.x] = x - v;
+        if (threadIdx.x < kRows * kWaves) rc[threadIdx.x] = x - v;
     }
     __syncthreads();
     const int64_t tb = off[blockIdx.x];
@@ -106,17 +107,27 @@ inline int64_t tiles_for(int64_t n) { return (n + kTile - 1) / kTile; }
 
 }  // namespace cmpct
 
+// Where split_if(n, ..., tmp, ...) leaves the passing count on the device
+// (the last word of its tile scan in `tmp`), for an emit_f that places the
+// failing elements after the passing ones; valid from the emit pass on.
+inline const int64_t *split_total_slot(int64_t n, DevBuf<unsigned char> &tmp)
+{
+    const int64_t nt = cmpct::tiles_for(n);
+    return (const int64_t *)tmp.ensure(sizeof(int64_t) * (2 * nt + 2)) + 2 * nt;
+}
+
 // Order-preserving split: emit(i, rank) for the elements passing pred,
 // emit_f(i, rank) for the others (each rank within its side); the passing
-// count lands in *d_total (device, int64) and, when `h_total` is non-null, on
-// the host (one stream sync).  EmitF = cmpct::NoEmit: plain compaction.
+// count lands in *d_total (device, int64; skipped when null) and, when
+// `h_total` is non-null, on the host (one stream sync).  EmitF =
+// cmpct::NoEmit: plain compaction.
 template <class Pred, class Emit, class EmitF>
 void split_if(int64_t n, Pred pred, Emit emit, EmitF emit_f, DevBuf<unsigned char> &tmp,
               DevBuf<unsigned char> &scan_tmp, hipStream_t s, int64_t *d_total, int64_t *h_total)
 {
     const int64_t nt = cmpct::tiles_for(n);
     if (n <= 0) {
-        DSS_HIP(hipMemsetAsync(d_total, 0, sizeof(int64_t), s));
+        if (d_total) DSS_HIP(hipMemsetAsync(d_total, 0, sizeof(int64_t), s));
         if (h_total) *h_total = 0;
         return;
     }
@@ -128,7 +139,7 @@ void split_if(int64_t n, Pred pred, Emit emit, EmitF emit_f, DevBuf<unsigned cha
     exclusive_scan_i64(cnt, off, nt, scan_tmp, s);
     hipLaunchKernelGGL((cmpct::k_cmp_emit<Pred, Emit, EmitF>), dim3((unsigned)nt), dim3(cmpct::kBlock), 0, s, n, pred,
                        emit, emit_f, (const int64_t *)off);
-    DSS_HIP(hipMemcpyAsync(d_total, off + nt, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+    if (d_total) DSS_HIP(hipMemcpyAsync(d_total, off + nt, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
     DSS_HIP(hipGetLastError());
     if (h_total) {
         DSS_HIP(hipMemcpyAsync(h_total, off + nt, sizeof(int64_t), hipMemcpyDeviceToHost, s));

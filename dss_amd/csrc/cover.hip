@@ -64,11 +64,16 @@ __device__ __forceinline__ int meta_face(uint32_t m) { return (int)((m >> 8) & 7
 
 __device__ __forceinline__ int64_t tid64() { return (int64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 
-__global__ void k_nverts(int64_t n, const int32_t *kind, const int64_t *voff, int64_t *nv)
+// (also zeroes the per-footprint flags and the list counters the setup
+// kernels accumulate into: six fill launches fewer per covering)
+__global__ void k_nverts(int64_t n, const int32_t *kind, const int64_t *voff, int64_t *nv, uint8_t *fan_fail,
+                         uint8_t *not_inner, uint8_t *bad, unsigned int *c0, unsigned int *c1, unsigned int *c2)
 {
     int64_t f = tid64();
+    if (f == 0) *c0 = *c1 = *c2 = 0u;
     if (f >= n) return;
     nv[f] = kind[f] == DSSG_KIND_CIRCLE ? 20 : (voff[f + 1] - voff[f]);
+    fan_fail[f] = not_inner[f] = bad[f] = 0;
 }
 
 // cos/sin of the 20 RegularLoop angles i * 2pi/20 (regular_loop.go), computed
@@ -2040,7 +2045,10 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
         out->offs = offs; out->cells = cells_.ensure(1); out->status = status; out->area_km2 = area; out->total_cells = 0;
         return;
     }
-    hipLaunchKernelGGL(k_nverts, dim3(grid_for(n, B)), dim3(B), 0, s, n, kind, voff, nv);
+    uint8_t *fan_fail = fanf_.ensure(n + 1), *not_inner = ninner_.ensure(n + 1), *bad = badv_.ensure(n + 1);
+    unsigned int *slow_n = slow_n_.ensure(1), *dlist_n = dlist_n_.ensure(1), *ulist_n = ulist_n_.ensure(1);
+    hipLaunchKernelGGL(k_nverts, dim3(grid_for(n, B)), dim3(B), 0, s, n, kind, voff, nv, fan_fail, not_inner, bad,
+                       slow_n, dlist_n, ulist_n);
     exclusive_scan_i64(nv, xoff, n, tmp_, s);
     int64_t nx = 0;
     DSS_HIP(hipMemcpyAsync(&nx, xoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -2051,21 +2059,13 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     uint32_t *st_i = st_i_.ensure(4 * n + 4), *st_j = st_j_.ensure(4 * n + 4), *finfo = finfo_.ensure(n + 1);
     uint4 *fbox = fbox_.ensure(n + 1);
     uint32_t *slow = slow_.ensure(n + 1);
-    unsigned int *slow_n = slow_n_.ensure(1);
-    uint8_t *fan_fail = fanf_.ensure(n + 1);
     CircleFrame *frames = (CircleFrame *)frames_.ensure(sizeof(CircleFrame) * (n + 1));
     uint32_t *vown = vown_.ensure(nx + 1);
     double *fwd = fwd_.ensure(nx + 1), *rev = rev_.ensure(nx + 1);
-    uint8_t *not_inner = ninner_.ensure(n + 1);
     uint32_t *perm = perm_.ensure(n + 1);
     uint8_t *omode = omode_.ensure(n + 1);
     int64_t *tcnt = tcnt_.ensure(n + 1), *toff = toff_.ensure(n + 2);
     uint32_t *towner = towner_.ensure(2 * nx + 1);  // <= 2 (n - 2) tasks per loop
-    DSS_HIP(hipMemsetAsync(slow_n, 0, sizeof(unsigned int), s));
-    DSS_HIP(hipMemsetAsync(fan_fail, 0, n, s));
-    DSS_HIP(hipMemsetAsync(not_inner, 0, n, s));
-    uint8_t *bad = badv_.ensure(n + 1);
-    DSS_HIP(hipMemsetAsync(bad, 0, n, s));
     partition_polygons_first(kind, perm, fcnt_.ensure(n + 2), n, tmp_, tmp2_, s);
     // per-vertex pre-pass: frames, owners, S2 points, fan terms
     hipLaunchKernelGGL(k_circle_frames, dim3(grid_for(n, B)), dim3(B), 0, s, n, kind, voff, lat, lng, radius_m, frames);
@@ -2091,7 +2091,6 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
                        fbox, fwd, rev, fan_fail, not_inner, omode, perm, rev_flag, bad, frames);
     int64_t *eoff = eoff_.ensure(n + 1);
     uint32_t *dlist = dlist_.ensure(n + 1);
-    unsigned int *dlist_n = dlist_n_.ensure(1);
     int64_t ne = 0;
     unsigned int nd_u = 0, ns_u = 0;
     // per footprint its clipped-edge items and the descent list, then one
@@ -2100,7 +2099,7 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     // even over an empty list) runs only when there are any, and the counts
     // are taken again after it
     for (int pass = 0; pass < 2; pass++) {
-        DSS_HIP(hipMemsetAsync(dlist_n, 0, sizeof(unsigned int), s));
+        if (pass) DSS_HIP(hipMemsetAsync(dlist_n, 0, sizeof(unsigned int), s));  // (pass 0: zeroed by k_nverts)
         hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv, dlist,
                            dlist_n);
         exclusive_scan_i64(nv, eoff, n, tmp_, s);
@@ -2125,8 +2124,6 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     // tested now, compacted after the counts
     unsigned long long *fkm = kmask_.ensure(8 * (n + 1)), *fum = fkm + 4 * (n + 1);
     uint32_t *ulist = ulist_.ensure(n + 1);
-    unsigned int *ulist_n = ulist_n_.ensure(1);
-    DSS_HIP(hipMemsetAsync(ulist_n, 0, sizeof(unsigned int), s));
     hipLaunchKernelGGL(k_cand_fp, dim3(grid_for(n, kFpPer)), dim3(kFpBlock), 0, s, n, flags, fbox, finfo, st_i, st_j,
                        xoff, nvx, uv, orig, rev_flag, fkm, fum, ulist, ulist_n);
     hipLaunchKernelGGL(k_cand_exact, dim3((unsigned)std::min<int64_t>(grid_for(n, B / 64), 1024)), dim3(B), 0, s, ulist,

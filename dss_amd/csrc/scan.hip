@@ -164,10 +164,11 @@ void partition_polygons_first(const int32_t *kind, uint32_t *perm, unsigned long
                               DevBuf<unsigned char> &tmp, DevBuf<unsigned char> &tmp2, hipStream_t s)
 {
     if (n <= 0) return;
-    // non-circles first (their count -> nsel[0]), then circles after them
-    int64_t *npoly = (int64_t *)nsel, *ncirc = (int64_t *)(nsel + 1);
-    compact_if(n, IsCircle{kind, false}, PlaceAt{perm, nullptr}, tmp, tmp2, s, npoly, nullptr);
-    compact_if(n, IsCircle{kind, true}, PlaceAt{perm, npoly}, tmp, tmp2, s, ncirc, nullptr);
+    // non-circles first, then circles after them: one split (count, scan,
+    // place both sides) instead of a compaction per side
+    (void)nsel;
+    split_if(n, IsCircle{kind, false}, PlaceAt{perm, nullptr}, PlaceAt{perm, split_total_slot(n, tmp)}, tmp, tmp2, s,
+             nullptr, nullptr);
 }
 
 void device_copy(void *dst, const void *src, size_t bytes, hipStream_t s)

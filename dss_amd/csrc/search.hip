@@ -2400,11 +2400,14 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     int64_t ucap_l = any_long ? std::max<int64_t>(units_cap_hint_l_, 1024) : 0;
     Unit *units = nullptr, *units_l = nullptr;
     const unsigned ugrid = (unsigned)std::min<int64_t>((nqc + 63) / 64 / (kBlock / 64) + 1, (int64_t)n_cu_ * 16);
+    bool ctl_fresh = true;  // the control block as the opening memset left it (the first build and join skip theirs)
     auto build_units = [&]() {
         units = (Unit *)units_buf_.ensure(sizeof(Unit) * (kRegions * (ucap + ucap_l) + 1));
         units_l = units + kRegions * ucap;
-        DSS_HIP(hipMemsetAsync(ctl + kCtlUnits, 0, kR * sizeof(unsigned long long), s));
-        DSS_HIP(hipMemsetAsync(ctl + kCtlUnitsL, 0, kR * sizeof(unsigned long long), s));
+        if (!ctl_fresh) {
+            DSS_HIP(hipMemsetAsync(ctl + kCtlUnits, 0, kR * sizeof(unsigned long long), s));
+            DSS_HIP(hipMemsetAsync(ctl + kCtlUnitsL, 0, kR * sizeof(unsigned long long), s));
+        }
         hipLaunchKernelGGL(k_units, dim3(ugrid), dim3(kBlock), 0, s, ix, skey, dnkeys, Regions{ctl + kCtlUnits, ucap},
                            units, Regions{ctl + kCtlUnitsL, ucap_l}, units_l, 64u, sq,
                            (const unsigned long long *)(ctl + kCtlDq), (long long)idx->tbase, idx->qshift);
@@ -2451,9 +2454,14 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         uint32_t *fills = fills_.ensure(nch + tnch + 1), *tfills = fills + nch;
         unsigned long long *tk = any_long ? tkey_.ensure(tcap + 1) : nullptr;
         DSS_HIP(hipMemsetAsync(fills, 0, sizeof(uint32_t) * (nch + tnch), s));
-        // (misc word 5, the long-query count of k_cell_query, survives)
-        DSS_HIP(hipMemsetAsync(ctl + kCtlMisc, 0, 5 * sizeof(unsigned long long), s));
-        DSS_HIP(hipMemsetAsync(ctl + kCtlMisc + 6, 0, (kCtlWords - kCtlMisc - 6) * sizeof(unsigned long long), s));
+        // (misc word 5, the long-query count of k_cell_query, survives; on the
+        // first attempt nothing has written these words since the opening
+        // memset but k_qwin's histogram, which nothing reads after k_qorder)
+        if (!ctl_fresh) {
+            DSS_HIP(hipMemsetAsync(ctl + kCtlMisc, 0, 5 * sizeof(unsigned long long), s));
+            DSS_HIP(hipMemsetAsync(ctl + kCtlMisc + 6, 0, (kCtlWords - kCtlMisc - 6) * sizeof(unsigned long long), s));
+        }
+        ctl_fresh = false;
         ja.ur = Regions{ctl + kCtlUnits, ucap};
         ja.out = OutArgs{oq, oe, OutStream{out_rcap_, fills, ctl + kCtlOut}, tk, OutStream{tag_rcap_, tfills, ctl + kCtlTOut},
                          eb, hbm, cnt};
