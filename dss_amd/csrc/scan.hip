@@ -18,8 +18,9 @@ __device__ __forceinline__ int64_t tid64_s() { return (int64_t)blockIdx.x * bloc
 //   k_scan_reduce  tile sums -> part[t]            (skipped for one tile)
 //   k_scan_parts   one block: exclusive scan of the tile sums, in place
 //   k_scan_down    tile t again: lane sums, block scan, + part[t] -> out
-// No look-back spin and no library state: 3 launches (1 for n <= 2048),
-// HBM 8n read twice + 8n written.
+// No look-back spin and no library state: 3 launches (1 for n <= 2048; 2 up
+// to 2M elements, k_scan_down_fold summing the tile sums itself), HBM 8n
+// read twice + 8n written.
 constexpr int kSBlock = 256, kSWaves = kSBlock / 64, kSItems = 8, kSTile = kSBlock * kSItems;
 
 __device__ __forceinline__ long long block_incl_scan_i64(long long x, long long *ws, long long &total)
@@ -107,6 +108,31 @@ __global__ __launch_bounds__(kSBlock) void k_scan_down(const int64_t *__restrict
     }
 }
 
+// k_scan_down for up to kSFoldTiles tiles without k_scan_parts: each block
+// sums the tile sums before it itself (<= 1024 L2-resident words), one
+// launch fewer per scan -- a 1M-element scan is 489 tiles.
+constexpr int64_t kSFoldTiles = 1024;
+__global__ __launch_bounds__(kSBlock) void k_scan_down_fold(const int64_t *__restrict__ in, int64_t n,
+                                                            const long long *__restrict__ part,
+                                                            int64_t *__restrict__ out)
+{
+    __shared__ long long ws[kSWaves];
+    long long pre = 0, total;
+    for (int64_t t = threadIdx.x; t < (int64_t)blockIdx.x; t += kSBlock) pre += part[t];
+    block_incl_scan_i64(pre, ws, total);
+    pre = total;  // the tiles before this one
+    const int64_t i0 = (int64_t)blockIdx.x * kSTile + (int64_t)threadIdx.x * kSItems;
+    long long v[kSItems];
+    const long long t = lane_items(in, n, i0, v);
+    long long run = block_incl_scan_i64(t, ws, total) - t + pre;
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[0] = 0;
+#pragma unroll
+    for (int u = 0; u < kSItems; u++) {
+        run += v[u];
+        if (i0 + u < n) out[i0 + u + 1] = run;
+    }
+}
+
 }  // namespace
 
 void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, DevBuf<unsigned char> &tmp, hipStream_t s)
@@ -120,6 +146,12 @@ void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, DevBuf<unsig
     if (nt > 1) {
         part = (long long *)tmp.ensure(sizeof(long long) * nt);
         hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nt), dim3(kSBlock), 0, s, in, n, part);
+        if (nt <= kSFoldTiles) {
+            hipLaunchKernelGGL(k_scan_down_fold, dim3((unsigned)nt), dim3(kSBlock), 0, s, in, n, (const long long *)part,
+                               out);
+            DSS_HIP(hipGetLastError());
+            return;
+        }
         hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(kSBlock), 0, s, part, nt);
     }
     hipLaunchKernelGGL(k_scan_down, dim3((unsigned)nt), dim3(kSBlock), 0, s, in, n, (const long long *)part, out);
