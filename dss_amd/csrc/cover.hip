@@ -1305,7 +1305,8 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
                                                       const uint32_t *st_j, const int64_t *xoff, const int32_t *nvx,
                                                       const double2 *uv, const uint8_t *origin_in,
                                                       const uint8_t *rev_flag, unsigned long long *fkm,
-                                                      unsigned long long *fum, uint32_t *ulist, unsigned int *ulist_n)
+                                                      unsigned long long *fum, uint32_t *ulist, unsigned int *ulist_n,
+                                                      const uint32_t *perm)
 {
     __shared__ uint4 s_bx[kFpPer];
     __shared__ uint32_t s_info[kFpPer], s_sti[kFpPer][4], s_stj[kFpPer][4];
@@ -1316,7 +1317,9 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
     const int t = threadIdx.x, lane = t & 63;
     const int64_t F0 = (int64_t)blockIdx.x * kFpPer;
     if (t < kFpPer) {
-        const int64_t f = F0 + t;
+        // footprints in k_setup's order (polygons, then circles): a block's
+        // loops are of one kind, so a wave's edge walks are of similar length
+        const int64_t f = F0 + t < n ? (int64_t)perm[F0 + t] : n;
         const bool fast = f < n && (flags[f] & FL_FAST);
         uint32_t cnt = 0, nvv = 0;
         if (fast) {
@@ -1398,7 +1401,7 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
     }
     __syncthreads();
     if (t < kFpPer) {
-        const int64_t f = F0 + t;
+        const int64_t f = F0 + t < n ? (int64_t)perm[F0 + t] : n;
         const bool has = f < n && s_cb[t + 1] > s_cb[t];
         if (has) {
             ulonglong2 *km = reinterpret_cast<ulonglong2 *>(fkm + 4 * f);
@@ -2125,7 +2128,7 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     unsigned long long *fkm = kmask_.ensure(8 * (n + 1)), *fum = fkm + 4 * (n + 1);
     uint32_t *ulist = ulist_.ensure(n + 1);
     hipLaunchKernelGGL(k_cand_fp, dim3(grid_for(n, kFpPer)), dim3(kFpBlock), 0, s, n, flags, fbox, finfo, st_i, st_j,
-                       xoff, nvx, uv, orig, rev_flag, fkm, fum, ulist, ulist_n);
+                       xoff, nvx, uv, orig, rev_flag, fkm, fum, ulist, ulist_n, perm);
     hipLaunchKernelGGL(k_cand_exact, dim3((unsigned)std::min<int64_t>(grid_for(n, B / 64), 1024)), dim3(B), 0, s, ulist,
                        ulist_n, st_id, st_i, st_j, finfo, xoff, xyz, nvx, orig, rev_flag, fkm, fum);
     // hierarchical descent for the rest (big, multi-face, polyline footprints)
