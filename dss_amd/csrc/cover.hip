@@ -265,10 +265,19 @@ __global__ void k_orient(int64_t n, const int32_t *kind, const int64_t *nslots, 
     bool near = true;
     V3 b = p[1];
     near &= a.x * b.x + a.y * b.y + a.z * b.z >= 0.99875;  // cos(0.05)
+    // a simple fan: every triangle (v0, vi, vi+1) and every (v0, v1, vi)
+    // robustly of one orientation -- the rays from v0 turn one way through
+    // less than a half turn, so the loop is simple (star-shaped from v0)
+    const V3 a1 = cross(a, b);
+    constexpr double kE = 2 * DSS_MAX_DET_ERR;
+    bool pos = true, neg = true;
     for (int i = 1; i + 1 < nv; i++) {
         const V3 c = p[i + 1];
         near &= a.x * c.x + a.y * c.y + a.z * c.z >= 0.99875;
         const double t = a.x * (b.y * c.z - b.z * c.y) + a.y * (b.z * c.x - b.x * c.z) + a.z * (b.x * c.y - b.y * c.x);
+        const double u = a1.x * c.x + a1.y * c.y + a1.z * c.z;  // det(v0, v1, vi)
+        pos &= (t > kE) & (u > kE);
+        neg &= (t < -kE) & (u < -kE);
         d += t;
         dabs += __builtin_fabs(t);
         b = c;
@@ -279,7 +288,10 @@ __global__ void k_orient(int64_t n, const int32_t *kind, const int64_t *nslots, 
     int m = 2;
     if (near && d > margin && ((d * 1.1) * DSS_EARTH_AREA_KM2) / 4.0 * DSS_PI < DSS_MAX_AREA_KM2) m = 0;  // = fan_area_km2
     else if (near && d < -margin) m = 1;
-    omode[f] = (uint8_t)m;
+    // bits 2, 3: the loop is a simple counter-clockwise / clockwise fan
+    // within 0.05 rad of v0 (k_setup skips the origin walk of a simple
+    // counter-clockwise loop whose cap excludes OriginPoint)
+    omode[f] = (uint8_t)(m | (near && pos ? 4 : 0) | (near && neg ? 8 : 0));
     tcnt[f] = (int64_t)(nv - 2) * (m == 2 ? 2 : 1);
 }
 
@@ -300,7 +312,7 @@ __global__ void k_fan_area(const int64_t *toff_end, const uint32_t *towner, cons
         const int n = (int)nslots[f];
         const int k = n - 2;
         int j = (int)(t - toff[f]);
-        const int m = omode[f];
+        const int m = omode[f] & 3;
         const bool r = m == 1 || (m == 2 && j >= k);
         if (m == 2 && j >= k) j -= k;
         const int i = 1 + j;
@@ -460,11 +472,27 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
             }
             l.n = nv;
             int om = 2;  // k_orient: which fan terms exist (FAST)
-            if constexpr (FAST) om = omode[f];
+            // a simple loop within 0.05 rad of v0 (k_orient) is inside its
+            // cap, so OriginPoint outside the cap is outside the loop once it
+            // runs counter-clockwise -- initOriginAndBound's walk finds
+            // "outside" there; the walk is skipped for the loop as given
+            // (simple ccw) or for its reversal (simple cw)
+            bool skip_fwd = false, skip_rev = false;
+            if constexpr (FAST) {
+                om = omode[f] & 3;
+                const int sf = omode[f] >> 2;
+                if (sf) {
+                    const V3 o = origin_point(), q = p[0];
+                    const bool ofar = q.x * o.x + q.y * o.y + q.z * o.z < 0.99875 - 1e-6;
+                    skip_fwd = ofar && (sf & 1);
+                    skip_rev = ofar && (sf & 2);
+                }
+            }
             if (om == 1) {
                 area = INFINITY;  // the forward sum is negative: ~4 pi, above the cap
             } else {
-                origin_of<FAST>(l, fail);
+                if (skip_fwd) l.origin_inside = false;
+                else origin_of<FAST>(l, fail);
                 if constexpr (FAST) area = fan_area_km2(fwd + xoff[f], nv, fail);
                 else area = area_km2_of<FAST>(l, fail);
             }
@@ -486,7 +514,8 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
                         p[j] = t;
                     }
                 }
-                origin_of<FAST>(l, fail);
+                if (skip_rev) l.origin_inside = false;
+                else origin_of<FAST>(l, fail);
                 if constexpr (FAST) area = fan_area_km2(rev + xoff[f], nv, fail, om == 1);
                 else area = area_km2_of<FAST>(l, fail);
                 if (bail()) return;
