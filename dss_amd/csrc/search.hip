@@ -104,7 +104,10 @@ struct Regions {
 // picks the shape from the previous batch's pass density (dense_out_).
 constexpr int kWaves = 4;  // waves per join workgroup
 constexpr int kJoinBpcSparse = 7, kJoinBpcDense = 6;
-constexpr int kStageSparse = 640, kStageDense = 1024;
+#ifndef DSS_STAGE_SPARSE
+#define DSS_STAGE_SPARSE 640
+#endif
+constexpr int kStageSparse = DSS_STAGE_SPARSE, kStageDense = 1024;
 #ifndef DSS_JOIN_LONG_WPE
 #define DSS_JOIN_LONG_WPE 1
 #endif
