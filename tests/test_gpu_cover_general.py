@@ -83,3 +83,68 @@ def test_general_pipeline_special_paths(oracle, seed):
     res = geo.cover_batch(kind, voff, lat, lng, rad)
     _check_batch(dict(status=status, offs=offs, cells=cells, area_km2=area), res)
     assert (status == 0).sum() > len(polys) // 2
+
+
+def _origin_latlng():
+    """OriginPoint (s2 point.go OriginPoint) in degrees."""
+    o = np.array([-0.0099994664350250197, 0.0025924542609324121, 0.99994664350250195])
+    o /= np.linalg.norm(o)
+    return float(np.degrees(np.arcsin(o[2]))), float(np.degrees(np.arctan2(o[1], o[0])))
+
+
+def _offset(lat, lng, dist_rad, bearing):
+    """The point dist_rad from (lat, lng) along bearing (radians)."""
+    la, ln = np.radians(lat), np.radians(lng)
+    la2 = np.arcsin(np.sin(la) * np.cos(dist_rad) + np.cos(la) * np.sin(dist_rad) * np.cos(bearing))
+    ln2 = ln + np.arctan2(np.sin(bearing) * np.sin(dist_rad) * np.cos(la), np.cos(dist_rad) - np.sin(la) * np.sin(la2))
+    return float(np.degrees(la2)), float(((np.degrees(ln2) + 180) % 360) - 180)
+
+
+def test_general_pipeline_around_origin_point(oracle):
+    """The setup's origin shortcuts (circles whose cap excludes OriginPoint;
+    polygons k_orient proves simple, counter-clockwise or clockwise, whose
+    0.05 rad cap excludes it) next to the footprints that keep the crossing
+    walk: circles and rings containing OriginPoint, passing just beside it,
+    and with their caps' edge at 0.99 .. 1.01 of the distance.  GPU (general
+    pipeline) == oracle, bit for bit."""
+    from dss_amd import geo
+    rng = np.random.default_rng(11)
+    olat, olng = _origin_latlng()
+    circles, polys = [], []
+    for r_m in (80.0, 1500.0, 30000.0):
+        r = r_m / 6371010.0
+        for f in (0.0, 0.5, 0.97, 0.999, 1.001, 1.03, 2.0, 10.0):
+            for b in (0.3, 2.1, 4.4):
+                circles.append((*_offset(olat, olng, f * r, b), r_m))
+    for ring in (2e-5, 4e-4, 8e-3):  # ring radius (rad)
+        for f in (0.0, 0.6, 1.02, 3.0, 0.05 / ring + 2.0, 0.05 / ring + 40.0):
+            for k in (3, 5, 9):
+                clat, clng = _offset(olat, olng, f * ring, rng.uniform(0, 2 * np.pi))
+                pts = [_offset(clat, clng, ring, 2 * np.pi * i / k) for i in range(k)]
+                polys.append(pts)
+                polys.append(pts[::-1])  # the other orientation (Q4 reversal of a clockwise ring)
+    base = [("c", c) for c in circles] + [("p", p) for p in polys]
+    reps = 17000 // len(base) + 1
+    kinds, verts, rads = [], [], []
+    for r in range(reps):
+        for t, g in base:
+            j = 0.0 if r == 0 else 1e-7
+            if t == "c":
+                kinds.append(1)
+                verts.append([(g[0] + rng.normal(0, j), g[1] + rng.normal(0, j))])
+                rads.append(g[2])
+            else:
+                kinds.append(0)
+                verts.append([(la + rng.normal(0, j), ln + rng.normal(0, j)) for la, ln in g])
+                rads.append(0.0)
+    assert len(kinds) > 16384
+    kind = np.array(kinds, np.int32)
+    voff = np.zeros(len(verts) + 1, np.int64)
+    voff[1:] = np.cumsum([len(v) for v in verts])
+    lat = np.array([q[0] for v in verts for q in v], dtype=np.float64)
+    lng = np.array([q[1] for v in verts for q in v], dtype=np.float64)
+    rad = np.array(rads, np.float32)
+    offs, cells, status, area = oracle.cover_batch(kind, voff, lat, lng, rad)
+    res = geo.cover_batch(kind, voff, lat, lng, rad)
+    _check_batch(dict(status=status, offs=offs, cells=cells, area_km2=area), res)
+    assert (status == 0).sum() > len(kinds) // 2
