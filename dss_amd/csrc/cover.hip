@@ -1155,17 +1155,23 @@ __global__ void k_emit(int64_t nn, const uint32_t *nf, const uint64_t *nid, cons
     for (int64_t q = 0; q < c; q++) cells[w + q] = first + (uint64_t)q * (lsb13 << 1);
 }
 
-__global__ void k_emit_big(const uint32_t *big, const uint32_t *nf, const uint64_t *nid, const uint32_t *nmeta,
-                           const int64_t *ipos, const int64_t *dpre, const int64_t *offs, uint64_t *cells)
+// A fixed grid striding over the device count of big items (launched
+// without reading the count back: no host sync after k_emit).
+__global__ void k_emit_big(const uint32_t *big, const int *nbig, const uint32_t *nf, const uint64_t *nid,
+                           const uint32_t *nmeta, const int64_t *ipos, const int64_t *dpre, const int64_t *offs,
+                           uint64_t *cells)
 {
-    uint32_t k = big[blockIdx.x];
-    int level = meta_level(nmeta[k]);
-    int64_t c = (int64_t)1 << (2 * (kCoverLevel - level));
-    uint64_t id = nid[k];
-    uint64_t lsb13 = lsb_for_level(kCoverLevel);
-    uint64_t first = id - cellid_lsb_dev(id) + lsb13;
-    int64_t w = item_pos(k, nf, ipos, dpre, offs);
-    for (int64_t q = threadIdx.x; q < c; q += blockDim.x) cells[w + q] = first + (uint64_t)q * (lsb13 << 1);
+    const int nb = *nbig;
+    for (int b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t k = big[b];
+        const int level = meta_level(nmeta[k]);
+        const int64_t c = (int64_t)1 << (2 * (kCoverLevel - level));
+        const uint64_t id = nid[k];
+        const uint64_t lsb13 = lsb_for_level(kCoverLevel);
+        const uint64_t first = id - cellid_lsb_dev(id) + lsb13;
+        const int64_t w = item_pos(k, nf, ipos, dpre, offs);
+        for (int64_t q = threadIdx.x; q < c; q += blockDim.x) cells[w + q] = first + (uint64_t)q * (lsb13 << 1);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2125,26 +2131,20 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     uint32_t *dlist = dlist_.ensure(n + 1);
     int64_t ne = 0;
     unsigned int nd_u = 0, ns_u = 0;
-    // per footprint its clipped-edge items and the descent list, then one
-    // sync for their totals; the exact setup of the footprints the triage
-    // left (a kernel whose 492 B of scratch per lane cost ~0.09 ms per launch
-    // even over an empty list) runs only when there are any, and the counts
-    // are taken again after it
-    for (int pass = 0; pass < 2; pass++) {
-        if (pass) DSS_HIP(hipMemsetAsync(dlist_n, 0, sizeof(unsigned int), s));  // (pass 0: zeroed by k_nverts)
-        hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv, dlist,
-                           dlist_n);
-        exclusive_scan_i64(nv, eoff, n, tmp_, s);
-        DSS_HIP(hipMemcpyAsync(&ne, eoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        DSS_HIP(hipMemcpyAsync(&nd_u, dlist_n, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
-        if (pass == 0) DSS_HIP(hipMemcpyAsync(&ns_u, slow_n, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
-        DSS_HIP(hipStreamSynchronize(s));
-        if (pass == 1 || ns_u == 0) break;
-        hipLaunchKernelGGL(k_setup<false>, dim3(std::min<unsigned>((ns_u + 63) / 64, 512u)), dim3(64), 0, s, slow, slow_n, n, kind,
-                           voff, lat, lng, radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id,
-                           st_i, st_j, finfo, fbox, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                           nullptr, nullptr);
-    }
+    // the exact setup of whatever the triage left, launched without reading
+    // the count back (a fixed grid strides over the device list; empty, it
+    // costs ~5 us: profiles/r05ak), then per footprint its clipped-edge items
+    // and the descent list, and one sync for their totals (round 4 read the
+    // counts twice, before and after the exact setup)
+    hipLaunchKernelGGL(k_setup<false>, dim3(256), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng, radius_m, xoff,
+                       xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, nullptr,
+                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+    hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv, dlist, dlist_n);
+    exclusive_scan_i64(nv, eoff, n, tmp_, s);
+    DSS_HIP(hipMemcpyAsync(&ne, eoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipMemcpyAsync(&nd_u, dlist_n, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipMemcpyAsync(&ns_u, slow_n, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+    DSS_HIP(hipStreamSynchronize(s));
     const int64_t nd = nd_u;  // descent footprints (big, multi-face, polyline): the only ones k_start visits
     if (nd > 0)
         hipLaunchKernelGGL(k_reverse_list, dim3((unsigned)std::min<int64_t>((nd + 3) / 4, 1024)), dim3(256), 0, s, dlist,
@@ -2246,12 +2246,8 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
         DSS_HIP(hipMemsetAsync(nbig, 0, sizeof(int), s));
         hipLaunchKernelGGL(k_emit, dim3(grid_for(nn, B)), dim3(B), 0, s, nn, F->f.p, F->id.p, F->meta.p, ipos, dpre, offs,
                            cells, big, nbig);
-        int hb = 0;
-        DSS_HIP(hipMemcpyAsync(&hb, nbig, sizeof(int), hipMemcpyDeviceToHost, s));
-        DSS_HIP(hipStreamSynchronize(s));
-        if (hb > 0)
-            hipLaunchKernelGGL(k_emit_big, dim3(hb), dim3(256), 0, s, big, F->f.p, F->id.p, F->meta.p, ipos, dpre, offs,
-                               cells);
+        hipLaunchKernelGGL(k_emit_big, dim3((unsigned)std::min<int64_t>(nn, 256)), dim3(256), 0, s, big,
+                           (const int *)nbig, F->f.p, F->id.p, F->meta.p, ipos, dpre, offs, cells);
     }
     out->offs = offs;
     out->cells = cells;
