@@ -1347,16 +1347,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
         ulonglong2 ps01 = ns01, ps23 = ns23;
         const bool usig = nsig;  // the signatures are loaded (else: per lane, on first need)
         bool lsig = false;
-        // the posting signature ORed down to 32 bits: a record's folded
-        // signature that misses it cannot overlap the full one (short joins
-        // without an owner filter: the fold rides in the record's owner slot)
-        constexpr bool kFold = !OWNER && !LONG;
-        uint32_t pfold = 0;
-        auto fold_sig = [](ulonglong2 a, ulonglong2 b) {
-            const unsigned long long f = a.x | a.y | b.x | b.y;
-            return (uint32_t)(f | (f >> 32));
-        };
-        if (kFold && usig) pfold = fold_sig(ps01, ps23);
         const bool pv = (uint32_t)lane < np && !is_dead(ix, pe & ~kFirstBit);  // tombstones match nothing
         un = next_unit();
         if (un >= 0) prefetch(un);
@@ -1408,7 +1398,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                     s_rt[w][slot] = make_longlong2(((long long)h0.y << 32) | (uint32_t)h0.x,
                                                    ((long long)h0.w << 32) | (uint32_t)h0.z);
                     s_ra[w][slot] = make_float4(__int_as_float(h1.x), __int_as_float(h1.y), __int_as_float(h1.z),
-                                                kFold ? __uint_as_float(fold_sig(g0, g1)) : __int_as_float(h1.w));
+                                                __int_as_float(h1.w));
                     s_rs[w][0][slot] = g0;
                     s_rs[w][1][slot] = g1;
                 }
@@ -1476,7 +1466,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                             const uint64_t p = d.p0 + (uint64_t)lane;
                             ps01 = ix.b_sig[2 * p];
                             ps23 = ix.b_sig[2 * p + 1];
-                            if (kFold) pfold = fold_sig(ps01, ps23);
                             lsig = true;
                         }
                     }
@@ -1485,10 +1474,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 while (need) {
                     const int j = __builtin_ctzll(need);
                     need &= need - 1;
-                    if (!kFold || (__float_as_uint(s_ra[w][j].w) & pfold) != 0u) {  // folds meet: the full test
-                        const ulonglong2 c0 = s_rs[w][0][j], c1 = s_rs[w][1][j];
-                        if (((c0.x & ps01.x) | (c0.y & ps01.y) | (c1.x & ps23.x) | (c1.y & ps23.y)) != 0ull) continue;
-                    }
+                    const ulonglong2 c0 = s_rs[w][0][j], c1 = s_rs[w][1][j];
+                    if (((c0.x & ps01.x) | (c0.y & ps01.y) | (c1.x & ps23.x) | (c1.y & ps23.y)) != 0ull) continue;
                     // (without long postings every posting's prefix is compact:
                     // all of its entity's cells lie in an 8 x 8 window)
                     bool k = !LONG || pcompact || ((RC >> j) & 1ull) || (plong && ((RL >> j) & 1ull));
