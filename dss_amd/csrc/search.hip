@@ -103,7 +103,10 @@ struct Regions {
 // pass density 0.45) keep 6 x 1024 (0.55 against 0.61 ms).  The search
 // picks the shape from the previous batch's pass density (dense_out_).
 constexpr int kWaves = 4;  // waves per join workgroup
-constexpr int kJoinBpcSparse = 7, kJoinBpcDense = 6;
+#ifndef DSS_JOIN_BPC_SPARSE
+#define DSS_JOIN_BPC_SPARSE 7
+#endif
+constexpr int kJoinBpcSparse = DSS_JOIN_BPC_SPARSE, kJoinBpcDense = 6;
 #ifndef DSS_STAGE_SPARSE
 #define DSS_STAGE_SPARSE 640
 #endif
