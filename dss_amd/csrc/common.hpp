@@ -86,7 +86,13 @@ void stage_check(hipStream_t s, const char *stage);
 // hand-written reduce-then-scan in scan.hip (in != out).
 void selftest_math(int op, int64_t n, const double *x, const double *y, double *out, hipStream_t s);
 void selftest_scan(int64_t n, int shift, const int64_t *in, int64_t *out, hipStream_t s);
-void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, DevBuf<unsigned char> &tmp, hipStream_t s);
+// mail (optional): a device-visible host word that also receives out[n]
+// (the total), written by the scan's last element -- read after a stream
+// sync without a copy launch
+void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, DevBuf<unsigned char> &tmp, hipStream_t s,
+                        int64_t *mail = nullptr);
+// up to three device uint32 counters into device-visible host words (one launch)
+void mail_counters(const unsigned int *a, const unsigned int *b, const unsigned int *c, int64_t *mail, hipStream_t s);
 // perm = footprint indices with every non-circle before every circle (order
 // within each part unspecified): per-footprint kernels then run one kind's
 // code path per wave.

@@ -2048,6 +2048,15 @@ void CoverEngine::run(int64_t n, const int32_t *kind, const int64_t *voff, const
     out->total_cells = total;
 }
 
+int64_t *CoverEngine::mailbox()
+{
+    if (!mail_h_) {
+        DSS_HIP(hipHostMalloc((void **)&mail_h_, 16 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent));
+        DSS_HIP(hipHostGetDevicePointer((void **)&mail_d_, mail_h_, 0));
+    }
+    return mail_d_;
+}
+
 void CoverEngine::init_tables(hipStream_t s)
 {
     if (tables_) return;
@@ -2087,10 +2096,12 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     unsigned int *slow_n = slow_n_.ensure(1), *dlist_n = dlist_n_.ensure(1), *ulist_n = ulist_n_.ensure(1);
     hipLaunchKernelGGL(k_nverts, dim3(grid_for(n, B)), dim3(B), 0, s, n, kind, voff, nv, fan_fail, not_inner, bad,
                        slow_n, dlist_n, ulist_n);
-    exclusive_scan_i64(nv, xoff, n, tmp_, s);
-    int64_t nx = 0;
-    DSS_HIP(hipMemcpyAsync(&nx, xoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    int64_t *mail = mailbox();  // [0] vertices [1] edge items [2] descent [3] exact setups [4] start nodes
+                                // [5] next frontier [6] open [7] cells
+    volatile const int64_t *mh = mail_h_;
+    exclusive_scan_i64(nv, xoff, n, tmp_, s, mail + 0);
     DSS_HIP(hipStreamSynchronize(s));
+    const int64_t nx = mh[0];
     V3 *xyz = (V3 *)xyz_.ensure((size_t)nx * 3 + 3);
     double2 *uv = uv_.ensure(nx + 1);
     uint64_t *st_id = st_id_.ensure(4 * n + 4);
@@ -2140,11 +2151,12 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
                        xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, nullptr,
                        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
     hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv, dlist, dlist_n);
-    exclusive_scan_i64(nv, eoff, n, tmp_, s);
-    DSS_HIP(hipMemcpyAsync(&ne, eoff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    DSS_HIP(hipMemcpyAsync(&nd_u, dlist_n, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
-    DSS_HIP(hipMemcpyAsync(&ns_u, slow_n, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+    exclusive_scan_i64(nv, eoff, n, tmp_, s, mail + 1);
+    mail_counters(dlist_n, slow_n, nullptr, mail + 2, s);
     DSS_HIP(hipStreamSynchronize(s));
+    ne = mh[1];
+    nd_u = (unsigned int)mh[2];
+    ns_u = (unsigned int)mh[3];
     const int64_t nd = nd_u;  // descent footprints (big, multi-face, polyline): the only ones k_start visits
     if (nd > 0)
         hipLaunchKernelGGL(k_reverse_list, dim3((unsigned)std::min<int64_t>((nd + 3) / 4, 1024)), dim3(256), 0, s, dlist,
@@ -2176,9 +2188,9 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
         hipLaunchKernelGGL(k_start<0>, dim3(grid_for(nd, 64)), dim3(64), 0, s, nd, dlist, xoff, xyz, mode, fmask, flags,
                            orig, nvx, eoff, clip_c, cflags, nv, soff, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                            nullptr);
-        exclusive_scan_i64(nv, soff, n, tmp_, s);
-        DSS_HIP(hipMemcpyAsync(&nn, soff + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        exclusive_scan_i64(nv, soff, n, tmp_, s, mail + 4);
         DSS_HIP(hipStreamSynchronize(s));
+        nn = mh[4];
     }
     int cur = 0;
     Frontier *F = &fr_[cur];
@@ -2205,17 +2217,16 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
                            act, c, xoff, xyz, mode, fmask, orig, nvx, eoff, clip_f, clip_c, cflags, flags, xlist, xlist_n);
         hipLaunchKernelGGL(k_expand_exact, dim3((unsigned)std::min<int64_t>(grid_for(nn, 64), 1024)), dim3(64), 0, s, xlist,
                            xlist_n, F->f.p, F->i.p, F->j.p, F->meta.p, act, c, xoff, xyz, mode, orig, nvx);
-        exclusive_scan_i64(c, pos, nn, tmp_, s);
+        exclusive_scan_i64(c, pos, nn, tmp_, s, mail + 5);
         DSS_HIP(hipMemsetAsync(any_open, 0, sizeof(int), s));
         Frontier *G = &fr_[cur ^ 1];
         G->ensure(4 * nn + 1);  // <= 4 children per node: no host round trip before the write
         hipLaunchKernelGGL(k_expand_write, dim3(grid_for(nn, B)), dim3(B), 0, s, nn, F->f.p, F->id.p, F->i.p, F->j.p,
                            F->meta.p, act, pos, G->f.p, G->id.p, G->i.p, G->j.p, G->meta.p, any_open);
-        int64_t nn2 = 0;
-        int open = 0;
-        DSS_HIP(hipMemcpyAsync(&nn2, pos + nn, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        DSS_HIP(hipMemcpyAsync(&open, any_open, sizeof(int), hipMemcpyDeviceToHost, s));
+        mail_counters(reinterpret_cast<const unsigned int *>(any_open), nullptr, nullptr, mail + 6, s);
         DSS_HIP(hipStreamSynchronize(s));
+        const int64_t nn2 = mh[5];
+        const int open = (int)mh[6];
         cur ^= 1;
         F = G;
         nn = nn2;
@@ -2230,14 +2241,13 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
                            icnt, dcnt);
     int64_t *tot64 = fc64_.ensure(n + 1), *dc64 = dc64_.ensure(n + 1), *dpre = dpre_.ensure(n + 1);
     hipLaunchKernelGGL(k_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, flags, fkm, dcnt, tot64, dc64);
-    exclusive_scan_i64(tot64, offs, n, tmp_, s);
-    int64_t total = 0;
+    exclusive_scan_i64(tot64, offs, n, tmp_, s, mail + 7);
     if (nn > 0) {
         exclusive_scan_i64(icnt, ipos, nn, tmp_, s);
         exclusive_scan_i64(dc64, dpre, n, tmp_, s);
     }
-    DSS_HIP(hipMemcpyAsync(&total, offs + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     DSS_HIP(hipStreamSynchronize(s));
+    const int64_t total = mh[7];
     uint64_t *cells = cells_.ensure(total + 1);
     hipLaunchKernelGGL(k_cand_emit, dim3(grid_for(n, B)), dim3(B), 0, s, n, flags, fkm, st_id, finfo, offs, cells);
     if (nn > 0) {

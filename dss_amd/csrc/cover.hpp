@@ -31,6 +31,7 @@ class CoverEngine {
         if (h_ev_) (void)hipEventSynchronize(h_ev_);
         if (h_offs_) (void)hipHostFree(h_offs_);
         if (h_ev_) (void)hipEventDestroy(h_ev_);
+        if (mail_h_) (void)hipHostFree(mail_h_);
     }
     // Device pointers in, context-owned device buffers out (see dssg_cells).
     // The wave path (one wavefront per footprint) covers every footprint it
@@ -61,6 +62,10 @@ class CoverEngine {
     DevBuf<uint64_t> w_cells_;
     std::vector<int64_t> h_cnt_;
     int64_t *h_offs_ = nullptr, h_offs_cap_ = 0;  // pinned
+    // the general path's counts, written by the kernels that produce them
+    // into fine-grained host memory (no copy launch per read-back)
+    int64_t *mail_h_ = nullptr, *mail_d_ = nullptr;
+    int64_t *mailbox();
     hipEvent_t h_ev_ = nullptr;                   // the last upload from h_offs_
     std::vector<uint8_t> h_slow_;
     DevBuf<int64_t> cnt_, xoff_, eoff_, soff_, offs_, ncnt_, npos_, fc64_;

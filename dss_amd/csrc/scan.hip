@@ -92,7 +92,8 @@ __global__ __launch_bounds__(kSBlock) void k_scan_parts(long long *__restrict__ 
 }
 
 __global__ __launch_bounds__(kSBlock) void k_scan_down(const int64_t *__restrict__ in, int64_t n,
-                                                       const long long *__restrict__ part, int64_t *__restrict__ out)
+                                                       const long long *__restrict__ part, int64_t *__restrict__ out,
+                                                       int64_t *mail)
 {
     __shared__ long long ws[kSWaves];
     const int64_t i0 = (int64_t)blockIdx.x * kSTile + (int64_t)threadIdx.x * kSItems;
@@ -105,6 +106,7 @@ __global__ __launch_bounds__(kSBlock) void k_scan_down(const int64_t *__restrict
     for (int u = 0; u < kSItems; u++) {
         run += v[u];
         if (i0 + u < n) out[i0 + u + 1] = run;  // out[k + 1] = in[0] + ... + in[k]
+        if (mail && i0 + u + 1 == n) *mail = run;
     }
 }
 
@@ -114,7 +116,7 @@ __global__ __launch_bounds__(kSBlock) void k_scan_down(const int64_t *__restrict
 constexpr int64_t kSFoldTiles = 1024;
 __global__ __launch_bounds__(kSBlock) void k_scan_down_fold(const int64_t *__restrict__ in, int64_t n,
                                                             const long long *__restrict__ part,
-                                                            int64_t *__restrict__ out)
+                                                            int64_t *__restrict__ out, int64_t *mail)
 {
     __shared__ long long ws[kSWaves];
     long long pre = 0, total;
@@ -130,15 +132,27 @@ __global__ __launch_bounds__(kSBlock) void k_scan_down_fold(const int64_t *__res
     for (int u = 0; u < kSItems; u++) {
         run += v[u];
         if (i0 + u < n) out[i0 + u + 1] = run;
+        if (mail && i0 + u + 1 == n) *mail = run;
+    }
+}
+
+__global__ void k_mail_counters(const unsigned int *a, const unsigned int *b, const unsigned int *c, int64_t *mail)
+{
+    if (threadIdx.x == 0) {
+        mail[0] = a ? (int64_t)*a : 0;
+        mail[1] = b ? (int64_t)*b : 0;
+        mail[2] = c ? (int64_t)*c : 0;
     }
 }
 
 }  // namespace
 
-void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, DevBuf<unsigned char> &tmp, hipStream_t s)
+void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, DevBuf<unsigned char> &tmp, hipStream_t s,
+                        int64_t *mail)
 {
     if (n <= 0) {
         DSS_HIP(hipMemsetAsync(out, 0, sizeof(int64_t), s));
+        if (mail) DSS_HIP(hipMemsetAsync(mail, 0, sizeof(int64_t), s));
         return;
     }
     const int64_t nt = (n + kSTile - 1) / kSTile;
@@ -148,13 +162,19 @@ void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, DevBuf<unsig
         hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nt), dim3(kSBlock), 0, s, in, n, part);
         if (nt <= kSFoldTiles) {
             hipLaunchKernelGGL(k_scan_down_fold, dim3((unsigned)nt), dim3(kSBlock), 0, s, in, n, (const long long *)part,
-                               out);
+                               out, mail);
             DSS_HIP(hipGetLastError());
             return;
         }
         hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(kSBlock), 0, s, part, nt);
     }
-    hipLaunchKernelGGL(k_scan_down, dim3((unsigned)nt), dim3(kSBlock), 0, s, in, n, (const long long *)part, out);
+    hipLaunchKernelGGL(k_scan_down, dim3((unsigned)nt), dim3(kSBlock), 0, s, in, n, (const long long *)part, out, mail);
+    DSS_HIP(hipGetLastError());
+}
+
+void mail_counters(const unsigned int *a, const unsigned int *b, const unsigned int *c, int64_t *mail, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_mail_counters, dim3(1), dim3(64), 0, s, a, b, c, mail);
     DSS_HIP(hipGetLastError());
 }
 
