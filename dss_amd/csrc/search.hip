@@ -2322,6 +2322,31 @@ int64_t SearchEngine::touched(const dssg_index *idx, int64_t nq, const int64_t *
     return (int64_t)fetch(sum, s);
 }
 
+// The words of the join's control block the host reads after the join --
+// per region the unit, long-unit, pair and tagged-key counters, and misc
+// words 0..5 -- gathered into fine-grained host memory (one small launch
+// instead of a copy of the whole block).
+__global__ void k_ctl_mail(const unsigned long long *ctl, int units, int units_l, int out, int tout, int misc,
+                           int stride, int64_t *mail)
+{
+    const int t = threadIdx.x;
+    if (t < 32) {
+        const int base = t < 8 ? units : t < 16 ? units_l : t < 24 ? out : tout;
+        mail[t] = (int64_t)ctl[base + (t & 7) * stride];
+    } else if (t < 38) {
+        mail[t] = (int64_t)ctl[misc + (t - 32)];
+    }
+}
+
+int64_t *SearchEngine::mailbox()
+{
+    if (!mail_h_) {
+        DSS_HIP(hipHostMalloc((void **)&mail_h_, 64 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent));
+        DSS_HIP(hipHostGetDevicePointer((void **)&mail_d_, mail_h_, 0));
+    }
+    return mail_d_;
+}
+
 void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_offs, const uint64_t *q_cells,
                           const float *q_alt_lo, const float *q_alt_hi, const int64_t *q_tlo, const int64_t *q_thi,
                           const int32_t *q_owner, hipStream_t s, dssg_pairs *out, int64_t nqc_known)
@@ -2503,8 +2528,20 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         }
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
         unsigned long long h[kCtlWords];
-        DSS_HIP(hipMemcpyAsync(h, ctl, sizeof(h), hipMemcpyDeviceToHost, s));
-        DSS_HIP(hipStreamSynchronize(s));
+        {
+            int64_t *mail = mailbox();
+            hipLaunchKernelGGL(k_ctl_mail, dim3(1), dim3(64), 0, s, (const unsigned long long *)ctl, kCtlUnits,
+                               kCtlUnitsL, kCtlOut, kCtlTOut, kCtlMisc, kRegStride, mail);
+            DSS_HIP(hipStreamSynchronize(s));
+            volatile const int64_t *mh = mail_h_;
+            for (int r = 0; r < kRegions; r++) {
+                h[kCtlUnits + r * kRegStride] = (unsigned long long)mh[r];
+                h[kCtlUnitsL + r * kRegStride] = (unsigned long long)mh[8 + r];
+                h[kCtlOut + r * kRegStride] = (unsigned long long)mh[16 + r];
+                h[kCtlTOut + r * kRegStride] = (unsigned long long)mh[24 + r];
+            }
+            for (int m = 0; m < 6; m++) h[kCtlMisc + m] = (unsigned long long)mh[32 + m];
+        }
         int64_t nu = 0, umax = 0, umax_l = 0, omax = 0, tmax = 0;
         for (int r = 0; r < kRegions; r++) {
             const int64_t u = (int64_t)h[kCtlUnits + r * kRegStride], ul = (int64_t)h[kCtlUnitsL + r * kRegStride];
@@ -2589,14 +2626,16 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             hipLaunchKernelGGL(k_tag_bounds, dim3(grid_for(nt, kBlock)), dim3(kBlock), 0, s, nt, k2, hb, bs, be);
             hipLaunchKernelGGL(k_tag_dedupe, dim3((unsigned)nb), dim3(kDedupBlock), 0, s, k2, bs, be, hbm, k1, bc, ovf,
                                cnt + 10);
-            exclusive_scan_i64(bc, bo, nb, tmp2_, s);
+            // distinct pairs of the regular buckets (the scan total) and the
+            // flagged buckets' count, through the host mailbox
+            int64_t *mail = mailbox();
+            exclusive_scan_i64(bc, bo, nb, tmp2_, s, mail + 40);
             hipLaunchKernelGGL(k_tag_emit, dim3((unsigned)nb), dim3(256), 0, s, k1, bs, bc, bo, eb, fq + n, fe + n);
-            unsigned long long tail[2];  // distinct pairs of the regular buckets, flagged buckets
-            device_copy(cnt + 11, bo + nb, sizeof(int64_t), s);
-            DSS_HIP(hipMemcpyAsync(tail, cnt + 10, sizeof(tail), hipMemcpyDeviceToHost, s));
+            mail_counters(reinterpret_cast<const unsigned int *>(cnt + 10), nullptr, nullptr, mail + 41, s);
             DSS_HIP(hipStreamSynchronize(s));
-            nuq = (int64_t)tail[1];
-            if (tail[0]) {  // flagged buckets: full sort of their keys
+            volatile const int64_t *mh = mail_h_;
+            nuq = mh[40];
+            if (mh[41]) {  // flagged buckets: full sort of their keys
                 int64_t no = 0, nov = 0;
                 compact_if(nt, PredOvf{k2, ovf, hb}, EmitShift{k2, k1, hbm}, tmp_, tmp2_, s, dtot, &no);
                 radix_sort_keys(k1, k2, no, qb + eb, tmp_, s);

@@ -65,6 +65,13 @@ namespace dss {
 
 class SearchEngine {
    public:
+    SearchEngine() = default;
+    SearchEngine(const SearchEngine &) = delete;
+    SearchEngine &operator=(const SearchEngine &) = delete;
+    ~SearchEngine()
+    {
+        if (mail_h_) (void)hipHostFree(mail_h_);
+    }
     // Postings are kept only for cells in [cell_lo, cell_hi] (a cell-range
     // shard); entity cell lists stay whole, so the smallest-shared-cell rule
     // emits every pair on exactly one shard (long x long pairs: see search()).
@@ -157,6 +164,9 @@ class SearchEngine {
     int64_t tag_rcap_ = 0;  // tagged-key slots per region
     int64_t units_cap_hint_ = 0, units_cap_hint_l_ = 0;
     int64_t long_units_prev_ = INT64_MAX / 2;  // the previous batch's long-variant units (sizes its launch)
+    // the join's control words, gathered into fine-grained host memory
+    int64_t *mail_h_ = nullptr, *mail_d_ = nullptr;
+    int64_t *mailbox();
     int occ_long_ = 0;                         // long-variant workgroups per CU
     bool timing_ = false;
     int64_t tag_bucket_avg_ = 2048;
