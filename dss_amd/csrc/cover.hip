@@ -782,9 +782,10 @@ __global__ __launch_bounds__(64) void k_start(int64_t nd, const uint32_t *dlist,
                         const uint8_t *flags, const uint8_t *origin_in, const int32_t *nvx, const int64_t *eoff,
                         const double4 *clip_c, const uint8_t *cflags, int64_t *cnt, const int64_t *soff,
                         uint32_t *nf, uint64_t *nid, uint32_t *ni, uint32_t *nj, uint32_t *nmeta, StartDesc *sdesc,
-                        unsigned int *sdesc_n)
+                        unsigned int *sdesc_n, unsigned int *xlist_n)
 {
     const int64_t k = tid64();
+    if (PASS == 0 && k == 0) *sdesc_n = *xlist_n = 0u;  // (pass 1 appends to the first, the descent to the second)
     if (k >= nd) return;
     const int64_t f = dlist[k];  // a descent footprint (k_edge_counts)
     uint8_t md = mode[f];
@@ -956,9 +957,10 @@ __global__ __launch_bounds__(64) void k_expand_count(int64_t nn, const uint32_t 
                                const uint32_t *nmeta, uint8_t *act, int64_t *cnt, const int64_t *xoff, const V3 *xyz,
                                const uint8_t *mode, const uint8_t *fmask, const uint8_t *origin_in, const int32_t *nvx,
                                const int64_t *eoff, const double4 *clip_f, const double4 *clip_c, const uint8_t *cflags,
-                               const uint8_t *flags, uint32_t *xlist, unsigned int *xlist_n)
+                               const uint8_t *flags, uint32_t *xlist, unsigned int *xlist_n, int *any_open)
 {
     const int64_t k = tid64();
+    if (k == 0) *any_open = 0;  // (set by this level's k_expand_write)
     bool defer = false;
     if (k < nn) {
         const uint32_t m = nmeta[k];
@@ -1072,9 +1074,10 @@ __global__ __launch_bounds__(64) void k_expand_exact(const uint32_t *xlist, cons
 
 __global__ void k_expand_write(int64_t nn, const uint32_t *nf, const uint64_t *nid, const uint32_t *ni, const uint32_t *nj,
                                const uint32_t *nmeta, const uint8_t *act, const int64_t *pos, uint32_t *of, uint64_t *oid,
-                               uint32_t *oi, uint32_t *oj, uint32_t *ometa, int *any_open)
+                               uint32_t *oi, uint32_t *oj, uint32_t *ometa, int *any_open, unsigned int *xlist_n)
 {
     int64_t k = tid64();
+    if (k == 0) *xlist_n = 0u;  // the next level's list (this level's k_expand_exact has read it)
     if (k >= nn) return;
     uint8_t a = act[k];
     if (a == 0) return;
@@ -1108,8 +1111,9 @@ __global__ void k_expand_write(int64_t nn, const uint32_t *nf, const uint64_t *n
 // HBM) and adds each sum with one global atomic.
 constexpr int kItemBlock = 256;
 __global__ __launch_bounds__(kItemBlock) void k_item_counts(int64_t nn, const uint32_t *nf, const uint32_t *nmeta,
-                                                            int64_t *icnt, unsigned long long *fcnt)
+                                                            int64_t *icnt, unsigned long long *fcnt, int *nbig)
 {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *nbig = 0;  // (k_emit appends)
     __shared__ unsigned long long s_sum[kItemBlock];
     const int64_t k0 = (int64_t)blockIdx.x * kItemBlock, k = k0 + threadIdx.x;
     const uint32_t f0 = nf[k0];
@@ -2183,11 +2187,17 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     }
     int64_t *soff = soff_.ensure(n + 1);
     int64_t nn = 0;
+    // the descent's list counters, zeroed by the kernel before the one that
+    // appends to them (k_start<0>: start descriptors and the first level's
+    // exact list; k_expand_count / _write: the open flag, the next list;
+    // k_item_counts: the big items) -- no fill launches
+    unsigned int *sdesc_n = sdesc_n_.ensure(1), *xlist_n = xlist_n_.ensure(1);
+    int *any_open = flag_.ensure(1);
     if (nd > 0) {  // (none: no start nodes, no second sync)
         DSS_HIP(hipMemsetAsync(nv, 0, sizeof(int64_t) * n, s));
         hipLaunchKernelGGL(k_start<0>, dim3(grid_for(nd, 64)), dim3(64), 0, s, nd, dlist, xoff, xyz, mode, fmask, flags,
                            orig, nvx, eoff, clip_c, cflags, nv, soff, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                           nullptr);
+                           sdesc_n, xlist_n);
         exclusive_scan_i64(nv, soff, n, tmp_, s, mail + 4);
         DSS_HIP(hipStreamSynchronize(s));
         nn = mh[4];
@@ -2197,32 +2207,27 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     F->ensure(nn + 1);
     if (nn > 0) {
         StartDesc *sdesc = (StartDesc *)sdesc_.ensure(sizeof(StartDesc) * (size_t)(24 * nd + 1));
-        unsigned int *sdesc_n = sdesc_n_.ensure(1);
-        DSS_HIP(hipMemsetAsync(sdesc_n, 0, sizeof(unsigned int), s));
         hipLaunchKernelGGL(k_start<1>, dim3(grid_for(nd, 64)), dim3(64), 0, s, nd, dlist, xoff, xyz, mode, fmask, flags,
                            orig, nvx, eoff, clip_c, cflags, nullptr, soff, F->f.p, F->id.p, F->i.p, F->j.p, F->meta.p,
-                           sdesc, sdesc_n);
+                           sdesc, sdesc_n, nullptr);
         hipLaunchKernelGGL(k_start13, dim3((unsigned)std::min<int64_t>((24 * nd + 3) / 4, 1024)), dim3(256), 0, s, sdesc,
                            sdesc_n, F->f.p, F->id.p, F->i.p, F->j.p, F->meta.p);
     }
-    int *any_open = flag_.ensure(1);
-    unsigned int *xlist_n = xlist_n_.ensure(1);
     for (int iter = 0; iter < 32 && nn > 0; iter++) {
         uint8_t *act = act_.ensure(nn + 1);
         int64_t *c = ncnt_.ensure(nn + 1);
         int64_t *pos = npos_.ensure(nn + 1);
-        DSS_HIP(hipMemsetAsync(xlist_n, 0, sizeof(unsigned int), s));
         uint32_t *xlist = xlist_.ensure(nn + 1);
         hipLaunchKernelGGL(k_expand_count, dim3(grid_for(nn, 64)), dim3(64), 0, s, nn, F->f.p, F->i.p, F->j.p, F->meta.p,
-                           act, c, xoff, xyz, mode, fmask, orig, nvx, eoff, clip_f, clip_c, cflags, flags, xlist, xlist_n);
+                           act, c, xoff, xyz, mode, fmask, orig, nvx, eoff, clip_f, clip_c, cflags, flags, xlist, xlist_n,
+                           any_open);
         hipLaunchKernelGGL(k_expand_exact, dim3((unsigned)std::min<int64_t>(grid_for(nn, 64), 1024)), dim3(64), 0, s, xlist,
                            xlist_n, F->f.p, F->i.p, F->j.p, F->meta.p, act, c, xoff, xyz, mode, orig, nvx);
         exclusive_scan_i64(c, pos, nn, tmp_, s, mail + 5);
-        DSS_HIP(hipMemsetAsync(any_open, 0, sizeof(int), s));
         Frontier *G = &fr_[cur ^ 1];
         G->ensure(4 * nn + 1);  // <= 4 children per node: no host round trip before the write
         hipLaunchKernelGGL(k_expand_write, dim3(grid_for(nn, B)), dim3(B), 0, s, nn, F->f.p, F->id.p, F->i.p, F->j.p,
-                           F->meta.p, act, pos, G->f.p, G->id.p, G->i.p, G->j.p, G->meta.p, any_open);
+                           F->meta.p, act, pos, G->f.p, G->id.p, G->i.p, G->j.p, G->meta.p, any_open, xlist_n);
         mail_counters(reinterpret_cast<const unsigned int *>(any_open), nullptr, nullptr, mail + 6, s);
         DSS_HIP(hipStreamSynchronize(s));
         const int64_t nn2 = mh[5];
@@ -2238,7 +2243,7 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     int64_t *icnt = ncnt_.ensure(nn + 1), *ipos = npos_.ensure(nn + 1);
     if (nn > 0)
         hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nn, kItemBlock)), dim3(kItemBlock), 0, s, nn, F->f.p, F->meta.p,
-                           icnt, dcnt);
+                           icnt, dcnt, any_open /* = nbig */);
     int64_t *tot64 = fc64_.ensure(n + 1), *dc64 = dc64_.ensure(n + 1), *dpre = dpre_.ensure(n + 1);
     hipLaunchKernelGGL(k_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, flags, fkm, dcnt, tot64, dc64);
     exclusive_scan_i64(tot64, offs, n, tmp_, s, mail + 7);
@@ -2252,8 +2257,7 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     hipLaunchKernelGGL(k_cand_emit, dim3(grid_for(n, B)), dim3(B), 0, s, n, flags, fkm, st_id, finfo, offs, cells);
     if (nn > 0) {
         uint32_t *big = big_.ensure(nn + 1);
-        int *nbig = flag_.ensure(1);
-        DSS_HIP(hipMemsetAsync(nbig, 0, sizeof(int), s));
+        int *nbig = any_open;  // (the flag word, zeroed by k_item_counts)
         hipLaunchKernelGGL(k_emit, dim3(grid_for(nn, B)), dim3(B), 0, s, nn, F->f.p, F->id.p, F->meta.p, ipos, dpre, offs,
                            cells, big, nbig);
         hipLaunchKernelGGL(k_emit_big, dim3((unsigned)std::min<int64_t>(nn, 256)), dim3(256), 0, s, big,
