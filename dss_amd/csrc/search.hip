@@ -2326,6 +2326,7 @@ int64_t SearchEngine::touched(const dssg_index *idx, int64_t nq, const int64_t *
 // per region the unit, long-unit, pair and tagged-key counters, and misc
 // words 0..5 -- gathered into fine-grained host memory (one small launch
 // instead of a copy of the whole block).
+static_assert(kRegions == 8, "k_ctl_mail gathers 8 region counters per kind");
 __global__ void k_ctl_mail(const unsigned long long *ctl, int units, int units_l, int out, int tout, int misc,
                            int stride, int64_t *mail)
 {
