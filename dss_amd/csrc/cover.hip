@@ -1516,24 +1516,62 @@ __global__ void k_counts(int64_t n, const uint8_t *flags, const unsigned long lo
 }
 
 // The kept direct candidates of a footprint at its CSR offset, in id order
-// (one thread per footprint; keys ascend with the cell id).
-__global__ void k_cand_emit(int64_t n, const uint8_t *flags, const unsigned long long *fkm, const uint64_t *st_id,
-                            const uint32_t *finfo, const int64_t *offs, uint64_t *cells)
+// (keys ascend with the cell id).  One wave per 64 footprints emits their
+// cells 64 at a time: output j of the wave belongs to the last lane whose
+// exclusive count prefix is <= j (a 6-step search over the lanes) and is the
+// (j - prefix)-th set bit of that lane's 256-bit mask, so the trip count is
+// the wave's mean count, not its largest, and neighbouring lanes store to
+// neighbouring cells.
+__global__ __launch_bounds__(kBlock) void k_cand_emit(int64_t n, const uint8_t *flags, const unsigned long long *fkm,
+                                                      const uint64_t *st_id, const uint32_t *finfo,
+                                                      const int64_t *offs, uint64_t *cells)
 {
+    const int lane = (int)(threadIdx.x & 63);
     const int64_t f = tid64();
-    if (f >= n || !(flags[f] & FL_FAST)) return;
-    int64_t w = offs[f];
-    const int L = (int)(finfo[f] & 31u);
-    const int sh = 2 * (kCoverLevel - L);
-    const uint64_t lsbL = lsb_for_level(L), lsb13 = lsb_for_level(kCoverLevel);
-    for (int q = 0; q < 4; q++) {
-        unsigned long long mk = fkm[4 * f + q];
-        while (mk) {
-            const int c = 64 * q + __builtin_ctzll(mk);
-            mk &= mk - 1;
-            const uint64_t r = (uint64_t)(c & ((1 << sh) - 1));
-            cells[w++] = st_id[4 * f + (c >> sh)] - lsbL + lsb13 + r * (lsb13 << 1);
+    if (f - lane >= n) return;  // whole waves
+    unsigned long long m0 = 0, m1 = 0, m2 = 0, m3 = 0;
+    if (f < n && (flags[f] & FL_FAST)) {
+        const ulonglong2 *km = reinterpret_cast<const ulonglong2 *>(fkm + 4 * f);
+        const ulonglong2 a = km[0], b = km[1];
+        m0 = a.x, m1 = a.y, m2 = b.x, m3 = b.y;
+    }
+    const int c = __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+    int incl = c;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    const int excl = incl - c, T = __shfl(incl, 63);
+    if (T == 0) return;
+    const int64_t w0 = c ? offs[f] : 0;
+    const int L0 = c ? (int)(finfo[f] & 31u) : kCoverLevel;
+    const uint64_t lsb13 = lsb_for_level(kCoverLevel);
+    for (int base = 0; base < T; base += 64) {  // uniform trip count: every lane shuffles
+        const int j = base + lane;
+        int o = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1)
+            if (__shfl(excl, o + step) <= j) o += step;  // o + step <= 63
+        int k = j - __shfl(excl, o);
+        const unsigned long long a0 = __shfl(m0, o), a1 = __shfl(m1, o), a2 = __shfl(m2, o), a3 = __shfl(m3, o);
+        const int64_t w = __shfl(w0, o) + k;
+        const int L = __shfl(L0, o);
+        if (j >= T) continue;
+        // the k-th set bit, in (word, bit) order
+        int q = 0;
+        unsigned long long mk = a0;
+        if (k >= __popcll(mk)) { k -= __popcll(mk); mk = a1; q = 1;
+            if (k >= __popcll(mk)) { k -= __popcll(mk); mk = a2; q = 2;
+                if (k >= __popcll(mk)) { k -= __popcll(mk); mk = a3; q = 3; } } }
+        int bit = 0;
+#pragma unroll
+        for (int wdt = 32; wdt > 0; wdt >>= 1) {
+            const int lo = __popcll(mk & ((1ull << wdt) - 1));
+            if (k >= lo) { k -= lo; mk >>= wdt; bit += wdt; }
         }
+        const int cc = 64 * q + bit, sh = 2 * (kCoverLevel - L);
+        const uint64_t r = (uint64_t)(cc & ((1 << sh) - 1));
+        cells[w] = st_id[4 * (f - lane + o) + (cc >> sh)] - lsb_for_level(L) + lsb13 + r * (lsb13 << 1);
     }
 }
 
