@@ -59,6 +59,11 @@ _JSON_FD = [None]
 # then stops the other ranks).
 STAGE_LIMIT_S = {"native exchange init": 300, "warmup": 900, "timed steps": 900,
                  "replica rate beside the sharded one": 900, "sharded phases": 900}
+# The sharded leg of an N > 1 replica run (sharded_leg): a stage of it that
+# runs past its limit ends the rank with status 0 -- the replica line is
+# complete -- and rank 0 prints that line with sharded.error set.
+LEG_LIMIT_S = 300
+_PENDING = [None, 0]  # rank 0's finished replica line while the sharded leg runs; this rank
 
 
 def keep_stdout_for_json():
@@ -95,6 +100,13 @@ def heartbeat(every=30.0):
         while True:
             time.sleep(every)
             log(f"[bench] alive {time.time() - t0:.0f}s, stage: {_STAGE[0]}")
+            if _STAGE[0].startswith("sharded leg") and time.time() - _STAGE[1] > LEG_LIMIT_S:
+                log(f"[bench] stage '{_STAGE[0]}' exceeded {LEG_LIMIT_S}s: the sharded leg is abandoned")
+                if _PENDING[0] is not None and _PENDING[1] == 0:
+                    _PENDING[0]["sharded"] = {"error": f"stage '{_STAGE[0]}' exceeded {LEG_LIMIT_S}s (a collective "
+                                                       f"presumed hung); the replica line stands"}
+                    emit(_PENDING[0])
+                os._exit(0)
             limit = STAGE_LIMIT_S.get(_STAGE[0])
             if limit and time.time() - _STAGE[1] > limit:
                 log(f"[bench] stage '{_STAGE[0]}' exceeded {limit}s: exiting (a collective is presumed hung)")
@@ -133,6 +145,10 @@ def parse_args(argv=None):
                     help="multi-GPU layout: replica (index on every GPU, query batches split across ranks, no "
                          "data-path collective; the default) or sharded (index split by S2 cell range, queries and "
                          "pairs exchanged by all-to-all, BASELINE's layout, with the replica rate reported beside it)")
+    ap.add_argument("--sharded-leg", type=int, default=1,
+                    help="N > 1, replica mode: after the replica line's steps, the same ranks time the cell-range "
+                         "shards (BASELINE's layout) over the library's RCCL exchange and attach them as the line's "
+                         "`sharded` record (value stays the replica rate); 0: skip")
     ap.add_argument("--exchange", choices=["native", "torch"], default=None,
                     help="sharded mode's all-to-alls: native (the library's own RCCL communicator, "
                          "dssg_sharded_search_device) or torch (torch.distributed; the instrumented path).  Default: "
@@ -450,8 +466,10 @@ def main():
     # timing max, parity flags).  With the library's own RCCL exchange it is
     # gloo, so each process holds one RCCL (the library's); the torch
     # exchange (fallback / rehearsals) runs over the PG or an RCCL subgroup.
-    native_wanted = mode == "sharded" and exchange == "native"
+    leg = mode == "replica" and world > 1 and args.sharded_leg != 0
+    native_wanted = (mode == "sharded" or leg) and exchange == "native"
     pg_backend = "gloo" if native_wanted else args.dist_backend
+    _PENDING[1] = rank
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")   # single-process sharded runs (no launcher)
     os.environ.setdefault("MASTER_PORT", "29533")
     if world > 1 or mode == "sharded":
@@ -515,52 +533,8 @@ def main():
                                f"beside it; the build's sorts are inside index_build_s"})
     sharded = native = None
     if mode == "sharded":
-        if native_wanted:
-            # the library's own communicators (queries; pairs home on a second
-            # stream); if any rank cannot open them (no RCCL to dlopen, init
-            # error) every rank falls back to the torch exchange, agreed by
-            # one all-reduce, and the line says so
-            stage("native exchange init")
-            ok = torch.ones(1)
-            err = None
-            # the ids travel once over the control group, with rank 0's
-            # success flag: every rank takes part in every broadcast, and no
-            # rank starts a communicator init another rank will not join
-            uids = torch.zeros(2, _lib.COMM_ID_BYTES + 1, dtype=torch.uint8)
-            if rank == 0:
-                try:
-                    for k in range(2):
-                        uids[k, :-1].copy_(torch.frombuffer(bytearray(shard.NativeComm.unique_id(ctx)),
-                                                            dtype=torch.uint8))
-                        uids[k, -1] = 1
-                except Exception as e:  # noqa: BLE001 -- reported in the result line
-                    err = f"{type(e).__name__}: {e}"
-            dist.broadcast(uids, 0)
-            if int(uids[:, -1].min()) == 1:
-                try:
-                    comms = [shard.NativeComm(ctx, world, rank, bytes(uids[k, :-1].numpy())) for k in range(2)]
-                    native = shard.NativeShardedSearch(ctx, comms[0], index, ranges, xcomm=comms[1],
-                                                       xstream=torch.cuda.Stream(device=dev))
-                except Exception as e:  # noqa: BLE001 -- reported in the result line
-                    err = f"{type(e).__name__}: {e}"
-                    ok.zero_()
-            else:
-                err = err or "rank 0 could not make an RCCL id"
-                ok.zero_()
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            if ok.item() < 1:
-                log(f"[rank {rank}] native exchange unavailable ({err}); using the torch exchange")
-                native = None
-                exchange = f"torch (native exchange init failed on some rank: {err})"
-        if native is None:
-            # the torch-collective exchange: over RCCL when the data path may
-            # use it (a subgroup beside the gloo control group), else staged
-            # through host memory (gloo rehearsals)
-            group = None
-            if pg_backend != "nccl" and args.dist_backend == "nccl":
-                group = dist.new_group(backend="nccl")
-            sharded = shard.ShardedSearch(ctx, index, ranges, group=group,
-                                          stage_host=group is None and pg_backend != "nccl")
+        native, sharded, exchange = make_exchange(args, ctx, dist, torch, dev, rank, index, ranges, exchange,
+                                                  native_wanted, pg_backend)
 
     def shard_search(cells, timed_phases=False):
         if native is not None:
@@ -637,6 +611,7 @@ def main():
     import ctypes as C
     ctx.L.dssg_set_timing(ctx.h, 1)
     cover_ms, join_ms, kern_ms = [], [], []
+    ctx.join_profile()  # (a counting build: clear what the timed steps summed)
     for _ in range(5):
         cells, pairs = step()
         ca, cb, cc = C.c_double(), C.c_double(), C.c_double()
@@ -645,6 +620,10 @@ def main():
         join_ms.append(cb.value)
         kern_ms.append(cc.value)
     ctx.L.dssg_set_timing(ctx.h, 0)
+    jprof = ctx.join_profile()
+    if jprof:  # per search (the 5 phase-timing steps, one pipeline)
+        jprof = {k: v / 5 for k, v in jprof.items()}
+        jprof["yield"] = jprof["kept"] / max(1.0, jprof["lane_tests"])
     n_keys, n_units, n_runs, n_iters, n_tests = (C.c_int64() for _ in range(5))
     ctx.check(ctx.L.dssg_search_counters(ctx.h, C.byref(n_keys), C.byref(n_units), C.byref(n_runs), C.byref(n_iters),
                                          C.byref(n_tests)))
@@ -690,12 +669,7 @@ def main():
                              i_cells_t, cells, pairs)
     result = None
     if rank == 0:
-        # last: the per-request calls reuse the context's cover / search
-        # buffers that `cells` and `pairs` point into
-        latency = None
-        if args.latency:
-            stage("single-request latency")
-            latency = request_latency(ctx, D, index, queries, qa, now)
+        latency = None  # (measured last, below)
         traffic = pmc_traffic("k_join", nq, ni)
         result = {
             "metric": "4D conflict queries/sec vs N-intent airspace",
@@ -714,7 +688,9 @@ def main():
                                    f"index, {W.CONFIG_NAMES[args.config]}, S2 level 13"
                                    + (" (SearchISAs semantics)" if rid else ""),
                        "queries_per_gpu_step": nq, "intents": ni, "postings": n_post, "index": index_info(ctx, index),
-                       "parallelism": f"query-sharded x{world}, index replicated", "scale": args.scale,
+                       "parallelism": f"query-sharded x{world}, index replicated"
+                                      + ("; the cell-range shards timed after by the same ranks: `sharded`" if leg else ""),
+                       "scale": args.scale,
                        "pipelines_per_gpu": 1 + len(workers), "pipelines_note": pipe_note},
             "coverings_per_s": world * nq / (cover_avg * 1e-3),
             "phase_ms": {"cover": cover_avg, "join": join_avg, "join_kernel": kern_avg_ms},
@@ -723,7 +699,9 @@ def main():
                           "wave_iters": n_iters.value, "lane_tests": n_tests.value, "flushes": n_fl.value,
                           "exact_merges": n_mg.value, "exact_merge_lanes": n_ml.value,
                           "long_pair_occurrences": n_tg.value, "long_queries": n_lq.value,
-                          "long_postings": n_lp.value},
+                          "long_postings": n_lp.value,
+                          "yield": r_tot / max(1, n_tests.value),
+                          "predicates": jprof},
             "index_build_s": build_s,
             "sort_phase": sort_ph,
             "cover_fp64": cover_fp64(nq, ni),
@@ -744,10 +722,191 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
         }
+        _PENDING[0] = result
+    if leg:
+        # BASELINE configs[2]'s layout timed by the same ranks after the
+        # replica line's steps (the line's value stays the replica rate)
+        rec = sharded_leg(args, ctx, D, dist, torch, dev, _lib, local, tunes, rank, world, nq, d_q, qargs, index,
+                          icells, (i_alo, i_ahi, i_t0, i_t1), i_cells_t, exchange, native_wanted, pg_backend)
+        if rank == 0:
+            result["sharded"] = rec
+    if rank == 0:
+        # last: the per-request calls reuse the context's cover / search
+        # buffers that `cells` and `pairs` point into
+        if args.latency:
+            stage("single-request latency")
+            result["request_latency"] = request_latency(ctx, D, index, queries, qa, now)
+        _PENDING[0] = None
         emit(result)
     ctx.L.dssg_index_free(index)
     if world > 1:
         dist.destroy_process_group()
+
+
+def make_exchange(args, ctx, dist, torch, dev, rank, index, ranges, exchange, native_wanted, pg_backend, tag=""):
+    """The sharded step's exchange: the library's own communicators (queries;
+    pairs home on a second stream) when wanted, else -- or if any rank cannot
+    open them (no RCCL to dlopen, init error; every rank falls back together,
+    agreed by one all-reduce, and the line says so) -- the torch-collective
+    exchange over RCCL (a subgroup beside the gloo control group) or staged
+    through host memory (gloo rehearsals).  Returns (native, sharded, exchange)."""
+    from dss_amd import _lib, shard
+    native = sharded = None
+    world = dist.get_world_size()
+    if native_wanted:
+        stage(tag + "native exchange init")
+        ok = torch.ones(1)
+        err = None
+        # the ids travel once over the control group, with rank 0's success
+        # flag: every rank takes part in every broadcast, and no rank starts a
+        # communicator init another rank will not join
+        uids = torch.zeros(2, _lib.COMM_ID_BYTES + 1, dtype=torch.uint8)
+        if rank == 0:
+            try:
+                for k in range(2):
+                    uids[k, :-1].copy_(torch.frombuffer(bytearray(shard.NativeComm.unique_id(ctx)), dtype=torch.uint8))
+                    uids[k, -1] = 1
+            except Exception as e:  # noqa: BLE001 -- reported in the result line
+                err = f"{type(e).__name__}: {e}"
+        dist.broadcast(uids, 0)
+        if int(uids[:, -1].min()) == 1:
+            try:
+                comms = [shard.NativeComm(ctx, world, rank, bytes(uids[k, :-1].numpy())) for k in range(2)]
+                native = shard.NativeShardedSearch(ctx, comms[0], index, ranges, xcomm=comms[1],
+                                                   xstream=torch.cuda.Stream(device=dev))
+            except Exception as e:  # noqa: BLE001 -- reported in the result line
+                err = f"{type(e).__name__}: {e}"
+                ok.zero_()
+        else:
+            err = err or "rank 0 could not make an RCCL id"
+            ok.zero_()
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if ok.item() < 1:
+            log(f"[rank {rank}] native exchange unavailable ({err}); using the torch exchange")
+            native = None
+            exchange = f"torch (native exchange init failed on some rank: {err})"
+    if native is None:
+        group = None
+        if pg_backend != "nccl" and args.dist_backend == "nccl":
+            group = dist.new_group(backend="nccl")
+        sharded = shard.ShardedSearch(ctx, index, ranges, group=group, stage_host=group is None and pg_backend != "nccl")
+    return native, sharded, exchange
+
+
+_ORACLE_SAMPLE = {}  # this rank's oracle pair keys of its parity sample (cpu_baseline), for the sharded leg
+
+
+def sharded_leg(args, ctx, D, dist, torch, dev, _lib, local, tunes, rank, world, nq, d_q, qargs, index, icells, iattrs,
+                i_cells_t, exchange, native_wanted, pg_backend):
+    """N > 1, replica mode: the cell-range shards BASELINE configs[2] names
+    (partitioned like the reference's scd_cells_operations PK
+    (cell_id, operation_id), pkg/scd/store/cockroach/store.go:140-147), timed
+    by the same rank processes after the replica steps -- under torchrun
+    there is no parent of ours to start a second set.  Each rank builds its
+    shard, opens the library's RCCL communicators (the control group is gloo,
+    so the library's RCCL is the process's only one), runs --warmup steps and
+    then exactly --steps sharded steps (cover ahead on the other pipelines,
+    route -> query all-to-all -> shard join -> pairs home on the exchange
+    stream), barrier + synchronize around them, max over ranks.  Parity on
+    every rank: its delivered pairs of its oracle sample == the oracle's pair
+    keys kept from the replica leg (exact), and its whole delivered set ==
+    the replica index's search of the same covering (count + checksum).
+    Returns the `sharded` record; {"error": ...} if the leg raised (a hung
+    collective ends the rank through the stage watchdog, LEG_LIMIT_S)."""
+    import traceback
+
+    from dss_amd import shard
+    rec = {"layout": f"cell-range shards x{world}: the intent index split at posting quantiles into {world} S2 "
+                     f"cell-id ranges (whole quads), one per GPU; queries routed to the shards owning their cells "
+                     f"and pairs routed home by all-to-all"}
+    shard_index = native = sharded = None
+    workers = []
+    try:
+        stage("sharded leg: shard build")
+        ranges = shard.cell_splitters(i_cells_t.cpu().numpy().view(np.uint64), world)
+        tb = time.time()
+        shard_index = D.build_index(ctx, icells, *iattrs, cell_range=ranges[rank])
+        torch.cuda.synchronize()
+        rec["index_build_s_rank0"] = time.time() - tb
+        rec["postings_rank0"] = int(ctx.L.dssg_index_num_postings(shard_index))
+        native, sharded, exchange = make_exchange(args, ctx, dist, torch, dev, rank, shard_index, ranges, exchange,
+                                                  native_wanted, pg_backend, tag="sharded leg: ")
+        rec["exchange"] = "the library's RCCL communicators (dssg_sharded_search_async_device)" \
+            if native is not None else exchange
+
+        def shard_search(cells, timed_phases=False):
+            if native is not None:
+                return native.step(cells.offs, cells.cells, nq, *qargs)
+            return sharded.step(cells.offs, cells.cells, nq, *qargs, timed=timed_phases)
+
+        stage("sharded leg: warmup")
+        for _ in range(max(1, args.warmup)):
+            shard_search(D.cover(ctx, d_q))
+        torch.cuda.synchronize()
+        workers, note = add_pipelines(args, torch, D, _lib, local, dev, tunes, d_q, None)
+        stage("sharded leg: timed steps")
+        el = timed(torch, dist, dev, world,
+                   lambda: cover_ahead_steps(torch, D, ctx, workers, d_q, args.steps, shard_search))
+        rec.update({"value": world * nq * args.steps / el, "unit": "queries/s", "ms_per_step": 1000.0 * el / args.steps,
+                    "steps": args.steps, "warmup": max(1, args.warmup), "pipelines_per_gpu": 1 + len(workers),
+                    "pipelines_note": note})
+        for wctx, _ in workers:
+            wctx.close()
+        workers = []
+        # one instrumented step: phases (max over ranks) and bytes moved
+        stage("sharded leg: phases")
+        names = ["route", "exchange_queries", "join", "route_pairs", "exchange_pairs"]
+        ctx.L.dssg_set_timing(ctx.h, 1)
+        if sharded is not None:
+            sharded.times = {}
+        cells = D.cover(ctx, d_q)
+        out = shard_search(cells, True)
+        torch.cuda.synchronize()
+        ctx.L.dssg_set_timing(ctx.h, 0)
+        if native is not None:
+            ms, cnt = native.stats()
+            moved = {k: cnt[k] for k in ("query_bytes_sent", "query_bytes_recv", "pair_bytes_sent", "pair_bytes_recv")}
+            ph = [ms[k] for k in names]
+        else:
+            ph = [1000.0 * sharded.times.get(k, 0.0) for k in names]
+            moved = dict(sharded.last_bytes)
+        rec["phase_ms_max_over_ranks"] = dict(zip(names, allreduce_vals(dist, torch, ph, dist.ReduceOp.MAX)))
+        rec["bytes_per_step_rank0"] = moved
+        # parity
+        stage("sharded leg: parity")
+        gq, ge = sample_pairs_host(ctx, D, torch, dev, out, nq)
+        got = (gq.astype(np.uint64) << np.uint64(32)) | ge.astype(np.uint64)
+        n_s, okeys = _ORACLE_SAMPLE.get("n", 0), _ORACLE_SAMPLE.get("keys")
+        o_ok = okeys is not None and np.array_equal(np.sort(got[gq < n_s]), okeys)
+        rp = D.search(ctx, index, cells, *qargs)
+        fq, fe = sample_pairs_host(ctx, D, torch, dev, rp, nq)
+        want = (fq.astype(np.uint64) << np.uint64(32)) | fe.astype(np.uint64)
+        w_ok = len(want) == len(got) and pair_checksum(want) == pair_checksum(got)
+        local_v = [1.0 if o_ok else 0.0, 1.0 if w_ok else 0.0, float(n_s), float(len(got)),
+                   float(sum(moved.values()))]
+        mins = allreduce_vals(dist, torch, local_v, dist.ReduceOp.MIN)
+        sums = allreduce_vals(dist, torch, local_v, dist.ReduceOp.SUM)
+        rec["bytes_per_step_all_ranks"] = sums[4]
+        rec["pairs_per_step_all_ranks"] = sums[3]
+        rec["parity"] = {"oracle_all_ranks_equal": bool(mins[0] == 1.0), "oracle_queries_all_ranks": int(sums[2]),
+                         "oracle_check": "per rank: its delivered pairs of the queries in its oracle sample (rank 0: "
+                                         "the CPU baseline's, the others: --parity-sample) == the oracle's pairs of "
+                                         "those queries, exactly",
+                         "all_ranks_equal": bool(mins[1] == 1.0),
+                         "whole_index_check": "per rank: count + sum(splitmix64(q << 32 | e)) of the delivered pairs "
+                                              "== the replica index's search of the same covering"}
+    except Exception as e:  # noqa: BLE001 -- reported in the line; the replica line stands
+        log(traceback.format_exc())
+        rec["error"] = f"{type(e).__name__}: {e}"
+    finally:
+        for wctx, _ in workers:
+            wctx.close()
+        if native is not None:
+            native.close()
+        if shard_index is not None:
+            ctx.L.dssg_index_free(shard_index)
+        torch.cuda.synchronize()
+    return rec
 
 
 def mix64(x: np.ndarray) -> np.ndarray:
@@ -1338,6 +1497,7 @@ def cpu_baseline(args, rank, n, intents, ia, queries, qa, now, intent_csr_fn, g_
     gk = np.sort((gq.astype(np.uint64) << np.uint64(32)) | ge.astype(np.uint64))
     ok = (rq.astype(np.uint64) << np.uint64(32)) | re.astype(np.uint64)
     ok.sort()
+    _ORACLE_SAMPLE.update(n=n, keys=ok)  # (the sharded leg checks its delivered pairs against these)
     parity = None
     if not args.no_verify:
         parity = {"queries": n, "of_batch": queries.n, "cells_equal": bool(np.array_equal(g_offs, qo) and

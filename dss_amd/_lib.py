@@ -157,6 +157,9 @@ def load():
         L.dssg_set_tuning.argtypes = [vp, C.c_char_p, C.c_int64]
         L.dssg_join_events.argtypes = [vp, P(i64), P(i64), P(i64), P(i64)]
         L.dssg_join_longs.argtypes = [vp, P(i64), P(i64)]
+        L.dssg_join_profile.argtypes = [vp, P(i64), C.c_int, P(C.c_int)]
+        L.dssg_join_profile_name.argtypes = [C.c_int]
+        L.dssg_join_profile_name.restype = C.c_char_p
         L.dssg_search_counters.argtypes = [vp, P(i64), P(i64), P(i64), P(i64), P(i64)]
         L.dssg_search_stats_device.argtypes = [vp, vp, i64, vp, vp, vp, P(i64), P(i64)]
         L.dssg_search_touched_device.argtypes = [vp, vp, i64, vp, vp, vp, P(i64)]
@@ -206,6 +209,16 @@ class Context:
     def set_tuning(self, key: str, value: int):
         """dssg_set_tuning (e.g. "tag_bucket_avg")."""
         self.check(self.L.dssg_set_tuning(self.h, key.encode(), int(value)))
+
+    def join_profile(self) -> dict | None:
+        """dssg_join_profile: the counting build's per-predicate sums since
+        the last call ({name: count}); None from the shipped library."""
+        buf = (C.c_int64 * 64)()
+        n = C.c_int()
+        self.check(self.L.dssg_join_profile(self.h, buf, 64, C.byref(n)))
+        if n.value == 0:
+            return None
+        return {self.L.dssg_join_profile_name(i).decode(): int(buf[i]) for i in range(n.value)}
 
     def close(self):
         if getattr(self, "h", None):

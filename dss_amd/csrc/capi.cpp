@@ -318,6 +318,15 @@ int dssg_join_longs(dssg_ctx *ctx, int64_t *long_queries, int64_t *long_postings
     return DSSG_OK;
 }
 
+int dssg_join_profile(dssg_ctx *ctx, int64_t *out, int n, int *written)
+{
+    if (!ctx || n < 0 || (n && !out) || !written) return DSSG_ERR_INVALID;
+    *written = 0;
+    return guarded(ctx, [&] { *written = dss::join_profile_read(out, n); });
+}
+
+const char *dssg_join_profile_name(int i) { return dss::join_profile_name(i); }
+
 int dssg_cover_batch_device(dssg_ctx *ctx, int64_t n, const int32_t *d_kind, const int64_t *d_voff, const double *d_lat,
                             const double *d_lng, const float *d_radius_m, void *stream, dssg_cells *out)
 {
@@ -960,9 +969,9 @@ int dssg_radix_sort_device(dssg_ctx *ctx, int key_bytes, int64_t n, int bits, co
             DSS_HIP(hipEventCreate(&e1));
             DSS_HIP(hipEventRecord(e0, s));
         }
-        if (key_bytes == 8 && d_vals_in)
-            dss::radix_sort_pairs((const unsigned long *)d_keys_in, (unsigned long *)d_keys_out, d_vals_in, d_vals_out, n,
-                                  bits, ctx->sort_tmp, s);
+        if (key_bytes == 8 && d_vals_in)  // (packed 8-B words when the keys' constant low bits hold the values)
+            dss::radix_sort_pairs_packed((const uint64_t *)d_keys_in, (uint64_t *)d_keys_out, d_vals_in, d_vals_out, n,
+                                         bits, ctx->sort_tmp, s);
         else if (key_bytes == 8)
             dss::radix_sort_keys((const unsigned long *)d_keys_in, (unsigned long *)d_keys_out, n, bits, ctx->sort_tmp, s);
         else
@@ -1212,6 +1221,20 @@ void sharded_step(dssg_ctx *ctx, dssg_comm *cq, dssg_comm *cx, const dssg_index 
         // is joined as given (no copies, no collectives)
         const int64_t nqc = d_q_offs == ctx->cov_offs && nq == ctx->cov_n ? ctx->cov_total : -1;
         ctx->search.search(shard, nq, d_q_offs, d_q_cells, d_q_alt_lo, d_q_alt_hi, d_q_tlo, d_q_thi, nullptr, s, out, nqc);
+        if (x != s) {
+            // async: like every routed step, the output lives in the buffer
+            // set of this step (valid until the second next call) -- the
+            // engine's result buffers are swapped into it, no copy
+            const int b = cx->flip;
+            cx->flip ^= 1;
+            if (!ctx->search.adopt_output(*out, cx->out_q[b], cx->out_e[b])) {
+                uint32_t *q = cx->out_q[b].ensure((size_t)out->n + 1), *e = cx->out_e[b].ensure((size_t)out->n + 1);
+                dss::device_copy(q, out->q, sizeof(uint32_t) * (size_t)out->n, s);
+                dss::device_copy(e, out->e, sizeof(uint32_t) * (size_t)out->n, s);
+                out->q = q;
+                out->e = e;
+            }
+        }
         out->n_tagged = 0;
         st.join_ms = -1;
         return;

@@ -56,7 +56,7 @@ struct IndexView {
     const longlong2 *b_t;
     const ulonglong2 *b_sig;
     const int32_t *b_owner;  // nullptr: built without owners
-    const uint32_t *b_mult;  // nullptr: every multiplicity is 1; else 8 bits per child of the quad
+    const uint32_t *b_mult;  // nullptr: every multiplicity is 1; else 8 bits per child (quads) or 32 (cells)
     const int64_t *e_offs;
     const uint64_t *e_cells;
     const int64_t *e_t1;     // entity end time (us)
@@ -134,10 +134,12 @@ __device__ __forceinline__ uint64_t quad_first_cell(const IndexView &a, uint32_t
     return a.irr_cells[slot - (uint32_t)a.n_dense];
 }
 // A posting's multiplicity for one child of its quad (the times (cell,
-// entity) occurs in the stored array: 8 bits per child, b_mult).
+// entity) occurs in the stored array: 8 bits per child at the quad grain, the
+// whole word at the cell grain -- b_mult).
 __device__ __forceinline__ uint32_t child_mult(const IndexView &a, uint64_t p, uint32_t bit)
 {
     if (!a.b_mult) return 1u;
+    if (a.gshift == kCellShift) return a.b_mult[p];
     return (a.b_mult[p] >> (8u * (uint32_t)__builtin_ctz(bit))) & 0xffu;
 }
 // Postings of a slot: [s, e), the regular ones [s, s + nreg).

@@ -140,13 +140,18 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scan(uint32_t *__restrict__ hist
     if (threadIdx.x == 0) dtot[blockIdx.x] = carry;
 }
 
-template <typename K, typename V, bool HAS_V>
+// PK (packed 8-B words, radix_sort_pairs_packed): bit 0 -- the pass reads
+// (key, value) and sorts the word (key & ~lomask) | value; bit 1 -- it writes
+// the word back out as (word & ~lomask) | kconst and value word & lomask.
+// Middle passes move the words alone (HAS_V false).
+template <typename K, typename V, bool HAS_V, int PK = 0>
 __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki, const V *__restrict__ vi,
                                                         K *__restrict__ ko, V *__restrict__ vo, int64_t n,
                                                         const int64_t *__restrict__ dn, int shift, int rbits,
                                                         const uint32_t *__restrict__ hist, int64_t stride,
-                                                        const uint32_t *__restrict__ dtot)
+                                                        const uint32_t *__restrict__ dtot, K lomask = 0, K kconst = 0)
 {
+    static_assert(PK == 0 || !HAS_V, "packed passes stage the words alone");
     if (dn) n = min(n, *dn);
     __shared__ uint32_t wh[kRWaves][kMaxDigits];  // per-wave digit counters, then their exclusive prefix over waves
     __shared__ uint32_t dstart[kMaxDigits];       // tile-local start of each digit
@@ -186,7 +191,8 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
     for (int j = 0; j < kItems; j++) {
         const int64_t i = sub + j * 64 + lane;
         const bool ok = i < n;
-        k[j] = ok ? ki[i] : K(0);
+        if constexpr ((PK & 1) != 0) k[j] = ok ? ((ki[i] & ~lomask) | (K)vi[i]) : K(0);
+        else k[j] = ok ? ki[i] : K(0);
         if (HAS_V) v[j] = ok ? vi[i] : V(0);
     }
 #pragma unroll
@@ -247,7 +253,12 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
     for (int i = tid; i < tile_n; i += kRBlock) {
         const K kk = sk[i];
         const uint32_t p = gbase[digit_of(kk, shift, mask)] + (uint32_t)i;
-        ko[p] = kk;
+        if constexpr ((PK & 2) != 0) {
+            ko[p] = (kk & ~lomask) | kconst;
+            vo[p] = (V)(kk & lomask);
+        } else {
+            ko[p] = kk;
+        }
         if (HAS_V) vo[p] = sv[i];
     }
 }
@@ -255,24 +266,39 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
 // OR over all keys of (key ^ keys[0]): the bits that vary.  Bits constant
 // across the batch need no pass (a level-13 cell id varies in bits 35..63
 // only, so a 64-bit (cell, entity) sort runs 4 passes instead of 8).
+// (vals != nullptr: the OR of the values too, in part[np + block] -- the
+// value bits a packed sort must leave room for)
 template <typename K>
 __global__ __launch_bounds__(kRBlock) void k_rs_varying(const K *__restrict__ keys, int64_t n,
-                                                        unsigned long long *__restrict__ part)
+                                                        unsigned long long *__restrict__ part,
+                                                        const uint32_t *__restrict__ vals = nullptr)
 {
-    __shared__ unsigned long long wacc[kRWaves];
+    __shared__ unsigned long long wacc[kRWaves], wv[kRWaves];
     const K k0 = keys[0];
-    unsigned long long acc = 0;
-    for (int64_t i = (int64_t)blockIdx.x * kRBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kRBlock)
+    unsigned long long acc = 0, vacc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kRBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kRBlock) {
         acc |= (unsigned long long)(keys[i] ^ k0);
+        if (vals) vacc |= vals[i];
+    }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) acc |= __shfl_xor(acc, off, 64);
-    if ((threadIdx.x & 63) == 0) wacc[threadIdx.x >> 6] = acc;
+    for (int off = 32; off > 0; off >>= 1) {
+        acc |= __shfl_xor(acc, off, 64);
+        vacc |= __shfl_xor(vacc, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        wacc[threadIdx.x >> 6] = acc;
+        wv[threadIdx.x >> 6] = vacc;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned long long r = 0;
+        unsigned long long r = 0, rv = 0;
 #pragma unroll
-        for (int i = 0; i < kRWaves; i++) r |= wacc[i];
+        for (int i = 0; i < kRWaves; i++) {
+            r |= wacc[i];
+            rv |= wv[i];
+        }
         part[blockIdx.x] = r;  // one partial per block: no same-address atomics
+        if (vals) part[gridDim.x + blockIdx.x] = rv;
     }
 }
 
@@ -360,7 +386,84 @@ void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, const int64_t
     }
 }
 
+// (u64 key, u32 value) pairs sorted as packed 8-B words when the keys' low
+// bits below their lowest varying bit are constant and wide enough for every
+// value (level-13 cell ids: bits 0..34 constant, entity ids < 2^32): the
+// first pass packs (key & ~lomask) | value, the middle passes move 8 B per
+// element instead of 12, the last unpacks.  Stable on the key bits, so equal
+// keys keep their input order -- (cell, entity) postings arriving in entity
+// order leave in PK (cell_id, operation_id) order.  Otherwise: radix_sort.
+void radix_sort_packed(const uint64_t *ki, uint64_t *ko, const uint32_t *vi, uint32_t *vo, int64_t n, int bits,
+                       DevBuf<unsigned char> &tmp, hipStream_t s)
+{
+    using K = uint64_t;
+    if (n <= 0) return;
+    if (n >= ((int64_t)1 << 32) - kTile) throw Error(DSSG_ERR_CAPACITY, "radix sort: more than 2^32 - 2048 keys");
+    if (bits > 64) bits = 64;
+    const int64_t ntiles = (n + kTile - 1) / kTile, stride = (ntiles + 3) & ~(int64_t)3;
+    const size_t hist_b = align256(sizeof(uint32_t) * kMaxDigits * stride), dtot_b = align256(sizeof(uint32_t) * kMaxDigits);
+    const int g = (int)std::min<int64_t>(ntiles, 1024);
+    unsigned long long var = 0, vor = 0, k0 = 0;
+    {
+        unsigned long long *vm = (unsigned long long *)tmp.ensure(
+                               std::max(hist_b + dtot_b, sizeof(unsigned long long) * (2 * g + 3))),
+                           *part = vm + 3;
+        hipLaunchKernelGGL(k_rs_varying<K>, dim3((unsigned)g), dim3(kRBlock), 0, s, ki, n, part, vi);
+        hipLaunchKernelGGL(k_rs_or_parts, dim3(1), dim3(kRBlock), 0, s, part, g, vm);
+        hipLaunchKernelGGL(k_rs_or_parts, dim3(1), dim3(kRBlock), 0, s, part + g, g, vm + 1);
+        unsigned long long h[2];
+        DSS_HIP(hipMemcpyAsync(h, vm, sizeof(h), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipMemcpyAsync(&k0, ki, sizeof(k0), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipStreamSynchronize(s));
+        var = h[0];
+        vor = h[1];
+    }
+    if (bits < 64) var &= (1ull << bits) - 1;
+    const int lo = var ? __builtin_ctzll(var) : 64, hi = var ? 64 - __builtin_clzll(var) : 0;
+    const int vbits = vor ? 64 - __builtin_clzll(vor) : 0;
+    if (var == 0 || vbits > lo) {  // nothing to sort, or no room for the values: the plain sort
+        radix_sort<K, uint32_t, true>(ki, ko, vi, vo, n, nullptr, bits, tmp, s);
+        return;
+    }
+    const K lomask = lo >= 64 ? ~0ull : ((1ull << lo) - 1), kconst = k0 & lomask;
+    const int span = hi - lo, passes = (span + kMaxDigitBits - 1) / kMaxDigitBits, rb = (span + passes - 1) / passes;
+    const size_t ka_b = passes > 1 ? align256(sizeof(K) * n) : 0;
+    unsigned char *t = tmp.ensure(hist_b + dtot_b + ka_b);
+    uint32_t *hist = (uint32_t *)t, *dtot = (uint32_t *)(t + hist_b);
+    K *kalt = (K *)(t + hist_b + dtot_b);
+    const K *src = ki;
+    for (int p = 0; p < passes; p++) {
+        const int shift = lo + p * rb, r = hi - shift < rb ? hi - shift : rb;
+        const bool to_out = ((passes - 1 - p) & 1) == 0;
+        K *dst = to_out ? ko : kalt;
+        hipLaunchKernelGGL(k_rs_hist<K>, dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src, n, nullptr, shift, r, hist,
+                           stride);
+        hipLaunchKernelGGL(k_rs_scan, dim3(1u << r), dim3(kRBlock), 0, s, hist, stride, ntiles, dtot);
+        const bool first = p == 0, last = p == passes - 1;
+        if (first && last)
+            hipLaunchKernelGGL((k_rs_scatter<K, uint32_t, false, 3>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src,
+                               vi, dst, vo, n, nullptr, shift, r, hist, stride, dtot, lomask, kconst);
+        else if (first)
+            hipLaunchKernelGGL((k_rs_scatter<K, uint32_t, false, 1>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src,
+                               vi, dst, vo, n, nullptr, shift, r, hist, stride, dtot, lomask, kconst);
+        else if (last)
+            hipLaunchKernelGGL((k_rs_scatter<K, uint32_t, false, 2>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src,
+                               vi, dst, vo, n, nullptr, shift, r, hist, stride, dtot, lomask, kconst);
+        else
+            hipLaunchKernelGGL((k_rs_scatter<K, uint32_t, false, 0>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src,
+                               vi, dst, vo, n, nullptr, shift, r, hist, stride, dtot, lomask, kconst);
+        DSS_HIP(hipGetLastError());
+        src = dst;
+    }
+}
+
 }  // namespace
+
+void radix_sort_pairs_packed(const uint64_t *ki, uint64_t *ko, const uint32_t *vi, uint32_t *vo, int64_t n, int bits,
+                             DevBuf<unsigned char> &tmp, hipStream_t s)
+{
+    radix_sort_packed(ki, ko, vi, vo, n, bits, tmp, s);
+}
 
 template <typename K, typename V>
 void radix_sort_pairs(const K *ki, K *ko, const V *vi, V *vo, int64_t n, int bits, DevBuf<unsigned char> &tmp,

@@ -119,6 +119,20 @@ constexpr int kJoinLongWpe = DSS_JOIN_LONG_WPE;  // the long variant's register 
 #define DSS_EMIT_DENSITY 4
 #endif
 constexpr int kEmitDensity = DSS_EMIT_DENSITY;
+
+// Counting build of the join (-DDSS_JOIN_PROFILE through tools/variants.sh;
+// never the shipped library): what becomes of every lane test -- which
+// predicate rejects it, how many reach the smallest-shared-cell check, how
+// many are kept -- plus the staging and emission shapes, summed over every
+// k_join launch into g_jprof and read (and cleared) by dssg_join_profile.
+// Slot meanings: kJProfNames in join_profile_read.
+constexpr int kJProf = 20;
+#ifdef DSS_JOIN_PROFILE
+__device__ unsigned long long g_jprof[kJProf];
+#define JPROF(i, v) (jp[i] += (unsigned long long)(v))
+#else
+#define JPROF(i, v) ((void)0)
+#endif
 // ---- level-13 decode + prefix signatures -----------------------------------
 __device__ __forceinline__ int s2pos_to_ij(int o, int pos) { return (int)((0x874B78B4u >> (8 * o + 2 * pos)) & 3u); }
 __device__ __forceinline__ int s2pos_to_orientation(int pos) { return (int)((0xC1u >> (2 * pos)) & 3u); }
@@ -468,6 +482,7 @@ struct EmitUniquePair {
     uint64_t *e_cells;
     uint32_t *pent;
     uint32_t *mult;
+    unsigned long long *big;  // set when a multiplicity exceeds the quad grain's 8 bits per child
     __device__ void operator()(int64_t i, int64_t r) const
     {
         uint32_t m = 1;
@@ -475,6 +490,7 @@ struct EmitUniquePair {
         e_cells[r] = cell[i];
         pent[r] = ent[i];
         mult[r] = m;
+        if (m > 255u) atomicMax(big, (unsigned long long)m);
     }
 };
 
@@ -515,7 +531,9 @@ __global__ void k_gather(int64_t NP, const uint32_t *pos, const uint32_t *pent, 
         const int64_t o = e_offs[e], oe = e_offs[e + 1];
         const uint64_t c = e_cells[i];
         uint32_t mask = child_bit(c, gshift), mm = 0;
-        if (mult) mm = min(mult[i], 255u) << (8u * (uint32_t)__builtin_ctz(mask));
+        // (quads: 8 bits per child -- the build takes the cell grain when a
+        // multiplicity exceeds 255 -- cells: the whole word)
+        if (mult) mm = gshift == kCellShift ? mult[i] : min(mult[i], 255u) << (8u * (uint32_t)__builtin_ctz(mask));
         for (int64_t r = (int64_t)i + 1; r < oe && r < (int64_t)i + 4; r++) {
             const uint64_t cr = e_cells[r];
             if (!same_quad(c, cr, gshift)) break;
@@ -1270,6 +1288,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
     const IndexView &ix = a.ix;
     WaveOut out, tout;  // pairs, tagged keys
     unsigned long long n_tests = 0, n_bcast = 0;
+#ifdef DSS_JOIN_PROFILE
+    unsigned long long jp[kJProf] = {};
+#endif
     // units: kRegions queues (the unit regions), a wave starts on its own
     // region's and moves on when it is drained; grabs of g units per atomic
     int qreg = (int)(blockIdx.x % kRegions), visited = 0;
@@ -1358,6 +1379,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
         s_pe[w][lane] = pent;  // (read after the wave barrier of the emission below)
         const unsigned long long vmask = __ballot(pv);
         if (!vmask) continue;  // (un, the next unit, is already in flight)
+        JPROF(13, lane == 0);
+        JPROF(19, lane == 0 ? __popcll(vmask) : 0);
         // tile time bounds (a regular tile is sorted by m = min(t0, t1)):
         // records whose window misses every posting are skipped (a long
         // tile: no bound)
@@ -1394,7 +1417,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 }
                 const unsigned long long relm = __ballot(rel);
                 const int nrel = uni32(__popcll(relm));
+                JPROF(12, r < x1);
                 if (!nrel) continue;
+                JPROF(10, lane == 0);
+                JPROF(11, lane == 0 ? nrel : 0);
                 const uint32_t slot = mbcnt64(relm);
                 __builtin_amdgcn_wave_barrier();
                 if (rel) {
@@ -1453,6 +1479,29 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                     mhi |= (uint32_t)pass << (j - 32);
                 }
                 const unsigned long long m = pv ? (((unsigned long long)mhi << 32) | mlo) & meets : 0ull;
+#ifdef DSS_JOIN_PROFILE
+                if (pv) {  // the first predicate (in this order) that rejects each test
+                    unsigned long long ct = 0, ca = 0, co = 0;
+                    for (int j = 0; j < nrel; j++) {
+                        const longlong2 rt = s_rt[w][j];
+                        const float4 ra = s_ra[w][j];
+                        const bool tp = (pt.y >= rt.x) & (pt.x <= rt.y);
+                        const bool ap = (pa.y >= ra.x) & (pa.x <= ra.y);
+                        const int32_t own = __float_as_int(ra.w);
+                        const bool op = !OWNER || (own < 0) | (pown == own);
+                        ct += !tp;
+                        ca += tp && !ap;
+                        co += tp && ap && !op;
+                    }
+                    const unsigned long long pta = ((unsigned long long)mhi << 32) | mlo;
+                    JPROF(0, nrel);
+                    JPROF(1, ct);
+                    JPROF(2, ca);
+                    JPROF(3, co);
+                    JPROF(4, __popcll(pta & ~meets));
+                    JPROF(5, __popcll(m));
+                }
+#endif
                 // (2) the quad of the smallest shared cell only (SQL DISTINCT,
                 // Q13): a rank-0 record (the query's first quad) or a posting in
                 // its entity's first quad has no cell below the quad on one
@@ -1462,6 +1511,15 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 // tagged set is deduplicated after the join); else exact merge.
                 unsigned long long keep = pfirst ? m : (m & R0);
                 unsigned long long need = m & ~keep;
+#ifdef DSS_JOIN_PROFILE
+                const unsigned long long need0 = need;
+                JPROF(6, __popcll(keep));
+                JPROF(7, __popcll(need0));
+                {
+                    const uint32_t wi = wave_max((uint32_t)__popcll(need0));
+                    JPROF(14, lane == 0 ? wi : 0u);
+                }
+#endif
                 if (!usig) {  // lazy signatures: the lanes that need them now
                     const bool want = need != 0ull && !lsig;
                     if (__ballot(want)) {
@@ -1489,6 +1547,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                     }
                     if (k) keep |= 1ull << j;
                 }
+#ifdef DSS_JOIN_PROFILE
+                JPROF(8, __popcll(need0 & ~keep));
+                JPROF(9, __popcll(keep));
+#endif
                 // (3) emission, the batch's pairs contiguous per stream (pairs;
                 // long x long keys): lane-major (each lane's pairs after the
                 // lanes before it; iterations = the largest lane count) at low
@@ -1500,12 +1562,20 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 const uint32_t incl = wave_incl_scan(cu | (ct << 16));
                 const uint32_t tot = (uint32_t)uni32(__builtin_amdgcn_readlane((int)incl, 63));
                 const int total_u = (int)(tot & 0xffffu), total_t = LONG ? (int)(tot >> 16) : 0;
+                JPROF(18, lane == 0 && !(total_u | total_t));
                 if (!(total_u | total_t)) continue;
                 WaveOut::Span su{}, st{};
                 if (total_u) su = out.reserve(a.out.ps, total_u);
                 if (LONG && total_t) st = tout.reserve(a.out.ts, total_t);
                 const bool wu = out.have != 0, wt = LONG && tout.have != 0;  // else counted only (rerun)
                 if ((int64_t)(total_u + total_t) * kEmitDensity <= (int64_t)nrel * __popcll(vmask)) {
+#ifdef DSS_JOIN_PROFILE
+                    {
+                        const uint32_t wi = wave_max((uint32_t)__popcll(keep));
+                        JPROF(15, lane == 0);
+                        JPROF(17, lane == 0 ? wi : 0u);
+                    }
+#endif
                     // (one loop per stream: no divergent double bodies)
                     if (!LONG && wu && total_u <= kOutStage) {  // (long variants: direct, no VGPR headroom)
                         // each lane's pairs into the wave's LDS stage as 16-bit
@@ -1563,6 +1633,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                         }
                     }
                 } else {
+                    JPROF(16, lane == 0);
                     const unsigned long long lm = LONG ? __ballot(plong) : 0ull;
                     unsigned long long ou = 0, ot = 0;
                     for (int j = 0; j < nrel; j++) {
@@ -1595,6 +1666,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
         atomicAdd(&a.out.counter[2], n_tests);
         atomicAdd(&a.out.counter[3], n_bcast);
     }
+#ifdef DSS_JOIN_PROFILE
+    for (int i = 0; i < kJProf; i++)
+        if (jp[i]) atomicAdd(&g_jprof[i], jp[i]);
+#endif
 }
 
 // Closing the output holes: chunk c holds fills[c] pairs at c * kOutChunk
@@ -2086,7 +2161,7 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     DevBuf<unsigned long long> stat_b;
     unsigned long long *stat = stat_b.ensure(80);  // [0..64] hist, 65..66 m range, 67 dcap, 68..69 dense range,
                                                    // 70 n_irr, 71 nlongfp, 72..73 runs/long, 74 max cell,
-                                                   // 75..76 grain counts
+                                                   // 75..76 grain counts, 77 largest multiplicity > 255
     DSS_HIP(hipMemsetAsync(stat, 0, 80 * sizeof(unsigned long long), s));
     {
         const unsigned long long init[2] = {~0ull, 0ull};
@@ -2114,11 +2189,12 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
         DevBuf<uint32_t> va, vb;
         uint64_t *k0 = ka.ensure(P + 1), *k1 = kb.ensure(P + 1);
         uint32_t *v0 = va.ensure(P + 1), *v1 = vb.ensure(P + 1);
-        radix_sort_pairs(cells, k1, (const uint32_t *)pent, v1, P, 64, tmp_, s);
+        radix_sort_pairs_packed(cells, (uint64_t *)k1, (const uint32_t *)pent, v1, P, 64, tmp_, s);
         radix_sort_pairs(v1, v0, k1, k0, P, bits_for(n), tmp_, s);  // (entity, cell)
         uint32_t *m = mult_b.ensure(P + 1);
         int64_t *dtot = (int64_t *)(stat + 78);
-        compact_if(P, PredUniquePair{v0, k0}, EmitUniquePair{P, v0, k0, e_cells, pent, m}, tmp_, tmp2_, s, dtot, &Pu);
+        compact_if(P, PredUniquePair{v0, k0}, EmitUniquePair{P, v0, k0, e_cells, pent, m, stat + 77}, tmp_, tmp2_, s,
+                   dtot, &Pu);
         hipLaunchKernelGGL(k_offs_from_sorted, dim3(grid_for(Pu, kBlock)), dim3(kBlock), 0, s, Pu, pent, n, e_offs);
         if (Pu == 0) DSS_HIP(hipMemsetAsync(e_offs, 0, sizeof(int64_t) * (n + 1), s));
         mult = m;
@@ -2175,6 +2251,10 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
         DSS_HIP(hipStreamSynchronize(s));
         gshift = 2 * g[0] >= 3 * g[1] ? kQuadShift : kCellShift;
     }
+    // a (cell, entity) repeated more than 255 times in a stored array (RID
+    // unnest(cells) multiplicities, MaxSubscriptionCount) does not fit the
+    // quad grain's 8 bits per child: the cell grain keeps the full 32 bits
+    if (general && h[77] != 0) gshift = kCellShift;
     idx->gshift = gshift;
     // (4) slots: dense range and the irregular side table
     const BuildCtx bc{e_cells, pent, t0, t1, cell_lo, cell_hi, gshift};
@@ -2662,6 +2742,32 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
         return;
     }
     throw Error(DSSG_ERR_DEVICE, "search: output size did not converge");
+}
+
+static const char *const kJProfNames[kJProf] = {
+    "lane_tests", "time_fail", "altitude_fail", "owner_fail", "quad_mask_fail", "pass",
+    "kept_first_group", "distinct_checks", "distinct_drops", "kept", "staged_batches", "staged_records",
+    "loaded_records", "units_with_work", "distinct_wave_iters", "emit_lane_major_batches",
+    "emit_record_major_batches", "emit_lane_major_wave_iters", "batches_without_pairs", "posting_lanes"};
+
+const char *join_profile_name(int i) { return i >= 0 && i < kJProf ? kJProfNames[i] : nullptr; }
+
+int join_profile_read(int64_t *out, int n)
+{
+#ifdef DSS_JOIN_PROFILE
+    unsigned long long h[kJProf] = {};
+    DSS_HIP(hipDeviceSynchronize());
+    DSS_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_jprof), sizeof(h), 0, hipMemcpyDeviceToHost));
+    const unsigned long long z[kJProf] = {};
+    DSS_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_jprof), z, sizeof(z), 0, hipMemcpyHostToDevice));
+    const int k = n < kJProf ? n : kJProf;
+    for (int i = 0; i < k; i++) out[i] = (int64_t)h[i];
+    return k;
+#else
+    (void)out;
+    (void)n;
+    return 0;
+#endif
 }
 
 }  // namespace dss

@@ -116,6 +116,22 @@ class SearchEngine {
         *lq = long_queries_;
         *lp = long_postings_;
     }
+    // Hands the engine-owned buffers holding `res` (the most recent result)
+    // to the caller in exchange for (q, e), which later searches reuse: the
+    // result then outlives the next search (the async sharded step's
+    // alternating buffer sets).  false if `res` is not in the engine's buffers.
+    bool adopt_output(const dssg_pairs &res, DevBuf<uint32_t> &q, DevBuf<uint32_t> &e)
+    {
+        auto give = [&](DevBuf<uint32_t> &a, DevBuf<uint32_t> &b) {
+            if (res.q != a.p || res.e != b.p) return false;
+            std::swap(a.p, q.p);
+            std::swap(a.cap, q.cap);
+            std::swap(b.p, e.p);
+            std::swap(b.cap, e.cap);
+            return true;
+        };
+        return give(oq_, oe_) || give(oq2_, oe2_);
+    }
     void last_join_events(int64_t *flushes, int64_t *merges, int64_t *merge_lanes) const
     {
         *flushes = flushes_;
@@ -180,5 +196,12 @@ class SearchEngine {
     hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
     void timing_events();
 };
+
+// The counting build's per-lane-test outcome sums over every k_join launch
+// since the last read (DSS_JOIN_PROFILE, search.hip); cleared by the read.
+// Returns the number of counters written (0 in the shipped library); their
+// names through join_profile_name(i).
+int join_profile_read(int64_t *out, int n);
+const char *join_profile_name(int i);
 
 }  // namespace dss

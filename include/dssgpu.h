@@ -471,6 +471,15 @@ int dssg_join_events(dssg_ctx *ctx, int64_t *flushes, int64_t *merges, int64_t *
  * when both are non-zero can a long x long pair exist, and only then does
  * the join run its tagging variant.  Any pointer may be NULL. */
 int dssg_join_longs(dssg_ctx *ctx, int64_t *long_queries, int64_t *long_postings);
+/* Per-predicate outcome counts of the join's lane tests (which predicate --
+ * time, altitude, owner, quad mask -- rejects each test, how many reach the
+ * smallest-shared-cell check and how many it drops, staging and emission
+ * shapes), summed over every join launch since the last call and cleared by
+ * it.  Only a counting build of the library (-DDSS_JOIN_PROFILE) counts:
+ * the shipped library sets *written = 0.  Names by dssg_join_profile_name
+ * (NULL past the last counter). */
+int dssg_join_profile(dssg_ctx *ctx, int64_t *out, int n, int *written);
+const char *dssg_join_profile_name(int i);
 /* Roofline accounting for a device query batch: total postings the join
  * scans (sum of M_q) and distinct candidate entities before the
  * altitude/time filter (sum of D_q), SURVEY.md s8(d). */

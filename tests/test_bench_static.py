@@ -66,3 +66,36 @@ def test_every_line_carries_baseline_parity_and_traffic():
         roof = {k.value: v for k, v in zip(res["roofline"].keys, res["roofline"].values)}
         assert "traffic" in roof and not (isinstance(roof["traffic"], ast.Constant) and roof["traffic"].value is None)
     assert "exchanged" in _result_dict("sharded_report")
+
+
+def test_sharded_leg_attached_to_the_replica_line():
+    """N > 1 replica runs time the cell-range shards in the same ranks
+    (VERDICT r5 item 2): main() hands the replica index to sharded_leg and
+    puts its record under result["sharded"]; the record carries the rate,
+    the phases and oracle parity on every rank."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert 'result["sharded"] = rec' in src
+    tree = ast.parse(src)
+    fn = next(n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "sharded_leg")
+    text = ast.get_source_segment(src, fn)
+    for key in ('"value"', '"ms_per_step"', '"oracle_all_ranks_equal"', '"all_ranks_equal"',
+                '"phase_ms_max_over_ranks"', 'rec["error"]'):
+        assert key in text, key
+
+
+def test_sharded_leg_watchdog_keeps_the_replica_line(tmp_path):
+    """A sharded-leg stage past its limit (a hung collective) ends the rank
+    with status 0 and rank 0 prints the finished replica line, with
+    sharded.error set -- the replica measurement is never lost."""
+    import json
+    import subprocess
+    import sys
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; bench.LEG_LIMIT_S = 0.3; "
+            "bench._PENDING[0] = {'metric': 'm', 'value': 1.0}; bench._PENDING[1] = 0; "
+            "bench.heartbeat(every=0.1); bench.stage('sharded leg: timed steps'); time.sleep(30)") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["value"] == 1.0 and "exceeded" in d["sharded"]["error"]

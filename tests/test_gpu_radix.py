@@ -77,6 +77,33 @@ def test_radix_sort_level13_cells():
     assert np.array_equal(ko, rk) and np.array_equal(vo, rv)
 
 
+PACKED = [  # (name, n, bits, key high bits, key low constant, key shift, value max): 8-B keys with values
+    ("level-13 ids, packed", 300_000, 64, 29, (1 << 34), 35, 2**32 - 1),
+    ("one pass, packed", 100_000, 64, 6, 0x123, 40, 2**32 - 1),
+    ("bits < 64, unsorted high bits kept", 200_000, 50, 10, 0x28, 38, 2**30),
+    ("values too wide: plain sort", 150_000, 64, 30, 0x7, 20, 2**31),
+    ("values fit the low bits", 150_000, 64, 30, 0x0, 20, 2**16),
+]
+
+
+@pytest.mark.parametrize("name,n,bits,hb,low,sh,vmax", PACKED)
+def test_radix_sort_packed_words(name, n, bits, hb, low, sh, vmax):
+    """The packed 8-B path (key bits below the lowest varying one constant and
+    wide enough for every value) and its fallback both equal the stable sort:
+    keys restored with their constant low bits and any unsorted high bits,
+    values carried."""
+    rng = np.random.default_rng(n + hb)
+    k = (rng.integers(0, 1 << hb, n, dtype=np.uint64) << np.uint64(sh)) | np.uint64(low)
+    k[: n // 4] = k[: n // 4] % np.uint64(1 << (sh + 3)) | np.uint64(low)  # duplicates
+    if bits < 64:  # random bits above the sorted ones ride along unsorted
+        k |= rng.integers(0, 1 << (64 - bits), n, dtype=np.uint64) << np.uint64(bits)
+    vals = rng.integers(0, vmax, n, dtype=np.uint64, endpoint=True).astype(np.uint32)
+    ko, vo, _ = gpu_sort(k, vals, bits, 8)
+    rk, rv = ref_sort(k, vals, bits)
+    assert np.array_equal(ko, rk), name
+    assert np.array_equal(vo, rv), name
+
+
 def test_radix_sort_rejects_aliasing():
     from dss_amd import _lib
     ctx = _lib.context()

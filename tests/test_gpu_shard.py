@@ -235,16 +235,24 @@ def test_native_rccl_one_rank_equals_full_search():
 
 def test_native_async_exchange_stream_one_rank():
     """dssg_sharded_search_async_device: the pairs' trip home on a second
-    communicator and stream.  On one rank with the general routing forced:
+    communicator and stream.  On one rank, identity and general routing:
     every step equals the whole-index search once the exchange stream has
-    run, a step's output stays valid through the next step (two buffer
-    sets), and the stats report the routed rows and no bytes to other ranks."""
+    run, and a step's output stays valid through the next step (two buffer
+    sets) -- the steps alternate between the batch and its first half, so a
+    reread of an overwritten buffer would show the other batch's pairs
+    (the identity path returned the engine's own buffers); the
+    stats report the routed rows and no bytes to other ranks."""
     import torch
     from dss_amd import _lib, device as D, shard
     from dss_amd.store import EntityIndex
     ci, cq, qa, ia, tlo, thi = _covered(0.05)
     full = EntityIndex(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1)
-    want = _keys(*full.search_batch(cq.offs, cq.cells, qa.alt_lo, qa.alt_hi, tlo, thi))
+    nq = len(cq.offs) - 1
+    half = nq // 2
+    wants = [_keys(*full.search_batch(cq.offs, cq.cells, qa.alt_lo, qa.alt_hi, tlo, thi)),
+             _keys(*full.search_batch(cq.offs[:half + 1], cq.cells[:int(cq.offs[half])], qa.alt_lo[:half],
+                                      qa.alt_hi[:half], tlo[:half], thi[:half]))]
+    assert len(wants[1]) < len(wants[0])
     ctx = _lib.context()
     comms = [shard.NativeComm(ctx, 1, 0, shard.NativeComm.unique_id(ctx)) for _ in range(2)]
     ranges = shard.cell_splitters(ci.cells, 1)
@@ -260,21 +268,22 @@ def test_native_async_exchange_stream_one_rank():
         for identity in (1, 0):
             ctx.set_tuning("route_identity", identity)
             prev = None
-            for k in range(3):
-                p = ns.step(offs.data_ptr(), cells.data_ptr(), len(cq.offs) - 1, *qargs)
+            for k in range(4):
+                which = k % 2
+                p = ns.step(offs.data_ptr(), cells.data_ptr(), half if which else nq, *qargs)
                 torch.cuda.synchronize()
                 got = _keys(D.copy_back(ctx, p.q, int(p.n), np.uint32), D.copy_back(ctx, p.e, int(p.n), np.uint32))
-                assert np.array_equal(got, want), (identity, k)
-                if prev is not None:  # the previous step's output, read after this step
-                    pq_, pn_ = prev
+                assert np.array_equal(got, wants[which]), (identity, k)
+                if prev is not None:  # the previous step's output (the other batch), read after this step
+                    pq_, pn_, pw = prev
                     again = _keys(D.copy_back(ctx, pq_.q, pn_, np.uint32), D.copy_back(ctx, pq_.e, pn_, np.uint32))
-                    assert np.array_equal(again, want), (identity, k)
-                prev = (p, int(p.n))
+                    assert np.array_equal(again, wants[pw]), (identity, k)
+                prev = (p, int(p.n), which)
             ms, cnt = ns.stats()
             if identity == 0:
                 assert cnt["rows"] > 0
                 assert cnt["query_bytes_sent"] == 0 and cnt["pair_bytes_sent"] == 0
-                assert cnt["shard_pairs"] == len(want)
+                assert cnt["shard_pairs"] == len(wants[1])  # (the last step: the half batch)
         # timing on: phases measured, touched postings counted
         ctx.set_tuning("route_identity", 0)
         ctx.L.dssg_set_timing(ctx.h, 1)

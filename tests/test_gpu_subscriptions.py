@@ -37,6 +37,28 @@ def test_max_count_counts_repeats_in_stored_arrays():
     assert MaxSubscriptionCountInCellsByOwner(idx, [OVERFLOW_CELL, POOL_CELL, POOL_CELL], 3, NOW) == 2
 
 
+def test_max_count_multiplicity_above_255():
+    """A cell repeated more than 255 times in one stored array (ADVICE r5:
+    the quad grain holds 8 bits per child): the build keeps the full count
+    (it takes the cell grain), whether the grain is picked or forced to quads."""
+    from dss_amd import _lib
+    from dss_amd.store import EntityIndex, MaxSubscriptionCountInCellsByOwner
+    sib = [(POOL_CELL & ~(3 << 35)) | (k << 35) for k in range(4)]  # the 4 level-13 cells of POOL_CELL's quad
+    cells = [sib[0]] * 300 + sib[1:] + [sib[2]] * 2
+    ctx = _lib.context()
+    try:
+        for grain in (0, 2):
+            ctx.set_tuning("index_grain", grain)
+            idx = EntityIndex.from_lists([cells, [sib[0]], sib], t1=[NOW + DAY] * 3, owner=[3, 3, 4])
+            assert ctx.L.dssg_index_grain(idx.h) == 13, grain
+            assert MaxSubscriptionCountInCellsByOwner(idx, [sib[0]], 3, NOW) == 301
+            assert MaxSubscriptionCountInCellsByOwner(idx, [sib[2], sib[3]], 3, NOW) == 3
+            assert MaxSubscriptionCountInCellsByOwner(idx, [sib[1]], 4, NOW) == 1
+            idx.free()
+    finally:
+        ctx.set_tuning("index_grain", 0)
+
+
 def test_notification_fanout_kat():
     # isa_test.go:266-324: 42 -> 43 on ISA insert -> 44 on ISA delete
     from dss_amd.store import UpdateNotificationIdxsInCells

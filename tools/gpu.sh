@@ -41,7 +41,8 @@ for step in "$@"; do
     echo "== $step"
     case $kind in
     tests)
-        timeout -k 10 ${TESTS_TIMEOUT:-600} python -u -m pytest ${rest:-tests} -m gpu -x -v --timeout 120 \
+        rest=${rest:-tests}
+        timeout -k 10 ${TESTS_TIMEOUT:-600} python -u -m pytest ${rest//,/ } -m gpu -x -v --timeout 120 \
             --timeout-method thread > "$O/$name.log" 2>&1 || { echo TESTS_FAILED; tail -40 "$O/$name.log"; exit 1; }
         tail -1 "$O/$name.log" ;;
     bench|quick)
