@@ -50,6 +50,7 @@ struct IndexView {
     const uint64_t *s_post;
     const uint32_t *s_nreg;
     const uint8_t *s_lfp;
+    const uint32_t *s_band;  // nullptr: one run per slot; else 8 band starts per slot (dssg_index.s_band)
     const uint32_t *b_e;
     const uint8_t *b_meta;
     const float2 *b_alt;
@@ -76,6 +77,7 @@ IndexView view_of(const dssg_index *idx)
     v.s_post = idx->s_post.p;
     v.s_nreg = idx->s_nreg.p;
     v.s_lfp = idx->s_lfp.p;
+    v.s_band = idx->n_bands > 1 ? idx->s_band.p : nullptr;
     v.b_e = idx->b_e.p;
     v.b_meta = idx->b_meta.p;
     v.b_alt = idx->b_alt.p;

@@ -501,16 +501,48 @@ __device__ __forceinline__ uint32_t slot_of(const IndexView &a, uint64_t c)
     return s;
 }
 
-// Second sort key of every posting (already sorted by m): slot << 1 | long.
+// Postings per slot (the altitude bands split the dense slots only).
+__global__ void k_slot_hist(int64_t NP, IndexView a, const uint32_t *pos, const uint64_t *cells, uint32_t *scnt)
+{
+    const int64_t j = tid64();
+    if (j >= NP) return;
+    atomicAdd(&scnt[slot_of(a, cells[pos[j]])], 1u);
+}
+
+// Slots with at least `dense` postings (do any bands apply?).
+__global__ void k_dense_slots(int64_t ns, const uint32_t *scnt, uint32_t dense, unsigned long long *cnt)
+{
+    const int64_t s = tid64();
+    wave_count(s < ns && scnt[s] >= dense, cnt);
+}
+
+struct BandThr {
+    float v[7];  // alt_lo quantile edges: band = #{v[b] <= alt_lo}
+};
+
+// Second sort key of every posting (already sorted by m): slot << 1 | long
+// (kshift 1), or with altitude bands slot << 4 | long << 3 | band (kshift 4;
+// band 0 unless the slot is dense and the posting regular).
 __global__ void k_slot_keys(int64_t NP, IndexView a, const uint32_t *pos, const uint64_t *cells, const uint32_t *pent,
-                            const int64_t *t0, const int64_t *t1, unsigned long long thr, uint32_t *key)
+                            const int64_t *t0, const int64_t *t1, unsigned long long thr, int kshift,
+                            const uint32_t *scnt, uint32_t dense, const float *alo, BandThr bt, int nb, uint32_t *key)
 {
     const int64_t j = tid64();
     if (j >= NP) return;
     const uint32_t i = pos[j];
     const uint32_t e = pent[i];
     const bool lng = duration(t0[e], t1[e]) > thr;
-    key[j] = slot_of(a, cells[i]) << 1 | (lng ? 1u : 0u);
+    const uint32_t sl = slot_of(a, cells[i]);
+    if (kshift == 1) {
+        key[j] = sl << 1 | (lng ? 1u : 0u);
+        return;
+    }
+    uint32_t band = 0;
+    if (!lng && scnt[sl] >= dense) {
+        const float x = alo[e];  // (NaN: band 0)
+        for (int b = 0; b < nb - 1; b++) band += x >= bt.v[b] ? 1u : 0u;
+    }
+    key[j] = sl << 4 | (lng ? 8u : 0u) | band;
 }
 
 // Posting attributes in final order: the quad's cell mask (the entity's run
@@ -558,20 +590,22 @@ __global__ void k_gather(int64_t NP, const uint32_t *pos, const uint32_t *pent, 
 }
 
 // Slot boundaries of the sorted postings: first / end / end of the regular
-// part (positions + 1; 0 = unset), the distinct-cell count, long postings.
-__global__ void k_slot_bounds(int64_t NP, const uint32_t *key, uint32_t *sfirst, uint32_t *send, uint32_t *sreg,
-                              unsigned long long *stat)
+// part (positions + 1; 0 = unset), band starts (bfirst, with bands), the
+// distinct-cell count, long postings.
+__global__ void k_slot_bounds(int64_t NP, const uint32_t *key, int kshift, uint32_t *sfirst, uint32_t *send,
+                              uint32_t *sreg, uint32_t *bfirst, unsigned long long *stat)
 {
     const int64_t j = tid64();
     bool run = false, lng = false;
     if (j < NP) {
-        const uint32_t k = key[j], s = k >> 1;
-        const bool first = j == 0 || (key[j - 1] >> 1) != s;
-        const bool last = j == NP - 1 || (key[j + 1] >> 1) != s;
-        lng = (k & 1u) != 0;
+        const uint32_t k = key[j], s = k >> kshift, lb = (uint32_t)kshift - 1u;
+        const bool first = j == 0 || (key[j - 1] >> kshift) != s;
+        const bool last = j == NP - 1 || (key[j + 1] >> kshift) != s;
+        lng = ((k >> lb) & 1u) != 0;
         if (first) sfirst[s] = (uint32_t)j + 1u;
         if (last) send[s] = (uint32_t)j + 1u;
-        if (!lng && (last || (key[j + 1] & 1u))) sreg[s] = (uint32_t)j + 1u;
+        if (!lng && (last || ((key[j + 1] >> lb) & 1u))) sreg[s] = (uint32_t)j + 1u;
+        if (bfirst && !lng && (first || key[j - 1] != k)) bfirst[(int64_t)s * 8 + (k & 7u)] = (uint32_t)j + 1u;
         run = first;
     }
     wave_count(run, &stat[0]);
@@ -579,7 +613,8 @@ __global__ void k_slot_bounds(int64_t NP, const uint32_t *key, uint32_t *sfirst,
 }
 
 __global__ void k_slot_counts(int64_t ns, const uint32_t *sfirst, const uint32_t *send, const uint32_t *sreg,
-                              int64_t *cnt, uint32_t *nreg, unsigned long long *maxc)
+                              const uint32_t *bfirst, int64_t *cnt, uint32_t *nreg, uint32_t *sband,
+                              unsigned long long *maxc)
 {
     const int64_t s = tid64();
     unsigned long long c = 0;
@@ -587,7 +622,19 @@ __global__ void k_slot_counts(int64_t ns, const uint32_t *sfirst, const uint32_t
         const uint32_t f = sfirst[s];
         c = f ? send[s] - f + 1 : 0;
         cnt[s] = (int64_t)c;
-        nreg[s] = (f && sreg[s]) ? sreg[s] - f + 1 : 0;
+        const uint32_t nr = (f && sreg[s]) ? sreg[s] - f + 1 : 0;
+        nreg[s] = nr;
+        if (sband) {  // band starts relative to the slot; an empty band starts where the next one does
+            uint32_t next = nr, rel[8];
+            for (int b = 7; b >= 0; b--) {
+                const uint32_t bf = bfirst[s * 8 + b];
+                if (f && bf) next = bf - f;
+                rel[b] = next;
+            }
+            uint4 *o = reinterpret_cast<uint4 *>(sband + s * 8);
+            o[0] = make_uint4(rel[0], rel[1], rel[2], rel[3]);
+            o[1] = make_uint4(rel[4], rel[5], rel[6], rel[7]);
+        }
     }
     for (int o = 32; o > 0; o >>= 1) c = max(c, __shfl_xor(c, o));
     if ((threadIdx.x & 63) == 0 && c) atomicMax(maxc, c);
@@ -595,10 +642,17 @@ __global__ void k_slot_counts(int64_t ns, const uint32_t *sfirst, const uint32_t
 
 // Slots holding a long-footprint posting: their join units take the long
 // join variant (the others' postings all have compact prefixes).
-__global__ void k_slot_lfp(int64_t NP, const uint32_t *key, const uint8_t *b_meta, uint8_t *s_lfp)
+__global__ void k_slot_lfp(int64_t NP, const uint32_t *key, int kshift, const uint8_t *b_meta, uint8_t *s_lfp)
 {
     const int64_t j = tid64();
-    if (j < NP && (b_meta[j] & kMetaLongFp)) s_lfp[key[j] >> 1] = 1;
+    if (j < NP && (b_meta[j] & kMetaLongFp)) s_lfp[key[j] >> kshift] = 1;
+}
+
+// Every k-th alt_lo (the band quantiles are taken on the host from these).
+__global__ void k_sample_f32(int64_t n, const float *x, int64_t ns, float *out)
+{
+    const int64_t k = tid64();
+    if (k < ns) out[k] = x[(int64_t)((double)k * (double)n / (double)ns)];
 }
 
 __global__ void k_owner_keys(int64_t n, const int32_t *owner, uint32_t *key, uint32_t *val)
@@ -888,6 +942,20 @@ __global__ __launch_bounds__(kBlock) void k_qrecs(QueryView qv, int64_t nqc, con
     for (int u = 0; u < 4; u++) dst[u] = src[u];
 }
 
+// The records in key (slot) order: rec2[i] = recs[low word of sval[i]],
+// four threads per 64-B record (16 B each, coalesced writes), over the
+// device key count.  A join unit's records are then one contiguous run that
+// every tile of the slot re-reads from L2, instead of 64-B gathers across the
+// query-ordered array (round 6: those gathers were most of k_join's HBM reads).
+__global__ void k_rec_permute(const int64_t *dnkeys, const uint64_t *sval, const QRec *recs, QRec *rec2)
+{
+    const int64_t t = tid64(), i = t >> 2;
+    if (i >= *dnkeys) return;
+    const int part = (int)(t & 3);
+    const int4 *src = reinterpret_cast<const int4 *>(recs + (uint32_t)sval[i]);
+    reinterpret_cast<int4 *>(rec2 + i)[part] = src[part];
+}
+
 // Lower / upper bound over a slot's regular postings (sorted by m).
 __device__ __forceinline__ uint64_t lb_m(const longlong2 *bt, uint64_t lo, uint64_t hi, long long x)
 {
@@ -936,6 +1004,19 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x)
     return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
+// Wave max / min of a float (no NaN) through an order-preserving u32 image.
+__device__ __forceinline__ uint32_t f32_key(float x)
+{
+    const uint32_t u = __float_as_uint(x);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float f32_of_key(uint32_t k)
+{
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+__device__ __forceinline__ float wave_max_f(float x) { return f32_of_key(wave_max(f32_key(x))); }
+__device__ __forceinline__ float wave_min_f(float x) { return f32_of_key(~wave_max(~f32_key(x))); }
+
 // An upper bound (within 2^24 us) of the wave maximum of a 64-bit time, by a
 // 32-bit DPP max of the times' top bits: the tile hull only needs to contain
 // every posting's window (a looser hull stages a few more records; the
@@ -965,9 +1046,11 @@ __device__ __forceinline__ uint32_t lb_u32(const uint32_t *x, uint32_t lo, uint3
 // tile (unit_ranges) -- and wide ones [w0, w1); a long tile meets every
 // record of the cell.  32 bytes.
 constexpr uint32_t kUnitLong = 0x80000000u;  // np: long-duration tile
+constexpr uint32_t kUnitBand = 0x40000000u;  // np: a tile of one altitude band (k_join stages by its altitude hull)
+constexpr uint32_t kUnitFlags = kUnitLong | kUnitBand;
 struct alignas(16) Unit {
     uint64_t p0;     // first posting
-    uint32_t np;     // postings (1..64) | kUnitLong
+    uint32_t np;     // postings (1..64) | kUnitLong | kUnitBand
     uint32_t slot;
     uint32_t n0, n1;  // narrow records
     uint32_t w0, w1;  // wide records
@@ -987,6 +1070,23 @@ __device__ __forceinline__ uint32_t lb_q(const uint64_t *sv, uint32_t lo, uint32
         else hi = m;
     }
     return lo;
+}
+
+// A banded slot's band starts relative to its first posting, rel[8] = the
+// end of its regular part.
+__device__ __forceinline__ void band_starts(const IndexView &a, uint32_t slot, uint32_t nreg, uint32_t rel[9])
+{
+    const uint4 *p = reinterpret_cast<const uint4 *>(a.s_band + (uint64_t)slot * 8);
+    const uint4 x = p[0], y = p[1];
+    rel[0] = x.x;
+    rel[1] = x.y;
+    rel[2] = x.z;
+    rel[3] = x.w;
+    rel[4] = y.x;
+    rel[5] = y.y;
+    rel[6] = y.z;
+    rel[7] = y.w;
+    rel[8] = nreg;
 }
 
 __device__ __forceinline__ void unit_ranges(const IndexView &a, Unit &d, const uint64_t *sq, long long dq, long long tbase,
@@ -1057,8 +1157,19 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
             s0 = a.s_post[slot];
             s1 = a.s_post[slot + 1];
             sr = s0 + a.s_nreg[slot];
-            ntr = (uint32_t)((sr - s0 + tp - 1) / tp);
-            nu = ntr + (uint32_t)((s1 - sr + tp - 1) / tp);
+            if (a.s_band) {  // regular tiles per altitude band
+                uint32_t rel[9];
+                band_starts(a, slot, (uint32_t)(sr - s0), rel);
+                int ne = 0;
+                for (int b = 0; b < 8; b++) {
+                    ntr += (rel[b + 1] - rel[b] + tp - 1) / tp;
+                    ne += rel[b + 1] > rel[b] ? 1 : 0;
+                }
+                if (ne > 1) ntr |= kUnitBand;  // (a flag bit above any tile count)
+            } else {
+                ntr = (uint32_t)((sr - s0 + tp - 1) / tp);
+            }
+            nu = (ntr & ~kUnitBand) + (uint32_t)((s1 - sr + tp - 1) / tp);
             lfp = a.s_lfp[slot] != 0;
         }
         const uint32_t ns_ = lfp ? 0u : nu, nl_ = lfp ? nu : 0u;
@@ -1083,7 +1194,7 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
         s_sr[wv][lane] = sr;
         s_s1[wv][lane] = s1;
         s_bu[wv][lane] = lfp ? bl : bs;
-        s_par[wv][lane] = make_uint4(ntr | (lfp ? 0x80000000u : 0u), slot, rw, re);
+        s_par[wv][lane] = make_uint4(ntr | (lfp ? kUnitLong : 0u), slot, rw, re);
         __builtin_amdgcn_wave_barrier();
         for (uint32_t u = (uint32_t)lane; u < tot; u += 64) {
             int lo = 0, hi = 63;  // the first lane L with s_xa[L] > u
@@ -1094,13 +1205,27 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
             }
             const uint32_t t = u - (lo ? s_xa[wv][lo - 1] : 0u);  // the unit's tile within its cell
             const uint4 pr = s_par[wv][lo];
-            const uint32_t lntr = pr.x & 0x7fffffffu;
-            const bool llfp = (pr.x >> 31) != 0;
+            const uint32_t lntr = pr.x & ~kUnitFlags;
+            const bool llfp = (pr.x & kUnitLong) != 0, lband = (pr.x & kUnitBand) != 0;
             const uint64_t l0 = s_s0[wv][lo], lr = s_sr[wv][lo], l1 = s_s1[wv][lo];
             Unit d;
             const bool lng = t >= lntr;
-            const uint64_t b = lng ? lr + (uint64_t)tp * (t - lntr) : l0 + (uint64_t)tp * t;
-            const uint64_t e = lng ? l1 : lr;
+            uint64_t b = lng ? lr + (uint64_t)tp * (t - lntr) : l0 + (uint64_t)tp * t;
+            uint64_t e = lng ? l1 : lr;
+            if (!lng && a.s_band) {  // the tile's band: bands in order, each tiled from its start
+                uint32_t rel[9];
+                band_starts(a, pr.y, (uint32_t)(lr - l0), rel);
+                uint32_t acc = 0;
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t nt = (rel[k + 1] - rel[k] + tp - 1) / tp;
+                    if (t < acc + nt) {
+                        b = l0 + rel[k] + (uint64_t)tp * (t - acc);
+                        e = l0 + rel[k + 1];
+                        break;
+                    }
+                    acc += nt;
+                }
+            }
             d.p0 = b;
             d.np = (uint32_t)min((uint64_t)tp, e - b) | (lng ? kUnitLong : 0u);
             d.slot = pr.y;
@@ -1109,6 +1234,7 @@ __global__ __launch_bounds__(kBlock) void k_units(IndexView a, const uint32_t *s
             d.w0 = lng ? pr.w : pr.z;
             d.w1 = pr.w;
             unit_ranges(a, d, sq, dq, tbase, qshift);  // a regular tile's record sub-ranges
+            if (lband && !lng) d.np |= kUnitBand;
             const unsigned long long wpos = s_bu[wv][lo] + t;
             const Regions &dr = llfp ? url : ur;
             Unit *du = llfp ? units_l : units;
@@ -1339,7 +1465,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
         ns01 = ns23 = make_ulonglong2(0, 0);
         const uint32_t nrec = (dn.n1 > dn.n0 ? dn.n1 - dn.n0 : 0u) + (dn.w1 > dn.w0 ? dn.w1 - dn.w0 : 0u);
         nsig = nrec > a.lazy_sig_recs;
-        if (nrec && (uint32_t)lane < (dn.np & ~kUnitLong)) {  // a tile no record can meet is skipped unloaded
+        if (nrec && (uint32_t)lane < (dn.np & ~kUnitFlags)) {  // a tile no record can meet is skipped unloaded
             const uint64_t p = dn.p0 + lane;
             ne = ix.b_e[p];
             nmeta = ix.b_meta[p];
@@ -1362,7 +1488,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
         d.n1 = (uint32_t)uni32((int)d.n1);
         d.w0 = (uint32_t)uni32((int)d.w0);
         d.w1 = (uint32_t)uni32((int)d.w1);
-        const uint32_t np = d.np & ~kUnitLong;
+        const uint32_t np = d.np & ~kUnitFlags;
         // ---- this lane's posting
         const longlong2 pt = nt;
         const float2 pa = na;
@@ -1390,6 +1516,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
             t0min = readlane64(m, 0);  // <= every t0 of the tile
             t1max = wave_max_bound((uint32_t)lane < np ? (pt.x > pt.y ? pt.x : pt.y) : LLONG_MIN);
         }
+        // a banded tile's altitude hull (its postings' [min alt_lo, max
+        // alt_hi]; NaN altitudes meet nothing and are left out): records
+        // outside it are not staged
+        float hlo = -INFINITY, hhi = INFINITY;
+        if (d.np & kUnitBand) {
+            hlo = wave_min_f(pv && pa.x == pa.x ? pa.x : INFINITY);
+            hhi = wave_max_f(pv && pa.y == pa.y ? pa.y : -INFINITY);
+        }
         const uint32_t ra0 = d.n0, ra1 = d.n1, rb0 = d.w0, rb1 = d.w1;
         const bool pfirst = (pe & kFirstBit) != 0;                  // entity's smallest cell
         const bool pcompact = (pmeta & kMetaCompact) != 0;          // compact prefix
@@ -1398,18 +1532,22 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
             const uint32_t x0 = part ? rb0 : ra0, x1 = part ? rb1 : ra1;
             for (uint32_t base = x0; base < x1; base += 64) {
                 // stage the batch's records whose window meets the tile's time
-                // hull, compacted to slots [0, nrel)
+                // hull (and a banded tile's altitude hull), compacted to slots
+                // [0, nrel).  (Round 6: batches filled to 64 staged records
+                // across loaded groups -- 35 % fewer batches on configs[2] --
+                // made k_join slower, 2.22 -> 2.31 ms: each batch boundary
+                // re-read a group through the dependent sval -> record loads.)
                 const uint32_t r = base + (uint32_t)lane;
                 bool rel = false;
                 int4 h0 = make_int4(0, 0, 0, 0), h1 = h0;
                 ulonglong2 g0 = make_ulonglong2(0, 0), g1 = g0;
                 if (r < x1) {
-                    const int4 *r4 = reinterpret_cast<const int4 *>(recs + (uint32_t)sval[r]);
+                    const int4 *r4 = reinterpret_cast<const int4 *>(recs + r);  // (key order: k_rec_permute)
                     h0 = r4[0];
                     h1 = r4[1];
                     const long long tlo = ((long long)h0.y << 32) | (uint32_t)h0.x;
                     const long long thi = ((long long)h0.w << 32) | (uint32_t)h0.z;
-                    rel = t1max >= tlo && t0min <= thi;
+                    rel = t1max >= tlo && t0min <= thi && __int_as_float(h1.y) >= hlo && __int_as_float(h1.x) <= hhi;
                     if (rel) {
                         g0 = reinterpret_cast<const ulonglong2 *>(r4)[2];
                         g1 = reinterpret_cast<const ulonglong2 *>(r4)[3];
@@ -1981,20 +2119,57 @@ __global__ __launch_bounds__(kBlock) void k_stats(IndexView a, QueryView qv, uns
 }
 
 // Small batches (the per-RPC path, pkg/scd/operations_handler.go:118-168:
-// one covering and one search per request): one wave per query cell that
-// opens a quad of the query, lanes over the quad's postings in the band
-// [tlo - dcap, thi] plus its long postings, the cell-mask and fused
+// one covering and one search per request): kSmallSplit waves per query cell
+// that opens a quad of the query, lanes over the quad's postings in the band
+// [tlo - dcap, thi] (found by 64-ary wave searches) plus its long postings,
+// the waves of one cell interleaved 64 postings apart; the cell-mask and fused
 // altitude/time/owner filter, and the smallest-shared-cell rule (SQL
 // DISTINCT, Q13) decided exactly by a merge of the two sorted cell lists
 // below the quad -- no query ordering, units or dedupe pass: one launch, its
-// pairs through one wave-aggregated atomic per 64 postings.
+// pairs through one wave-aggregated atomic per 64 postings.  (Round 6: one
+// wave per cell walked a hot quad's ~1.5k-posting band in ~24 dependent
+// steps after two 14-step binary searches -- 0.10 -> 0.14 ms per batch of
+// ~18 requests once quads doubled the postings per group, profiles/r06e.)
 constexpr int kSmallBlock = 256;
+constexpr int kSmallSplit = 4;  // waves per query cell
+
+// First p in [lo, hi) with m(p) >= x (hi if none), the wave probing 64
+// evenly spaced positions per round: ceil(log64) rounds of one load each
+// instead of log2 dependent loads.  Wave-uniform.
+__device__ __forceinline__ uint64_t wave_lb_m(const longlong2 *bt, uint64_t lo, uint64_t hi, long long x)
+{
+    const int lane = threadIdx.x & 63;
+    while (hi - lo > 64) {
+        const uint64_t step = (hi - lo + 63) / 64;
+        const uint64_t p = lo + (uint64_t)lane * step;
+        bool below = false;
+        if (p < hi) {
+            const longlong2 t = bt[p];
+            below = tmin2(t.x, t.y) < x;
+        }
+        const int c = __popcll(__ballot(below));  // probes 0..c-1 lie below x (m is sorted)
+        if (c == 0) return lo;
+        const uint64_t nlo = lo + (uint64_t)(c - 1) * step + 1, nhi = lo + (uint64_t)c * step;
+        lo = nlo;
+        hi = nhi < hi ? nhi : hi;
+    }
+    const uint64_t p = lo + (uint64_t)lane;
+    bool below = false;
+    if (p < hi) {
+        const longlong2 t = bt[p];
+        below = tmin2(t.x, t.y) < x;
+    }
+    return lo + (uint64_t)__popcll(__ballot(below));
+}
+
 __global__ __launch_bounds__(kSmallBlock) void k_small_join(IndexView ix, QueryView qv, int64_t nqc, int64_t cap,
                                                              uint32_t *__restrict__ oq, uint32_t *__restrict__ oe,
                                                              unsigned long long *__restrict__ count)
 {
     const int lane = threadIdx.x & 63;
-    const int64_t k = (int64_t)blockIdx.x * (kSmallBlock / 64) + (threadIdx.x >> 6);
+    const int64_t wv = (int64_t)blockIdx.x * (kSmallBlock / 64) + (threadIdx.x >> 6);
+    const int64_t k = wv / kSmallSplit;
+    const uint64_t part = (uint64_t)(wv % kSmallSplit);
     if (k >= nqc) return;  // wave-uniform
     int64_t lo = 0, hi = qv.nq;  // the cell's query: offs[lo] <= k < offs[hi]
     while (hi - lo > 1) {
@@ -2019,37 +2194,55 @@ __global__ __launch_bounds__(kSmallBlock) void k_small_join(IndexView ix, QueryV
     const long long tlo = qv.tlo[q], thi = qv.thi[q];
     const float alo = qv.alo[q], ahi = qv.ahi[q];
     const int32_t own = qv.owner ? qv.owner[q] : -1;
-    // a regular posting (|t1 - t0| <= dcap) meets [tlo, thi] only if its start m is in [tlo - dcap, thi]
+    // a regular posting (|t1 - t0| <= dcap) meets [tlo, thi] only if its start m is in [tlo - dcap, thi]:
+    // one range of each m-ordered run (the regular part, or each altitude band of it), then the long postings
     const long long mlo = tlo < LLONG_MIN + ix.dcap ? LLONG_MIN : tlo - ix.dcap;
-    const uint64_t r0 = lb_m(ix.b_t, s0, sr, mlo), r1 = ub_m(ix.b_t, r0, sr, thi);
-    const uint64_t nreg = r1 - r0, ntot = nreg + (s1 - sr);
-    for (uint64_t b = 0; b < ntot; b += 64) {
-        const uint64_t t = b + (uint64_t)lane;
-        bool keep = false;
-        uint32_t ent = 0;
-        if (t < ntot) {
-            const uint64_t p = t < nreg ? r0 + t : sr + (t - nreg);
-            const longlong2 pt = ix.b_t[p];
-            const float2 pa = ix.b_alt[p];
-            const uint32_t pe = ix.b_e[p];
-            ent = pe & ~kFirstBit;
-            // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels)
-            bool pass = (pt.y >= tlo) & (pt.x <= thi) & (pa.y >= alo) & (pa.x <= ahi) &
-                        ((ix.b_meta[p] & qmask) != 0);
-            if (own >= 0) pass &= ix.b_owner[p] == own;
-            if (pass && !is_dead(ix, ent))
-                keep = k == c0 || (pe & kFirstBit) || no_smaller_shared<2>(ix, ent, cq0, qv.cells + c0, k - c0);
+    uint32_t rel[9];
+    int nrun = 1;
+    rel[0] = 0;
+    rel[1] = (uint32_t)(sr - s0);
+    if (ix.s_band) {
+        band_starts(ix, slot, (uint32_t)(sr - s0), rel);
+        nrun = 8;
+    }
+    for (int run = 0; run <= nrun; run++) {
+        uint64_t r0 = sr, r1 = s1;  // (run == nrun: the long postings)
+        if (run < nrun) {
+            const uint64_t a0 = s0 + rel[run], a1 = s0 + rel[run + 1];
+            if (a1 <= a0) continue;
+            r0 = wave_lb_m(ix.b_t, a0, a1, mlo);
+            // (ub: the first m > thi = the first m >= thi + 1; thi = LLONG_MAX: the run's end)
+            r1 = thi == LLONG_MAX ? a1 : wave_lb_m(ix.b_t, r0, a1, thi + 1);
         }
-        const unsigned long long m = __ballot(keep);
-        if (!m) continue;
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(count, (unsigned long long)__popcll(m));
-        base = uni64_lane0(base);
-        if (keep) {
-            const unsigned long long pos = base + mbcnt64(m);
-            if ((int64_t)pos < cap) {  // else counted only: the host regrows and reruns
-                oq[pos] = q;
-                oe[pos] = ent;
+        const uint64_t ntot = r1 - r0;
+        for (uint64_t b = part * 64; b < ntot; b += kSmallSplit * 64) {
+            const uint64_t t = b + (uint64_t)lane;
+            bool keep = false;
+            uint32_t ent = 0;
+            if (t < ntot) {
+                const uint64_t p = r0 + t;
+                const longlong2 pt = ix.b_t[p];
+                const float2 pa = ix.b_alt[p];
+                const uint32_t pe = ix.b_e[p];
+                ent = pe & ~kFirstBit;
+                // COALESCE'd predicates of operations.go:394-402 (NULL -> sentinels)
+                bool pass = (pt.y >= tlo) & (pt.x <= thi) & (pa.y >= alo) & (pa.x <= ahi) &
+                            ((ix.b_meta[p] & qmask) != 0);
+                if (own >= 0) pass &= ix.b_owner[p] == own;
+                if (pass && !is_dead(ix, ent))
+                    keep = k == c0 || (pe & kFirstBit) || no_smaller_shared<2>(ix, ent, cq0, qv.cells + c0, k - c0);
+            }
+            const unsigned long long m = __ballot(keep);
+            if (!m) continue;
+            unsigned long long base = 0;
+            if (lane == 0) base = atomicAdd(count, (unsigned long long)__popcll(m));
+            base = uni64_lane0(base);
+            if (keep) {
+                const unsigned long long pos = base + mbcnt64(m);
+                if ((int64_t)pos < cap) {  // else counted only: the host regrows and reruns
+                    oq[pos] = q;
+                    oe[pos] = ent;
+                }
             }
         }
     }
@@ -2118,7 +2311,8 @@ void SearchEngine::search_small(const dssg_index *idx, int64_t nq, const int64_t
         uint32_t *oq = oq_.ensure(small_cap_ + 1), *oe = oe_.ensure(small_cap_ + 1);
         DSS_HIP(hipMemsetAsync(count, 0, sizeof(unsigned long long), s));
         if (timing_) DSS_HIP(hipEventRecord(ev0_, s));
-        hipLaunchKernelGGL(k_small_join, dim3(grid_for(nqc, kSmallBlock / 64)), dim3(kSmallBlock), 0, s, ix, qv, nqc,
+        hipLaunchKernelGGL(k_small_join, dim3(grid_for(nqc * kSmallSplit, kSmallBlock / 64)), dim3(kSmallBlock), 0, s,
+                           ix, qv, nqc,
                            small_cap_, oq, oe, count);
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));
         const int64_t n = (int64_t)fetch(count, s);
@@ -2301,10 +2495,47 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     IndexView pv = view_of(idx);  // slots only (postings not built yet)
     DevBuf<uint32_t> key_b, key2_b, pos2_b;
     uint32_t *key = key_b.ensure(NP + 1), *key2 = key2_b.ensure(NP + 1), *pos2 = pos2_b.ensure(NP + 1);
+    // altitude bands (tools/band_sim.py): the regular postings
+    // of slots with >= band_dense_ of them split into bands_ runs by alt_lo
+    // quantile, so a 64-posting tile's altitude hull excludes the records of
+    // other altitudes (configs[2]: 38 % of the lane tests failed on altitude)
+    int nb = 1, kshift = 1;
+    BandThr bt{};
+    DevBuf<uint32_t> scnt_b;
+    const uint32_t *scnt = nullptr;
+    const uint32_t dense = (uint32_t)std::min<int64_t>(band_dense_, 0xffffffffll);
+    if (bands_ > 1 && NP && n && ns < ((int64_t)1 << 27)) {
+        uint32_t *sc = scnt_b.ensure(ns + 1);
+        DSS_HIP(hipMemsetAsync(sc, 0, sizeof(uint32_t) * (ns + 1), s));
+        hipLaunchKernelGGL(k_slot_hist, dim3(grid_for(NP, kBlock)), dim3(kBlock), 0, s, NP, pv, pos, e_cells, sc);
+        unsigned long long *nd = stat + 77;  // (the multiplicity word is consumed)
+        DSS_HIP(hipMemsetAsync(nd, 0, sizeof(unsigned long long), s));
+        hipLaunchKernelGGL(k_dense_slots, dim3(grid_for(ns, kBlock)), dim3(kBlock), 0, s, ns, sc, dense, nd);
+        constexpr int64_t kSamples = 8192;
+        const int64_t m = std::min<int64_t>(kSamples, n);
+        DevBuf<float> smp_b;
+        float *smp = smp_b.ensure(m + 1);
+        hipLaunchKernelGGL(k_sample_f32, dim3(grid_for(m, kBlock)), dim3(kBlock), 0, s, n, alt_lo, m, smp);
+        std::vector<float> hs((size_t)m);
+        unsigned long long ndense = 0;
+        DSS_HIP(hipMemcpyAsync(hs.data(), smp, sizeof(float) * m, hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipMemcpyAsync(&ndense, nd, sizeof(ndense), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipStreamSynchronize(s));
+        hs.erase(std::remove_if(hs.begin(), hs.end(), [](float x) { return x != x; }), hs.end());
+        std::sort(hs.begin(), hs.end());
+        if (ndense > 0 && !hs.empty() && hs.front() < hs.back()) {
+            nb = std::min(bands_, 8);
+            kshift = 4;
+            for (int b = 0; b < nb - 1; b++) bt.v[b] = hs[(size_t)((b + 1) * hs.size() / (size_t)nb)];
+            scnt = sc;
+        }
+    }
+    idx->n_bands = nb;
     if (NP)
         hipLaunchKernelGGL(k_slot_keys, dim3(grid_for(NP, kBlock)), dim3(kBlock), 0, s, NP, pv, pos, e_cells, pent, t0, t1,
-                           thr, key);
-    radix_sort_pairs(key, key2, pos, pos2, NP, bits_for(ns) + 1, tmp_, s);
+                           thr, kshift, scnt, dense, alt_lo, bt, nb, key);
+    radix_sort_pairs(key, key2, pos, pos2, NP, bits_for(ns) + kshift, tmp_, s);
+    scnt_b.release();
     key_b.release();
     pos_b.release();
     tmp_.release();  // the sort's alternate buffers
@@ -2325,26 +2556,35 @@ void SearchEngine::build(dssg_index *idx, int64_t n, const int64_t *cell_offs, c
     dec_b.release();
     // (7) slot table: s_post (first posting per slot, scan of counts), s_nreg
     {
-        DevBuf<uint32_t> f_b, e_b, r_b;
+        DevBuf<uint32_t> f_b, e_b, r_b, bf_b;
         uint32_t *sf = f_b.ensure(ns + 1), *se = e_b.ensure(ns + 1), *sr = r_b.ensure(ns + 1);
+        uint32_t *bfirst = nullptr, *sband = nullptr;
         DSS_HIP(hipMemsetAsync(sf, 0, sizeof(uint32_t) * (ns + 1), s));
         DSS_HIP(hipMemsetAsync(se, 0, sizeof(uint32_t) * (ns + 1), s));
         DSS_HIP(hipMemsetAsync(sr, 0, sizeof(uint32_t) * (ns + 1), s));
+        if (nb > 1) {
+            bfirst = bf_b.ensure(8 * (ns + 1));
+            DSS_HIP(hipMemsetAsync(bfirst, 0, sizeof(uint32_t) * 8 * (ns + 1), s));
+            sband = idx->s_band.ensure_exact(8 * (ns + 1));
+        } else {
+            idx->s_band.release();
+        }
         if (NP)
-            hipLaunchKernelGGL(k_slot_bounds, dim3(grid_for(NP, kBlock)), dim3(kBlock), 0, s, NP, key2, sf, se, sr,
-                               stat + 72);
+            hipLaunchKernelGGL(k_slot_bounds, dim3(grid_for(NP, kBlock)), dim3(kBlock), 0, s, NP, key2, kshift, sf, se,
+                               sr, bfirst, stat + 72);
         DevBuf<int64_t> c_b, o_b;
         int64_t *cnt = c_b.ensure(ns + 1), *off = o_b.ensure(ns + 2);
         uint32_t *nreg = idx->s_nreg.ensure_exact(ns + 1);
         if (ns)
-            hipLaunchKernelGGL(k_slot_counts, dim3(grid_for(ns, kBlock)), dim3(kBlock), 0, s, ns, sf, se, sr, cnt, nreg,
-                               stat + 74);
+            hipLaunchKernelGGL(k_slot_counts, dim3(grid_for(ns, kBlock)), dim3(kBlock), 0, s, ns, sf, se, sr,
+                               (const uint32_t *)bfirst, cnt, nreg, sband, stat + 74);
         exclusive_scan_i64(cnt, off, ns, tmp2_, s);
         uint64_t *sp = idx->s_post.ensure_exact(ns + 1);
         hipLaunchKernelGGL(k_u64_store, dim3(grid_for(ns + 1, kBlock)), dim3(kBlock), 0, s, ns + 1, off, sp);
         uint8_t *lfp = idx->s_lfp.ensure_exact(ns + 1);
         DSS_HIP(hipMemsetAsync(lfp, 0, ns + 1, s));
-        if (NP) hipLaunchKernelGGL(k_slot_lfp, dim3(grid_for(NP, kBlock)), dim3(kBlock), 0, s, NP, key2, b_meta, lfp);
+        if (NP)
+            hipLaunchKernelGGL(k_slot_lfp, dim3(grid_for(NP, kBlock)), dim3(kBlock), 0, s, NP, key2, kshift, b_meta, lfp);
     }
     stage_check(s, "index build: slot table");
     // (8) entity-level attributes: ends_at, owner, owner -> entities, counters
@@ -2497,6 +2737,9 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     const int64_t *dnkeys = qo + nq;
     radix_sort_pairs_dn(key, skey, val, sval, nqc, dnkeys, bits_for(idx->n_slots()) + 1, tmp_, s);
     const uint64_t *sq = sval;  // (quantised starts in the high words)
+    QRec *recs_k = (QRec *)rec2_.ensure(sizeof(QRec) * (nqc + 1));
+    hipLaunchKernelGGL(k_rec_permute, dim3(grid_for(4 * nqc, kBlock)), dim3(kBlock), 0, s, dnkeys,
+                       (const uint64_t *)sval, (const QRec *)recs, recs_k);
     // (5) join units = 64-posting tiles of every cell the batch meets, each
     // with the records it can meet
     if (n_cu_ == 0) {
@@ -2583,7 +2826,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
                                      : (q_owner ? k_join<true, false, false, true> : k_join<false, false, false, true>))
                             : (dense ? (q_owner ? k_join<true, false, true, false> : k_join<false, false, true, false>)
                                      : (q_owner ? k_join<true, false, false, false> : k_join<false, false, false, false>));
-        hipLaunchKernelGGL(kshort, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs,
+        hipLaunchKernelGGL(kshort, dim3(nblocks), dim3(64 * kWaves), 0, s, ja, (const QRec *)recs_k,
                            (const uint64_t *)sval, (const Unit *)units, ctl + kCtlQueue);
         if (any_long) {  // the same output streams, continued
             auto klong = quads ? (q_owner ? k_join<true, true, false, true> : k_join<false, true, false, true>)
@@ -2604,7 +2847,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
             const int64_t want = (long_units_prev_ + 8 * kWaves - 1) / (8 * kWaves);
             const unsigned lblocks = (unsigned)std::max<int64_t>(
                 std::min<int64_t>((int64_t)n_cu_ * occ_long_, std::max<int64_t>(want, n_cu_)), 1);
-            hipLaunchKernelGGL(klong, dim3(lblocks), dim3(64 * kWaves), 0, s, jl, (const QRec *)recs,
+            hipLaunchKernelGGL(klong, dim3(lblocks), dim3(64 * kWaves), 0, s, jl, (const QRec *)recs_k,
                                (const uint64_t *)sval, (const Unit *)units_l, ctl + kCtlQueueL);
         }
         if (timing_) DSS_HIP(hipEventRecord(ev1_, s));

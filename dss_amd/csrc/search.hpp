@@ -30,6 +30,12 @@ struct dssg_index {
     dss::DevBuf<uint64_t> s_post;     // n_slots + 1: first posting of each slot
     dss::DevBuf<uint32_t> s_nreg;     // n_slots: regular-duration postings of the slot
     dss::DevBuf<uint8_t> s_lfp;       // n_slots: 1 = the slot holds a long-footprint posting (join variant)
+    // altitude bands (n_bands > 1): a slot with >= band_dense postings keeps its
+    // regular postings as n_bands runs by alt_lo (global quantiles), each in
+    // m order; s_band[8 * slot + b] = start of band b relative to s_post[slot]
+    // (band b ends where b + 1 starts, the last at s_nreg); other slots: one run
+    dss::DevBuf<uint32_t> s_band;     // 8 * n_slots (n_bands > 1)
+    int n_bands = 1;
     // ---- time --------------------------------------------------------------------
     int64_t dcap = 0;      // max duration of a regular posting's entity (us)
     int gshift = 37;       // posting groups: cell >> gshift (37: quads = level-12 cells, 35: level-13 cells)
@@ -107,6 +113,15 @@ class SearchEngine {
     // entity's cells fill them: >= 1.5 cells per (entity, quad)), 1 level-13
     // cells, 2 quads (level-12 cells)
     void set_grain(int v) { grain_ = v; }
+    // altitude bands of the dense slots of later builds (1: none; 2..8) and the
+    // slot size from which they apply
+    void set_bands(int nb, int64_t dense)
+    {
+        bands_ = nb;
+        band_dense_ = dense;
+    }
+    int bands() const { return bands_; }
+    int64_t band_dense() const { return band_dense_; }
     double last_join_kernel_ms() const { return join_ms_; }
     int64_t last_units() const { return units_; }
     int64_t last_keys() const { return keys_; }
@@ -167,7 +182,7 @@ class SearchEngine {
     DevBuf<int64_t> qcnt_, qoff_, rcnt_, roff_, ucnt_, uoff_, cnt64_;
     DevBuf<uint64_t> kv64_, kv64b_;  // query-cell keys' values: cell | quantised start << 32
     DevBuf<uint8_t> qlong_;
-    DevBuf<unsigned char> rec_, units_buf_, batch_buf_;
+    DevBuf<unsigned char> rec_, rec2_, units_buf_, batch_buf_;  // rec2_: the records in key order
     DevBuf<unsigned long long> counter_, regcnt_;
     DevBuf<uint32_t> oq_, oe_, oq2_, oe2_, fills_;
     DevBuf<unsigned long long> work_;
@@ -190,6 +205,8 @@ class SearchEngine {
     bool dense_out_ = false;  // the previous batch's pass density was high: k_join's 6 x 1024-pair stage shape
     int join_shape_ = 0;      // 0: by dense_out_; 1: the sparse shape; 2: the dense shape (tests)
     int grain_ = 0;           // 0: auto; 1: cells; 2: quads
+    int bands_ = 4;           // altitude bands of dense slots (1: none) -- DESIGN.md s4
+    int64_t band_dense_ = 1024;
     double join_ms_ = 0;
     int64_t units_ = 0, keys_ = 0, runs_ = 0, iters_ = 0, tests_ = 0;
     int64_t flushes_ = 0, merges_ = 0, merge_lanes_ = 0, tagged_ = 0, long_queries_ = 0, long_postings_ = 0;

@@ -451,8 +451,12 @@ void dssg_set_timing(dssg_ctx *ctx, int enabled);
  * (0: picked per batch from the previous batch's pass density, the default;
  * 1: 7 workgroups per CU with 640-pair stages; 2: 6 with 1024);
  * "index_grain" = the posting grain of the indexes this context builds (0:
- * picked per build, the default; 1: level-13 cells; 2: quads).  Unknown key
- * or value: DSSG_ERR_INVALID. */
+ * picked per build, the default; 1: level-13 cells; 2: quads);
+ * "index_bands" = altitude bands of the dense posting groups of later builds
+ * (1: none, 2..8; default 4: a group's regular postings in alt_lo-quantile
+ * runs, so a join tile's altitude hull skips records); "band_dense" = the
+ * group size (postings, >= 64) from which the bands apply (default 1024).
+ * Results do not depend on either.  Unknown key or value: DSSG_ERR_INVALID. */
 int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value);
 /* Work counters of the most recent search: query-cell keys (cells of the
  * batch whose cell holds postings), join units (<= 64 records x a posting
