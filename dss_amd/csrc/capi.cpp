@@ -1216,6 +1216,9 @@ void sharded_step(dssg_ctx *ctx, dssg_comm *cq, dssg_comm *cx, const dssg_index 
 {
     const int W = cq->nranks, me = cq->rank;
     if (cx->nranks != W || cx->rank != me) throw dss::Error(DSSG_ERR_INVALID, "sharded step: communicators differ");
+    // a shard joins up to W * nq routed rows in one search (2^25 queries per call)
+    if ((int64_t)W * nq >= ((int64_t)1 << 25))
+        throw dss::Error(DSSG_ERR_INVALID, "sharded step: nranks x nq must stay below 2^25 routed rows per shard");
     dss::ShardStats &st = ctx->shard_stats;
     st = dss::ShardStats{};
     hipEvent_t *ev = ctx->shard_ev;

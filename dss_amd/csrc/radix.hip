@@ -48,7 +48,6 @@ constexpr int kDPT = kMaxDigits / kRBlock;       // digits per thread in the per
 constexpr int kRWaves = kRBlock / 64;
 constexpr int kItems = DSS_RADIX_ITEMS;
 constexpr int kTile = kRBlock * kItems;  // 2048 keys per block
-constexpr int kWaveTile = 64 * kItems;   // 512 keys per wave, contiguous
 
 template <typename K>
 __device__ __forceinline__ uint32_t digit_of(K k, int shift, uint32_t mask)
@@ -85,7 +84,7 @@ __device__ __forceinline__ uint32_t block_incl_scan(uint32_t x, uint32_t *ws, ui
     return x + pre;
 }
 
-template <typename K>
+template <typename K, int ITEMS = kItems>
 __global__ __launch_bounds__(kRBlock) void k_rs_hist(const K *__restrict__ keys, int64_t n, const int64_t *__restrict__ dn,
                                                      int shift, int rbits, uint32_t *__restrict__ hist, int64_t stride)
 {
@@ -95,16 +94,34 @@ __global__ __launch_bounds__(kRBlock) void k_rs_hist(const K *__restrict__ keys,
     const uint32_t nd = 1u << rbits, mask = nd - 1;
     for (int i = tid; i < kRWaves * kMaxDigits; i += kRBlock) (&h[0][0])[i] = 0;
     __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * kTile;
-    K k[kItems];
+    const int64_t base = (int64_t)blockIdx.x * (kRBlock * ITEMS);
+    K k[ITEMS];
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
+    for (int j = 0; j < ITEMS; j++) {
         const int64_t i = base + j * kRBlock + tid;
         k[j] = i < n ? keys[i] : K(0);
     }
+#ifdef DSS_HIST_MATCH
+    // (variant) lanes of one digit found by ballot match, one LDS add per run:
+    // clustered keys (hotspot cells) otherwise serialise on the same counter
+    const int lane = tid & 63;
 #pragma unroll
-    for (int j = 0; j < kItems; j++)
+    for (int j = 0; j < ITEMS; j++) {
+        const bool ok = base + j * kRBlock + tid < n;
+        const uint32_t d = digit_of(k[j], shift, mask);
+        unsigned long long m = __ballot(ok);
+        for (int b = 0; b < rbits; b++) {
+            const unsigned long long bb = __ballot((d >> b) & 1u);
+            m &= ((d >> b) & 1u) ? bb : ~bb;
+        }
+        if (ok && lanes_below(m) == 0) atomicAdd(&h[w][d], (uint32_t)__popcll(m));
+        (void)lane;
+    }
+#else
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++)
         if (base + j * kRBlock + tid < n) atomicAdd(&h[w][digit_of(k[j], shift, mask)], 1u);
+#endif
     __syncthreads();
     for (int d = tid; d < (int)nd; d += kRBlock) {
         uint32_t c = 0;
@@ -144,7 +161,7 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scan(uint32_t *__restrict__ hist
 // (key, value) and sorts the word (key & ~lomask) | value; bit 1 -- it writes
 // the word back out as (word & ~lomask) | kconst and value word & lomask.
 // Middle passes move the words alone (HAS_V false).
-template <typename K, typename V, bool HAS_V, int PK = 0>
+template <typename K, typename V, bool HAS_V, int PK = 0, int ITEMS = kItems>
 __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki, const V *__restrict__ vi,
                                                         K *__restrict__ ko, V *__restrict__ vo, int64_t n,
                                                         const int64_t *__restrict__ dn, int shift, int rbits,
@@ -157,8 +174,9 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
     __shared__ uint32_t dstart[kMaxDigits];       // tile-local start of each digit
     __shared__ uint32_t gbase[kMaxDigits];        // global position of tile slot 0 of each digit
     __shared__ uint32_t ws[kRWaves];
-    __shared__ K sk[kTile];
-    __shared__ V sv[HAS_V ? kTile : 1];
+    constexpr int kT = kRBlock * ITEMS, kWT = 64 * ITEMS;
+    __shared__ K sk[kT];
+    __shared__ V sv[HAS_V ? kT : 1];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t nd = 1u << rbits, mask = nd - 1;
     for (int i = tid; i < kRWaves * kMaxDigits; i += kRBlock) (&wh[0][0])[i] = 0;
@@ -183,12 +201,12 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
         }
     }
 
-    const int64_t sub = (int64_t)blockIdx.x * kTile + (int64_t)w * kWaveTile;
-    K k[kItems];
-    V v[kItems];
-    uint32_t loc[kItems];
+    const int64_t sub = (int64_t)blockIdx.x * kT + (int64_t)w * kWT;
+    K k[ITEMS];
+    V v[ITEMS];
+    uint32_t loc[ITEMS];
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
+    for (int j = 0; j < ITEMS; j++) {
         const int64_t i = sub + j * 64 + lane;
         const bool ok = i < n;
         if constexpr ((PK & 1) != 0) k[j] = ok ? ((ki[i] & ~lomask) | (K)vi[i]) : K(0);
@@ -196,7 +214,7 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
         if (HAS_V) v[j] = ok ? vi[i] : V(0);
     }
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
+    for (int j = 0; j < ITEMS; j++) {
         const bool ok = sub + j * 64 + lane < n;
         const uint32_t d = digit_of(k[j], shift, mask);
         unsigned long long m = __ballot(ok);
@@ -239,7 +257,7 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
+    for (int j = 0; j < ITEMS; j++) {
         if (sub + j * 64 + lane < n) {
             const uint32_t d = digit_of(k[j], shift, mask);
             const uint32_t slot = dstart[d] + wh[w][d] + loc[j];
@@ -248,8 +266,8 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
         }
     }
     __syncthreads();
-    const int64_t rem = n - (int64_t)blockIdx.x * kTile;
-    const int tile_n = rem < kTile ? (int)rem : kTile;
+    const int64_t rem = n - (int64_t)blockIdx.x * kT;
+    const int tile_n = rem < kT ? (int)rem : kT;
     for (int i = tid; i < tile_n; i += kRBlock) {
         const K kk = sk[i];
         const uint32_t p = gbase[digit_of(kk, shift, mask)] + (uint32_t)i;
@@ -397,10 +415,17 @@ void radix_sort_packed(const uint64_t *ki, uint64_t *ko, const uint32_t *vi, uin
                        DevBuf<unsigned char> &tmp, hipStream_t s)
 {
     using K = uint64_t;
+    // 4096-word tiles (16 per thread): the words alone need 32 KiB of LDS
+    // staging, and a digit's run per tile is twice as long as at 2048 (the
+    // scatter's writes are the pass's cost where the low digits are random)
+#ifndef DSS_PACKED_ITEMS
+#define DSS_PACKED_ITEMS 16
+#endif
+    constexpr int kPI = DSS_PACKED_ITEMS, kPT = kRBlock * kPI;
     if (n <= 0) return;
-    if (n >= ((int64_t)1 << 32) - kTile) throw Error(DSSG_ERR_CAPACITY, "radix sort: more than 2^32 - 2048 keys");
+    if (n >= ((int64_t)1 << 32) - kPT) throw Error(DSSG_ERR_CAPACITY, "radix sort: more than 2^32 - 4096 keys");
     if (bits > 64) bits = 64;
-    const int64_t ntiles = (n + kTile - 1) / kTile, stride = (ntiles + 3) & ~(int64_t)3;
+    const int64_t ntiles = (n + kPT - 1) / kPT, stride = (ntiles + 3) & ~(int64_t)3;
     const size_t hist_b = align256(sizeof(uint32_t) * kMaxDigits * stride), dtot_b = align256(sizeof(uint32_t) * kMaxDigits);
     const int g = (int)std::min<int64_t>(ntiles, 1024);
     unsigned long long var = 0, vor = 0, k0 = 0;
@@ -436,22 +461,22 @@ void radix_sort_packed(const uint64_t *ki, uint64_t *ko, const uint32_t *vi, uin
         const int shift = lo + p * rb, r = hi - shift < rb ? hi - shift : rb;
         const bool to_out = ((passes - 1 - p) & 1) == 0;
         K *dst = to_out ? ko : kalt;
-        hipLaunchKernelGGL(k_rs_hist<K>, dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src, n, nullptr, shift, r, hist,
-                           stride);
+        hipLaunchKernelGGL((k_rs_hist<K, kPI>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src, n, nullptr, shift, r,
+                           hist, stride);
         hipLaunchKernelGGL(k_rs_scan, dim3(1u << r), dim3(kRBlock), 0, s, hist, stride, ntiles, dtot);
         const bool first = p == 0, last = p == passes - 1;
         if (first && last)
-            hipLaunchKernelGGL((k_rs_scatter<K, uint32_t, false, 3>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src,
-                               vi, dst, vo, n, nullptr, shift, r, hist, stride, dtot, lomask, kconst);
+            hipLaunchKernelGGL((k_rs_scatter<K, uint32_t, false, 3, kPI>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s,
+                               src, vi, dst, vo, n, nullptr, shift, r, hist, stride, dtot, lomask, kconst);
         else if (first)
-            hipLaunchKernelGGL((k_rs_scatter<K, uint32_t, false, 1>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src,
-                               vi, dst, vo, n, nullptr, shift, r, hist, stride, dtot, lomask, kconst);
+            hipLaunchKernelGGL((k_rs_scatter<K, uint32_t, false, 1, kPI>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s,
+                               src, vi, dst, vo, n, nullptr, shift, r, hist, stride, dtot, lomask, kconst);
         else if (last)
-            hipLaunchKernelGGL((k_rs_scatter<K, uint32_t, false, 2>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src,
-                               vi, dst, vo, n, nullptr, shift, r, hist, stride, dtot, lomask, kconst);
+            hipLaunchKernelGGL((k_rs_scatter<K, uint32_t, false, 2, kPI>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s,
+                               src, vi, dst, vo, n, nullptr, shift, r, hist, stride, dtot, lomask, kconst);
         else
-            hipLaunchKernelGGL((k_rs_scatter<K, uint32_t, false, 0>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src,
-                               vi, dst, vo, n, nullptr, shift, r, hist, stride, dtot, lomask, kconst);
+            hipLaunchKernelGGL((k_rs_scatter<K, uint32_t, false, 0, kPI>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s,
+                               src, vi, dst, vo, n, nullptr, shift, r, hist, stride, dtot, lomask, kconst);
         DSS_HIP(hipGetLastError());
         src = dst;
     }

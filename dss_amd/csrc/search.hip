@@ -2778,7 +2778,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     if (out_rcap_ == 0) out_rcap_ = ((int64_t)nq * 16 / kRegions / kOutChunk + 2) * kOutChunk;
     if (any_long && tag_rcap_ == 0) tag_rcap_ = ((int64_t)nq * 4 / kRegions / kOutChunk + 2) * kOutChunk;
     const int qb = bits_for(nq), eb = bits_for(idx->n_e);
-    const int hbm = std::min(24, 64 - qb - eb);  // qb <= 29, eb <= 32: 3 <= hbm <= 24
+    const int hbm = std::min(24, 64 - qb - eb);  // qb <= 25 (kMaxBatchQ), eb <= 32: 7 <= hbm <= 24
     // closing the holes of partly filled / unreserved chunks below n with the
     // entries at or above n
     auto close_holes = [&](int64_t nch, const uint32_t *fills, int64_t n, auto mover) {

@@ -198,6 +198,9 @@ int32_t dssg_index_grain(const dssg_index *idx);      /* S2 level of the posting
  *   AND e.alt_hi >= q.alt_lo AND e.alt_lo <= q.alt_hi
  *   AND (q.owner < 0 OR e.owner == q.owner)
  * q.tlo must be > INT64_MIN (it always carries `now` or `earliest`).
+ * Limits per call: nq < 2^25 queries (a join record keeps the query id below
+ * its flag bits) and < 2^32 - 1 query cells; beyond either, DSSG_ERR_INVALID
+ * / DSSG_ERR_CAPACITY -- split the batch.
  */
 int dssg_search_device(dssg_ctx *ctx, const dssg_index *idx, int64_t nq, const int64_t *d_q_offs,
                        const uint64_t *d_q_cells, const float *d_q_alt_lo, const float *d_q_alt_hi,
@@ -406,6 +409,9 @@ void dssg_comm_free(dssg_comm *comm);
  * (the own block, send_bytes[rank] == recv_bytes[rank], is copied locally). */
 int dssg_comm_alltoallv_device(dssg_ctx *ctx, dssg_comm *comm, const void *d_send, const int64_t *send_bytes,
                                void *d_recv, const int64_t *recv_bytes, void *stream);
+/* A sharded step joins on each shard the rows routed to it from every rank:
+ * up to nranks * nq rows, which must stay below the search's 2^25 queries
+ * per call (checked: DSSG_ERR_INVALID; the caller splits its batch). */
 int dssg_sharded_search_device(dssg_ctx *ctx, dssg_comm *comm, const dssg_index *shard, const uint64_t *d_part_hi,
                                int64_t nq, const int64_t *d_q_offs, const uint64_t *d_q_cells,
                                const float *d_q_alt_lo, const float *d_q_alt_hi, const int64_t *d_q_tlo,
