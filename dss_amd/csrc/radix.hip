@@ -433,15 +433,22 @@ void radix_sort_packed(const uint64_t *ki, uint64_t *ko, const uint32_t *vi, uin
         unsigned long long *vm = (unsigned long long *)tmp.ensure(
                                std::max(hist_b + dtot_b, sizeof(unsigned long long) * (2 * g + 3))),
                            *part = vm + 3;
-        hipLaunchKernelGGL(k_rs_varying<K>, dim3((unsigned)g), dim3(kRBlock), 0, s, ki, n, part, vi);
+        // the keys' varying bits first; the values are scanned only when the
+        // keys' constant low bits are fewer than 32 (level-13 ids: 35)
+        hipLaunchKernelGGL(k_rs_varying<K>, dim3((unsigned)g), dim3(kRBlock), 0, s, ki, n, part, nullptr);
         hipLaunchKernelGGL(k_rs_or_parts, dim3(1), dim3(kRBlock), 0, s, part, g, vm);
-        hipLaunchKernelGGL(k_rs_or_parts, dim3(1), dim3(kRBlock), 0, s, part + g, g, vm + 1);
-        unsigned long long h[2];
-        DSS_HIP(hipMemcpyAsync(h, vm, sizeof(h), hipMemcpyDeviceToHost, s));
+        DSS_HIP(hipMemcpyAsync(&var, vm, sizeof(var), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipMemcpyAsync(&k0, ki, sizeof(k0), hipMemcpyDeviceToHost, s));
         DSS_HIP(hipStreamSynchronize(s));
-        var = h[0];
-        vor = h[1];
+        const unsigned long long vsorted = bits < 64 ? var & ((1ull << bits) - 1) : var;
+        if (vsorted != 0 && __builtin_ctzll(vsorted) < 32) {
+            hipLaunchKernelGGL(k_rs_varying<K>, dim3((unsigned)g), dim3(kRBlock), 0, s, ki, n, part, vi);
+            hipLaunchKernelGGL(k_rs_or_parts, dim3(1), dim3(kRBlock), 0, s, part + g, g, vm + 1);
+            DSS_HIP(hipMemcpyAsync(&vor, vm + 1, sizeof(vor), hipMemcpyDeviceToHost, s));
+            DSS_HIP(hipStreamSynchronize(s));
+        } else {
+            vor = 0xffffffffull;  // any u32 value fits below bit 32
+        }
     }
     if (bits < 64) var &= (1ull << bits) - 1;
     const int lo = var ? __builtin_ctzll(var) : 64, hi = var ? 64 - __builtin_clzll(var) : 0;
