@@ -62,7 +62,7 @@ STAGE_LIMIT_S = {"native exchange init": 300, "warmup": 900, "timed steps": 900,
 # The sharded leg of an N > 1 replica run (sharded_leg): a stage of it that
 # runs past its limit ends the rank with status 0 -- the replica line is
 # complete -- and rank 0 prints that line with sharded.error set.
-LEG_LIMIT_S = 300
+LEG_LIMIT_S = 120  # (each legit stage of the leg takes seconds at full size; a hang costs at most this)
 _PENDING = [None, 0]  # rank 0's finished replica line while the sharded leg runs; this rank
 
 

@@ -47,7 +47,6 @@ constexpr int kMaxDigits = 1 << kMaxDigitBits;
 constexpr int kDPT = kMaxDigits / kRBlock;       // digits per thread in the per-digit phases
 constexpr int kRWaves = kRBlock / 64;
 constexpr int kItems = DSS_RADIX_ITEMS;
-constexpr int kTile = kRBlock * kItems;  // 2048 keys per block
 
 template <typename K>
 __device__ __forceinline__ uint32_t digit_of(K k, int shift, uint32_t mask)
@@ -344,9 +343,12 @@ template <typename K, typename V, bool HAS_V>
 void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, const int64_t *dn, int bits, DevBuf<unsigned char> &tmp,
                 hipStream_t s)
 {
+    // 8-B keys alone: 4096-key tiles (16 per thread; 32 KiB of LDS staging,
+    // twice the digit-run length per tile -- the packed path's measurement)
+    constexpr int IT = (!HAS_V && sizeof(K) == 8) ? 2 * kItems : kItems, kT = kRBlock * IT;
     if (n <= 0) return;
     // positions are uint32: the digit offsets of the last tile stay < 2^32
-    if (n >= ((int64_t)1 << 32) - kTile) throw Error(DSSG_ERR_CAPACITY, "radix sort: more than 2^32 - 2048 keys");
+    if (n >= ((int64_t)1 << 32) - kT) throw Error(DSSG_ERR_CAPACITY, "radix sort: more than 2^32 - 4096 keys");
     const int kbits = (int)(8 * sizeof(K));
     if (bits > kbits) bits = kbits;
     if (bits <= 0) {
@@ -354,7 +356,7 @@ void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, const int64_t
         if (HAS_V) device_copy(vo, vi, sizeof(V) * n, s);
         return;
     }
-    const int64_t ntiles = (n + kTile - 1) / kTile, stride = (ntiles + 3) & ~(int64_t)3;
+    const int64_t ntiles = (n + kT - 1) / kT, stride = (ntiles + 3) & ~(int64_t)3;
     const size_t hist_b = align256(sizeof(uint32_t) * kMaxDigits * stride), dtot_b = align256(sizeof(uint32_t) * kMaxDigits);
     // wide keys: sort only the span of bits that vary (one read + one host
     // sync, against up to 4 passes saved)
@@ -394,9 +396,9 @@ void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, const int64_t
         const bool to_out = ((passes - 1 - p) & 1) == 0;
         K *dst = to_out ? ko : kalt;
         V *dstv = to_out ? vo : valt;
-        hipLaunchKernelGGL(k_rs_hist<K>, dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src, n, dn, shift, r, hist, stride);
+        hipLaunchKernelGGL((k_rs_hist<K, IT>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src, n, dn, shift, r, hist, stride);
         hipLaunchKernelGGL(k_rs_scan, dim3(1u << r), dim3(kRBlock), 0, s, hist, stride, ntiles, dtot);
-        hipLaunchKernelGGL((k_rs_scatter<K, V, HAS_V>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src, srcv, dst, dstv,
+        hipLaunchKernelGGL((k_rs_scatter<K, V, HAS_V, 0, IT>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s, src, srcv, dst, dstv,
                            n, dn, shift, r, hist, stride, dtot);
         DSS_HIP(hipGetLastError());
         src = dst;

@@ -1471,6 +1471,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
             nmeta = ix.b_meta[p];
             nt = ix.b_t[p];
             na = ix.b_alt[p];
+            // (round 6: skipping the load for an entity's first quad, whose
+            // pairs are all kept, made the load wait on b_e: 2.07 -> 2.10 ms)
             if (nsig) {
                 ns01 = ix.b_sig[2 * p];
                 ns23 = ix.b_sig[2 * p + 1];
@@ -2722,6 +2724,10 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     hipLaunchKernelGGL(k_qorder, dim3(grid_for(nq, kBlock)), dim3(kBlock), 0, s, nq, q_tlo, q_thi, (long long)idx->tbase,
                        idx->qshift, (double)idx->dcap, (const unsigned long long *)(ctl + kCtlWin), ok0, ov0,
                        ctl + kCtlDq);
+    // (round 6: a one-pass counting sort here -- ties need no order -- took
+    // 0.6 ms: the clamped NULL starts of ~2.5 % of the queries share one
+    // counter, and same-address atomics serialise; the 2-pass radix sort's
+    // per-tile histograms do not)
     radix_sort_pairs(ok0, ok1, ov0, perm, nq, kOrderBits, tmp_, s);
     // (3) keys (slot << 1 | wide, query cell) in that order; records per cell
     int64_t *qc = qcnt_.ensure(nq + 1), *qo = qoff_.ensure(nq + 2);
