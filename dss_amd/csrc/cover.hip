@@ -2189,6 +2189,8 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     // costs ~5 us: profiles/r05ak), then per footprint its clipped-edge items
     // and the descent list, and one sync for their totals (round 4 read the
     // counts twice, before and after the exact setup)
+    // (the ~1 footprint per 1M the triage leaves costs ~0.09 ms: one thread's
+    // serial exact path; a 4-block grid measured the same, profiles/r06p)
     hipLaunchKernelGGL(k_setup<false>, dim3(256), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng, radius_m, xoff,
                        xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, nullptr,
                        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);

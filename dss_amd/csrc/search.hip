@@ -10,28 +10,30 @@
 //
 // Index: one posting per (entity, quad) -- a quad is the
 // level-12 parent of 2 x 2 level-13 cells, the posting carries the mask of the
-// entity's cells in it -- sorted by (quad, duration class, m = min(t0, t1));
-// a quad's postings are found with one dense lookup (slot = cell >> 37 for
-// level-13 ids; a sorted side table for any other id, each its own quad --
-// the reference tests use invalid face-7 ids, Q12).  A query and an entity
-// meet in a quad where their masks intersect, and the pair is emitted in the
-// quad holding their smallest shared cell (SQL DISTINCT).
-// Filter attributes (altitudes, times, a 256-bit "near prefix" signature) are
-// inlined per posting, SoA.  No posting is copied: 2.2e9 postings (configs[4],
-// 50M corridors) fit one GPU.
+// entity's cells in it -- sorted by (quad, duration class, altitude band,
+// m = min(t0, t1)): a dense quad's regular postings form 4 runs by alt_lo
+// quantile, each in m order; a quad's postings are found with one dense
+// lookup (slot = cell >> 37 for level-13 ids; a sorted side table for any
+// other id, each its own quad -- the reference tests use invalid face-7 ids,
+// Q12).  A query and an entity meet in a quad where their masks intersect,
+// and the pair is emitted in the quad holding their smallest shared cell (SQL
+// DISTINCT).  Filter attributes (altitudes, times, a 256-bit "near prefix"
+// signature) are inlined per posting, SoA.  No posting is copied: 2.2e9
+// postings (configs[4], 50M corridors) fit one GPU.
 //
-// Search, a band join per cell:
+// Search, a band join per quad:
 //   * queries are ordered by start time (narrow windows first, wide ones
-//     after), their cells emitted in that order and stably grouped by cell,
-//     so a cell's query records come sorted by tlo;
-//   * a join unit = (cell, <= 64 consecutive records); a record can only meet
-//     a regular posting with m in [tlo - dcap, thi], so the unit scans the one
-//     contiguous posting range [min tlo - dcap, max thi] (binary search) plus
-//     the cell's long-duration postings;
-//   * one wavefront per unit, lane = record: postings are staged in LDS 64 at
-//     a time and broadcast; each lane ORs the fused altitude/time/owner
-//     predicate into a 64-bit mask, then walks its set bits to apply the
-//     smallest-shared-cell rule (SQL DISTINCT, Q13) and stage the pairs.
+//     after), one 64-B record per (query, quad) emitted in that order, the
+//     keys stably grouped by quad and the records permuted into that order,
+//     so a quad's records are one contiguous run sorted by start;
+//   * a join unit = one tile of <= 64 postings of a quad (one band of it) x
+//     the quad's records whose start can meet the tile (k_units);
+//   * one wavefront per unit, lane = posting (in registers): the records are
+//     loaded 64 at a time, those meeting the tile's time hull (and a banded
+//     tile's altitude hull) staged in LDS and broadcast; each lane ORs the
+//     fused altitude/time/owner predicate into a 64-bit mask, ANDs the quad
+//     cell masks, applies the smallest-shared-cell rule (SQL DISTINCT, Q13)
+//     and the batch's pairs leave contiguously.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -126,7 +128,7 @@ constexpr int kEmitDensity = DSS_EMIT_DENSITY;
 // many are kept -- plus the staging and emission shapes, summed over every
 // k_join launch into g_jprof and read (and cleared) by dssg_join_profile.
 // Slot meanings: kJProfNames in join_profile_read.
-constexpr int kJProf = 20;
+constexpr int kJProf = 22;
 #ifdef DSS_JOIN_PROFILE
 __device__ unsigned long long g_jprof[kJProf];
 #define JPROF(i, v) (jp[i] += (unsigned long long)(v))
@@ -1652,6 +1654,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 unsigned long long keep = pfirst ? m : (m & R0);
                 unsigned long long need = m & ~keep;
 #ifdef DSS_JOIN_PROFILE
+                unsigned long long unc = 0;
                 const unsigned long long need0 = need;
                 JPROF(6, __popcll(keep));
                 JPROF(7, __popcll(need0));
@@ -1680,6 +1683,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                     // (without long postings every posting's prefix is compact:
                     // all of its entity's cells lie in an 8 x 8 window)
                     bool k = !LONG || pcompact || ((RC >> j) & 1ull) || (plong && ((RL >> j) & 1ull));
+#ifdef DSS_JOIN_PROFILE
+                    if (LONG && !(pcompact || ((RC >> j) & 1ull)) && plong && ((RL >> j) & 1ull)) unc |= 1ull << j;
+#endif
                     if (LONG && !k) {  // neither prefix compact, not both long (rare; needs long postings)
                         const uint32_t q = (uint32_t)__float_as_int(s_ra[w][j].z) & ~kQFlags;
                         k = no_smaller_shared<2>(ix, pent, quad_first_cell(ix, d.slot), a.qv.cells + a.qv.offs[q],
@@ -1697,7 +1703,17 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 // pass density, else record-major (one coalesced row per record:
                 // dense batches would scatter too many lane stores).  Both
                 // streams' counts ride one scan (16-bit halves: <= 64 x 64).
+                // long x long pairs are tagged (deduplicated after the join).
+                // (Round 6: sending those kept in a first quad -- exactly their
+                // smallest shared quad -- out untagged cut configs[4]'s tagged
+                // occurrences 203M -> 173M at scale 0.2, but telling a tagged
+                // pair whose smallest shared quad is a first quad needs list
+                // searches per distinct pair: join phase 13.8 -> 69 ms.)
                 const unsigned long long tagm = (LONG && plong) ? (keep & RL) : 0ull;
+#ifdef DSS_JOIN_PROFILE
+                JPROF(20, __popcll(tagm & ~need0));       // long x long kept in a first quad (exact)
+                JPROF(21, __popcll(tagm & unc));          // long x long kept uncertain (neither prefix compact)
+#endif
                 const uint32_t cu = (uint32_t)__popcll(keep & ~tagm), ct = (uint32_t)__popcll(tagm);
                 const uint32_t incl = wave_incl_scan(cu | (ct << 16));
                 const uint32_t tot = (uint32_t)uni32(__builtin_amdgcn_readlane((int)incl, 63));
@@ -1774,12 +1790,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                     }
                 } else {
                     JPROF(16, lane == 0);
-                    const unsigned long long lm = LONG ? __ballot(plong) : 0ull;
                     unsigned long long ou = 0, ot = 0;
                     for (int j = 0; j < nrel; j++) {
                         const unsigned long long kj = __ballot((keep >> j) & 1ull);
                         if (!kj) continue;
-                        const unsigned long long kt = (LONG && ((RL >> j) & 1ull)) ? (kj & lm) : 0ull, ku = kj & ~kt;
+                        // (the lanes that tag record j: tagm, as the counts above)
+                        const unsigned long long kt = LONG ? __ballot((tagm >> j) & 1ull) : 0ull, ku = kj & ~kt;
                         const uint32_t q =
                             (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s_ra[w][j].z)) & ~kQFlags;
                         if ((ku >> lane) & 1ull) {
@@ -2025,6 +2041,9 @@ __global__ void k_tag_emit(const unsigned long long *__restrict__ stage, const i
 // cell_lo > 0 drops the pairs that also share a cell below cell_lo (a
 // two-pointer walk over the two sorted lists' cells below cell_lo; both lists
 // are whole on every shard).
+// On a cell-range shard past the first: the distinct tagged (long x long)
+// pairs sharing a cell below the shard's range are another shard's (exactly
+// once across shards).
 __global__ void k_tag_shard_keep(int64_t n, const uint32_t *__restrict__ q, const uint32_t *__restrict__ e,
                                  QueryView qv, IndexView ix, uint64_t cell_lo, uint8_t *__restrict__ keep)
 {
@@ -2997,7 +3016,8 @@ static const char *const kJProfNames[kJProf] = {
     "lane_tests", "time_fail", "altitude_fail", "owner_fail", "quad_mask_fail", "pass",
     "kept_first_group", "distinct_checks", "distinct_drops", "kept", "staged_batches", "staged_records",
     "loaded_records", "units_with_work", "distinct_wave_iters", "emit_lane_major_batches",
-    "emit_record_major_batches", "emit_lane_major_wave_iters", "batches_without_pairs", "posting_lanes"};
+    "emit_record_major_batches", "emit_lane_major_wave_iters", "batches_without_pairs", "posting_lanes",
+    "long_pairs_kept_first_quad", "long_pairs_kept_uncertain"};
 
 const char *join_profile_name(int i) { return i >= 0 && i < kJProf ? kJProfNames[i] : nullptr; }
 

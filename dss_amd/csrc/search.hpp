@@ -2,14 +2,16 @@
 #pragma once
 #include "common.hpp"
 
-// HBM-resident entity index.  One posting per unique (cell,
-// entity) of the cell range this index serves, sorted by
-//   (slot, duration class, m = min(t0, t1)):
-// a cell's postings are contiguous; within a cell the "regular" postings
-// (entity duration |t1 - t0| <= dcap_thr) come first, sorted by start time m,
-// then the long-duration ones.  A query window [tlo, thi] can only meet a
-// regular posting with m in [tlo - dcap, thi] -- one contiguous range per cell
-// (the band join of search.hip) -- and every long posting of the cell.
+// HBM-resident entity index.  One posting per (entity, group)
+// of the cell range this index serves (a group: a quad or a level-13 cell, by
+// gshift), sorted by
+//   (slot, duration class, altitude band, m = min(t0, t1)):
+// a group's postings are contiguous; within it the "regular" postings (entity
+// duration |t1 - t0| <= dcap_thr) come first -- in one run, or in a dense
+// group in n_bands runs by alt_lo quantile -- each run sorted by start time
+// m, then the long-duration ones.  A query window [tlo, thi] can only meet a
+// regular posting with m in [tlo - dcap, thi] -- one contiguous range per run
+// (the band join of search.hip) -- and every long posting of the group.
 struct dssg_index {
     int64_t n_e = 0;        // entities
     int64_t n_p = 0;        // postings held (unique (cell, entity) in range, ends_at not NULL)

@@ -72,6 +72,32 @@ def test_config_parity_both_grains(oracle, cfg, scale, grain):
     assert np.array_equal(_keys(gq, ge), _keys(oq, oe))
 
 
+# The round-6 index options forced away from their defaults: altitude bands
+# off / 8 bands / bands from 64 postings: identical pair sets to the oracle's.
+@pytest.mark.parametrize("key,value", [("index_bands", 1), ("index_bands", 8), ("band_dense", 64)])
+@pytest.mark.parametrize("cfg,scale", [(2, 0.1), (4, 0.01)])
+def test_join_options_parity(oracle, cfg, scale, key, value):
+    from dss_amd import _lib, geo, workload as W
+    from dss_amd.store import EntityIndex
+    _, q, qa, it, ia, now = W.config(cfg, scale=scale)
+    ci = geo.cover_batch(it.kind, it.voff, it.lat, it.lng, it.radius_m)
+    cq = geo.cover_batch(q.kind, q.voff, q.lat, q.lng, q.radius_m)
+    tlo, thi = W.query_bounds(qa, now)
+    ctx = _lib.context(0)
+    default = {"index_bands": 4, "band_dense": 1024}[key]
+    ctx.set_tuning(key, value)
+    try:
+        idx = EntityIndex(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1)
+        gq, ge = idx.search_operations_batch(cq.offs, cq.cells, qa.alt_lo, qa.alt_hi, qa.t0, qa.t1, now)
+    finally:
+        ctx.set_tuning(key, default)
+    oq, oe = oracle.search(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1, None, cq.offs, cq.cells, qa.alt_lo,
+                           qa.alt_hi, tlo, thi)
+    assert len(oq) > 0
+    assert np.array_equal(_keys(gq, ge), _keys(oq, oe))
+    idx.free()
+
+
 def test_grain_picked_by_footprint_shape():
     """Auto grain: quads for metro footprints (~6 cells, ~2 per quad), cells
     for RID city blocks (~1.4 cells, ~1.2 per quad)."""

@@ -49,6 +49,7 @@ for step in "$@"; do
         cfg=${rest%%:*}
         args=""
         [ "$rest" != "$cfg" ] && args=${rest#*:}
+        args=${args//:/ }  # (several bench args: ARG1:ARG2)
         extra=""
         lim=${BENCH_TIMEOUT:-600}
         if [ $kind = quick ]; then
@@ -64,6 +65,7 @@ for step in "$@"; do
         vs=${r2%%:*}
         args=""
         [ "$r2" != "$vs" ] && args=${r2#*:}
+        args=${args//:/ }
         for v in ${vs//,/ }; do
             if [ "$v" = base ]; then unset DSS_AMD_LIB; else export DSS_AMD_LIB=$GRAFT_REPO_ROOT/dss_amd/variants/$v.so; fi
             timeout -k 10 ${BENCH_TIMEOUT:-300} python -u bench.py --config "$cfg" --steps ${STEPS:-10} --warmup 2 \
