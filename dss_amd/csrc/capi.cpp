@@ -254,12 +254,17 @@ int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value)
         ctx->search.set_join_shape((int)value);
         return DSSG_OK;
     }
+    if (std::string(key) == "record_order") {  // join records: 0 auto (default), 1 query order, 2 key order
+        if (value < 0 || value > 2) return DSSG_ERR_INVALID;
+        ctx->search.set_rec_order((int)value);
+        return DSSG_OK;
+    }
     if (std::string(key) == "index_bands") {  // altitude bands of dense slots (1: none, 2..8; default 4)
         if (value < 1 || value > 8) return DSSG_ERR_INVALID;
         ctx->search.set_bands((int)value, ctx->search.band_dense());
         return DSSG_OK;
     }
-    if (std::string(key) == "band_dense") {  // slot size (postings) from which the bands apply (default 1024)
+    if (std::string(key) == "band_dense") {  // slot size (postings) from which the bands apply (default 4096)
         if (value < 64) return DSSG_ERR_INVALID;
         ctx->search.set_bands(ctx->search.bands(), value);
         return DSSG_OK;

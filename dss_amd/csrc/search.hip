@@ -944,6 +944,7 @@ __global__ __launch_bounds__(kBlock) void k_qrecs(QueryView qv, int64_t nqc, con
     for (int u = 0; u < 4; u++) dst[u] = src[u];
 }
 
+constexpr int64_t kRecPermuteMin = 8192;  // largest group (postings) from which records go in key order
 // The records in key (slot) order: rec2[i] = recs[low word of sval[i]],
 // four threads per 64-B record (16 B each, coalesced writes), over the
 // device key count.  A join unit's records are then one contiguous run that
@@ -1389,6 +1390,7 @@ struct JoinArgs {
     Regions ur;                        // units (k_units)
     OutArgs out;
     uint32_t lazy_sig_recs;            // units with more records prefetch the posting signatures
+    uint32_t rec_indirect;             // records in query order, found through sval (no k_rec_permute)
 };
 
 // One wavefront per unit, lane = posting (the tile stays in registers); the
@@ -1546,7 +1548,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                 int4 h0 = make_int4(0, 0, 0, 0), h1 = h0;
                 ulonglong2 g0 = make_ulonglong2(0, 0), g1 = g0;
                 if (r < x1) {
-                    const int4 *r4 = reinterpret_cast<const int4 *>(recs + r);  // (key order: k_rec_permute)
+                    const int4 *r4 = reinterpret_cast<const int4 *>(recs + (a.rec_indirect ? (uint32_t)sval[r] : r));
                     h0 = r4[0];
                     h1 = r4[1];
                     const long long tlo = ((long long)h0.y << 32) | (uint32_t)h0.x;
@@ -2762,9 +2764,18 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     const int64_t *dnkeys = qo + nq;
     radix_sort_pairs_dn(key, skey, val, sval, nqc, dnkeys, bits_for(idx->n_slots()) + 1, tmp_, s);
     const uint64_t *sq = sval;  // (quantised starts in the high words)
-    QRec *recs_k = (QRec *)rec2_.ensure(sizeof(QRec) * (nqc + 1));
-    hipLaunchKernelGGL(k_rec_permute, dim3(grid_for(4 * nqc, kBlock)), dim3(kBlock), 0, s, dnkeys,
-                       (const uint64_t *)sval, (const QRec *)recs, recs_k);
+    // the records in key order when the index holds groups whose record runs
+    // outgrow L2 (configs[2]'s hotspot quads: k_join 2.22 -> 2.05 ms for a
+    // 0.094-ms permutation); with only moderate groups (configs[1]'s ~3k
+    // postings per quad) the gathers through sval hit L2 and the permutation
+    // would cost more than it saves
+    const bool key_order = rec_order_ == 2 || (rec_order_ == 0 && idx->max_cell_postings >= kRecPermuteMin);
+    QRec *recs_k = recs;
+    if (key_order) {
+        recs_k = (QRec *)rec2_.ensure(sizeof(QRec) * (nqc + 1));
+        hipLaunchKernelGGL(k_rec_permute, dim3(grid_for(4 * nqc, kBlock)), dim3(kBlock), 0, s, dnkeys,
+                           (const uint64_t *)sval, (const QRec *)recs, recs_k);
+    }
     // (5) join units = 64-posting tiles of every cell the batch meets, each
     // with the records it can meet
     if (n_cu_ == 0) {
@@ -2798,6 +2809,7 @@ void SearchEngine::search(const dssg_index *idx, int64_t nq, const int64_t *q_of
     ja.ix = ix;
     ja.qv = qv;
     ja.lazy_sig_recs = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(lazy_sig_recs_, 0xffffffffll));
+    ja.rec_indirect = key_order ? 0u : 1u;
     const bool dense = join_shape_ == 0 ? dense_out_ : join_shape_ == 2;
     const unsigned nblocks = (unsigned)n_cu_ * (dense ? kJoinBpcDense : kJoinBpcSparse);
     if (out_rcap_ == 0) out_rcap_ = ((int64_t)nq * 16 / kRegions / kOutChunk + 2) * kOutChunk;

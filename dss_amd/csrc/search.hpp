@@ -123,6 +123,7 @@ class SearchEngine {
         band_dense_ = dense;
     }
     int bands() const { return bands_; }
+    void set_rec_order(int v) { rec_order_ = v; }
     int64_t band_dense() const { return band_dense_; }
     double last_join_kernel_ms() const { return join_ms_; }
     int64_t last_units() const { return units_; }
@@ -208,7 +209,8 @@ class SearchEngine {
     int join_shape_ = 0;      // 0: by dense_out_; 1: the sparse shape; 2: the dense shape (tests)
     int grain_ = 0;           // 0: auto; 1: cells; 2: quads
     int bands_ = 4;           // altitude bands of dense slots (1: none) -- DESIGN.md s4
-    int64_t band_dense_ = 1024;
+    int rec_order_ = 0;        // join records: 0 auto (key order for indexes with groups >= 8192 postings), 1 query, 2 key
+    int64_t band_dense_ = 4096;  // (1024 banded configs[1]'s ~3k-posting quads: k_join 0.90 -> 1.01 ms)
     double join_ms_ = 0;
     int64_t units_ = 0, keys_ = 0, runs_ = 0, iters_ = 0, tests_ = 0;
     int64_t flushes_ = 0, merges_ = 0, merge_lanes_ = 0, tagged_ = 0, long_queries_ = 0, long_postings_ = 0;

@@ -461,8 +461,12 @@ void dssg_set_timing(dssg_ctx *ctx, int enabled);
  * "index_bands" = altitude bands of the dense posting groups of later builds
  * (1: none, 2..8; default 4: a group's regular postings in alt_lo-quantile
  * runs, so a join tile's altitude hull skips records); "band_dense" = the
- * group size (postings, >= 64) from which the bands apply (default 1024).
- * Results do not depend on either.  Unknown key or value: DSSG_ERR_INVALID. */
+ * group size (postings, >= 64) from which the bands apply (default 4096);
+ * "record_order" = where the join reads its query records (0: picked per
+ * index, the default -- key order when some group holds >= 8192 postings;
+ * 1: query order through the sorted keys; 2: key order, permuted after the
+ * key sort).  Results do not depend on any of them.  Unknown key or value:
+ * DSSG_ERR_INVALID. */
 int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value);
 /* Work counters of the most recent search: query-cell keys (cells of the
  * batch whose cell holds postings), join units (<= 64 records x a posting

@@ -72,11 +72,16 @@ def test_config_parity_both_grains(oracle, cfg, scale, grain):
     assert np.array_equal(_keys(gq, ge), _keys(oq, oe))
 
 
-# The round-6 index options forced away from their defaults: altitude bands
-# off / 8 bands / bands from 64 postings: identical pair sets to the oracle's.
-@pytest.mark.parametrize("key,value", [("index_bands", 1), ("index_bands", 8), ("band_dense", 64)])
+# The round-6 index / join options away from their defaults (4 altitude
+# bands from 4096 postings per group and records in key order from 8192,
+# which the small test airspaces never reach): bands off, 8 bands from 256
+# postings, 4 from 64 and from 1024, records in query or in key order --
+# identical pair sets to the oracle's.
+@pytest.mark.parametrize("opts", [{"index_bands": 1}, {"index_bands": 8, "band_dense": 256}, {"band_dense": 64},
+                                  {"band_dense": 1024}, {"record_order": 1}, {"record_order": 2},
+                                  {"band_dense": 64, "record_order": 2}])
 @pytest.mark.parametrize("cfg,scale", [(2, 0.1), (4, 0.01)])
-def test_join_options_parity(oracle, cfg, scale, key, value):
+def test_join_options_parity(oracle, cfg, scale, opts):
     from dss_amd import _lib, geo, workload as W
     from dss_amd.store import EntityIndex
     _, q, qa, it, ia, now = W.config(cfg, scale=scale)
@@ -84,17 +89,26 @@ def test_join_options_parity(oracle, cfg, scale, key, value):
     cq = geo.cover_batch(q.kind, q.voff, q.lat, q.lng, q.radius_m)
     tlo, thi = W.query_bounds(qa, now)
     ctx = _lib.context(0)
-    default = {"index_bands": 4, "band_dense": 1024}[key]
-    ctx.set_tuning(key, value)
+    defaults = {"index_bands": 4, "band_dense": 4096, "record_order": 0}
     try:
+        for k, v in opts.items():
+            ctx.set_tuning(k, v)
         idx = EntityIndex(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1)
         gq, ge = idx.search_operations_batch(cq.offs, cq.cells, qa.alt_lo, qa.alt_hi, qa.t0, qa.t1, now)
     finally:
-        ctx.set_tuning(key, default)
+        for k in opts:
+            ctx.set_tuning(k, defaults[k])
     oq, oe = oracle.search(ci.offs, ci.cells, ia.alt_lo, ia.alt_hi, ia.t0, ia.t1, None, cq.offs, cq.cells, qa.alt_lo,
                            qa.alt_hi, tlo, thi)
     assert len(oq) > 0
     assert np.array_equal(_keys(gq, ge), _keys(oq, oe))
+    # the per-request small join (<= 4096 queries) over the same index: each
+    # band's m range searched separately
+    k = 300
+    sq, se = idx.search_operations_batch(cq.offs[:k + 1], cq.cells[:int(cq.offs[k])], qa.alt_lo[:k], qa.alt_hi[:k],
+                                         qa.t0[:k], qa.t1[:k], now)
+    sel = oq < k
+    assert np.array_equal(_keys(sq, se), _keys(oq[sel], oe[sel]))
     idx.free()
 
 
