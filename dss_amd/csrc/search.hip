@@ -900,7 +900,10 @@ __global__ void k_qcount(int64_t nq, const uint32_t *perm, const uint32_t *qvali
 // near-prefix signature of its cells below the group (the prefix's decodes
 // loaded 8 at a time).  (Round 5 fused the key emission into this pass and
 // writes records only where a key points: half the cells of a quad-grain
-// batch carry none.)
+// batch carry none.  Round 6: records at their cell index instead -- one
+// coalesced store per block, k_qrecs 0.231 -> 0.215 ms -- left a sparse
+// array whose gathers cost the join more: join phase +0.03 ms on configs[1]
+// and [2], profiles/r06x.)
 __global__ __launch_bounds__(kBlock) void k_qrecs(QueryView qv, int64_t nqc, const uint32_t *cq, const uint32_t *dec,
                                                   const uint32_t *cslot, const uint8_t *qlong, const uint32_t *vpre,
                                                   const uint32_t *qvb, const uint32_t *rank, const uint32_t *okey,
