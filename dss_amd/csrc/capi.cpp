@@ -282,6 +282,10 @@ int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value)
         ctx->route_identity = value != 0;
         return DSSG_OK;
     }
+    if (std::string(key) == "cover_exact_setup") {  // 1: every general-path footprint through the exact setup (tests)
+        ctx->cover.set_all_exact(value != 0);
+        return DSSG_OK;
+    }
     if (std::string(key) == "cover_wave") {  // max batch of the wave-path covering (0: general pipeline only)
         ctx->cover.set_wave_max(value);
         return DSSG_OK;

@@ -13,7 +13,9 @@
 //              (u,v) images, Loop.Area's fan terms (one thread per vertex /
 //              needed triangle)
 //   k_setup    one thread per footprint: origin containment, area sum,
-//              reversal, status/mode, touched-face mask, start cells
+//              reversal, status/mode, touched-face mask, start cells, with
+//              triage predicates; k_setup_exact redoes the few footprints the
+//              triage cannot decide, one wave each, exactly
 //   k_cand_fp / k_cand_exact
 //              direct candidates of the single-face small loops (most
 //              footprints): the cells of their padded bound, tested exactly
@@ -52,6 +54,13 @@ enum : uint8_t { FL_SMALL = 1, FL_PLANAR = 2, FL_FAST = 4 };
 // level >= kFastMinLevel (<= 4 * 4^(13 - L) level-13 candidates).
 constexpr int kFastMinLevel = 10;
 constexpr int kCandStageV = 2048;  // (u,v) vertices a k_cand_fp block stages in LDS (float2: 16 KiB)
+#ifndef DSS_CAND_MODE
+#define DSS_CAND_MODE 1
+#endif
+#ifndef DSS_CAND_ROWS
+#define DSS_CAND_ROWS 512
+#endif
+constexpr int kCandStageR = DSS_CAND_MODE == 0 ? 1 : DSS_CAND_ROWS;   // bound rows whose edge masks a k_cand_fp block keeps in LDS (8 KiB)
 // node meta: level (bits 0-4), orientation (5-6), done (7), face (8-10)
 __device__ __forceinline__ uint32_t pack_meta(int level, int orient, int done, int face)
 {
@@ -352,51 +361,83 @@ __device__ __forceinline__ double fan_area_km2(const double *t, int n, bool &fai
     return (area * DSS_EARTH_AREA_KM2) / 4.0 * DSS_PI;
 }
 
-template <bool FAST>
-__device__ __forceinline__ void origin_of(LoopView &l, bool &fail)
+// The tail both setups share: a small loop inside one face (u,v bound
+// [ulo, uhi] x [vlo, vhi] on face0) gets planar containment unless the bound
+// comes near OriginPoint's projection (see planar_contains), and its start
+// block (as k_start would choose it), if small enough, becomes the direct
+// candidates' frame (FL_FAST).  Returns the flags to OR in.
+__device__ __forceinline__ uint8_t direct_frame(int64_t f, int face0, double ulo, double uhi, double vlo, double vhi,
+                                                uint64_t *st_id, uint32_t *st_i, uint32_t *st_j, uint32_t *finfo,
+                                                uint4 *fbox, bool write)
 {
-    if constexpr (FAST) fastp::loop_init_origin(l, fail);
-    else loop_init_origin(l);
-}
-template <bool FAST>
-__device__ __forceinline__ double area_km2_of(const LoopView &l, bool &fail)
-{
-    if constexpr (FAST) return fastp::loop_area_km2(l, fail);
-    else return loop_area_km2(l);
+    uint8_t fl = 0;
+    bool near_origin = false;
+    if (face0 == xyz_face(origin_point())) {
+        double ou, ov;
+        valid_face_xyz_to_uv(face0, origin_point(), ou, ov);
+        near_origin = ou >= ulo - 1e-6 && ou <= uhi + 1e-6 && ov >= vlo - 1e-6 && ov <= vhi + 1e-6;
+    }
+    if (!near_origin) fl |= FL_PLANAR;
+    const double m = 1e-7;
+    FaceBox b{ulo - m, uhi + m, vlo - m, vhi + m};
+    uint64_t id[4];
+    uint32_t ii[4], jj[4], mt[4];
+    const int k = start_cells(b, face0, id, ii, jj, mt);
+    const int L = meta_level(mt[0]);
+    if (k > 0 && L >= kFastMinLevel) {
+        fl |= FL_FAST;
+        if (!write) return fl;
+        uint32_t info = (uint32_t)L | ((uint32_t)k << 5);
+        for (int q = 0; q < k; q++) {
+            st_id[4 * f + q] = id[q];
+            st_i[4 * f + q] = ii[q];
+            st_j[4 * f + q] = jj[q];
+            info |= (uint32_t)meta_orient(mt[q]) << (8 + 2 * q);
+        }
+        finfo[f] = info;
+        // level-13 (i, j) range of the padded bound: candidates outside it
+        // are > 1e-7 (uv) from every vertex, so neither touch an edge nor
+        // lie inside this single-face loop
+        const int sh13 = kMaxLevel - kCoverLevel;
+        fbox[f] = make_uint4((uint32_t)(st_to_ij(uv_to_st(fmax(b.ulo, -1.0))) >> sh13),
+                             (uint32_t)(st_to_ij(uv_to_st(fmin(b.uhi, 1.0))) >> sh13),
+                             (uint32_t)(st_to_ij(uv_to_st(fmax(b.vlo, -1.0))) >> sh13),
+                             (uint32_t)(st_to_ij(uv_to_st(fmin(b.vhi, 1.0))) >> sh13));
+    }
+    return fl;
 }
 
-// One thread per footprint.  FAST: triage-only predicates (no out-of-line
-// exact arithmetic, so no call-ABI spills); a footprint the triage cannot
-// decide is appended to slow_list and redone by the exact instance, a small
-// grid that strides over that list only.
-template <bool FAST>
+// One thread per footprint, triage-only predicates (no out-of-line exact
+// arithmetic, so no call-ABI spills).  A footprint the triage cannot decide
+// is appended to slow_list and redone by k_setup_exact, which strides over
+// that list only.
 __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsigned int *slow_n, const int32_t *kind,
                                           const int64_t *voff, const double *lat, const double *lng,
-                                          const float *radius_m, const int64_t *xoff, V3 *xyz, int32_t *status,
-                                          double *area_out, uint8_t *mode, uint8_t *origin_in, uint8_t *fmask,
-                                          uint8_t *flags, int32_t *nvx, double2 *uv, uint64_t *st_id, uint32_t *st_i,
-                                          uint32_t *st_j, uint32_t *finfo, uint4 *fbox,
-                                          const double *fwd, const double *rev, const uint8_t *fan_fail,
-                                          const uint8_t *not_inner, const uint8_t *omode, uint8_t *rev_out,
-                                          const uint8_t *bad_in, const CircleFrame *frames)
+                                          const float *radius_m, const int64_t *xoff, const V3 *xyz, int32_t *status, double *area_out,
+                                          uint8_t *mode, uint8_t *origin_in, uint8_t *fmask, uint8_t *flags,
+                                          int32_t *nvx, const double2 *uv, uint64_t *st_id, uint32_t *st_i,
+                                          uint32_t *st_j, uint32_t *finfo, uint4 *fbox, const double *fwd,
+                                          const double *rev, const uint8_t *fan_fail, const uint8_t *not_inner,
+                                          const uint8_t *omode, uint8_t *rev_out, const uint8_t *bad_in,
+                                          const CircleFrame *frames, bool all_exact)
 {
-    bool fail = false;
-    if constexpr (FAST) rev_out[f] = 0;  // (set before any bail: the exact instance reverses in place itself)
+    bool fail = all_exact;  // (a test knob: every footprint through k_setup_exact)
     auto bail = [&]() {
-        if constexpr (FAST) {
-            if (fail) {
-                // redone by the exact instance, launched only when the list
-                // is not empty; until then k_edge_counts sees nothing here
-                slow_list[atomicAdd(slow_n, 1u)] = (uint32_t)f;
-                mode[f] = MODE_NONE;
-                flags[f] = 0;
-            }
+        if (fail) {
+            // redone by k_setup_exact (which sets the reversal flag itself);
+            // until then k_edge_counts sees nothing here
+            slow_list[atomicAdd(slow_n, 1u)] = (uint32_t)f;
+            mode[f] = MODE_NONE;
+            flags[f] = 0;
+            rev_out[f] = 0;
         }
-        return FAST && fail;
+        return fail;
     };
-    int k = kind[f];
-    int64_t v0 = voff[f];
-    V3 *p = xyz + xoff[f];
+    if (bail()) return;
+    rev_out[f] = 0;
+    const int k = kind[f];
+    const int64_t v0 = voff[f];
+    const V3 *p = xyz + xoff[f];
     int st = DSSG_ST_OK;
     uint8_t md = MODE_NONE;
     double area = 0;
@@ -404,120 +445,72 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
     bool small = false;
     LoopView l{p, 0, false};
     if (k == DSSG_KIND_CIRCLE) {
-        double la = lat[v0], ln = lng[v0];
-        float r = radius_m[f];
+        const double la = lat[v0], ln = lng[v0];
+        const float r = radius_m[f];
         if (la > 90.0 || la < -90.0 || ln > 180.0 || ln < -180.0) st = DSSG_ST_BAD_COORD_SET;
         else if (!(r > 0)) st = DSSG_ST_RADIUS;
         else {
-            // regular_loop.go RegularLoop(center, DistanceMetersToAngle(r), 20)
-            double radius = (double)r / DSS_RADIUS_EARTH_M;
-            if constexpr (!FAST) {  // FAST: k_circle_frames + k_verts wrote the vertices
-                V3 c = point_from_degrees(la, ln);
-                V3 c1 = ortho(c), c0 = cross(c1, c);
-                double z = go_cos(radius), rr = go_sin(radius);
-                for (int i = 0; i < 20; i++) {
-                    double px = rr * c_circle_cos[i], py = rr * c_circle_sin[i], pz = z;
-                    V3 q = v3(c0.x * px + c1.x * py + c.x * pz, c0.y * px + c1.y * py + c.y * pz,
-                              c0.z * px + c1.z * py + c.z * pz);
-                    p[i] = normalize(q);
-                }
-            }
+            // regular_loop.go RegularLoop(center, DistanceMetersToAngle(r), 20):
+            // k_circle_frames + k_verts wrote the vertices
+            const double radius = (double)r / DSS_RADIUS_EARTH_M;
             nv = 20;
             l.n = 20;
             // RegularLoop is simple and lies in its cap (centre, radius):
             // OriginPoint clearly outside the cap is outside the loop, which
             // is what initOriginAndBound's crossing walk finds there (the
             // circles' walks were ~0.05 of k_setup's 0.37 ms on configs[2])
-            bool far = false;
-            if constexpr (FAST) {
-                const CircleFrame &F = frames[f];
-                const V3 o = origin_point();
-                far = radius > 1e-7 && radius < 0.5 &&
-                      F.c.x * o.x + F.c.y * o.y + F.c.z * o.z < F.z - 1e-6 * F.rr - 1e-12;  // angle > radius + 1e-6
-            }
+            const CircleFrame &F = frames[f];
+            const V3 o = origin_point();
+            const bool far = radius > 1e-7 && radius < 0.5 &&
+                             F.c.x * o.x + F.c.y * o.y + F.c.z * o.z < F.z - 1e-6 * F.rr - 1e-12;  // angle > radius + 1e-6
             if (far) l.origin_inside = false;
-            else origin_of<FAST>(l, fail);
+            else fastp::loop_init_origin(l, fail);
             if (bail()) return;
             md = MODE_LOOP;
             small = radius < 0.5;
         }
     } else {
         nv = (int)(voff[f + 1] - v0);
-        if (k == DSSG_KIND_POLYGON) {  // Q17: range check precedes the count check
-            // (FAST: flagged per vertex by k_verts) 4 vertices' loads in
-            // flight together; the verdict is the same whichever
-            // out-of-range vertex is seen first
-            bool bad = false;
-            if constexpr (FAST) bad = bad_in[f] != 0;
-            for (int i0 = 0; !FAST && i0 < nv && !bad; i0 += 4) {
-                double la[4], ln[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int i = i0 + u < nv ? i0 + u : nv - 1;
-                    la[u] = lat[v0 + i];
-                    ln[u] = lng[v0 + i];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    bad |= la[u] > 90.0 || la[u] < -90.0 || ln[u] > 180.0 || ln[u] < -180.0;
-            }
-            if (bad) st = DSSG_ST_BAD_COORD_SET;
-        }
+        // Q17: range check (flagged per vertex by k_verts) precedes the count check
+        if (k == DSSG_KIND_POLYGON && bad_in[f]) st = DSSG_ST_BAD_COORD_SET;
         if (st == DSSG_ST_OK && nv < 3) st = DSSG_ST_NOT_ENOUGH_POINTS;
         if (st == DSSG_ST_OK) {
-            if constexpr (!FAST) {  // FAST: k_verts wrote the vertices
-                for (int i = 0; i < nv; i++) p[i] = point_from_degrees(lat[v0 + i], lng[v0 + i]);
-            } else {
-                fail |= fan_fail[f] != 0;
-            }
+            fail |= fan_fail[f] != 0;
             l.n = nv;
-            int om = 2;  // k_orient: which fan terms exist (FAST)
+            const int om = omode[f] & 3;  // k_orient: which fan terms exist
             // a simple loop within 0.05 rad of v0 (k_orient) is inside its
             // cap, so OriginPoint outside the cap is outside the loop once it
             // runs counter-clockwise -- initOriginAndBound's walk finds
             // "outside" there; the walk is skipped for the loop as given
             // (simple ccw) or for its reversal (simple cw)
             bool skip_fwd = false, skip_rev = false;
-            if constexpr (FAST) {
-                om = omode[f] & 3;
-                const int sf = omode[f] >> 2;
-                if (sf) {
-                    const V3 o = origin_point(), q = p[0];
-                    const bool ofar = q.x * o.x + q.y * o.y + q.z * o.z < 0.99875 - 1e-6;
-                    skip_fwd = ofar && (sf & 1);
-                    skip_rev = ofar && (sf & 2);
-                }
+            const int sf = omode[f] >> 2;
+            if (sf) {
+                const V3 o = origin_point(), q = p[0];
+                const bool ofar = q.x * o.x + q.y * o.y + q.z * o.z < 0.99875 - 1e-6;
+                skip_fwd = ofar && (sf & 1);
+                skip_rev = ofar && (sf & 2);
             }
             if (om == 1) {
                 area = INFINITY;  // the forward sum is negative: ~4 pi, above the cap
             } else {
                 if (skip_fwd) l.origin_inside = false;
-                else origin_of<FAST>(l, fail);
-                if constexpr (FAST) area = fan_area_km2(fwd + xoff[f], nv, fail);
-                else area = area_km2_of<FAST>(l, fail);
+                else fastp::loop_init_origin(l, fail);
+                area = fan_area_km2(fwd + xoff[f], nv, fail);
             }
-            if (FAST && om == 0 && area > DSS_MAX_AREA_KM2) fail = true;  // mispredicted: no reversed terms
+            if (om == 0 && area > DSS_MAX_AREA_KM2) fail = true;  // mispredicted: no reversed terms
             if (bail()) return;
-            if (area > DSS_MAX_AREA_KM2) {  // Q4: reverse in place and rebuild
-                if constexpr (FAST) {
-                    // the reversed loop through a reversed view (LoopView.rev):
-                    // later kernels read it through rev_out, and k_reverse_list
-                    // moves only the descent footprints' vertices -- this
-                    // thread's serial walk of them cost 0.16 of k_setup's
-                    // 0.55 ms on configs[2]
-                    l.rev = true;
-                    rev_out[f] = 1;
-                } else {
-                    for (int i = 0, j = nv - 1; i < j; i++, j--) {
-                        V3 t = p[i];
-                        p[i] = p[j];
-                        p[j] = t;
-                    }
-                }
+            if (area > DSS_MAX_AREA_KM2) {
+                // Q4's in-place reversal through a reversed view (LoopView.rev):
+                // later kernels read it through rev_out, and k_reverse_list
+                // moves only the descent footprints' vertices -- this thread's
+                // serial walk of them cost 0.16 of k_setup's 0.55 ms on
+                // configs[2]
+                l.rev = true;
+                rev_out[f] = 1;
                 if (skip_rev) l.origin_inside = false;
-                else origin_of<FAST>(l, fail);
-                if constexpr (FAST) area = fan_area_km2(rev + xoff[f], nv, fail, om == 1);
-                else area = area_km2_of<FAST>(l, fail);
+                else fastp::loop_init_origin(l, fail);
+                area = fan_area_km2(rev + xoff[f], nv, fail, om == 1);
                 if (bail()) return;
             }
             if (area > DSS_MAX_AREA_KM2) st = DSSG_ST_AREA_TOO_LARGE;
@@ -527,20 +520,18 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
     }
     uint8_t mask = 0;
     bool inner = true;
-    bool fast_inner = false;
-    if constexpr (FAST) fast_inner = md == MODE_LOOP && !not_inner[f];
-    if (fast_inner) {  // k_fan: every edge lies inside the face of vertex 0
+    if (md == MODE_LOOP && !not_inner[f]) {  // k_fan: every edge lies inside the face of vertex 0
         mask = (uint8_t)(1u << xyz_face(p[0]));
     } else if (md != MODE_NONE) {
-        int ne = md == MODE_LOOP ? nv : nv - 1;
-        int face0 = xyz_face(p[0]);
+        const int ne = md == MODE_LOOP ? nv : nv - 1;
+        const int face0 = xyz_face(p[0]);
         for (int e = 0; e < ne; e++) {
-            V3 a = p[e], b = p[(e + 1) % nv];
+            const V3 a = p[e], b = p[(e + 1) % nv];
             if (edge_inside_face(a, b, face0)) { mask |= (uint8_t)(1u << face0); continue; }
             inner = false;
             for (int fc = 0; fc < 6; fc++) {
-                double uv[4];
-                if (clip_to_padded_face(a, b, fc, kCoarsePad, uv)) mask |= (uint8_t)(1u << fc);
+                double w[4];
+                if (clip_to_padded_face(a, b, fc, kCoarsePad, w)) mask |= (uint8_t)(1u << fc);
             }
         }
         if (md == MODE_POLYLINE) {
@@ -565,90 +556,236 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
     // in those points' bound (a face corner inside the part included, since
     // the part's boundary then reaches both face edges through it).
     uint8_t fl = (md == MODE_POLYLINE || (md == MODE_LOOP && small)) ? FL_SMALL : 0;
-    // Planar containment (see planar_contains) and direct candidates: a small
-    // loop inside one face whose (u,v) bound does not come near OriginPoint's
-    // projection.
     if (md == MODE_LOOP && small && inner && __builtin_popcount(mask) == 1) {
-        const int face0 = xyz_face(p[0]);
-        double2 *uvp = uv + xoff[f];
+        const double2 *uvp = uv + xoff[f];  // projected by k_fan
         double ulo = 1e300, uhi = -1e300, vlo = 1e300, vhi = -1e300;
 #pragma unroll 4
         for (int i = 0; i < nv; i++) {
-            double u, v;
-            if constexpr (FAST) {  // projected by k_fan
-                const double2 w = uvp[i];
-                u = w.x;
-                v = w.y;
-            } else {
-                valid_face_xyz_to_uv(face0, p[i], u, v);  // = ClipToPaddedFace's same-face fast path
-                uvp[i] = make_double2(u, v);
-            }
-            ulo = fmin(ulo, u); uhi = fmax(uhi, u); vlo = fmin(vlo, v); vhi = fmax(vhi, v);
+            const double2 w = uvp[i];
+            ulo = fmin(ulo, w.x); uhi = fmax(uhi, w.x); vlo = fmin(vlo, w.y); vhi = fmax(vhi, w.y);
         }
-        bool near_origin = false;
-        if (face0 == xyz_face(origin_point())) {
-            double ou, ov;
-            valid_face_xyz_to_uv(face0, origin_point(), ou, ov);
-            near_origin = ou >= ulo - 1e-6 && ou <= uhi + 1e-6 && ov >= vlo - 1e-6 && ov <= vhi + 1e-6;
-        }
-        if (!near_origin) fl |= FL_PLANAR;
-        // start block (as k_start would choose it); small enough -> direct candidates
-        const double m = 1e-7;
-        FaceBox b{ulo - m, uhi + m, vlo - m, vhi + m};
-        uint64_t id[4];
-        uint32_t ii[4], jj[4], mt[4];
-        const int k = start_cells(b, face0, id, ii, jj, mt);
-        const int L = meta_level(mt[0]);
-        if (k > 0 && L >= kFastMinLevel) {
-            fl |= FL_FAST;
-            uint32_t info = (uint32_t)L | ((uint32_t)k << 5);
-            for (int q = 0; q < k; q++) {
-                st_id[4 * f + q] = id[q];
-                st_i[4 * f + q] = ii[q];
-                st_j[4 * f + q] = jj[q];
-                info |= (uint32_t)meta_orient(mt[q]) << (8 + 2 * q);
-            }
-            finfo[f] = info;
-            // level-13 (i, j) range of the padded bound: candidates outside it
-            // are > 1e-7 (uv) from every vertex, so neither touch an edge nor
-            // lie inside this single-face loop
-            const int sh13 = kMaxLevel - kCoverLevel;
-            fbox[f] = make_uint4((uint32_t)(st_to_ij(uv_to_st(fmax(b.ulo, -1.0))) >> sh13),
-                                 (uint32_t)(st_to_ij(uv_to_st(fmin(b.uhi, 1.0))) >> sh13),
-                                 (uint32_t)(st_to_ij(uv_to_st(fmax(b.vlo, -1.0))) >> sh13),
-                                 (uint32_t)(st_to_ij(uv_to_st(fmin(b.vhi, 1.0))) >> sh13));
-        }
+        fl |= direct_frame(f, xyz_face(p[0]), ulo, uhi, vlo, vhi, st_id, st_i, st_j, finfo, fbox, true);
     }
     flags[f] = fl;
     nvx[f] = nv;
 }
 
-template <bool FAST>
 #ifndef DSS_SETUP_WPE
 #define DSS_SETUP_WPE 1
 #endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAST ? DSS_SETUP_WPE : 1))) void k_setup(uint32_t *slow_list, unsigned int *slow_n, int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
-                        const float *radius_m, const int64_t *xoff, V3 *xyz, int32_t *status, double *area_out,
-                        uint8_t *mode, uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx, double2 *uv,
-                        uint64_t *st_id, uint32_t *st_i, uint32_t *st_j, uint32_t *finfo,
-                        uint4 *fbox, const double *fwd, const double *rev, const uint8_t *fan_fail,
-                        const uint8_t *not_inner, const uint8_t *omode, const uint32_t *perm, uint8_t *rev_out,
-                        const uint8_t *bad_in, const CircleFrame *frames)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DSS_SETUP_WPE))) void k_setup(
+    uint32_t *slow_list, unsigned int *slow_n, int64_t n, const int32_t *kind, const int64_t *voff, const double *lat,
+    const double *lng, const float *radius_m, const int64_t *xoff, const V3 *xyz, int32_t *status, double *area_out, uint8_t *mode,
+    uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx, const double2 *uv, uint64_t *st_id,
+    uint32_t *st_i, uint32_t *st_j, uint32_t *finfo, uint4 *fbox, const double *fwd, const double *rev,
+    const uint8_t *fan_fail, const uint8_t *not_inner, const uint8_t *omode, const uint32_t *perm, uint8_t *rev_out,
+    const uint8_t *bad_in, const CircleFrame *frames, int all_exact)
 {
-    int64_t f = tid64();
-    if constexpr (FAST) {
-        if (f >= n) return;
-        f = perm[f];  // polygons first, then circles: waves run one kind's path
-    } else {  // a small grid strides over the footprints the triage left undecided
-        for (int64_t i = f; i < (int64_t)*slow_n; i += (int64_t)gridDim.x * blockDim.x)
-            setup_one<false>(slow_list[i], nullptr, nullptr, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out,
-                             mode, origin_in, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, nullptr,
-                             nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
-        return;
+    const int64_t t = tid64();
+    if (t >= n) return;
+    // polygons first, then circles: waves run one kind's path
+    setup_one(perm[t], slow_list, slow_n, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out, mode, origin_in,
+              fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, fwd, rev, fan_fail, not_inner, omode, rev_out,
+              bad_in, frames, all_exact != 0);
+}
+
+// ---------------------------------------------------------------------------
+// The exact setup of the footprints the triage left undecided, one wave per
+// listed footprint: setup_one's steps with the exact predicates of
+// loopdev.cuh / s2dev.cuh (loop.go as written, no shortcuts), the per-vertex
+// and per-edge loops spread over the lanes.
+//  * Vertices: k_verts' S2 points (the same expressions as PointFromLatLng /
+//    RegularLoop, -ffp-contract=off).
+//  * The origin walk (initOriginAndBound -> bruteForceContainsPoint): each
+//    lane tests its edges with a fresh EdgeCrosser restarted at the edge's
+//    first vertex.  The chain's cached orientation of that vertex is the
+//    same triage sign or its exact resolution, and every branch that reads
+//    an undecided one resolves it the same way, so each edge's verdict is
+//    the chain's; the wave counts the crossings by ballot.
+//  * Area (surfaceIntegralFloat64(SignedArea)): when every vertex lies
+//    within maxLength of v0 the fan origin never moves; the lanes compute
+//    the terms and the wave sums them in index order -- the serial sum, bit
+//    for bit.  Otherwise (and for IsNormalized's bands) the serial code.
+//  * Q4's reversal through the reversed view and rev_out, as k_setup does.
+//  * The face mask: edges over the lanes, bits OR-ed by ballot.
+// One lane's serial exact walk of one footprint cost ~0.09 ms per configs[2]
+// covering (profiles/r05ao), the whole GPU waiting on it.
+__device__ bool wave_loop_contains(const LoopView &l, V3 pt, int lane)
+{
+    int cnt = 0;
+    for (int i0 = 1; i0 <= l.n; i0 += 64) {
+        const int i = i0 + lane;
+        bool x = false;
+        if (i <= l.n) {
+            EdgeCrosser e;
+            e.init(origin_point(), pt);
+            e.restart_at(l.vertex(i - 1));
+            x = e.edge_or_vertex_chain_crossing(l.vertex(i));
+        }
+        cnt += __popcll(__ballot(x));
     }
-    setup_one<true>(f, slow_list, slow_n, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out, mode, origin_in,
-                    fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, fwd, rev, fan_fail, not_inner, omode,
-                    rev_out, bad_in, frames);
+    return l.origin_inside != ((cnt & 1) != 0);
+}
+
+__device__ void wave_init_origin(LoopView &l, int lane)
+{
+    const V3 v0 = l.at(0), v1 = l.at(1), v2 = l.at(2);
+    const bool v1_inside = !eq(v0, v1) && !eq(v2, v1) && angle_contains_vertex(v0, v1, v2);
+    l.origin_inside = false;
+    if (v1_inside != wave_loop_contains(l, v1, lane)) l.origin_inside = true;
+}
+
+// (the rare serial pieces out of line: inlined, they pushed the kernel to
+// 256 VGPRs and scratch)
+__device__ __noinline__ double serial_area_sum(const LoopView l) { return loop_signed_area_sum(l); }
+__device__ __noinline__ bool serial_is_normalized(const LoopView l) { return loop_is_normalized(l); }
+__device__ __noinline__ uint32_t clip_face_mask(V3 a, V3 b)
+{
+    uint32_t m = 0;
+    for (int fc = 0; fc < 6; fc++) {
+        double w4[4];
+        if (clip_to_padded_face(a, b, fc, kCoarsePad, w4)) m |= 1u << fc;
+    }
+    return m;
+}
+
+// loop.go Area, then loopAreaKm2 (Q1)
+__device__ double wave_area_km2(const LoopView &l, int lane)
+{
+    const int n = l.n;
+    const V3 v0 = l.vertex(0);
+    bool moves = false;
+    for (int i = 2 + lane; i < n; i += 64) moves |= angle(l.vertex(i), v0) > DSS_SURFACE_MAX_LENGTH;
+    double area = 0;
+    if (__ballot(moves)) {
+        area = serial_area_sum(l);  // (every lane: the serial walk)
+    } else {
+        for (int i0 = 1; i0 + 1 < n; i0 += 64) {
+            const int i = i0 + lane;
+            const double t = i + 1 < n ? signed_area(v0, l.vertex(i), l.vertex(i + 1)) : 0.0;
+            const int cnt = min(64, n - 1 - i0);
+            for (int u = 0; u < cnt; u++) area += __shfl(t, u);
+        }
+    }
+    const double max_error = turning_angle_max_error(l);
+    if (area < 0) area += 4 * DSS_PI;
+    if (area > 4 * DSS_PI) area = 4 * DSS_PI;
+    if (area < 0) area = 0;
+    if (area < max_error && !serial_is_normalized(l)) area = 4 * DSS_PI;
+    else if (area > (4 * DSS_PI - max_error) && serial_is_normalized(l)) area = 0;
+    return (area * DSS_EARTH_AREA_KM2) / 4.0 * DSS_PI;
+}
+
+__device__ __forceinline__ double wave_min_d(double x)
+{
+    for (int o = 32; o > 0; o >>= 1) x = fmin(x, __shfl_xor(x, o));
+    return x;
+}
+__device__ __forceinline__ double wave_max_d(double x)
+{
+    for (int o = 32; o > 0; o >>= 1) x = fmax(x, __shfl_xor(x, o));
+    return x;
+}
+
+__global__ __launch_bounds__(256) void k_setup_exact(const uint32_t *slow_list, const unsigned int *slow_n,
+                                                     const int32_t *kind, const int64_t *voff, const double *lat,
+                                                     const double *lng, const float *radius_m, const int64_t *xoff,
+                                                     const V3 *xyz, int32_t *status, double *area_out, uint8_t *mode,
+                                                     uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx,
+                                                     const double2 *uv, uint64_t *st_id, uint32_t *st_i,
+                                                     uint32_t *st_j, uint32_t *finfo, uint4 *fbox, uint8_t *rev_out,
+                                                     const uint8_t *bad_in)
+{
+    const int lane = threadIdx.x & 63;
+    const unsigned int ns = *slow_n;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
+    for (int64_t w = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); w < (int64_t)ns; w += nw) {
+        const int64_t f = slow_list[w];
+        const int k = kind[f];
+        const int64_t v0 = voff[f];
+        int st = DSSG_ST_OK;
+        uint8_t md = MODE_NONE;
+        double area = 0;
+        int nv = 0;
+        bool small = false;
+        LoopView l{xyz + xoff[f], 0, false};
+        if (k == DSSG_KIND_CIRCLE) {
+            const double la = lat[v0], ln = lng[v0];
+            const float r = radius_m[f];
+            if (la > 90.0 || la < -90.0 || ln > 180.0 || ln < -180.0) st = DSSG_ST_BAD_COORD_SET;
+            else if (!(r > 0)) st = DSSG_ST_RADIUS;
+            else {
+                nv = l.n = 20;
+                wave_init_origin(l, lane);
+                md = MODE_LOOP;
+                small = (double)r / DSS_RADIUS_EARTH_M < 0.5;
+            }
+        } else {
+            nv = (int)(voff[f + 1] - v0);
+            if (k == DSSG_KIND_POLYGON && bad_in[f]) st = DSSG_ST_BAD_COORD_SET;  // Q17
+            if (st == DSSG_ST_OK && nv < 3) st = DSSG_ST_NOT_ENOUGH_POINTS;
+            if (st == DSSG_ST_OK) {
+                l.n = nv;
+                // (Area does not read the origin: one walk, for the loop as kept)
+                area = wave_area_km2(l, lane);
+                if (area > DSS_MAX_AREA_KM2) {  // Q4
+                    l.rev = true;
+                    area = wave_area_km2(l, lane);
+                }
+                wave_init_origin(l, lane);
+                if (area > DSS_MAX_AREA_KM2) st = DSSG_ST_AREA_TOO_LARGE;
+                else if (area <= 0) md = MODE_POLYLINE;  // Q3
+                else { md = MODE_LOOP; small = true; }
+            }
+        }
+        uint32_t m = 0;
+        bool out = false;
+        if (md != MODE_NONE) {
+            const int ne = md == MODE_LOOP ? nv : nv - 1;
+            const int face0 = xyz_face(l.at(0));
+            for (int e = lane; e < ne; e += 64) {
+                const V3 a = l.at(e), b = l.at(e + 1 < nv ? e + 1 : 0);
+                if (edge_inside_face(a, b, face0)) { m |= 1u << face0; continue; }
+                out = true;
+                m |= clip_face_mask(a, b);
+            }
+            if (md == MODE_POLYLINE)
+                for (int i = lane; i < nv; i += 64)
+                    for (int fc = 0; fc < 6; fc++) {
+                        double u, v;
+                        if (face_xyz_to_uv(fc, l.at(i), u, v) && __builtin_fabs(u) <= 1 + kCoarsePad &&
+                            __builtin_fabs(v) <= 1 + kCoarsePad)
+                            m |= 1u << fc;
+                    }
+        }
+        uint8_t mask = 0;
+        for (int fc = 0; fc < 6; fc++)
+            if (__ballot((m >> fc) & 1u)) mask |= (uint8_t)(1u << fc);
+        const bool inner = __ballot(out) == 0ull;
+        uint8_t fl = (md == MODE_POLYLINE || (md == MODE_LOOP && small)) ? FL_SMALL : 0;
+        if (md == MODE_LOOP && small && inner && __builtin_popcount(mask) == 1) {
+            // (u,v) images on the face of vertex 0 (k_fan's, memory order: the
+            // loop's one face whichever way it runs)
+            const double2 *uvp = uv + xoff[f];
+            double ulo = 1e300, uhi = -1e300, vlo = 1e300, vhi = -1e300;
+            for (int i = lane; i < nv; i += 64) {
+                const double2 w2 = uvp[i];
+                ulo = fmin(ulo, w2.x); uhi = fmax(uhi, w2.x); vlo = fmin(vlo, w2.y); vhi = fmax(vhi, w2.y);
+            }
+            ulo = wave_min_d(ulo); uhi = wave_max_d(uhi); vlo = wave_min_d(vlo); vhi = wave_max_d(vhi);
+            fl |= direct_frame(f, xyz_face(l.at(0)), ulo, uhi, vlo, vhi, st_id, st_i, st_j, finfo, fbox, lane == 0);
+        }
+        if (lane == 0) {
+            status[f] = st;
+            area_out[f] = area;
+            mode[f] = md;
+            origin_in[f] = l.origin_inside ? 1 : 0;
+            fmask[f] = mask;
+            flags[f] = fl;
+            nvx[f] = nv;
+            rev_out[f] = l.rev ? 1 : 0;
+        }
+    }
 }
 
 // Q4's in-place reversal, moved out of k_setup<true> (its serial walk of a
@@ -1284,12 +1421,100 @@ __device__ __forceinline__ int cand_edges_uv(uint32_t i, uint32_t j, const doubl
 // than 1e-6 cannot); then only the marked edges run the exact tests, in the
 // same double arithmetic -- the result is cand_edges_uv's.  NaN end points
 // fail every float comparison, so their edges stay marked.
-__device__ __forceinline__ int cand_edges_uv_f(uint32_t i, uint32_t j, const double2 *upg, bool rev,
-                                               const float2 *upf, int nv, bool planar, bool origin_in)
+constexpr float kSlack = 1e-6f;
+__device__ __forceinline__ double cell_lo_uv(uint32_t i) { return st_to_uv((double)i / (double)kMaxSize); }
+__device__ __forceinline__ double cell_hi_uv(uint32_t i)
+{
+    return st_to_uv((double)(i + (1u << (kMaxLevel - kCoverLevel))) / (double)kMaxSize);
+}
+__device__ __forceinline__ double cell_mid_uv(uint32_t i)
+{
+    return st_to_uv(0.5 / (double)kMaxSize * (2.0 * (double)i + (double)(1u << (kMaxLevel - kCoverLevel))));
+}
+
+// The v half of the prefilter, the same for every cell of a level-13 row j:
+// the edges whose end points are not both beyond the row's padded v range
+// (*nearv) and those not both above or both below its centre line (*strad).
+__device__ __forceinline__ void row_masks(uint32_t j, const float2 *upf, int nv, unsigned long long &nearv,
+                                          unsigned long long &strad)
+{
+    const double pm = kFinePad;
+    const double vlo = cell_lo_uv(j), vhi = cell_hi_uv(j), vc = cell_mid_uv(j);
+    const float rlv = (float)(vlo - pm) - kSlack, rhv = (float)(vhi + pm) + kSlack;
+    const float vcl = (float)vc - kSlack, vch = (float)vc + kSlack;
+    nearv = strad = 0;
+    float2 a = upf[0];
+    for (int e = 0; e < nv; e++) {
+        const float2 b = upf[e + 1 < nv ? e + 1 : 0];
+        const bool far = ((a.y < rlv) & (b.y < rlv)) | ((a.y > rhv) & (b.y > rhv));
+        const bool level = ((a.y > vch) & (b.y > vch)) | ((a.y < vcl) & (b.y < vcl));
+        nearv |= (unsigned long long)!far << e;
+        strad |= (unsigned long long)!level << e;
+        a = b;
+    }
+}
+
+// The u half for the cell at level-30 column i over the row's near edges,
+// then the exact tests of the marked edges.
+__device__ __forceinline__ int cand_edges_rows(uint32_t i, uint32_t j, const double2 *upg, bool rev,
+                                               const float2 *upf, int nv, unsigned long long nearv,
+                                               unsigned long long strad, bool planar, bool origin_in)
 {
     // (the exact tests read the loop from global memory; rev: a loop k_setup
     // reversed without moving it, read mirrored -- the float stage is in
     // loop order already)
+    auto at = [&](int e) { return upg[rev ? nv - 1 - e : e]; };
+    const double pm = kFinePad;
+    const double ulo = cell_lo_uv(i), uhi = cell_hi_uv(i);
+    const float rlu = (float)(ulo - pm) - kSlack, rhu = (float)(uhi + pm) + kSlack;
+    unsigned long long near = 0;
+#if DSS_CAND_MODE == 2
+    float ax = upf[0].x;
+    for (int e = 0; e < nv; e++) {
+        const float bx = upf[e + 1 < nv ? e + 1 : 0].x;
+        const bool far = ((ax < rlu) & (bx < rlu)) | ((ax > rhu) & (bx > rhu));
+        near |= (unsigned long long)!far << e;
+        ax = bx;
+    }
+    near &= nearv;
+#else
+    while (nearv) {
+        const int e = __builtin_ctzll(nearv);
+        nearv &= nearv - 1;
+        const float2 a = upf[e], b = upf[e + 1 < nv ? e + 1 : 0];
+        const bool far = ((a.x < rlu) & (b.x < rlu)) | ((a.x > rhu) & (b.x > rhu));
+        near |= (unsigned long long)!far << e;
+    }
+#endif
+    if (near) {
+        const double vlo = cell_lo_uv(j), vhi = cell_hi_uv(j);
+        do {
+            const int e = __builtin_ctzll(near);
+            near &= near - 1;
+            const double2 x = at(e), y = at(e + 1 < nv ? e + 1 : 0);
+            if (edge_intersects_rect(x.x, x.y, y.x, y.y, ulo - pm, uhi + pm, vlo - pm, vhi + pm)) return 1;
+        } while (near);
+    }
+    if (!planar) return 2;
+    const double uc = cell_mid_uv(i), vc = cell_mid_uv(j);
+    bool par = false;
+    while (strad) {
+        const int e = __builtin_ctzll(strad);
+        strad &= strad - 1;
+        const double2 x = at(e), y = at(e + 1 < nv ? e + 1 : 0);
+        if ((x.y > vc) != (y.y > vc)) {
+            const double d = y.y - x.y;
+            const double lhs = (uc - x.x) * d, rhs = (vc - x.y) * (y.x - x.x);
+            if (d > 0 ? lhs < rhs : lhs > rhs) par = !par;
+        }
+    }
+    return (origin_in != par) ? 1 : 0;
+}
+
+// Both halves per cell (a footprint whose rows did not fit the block's stage).
+__device__ __forceinline__ int cand_edges_uv_f0(uint32_t i, uint32_t j, const double2 *upg, bool rev,
+                                               const float2 *upf, int nv, bool planar, bool origin_in)
+{
     auto at = [&](int e) { return upg[rev ? nv - 1 - e : e]; };
     const uint32_t size = 1u << (kMaxLevel - kCoverLevel);
     const double ulo = st_to_uv((double)i / (double)kMaxSize), uhi = st_to_uv((double)(i + size) / (double)kMaxSize);
@@ -1297,7 +1522,6 @@ __device__ __forceinline__ int cand_edges_uv_f(uint32_t i, uint32_t j, const dou
     const double pm = kFinePad;
     const double half = 0.5 / (double)kMaxSize, sz = (double)size;
     const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
-    constexpr float kSlack = 1e-6f;
     const float rlu = (float)(ulo - pm) - kSlack, rhu = (float)(uhi + pm) + kSlack;
     const float rlv = (float)(vlo - pm) - kSlack, rhv = (float)(vhi + pm) + kSlack;
     const float vcl = (float)vc - kSlack, vch = (float)vc + kSlack;
@@ -1332,13 +1556,23 @@ __device__ __forceinline__ int cand_edges_uv_f(uint32_t i, uint32_t j, const dou
     }
     return (origin_in != par) ? 1 : 0;
 }
+__device__ __forceinline__ int cand_edges_uv_f(uint32_t i, uint32_t j, const double2 *upg, bool rev,
+                                               const float2 *upf, int nv, bool planar, bool origin_in)
+{
+    unsigned long long nearv, strad;
+    row_masks(j, upf, nv, nearv, strad);
+    return cand_edges_rows(i, j, upg, rev, upf, nv, nearv, strad, planar, origin_in);
+}
 
 // One block per kFpPer consecutive footprints: wave 0 loads their bounds,
 // start cells and flags into LDS (one round trip for the block, none per
-// candidate), the block stages their (u,v) vertices, then its threads stride
-// over the block's bound cells (footprint by LDS search, cell by position in
-// its bound) and set key bits in the footprints' LDS masks.  Wave 0 writes the
-// kept masks, and lists the footprints with undecided bits for k_cand_exact.
+// candidate), the block stages their (u,v) vertices, then the edge masks of
+// every row of their bounds (row_masks: the v half of the prefilter, once per
+// row instead of once per cell -- a cell then walks only the edges that
+// reach its row), then its threads stride over the block's bound cells
+// (footprint by LDS search, cell by position in its bound) and set key bits
+// in the footprints' LDS masks.  Wave 0 writes the kept masks, and lists the
+// footprints with undecided bits for k_cand_exact.
 __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *flags, const uint4 *fbox,
                                                       const uint32_t *finfo, const uint32_t *st_i,
                                                       const uint32_t *st_j, const int64_t *xoff, const int32_t *nvx,
@@ -1350,6 +1584,8 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
     __shared__ uint4 s_bx[kFpPer];
     __shared__ uint32_t s_info[kFpPer], s_sti[kFpPer][4], s_stj[kFpPer][4];
     __shared__ int s_cb[kFpPer + 1], s_vb[kFpPer], s_nv[kFpPer], s_fl[kFpPer], s_vp[kFpPer + 1];
+    __shared__ int s_rp[kFpPer + 1], s_rb[kFpPer];
+    __shared__ unsigned long long s_rnear[kCandStageR], s_rstrad[kCandStageR];
     __shared__ int64_t s_xo[kFpPer];
     __shared__ unsigned long long s_km[kFpPer][4], s_um[kFpPer][4];
     __shared__ float2 s_uvf[kCandStageV];  // the block's (u,v) vertices in float (cand_edges_uv_f's prefilter)
@@ -1360,7 +1596,7 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
         // loops are of one kind, so a wave's edge walks are of similar length
         const int64_t f = F0 + t < n ? (int64_t)perm[F0 + t] : n;
         const bool fast = f < n && (flags[f] & FL_FAST);
-        uint32_t cnt = 0, nvv = 0;
+        uint32_t cnt = 0, nvv = 0, rows = 0;
         if (fast) {
             const uint4 bx = fbox[f];
             s_bx[t] = bx;
@@ -1374,19 +1610,25 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
             nvv = (uint32_t)nvx[f];
             s_fl[t] = ((flags[f] & FL_PLANAR) ? 1 : 0) | (origin_in[f] ? 2 : 0) | (rev_flag[f] ? 4 : 0);
             cnt = (bx.y - bx.x + 1) * (bx.w - bx.z + 1);
+            rows = nvv <= 64 ? bx.w - bx.z + 1 : 0;
         }
         s_nv[t] = (int)nvv;
 #pragma unroll
         for (int q = 0; q < 4; q++) s_km[t][q] = s_um[t][q] = 0ull;
-        // candidate and vertex prefixes over the block's footprints (wave scans)
-        uint32_t ci = cnt, vi = nvv;
+        // candidate, vertex and row prefixes over the block's footprints (wave scans)
+        uint32_t ci = cnt, vi = nvv, ri = rows;
         for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t a = (uint32_t)__shfl_up((int)ci, o), b = (uint32_t)__shfl_up((int)vi, o);
+            const uint32_t a = (uint32_t)__shfl_up((int)ci, o), b = (uint32_t)__shfl_up((int)vi, o),
+                           c = (uint32_t)__shfl_up((int)ri, o);
             if (lane >= o) {
                 ci += a;
                 vi += b;
+                ri += c;
             }
         }
+        s_rp[t + 1] = (int)ri;
+        if (t == 0) s_rp[0] = 0;
+        s_rb[t] = ri <= (uint32_t)kCandStageR ? (int)(ri - rows) : -1;  // LDS row offset, or -1: per-cell masks
         s_cb[t + 1] = (int)ci;
         if (t == 0) s_cb[0] = 0;
         s_vb[t] = vi <= (uint32_t)kCandStageV ? (int)(vi - nvv) : -1;  // LDS offset, or -1: read from global
@@ -1411,6 +1653,20 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
         s_uvf[k] = make_float2((float)w.x, (float)w.y);
     }
     __syncthreads();
+    // the edge masks of the bound rows of the staged footprints
+    const int nrs = DSS_CAND_MODE == 0 ? 0 : min(s_rp[kFpPer], kCandStageR);
+    for (int k = t; k < nrs; k += kFpBlock) {
+        int lo = 0, hi = kFpPer;  // s_rp[lo] <= k < s_rp[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_rp[mid] <= k) lo = mid;
+            else hi = mid;
+        }
+        if (s_vb[lo] < 0) continue;  // (its cells read the loop from global memory)
+        const uint32_t j13 = s_bx[lo].z + (uint32_t)(k - s_rp[lo]);
+        row_masks(j13 << (kMaxLevel - kCoverLevel), s_uvf + s_vb[lo], s_nv[lo], s_rnear[k], s_rstrad[k]);
+    }
+    __syncthreads();
     const int total = s_cb[kFpPer];
     for (int k = t; k < total; k += kFpBlock) {
         int lo = 0, hi = kFpPer;  // s_cb[lo] <= k < s_cb[hi]
@@ -1429,12 +1685,18 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
         // (staged vertices are in loop order already; unstaged ones are read
         // through the reversal)
         const double2 *up = uv + s_xo[lo];
-        const int nvf = s_nv[lo];
-        const int v = vb >= 0 && nvf <= 64
-                          ? cand_edges_uv_f(i13 << (kMaxLevel - kCoverLevel), j13 << (kMaxLevel - kCoverLevel), up,
-                                            (fl & 4) != 0, s_uvf + vb, nvf, (fl & 1) != 0, (fl & 2) != 0)
-                          : cand_edges_uv(i13 << (kMaxLevel - kCoverLevel), j13 << (kMaxLevel - kCoverLevel), up, nvf,
-                                          (fl & 1) != 0, (fl & 2) != 0, (fl & 4) != 0);
+        const int nvf = s_nv[lo], rb = s_rb[lo];
+        const uint32_t i30 = i13 << (kMaxLevel - kCoverLevel), j30 = j13 << (kMaxLevel - kCoverLevel);
+        int v;
+        if (DSS_CAND_MODE == 0 && vb >= 0 && nvf <= 64)
+            v = cand_edges_uv_f0(i30, j30, up, (fl & 4) != 0, s_uvf + vb, nvf, (fl & 1) != 0, (fl & 2) != 0);
+        else if (vb >= 0 && nvf <= 64 && rb >= 0)
+            v = cand_edges_rows(i30, j30, up, (fl & 4) != 0, s_uvf + vb, nvf, s_rnear[rb + dj], s_rstrad[rb + dj],
+                                (fl & 1) != 0, (fl & 2) != 0);
+        else if (vb >= 0 && nvf <= 64)
+            v = cand_edges_uv_f(i30, j30, up, (fl & 4) != 0, s_uvf + vb, nvf, (fl & 1) != 0, (fl & 2) != 0);
+        else
+            v = cand_edges_uv(i30, j30, up, nvf, (fl & 1) != 0, (fl & 2) != 0, (fl & 4) != 0);
         if (v == 1) atomicOr(&s_km[lo][key >> 6], 1ull << (key & 63));
         else if (v == 2) atomicOr(&s_um[lo][key >> 6], 1ull << (key & 63));
     }
@@ -1609,16 +1871,6 @@ struct WaveRec {              // a wave-path footprint's kept candidates
     uint32_t pad;
 };
 
-__device__ __forceinline__ double wave_min_d(double x)
-{
-    for (int o = 32; o > 0; o >>= 1) x = fmin(x, __shfl_xor(x, o));
-    return x;
-}
-__device__ __forceinline__ double wave_max_d(double x)
-{
-    for (int o = 32; o > 0; o >>= 1) x = fmax(x, __shfl_xor(x, o));
-    return x;
-}
 
 __global__ __launch_bounds__(64 * kWaveFp) void k_cover_wave(int64_t n, const int32_t *kind, const int64_t *voff,
                                                             const double *lat, const double *lng,
@@ -2177,23 +2429,21 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     hipLaunchKernelGGL(k_fan_area, dim3(std::min<int64_t>(grid_for(2 * nx + 1, B), 2048)), dim3(B), 0, s, toff + n,
                        towner, toff, omode, nv, xoff, xyz, fwd, rev, fan_fail);
     uint8_t *rev_flag = revf_.ensure(n + 1);
-    hipLaunchKernelGGL(k_setup<true>, dim3(grid_for(n, 64)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng,
-                       radius_m, xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo,
-                       fbox, fwd, rev, fan_fail, not_inner, omode, perm, rev_flag, bad, frames);
+    hipLaunchKernelGGL(k_setup, dim3(grid_for(n, 64)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng, radius_m,
+                       xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, fwd,
+                       rev, fan_fail, not_inner, omode, perm, rev_flag, bad, frames, all_exact_ ? 1 : 0);
     int64_t *eoff = eoff_.ensure(n + 1);
     uint32_t *dlist = dlist_.ensure(n + 1);
     int64_t ne = 0;
     unsigned int nd_u = 0, ns_u = 0;
-    // the exact setup of whatever the triage left, launched without reading
-    // the count back (a fixed grid strides over the device list; empty, it
-    // costs ~5 us: profiles/r05ak), then per footprint its clipped-edge items
-    // and the descent list, and one sync for their totals (round 4 read the
-    // counts twice, before and after the exact setup)
-    // (the ~1 footprint per 1M the triage leaves costs ~0.09 ms: one thread's
-    // serial exact path; a 4-block grid measured the same, profiles/r06p)
-    hipLaunchKernelGGL(k_setup<false>, dim3(256), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng, radius_m, xoff,
-                       xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, nullptr,
-                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+    // the exact setup of whatever the triage left (~1 footprint per 1M on
+    // configs[2]), launched without reading the count back: a fixed grid of
+    // waves strides over the device list (empty, it costs one small launch),
+    // then per footprint its clipped-edge items and the descent list, and one
+    // sync for their totals
+    hipLaunchKernelGGL(k_setup_exact, dim3(16), dim3(256), 0, s, slow, slow_n, kind, voff, lat, lng, radius_m, xoff,
+                       xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, rev_flag,
+                       bad);
     hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv, dlist, dlist_n);
     exclusive_scan_i64(nv, eoff, n, tmp_, s, mail + 1);
     mail_counters(dlist_n, slow_n, nullptr, mail + 2, s);

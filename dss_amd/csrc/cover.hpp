@@ -43,12 +43,15 @@ class CoverEngine {
     // force it for every batch)
     void set_wave_max(int64_t n) { wave_ = n > 0; wave_max_ = n; }
     int64_t last_slow() const { return last_slow_; }
+    // (tests) every general-path footprint through the exact setup
+    void set_all_exact(bool on) { all_exact_ = on; }
 
    private:
     void run_general(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
                      const float *radius_m, hipStream_t s, dssg_cells *out);
     void init_tables(hipStream_t s);
     bool wave_ = true;
+    bool all_exact_ = false;
     int64_t wave_max_ = 16384;
     int64_t last_slow_ = 0;
     // wave path: per-footprint outputs, the slow sub-batch, the merged CSR
