@@ -76,14 +76,25 @@ __device__ __forceinline__ int64_t tid64() { return (int64_t)blockIdx.x * blockD
 // (also zeroes the per-footprint flags and the list counters the setup
 // kernels accumulate into: six fill launches fewer per covering)
 __global__ void k_nverts(int64_t n, const int32_t *kind, const int64_t *voff, int64_t *nv, uint8_t *fan_fail,
-                         uint8_t *not_inner, uint8_t *bad, unsigned int *c0, unsigned int *c1, unsigned int *c2)
+                         uint8_t *not_inner, uint8_t *bad, unsigned int *c0, unsigned int *c1, unsigned int *c2,
+                         longlong4 *fbb)
 {
     int64_t f = tid64();
     if (f == 0) *c0 = *c1 = *c2 = 0u;
     if (f >= n) return;
     nv[f] = kind[f] == DSSG_KIND_CIRCLE ? 20 : (voff[f + 1] - voff[f]);
     fan_fail[f] = not_inner[f] = bad[f] = 0;
+    if (fbb) fbb[f] = make_longlong4(LLONG_MAX, LLONG_MIN, LLONG_MAX, LLONG_MIN);  // k_fan's (u,v) bound, empty
 }
+
+// A double as a signed 64-bit key of the same order (non-NaN): k_fan's bound
+// words take atomicMin / atomicMax for a footprint split across waves.
+__device__ __forceinline__ long long ord_key(double x)
+{
+    const long long b = __double_as_longlong(x);
+    return b ^ ((b >> 63) & 0x7fffffffffffffffll);
+}
+__device__ __forceinline__ double ord_val(long long k) { return __longlong_as_double(k ^ ((k >> 63) & 0x7fffffffffffffffll)); }
 
 // cos/sin of the 20 RegularLoop angles i * 2pi/20 (regular_loop.go), computed
 // on the host with the same Go-math restatement (gomath.cuh is host+device).
@@ -190,12 +201,30 @@ __global__ void k_circle_frames(int64_t n, const int32_t *kind, const int64_t *v
     fr[f] = CircleFrame{c, c0, c1, go_cos(radius), go_sin(radius)};
 }
 
-// Owner footprint of every vertex slot.
-__global__ void k_vowner(int64_t n, const int64_t *xoff, uint32_t *vown)
+// Owner footprint of every slot of a CSR layout (offs: n + 1 offsets; perm:
+// the footprint of CSR position t, nullptr for footprint order).
+__global__ void k_vowner(int64_t n, const int64_t *offs, uint32_t *vown, const uint32_t *perm = nullptr)
 {
-    const int64_t f = tid64();
-    if (f >= n) return;
-    for (int64_t x = xoff[f]; x < xoff[f + 1]; x++) vown[x] = (uint32_t)f;
+    const int64_t t = tid64();
+    if (t >= n) return;
+    const uint32_t f = perm ? perm[t] : (uint32_t)t;
+    for (int64_t x = offs[t]; x < offs[t + 1]; x++) vown[x] = f;
+}
+
+// Vertex slots laid out in k_setup's footprint order (polygons, then
+// circles): the per-slot kernels' waves then run one kind's path (k_verts:
+// Cephes sincos for a polygon vertex, a frame product for a circle's), and
+// k_setup's lanes read neighbouring slot ranges.
+__global__ void k_perm_counts(int64_t n, const uint32_t *perm, const int64_t *nv, int64_t *nvp)
+{
+    const int64_t t = tid64();
+    if (t < n) nvp[t] = nv[perm[t]];
+}
+__global__ void k_perm_offsets(int64_t n, const uint32_t *perm, const int64_t *xoffp, int64_t *xoff)
+{
+    const int64_t t = tid64();
+    if (t < n) xoff[perm[t]] = xoffp[t];
+    if (t == 0) xoff[n] = xoffp[n];
 }
 
 // One thread per vertex slot: S2 point of a polygon vertex
@@ -228,21 +257,60 @@ __global__ void k_verts(int64_t nx, const uint32_t *vown, const int32_t *kind, c
 // for single-face small loops) and whether edge (i, i+1) lies inside that
 // face (any edge that does not clears the footprint's inner flag:
 // not_inner[f] = 1).
+// fbb (when given): each footprint's (u,v) bound over its slots (the fmin /
+// fmax k_setup's planar branch takes), reduced over the wave's lanes of one
+// footprint (slots are contiguous) by the first of them: stored when the
+// footprint lies in the wave, atomicMin / atomicMax of order keys when it
+// straddles waves.  min / max are exact, so the bound is the serial one's.
 __global__ void k_fan(int64_t nx, const uint32_t *vown, const int64_t *nslots, const int64_t *xoff, const V3 *xyz,
-                      double2 *uv, uint8_t *not_inner)
+                      double2 *uv, uint8_t *not_inner, longlong4 *fbb)
 {
     const int64_t x = tid64();
-    if (x >= nx) return;
-    const uint32_t f = vown[x];
-    const int n = (int)nslots[f];
-    const int i = (int)(x - xoff[f]);
-    if (n < 3) return;
-    const V3 *p = xyz + xoff[f];
-    const int face0 = xyz_face(p[0]);
-    double u, v;
-    valid_face_xyz_to_uv(face0, p[i], u, v);  // = ClipToPaddedFace's same-face fast path
-    uv[x] = make_double2(u, v);
-    if (!edge_inside_face(p[i], p[i + 1 == n ? 0 : i + 1], face0)) not_inner[f] = 1;
+    const int lane = (int)(threadIdx.x & 63);
+    uint32_t f = 0xffffffffu;
+    int n = 0, i = 0;
+    int64_t x0 = 0;
+    if (x < nx) {
+        f = vown[x];
+        n = (int)nslots[f];
+        x0 = xoff[f];
+        i = (int)(x - x0);
+    }
+    const bool ok = x < nx && n >= 3;
+    double u = 0, v = 0;
+    if (ok) {
+        const V3 *p = xyz + x0;
+        const int face0 = xyz_face(p[0]);
+        valid_face_xyz_to_uv(face0, p[i], u, v);  // = ClipToPaddedFace's same-face fast path
+        uv[x] = make_double2(u, v);
+        if (!edge_inside_face(p[i], p[i + 1 == n ? 0 : i + 1], face0)) not_inner[f] = 1;
+    }
+    if (!fbb) return;  // (uniform)
+    if (!ok) f = 0xffffffffu;
+    double ulo = ok ? u : INFINITY, uhi = ok ? u : -INFINITY, vlo = ok ? v : INFINITY, vhi = ok ? v : -INFINITY;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t fo = (uint32_t)__shfl_down((int)f, o);
+        const double a = __shfl_down(ulo, o), b = __shfl_down(uhi, o), c = __shfl_down(vlo, o), d = __shfl_down(vhi, o);
+        if (lane + o < 64 && fo == f) {
+            ulo = fmin(ulo, a);
+            uhi = fmax(uhi, b);
+            vlo = fmin(vlo, c);
+            vhi = fmax(vhi, d);
+        }
+    }
+    const uint32_t fp = (uint32_t)__shfl_up((int)f, 1);
+    if (!ok || (lane > 0 && fp == f)) return;
+    // the head of this wave's run of the footprint's slots
+    if (i == 0 && ((x0 + n - 1) >> 6) == (x >> 6)) {
+        fbb[f] = make_longlong4(ord_key(ulo), ord_key(uhi), ord_key(vlo), ord_key(vhi));
+    } else {
+        long long *w = reinterpret_cast<long long *>(fbb + f);
+        atomicMin(w, ord_key(ulo));
+        atomicMax(w + 1, ord_key(uhi));
+        atomicMin(w + 2, ord_key(vlo));
+        atomicMax(w + 3, ord_key(vhi));
+    }
 }
 
 // Fan-term orientation of a non-circle loop (n >= 3 vertices).  loop.go Area
@@ -419,7 +487,7 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
                                           uint32_t *st_j, uint32_t *finfo, uint4 *fbox, const double *fwd,
                                           const double *rev, const uint8_t *fan_fail, const uint8_t *not_inner,
                                           const uint8_t *omode, uint8_t *rev_out, const uint8_t *bad_in,
-                                          const CircleFrame *frames, bool all_exact)
+                                          const CircleFrame *frames, const longlong4 *fbb, bool all_exact)
 {
     bool fail = all_exact;  // (a test knob: every footprint through k_setup_exact)
     auto bail = [&]() {
@@ -557,12 +625,17 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
     // the part's boundary then reaches both face edges through it).
     uint8_t fl = (md == MODE_POLYLINE || (md == MODE_LOOP && small)) ? FL_SMALL : 0;
     if (md == MODE_LOOP && small && inner && __builtin_popcount(mask) == 1) {
-        const double2 *uvp = uv + xoff[f];  // projected by k_fan
         double ulo = 1e300, uhi = -1e300, vlo = 1e300, vhi = -1e300;
+        if (fbb) {  // reduced by k_fan
+            const longlong4 b = fbb[f];
+            ulo = ord_val(b.x); uhi = ord_val(b.y); vlo = ord_val(b.z); vhi = ord_val(b.w);
+        } else {
+            const double2 *uvp = uv + xoff[f];  // projected by k_fan
 #pragma unroll 4
-        for (int i = 0; i < nv; i++) {
-            const double2 w = uvp[i];
-            ulo = fmin(ulo, w.x); uhi = fmax(uhi, w.x); vlo = fmin(vlo, w.y); vhi = fmax(vhi, w.y);
+            for (int i = 0; i < nv; i++) {
+                const double2 w = uvp[i];
+                ulo = fmin(ulo, w.x); uhi = fmax(uhi, w.x); vlo = fmin(vlo, w.y); vhi = fmax(vhi, w.y);
+            }
         }
         fl |= direct_frame(f, xyz_face(p[0]), ulo, uhi, vlo, vhi, st_id, st_i, st_j, finfo, fbox, true);
     }
@@ -579,14 +652,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DSS_SETUP_WP
     uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx, const double2 *uv, uint64_t *st_id,
     uint32_t *st_i, uint32_t *st_j, uint32_t *finfo, uint4 *fbox, const double *fwd, const double *rev,
     const uint8_t *fan_fail, const uint8_t *not_inner, const uint8_t *omode, const uint32_t *perm, uint8_t *rev_out,
-    const uint8_t *bad_in, const CircleFrame *frames, int all_exact)
+    const uint8_t *bad_in, const CircleFrame *frames, const longlong4 *fbb, int all_exact)
 {
     const int64_t t = tid64();
     if (t >= n) return;
     // polygons first, then circles: waves run one kind's path
     setup_one(perm[t], slow_list, slow_n, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out, mode, origin_in,
               fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, fwd, rev, fan_fail, not_inner, omode, rev_out,
-              bad_in, frames, all_exact != 0);
+              bad_in, frames, fbb, all_exact != 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -726,13 +799,15 @@ __global__ __launch_bounds__(256) void k_setup_exact(const uint32_t *slow_list, 
             if (st == DSSG_ST_OK && nv < 3) st = DSSG_ST_NOT_ENOUGH_POINTS;
             if (st == DSSG_ST_OK) {
                 l.n = nv;
-                // (Area does not read the origin: one walk, for the loop as kept)
+                // (the origin first, as the loop's construction runs it: Area's
+                // IsNormalized bands read it through the pole containment)
+                wave_init_origin(l, lane);
                 area = wave_area_km2(l, lane);
                 if (area > DSS_MAX_AREA_KM2) {  // Q4
                     l.rev = true;
+                    wave_init_origin(l, lane);
                     area = wave_area_km2(l, lane);
                 }
-                wave_init_origin(l, lane);
                 if (area > DSS_MAX_AREA_KM2) st = DSSG_ST_AREA_TOO_LARGE;
                 else if (area <= 0) md = MODE_POLYLINE;  // Q3
                 else { md = MODE_LOOP; small = true; }
@@ -2388,12 +2463,24 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     }
     uint8_t *fan_fail = fanf_.ensure(n + 1), *not_inner = ninner_.ensure(n + 1), *bad = badv_.ensure(n + 1);
     unsigned int *slow_n = slow_n_.ensure(1), *dlist_n = dlist_n_.ensure(1), *ulist_n = ulist_n_.ensure(1);
+    longlong4 *fbb = fan_bbox_ ? (longlong4 *)fbb_.ensure(4 * (n + 1)) : nullptr;
     hipLaunchKernelGGL(k_nverts, dim3(grid_for(n, B)), dim3(B), 0, s, n, kind, voff, nv, fan_fail, not_inner, bad,
-                       slow_n, dlist_n, ulist_n);
+                       slow_n, dlist_n, ulist_n, fbb);
     int64_t *mail = mailbox();  // [0] vertices [1] edge items [2] descent [3] exact setups [4] start nodes
                                 // [5] next frontier [6] open [7] cells
     volatile const int64_t *mh = mail_h_;
-    exclusive_scan_i64(nv, xoff, n, tmp_, s, mail + 0);
+    uint32_t *perm = perm_.ensure(n + 1);
+    partition_polygons_first(kind, perm, fcnt_.ensure(n + 2), n, tmp_, tmp2_, s);
+    int64_t *xoffp = xoff;
+    if (slot_order_) {
+        int64_t *nvp = nvp_.ensure(n + 1);
+        xoffp = xoffp_.ensure(n + 1);
+        hipLaunchKernelGGL(k_perm_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, perm, nv, nvp);
+        exclusive_scan_i64(nvp, xoffp, n, tmp_, s, mail + 0);
+        hipLaunchKernelGGL(k_perm_offsets, dim3(grid_for(n, B)), dim3(B), 0, s, n, perm, xoffp, xoff);
+    } else {
+        exclusive_scan_i64(nv, xoff, n, tmp_, s, mail + 0);
+    }
     DSS_HIP(hipStreamSynchronize(s));
     const int64_t nx = mh[0];
     V3 *xyz = (V3 *)xyz_.ensure((size_t)nx * 3 + 3);
@@ -2405,33 +2492,31 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     CircleFrame *frames = (CircleFrame *)frames_.ensure(sizeof(CircleFrame) * (n + 1));
     uint32_t *vown = vown_.ensure(nx + 1);
     double *fwd = fwd_.ensure(nx + 1), *rev = rev_.ensure(nx + 1);
-    uint32_t *perm = perm_.ensure(n + 1);
     uint8_t *omode = omode_.ensure(n + 1);
     int64_t *tcnt = tcnt_.ensure(n + 1), *toff = toff_.ensure(n + 2);
     uint32_t *towner = towner_.ensure(2 * nx + 1);  // <= 2 (n - 2) tasks per loop
-    partition_polygons_first(kind, perm, fcnt_.ensure(n + 2), n, tmp_, tmp2_, s);
     // per-vertex pre-pass: frames, owners, S2 points, fan terms
     hipLaunchKernelGGL(k_circle_frames, dim3(grid_for(n, B)), dim3(B), 0, s, n, kind, voff, lat, lng, radius_m, frames);
-    hipLaunchKernelGGL(k_vowner, dim3(grid_for(n, B)), dim3(B), 0, s, n, xoff, vown);
+    hipLaunchKernelGGL(k_vowner, dim3(grid_for(n, B)), dim3(B), 0, s, n, xoffp, vown, slot_order_ ? perm : nullptr);
     if (nx > 0) {
         hipLaunchKernelGGL(k_verts, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, kind, voff, lat, lng, xoff, frames, xyz,
                            bad);
         // (k_fan fused into k_verts -- neighbours by shuffle, recomputed across
         // wave edges -- measured slower: 0.355 against 0.317 ms, r05v)
-        hipLaunchKernelGGL(k_fan, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, nv, xoff, xyz, uv, not_inner);
+        hipLaunchKernelGGL(k_fan, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, nv, xoff, xyz, uv, not_inner, fbb);
     }
     // fan triangle terms of Loop.Area: orientation first, then one thread per
     // triangle actually needed (no lanes idle on circles or on the orientation
     // that is never summed)
     hipLaunchKernelGGL(k_orient, dim3(grid_for(n, B)), dim3(B), 0, s, n, kind, nv, xoff, xyz, omode, tcnt);
     exclusive_scan_i64(tcnt, toff, n, tmp_, s);
-    hipLaunchKernelGGL(k_vowner, dim3(grid_for(n, B)), dim3(B), 0, s, n, toff, towner);
+    hipLaunchKernelGGL(k_vowner, dim3(grid_for(n, B)), dim3(B), 0, s, n, toff, towner, nullptr);
     hipLaunchKernelGGL(k_fan_area, dim3(std::min<int64_t>(grid_for(2 * nx + 1, B), 2048)), dim3(B), 0, s, toff + n,
                        towner, toff, omode, nv, xoff, xyz, fwd, rev, fan_fail);
     uint8_t *rev_flag = revf_.ensure(n + 1);
     hipLaunchKernelGGL(k_setup, dim3(grid_for(n, 64)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng, radius_m,
                        xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, fwd,
-                       rev, fan_fail, not_inner, omode, perm, rev_flag, bad, frames, all_exact_ ? 1 : 0);
+                       rev, fan_fail, not_inner, omode, perm, rev_flag, bad, frames, fbb, all_exact_ ? 1 : 0);
     int64_t *eoff = eoff_.ensure(n + 1);
     uint32_t *dlist = dlist_.ensure(n + 1);
     int64_t ne = 0;
@@ -2471,7 +2556,7 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     uint8_t *cflags = cflags_.ensure(ne + 1);
     if (ne > 0) {
         uint32_t *eown = eown_.ensure(ne + 1);
-        hipLaunchKernelGGL(k_vowner, dim3(grid_for(n, B)), dim3(B), 0, s, n, eoff, eown);
+        hipLaunchKernelGGL(k_vowner, dim3(grid_for(n, B)), dim3(B), 0, s, n, eoff, eown, nullptr);
         hipLaunchKernelGGL(k_clip_items, dim3(grid_for(ne, B)), dim3(B), 0, s, ne, eown, xoff, xyz, mode, fmask, nvx, eoff,
                            clip_f, clip_c, cflags);
     }

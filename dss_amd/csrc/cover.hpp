@@ -45,6 +45,10 @@ class CoverEngine {
     int64_t last_slow() const { return last_slow_; }
     // (tests) every general-path footprint through the exact setup
     void set_all_exact(bool on) { all_exact_ = on; }
+    // vertex slots in k_setup's footprint order (default) or in footprint order
+    void set_slot_order(bool kind_major) { slot_order_ = kind_major; }
+    // each footprint's (u,v) bound reduced by k_fan (default) or summed by k_setup
+    void set_fan_bbox(bool on) { fan_bbox_ = on; }
 
    private:
     void run_general(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
@@ -52,6 +56,15 @@ class CoverEngine {
     void init_tables(hipStream_t s);
     bool wave_ = true;
     bool all_exact_ = false;
+#ifndef DSS_SLOT_ORDER
+#define DSS_SLOT_ORDER 0
+#endif
+#ifndef DSS_FAN_BBOX
+#define DSS_FAN_BBOX 0
+#endif
+    bool slot_order_ = DSS_SLOT_ORDER != 0;
+    bool fan_bbox_ = DSS_FAN_BBOX != 0;
+    DevBuf<long long> fbb_;
     int64_t wave_max_ = 16384;
     int64_t last_slow_ = 0;
     // wave path: per-footprint outputs, the slow sub-batch, the merged CSR
@@ -71,7 +84,7 @@ class CoverEngine {
     int64_t *mailbox();
     hipEvent_t h_ev_ = nullptr;                   // the last upload from h_offs_
     std::vector<uint8_t> h_slow_;
-    DevBuf<int64_t> cnt_, xoff_, eoff_, soff_, offs_, ncnt_, npos_, fc64_;
+    DevBuf<int64_t> cnt_, xoff_, eoff_, soff_, offs_, ncnt_, npos_, fc64_, nvp_, xoffp_;
     DevBuf<int32_t> status_, nvx_;
     DevBuf<double> area_, xyz_;
     DevBuf<uint8_t> mode_, orig_, fmask_, flags_, cflags_, act_;
