@@ -282,14 +282,6 @@ int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value)
         ctx->route_identity = value != 0;
         return DSSG_OK;
     }
-    if (std::string(key) == "radix_onesweep") {  // the packed radix sort: 1 decoupled look-back (default), 0 per-pass histograms
-        dss::set_radix_onesweep(value != 0);
-        return DSSG_OK;
-    }
-    if (std::string(key) == "cover_fan_bbox") {  // 1: k_fan reduces each footprint's (u,v) bound (default), 0: k_setup
-        ctx->cover.set_fan_bbox(value != 0);
-        return DSSG_OK;
-    }
     if (std::string(key) == "cover_slot_order") {  // 1: vertex slots polygons first (default), 0: footprint order
         ctx->cover.set_slot_order(value != 0);
         return DSSG_OK;

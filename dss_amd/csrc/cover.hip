@@ -54,13 +54,6 @@ enum : uint8_t { FL_SMALL = 1, FL_PLANAR = 2, FL_FAST = 4 };
 // level >= kFastMinLevel (<= 4 * 4^(13 - L) level-13 candidates).
 constexpr int kFastMinLevel = 10;
 constexpr int kCandStageV = 2048;  // (u,v) vertices a k_cand_fp block stages in LDS (float2: 16 KiB)
-#ifndef DSS_CAND_MODE
-#define DSS_CAND_MODE 1
-#endif
-#ifndef DSS_CAND_ROWS
-#define DSS_CAND_ROWS 512
-#endif
-constexpr int kCandStageR = DSS_CAND_MODE == 0 ? 1 : DSS_CAND_ROWS;   // bound rows whose edge masks a k_cand_fp block keeps in LDS (8 KiB)
 // node meta: level (bits 0-4), orientation (5-6), done (7), face (8-10)
 __device__ __forceinline__ uint32_t pack_meta(int level, int orient, int done, int face)
 {
@@ -76,25 +69,14 @@ __device__ __forceinline__ int64_t tid64() { return (int64_t)blockIdx.x * blockD
 // (also zeroes the per-footprint flags and the list counters the setup
 // kernels accumulate into: six fill launches fewer per covering)
 __global__ void k_nverts(int64_t n, const int32_t *kind, const int64_t *voff, int64_t *nv, uint8_t *fan_fail,
-                         uint8_t *not_inner, uint8_t *bad, unsigned int *c0, unsigned int *c1, unsigned int *c2,
-                         longlong4 *fbb)
+                         uint8_t *not_inner, uint8_t *bad, unsigned int *c0, unsigned int *c1, unsigned int *c2)
 {
     int64_t f = tid64();
     if (f == 0) *c0 = *c1 = *c2 = 0u;
     if (f >= n) return;
     nv[f] = kind[f] == DSSG_KIND_CIRCLE ? 20 : (voff[f + 1] - voff[f]);
     fan_fail[f] = not_inner[f] = bad[f] = 0;
-    if (fbb) fbb[f] = make_longlong4(LLONG_MAX, LLONG_MIN, LLONG_MAX, LLONG_MIN);  // k_fan's (u,v) bound, empty
 }
-
-// A double as a signed 64-bit key of the same order (non-NaN): k_fan's bound
-// words take atomicMin / atomicMax for a footprint split across waves.
-__device__ __forceinline__ long long ord_key(double x)
-{
-    const long long b = __double_as_longlong(x);
-    return b ^ ((b >> 63) & 0x7fffffffffffffffll);
-}
-__device__ __forceinline__ double ord_val(long long k) { return __longlong_as_double(k ^ ((k >> 63) & 0x7fffffffffffffffll)); }
 
 // cos/sin of the 20 RegularLoop angles i * 2pi/20 (regular_loop.go), computed
 // on the host with the same Go-math restatement (gomath.cuh is host+device).
@@ -257,60 +239,21 @@ __global__ void k_verts(int64_t nx, const uint32_t *vown, const int32_t *kind, c
 // for single-face small loops) and whether edge (i, i+1) lies inside that
 // face (any edge that does not clears the footprint's inner flag:
 // not_inner[f] = 1).
-// fbb (when given): each footprint's (u,v) bound over its slots (the fmin /
-// fmax k_setup's planar branch takes), reduced over the wave's lanes of one
-// footprint (slots are contiguous) by the first of them: stored when the
-// footprint lies in the wave, atomicMin / atomicMax of order keys when it
-// straddles waves.  min / max are exact, so the bound is the serial one's.
 __global__ void k_fan(int64_t nx, const uint32_t *vown, const int64_t *nslots, const int64_t *xoff, const V3 *xyz,
-                      double2 *uv, uint8_t *not_inner, longlong4 *fbb)
+                      double2 *uv, uint8_t *not_inner)
 {
     const int64_t x = tid64();
-    const int lane = (int)(threadIdx.x & 63);
-    uint32_t f = 0xffffffffu;
-    int n = 0, i = 0;
-    int64_t x0 = 0;
-    if (x < nx) {
-        f = vown[x];
-        n = (int)nslots[f];
-        x0 = xoff[f];
-        i = (int)(x - x0);
-    }
-    const bool ok = x < nx && n >= 3;
-    double u = 0, v = 0;
-    if (ok) {
-        const V3 *p = xyz + x0;
-        const int face0 = xyz_face(p[0]);
-        valid_face_xyz_to_uv(face0, p[i], u, v);  // = ClipToPaddedFace's same-face fast path
-        uv[x] = make_double2(u, v);
-        if (!edge_inside_face(p[i], p[i + 1 == n ? 0 : i + 1], face0)) not_inner[f] = 1;
-    }
-    if (!fbb) return;  // (uniform)
-    if (!ok) f = 0xffffffffu;
-    double ulo = ok ? u : INFINITY, uhi = ok ? u : -INFINITY, vlo = ok ? v : INFINITY, vhi = ok ? v : -INFINITY;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t fo = (uint32_t)__shfl_down((int)f, o);
-        const double a = __shfl_down(ulo, o), b = __shfl_down(uhi, o), c = __shfl_down(vlo, o), d = __shfl_down(vhi, o);
-        if (lane + o < 64 && fo == f) {
-            ulo = fmin(ulo, a);
-            uhi = fmax(uhi, b);
-            vlo = fmin(vlo, c);
-            vhi = fmax(vhi, d);
-        }
-    }
-    const uint32_t fp = (uint32_t)__shfl_up((int)f, 1);
-    if (!ok || (lane > 0 && fp == f)) return;
-    // the head of this wave's run of the footprint's slots
-    if (i == 0 && ((x0 + n - 1) >> 6) == (x >> 6)) {
-        fbb[f] = make_longlong4(ord_key(ulo), ord_key(uhi), ord_key(vlo), ord_key(vhi));
-    } else {
-        long long *w = reinterpret_cast<long long *>(fbb + f);
-        atomicMin(w, ord_key(ulo));
-        atomicMax(w + 1, ord_key(uhi));
-        atomicMin(w + 2, ord_key(vlo));
-        atomicMax(w + 3, ord_key(vhi));
-    }
+    if (x >= nx) return;
+    const uint32_t f = vown[x];
+    const int n = (int)nslots[f];
+    const int i = (int)(x - xoff[f]);
+    if (n < 3) return;
+    const V3 *p = xyz + xoff[f];
+    const int face0 = xyz_face(p[0]);
+    double u, v;
+    valid_face_xyz_to_uv(face0, p[i], u, v);  // = ClipToPaddedFace's same-face fast path
+    uv[x] = make_double2(u, v);
+    if (!edge_inside_face(p[i], p[i + 1 == n ? 0 : i + 1], face0)) not_inner[f] = 1;
 }
 
 // Fan-term orientation of a non-circle loop (n >= 3 vertices).  loop.go Area
@@ -402,20 +345,25 @@ __global__ void k_fan_area(const int64_t *toff_end, const uint32_t *towner, cons
     }
 }
 
+#ifndef DSS_SETUP_BATCH
+#define DSS_SETUP_BATCH 4
+#endif
+constexpr int kSetupBatch = DSS_SETUP_BATCH;  // k_setup's per-footprint loads in flight (fan terms, (u,v) bound)
+
 // loop.go Area from the precomputed fan terms (same summation order as
 // surfaceIntegralFloat64), then loopAreaKm2.  Fails over to the exact path
 // in the bands where Area consults IsNormalized.
 __device__ __forceinline__ double fan_area_km2(const double *t, int n, bool &fail, bool rev_only = false)
 {
-    // terms loaded 4 at a time, summed in index order (the order of
+    // terms loaded kSetupBatch at a time, summed in index order (the order of
     // surfaceIntegralFloat64, so the sum is bit-identical)
     double area = 0;
-    for (int i0 = 1; i0 + 1 < n; i0 += 4) {
-        double x[4];
+    for (int i0 = 1; i0 + 1 < n; i0 += kSetupBatch) {
+        double x[kSetupBatch];
 #pragma unroll
-        for (int u = 0; u < 4; u++) x[u] = t[i0 + u + 1 < n ? i0 + u : i0];
+        for (int u = 0; u < kSetupBatch; u++) x[u] = t[i0 + u + 1 < n ? i0 + u : i0];
 #pragma unroll
-        for (int u = 0; u < 4; u++)
+        for (int u = 0; u < kSetupBatch; u++)
             if (i0 + u + 1 < n) area += x[u];
     }
     const double max_error = DSS_TURN_ANGLE_ERR_PER_VERTEX * (double)n;
@@ -487,7 +435,7 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
                                           uint32_t *st_j, uint32_t *finfo, uint4 *fbox, const double *fwd,
                                           const double *rev, const uint8_t *fan_fail, const uint8_t *not_inner,
                                           const uint8_t *omode, uint8_t *rev_out, const uint8_t *bad_in,
-                                          const CircleFrame *frames, const longlong4 *fbb, bool all_exact)
+                                          const CircleFrame *frames, bool all_exact)
 {
     bool fail = all_exact;  // (a test knob: every footprint through k_setup_exact)
     auto bail = [&]() {
@@ -625,16 +573,15 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
     // the part's boundary then reaches both face edges through it).
     uint8_t fl = (md == MODE_POLYLINE || (md == MODE_LOOP && small)) ? FL_SMALL : 0;
     if (md == MODE_LOOP && small && inner && __builtin_popcount(mask) == 1) {
+        const double2 *uvp = uv + xoff[f];  // projected by k_fan
         double ulo = 1e300, uhi = -1e300, vlo = 1e300, vhi = -1e300;
-        if (fbb) {  // reduced by k_fan
-            const longlong4 b = fbb[f];
-            ulo = ord_val(b.x); uhi = ord_val(b.y); vlo = ord_val(b.z); vhi = ord_val(b.w);
-        } else {
-            const double2 *uvp = uv + xoff[f];  // projected by k_fan
-#pragma unroll 4
-            for (int i = 0; i < nv; i++) {
-                const double2 w = uvp[i];
-                ulo = fmin(ulo, w.x); uhi = fmax(uhi, w.x); vlo = fmin(vlo, w.y); vhi = fmax(vhi, w.y);
+        for (int i0 = 0; i0 < nv; i0 += kSetupBatch) {  // (a batch's loads in flight together; repeats are harmless)
+            double2 w[kSetupBatch];
+#pragma unroll
+            for (int u = 0; u < kSetupBatch; u++) w[u] = uvp[i0 + u < nv ? i0 + u : i0];
+#pragma unroll
+            for (int u = 0; u < kSetupBatch; u++) {
+                ulo = fmin(ulo, w[u].x); uhi = fmax(uhi, w[u].x); vlo = fmin(vlo, w[u].y); vhi = fmax(vhi, w[u].y);
             }
         }
         fl |= direct_frame(f, xyz_face(p[0]), ulo, uhi, vlo, vhi, st_id, st_i, st_j, finfo, fbox, true);
@@ -652,14 +599,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DSS_SETUP_WP
     uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx, const double2 *uv, uint64_t *st_id,
     uint32_t *st_i, uint32_t *st_j, uint32_t *finfo, uint4 *fbox, const double *fwd, const double *rev,
     const uint8_t *fan_fail, const uint8_t *not_inner, const uint8_t *omode, const uint32_t *perm, uint8_t *rev_out,
-    const uint8_t *bad_in, const CircleFrame *frames, const longlong4 *fbb, int all_exact)
+    const uint8_t *bad_in, const CircleFrame *frames, int all_exact)
 {
     const int64_t t = tid64();
     if (t >= n) return;
     // polygons first, then circles: waves run one kind's path
     setup_one(perm[t], slow_list, slow_n, kind, voff, lat, lng, radius_m, xoff, xyz, status, area_out, mode, origin_in,
               fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, fwd, rev, fan_fail, not_inner, omode, rev_out,
-              bad_in, frames, fbb, all_exact != 0);
+              bad_in, frames, all_exact != 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1496,100 +1443,12 @@ __device__ __forceinline__ int cand_edges_uv(uint32_t i, uint32_t j, const doubl
 // than 1e-6 cannot); then only the marked edges run the exact tests, in the
 // same double arithmetic -- the result is cand_edges_uv's.  NaN end points
 // fail every float comparison, so their edges stay marked.
-constexpr float kSlack = 1e-6f;
-__device__ __forceinline__ double cell_lo_uv(uint32_t i) { return st_to_uv((double)i / (double)kMaxSize); }
-__device__ __forceinline__ double cell_hi_uv(uint32_t i)
-{
-    return st_to_uv((double)(i + (1u << (kMaxLevel - kCoverLevel))) / (double)kMaxSize);
-}
-__device__ __forceinline__ double cell_mid_uv(uint32_t i)
-{
-    return st_to_uv(0.5 / (double)kMaxSize * (2.0 * (double)i + (double)(1u << (kMaxLevel - kCoverLevel))));
-}
-
-// The v half of the prefilter, the same for every cell of a level-13 row j:
-// the edges whose end points are not both beyond the row's padded v range
-// (*nearv) and those not both above or both below its centre line (*strad).
-__device__ __forceinline__ void row_masks(uint32_t j, const float2 *upf, int nv, unsigned long long &nearv,
-                                          unsigned long long &strad)
-{
-    const double pm = kFinePad;
-    const double vlo = cell_lo_uv(j), vhi = cell_hi_uv(j), vc = cell_mid_uv(j);
-    const float rlv = (float)(vlo - pm) - kSlack, rhv = (float)(vhi + pm) + kSlack;
-    const float vcl = (float)vc - kSlack, vch = (float)vc + kSlack;
-    nearv = strad = 0;
-    float2 a = upf[0];
-    for (int e = 0; e < nv; e++) {
-        const float2 b = upf[e + 1 < nv ? e + 1 : 0];
-        const bool far = ((a.y < rlv) & (b.y < rlv)) | ((a.y > rhv) & (b.y > rhv));
-        const bool level = ((a.y > vch) & (b.y > vch)) | ((a.y < vcl) & (b.y < vcl));
-        nearv |= (unsigned long long)!far << e;
-        strad |= (unsigned long long)!level << e;
-        a = b;
-    }
-}
-
-// The u half for the cell at level-30 column i over the row's near edges,
-// then the exact tests of the marked edges.
-__device__ __forceinline__ int cand_edges_rows(uint32_t i, uint32_t j, const double2 *upg, bool rev,
-                                               const float2 *upf, int nv, unsigned long long nearv,
-                                               unsigned long long strad, bool planar, bool origin_in)
+__device__ __forceinline__ int cand_edges_uv_f(uint32_t i, uint32_t j, const double2 *upg, bool rev,
+                                               const float2 *upf, int nv, bool planar, bool origin_in)
 {
     // (the exact tests read the loop from global memory; rev: a loop k_setup
     // reversed without moving it, read mirrored -- the float stage is in
     // loop order already)
-    auto at = [&](int e) { return upg[rev ? nv - 1 - e : e]; };
-    const double pm = kFinePad;
-    const double ulo = cell_lo_uv(i), uhi = cell_hi_uv(i);
-    const float rlu = (float)(ulo - pm) - kSlack, rhu = (float)(uhi + pm) + kSlack;
-    unsigned long long near = 0;
-#if DSS_CAND_MODE == 2
-    float ax = upf[0].x;
-    for (int e = 0; e < nv; e++) {
-        const float bx = upf[e + 1 < nv ? e + 1 : 0].x;
-        const bool far = ((ax < rlu) & (bx < rlu)) | ((ax > rhu) & (bx > rhu));
-        near |= (unsigned long long)!far << e;
-        ax = bx;
-    }
-    near &= nearv;
-#else
-    while (nearv) {
-        const int e = __builtin_ctzll(nearv);
-        nearv &= nearv - 1;
-        const float2 a = upf[e], b = upf[e + 1 < nv ? e + 1 : 0];
-        const bool far = ((a.x < rlu) & (b.x < rlu)) | ((a.x > rhu) & (b.x > rhu));
-        near |= (unsigned long long)!far << e;
-    }
-#endif
-    if (near) {
-        const double vlo = cell_lo_uv(j), vhi = cell_hi_uv(j);
-        do {
-            const int e = __builtin_ctzll(near);
-            near &= near - 1;
-            const double2 x = at(e), y = at(e + 1 < nv ? e + 1 : 0);
-            if (edge_intersects_rect(x.x, x.y, y.x, y.y, ulo - pm, uhi + pm, vlo - pm, vhi + pm)) return 1;
-        } while (near);
-    }
-    if (!planar) return 2;
-    const double uc = cell_mid_uv(i), vc = cell_mid_uv(j);
-    bool par = false;
-    while (strad) {
-        const int e = __builtin_ctzll(strad);
-        strad &= strad - 1;
-        const double2 x = at(e), y = at(e + 1 < nv ? e + 1 : 0);
-        if ((x.y > vc) != (y.y > vc)) {
-            const double d = y.y - x.y;
-            const double lhs = (uc - x.x) * d, rhs = (vc - x.y) * (y.x - x.x);
-            if (d > 0 ? lhs < rhs : lhs > rhs) par = !par;
-        }
-    }
-    return (origin_in != par) ? 1 : 0;
-}
-
-// Both halves per cell (a footprint whose rows did not fit the block's stage).
-__device__ __forceinline__ int cand_edges_uv_f0(uint32_t i, uint32_t j, const double2 *upg, bool rev,
-                                               const float2 *upf, int nv, bool planar, bool origin_in)
-{
     auto at = [&](int e) { return upg[rev ? nv - 1 - e : e]; };
     const uint32_t size = 1u << (kMaxLevel - kCoverLevel);
     const double ulo = st_to_uv((double)i / (double)kMaxSize), uhi = st_to_uv((double)(i + size) / (double)kMaxSize);
@@ -1597,6 +1456,7 @@ __device__ __forceinline__ int cand_edges_uv_f0(uint32_t i, uint32_t j, const do
     const double pm = kFinePad;
     const double half = 0.5 / (double)kMaxSize, sz = (double)size;
     const double uc = st_to_uv(half * (2.0 * (double)i + sz)), vc = st_to_uv(half * (2.0 * (double)j + sz));
+    constexpr float kSlack = 1e-6f;
     const float rlu = (float)(ulo - pm) - kSlack, rhu = (float)(uhi + pm) + kSlack;
     const float rlv = (float)(vlo - pm) - kSlack, rhv = (float)(vhi + pm) + kSlack;
     const float vcl = (float)vc - kSlack, vch = (float)vc + kSlack;
@@ -1631,23 +1491,13 @@ __device__ __forceinline__ int cand_edges_uv_f0(uint32_t i, uint32_t j, const do
     }
     return (origin_in != par) ? 1 : 0;
 }
-__device__ __forceinline__ int cand_edges_uv_f(uint32_t i, uint32_t j, const double2 *upg, bool rev,
-                                               const float2 *upf, int nv, bool planar, bool origin_in)
-{
-    unsigned long long nearv, strad;
-    row_masks(j, upf, nv, nearv, strad);
-    return cand_edges_rows(i, j, upg, rev, upf, nv, nearv, strad, planar, origin_in);
-}
 
 // One block per kFpPer consecutive footprints: wave 0 loads their bounds,
 // start cells and flags into LDS (one round trip for the block, none per
-// candidate), the block stages their (u,v) vertices, then the edge masks of
-// every row of their bounds (row_masks: the v half of the prefilter, once per
-// row instead of once per cell -- a cell then walks only the edges that
-// reach its row), then its threads stride over the block's bound cells
-// (footprint by LDS search, cell by position in its bound) and set key bits
-// in the footprints' LDS masks.  Wave 0 writes the kept masks, and lists the
-// footprints with undecided bits for k_cand_exact.
+// candidate), the block stages their (u,v) vertices, then its threads stride
+// over the block's bound cells (footprint by LDS search, cell by position in
+// its bound) and set key bits in the footprints' LDS masks.  Wave 0 writes the
+// kept masks, and lists the footprints with undecided bits for k_cand_exact.
 __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *flags, const uint4 *fbox,
                                                       const uint32_t *finfo, const uint32_t *st_i,
                                                       const uint32_t *st_j, const int64_t *xoff, const int32_t *nvx,
@@ -1659,8 +1509,6 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
     __shared__ uint4 s_bx[kFpPer];
     __shared__ uint32_t s_info[kFpPer], s_sti[kFpPer][4], s_stj[kFpPer][4];
     __shared__ int s_cb[kFpPer + 1], s_vb[kFpPer], s_nv[kFpPer], s_fl[kFpPer], s_vp[kFpPer + 1];
-    __shared__ int s_rp[kFpPer + 1], s_rb[kFpPer];
-    __shared__ unsigned long long s_rnear[kCandStageR], s_rstrad[kCandStageR];
     __shared__ int64_t s_xo[kFpPer];
     __shared__ unsigned long long s_km[kFpPer][4], s_um[kFpPer][4];
     __shared__ float2 s_uvf[kCandStageV];  // the block's (u,v) vertices in float (cand_edges_uv_f's prefilter)
@@ -1671,7 +1519,7 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
         // loops are of one kind, so a wave's edge walks are of similar length
         const int64_t f = F0 + t < n ? (int64_t)perm[F0 + t] : n;
         const bool fast = f < n && (flags[f] & FL_FAST);
-        uint32_t cnt = 0, nvv = 0, rows = 0;
+        uint32_t cnt = 0, nvv = 0;
         if (fast) {
             const uint4 bx = fbox[f];
             s_bx[t] = bx;
@@ -1685,25 +1533,19 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
             nvv = (uint32_t)nvx[f];
             s_fl[t] = ((flags[f] & FL_PLANAR) ? 1 : 0) | (origin_in[f] ? 2 : 0) | (rev_flag[f] ? 4 : 0);
             cnt = (bx.y - bx.x + 1) * (bx.w - bx.z + 1);
-            rows = nvv <= 64 ? bx.w - bx.z + 1 : 0;
         }
         s_nv[t] = (int)nvv;
 #pragma unroll
         for (int q = 0; q < 4; q++) s_km[t][q] = s_um[t][q] = 0ull;
-        // candidate, vertex and row prefixes over the block's footprints (wave scans)
-        uint32_t ci = cnt, vi = nvv, ri = rows;
+        // candidate and vertex prefixes over the block's footprints (wave scans)
+        uint32_t ci = cnt, vi = nvv;
         for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t a = (uint32_t)__shfl_up((int)ci, o), b = (uint32_t)__shfl_up((int)vi, o),
-                           c = (uint32_t)__shfl_up((int)ri, o);
+            const uint32_t a = (uint32_t)__shfl_up((int)ci, o), b = (uint32_t)__shfl_up((int)vi, o);
             if (lane >= o) {
                 ci += a;
                 vi += b;
-                ri += c;
             }
         }
-        s_rp[t + 1] = (int)ri;
-        if (t == 0) s_rp[0] = 0;
-        s_rb[t] = ri <= (uint32_t)kCandStageR ? (int)(ri - rows) : -1;  // LDS row offset, or -1: per-cell masks
         s_cb[t + 1] = (int)ci;
         if (t == 0) s_cb[0] = 0;
         s_vb[t] = vi <= (uint32_t)kCandStageV ? (int)(vi - nvv) : -1;  // LDS offset, or -1: read from global
@@ -1728,20 +1570,6 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
         s_uvf[k] = make_float2((float)w.x, (float)w.y);
     }
     __syncthreads();
-    // the edge masks of the bound rows of the staged footprints
-    const int nrs = DSS_CAND_MODE == 0 ? 0 : min(s_rp[kFpPer], kCandStageR);
-    for (int k = t; k < nrs; k += kFpBlock) {
-        int lo = 0, hi = kFpPer;  // s_rp[lo] <= k < s_rp[hi]
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (s_rp[mid] <= k) lo = mid;
-            else hi = mid;
-        }
-        if (s_vb[lo] < 0) continue;  // (its cells read the loop from global memory)
-        const uint32_t j13 = s_bx[lo].z + (uint32_t)(k - s_rp[lo]);
-        row_masks(j13 << (kMaxLevel - kCoverLevel), s_uvf + s_vb[lo], s_nv[lo], s_rnear[k], s_rstrad[k]);
-    }
-    __syncthreads();
     const int total = s_cb[kFpPer];
     for (int k = t; k < total; k += kFpBlock) {
         int lo = 0, hi = kFpPer;  // s_cb[lo] <= k < s_cb[hi]
@@ -1760,18 +1588,12 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
         // (staged vertices are in loop order already; unstaged ones are read
         // through the reversal)
         const double2 *up = uv + s_xo[lo];
-        const int nvf = s_nv[lo], rb = s_rb[lo];
-        const uint32_t i30 = i13 << (kMaxLevel - kCoverLevel), j30 = j13 << (kMaxLevel - kCoverLevel);
-        int v;
-        if (DSS_CAND_MODE == 0 && vb >= 0 && nvf <= 64)
-            v = cand_edges_uv_f0(i30, j30, up, (fl & 4) != 0, s_uvf + vb, nvf, (fl & 1) != 0, (fl & 2) != 0);
-        else if (vb >= 0 && nvf <= 64 && rb >= 0)
-            v = cand_edges_rows(i30, j30, up, (fl & 4) != 0, s_uvf + vb, nvf, s_rnear[rb + dj], s_rstrad[rb + dj],
-                                (fl & 1) != 0, (fl & 2) != 0);
-        else if (vb >= 0 && nvf <= 64)
-            v = cand_edges_uv_f(i30, j30, up, (fl & 4) != 0, s_uvf + vb, nvf, (fl & 1) != 0, (fl & 2) != 0);
-        else
-            v = cand_edges_uv(i30, j30, up, nvf, (fl & 1) != 0, (fl & 2) != 0, (fl & 4) != 0);
+        const int nvf = s_nv[lo];
+        const int v = vb >= 0 && nvf <= 64
+                          ? cand_edges_uv_f(i13 << (kMaxLevel - kCoverLevel), j13 << (kMaxLevel - kCoverLevel), up,
+                                            (fl & 4) != 0, s_uvf + vb, nvf, (fl & 1) != 0, (fl & 2) != 0)
+                          : cand_edges_uv(i13 << (kMaxLevel - kCoverLevel), j13 << (kMaxLevel - kCoverLevel), up, nvf,
+                                          (fl & 1) != 0, (fl & 2) != 0, (fl & 4) != 0);
         if (v == 1) atomicOr(&s_km[lo][key >> 6], 1ull << (key & 63));
         else if (v == 2) atomicOr(&s_um[lo][key >> 6], 1ull << (key & 63));
     }
@@ -2463,9 +2285,8 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     }
     uint8_t *fan_fail = fanf_.ensure(n + 1), *not_inner = ninner_.ensure(n + 1), *bad = badv_.ensure(n + 1);
     unsigned int *slow_n = slow_n_.ensure(1), *dlist_n = dlist_n_.ensure(1), *ulist_n = ulist_n_.ensure(1);
-    longlong4 *fbb = fan_bbox_ ? (longlong4 *)fbb_.ensure(4 * (n + 1)) : nullptr;
     hipLaunchKernelGGL(k_nverts, dim3(grid_for(n, B)), dim3(B), 0, s, n, kind, voff, nv, fan_fail, not_inner, bad,
-                       slow_n, dlist_n, ulist_n, fbb);
+                       slow_n, dlist_n, ulist_n);
     int64_t *mail = mailbox();  // [0] vertices [1] edge items [2] descent [3] exact setups [4] start nodes
                                 // [5] next frontier [6] open [7] cells
     volatile const int64_t *mh = mail_h_;
@@ -2503,7 +2324,7 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
                            bad);
         // (k_fan fused into k_verts -- neighbours by shuffle, recomputed across
         // wave edges -- measured slower: 0.355 against 0.317 ms, r05v)
-        hipLaunchKernelGGL(k_fan, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, nv, xoff, xyz, uv, not_inner, fbb);
+        hipLaunchKernelGGL(k_fan, dim3(grid_for(nx, B)), dim3(B), 0, s, nx, vown, nv, xoff, xyz, uv, not_inner);
     }
     // fan triangle terms of Loop.Area: orientation first, then one thread per
     // triangle actually needed (no lanes idle on circles or on the orientation
@@ -2516,7 +2337,7 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     uint8_t *rev_flag = revf_.ensure(n + 1);
     hipLaunchKernelGGL(k_setup, dim3(grid_for(n, 64)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng, radius_m,
                        xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, fwd,
-                       rev, fan_fail, not_inner, omode, perm, rev_flag, bad, frames, fbb, all_exact_ ? 1 : 0);
+                       rev, fan_fail, not_inner, omode, perm, rev_flag, bad, frames, all_exact_ ? 1 : 0);
     int64_t *eoff = eoff_.ensure(n + 1);
     uint32_t *dlist = dlist_.ensure(n + 1);
     int64_t ne = 0;

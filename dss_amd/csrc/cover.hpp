@@ -47,8 +47,6 @@ class CoverEngine {
     void set_all_exact(bool on) { all_exact_ = on; }
     // vertex slots in k_setup's footprint order (default) or in footprint order
     void set_slot_order(bool kind_major) { slot_order_ = kind_major; }
-    // each footprint's (u,v) bound reduced by k_fan (default) or summed by k_setup
-    void set_fan_bbox(bool on) { fan_bbox_ = on; }
 
    private:
     void run_general(int64_t n, const int32_t *kind, const int64_t *voff, const double *lat, const double *lng,
@@ -59,12 +57,7 @@ class CoverEngine {
 #ifndef DSS_SLOT_ORDER
 #define DSS_SLOT_ORDER 0
 #endif
-#ifndef DSS_FAN_BBOX
-#define DSS_FAN_BBOX 0
-#endif
     bool slot_order_ = DSS_SLOT_ORDER != 0;
-    bool fan_bbox_ = DSS_FAN_BBOX != 0;
-    DevBuf<long long> fbb_;
     int64_t wave_max_ = 16384;
     int64_t last_slow_ = 0;
     // wave path: per-footprint outputs, the slow sub-batch, the merged CSR

@@ -160,35 +160,15 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scan(uint32_t *__restrict__ hist
 // (key, value) and sorts the word (key & ~lomask) | value; bit 1 -- it writes
 // the word back out as (word & ~lomask) | kconst and value word & lomask.
 // Middle passes move the words alone (HAS_V false).
-// OS (onesweep, the packed path): no per-pass tile histogram -- the tile
-// takes the next tile id from *tile_ctr, and after ranking its keys publishes
-// its digit counts in status[tile][d] (flag AGG) and looks back over the
-// earlier tiles' words, adding counts until a flag PREFIX, then publishes its
-// own inclusive prefix (flag PREFIX): decoupled look-back.  dtot = each
-// digit's global start (k_os_digits).  The tile ids come from the counter in
-// the order tiles start, so every tile a look-back waits on is already running.
-// The passes of one sort share the status words: pass p's flags are AGG =
-// 2p + 1, PREFIX = 2p + 2 (epoch = 2p), so a word still holding an earlier
-// pass's flag reads as not ready and the array is zeroed once per sort.
-template <typename K, typename V, bool HAS_V, int PK = 0, int ITEMS = kItems, bool OS = false>
+template <typename K, typename V, bool HAS_V, int PK = 0, int ITEMS = kItems>
 __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki, const V *__restrict__ vi,
                                                         K *__restrict__ ko, V *__restrict__ vo, int64_t n,
                                                         const int64_t *__restrict__ dn, int shift, int rbits,
                                                         const uint32_t *__restrict__ hist, int64_t stride,
-                                                        const uint32_t *__restrict__ dtot, K lomask = 0, K kconst = 0,
-                                                        unsigned long long *__restrict__ status = nullptr,
-                                                        unsigned int *__restrict__ tile_ctr = nullptr,
-                                                        unsigned int epoch = 0)
+                                                        const uint32_t *__restrict__ dtot, K lomask = 0, K kconst = 0)
 {
     static_assert(PK == 0 || !HAS_V, "packed passes stage the words alone");
     if (dn) n = min(n, *dn);
-    __shared__ uint32_t s_tile;
-    uint32_t tile = blockIdx.x;
-    if constexpr (OS) {
-        if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);
-        __syncthreads();
-        tile = s_tile;
-    }
     __shared__ uint32_t wh[kRWaves][kMaxDigits];  // per-wave digit counters, then their exclusive prefix over waves
     __shared__ uint32_t dstart[kMaxDigits];       // tile-local start of each digit
     __shared__ uint32_t gbase[kMaxDigits];        // global position of tile slot 0 of each digit
@@ -201,16 +181,16 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
     for (int i = tid; i < kRWaves * kMaxDigits; i += kRBlock) (&wh[0][0])[i] = 0;
     // global start of digits kDPT*tid .. +kDPT-1 in this tile: all smaller
     // digits + the same digit in earlier tiles
+    uint32_t dt[kDPT], dsum = 0;
+#pragma unroll
+    for (int u = 0; u < kDPT; u++) {
+        const uint32_t d = (uint32_t)(kDPT * tid + u);
+        dt[u] = d < nd ? dtot[d] : 0u;
+        dsum += dt[u];
+    }
     uint32_t unused;
     uint32_t gstart[kDPT];
-    if constexpr (!OS) {
-        uint32_t dt[kDPT], dsum = 0;
-#pragma unroll
-        for (int u = 0; u < kDPT; u++) {
-            const uint32_t d = (uint32_t)(kDPT * tid + u);
-            dt[u] = d < nd ? dtot[d] : 0u;
-            dsum += dt[u];
-        }
+    {
         uint32_t run = block_incl_scan(dsum, ws, unused) - dsum;
 #pragma unroll
         for (int u = 0; u < kDPT; u++) {
@@ -220,7 +200,7 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
         }
     }
 
-    const int64_t sub = (int64_t)tile * kT + (int64_t)w * kWT;
+    const int64_t sub = (int64_t)blockIdx.x * kT + (int64_t)w * kWT;
     K k[ITEMS];
     V v[ITEMS];
     uint32_t loc[ITEMS];
@@ -264,36 +244,6 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
         cnt[u] = c;
         csum += c;
     }
-    if constexpr (OS) {
-        // gstart = the digit's global start (dtot = gdig) + its count in the
-        // tiles before this one (look-back)
-#pragma unroll
-        for (int u = 0; u < kDPT; u++) {
-            const uint32_t d = (uint32_t)(kDPT * tid + u);
-            if (d >= nd) { gstart[u] = 0; continue; }
-            const unsigned long long agg = (unsigned long long)(epoch + 1) << 32,
-                                     pre = (unsigned long long)(epoch + 2) << 32;
-            unsigned long long *my = status + (int64_t)tile * kMaxDigits + d;
-            if (tile == 0) {
-                __hip_atomic_store(my, pre | cnt[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                gstart[u] = dtot[d];
-                continue;
-            }
-            __hip_atomic_store(my, agg | cnt[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t excl = 0;
-            for (const unsigned long long *q = my - kMaxDigits;; q -= kMaxDigits) {
-                unsigned long long x;
-                do {
-                    x = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } while ((x >> 32) <= epoch);
-                excl += (uint32_t)x;
-                if ((x >> 32) == epoch + 2) break;
-            }
-            __hip_atomic_store(my, pre | (unsigned long long)(excl + cnt[u]), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            gstart[u] = dtot[d] + excl;
-        }
-    }
     {
         uint32_t st = block_incl_scan(csum, ws, unused) - csum;
 #pragma unroll
@@ -315,7 +265,7 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
         }
     }
     __syncthreads();
-    const int64_t rem = n - (int64_t)tile * kT;
+    const int64_t rem = n - (int64_t)blockIdx.x * kT;
     const int tile_n = rem < kT ? (int)rem : kT;
     for (int i = tid; i < tile_n; i += kRBlock) {
         const K kk = sk[i];
@@ -328,56 +278,6 @@ __global__ __launch_bounds__(kRBlock) void k_rs_scatter(const K *__restrict__ ki
         }
         if (HAS_V) vo[p] = sv[i];
     }
-}
-
-// Onesweep front: the global digit counts of every pass of a packed sort in
-// one read of the keys (pass p: bits lo + p rb .. , at most hi), per-block
-// partials part[block][p][d] (no same-address global atomics), grid-stride
-// over 4096-key chunks.
-constexpr int kOsMaxPasses = 8;
-__global__ __launch_bounds__(kRBlock) void k_os_hist(const uint64_t *__restrict__ keys, int64_t n, int lo, int rb,
-                                                     int hi, int passes, uint32_t *__restrict__ part)
-{
-    __shared__ uint32_t h[kRWaves][kOsMaxPasses * kMaxDigits];
-    const int tid = threadIdx.x, w = tid >> 6;
-    for (int i = tid; i < kRWaves * kOsMaxPasses * kMaxDigits; i += kRBlock) (&h[0][0])[i] = 0;
-    __syncthreads();
-    constexpr int kC = kRBlock * 16;
-    for (int64_t base = (int64_t)blockIdx.x * kC; base < n; base += (int64_t)gridDim.x * kC) {
-        uint64_t k[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const int64_t i = base + j * kRBlock + tid;
-            k[j] = i < n ? keys[i] : 0ull;
-        }
-        for (int p = 0; p < passes; p++) {
-            const int sh = lo + p * rb, r = hi - sh < rb ? hi - sh : rb;
-            const uint32_t mask = (1u << r) - 1u;
-#pragma unroll
-            for (int j = 0; j < 16; j++)
-                if (base + j * kRBlock + tid < n) atomicAdd(&h[w][p * kMaxDigits + ((uint32_t)(k[j] >> sh) & mask)], 1u);
-        }
-    }
-    __syncthreads();
-    for (int i = tid; i < passes * kMaxDigits; i += kRBlock) {
-        uint32_t c = 0;
-#pragma unroll
-        for (int q = 0; q < kRWaves; q++) c += h[q][i];
-        part[(int64_t)blockIdx.x * passes * kMaxDigits + i] = c;
-    }
-}
-
-// One block per pass: digit d's total over the partials, then the exclusive
-// scan over digits -> gdig[p][d], the digit's global start.
-__global__ __launch_bounds__(kRBlock) void k_os_digits(const uint32_t *__restrict__ part, int nb, int passes,
-                                                       uint32_t *__restrict__ gdig)
-{
-    __shared__ uint32_t ws[kRWaves];
-    const int p = blockIdx.x, d = threadIdx.x;
-    uint32_t c = 0;
-    for (int b = 0; b < nb; b++) c += part[((int64_t)b * passes + p) * kMaxDigits + d];
-    uint32_t total;
-    gdig[p * kMaxDigits + d] = block_incl_scan(c, ws, total) - c;
 }
 
 // OR over all keys of (key ^ keys[0]): the bits that vary.  Bits constant
@@ -438,11 +338,6 @@ __global__ __launch_bounds__(kRBlock) void k_rs_or_parts(const unsigned long lon
 }
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
-
-#ifndef DSS_ONESWEEP
-#define DSS_ONESWEEP 0
-#endif
-bool g_onesweep = DSS_ONESWEEP != 0;  // the packed sort's look-back path (dssg_set_tuning "radix_onesweep")
 
 template <typename K, typename V, bool HAS_V>
 void radix_sort(const K *ki, K *ko, const V *vi, V *vo, int64_t n, const int64_t *dn, int bits, DevBuf<unsigned char> &tmp,
@@ -567,41 +462,6 @@ void radix_sort_packed(const uint64_t *ki, uint64_t *ko, const uint32_t *vi, uin
     const K lomask = lo >= 64 ? ~0ull : ((1ull << lo) - 1), kconst = k0 & lomask;
     const int span = hi - lo, passes = (span + kMaxDigitBits - 1) / kMaxDigitBits, rb = (span + passes - 1) / passes;
     const size_t ka_b = passes > 1 ? align256(sizeof(K) * n) : 0;
-    if (g_onesweep && passes <= kOsMaxPasses && kMaxDigits == kRBlock) {
-        // one read for every pass's digit counts, then per pass one scatter
-        // with decoupled look-back (no per-pass histogram read of the keys)
-        const int nb = (int)std::min<int64_t>(ntiles, 512);
-        const size_t part_b = align256(sizeof(uint32_t) * nb * passes * kMaxDigits),
-                     gdig_b = align256(sizeof(uint32_t) * passes * kMaxDigits),
-                     st_b = align256(sizeof(unsigned long long) * ntiles * kMaxDigits), ctr_b = 256;
-        unsigned char *t = tmp.ensure(part_b + gdig_b + st_b + ctr_b + ka_b);
-        uint32_t *part = (uint32_t *)t, *gdig = (uint32_t *)(t + part_b);
-        unsigned long long *status = (unsigned long long *)(t + part_b + gdig_b);
-        unsigned int *ctr = (unsigned int *)(t + part_b + gdig_b + st_b);
-        K *kalt = (K *)(t + part_b + gdig_b + st_b + ctr_b);
-        DSS_HIP(hipMemsetAsync(status, 0, st_b + ctr_b, s));
-        hipLaunchKernelGGL(k_os_hist, dim3((unsigned)nb), dim3(kRBlock), 0, s, ki, n, lo, rb, hi, passes, part);
-        hipLaunchKernelGGL(k_os_digits, dim3((unsigned)passes), dim3(kRBlock), 0, s, part, nb, passes, gdig);
-        const K *src = ki;
-        for (int p = 0; p < passes; p++) {
-            const int shift = lo + p * rb, r = hi - shift < rb ? hi - shift : rb;
-            const bool to_out = ((passes - 1 - p) & 1) == 0, first = p == 0, last = p == passes - 1;
-            K *dst = to_out ? ko : kalt;
-            const uint32_t *gd = gdig + p * kMaxDigits;
-            const unsigned int ep = 2u * (unsigned)p;
-#define DSS_OS_SCATTER(PKV)                                                                                          \
-    hipLaunchKernelGGL((k_rs_scatter<K, uint32_t, false, PKV, kPI, true>), dim3((unsigned)ntiles), dim3(kRBlock), 0, s, \
-                       src, vi, dst, vo, n, nullptr, shift, r, nullptr, 0, gd, lomask, kconst, status, ctr + p, ep)
-            if (first && last) DSS_OS_SCATTER(3);
-            else if (first) DSS_OS_SCATTER(1);
-            else if (last) DSS_OS_SCATTER(2);
-            else DSS_OS_SCATTER(0);
-#undef DSS_OS_SCATTER
-            DSS_HIP(hipGetLastError());
-            src = dst;
-        }
-        return;
-    }
     unsigned char *t = tmp.ensure(hist_b + dtot_b + ka_b);
     uint32_t *hist = (uint32_t *)t, *dtot = (uint32_t *)(t + hist_b);
     K *kalt = (K *)(t + hist_b + dtot_b);
@@ -632,8 +492,6 @@ void radix_sort_packed(const uint64_t *ki, uint64_t *ko, const uint32_t *vi, uin
 }
 
 }  // namespace
-
-void set_radix_onesweep(bool on) { g_onesweep = on; }
 
 void radix_sort_pairs_packed(const uint64_t *ki, uint64_t *ko, const uint32_t *vi, uint32_t *vo, int64_t n, int bits,
                              DevBuf<unsigned char> &tmp, hipStream_t s)

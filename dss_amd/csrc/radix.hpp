@@ -22,8 +22,6 @@ void radix_sort_pairs_dn(const K *ki, K *ko, const V *vi, V *vo, int64_t n_max, 
 // (u64 key, u32 value) pairs, as radix_sort_pairs, moved as packed 8-B words
 // when the keys' constant low bits leave room for the values (level-13 cell
 // ids with entity ids): 8 B per element per middle pass instead of 12.
-// (tests / A-B) the packed sort's onesweep path on or off (default on)
-void set_radix_onesweep(bool on);
 void radix_sort_pairs_packed(const uint64_t *ki, uint64_t *ko, const uint32_t *vi, uint32_t *vo, int64_t n, int bits,
                              DevBuf<unsigned char> &tmp, hipStream_t s);
 

@@ -19,7 +19,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 COVER_WAVE_DEFAULT = 16384  # CoverEngine::wave_max_
-SLOT_ORDER_DEFAULT, FAN_BBOX_DEFAULT = 0, 0  # CoverEngine::slot_order_, fan_bbox_
+SLOT_ORDER_DEFAULT = 0  # CoverEngine::slot_order_
 
 
 @pytest.fixture
@@ -112,24 +112,21 @@ def test_exact_setup_metro_seeds(exact_setup, oracle):
         _check(oracle, fp.kind, fp.voff, fp.lat, fp.lng, fp.radius_m)
 
 
-@pytest.mark.parametrize("slot_order,fan_bbox", [(1, 1), (0, 1), (1, 0), (0, 0)])
-def test_cover_layout_options(oracle, slot_order, fan_bbox):
-    """The general pipeline's layout options give the oracle's coverings
-    either way: vertex slots polygons-first (k_setup's order) or in footprint
-    order ("cover_slot_order"), and each footprint's (u,v) bound reduced by
-    k_fan across lanes and waves or by k_setup's loop ("cover_fan_bbox")."""
+@pytest.mark.parametrize("slot_order", [1, 0])
+def test_cover_slot_order(oracle, slot_order):
+    """The general pipeline gives the oracle's coverings with its vertex
+    slots polygons-first (k_setup's footprint order) or in footprint order
+    ("cover_slot_order")."""
     from dss_amd import _lib
     from dss_amd import workload as W
     from test_gpu_cover_general import _base_footprints
     ctx = _lib.context(0)
     ctx.set_tuning("cover_wave", 0)
     ctx.set_tuning("cover_slot_order", slot_order)
-    ctx.set_tuning("cover_fan_bbox", fan_bbox)
     try:
         _, q, _, _, _, _ = W.config(2, scale=0.002)
         _check(oracle, q.kind, q.voff, q.lat, q.lng, q.radius_m)
         _check(oracle, *_flat(_base_footprints(np.random.default_rng(3))))
     finally:
         ctx.set_tuning("cover_slot_order", SLOT_ORDER_DEFAULT)
-        ctx.set_tuning("cover_fan_bbox", FAN_BBOX_DEFAULT)
         ctx.set_tuning("cover_wave", COVER_WAVE_DEFAULT)

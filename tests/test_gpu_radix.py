@@ -86,24 +86,8 @@ PACKED = [  # (name, n, bits, key high bits, key low constant, key shift, value 
 ]
 
 
-ONESWEEP_DEFAULT = 0  # radix.hip g_onesweep
-
-
-@pytest.fixture(params=[1, 0], ids=["onesweep", "per-pass-hist"])
-def onesweep(request):
-    """The packed sort both ways: decoupled look-back (one histogram read for
-    every pass) and per-pass tile histograms."""
-    from dss_amd import _lib
-    ctx = _lib.context()
-    ctx.set_tuning("radix_onesweep", request.param)
-    try:
-        yield request.param
-    finally:
-        ctx.set_tuning("radix_onesweep", ONESWEEP_DEFAULT)
-
-
 @pytest.mark.parametrize("name,n,bits,hb,low,sh,vmax", PACKED)
-def test_radix_sort_packed_words(onesweep, name, n, bits, hb, low, sh, vmax):
+def test_radix_sort_packed_words(name, n, bits, hb, low, sh, vmax):
     """The packed 8-B path (key bits below the lowest varying one constant and
     wide enough for every value) and its fallback both equal the stable sort:
     keys restored with their constant low bits and any unsorted high bits,
@@ -118,23 +102,6 @@ def test_radix_sort_packed_words(onesweep, name, n, bits, hb, low, sh, vmax):
     rk, rv = ref_sort(k, vals, bits)
     assert np.array_equal(ko, rk), name
     assert np.array_equal(vo, rv), name
-
-
-def test_radix_sort_packed_many_tiles(onesweep):
-    """20M level-13-shaped (cell, entity) postings, 70 % of them in a few
-    hotspot cells (long runs of one digit: the look-back's counts of a digit
-    cross many tiles), entity ids in input order: the index build's sort at a
-    size where thousands of tiles run concurrently."""
-    rng = np.random.default_rng(5)
-    n = 20_000_000
-    cells = rng.integers(0, 1 << 29, n, dtype=np.uint64)
-    hot = rng.random(n) < 0.7
-    cells[hot] = rng.integers(0, 40, int(hot.sum()), dtype=np.uint64) * np.uint64(7919)
-    k = (cells << np.uint64(35)) | np.uint64(1 << 34)
-    vals = np.arange(n, dtype=np.uint32)
-    ko, vo, _ = gpu_sort(k, vals, 64, 8)
-    order = np.argsort(k, kind="stable")
-    assert np.array_equal(ko, k[order]) and np.array_equal(vo, vals[order])
 
 
 def test_radix_sort_rejects_aliasing():
