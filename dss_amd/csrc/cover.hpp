@@ -55,7 +55,7 @@ class CoverEngine {
     bool wave_ = true;
     bool all_exact_ = false;
 #ifndef DSS_SLOT_ORDER
-#define DSS_SLOT_ORDER 0
+#define DSS_SLOT_ORDER 1
 #endif
     bool slot_order_ = DSS_SLOT_ORDER != 0;
     int64_t wave_max_ = 16384;

@@ -19,7 +19,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 COVER_WAVE_DEFAULT = 16384  # CoverEngine::wave_max_
-SLOT_ORDER_DEFAULT = 0  # CoverEngine::slot_order_
+SLOT_ORDER_DEFAULT = 1  # CoverEngine::slot_order_
 
 
 @pytest.fixture

@@ -9,8 +9,8 @@ oracle bit for bit (status, cells, area):
 * small loops with vertices on level-13 cell corners and edges 1e-15..1e-12
   off cell boundary lines (k_cand_fp's float prefilter next to the exact
   double tests);
-* footprints that the triage hands to the exact setup (k_setup<false>,
-  launched only when the list is not empty): fan loops around a pole.
+* footprints that the triage hands to the exact setup (k_setup_exact,
+  a wave per listed footprint): fan loops around a pole.
 
 Semantics: pkg/geo/s2.go:99-122 (Covering), pkg/models/geo.go:224-268.
 """

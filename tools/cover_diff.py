@@ -42,11 +42,11 @@ def main():
     offs, cells, status, area = O.cover_batch(kind, voff, lat, lng, rad)
     area = np.asarray(area, np.float64)
     ctx = _lib.context(0)
-    for knobs in ({}, {"cover_slot_order": 1}, {"cover_exact_setup": 1}, {"cover_slot_order": 1, "cover_exact_setup": 1}):
+    for knobs in ({}, {"cover_slot_order": 0}, {"cover_exact_setup": 1}, {"cover_slot_order": 0, "cover_exact_setup": 1}):
         for k, v in knobs.items():
             ctx.set_tuning(k, v)
         r = geo.cover_batch(kind, voff, lat, lng, rad)
-        ctx.set_tuning("cover_slot_order", 0)
+        ctx.set_tuning("cover_slot_order", 1)
         ctx.set_tuning("cover_exact_setup", 0)
         bad = np.nonzero((r.status != status) | (np.diff(r.offs) != np.diff(offs)) |
                          (r.area_km2.view(np.uint64) != area.view(np.uint64)))[0]
