@@ -707,7 +707,9 @@ __device__ __forceinline__ double wave_max_d(double x)
     return x;
 }
 
-__global__ __launch_bounds__(256) void k_setup_exact(const uint32_t *slow_list, const unsigned int *slow_n,
+// k_setup_exact's fixed grid (4 x 64 threads measured the same, profiles/r07e)
+constexpr int kExactGrid = 16, kExactBlock = 256;
+__global__ __launch_bounds__(kExactBlock) void k_setup_exact(const uint32_t *slow_list, const unsigned int *slow_n,
                                                      const int32_t *kind, const int64_t *voff, const double *lat,
                                                      const double *lng, const float *radius_m, const int64_t *xoff,
                                                      const V3 *xyz, int32_t *status, double *area_out, uint8_t *mode,
@@ -1348,10 +1350,6 @@ __global__ void k_emit_big(const uint32_t *big, const int *nbig, const uint32_t 
 // (kept, undecided) whose bit order is the cell-id order of the output.
 constexpr int kFpBlock = 256;  // threads of a k_cand_fp block
 constexpr int kFpPer = 64;     // footprints per k_cand_fp block (one wave loads them)
-#ifndef DSS_CAND_MAP
-#define DSS_CAND_MAP 0
-#endif
-constexpr int kCandMap = 4096;  // candidates whose footprint a k_cand_fp block maps in LDS (DSS_CAND_MAP)
 
 // Key of level-13 cell (i13, j13) of footprint f, or -1 outside its start
 // cells (cannot happen for a cell of the bound).
@@ -1516,10 +1514,6 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
     __shared__ int64_t s_xo[kFpPer];
     __shared__ unsigned long long s_km[kFpPer][4], s_um[kFpPer][4];
     __shared__ float2 s_uvf[kCandStageV];  // the block's (u,v) vertices in float (cand_edges_uv_f's prefilter)
-#if DSS_CAND_MAP
-    __shared__ uint8_t s_own[kCandMap];      // candidate -> footprint (the first kCandMap candidates)
-    __shared__ uint32_t s_wm[kFpPer];        // 2^16 / bound width, rounded up (d / w = d * wm >> 16 for d < 256)
-#endif
     const int t = threadIdx.x, lane = t & 63;
     const int64_t F0 = (int64_t)blockIdx.x * kFpPer;
     if (t < kFpPer) {
@@ -1545,12 +1539,6 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
         s_nv[t] = (int)nvv;
 #pragma unroll
         for (int q = 0; q < 4; q++) s_km[t][q] = s_um[t][q] = 0ull;
-#if DSS_CAND_MAP
-        {
-            const uint32_t wb = fast ? s_bx[t].y - s_bx[t].x + 1 : 1u;
-            s_wm[t] = (65536u + wb - 1u) / wb;
-        }
-#endif
         // candidate and vertex prefixes over the block's footprints (wave scans)
         uint32_t ci = cnt, vi = nvv;
         for (int o = 1; o < 64; o <<= 1) {
@@ -1571,12 +1559,6 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
     // by LDS search: the last footprint whose prefix is <= k holds it), so a
     // block of small footprints (configs[3]'s 4-gons) does not walk them one
     // footprint per wave
-#if DSS_CAND_MAP
-    {  // four threads per footprint write its candidates' owner bytes
-        const int fo = t >> 2, c1 = min(s_cb[fo + 1], kCandMap);
-        for (int k = s_cb[fo] + (t & 3); k < c1; k += 4) s_own[k] = (uint8_t)fo;
-    }
-#endif
     const int nvs = min(s_vp[kFpPer], kCandStageV);
     for (int k = t; k < nvs; k += kFpBlock) {
         int lo = 0, hi = kFpPer;  // s_vp[lo] <= k < s_vp[hi]
@@ -1592,28 +1574,18 @@ __global__ __launch_bounds__(kFpBlock) void k_cand_fp(int64_t n, const uint8_t *
     __syncthreads();
     const int total = s_cb[kFpPer];
     for (int k = t; k < total; k += kFpBlock) {
-        int lo = 0;
-#if DSS_CAND_MAP
-        if (k < kCandMap) {
-            lo = s_own[k];
-        } else
-#endif
-        {
-            int hi = kFpPer;  // s_cb[lo] <= k < s_cb[hi]
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (s_cb[mid] <= k) lo = mid;
-                else hi = mid;
-            }
+        // (round 6: an LDS candidate -> footprint byte map and a magic-number
+        // division instead of this search and d / w measured slower, 0.294
+        // -> 0.315 ms, profiles/r07e)
+        int lo = 0, hi = kFpPer;  // s_cb[lo] <= k < s_cb[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_cb[mid] <= k) lo = mid;
+            else hi = mid;
         }
         const uint4 bx = s_bx[lo];
         const uint32_t w = bx.y - bx.x + 1, d = (uint32_t)(k - s_cb[lo]);
-#if DSS_CAND_MAP
-        const uint32_t dj = (d * s_wm[lo]) >> 16;  // (d < 256 <= 2^16 / w: exact)
-#else
-        const uint32_t dj = d / w;
-#endif
-        const uint32_t i13 = bx.x + (d - dj * w), j13 = bx.z + dj;
+        const uint32_t dj = d / w, i13 = bx.x + (d - dj * w), j13 = bx.z + dj;
         const uint32_t info = s_info[lo];
         const int key = rect_key(i13, j13, s_sti[lo], s_stj[lo], info);
         if (key < 0) continue;
@@ -2380,7 +2352,7 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     // waves strides over the device list (empty, it costs one small launch),
     // then per footprint its clipped-edge items and the descent list, and one
     // sync for their totals
-    hipLaunchKernelGGL(k_setup_exact, dim3(16), dim3(256), 0, s, slow, slow_n, kind, voff, lat, lng, radius_m, xoff,
+    hipLaunchKernelGGL(k_setup_exact, dim3(kExactGrid), dim3(kExactBlock), 0, s, slow, slow_n, kind, voff, lat, lng, radius_m, xoff,
                        xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, rev_flag,
                        bad);
     hipLaunchKernelGGL(k_edge_counts, dim3(grid_for(n, B)), dim3(B), 0, s, n, mode, fmask, flags, nvx, nv, dlist, dlist_n);
