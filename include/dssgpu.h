@@ -465,7 +465,14 @@ void dssg_set_timing(dssg_ctx *ctx, int enabled);
  * "record_order" = where the join reads its query records (0: picked per
  * index, the default -- key order when some group holds >= 8192 postings;
  * 1: query order through the sorted keys; 2: key order, permuted after the
- * key sort).  Results do not depend on any of them.  Unknown key or value:
+ * key sort); "small_search" = the largest batch (queries) the one-launch
+ * small join takes (default 4096; 0: never); "route_identity" (below);
+ * "cover_wave" = the largest batch (footprints) the covering's
+ * wave-per-footprint path takes (default 16384; 0: never);
+ * "cover_slot_order" = the general covering's vertex slots polygons first
+ * (1, the default) or in footprint order (0); "cover_exact_setup" = 1 sends
+ * every general-path footprint through the exact setup (tests; default 0).
+ * Results do not depend on any of them.  Unknown key or value:
  * DSSG_ERR_INVALID. */
 int dssg_set_tuning(dssg_ctx *ctx, const char *key, int64_t value);
 /* Work counters of the most recent search: query-cell keys (cells of the
