@@ -117,9 +117,6 @@ constexpr int kStageSparse = DSS_STAGE_SPARSE, kStageDense = 1024;
 #define DSS_JOIN_LONG_WPE 1
 #endif
 constexpr int kJoinLongWpe = DSS_JOIN_LONG_WPE;  // the long variant's register budget (waves per SIMD)
-#ifndef DSS_DISTINCT_RM
-#define DSS_DISTINCT_RM 0
-#endif
 #ifndef DSS_EMIT_DENSITY
 #define DSS_EMIT_DENSITY 4
 #endif
@@ -1682,34 +1679,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(LON
                         }
                     }
                 }
-#if DSS_DISTINCT_RM
-                // (variant) record-major: one broadcast signature per record some
-                // lane must check (mode 2: when those are few against the
-                // longest lane's checks)
-                bool rm = !LONG;
-                unsigned long long anyneed = 0;
-                if (!LONG) {
-                    anyneed = need;
-#pragma unroll
-                    for (int o = 32; o > 0; o >>= 1) anyneed |= __shfl_xor(anyneed, o);
-                    anyneed = uni64(anyneed);
-                    if (DSS_DISTINCT_RM == 2) {
-                        const uint32_t mx = wave_max((uint32_t)__popcll(need));
-                        rm = (uint32_t)__popcll(anyneed) <= 2u * mx;
-                    }
-                }
-                if (rm) {
-                    while (anyneed) {
-                        const int j = __builtin_ctzll(anyneed);
-                        anyneed &= anyneed - 1;
-                        const ulonglong2 c0 = s_rs[w][0][j], c1 = s_rs[w][1][j];
-                        const bool ov = ((c0.x & ps01.x) | (c0.y & ps01.y) | (c1.x & ps23.x) | (c1.y & ps23.y)) != 0ull;
-                        if (((need >> j) & 1ull) && !ov) keep |= 1ull << j;
-                    }
-                    need = 0;
-                }
-#endif
-                // lane-major (each lane walks its own checks): full batches
+                // lane-major (each lane walks its own checks; round 6: record-major
+                // -- one broadcast signature per record some lane needs -- made
+                // k_join slower on configs[1] / [2] / [3]: 2.03 -> 2.14 ms on [2],
+                // profiles/r07h)
                 while (need) {
                     const int j = __builtin_ctzll(need);
                     need &= need - 1;
