@@ -2366,9 +2366,24 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     if (nd > 0)
         hipLaunchKernelGGL(k_reverse_list, dim3((unsigned)std::min<int64_t>((nd + 3) / 4, 1024)), dim3(256), 0, s, dlist,
                            dlist_n, xoff, nvx, rev_flag, xyz, uv);
-    if (std::getenv("DSS_COVER_STATS"))
+    if (std::getenv("DSS_COVER_STATS")) {
         fprintf(stderr, "[cover] n %lld vertices %lld clipped edges %lld descent %lld exact-setup %u\n", (long long)n,
                 (long long)nx, (long long)ne, (long long)nd, ns_u);
+        // (the exact setup's footprints: kind, vertex count, status, mode, flags)
+        for (unsigned int i = 0; i < ns_u && i < 8; i++) {
+            uint32_t f = 0;
+            int32_t k = 0, st = 0, nvv = 0;
+            uint8_t md = 0, fl = 0;
+            DSS_HIP(hipMemcpy(&f, slow + i, sizeof(f), hipMemcpyDeviceToHost));
+            DSS_HIP(hipMemcpy(&k, kind + f, sizeof(k), hipMemcpyDeviceToHost));
+            DSS_HIP(hipMemcpy(&st, status + f, sizeof(st), hipMemcpyDeviceToHost));
+            DSS_HIP(hipMemcpy(&nvv, nvx + f, sizeof(nvv), hipMemcpyDeviceToHost));
+            DSS_HIP(hipMemcpy(&md, mode + f, 1, hipMemcpyDeviceToHost));
+            DSS_HIP(hipMemcpy(&fl, flags + f, 1, hipMemcpyDeviceToHost));
+            fprintf(stderr, "[cover]   exact-setup footprint %u: kind %d vertices %d status %d mode %d flags %d\n", f, k,
+                    nvv, st, (int)md, (int)fl);
+        }
+    }
     // direct candidates (most footprints): the cells of each one's bound,
     // tested now, compacted after the counts
     unsigned long long *fkm = kmask_.ensure(8 * (n + 1)), *fum = fkm + 4 * (n + 1);
