@@ -593,7 +593,8 @@ __device__ __forceinline__ void setup_one(int64_t f, uint32_t *slow_list, unsign
 #ifndef DSS_SETUP_WPE
 #define DSS_SETUP_WPE 1
 #endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DSS_SETUP_WPE))) void k_setup(
+constexpr int kSetupBlock = 64;  // (256-thread blocks: 0.306 -> 0.315 ms, profiles/r07n)
+__global__ __launch_bounds__(kSetupBlock) __attribute__((amdgpu_waves_per_eu(DSS_SETUP_WPE))) void k_setup(
     uint32_t *slow_list, unsigned int *slow_n, int64_t n, const int32_t *kind, const int64_t *voff, const double *lat,
     const double *lng, const float *radius_m, const int64_t *xoff, const V3 *xyz, int32_t *status, double *area_out, uint8_t *mode,
     uint8_t *origin_in, uint8_t *fmask, uint8_t *flags, int32_t *nvx, const double2 *uv, uint64_t *st_id,
@@ -1348,7 +1349,7 @@ __global__ void k_emit_big(const uint32_t *big, const int *nbig, const uint32_t 
 // the start cells' level-13 descendants in id order (start cell s, Hilbert
 // position inside it), so a footprint's verdicts are two 256-bit masks
 // (kept, undecided) whose bit order is the cell-id order of the output.
-constexpr int kFpBlock = 256;  // threads of a k_cand_fp block
+constexpr int kFpBlock = 256;  // threads of a k_cand_fp block (128: 0.29 -> 0.42 ms; 512: same, profiles/r07n)
 constexpr int kFpPer = 64;     // footprints per k_cand_fp block (one wave loads them)
 
 // Key of level-13 cell (i13, j13) of footprint f, or -1 outside its start
@@ -2340,7 +2341,7 @@ void CoverEngine::run_general(int64_t n, const int32_t *kind, const int64_t *vof
     hipLaunchKernelGGL(k_fan_area, dim3(std::min<int64_t>(grid_for(2 * nx + 1, B), 2048)), dim3(B), 0, s, toff + n,
                        towner, toff, omode, nv, xoff, xyz, fwd, rev, fan_fail);
     uint8_t *rev_flag = revf_.ensure(n + 1);
-    hipLaunchKernelGGL(k_setup, dim3(grid_for(n, 64)), dim3(64), 0, s, slow, slow_n, n, kind, voff, lat, lng, radius_m,
+    hipLaunchKernelGGL(k_setup, dim3(grid_for(n, kSetupBlock)), dim3(kSetupBlock), 0, s, slow, slow_n, n, kind, voff, lat, lng, radius_m,
                        xoff, xyz, status, area, mode, orig, fmask, flags, nvx, uv, st_id, st_i, st_j, finfo, fbox, fwd,
                        rev, fan_fail, not_inner, omode, perm, rev_flag, bad, frames, all_exact_ ? 1 : 0);
     int64_t *eoff = eoff_.ensure(n + 1);
