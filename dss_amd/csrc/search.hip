@@ -118,7 +118,7 @@ constexpr int kStageSparse = DSS_STAGE_SPARSE, kStageDense = 1024;
 #endif
 constexpr int kJoinLongWpe = DSS_JOIN_LONG_WPE;  // the long variant's register budget (waves per SIMD)
 #ifndef DSS_EMIT_DENSITY
-#define DSS_EMIT_DENSITY 4
+#define DSS_EMIT_DENSITY 2
 #endif
 constexpr int kEmitDensity = DSS_EMIT_DENSITY;
 

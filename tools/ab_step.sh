@@ -1,6 +1,6 @@
 #!/bin/bash
 # Whole-step A/B with 3 pipelines (the bench line's own setting, where the
-# kernels of different pipelines overlap): bench.py on configs[2] under each
+# kernels of different pipelines overlap): bench.py on configs[CFG, default 2] under each
 # library, alternating, twice; then one PMC pass per library (VALU, SALU, LDS
 # instructions and waves per kernel).  base = the in-tree library; others from
 # dss_amd/variants/ (tools/variants.sh).  Results under gpurun_out/TAG/.
@@ -10,7 +10,7 @@ TAG=${1:-ab_step}
 VS=${2:-base}
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/$TAG; mkdir -p $O
-A="--config 2 --steps 40 --warmup 5 --no-verify --cpu-sample 0 --latency 0 --survey-model 0"
+A="--config ${CFG:-2} --steps 40 --warmup 5 --no-verify --cpu-sample 0 --latency 0 --survey-model 0"
 for r in 1 2; do
   for v in ${VS//,/ }; do
     if [ $v = base ]; then unset DSS_AMD_LIB; else export DSS_AMD_LIB=$GRAFT_REPO_ROOT/dss_amd/variants/$v.so; fi
