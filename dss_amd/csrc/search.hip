@@ -102,13 +102,19 @@ struct Regions {
 // (configs[2]: ~6 pairs per staged record) run 7 workgroups per CU with a
 // 640-pair stage per wave (k_join 3.45 -> 3.24 ms against 6 x 1024);
 // dense-output joins (configs[3], RID 30-s windows: ~29 pairs per record,
-// pass density 0.45) keep 6 x 1024 (0.55 against 0.61 ms).  The search
-// picks the shape from the previous batch's pass density (dense_out_).
+// pass density 0.45) take 1024-pair stages at 3 workgroups per CU (round 6,
+// on the 3-pipeline step: configs[3] 867 -> 973M q/s against 6, k_join 0.53
+// -> 0.46 ms; 2 gave the step +3 % more with a slower join, profiles/r07z).
+// The search picks the shape from the previous batch's pass density
+// (dense_out_).
 constexpr int kWaves = 4;  // waves per join workgroup
 #ifndef DSS_JOIN_BPC_SPARSE
 #define DSS_JOIN_BPC_SPARSE 7
 #endif
-constexpr int kJoinBpcSparse = DSS_JOIN_BPC_SPARSE, kJoinBpcDense = 6;
+#ifndef DSS_JOIN_BPC_DENSE
+#define DSS_JOIN_BPC_DENSE 3
+#endif
+constexpr int kJoinBpcSparse = DSS_JOIN_BPC_SPARSE, kJoinBpcDense = DSS_JOIN_BPC_DENSE;
 #ifndef DSS_STAGE_SPARSE
 #define DSS_STAGE_SPARSE 640
 #endif
